@@ -1,0 +1,242 @@
+#!/usr/bin/env python3
+"""Throughput benchmark of the PWG generator hot path on MI355X.
+
+Workload (BASELINE.json metric "audio samples/sec/GPU (24 kHz PWG, 80-band mel)", configs[4]):
+LibriTTS parallel_wavegan.v1 generator (30 layers, 24 kHz, hop 300), random-init seeded
+weights, a batch of synthetic utterances per GPU with T'_i = RandomState(3).randint(80, 1200)
+mel frames (1-15 s of audio each). One "step" = one generator forward over the whole batch
+(every kernel of the hot path), inputs resident in HBM before the timed region.
+
+Multi-GPU: one process per GPU (torch.distributed.run), utterances are independent so the data
+path has no collective; rank 0's packed weights are RCCL-broadcast once at start-up.
+Weak scaling: every rank runs the same per-GPU batch shape.
+
+Prints ONE JSON line (rank 0) with the contract fields plus "roofline" and "cpu_baseline".
+"""
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from parallelwavegan_amd import Engine, _lib, configs, synthetic  # noqa: E402
+from parallelwavegan_amd.sharding import broadcast_packed_weights, max_over_ranks  # noqa: E402
+
+FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: Peak FP32 (matrix) = vector, spec
+HBM_PEAK_GBS = 8000.0
+
+
+def layer_flops_per_sample(params):
+    """Algorithmic FLOP per output sample of ONE residual layer in the reference formulation
+    (SURVEY.md sec 8(a) a10): 2 * (K*R*G + A*G + GH*S + GH*R)."""
+    R, G, S, A, K = (params[k] for k in ("residual_channels", "gate_channels", "skip_channels",
+                                         "aux_channels", "kernel_size"))
+    return 2 * (K * R * G + A * G + (G // 2) * S + (G // 2) * R)
+
+
+def layer_bytes_per_sample(params):
+    """Algorithmic HBM bytes per output sample of one residual layer (fp32, layer-streaming):
+    read x (R) + c_up (A) + skip (S), write x (R) + skip (S)."""
+    R, S, A = params["residual_channels"], params["skip_channels"], params["aux_channels"]
+    return 4 * (2 * R + A + 2 * S)
+
+
+def model_flops_per_sample(params):
+    """Whole-forward algorithmic FLOP per sample (2,591,262 for LibriTTS v1)."""
+    L = params["layers"]
+    R, S, A, O = params["residual_channels"], params["skip_channels"], params["aux_channels"], params["out_channels"]
+    scales = params["upsample_params"]["upsample_scales"]
+    H = int(np.prod(scales))
+    w = params["aux_context_window"]
+    conv_in = A * A * (2 * w + 1) / H
+    fir, n = 0.0, 1
+    for s in scales:
+        n *= s
+        fir += A * (2 * s + 1) * n / H
+    head = S * S + S * O + R
+    return L * layer_flops_per_sample(params) + 2 * (conv_in + fir + head)
+
+
+def dist_setup(n_gpus):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        dist.init_process_group("nccl", device_id=dev)
+        return dist.get_rank(), world, dev
+    if n_gpus != 1:
+        print(f"[bench] --gpus {n_gpus} without torch.distributed.run: running 1 process", file=sys.stderr)
+    return 0, 1, torch.device("cuda", 0)
+
+
+def cpu_baseline(params, sd, lengths, H, seconds_budget):
+    """Time the torch-CPU restatement of the reference (oracle/pwg_torch_cpu.py, same aten op
+    sequence as the reference) on a bounded sample of the same workload, B=1 per utterance like
+    bin/decode.py. Returns (samples/s, threads, description)."""
+    from oracle.pwg_torch_cpu import TorchCPUGenerator
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    gen = TorchCPUGenerator(sd, params)
+    A = params["aux_channels"]
+    gen.inference(synthetic.make_mel(40, A, seed=99), synthetic.make_noise(40 * H, seed=98))  # warm-up
+    done_samples, t_total, used = 0, 0.0, 0
+    for i, f in enumerate(lengths):
+        mel = synthetic.make_mel(int(f), A, seed=1000 + i)
+        noise = synthetic.make_noise(int(f) * H, seed=2000 + i)
+        t0 = time.perf_counter()
+        gen.inference(mel, noise)
+        t_total += time.perf_counter() - t0
+        done_samples += int(f) * H
+        used += 1
+        if t_total >= seconds_budget:
+            break
+    desc = f"{used} LibriTTS-v1 utterances ({done_samples} samples, first of the bench batch), B=1, torch-CPU aten restatement"
+    return done_samples / t_total, threads, desc
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="libritts_v1", choices=["libritts_v1", "ljspeech_v1", "yesno_debug"])
+    ap.add_argument("--utts", type=int, default=32, help="utterances per GPU per step")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (0 = skip)")
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "layer_traffic.json"))
+    args = ap.parse_args()
+
+    rank, world, dev = dist_setup(args.gpus)
+    _lib.build()
+    params = configs.generator_params(args.config)
+    fs = configs.SAMPLING_RATE[args.config]
+    eng = Engine(params, dev)
+    H = eng.upsample_factor
+    A = params["aux_channels"]
+
+    # weights: packed on rank 0, RCCL-broadcast to the other ranks (one collective, start-up only)
+    sd = synthetic.make_state_dict(params, seed=0)
+    if rank == 0:
+        packed = torch.from_numpy(eng.pack(sd)).to(dev)
+    else:
+        packed = torch.empty(eng.packed_weight_count, dtype=torch.float32, device=dev)
+    broadcast_packed_weights(packed, src=0)
+    eng.set_packed(packed)
+
+    # this rank's utterances: same lengths on every rank (weak scaling), rank-specific content
+    lengths = synthetic.libritts_lengths(args.utts, seed=3)
+    plan = eng.plan(lengths.tolist())
+    rs = np.random.RandomState(100 + rank)
+    mel = torch.from_numpy(rs.standard_normal(int(lengths.sum()) * A).astype(np.float32)).to(dev)
+    noise = torch.from_numpy(rs.standard_normal(plan.total_samples).astype(np.float32)).to(dev)
+    out = torch.empty(plan.total_samples * params["out_channels"], dtype=torch.float32, device=dev)
+    torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        eng.run(plan, mel, noise, out)
+    torch.cuda.synchronize(dev)
+
+    eng.set_timing(True)
+    eng.collect_timing()  # clear
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.run(plan, mel, noise, out)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    eng.set_timing(False)
+    timing = eng.collect_timing()
+    elapsed = max_over_ranks(elapsed, dev)
+    if not torch.isfinite(out).all():
+        raise RuntimeError("non-finite generator output")
+
+    samples_per_step = plan.total_samples * world
+    value = samples_per_step * args.steps / elapsed
+    per_gpu = value / world
+    layer_ms, layer_n = timing["residual_layer"]
+    layer_avg_s = layer_ms / 1e3 / max(layer_n, 1)
+    flops_launch = layer_flops_per_sample(params) * plan.total_samples
+    achieved_tflops = flops_launch / layer_avg_s / 1e12
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            if tj.get("config") == args.config and tj.get("utts") == args.utts:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    cpu = None
+    if args.cpu_seconds > 0 and world == 1:
+        v, cores, desc = cpu_baseline(params, sd, lengths, H, args.cpu_seconds)
+        cpu = {"value": round(v, 1), "unit": "audio samples/s", "cores": cores, "kind": "port", "sample": desc}
+
+    res = {
+        "metric": "audio samples/sec/GPU (24 kHz PWG, 80-band mel) + RTF at 1/2/4/8 MI355X",
+        "value": round(value, 1),
+        "unit": "audio samples/s (whole job, all GPUs)",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (seeded N(0,1) mel + noise, seeded kaiming-init weights)",
+        "config": {
+            "workload": f"{args.config} generator inference, {args.utts} ragged utterances per GPU per step",
+            "model": "ParallelWaveGANGenerator",
+            "sampling_rate": fs,
+            "hop": H,
+            "global_batch": args.utts * world,
+            "frames_per_gpu": int(lengths.sum()),
+            "samples_per_step_per_gpu": int(plan.total_samples),
+            "parallelism": f"utterance-sharded x{world} (no data-path collective; RCCL weight broadcast at start)",
+        },
+        "value_per_gpu": round(per_gpu, 1),
+        "x_realtime_per_gpu": round(per_gpu / fs, 1),
+        "rtf_per_gpu": per_gpu and fs / per_gpu,
+        "kernel_ms_per_step": {k: round(ms / args.steps, 3) for k, (ms, _) in timing.items()},
+        "roofline": {
+            "kernel": "pwg_layer_kernel<4,4> (one fused WaveNet residual layer)",
+            "bound": "mfma",
+            "achieved": round(achieved_tflops, 3),
+            "peak": FP32_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 4),
+            "traffic": traffic,
+            "flop_per_launch": int(flops_launch),
+            "algorithmic_bytes_per_launch": int(layer_bytes_per_sample(params) * plan.total_samples),
+            "avg_launch_ms": round(layer_avg_s * 1e3, 4),
+            "launches_timed": layer_n,
+        },
+        "model_flop_per_sample": round(model_flops_per_sample(params), 1),
+        "model_tflops": round(value / world * model_flops_per_sample(params) / 1e12, 3),
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,161 @@
+/*
+ * pwg.h — C-ABI of the MI355X-native Parallel WaveGAN generator inference engine.
+ *
+ * The reference has no FFI for this path: its "operator API" is the Python class
+ * parallel_wavegan.models.ParallelWaveGANGenerator looked up by string
+ * (/root/reference/parallel_wavegan/utils/utils.py:317-327). Each entry point
+ * below replaces one piece of that class; the Python drop-in
+ * (parallelwavegan_amd/models.py) binds them through ctypes
+ * (parallelwavegan_amd/_lib.py). Signatures carry only plain pointers, sizes and
+ * an opaque stream; no torch types cross this boundary.
+ *
+ *   pwg_create / PwgConfig      <- ParallelWaveGANGenerator.__init__
+ *                                  models/parallel_wavegan.py:24-142 (constructor args)
+ *   pwg_ref_weight_count        <- the generator state_dict after remove_weight_norm
+ *   pwg_pack_weights            <- remove_weight_norm + parameters, models/parallel_wavegan.py:175-185
+ *                                  (the caller folds g*v/||v||; this packs for the kernels)
+ *   pwg_plan_create             <- per-call shape logic of inference()/forward()
+ *                                  models/parallel_wavegan.py:231-263 and :144-173
+ *   pwg_run                     <- ParallelWaveGANGenerator.forward (upsample_net -> first_conv ->
+ *                                  30 residual blocks -> skip sum -> last_conv_layers)
+ *                                  models/parallel_wavegan.py:144-173,
+ *                                  layers/upsample.py:112-128,178-194, layers/residual_block.py:102-140
+ *   pwg_receptive_field_size    <- ParallelWaveGANGenerator.receptive_field_size :197-211
+ *
+ * Error behaviour mirrors the reference: a Python `assert` there maps to
+ * PWG_ERR_ASSERT (AssertionError), argument errors to PWG_ERR_INVALID
+ * (ValueError), unsupported constructor options to PWG_ERR_UNSUPPORTED
+ * (NotImplementedError), HIP failures to PWG_ERR_HIP (RuntimeError).
+ * pwg_last_error() returns a thread-local message for the last failure.
+ *
+ * Threading: a handle/plan is not thread-safe; work is enqueued on the caller's
+ * HIP stream (hipStream_t passed as void*), nothing synchronises the host except
+ * pwg_plan_create (descriptor upload) and pwg_timing_collect.
+ */
+#ifndef PWG_H_
+#define PWG_H_
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PWG_ABI_VERSION 1
+#if defined(__GNUC__) || defined(__clang__)
+#define PWG_API __attribute__((visibility("default")))
+#else
+#define PWG_API
+#endif
+#define PWG_MAX_SCALES 8
+
+enum {
+  PWG_OK = 0,
+  PWG_ERR_INVALID = 1,     /* ValueError */
+  PWG_ERR_ASSERT = 2,      /* AssertionError */
+  PWG_ERR_HIP = 3,         /* RuntimeError (HIP runtime failure) */
+  PWG_ERR_UNSUPPORTED = 4  /* NotImplementedError */
+};
+
+/* Input layouts accepted by pwg_plan_create / pwg_run. */
+enum {
+  /* inference(): per utterance c (T'_u, aux) frames-major, utterances concatenated
+   * along frames; optional (c-mean)/scale; ReplicationPad1d(aux_context_window)
+   * applied inside the engine (models/parallel_wavegan.py:254-262).
+   * noise x: per utterance (T_u, 1) concatenated -> (sum T_u).
+   * out: per utterance (T_u, out_channels) concatenated. */
+  PWG_LAYOUT_INFERENCE = 0,
+  /* forward(z, c): c (B, aux, T' + 2w) channel-major, already context-padded by the
+   * caller (models/parallel_wavegan.py:144-158); z (B, 1, T); out (B, out_channels, T).
+   * All B items share T' (the reference's batched API is equal-length). */
+  PWG_LAYOUT_FORWARD = 1
+};
+
+/* Timing buckets reported by pwg_timing_collect. */
+enum {
+  PWG_KERNEL_CONV_IN = 0,
+  PWG_KERNEL_UPSAMPLE = 1,
+  PWG_KERNEL_FIRST_CONV = 2,
+  PWG_KERNEL_RESIDUAL_LAYER = 3,
+  PWG_KERNEL_HEAD = 4,
+  PWG_NUM_KERNELS = 5
+};
+
+/* Mirrors ParallelWaveGANGenerator.__init__ arguments
+ * (models/parallel_wavegan.py:24-43). dropout is inference-irrelevant;
+ * bias=False is expressed by zero biases in the reference-order weights. */
+typedef struct PwgConfig {
+  int in_channels;          /* must be 1 */
+  int out_channels;
+  int kernel_size;          /* odd (non-causal) */
+  int layers;
+  int stacks;               /* layers % stacks == 0 (AssertionError otherwise) */
+  int residual_channels;
+  int gate_channels;        /* even */
+  int skip_channels;
+  int aux_channels;
+  int aux_context_window;
+  int use_causal_conv;
+  int use_conv_in;          /* 1: "ConvInUpsampleNetwork", 0: "UpsampleNetwork" */
+  int num_scales;
+  int upsample_scales[PWG_MAX_SCALES];
+} PwgConfig;
+
+typedef struct PwgHandle PwgHandle;
+typedef struct PwgPlan PwgPlan;
+
+PWG_API int pwg_abi_version(void);
+PWG_API const char* pwg_last_error(void);
+
+PWG_API int pwg_create(const PwgConfig* cfg, int device, PwgHandle** out);
+PWG_API void pwg_destroy(PwgHandle* h);
+
+/* receptive field (kernel_size-1)*sum(dilations)+1, models/parallel_wavegan.py:197-211 */
+PWG_API long long pwg_receptive_field_size(const PwgHandle* h);
+PWG_API long long pwg_upsample_factor(const PwgHandle* h);
+
+/* Number of floats in the reference-order flat weight vector (after weight-norm
+ * folding), in this order:
+ *   first_conv.weight (R,in,1), first_conv.bias (R)
+ *   upsample_net.conv_in.weight (A,A,KW)            [only when use_conv_in]
+ *   upsample_net.upsample.up_layers.{1,3,..}.weight (2s+1) per scale
+ *   per layer l: conv.weight (G,R,K), conv.bias (G), conv1x1_aux.weight (G,A),
+ *                conv1x1_skip.weight (S,G/2), conv1x1_skip.bias (S),
+ *                conv1x1_out.weight (R,G/2), conv1x1_out.bias (R)
+ *   last_conv_layers.1.weight (S,S), .bias (S), last_conv_layers.3.weight (O,S), .bias (O)
+ * Missing biases (bias=False) are passed as zeros. */
+PWG_API long long pwg_ref_weight_count(const PwgHandle* h);
+/* Number of floats of the kernel-ready packed weight image (fp32). */
+PWG_API long long pwg_packed_weight_count(const PwgHandle* h);
+/* Host -> host: pack reference-order weights into the kernel image. The caller
+ * uploads the image to device memory (and may RCCL-broadcast it). */
+PWG_API int pwg_pack_weights(const PwgHandle* h, const float* ref_host, float* packed_host);
+
+/* Plan a batch of n_utts utterances with frames[u] mel frames each. */
+PWG_API int pwg_plan_create(PwgHandle* h, int n_utts, const long long* frames, int layout, PwgPlan** out);
+PWG_API void pwg_plan_destroy(PwgPlan* p);
+PWG_API long long pwg_plan_total_samples(const PwgPlan* p);   /* sum_u frames[u]*upsample_factor */
+PWG_API long long pwg_plan_padded_samples(const PwgPlan* p);  /* HBM time axis incl. segment padding */
+PWG_API long long pwg_plan_workspace_bytes(const PwgPlan* p);
+
+/* Enqueue one generator forward over the planned batch on `stream`.
+ *   packed   device, pwg_packed_weight_count floats
+ *   mel      device, layout-dependent (see PWG_LAYOUT_*)
+ *   noise    device, sum_u T_u floats
+ *   mean/scale device (aux floats) or NULL: (c-mean)/scale before padding
+ *              (models/parallel_wavegan.py:259-260); PWG_LAYOUT_INFERENCE only
+ *   out      device, sum_u T_u * out_channels floats
+ *   workspace device, pwg_plan_workspace_bytes bytes, 256-B aligned */
+PWG_API int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* noise,
+            const float* mean, const float* scale, float* out, void* workspace, void* stream);
+
+/* Per-kernel HIP-event timing of pwg_run (off by default). collect synchronises
+ * on the recorded events, adds ms and launch counts per PWG_KERNEL_* bucket into
+ * the caller's arrays and clears the records. */
+PWG_API int pwg_set_timing(PwgHandle* h, int enable);
+PWG_API int pwg_timing_collect(PwgHandle* h, double* ms, long long* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PWG_H_ */

@@ -1,0 +1,177 @@
+"""ctypes binding of the engine's C-ABI (include/pwg.h) and its in-tree build.
+
+The shared library is built IN-TREE (parallelwavegan_amd/lib/libpwg_hip.so) by ``build()``
+with hipcc for gfx950 so it travels with the repository snapshot. There is no fallback: if the
+library is missing, ``load()`` raises, and so does every GPU entry point that needs it.
+
+``torch`` must be imported before the library is loaded: torch ships its own
+libamdhip64.so.7 and the dynamic loader then resolves our NEEDED entry to that same runtime
+(one HIP runtime per process, so torch device pointers and streams are valid here).
+"""
+
+import ctypes
+import os
+import subprocess
+import threading
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+LIB_DIR = os.path.join(PKG_DIR, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libpwg_hip.so")
+CSRC = [
+    os.path.join(PKG_DIR, "csrc", "pwg_kernels.hip"),
+    os.path.join(PKG_DIR, "csrc", "pwg_capi.hip"),
+]
+HEADERS = [
+    os.path.join(REPO_DIR, "include", "pwg.h"),
+    os.path.join(PKG_DIR, "csrc", "pwg_internal.h"),
+]
+OFFLOAD_ARCH = "gfx950"
+
+PWG_OK = 0
+PWG_ERR_INVALID = 1
+PWG_ERR_ASSERT = 2
+PWG_ERR_HIP = 3
+PWG_ERR_UNSUPPORTED = 4
+
+PWG_LAYOUT_INFERENCE = 0
+PWG_LAYOUT_FORWARD = 1
+
+KERNEL_BUCKETS = ("conv_in", "upsample", "first_conv", "residual_layer", "head")
+PWG_MAX_SCALES = 8
+
+# Every symbol include/pwg.h declares (checked by tests/test_abi.py).
+EXPORTED_SYMBOLS = (
+    "pwg_abi_version",
+    "pwg_last_error",
+    "pwg_create",
+    "pwg_destroy",
+    "pwg_receptive_field_size",
+    "pwg_upsample_factor",
+    "pwg_ref_weight_count",
+    "pwg_packed_weight_count",
+    "pwg_pack_weights",
+    "pwg_plan_create",
+    "pwg_plan_destroy",
+    "pwg_plan_total_samples",
+    "pwg_plan_padded_samples",
+    "pwg_plan_workspace_bytes",
+    "pwg_run",
+    "pwg_set_timing",
+    "pwg_timing_collect",
+)
+
+
+class PwgConfig(ctypes.Structure):
+    _fields_ = [
+        ("in_channels", ctypes.c_int),
+        ("out_channels", ctypes.c_int),
+        ("kernel_size", ctypes.c_int),
+        ("layers", ctypes.c_int),
+        ("stacks", ctypes.c_int),
+        ("residual_channels", ctypes.c_int),
+        ("gate_channels", ctypes.c_int),
+        ("skip_channels", ctypes.c_int),
+        ("aux_channels", ctypes.c_int),
+        ("aux_context_window", ctypes.c_int),
+        ("use_causal_conv", ctypes.c_int),
+        ("use_conv_in", ctypes.c_int),
+        ("num_scales", ctypes.c_int),
+        ("upsample_scales", ctypes.c_int * PWG_MAX_SCALES),
+    ]
+
+
+def _needs_build():
+    if not os.path.exists(LIB_PATH):
+        return True
+    t = os.path.getmtime(LIB_PATH)
+    return any(os.path.getmtime(p) > t for p in CSRC + HEADERS)
+
+
+def build(force=False, verbose=False):
+    """Compile the HIP kernels + C-ABI into parallelwavegan_amd/lib/libpwg_hip.so (gfx950)."""
+    if not force and not _needs_build():
+        return LIB_PATH
+    os.makedirs(LIB_DIR, exist_ok=True)
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    tmp = LIB_PATH + ".tmp.%d" % os.getpid()
+    cmd = [
+        hipcc,
+        f"--offload-arch={OFFLOAD_ARCH}",
+        "-O3",
+        "-std=c++17",
+        "-fPIC",
+        "-shared",
+        "-fvisibility=hidden",
+        "-mcode-object-version=5",
+        "-Wall",
+        "-o",
+        tmp,
+    ] + CSRC
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError("hipcc failed:\n" + " ".join(cmd) + "\n" + res.stdout + res.stderr)
+    if verbose and (res.stdout or res.stderr):
+        print(res.stdout + res.stderr)
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load():
+    """Load the built library (raises if it is missing: no CPU fallback exists)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            )
+        import torch  # noqa: F401  (bind our NEEDED libamdhip64.so.7 to torch's HIP runtime)
+
+        lib = ctypes.CDLL(LIB_PATH)
+        vp = ctypes.c_void_p
+        ll = ctypes.c_longlong
+        lib.pwg_abi_version.restype = ctypes.c_int
+        lib.pwg_last_error.restype = ctypes.c_char_p
+        lib.pwg_create.argtypes = [ctypes.POINTER(PwgConfig), ctypes.c_int, ctypes.POINTER(vp)]
+        lib.pwg_destroy.argtypes = [vp]
+        lib.pwg_destroy.restype = None
+        for name in ("pwg_receptive_field_size", "pwg_upsample_factor", "pwg_ref_weight_count",
+                     "pwg_packed_weight_count"):
+            getattr(lib, name).argtypes = [vp]
+            getattr(lib, name).restype = ll
+        lib.pwg_pack_weights.argtypes = [vp, vp, vp]
+        lib.pwg_plan_create.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ll), ctypes.c_int, ctypes.POINTER(vp)]
+        lib.pwg_plan_destroy.argtypes = [vp]
+        lib.pwg_plan_destroy.restype = None
+        for name in ("pwg_plan_total_samples", "pwg_plan_padded_samples", "pwg_plan_workspace_bytes"):
+            getattr(lib, name).argtypes = [vp]
+            getattr(lib, name).restype = ll
+        lib.pwg_run.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp]
+        lib.pwg_set_timing.argtypes = [vp, ctypes.c_int]
+        lib.pwg_timing_collect.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ll)]
+        if lib.pwg_abi_version() != 1:
+            raise RuntimeError("libpwg_hip ABI version mismatch")
+        _lib = lib
+        return lib
+
+
+_ERRORS = {
+    PWG_ERR_INVALID: ValueError,
+    PWG_ERR_ASSERT: AssertionError,
+    PWG_ERR_HIP: RuntimeError,
+    PWG_ERR_UNSUPPORTED: NotImplementedError,
+}
+
+
+def check(rc):
+    """Raise the reference's exception type for a non-zero status (include/pwg.h)."""
+    if rc == PWG_OK:
+        return
+    msg = load().pwg_last_error().decode(errors="replace")
+    raise _ERRORS.get(rc, RuntimeError)(msg)

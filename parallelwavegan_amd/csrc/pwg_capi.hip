@@ -1,0 +1,480 @@
+// C-ABI of the engine (include/pwg.h): config validation, weight packing, batch planning,
+// launch sequencing and HIP-event timing. Kernels live in pwg_kernels.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/pwg.h"
+#include "pwg_internal.h"
+
+using namespace pwg;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  return fail(PWG_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+size_t align64(size_t n) { return (n + 63) / 64 * 64; }
+size_t align_bytes(size_t n) { return (n + 255) / 256 * 256; }
+
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = true;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) { ok = false; return; }
+    if (prev != dev && hipSetDevice(dev) != hipSuccess) ok = false;
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+struct TimingRecord {
+  int bucket;
+  hipEvent_t start, stop;
+};
+
+}  // namespace
+
+struct PwgHandle {
+  PwgConfig cfg;
+  int device;
+  // derived shapes
+  int R, G, GH, GHPAD, MT, S, M2T, A, KS, KW, O, L, lps, K1, K1pad, NQ;
+  std::vector<int> dil;
+  // packed image offsets (floats)
+  size_t off_first_w, off_first_b, off_conv_in, off_taps;
+  size_t off_layers, layer_stride, lo_wg, lo_bg, lo_w2, lo_b2;
+  size_t off_head_w1, off_head_b1, off_head_w2, off_head_b2, packed_total;
+  long long ref_total;
+  // timing
+  bool timing = false;
+  std::vector<TimingRecord> records;
+  std::vector<hipEvent_t> event_pool;
+};
+
+struct PwgPlan {
+  PwgHandle* h;
+  int layout;
+  int n_utts;
+  std::vector<UttDesc> utts;
+  long long n_tiles, Tpad, F_total, T_total;
+  UttDesc* d_utts = nullptr;
+  int* d_tile_utt = nullptr;
+  // workspace offsets (bytes)
+  size_t ws_x0, ws_x1, ws_skip, ws_cup, ws_c1, ws_total;
+};
+
+extern "C" {
+
+int pwg_abi_version(void) { return PWG_ABI_VERSION; }
+const char* pwg_last_error(void) { return g_err.c_str(); }
+
+int pwg_create(const PwgConfig* cfg, int device, PwgHandle** out) {
+  if (!cfg || !out) return fail(PWG_ERR_INVALID, "null argument");
+  const PwgConfig& c = *cfg;
+  if (c.in_channels != 1) return fail(PWG_ERR_UNSUPPORTED, "in_channels != 1 is not supported");
+  if (c.out_channels < 1) return fail(PWG_ERR_INVALID, "out_channels must be >= 1");
+  if (c.layers < 1 || c.stacks < 1) return fail(PWG_ERR_INVALID, "layers and stacks must be >= 1");
+  if (c.layers % c.stacks != 0) return fail(PWG_ERR_ASSERT, "layers % stacks == 0");
+  if (c.kernel_size < 1) return fail(PWG_ERR_INVALID, "kernel_size must be >= 1");
+  if (!c.use_causal_conv && (c.kernel_size - 1) % 2 != 0)
+    return fail(PWG_ERR_ASSERT, "Not support even number kernel size.");
+  if (c.gate_channels < 2 || c.gate_channels % 2 != 0)
+    return fail(PWG_ERR_INVALID, "gate_channels must be even (split into tanh/sigmoid halves)");
+  if (c.residual_channels < 1 || c.skip_channels < 1 || c.aux_channels < 1)
+    return fail(PWG_ERR_UNSUPPORTED, "residual/skip/aux channels must be >= 1");
+  if (c.aux_context_window < 0) return fail(PWG_ERR_INVALID, "aux_context_window must be >= 0");
+  if (c.num_scales < 1 || c.num_scales > PWG_MAX_SCALES)
+    return fail(PWG_ERR_UNSUPPORTED, "1..8 upsample scales supported");
+  for (int i = 0; i < c.num_scales; ++i)
+    if (c.upsample_scales[i] < 1) return fail(PWG_ERR_INVALID, "upsample scales must be >= 1");
+
+  PwgHandle* h = new PwgHandle();
+  h->cfg = c;
+  h->device = device;
+  h->R = c.residual_channels;
+  h->G = c.gate_channels;
+  h->GH = c.gate_channels / 2;
+  h->S = c.skip_channels;
+  h->A = c.aux_channels;
+  h->KS = c.kernel_size;
+  h->O = c.out_channels;
+  h->L = c.layers;
+  h->lps = c.layers / c.stacks;
+  h->KW = c.use_conv_in ? (c.use_causal_conv ? c.aux_context_window + 1 : 2 * c.aux_context_window + 1) : 1;
+  h->GHPAD = h->GH <= 16 ? 16 : (h->GH + 31) / 32 * 32;
+  h->MT = h->GHPAD <= 16 ? 1 : h->GHPAD / 16;
+  h->NQ = h->GHPAD / 2;
+  h->M2T = (h->S + h->R + 31) / 32;
+  h->K1 = h->KS * h->R + h->A;
+  h->K1pad = (h->K1 + KC - 1) / KC * KC;
+  if (!(h->MT == 1 || h->MT == 2 || h->MT == 4) || !(h->M2T == 1 || h->M2T == 2 || h->M2T == 4)) {
+    delete h;
+    return fail(PWG_ERR_UNSUPPORTED, "gate_channels <= 128 and skip+residual <= 128 supported");
+  }
+  if (h->S > 128) { delete h; return fail(PWG_ERR_UNSUPPORTED, "skip_channels <= 128 supported"); }
+  for (int l = 0; l < h->L; ++l) {
+    long long d = 1LL << (l % h->lps);
+    if (d > (1LL << 24)) { delete h; return fail(PWG_ERR_UNSUPPORTED, "dilation too large"); }
+    h->dil.push_back((int)d);
+  }
+  // upsampler LDS widths for one TILE of output: a stage whose output spans W samples reads at
+  // most ceil((W-1)/s)+3 input samples (any alignment, causal or not)
+  {
+    long long w = TILE;
+    for (int i = c.num_scales - 1; i >= 0; --i) {
+      const int s = c.upsample_scales[i];
+      w = (w - 1 + s - 1) / s + 3;
+      if (w > UP_MAXW) { delete h; return fail(PWG_ERR_UNSUPPORTED, "upsample stage too wide for LDS"); }
+    }
+  }
+  // packed image layout
+  size_t o = 0;
+  h->off_first_w = o; o += align64(h->R);
+  h->off_first_b = o; o += align64(h->R);
+  h->off_conv_in = o; o += align64((size_t)h->A * h->A * h->KW);
+  h->off_taps = o;
+  {
+    size_t nt = 0;
+    for (int i = 0; i < c.num_scales; ++i) nt += 2 * c.upsample_scales[i] + 1;
+    o += align64(nt);
+  }
+  h->lo_wg = 0;
+  h->lo_bg = h->lo_wg + align64((size_t)(h->K1pad / 2) * h->MT * 64);
+  h->lo_w2 = h->lo_bg + align64(2 * h->GHPAD);
+  h->lo_b2 = h->lo_w2 + align64((size_t)h->NQ * h->M2T * 64);
+  h->layer_stride = h->lo_b2 + align64(32 * h->M2T);
+  h->off_layers = o; o += h->layer_stride * h->L;
+  h->off_head_w1 = o; o += align64((size_t)h->S * h->S);
+  h->off_head_b1 = o; o += align64(h->S);
+  h->off_head_w2 = o; o += align64((size_t)h->O * h->S);
+  h->off_head_b2 = o; o += align64(h->O);
+  h->packed_total = o;
+
+  long long rt = 0;
+  rt += h->R + h->R;
+  if (c.use_conv_in) rt += (long long)h->A * h->A * h->KW;
+  for (int i = 0; i < c.num_scales; ++i) rt += 2 * c.upsample_scales[i] + 1;
+  rt += (long long)h->L * ((long long)h->G * h->R * h->KS + h->G + (long long)h->G * h->A +
+                           (long long)h->S * h->GH + h->S + (long long)h->R * h->GH + h->R);
+  rt += (long long)h->S * h->S + h->S + (long long)h->O * h->S + h->O;
+  h->ref_total = rt;
+  *out = h;
+  return PWG_OK;
+}
+
+void pwg_destroy(PwgHandle* h) {
+  if (!h) return;
+  {
+    DeviceGuard g(h->device);
+    for (auto& r : h->records) { (void)hipEventDestroy(r.start); (void)hipEventDestroy(r.stop); }
+    for (auto e : h->event_pool) (void)hipEventDestroy(e);
+  }
+  delete h;
+}
+
+long long pwg_receptive_field_size(const PwgHandle* h) {
+  long long s = 0;
+  for (int d : h->dil) s += d;
+  return (long long)(h->KS - 1) * s + 1;
+}
+
+long long pwg_upsample_factor(const PwgHandle* h) {
+  long long f = 1;
+  for (int i = 0; i < h->cfg.num_scales; ++i) f *= h->cfg.upsample_scales[i];
+  return f;
+}
+
+long long pwg_ref_weight_count(const PwgHandle* h) { return h->ref_total; }
+long long pwg_packed_weight_count(const PwgHandle* h) { return (long long)h->packed_total; }
+
+int pwg_pack_weights(const PwgHandle* h, const float* ref, float* pk) {
+  if (!h || !ref || !pk) return fail(PWG_ERR_INVALID, "null argument");
+  std::memset(pk, 0, sizeof(float) * h->packed_total);
+  const PwgConfig& c = h->cfg;
+  const int R = h->R, G = h->G, GH = h->GH, GHPAD = h->GHPAD, MT = h->MT, S = h->S, M2T = h->M2T;
+  const int A = h->A, KS = h->KS, KW = h->KW, O = h->O;
+  const float* p = ref;
+  for (int i = 0; i < R; ++i) pk[h->off_first_w + i] = *p++;
+  for (int i = 0; i < R; ++i) pk[h->off_first_b + i] = *p++;
+  if (c.use_conv_in) {
+    for (size_t i = 0; i < (size_t)A * A * KW; ++i) pk[h->off_conv_in + i] = *p++;
+  } else {
+    pk[h->off_conv_in] = 1.f;  // unused (identity path)
+  }
+  {
+    size_t t = 0;
+    for (int i = 0; i < c.num_scales; ++i)
+      for (int k = 0; k < 2 * c.upsample_scales[i] + 1; ++k) pk[h->off_taps + t++] = *p++;
+  }
+  for (int l = 0; l < h->L; ++l) {
+    const float* wd = p; p += (size_t)G * R * KS;   // conv.weight [G][R][KS]
+    const float* bd = p; p += G;                      // conv.bias
+    const float* wa = p; p += (size_t)G * A;          // conv1x1_aux.weight [G][A]
+    const float* ws = p; p += (size_t)S * GH;         // conv1x1_skip.weight [S][GH]
+    const float* bs = p; p += S;
+    const float* wo = p; p += (size_t)R * GH;         // conv1x1_out.weight [R][GH]
+    const float* bo = p; p += R;
+    float* L0 = pk + h->off_layers + h->layer_stride * l;
+    // packed gate row -> reference gate row (or -1 for zero padding rows)
+    auto gate_row = [&](int prow) -> int {
+      if (prow < GHPAD) return prow < GH ? prow : -1;
+      const int q = prow - GHPAD;
+      return q < GH ? GH + q : -1;
+    };
+    auto wcat = [&](int grow, int k) -> float {
+      if (grow < 0) return 0.f;
+      if (k < KS * R) {
+        const int tap = k / R, ch = k % R;
+        return wd[((size_t)grow * R + ch) * KS + tap];
+      }
+      if (k < KS * R + A) return wa[(size_t)grow * A + (k - KS * R)];
+      return 0.f;
+    };
+    float* wg = L0 + h->lo_wg;
+    for (int s = 0; s < h->K1pad / 2; ++s)
+      for (int m = 0; m < MT; ++m)
+        for (int lane = 0; lane < 64; ++lane)
+          wg[((size_t)s * MT + m) * 64 + lane] = wcat(gate_row(32 * m + (lane & 31)), 2 * s + (lane >> 5));
+    float* bg = L0 + h->lo_bg;
+    for (int prow = 0; prow < 2 * GHPAD; ++prow) {
+      const int gr = gate_row(prow);
+      bg[prow] = gr < 0 ? 0.f : bd[gr];
+    }
+    float* w2 = L0 + h->lo_w2;
+    for (int q = 0; q < h->NQ; ++q)
+      for (int m2 = 0; m2 < M2T; ++m2)
+        for (int lane = 0; lane < 64; ++lane) {
+          const int row2 = 32 * m2 + (lane & 31);
+          const int r = q & 15, gm = q >> 4;
+          const int ch = 32 * gm + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          float v = 0.f;
+          if (ch < GH) {
+            if (row2 < S) v = ws[(size_t)row2 * GH + ch];
+            else if (row2 < S + R) v = wo[(size_t)(row2 - S) * GH + ch];
+          }
+          w2[((size_t)q * M2T + m2) * 64 + lane] = v;
+        }
+    float* b2 = L0 + h->lo_b2;
+    for (int row2 = 0; row2 < 32 * M2T; ++row2)
+      b2[row2] = row2 < S ? bs[row2] : (row2 < S + R ? bo[row2 - S] : 0.f);
+  }
+  for (size_t i = 0; i < (size_t)S * S; ++i) pk[h->off_head_w1 + i] = *p++;
+  for (int i = 0; i < S; ++i) pk[h->off_head_b1 + i] = *p++;
+  for (size_t i = 0; i < (size_t)O * S; ++i) pk[h->off_head_w2 + i] = *p++;
+  for (int i = 0; i < O; ++i) pk[h->off_head_b2 + i] = *p++;
+  if ((long long)(p - ref) != h->ref_total) return fail(PWG_ERR_INVALID, "internal: weight count mismatch");
+  return PWG_OK;
+}
+
+int pwg_plan_create(PwgHandle* h, int n_utts, const long long* frames, int layout, PwgPlan** out) {
+  if (!h || !out || (n_utts > 0 && !frames)) return fail(PWG_ERR_INVALID, "null argument");
+  if (n_utts < 1) return fail(PWG_ERR_INVALID, "n_utts must be >= 1");
+  if (layout != PWG_LAYOUT_INFERENCE && layout != PWG_LAYOUT_FORWARD)
+    return fail(PWG_ERR_INVALID, "unknown input layout");
+  if (!h->cfg.use_conv_in && h->cfg.aux_context_window != 0)
+    return fail(PWG_ERR_ASSERT, "c.size(-1) == z.size(-1): UpsampleNetwork needs aux_context_window == 0");
+  const long long H = pwg_upsample_factor(h);
+  const int w = h->cfg.aux_context_window;
+  PwgPlan* p = new PwgPlan();
+  p->h = h;
+  p->layout = layout;
+  p->n_utts = n_utts;
+  long long seg = 0, fb = 0, io = 0, mel = 0;
+  for (int u = 0; u < n_utts; ++u) {
+    const long long f = frames[u];
+    if (f < 1) { delete p; return fail(PWG_ERR_INVALID, "every utterance needs >= 1 mel frame"); }
+    if (layout == PWG_LAYOUT_FORWARD && f != frames[0]) {
+      delete p;
+      return fail(PWG_ERR_INVALID, "forward layout needs equal-length batch items");
+    }
+    UttDesc d;
+    d.seg_base = seg;
+    d.T = f * H;
+    d.frame_base = fb;
+    d.frames = f;
+    d.mel_off = mel;
+    d.io_off = io;
+    p->utts.push_back(d);
+    seg += (d.T + SEG - 1) / SEG * SEG;
+    fb += f;
+    io += d.T;
+    mel += layout == PWG_LAYOUT_INFERENCE ? f * h->A : (f + 2 * w) * h->A;
+  }
+  p->Tpad = seg;
+  p->F_total = fb;
+  p->T_total = io;
+  p->n_tiles = seg / TILE;
+  std::vector<int> tile_utt(p->n_tiles);
+  for (int u = 0; u < n_utts; ++u) {
+    const long long b = p->utts[u].seg_base / TILE;
+    const long long e = (p->utts[u].seg_base + (p->utts[u].T + SEG - 1) / SEG * SEG) / TILE;
+    for (long long t = b; t < e; ++t) tile_utt[t] = u;
+  }
+  size_t o = 0;
+  p->ws_x0 = o; o += align_bytes(sizeof(float) * h->R * p->Tpad);
+  p->ws_x1 = o; o += align_bytes(sizeof(float) * h->R * p->Tpad);
+  p->ws_skip = o; o += align_bytes(sizeof(float) * h->S * p->Tpad);
+  p->ws_cup = o; o += align_bytes(sizeof(float) * h->A * p->Tpad);
+  p->ws_c1 = o; o += align_bytes(sizeof(float) * h->A * p->F_total);
+  p->ws_total = o;
+
+  DeviceGuard g(h->device);
+  if (!g.ok) { delete p; return fail(PWG_ERR_HIP, "hipSetDevice failed"); }
+  hipError_t e = hipMalloc(&p->d_utts, sizeof(UttDesc) * n_utts);
+  if (e == hipSuccess) e = hipMalloc(&p->d_tile_utt, sizeof(int) * p->n_tiles);
+  if (e == hipSuccess) e = hipMemcpy(p->d_utts, p->utts.data(), sizeof(UttDesc) * n_utts, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(p->d_tile_utt, tile_utt.data(), sizeof(int) * p->n_tiles, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    const int rc = hip_fail(e, "plan descriptor upload");
+    pwg_plan_destroy(p);
+    return rc;
+  }
+  *out = p;
+  return PWG_OK;
+}
+
+void pwg_plan_destroy(PwgPlan* p) {
+  if (!p) return;
+  {
+    DeviceGuard g(p->h->device);
+    if (p->d_utts) (void)hipFree(p->d_utts);
+    if (p->d_tile_utt) (void)hipFree(p->d_tile_utt);
+  }
+  delete p;
+}
+
+long long pwg_plan_total_samples(const PwgPlan* p) { return p->T_total; }
+long long pwg_plan_padded_samples(const PwgPlan* p) { return p->Tpad; }
+long long pwg_plan_workspace_bytes(const PwgPlan* p) { return (long long)p->ws_total; }
+
+static hipEvent_t pool_get(PwgHandle* h) {
+  if (!h->event_pool.empty()) {
+    hipEvent_t e = h->event_pool.back();
+    h->event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* noise, const float* mean,
+            const float* scale, float* out, void* workspace, void* stream) {
+  if (!p || !packed || !mel || !noise || !out || !workspace) return fail(PWG_ERR_INVALID, "null argument");
+  if (((uintptr_t)workspace & 255) != 0) return fail(PWG_ERR_INVALID, "workspace must be 256-byte aligned");
+  if ((mean == nullptr) != (scale == nullptr)) return fail(PWG_ERR_INVALID, "mean and scale go together");
+  if (mean != nullptr && p->layout != PWG_LAYOUT_INFERENCE)
+    return fail(PWG_ERR_INVALID, "normalize_before is an inference() option");
+  PwgHandle* h = p->h;
+  DeviceGuard g(h->device);
+  if (!g.ok) return fail(PWG_ERR_HIP, "hipSetDevice failed");
+  hipStream_t s = (hipStream_t)stream;
+  char* ws = (char*)workspace;
+  float* x0 = (float*)(ws + p->ws_x0);
+  float* x1 = (float*)(ws + p->ws_x1);
+  float* skip = (float*)(ws + p->ws_skip);
+  float* cup = (float*)(ws + p->ws_cup);
+  float* c1 = (float*)(ws + p->ws_c1);
+
+  auto timed = [&](int bucket, auto&& launch) -> hipError_t {
+    if (!h->timing) return launch();
+    hipEvent_t a = pool_get(h), b = pool_get(h);
+    if (!a || !b) return hipErrorOutOfMemory;
+    hipError_t e = hipEventRecord(a, s);
+    if (e != hipSuccess) return e;
+    e = launch();
+    if (e != hipSuccess) return e;
+    e = hipEventRecord(b, s);
+    h->records.push_back({bucket, a, b});
+    return e;
+  };
+
+  hipError_t e;
+  ConvInArgs ca;
+  ca.mel = mel; ca.mean = mean; ca.scale = scale; ca.w = packed + h->off_conv_in; ca.c1 = c1;
+  ca.utts = p->d_utts; ca.n_utts = p->n_utts; ca.F_total = p->F_total; ca.A = h->A; ca.KW = h->KW;
+  ca.ctx = h->cfg.aux_context_window; ca.layout = p->layout; ca.use_conv_in = h->cfg.use_conv_in;
+  e = timed(PWG_KERNEL_CONV_IN, [&] { return launch_conv_in(ca, s); });
+  if (e != hipSuccess) return hip_fail(e, "conv_in launch");
+
+  UpsampleArgs ua;
+  ua.c1 = c1; ua.cup = cup; ua.taps = packed + h->off_taps; ua.tile_utt = p->d_tile_utt; ua.utts = p->d_utts;
+  ua.F_total = p->F_total; ua.Tpad = p->Tpad; ua.A = h->A; ua.n_scales = h->cfg.num_scales;
+  for (int i = 0; i < MAX_SCALES; ++i) ua.scales[i] = i < h->cfg.num_scales ? h->cfg.upsample_scales[i] : 1;
+  ua.causal = h->cfg.use_causal_conv;
+  e = timed(PWG_KERNEL_UPSAMPLE, [&] { return launch_upsample(ua, p->n_tiles, s); });
+  if (e != hipSuccess) return hip_fail(e, "upsample launch");
+
+  FirstConvArgs fa;
+  fa.noise = noise; fa.w = packed + h->off_first_w; fa.b = packed + h->off_first_b; fa.x = x0;
+  fa.tile_utt = p->d_tile_utt; fa.utts = p->d_utts; fa.Tpad = p->Tpad; fa.R = h->R;
+  e = timed(PWG_KERNEL_FIRST_CONV, [&] { return launch_first_conv(fa, p->n_tiles, s); });
+  if (e != hipSuccess) return hip_fail(e, "first_conv launch");
+
+  float* xin = x0;
+  float* xout = x1;
+  for (int l = 0; l < h->L; ++l) {
+    const float* L0 = packed + h->off_layers + h->layer_stride * l;
+    LayerArgs la;
+    la.x_in = xin; la.x_out = xout; la.skip = skip; la.cup = cup;
+    la.wg = L0 + h->lo_wg; la.bg = L0 + h->lo_bg; la.w2 = L0 + h->lo_w2; la.b2 = L0 + h->lo_b2;
+    la.tile_utt = p->d_tile_utt; la.utts = p->d_utts; la.Tpad = p->Tpad;
+    la.R = h->R; la.S = h->S; la.A = h->A; la.KS = h->KS; la.K1pad = h->K1pad; la.dil = h->dil[l];
+    la.tap_center = h->cfg.use_causal_conv ? h->KS - 1 : (h->KS - 1) / 2;
+    la.first = l == 0;
+    e = timed(PWG_KERNEL_RESIDUAL_LAYER, [&] { return launch_layer(la, h->MT, h->M2T, p->n_tiles, s); });
+    if (e != hipSuccess) return hip_fail(e, "residual layer launch");
+    std::swap(xin, xout);
+  }
+
+  HeadArgs ha;
+  ha.skip = skip; ha.w1 = packed + h->off_head_w1; ha.b1 = packed + h->off_head_b1;
+  ha.w2 = packed + h->off_head_w2; ha.b2 = packed + h->off_head_b2; ha.out = out;
+  ha.tile_utt = p->d_tile_utt; ha.utts = p->d_utts; ha.Tpad = p->Tpad; ha.S = h->S; ha.O = h->O;
+  ha.skip_scale = (float)std::sqrt(1.0 / h->L);
+  if (p->layout == PWG_LAYOUT_INFERENCE) { ha.out_stride_t = h->O; ha.out_stride_o = 1; }
+  else { ha.out_stride_t = 1; ha.out_stride_o = p->utts[0].T; }
+  e = timed(PWG_KERNEL_HEAD, [&] { return launch_head(ha, p->n_tiles, s); });
+  if (e != hipSuccess) return hip_fail(e, "head launch");
+  return PWG_OK;
+}
+
+int pwg_set_timing(PwgHandle* h, int enable) {
+  if (!h) return fail(PWG_ERR_INVALID, "null handle");
+  h->timing = enable != 0;
+  return PWG_OK;
+}
+
+int pwg_timing_collect(PwgHandle* h, double* ms, long long* launches) {
+  if (!h || !ms || !launches) return fail(PWG_ERR_INVALID, "null argument");
+  DeviceGuard g(h->device);
+  for (auto& r : h->records) {
+    hipError_t e = hipEventSynchronize(r.stop);
+    float t = 0.f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&t, r.start, r.stop);
+    if (e != hipSuccess) return hip_fail(e, "timing collect");
+    ms[r.bucket] += t;
+    launches[r.bucket] += 1;
+    h->event_pool.push_back(r.start);
+    h->event_pool.push_back(r.stop);
+  }
+  h->records.clear();
+  return PWG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,330 @@
+"""Host-side engine over the C-ABI: config translation, weight flattening/packing, batch plans,
+workspace and launch on the caller's current HIP stream.
+
+This module is plumbing around ``libpwg_hip.so``; all generator arithmetic runs in the HIP
+kernels. torch is used for device memory and the current stream only.
+"""
+
+import ctypes
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+def _scales(params):
+    return list(params.get("upsample_params", {}).get("upsample_scales", [4, 4, 4, 4]))
+
+
+def make_config(params):
+    """Translate ParallelWaveGANGenerator constructor kwargs (models/parallel_wavegan.py:24-43)
+    into a PwgConfig, raising NotImplementedError for options outside the hot path."""
+    up = dict(params.get("upsample_params", {"upsample_scales": [4, 4, 4, 4]}))
+    if not params.get("upsample_conditional_features", True):
+        raise NotImplementedError("upsample_conditional_features=False is not supported")
+    net = params.get("upsample_net", "ConvInUpsampleNetwork")
+    if net not in ("ConvInUpsampleNetwork", "UpsampleNetwork"):
+        raise NotImplementedError(f"upsample_net={net!r} is not supported")
+    if up.get("nonlinear_activation") is not None:
+        raise NotImplementedError("upsample nonlinear_activation is not supported")
+    if up.get("freq_axis_kernel_size", 1) != 1:
+        raise NotImplementedError("freq_axis_kernel_size != 1 is not supported")
+    if up.get("interpolate_mode", "nearest") != "nearest":
+        raise NotImplementedError("only nearest interpolation is supported")
+    scales = list(up.get("upsample_scales", [4, 4, 4, 4]))
+    if not 1 <= len(scales) <= _lib.PWG_MAX_SCALES:
+        raise NotImplementedError("1..8 upsample scales supported")
+    cfg = _lib.PwgConfig()
+    cfg.in_channels = int(params.get("in_channels", 1))
+    cfg.out_channels = int(params.get("out_channels", 1))
+    cfg.kernel_size = int(params.get("kernel_size", 3))
+    cfg.layers = int(params.get("layers", 30))
+    cfg.stacks = int(params.get("stacks", 3))
+    cfg.residual_channels = int(params.get("residual_channels", 64))
+    cfg.gate_channels = int(params.get("gate_channels", 128))
+    cfg.skip_channels = int(params.get("skip_channels", 64))
+    cfg.aux_channels = int(params.get("aux_channels", 80))
+    cfg.aux_context_window = int(params.get("aux_context_window", 2))
+    cfg.use_causal_conv = int(bool(params.get("use_causal_conv", False)))
+    cfg.use_conv_in = int(net == "ConvInUpsampleNetwork")
+    cfg.num_scales = len(scales)
+    for i, s in enumerate(scales):
+        cfg.upsample_scales[i] = int(s)
+    return cfg
+
+
+def ref_weight_keys(params):
+    """(state-dict key, rows) in the C-ABI's reference order (include/pwg.h,
+    pwg_ref_weight_count). key is ``None`` for an absent bias (bias=False), passed as ``rows``
+    zeros."""
+    L = int(params.get("layers", 30))
+    G = int(params.get("gate_channels", 128))
+    S = int(params.get("skip_channels", 64))
+    R = int(params.get("residual_channels", 64))
+    net = params.get("upsample_net", "ConvInUpsampleNetwork")
+    bias = params.get("bias", True)
+    keys = [("first_conv.weight", 0), ("first_conv.bias", 0)]
+    if net == "ConvInUpsampleNetwork":
+        keys.append(("upsample_net.conv_in.weight", 0))
+        prefix = "upsample_net.upsample.up_layers"
+    else:
+        prefix = "upsample_net.up_layers"
+    for i in range(len(_scales(params))):
+        keys.append((f"{prefix}.{2 * i + 1}.weight", 0))
+    for l in range(L):
+        p = f"conv_layers.{l}"
+        keys += [
+            (f"{p}.conv.weight", 0),
+            (f"{p}.conv.bias" if bias else None, G),
+            (f"{p}.conv1x1_aux.weight", 0),
+            (f"{p}.conv1x1_skip.weight", 0),
+            (f"{p}.conv1x1_skip.bias" if bias else None, S),
+            (f"{p}.conv1x1_out.weight", 0),
+            (f"{p}.conv1x1_out.bias" if bias else None, R),
+        ]
+    keys += [
+        ("last_conv_layers.1.weight", 0),
+        ("last_conv_layers.1.bias", 0),
+        ("last_conv_layers.3.weight", 0),
+        ("last_conv_layers.3.bias", 0),
+    ]
+    return keys
+
+
+def _to_numpy(v):
+    return v.detach().cpu().numpy() if torch.is_tensor(v) else np.asarray(v)
+
+
+def fold_weight_norm(state):
+    """{k: ndarray} with weight_g/weight_v pairs folded to ``weight`` = g * v / ||v|| (norm over
+    every dim but 0), the torch.nn.utils.weight_norm(dim=0) definition used by
+    apply_weight_norm/remove_weight_norm (models/parallel_wavegan.py:175-195). Load-time
+    parameter preprocessing, not part of the forward."""
+    out = {}
+    for k, v in state.items():
+        if k.endswith(".weight_g"):
+            continue
+        if k.endswith(".weight_v"):
+            base = k[: -len(".weight_v")]
+            g = torch.from_numpy(np.ascontiguousarray(_to_numpy(state[base + ".weight_g"]), np.float32))
+            vv = torch.from_numpy(np.ascontiguousarray(_to_numpy(v), np.float32))
+            out[base + ".weight"] = torch._weight_norm(vv, g, 0).numpy()
+        else:
+            out[k] = _to_numpy(v)
+    return out
+
+
+class HostHandle:
+    """A pwg handle used for host-only work (packing, shape queries); needs no GPU."""
+
+    def __init__(self, params):
+        self._lib = _lib.load()
+        self.params = dict(params)
+        self.config = make_config(self.params)
+        h = ctypes.c_void_p()
+        _lib.check(self._lib.pwg_create(ctypes.byref(self.config), 0, ctypes.byref(h)))
+        self._h = h
+        self.receptive_field_size = self._lib.pwg_receptive_field_size(h)
+        self.upsample_factor = self._lib.pwg_upsample_factor(h)
+        self.ref_weight_count = self._lib.pwg_ref_weight_count(h)
+        self.packed_weight_count = self._lib.pwg_packed_weight_count(h)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            self._lib.pwg_destroy(h)
+            self._h = None
+
+    def flatten_state_dict(self, state):
+        """Reference-order flat float32 vector (include/pwg.h) from a state dict."""
+        folded = fold_weight_norm(state)
+        fill = []
+        for k, rows in ref_weight_keys(self.params):
+            if k is None:
+                fill.append(np.zeros(rows, np.float32))
+                continue
+            if k not in folded:
+                raise KeyError(f"missing generator weight {k!r}")
+            fill.append(np.ascontiguousarray(folded[k], dtype=np.float32).reshape(-1))
+        flat = np.concatenate(fill).astype(np.float32)
+        if flat.size != self.ref_weight_count:
+            raise ValueError(f"weight count {flat.size} != expected {self.ref_weight_count}")
+        return flat
+
+    def pack(self, state):
+        """Host-side packed image (np.float32, pwg_packed_weight_count)."""
+        flat = self.flatten_state_dict(state)
+        packed = np.empty(self.packed_weight_count, np.float32)
+        _lib.check(self._lib.pwg_pack_weights(self._h, flat.ctypes.data, packed.ctypes.data))
+        return packed
+
+
+class Plan:
+    """A planned batch (pwg_plan_create): utterance descriptors uploaded once, reusable for
+    every batch of the same lengths."""
+
+    def __init__(self, engine, frames, layout):
+        lib = _lib.load()
+        self.engine = engine
+        self.frames = tuple(int(f) for f in frames)
+        self.layout = layout
+        arr = (ctypes.c_longlong * len(self.frames))(*self.frames)
+        ptr = ctypes.c_void_p()
+        _lib.check(lib.pwg_plan_create(engine._h, len(self.frames), arr, layout, ctypes.byref(ptr)))
+        self._p = ptr
+        self.total_samples = lib.pwg_plan_total_samples(ptr)
+        self.padded_samples = lib.pwg_plan_padded_samples(ptr)
+        self.workspace_bytes = lib.pwg_plan_workspace_bytes(ptr)
+        self._lib = lib
+
+    def __del__(self):
+        p = getattr(self, "_p", None)
+        if p is not None and p.value:
+            self._lib.pwg_plan_destroy(p)
+            self._p = None
+
+
+class Engine:
+    """One generator configuration on one device.
+
+    ``load_state_dict`` takes a generator state dict (folded or weight-norm form), packs it with
+    pwg_pack_weights and uploads the image; ``run`` launches one forward of a plan.
+    """
+
+    def __init__(self, params, device):
+        self.params = dict(params)
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise RuntimeError("the PWG engine runs on a ROCm GPU only (no CPU fallback)")
+        lib = _lib.load()
+        self._lib = lib
+        self.config = make_config(self.params)
+        h = ctypes.c_void_p()
+        idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        _lib.check(lib.pwg_create(ctypes.byref(self.config), idx, ctypes.byref(h)))
+        self._h = h
+        self.receptive_field_size = lib.pwg_receptive_field_size(h)
+        self.upsample_factor = lib.pwg_upsample_factor(h)
+        self.ref_weight_count = lib.pwg_ref_weight_count(h)
+        self.packed_weight_count = lib.pwg_packed_weight_count(h)
+        self.packed = None
+        self._plans = OrderedDict()
+        self._workspace = None
+        self.timing_enabled = False
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            self._plans = OrderedDict()
+            self._lib.pwg_destroy(h)
+            self._h = None
+
+    # ---------------------------------------------------------------- weights
+    flatten_state_dict = HostHandle.flatten_state_dict
+    pack = HostHandle.pack
+
+    def load_state_dict(self, state):
+        packed = self.pack(state)
+        self.set_packed(torch.from_numpy(packed).to(self.device))
+        return self.packed
+
+    def set_packed(self, packed_dev):
+        if packed_dev.device != self.device or packed_dev.dtype != torch.float32:
+            raise ValueError("packed weights must be float32 on the engine's device")
+        if packed_dev.numel() != self.packed_weight_count or not packed_dev.is_contiguous():
+            raise ValueError("packed weight image has the wrong size")
+        self.packed = packed_dev
+
+    # ---------------------------------------------------------------- plans
+    def plan(self, frames, layout=_lib.PWG_LAYOUT_INFERENCE):
+        key = (tuple(int(f) for f in frames), layout)
+        p = self._plans.get(key)
+        if p is None:
+            p = Plan(self, key[0], layout)
+            self._plans[key] = p
+            while len(self._plans) > 16:
+                self._plans.popitem(last=False)
+        else:
+            self._plans.move_to_end(key)
+        return p
+
+    def workspace(self, nbytes):
+        if self._workspace is None or self._workspace.numel() < nbytes:
+            self._workspace = None
+            self._workspace = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=self.device)
+        return self._workspace
+
+    # ---------------------------------------------------------------- timing
+    def set_timing(self, enable):
+        self.timing_enabled = bool(enable)
+        _lib.check(self._lib.pwg_set_timing(self._h, int(enable)))
+
+    def collect_timing(self):
+        ms = (ctypes.c_double * len(_lib.KERNEL_BUCKETS))()
+        n = (ctypes.c_longlong * len(_lib.KERNEL_BUCKETS))()
+        _lib.check(self._lib.pwg_timing_collect(self._h, ms, n))
+        return {k: (ms[i], n[i]) for i, k in enumerate(_lib.KERNEL_BUCKETS)}
+
+    # ---------------------------------------------------------------- run
+    def run(self, plan, mel, noise, out, mean=None, scale=None, stream=None):
+        """Enqueue one forward of ``plan`` on ``stream`` (default: torch's current stream)."""
+        if self.packed is None:
+            raise RuntimeError("no weights loaded")
+        for name, t in (("mel", mel), ("noise", noise), ("out", out)):
+            if t.device != self.device or t.dtype != torch.float32 or not t.is_contiguous():
+                raise ValueError(f"{name} must be a contiguous float32 tensor on {self.device}")
+        A = self.config.aux_channels
+        w = self.config.aux_context_window
+        nf = sum(plan.frames)
+        want_mel = nf * A if plan.layout == _lib.PWG_LAYOUT_INFERENCE else len(plan.frames) * A * (plan.frames[0] + 2 * w)
+        if mel.numel() != want_mel:
+            raise ValueError(f"mel has {mel.numel()} elements, plan needs {want_mel}")
+        if noise.numel() != plan.total_samples:
+            raise ValueError(f"noise has {noise.numel()} elements, plan needs {plan.total_samples}")
+        if out.numel() != plan.total_samples * self.config.out_channels:
+            raise ValueError("output buffer has the wrong size")
+        mp = sp = None
+        if mean is not None:
+            mean = mean.to(self.device, torch.float32).contiguous()
+            scale = scale.to(self.device, torch.float32).contiguous()
+            mp, sp = mean.data_ptr(), scale.data_ptr()
+        ws = self.workspace(plan.workspace_bytes)
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device)
+        _lib.check(
+            self._lib.pwg_run(
+                plan._p,
+                self.packed.data_ptr(),
+                mel.data_ptr(),
+                noise.data_ptr(),
+                mp,
+                sp,
+                out.data_ptr(),
+                ws.data_ptr(),
+                stream.cuda_stream,
+            )
+        )
+        return out
+
+    def infer(self, mels, noises, mean=None, scale=None):
+        """Ragged batch of inference() calls in ONE engine pass.
+
+        mels: list of (T'_u, aux) float32 device tensors; noises: list of (T_u,) or (T_u, 1).
+        Returns a list of (T_u, out_channels) tensors (views of one output buffer).
+        """
+        frames = [int(m.shape[0]) for m in mels]
+        plan = self.plan(frames, _lib.PWG_LAYOUT_INFERENCE)
+        mel = torch.cat([m.reshape(-1) for m in mels]) if len(mels) > 1 else mels[0].reshape(-1).contiguous()
+        noise = torch.cat([n.reshape(-1) for n in noises]) if len(noises) > 1 else noises[0].reshape(-1).contiguous()
+        O = self.config.out_channels
+        out = torch.empty(plan.total_samples * O, dtype=torch.float32, device=self.device)
+        self.run(plan, mel, noise, out, mean, scale)
+        res, off = [], 0
+        H = self.upsample_factor
+        for f in frames:
+            T = f * H
+            res.append(out[off * O:(off + T) * O].view(T, O))
+            off += T
+        return res

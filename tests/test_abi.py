@@ -1,0 +1,153 @@
+"""The C-ABI library builds, loads and exports every symbol include/pwg.h declares; host-side
+logic (config validation -> exception mapping, weight counts, packing) behaves. CPU only: no
+call here launches a kernel or touches device memory."""
+
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+from parallelwavegan_amd import _lib, configs, synthetic
+from parallelwavegan_amd.engine import HostHandle, make_config, ref_weight_keys
+
+
+def _declared_symbols():
+    src = open(os.path.join(REPO, "include", "pwg.h")).read()
+    return sorted(set(re.findall(r"PWG_API\s+[\w\s\*]+?\b(pwg_\w+)\s*\(", src)))
+
+
+def test_header_declarations_match_binding_list():
+    assert _declared_symbols() == sorted(_lib.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol(built_lib):
+    for name in _declared_symbols():
+        assert hasattr(built_lib, name), name
+        assert ctypes.cast(getattr(built_lib, name), ctypes.c_void_p).value
+
+
+def test_library_exports_nothing_else(built_lib):
+    import subprocess
+
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = sorted({ln.split()[-1] for ln in out.splitlines() if " T " in ln})
+    assert exported == sorted(_lib.EXPORTED_SYMBOLS)
+
+
+def test_library_is_gfx950_code_object(built_lib):
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_abi_version(built_lib):
+    assert built_lib.pwg_abi_version() == 1
+
+
+@pytest.mark.parametrize("name", ["yesno_debug", "ljspeech_v1", "libritts_v1", "reference_test"])
+def test_weight_counts_match_state_dict(built_lib, name):
+    params = configs.generator_params(name)
+    h = HostHandle(params)
+    n = sum(int(np.prod(s)) for _, s in synthetic.parameter_shapes(params))
+    assert h.ref_weight_count == n
+    keys = [k for k, _ in ref_weight_keys(params) if k is not None]
+    assert sorted(keys) == sorted(k for k, _ in synthetic.parameter_shapes(params))
+
+
+def test_receptive_field_and_upsample_factor(built_lib):
+    h = HostHandle(configs.generator_params("ljspeech_v1"))
+    assert h.receptive_field_size == 6139  # models/parallel_wavegan.py:197-211, SURVEY a14
+    assert h.upsample_factor == 256
+    h = HostHandle(configs.generator_params("yesno_debug"))
+    assert h.receptive_field_size == 4093  # 2*(2*1023)+1 (SURVEY a14 says 2047: miscount)
+    assert HostHandle(configs.generator_params("libritts_v1")).upsample_factor == 300
+
+
+@pytest.mark.parametrize(
+    "override, exc",
+    [
+        (dict(layers=10, stacks=3), AssertionError),  # parallel_wavegan.py:77
+        (dict(kernel_size=4), AssertionError),  # residual_block.py:77
+        (dict(in_channels=2), NotImplementedError),
+        (dict(gate_channels=512), NotImplementedError),
+        (dict(gate_channels=7), ValueError),
+        (dict(upsample_net="MelGANGenerator"), NotImplementedError),
+        (dict(upsample_params={"upsample_scales": [4], "nonlinear_activation": "ReLU"}), NotImplementedError),
+    ],
+)
+def test_invalid_configs_raise_reference_exceptions(built_lib, override, exc):
+    params = configs.generator_params("ljspeech_v1", **override)
+    with pytest.raises(exc):
+        HostHandle(params)
+
+
+def _ref_pack_gate(wd, wa, G, R, A, KS, lane, s, m):
+    """Independent restatement of the gate A-fragment element (kernel docs in pwg_kernels.hip)."""
+    GH = G // 2
+    GHPAD = 16 if GH <= 16 else (GH + 31) // 32 * 32
+    prow = 32 * m + (lane & 31)
+    k = 2 * s + (lane >> 5)
+    grow = (prow if prow < GH else None) if prow < GHPAD else (GH + prow - GHPAD if prow - GHPAD < GH else None)
+    if grow is None:
+        return 0.0
+    if k < KS * R:
+        return wd[grow, k % R, k // R]
+    if k < KS * R + A:
+        return wa[grow, k - KS * R, 0]
+    return 0.0
+
+
+@pytest.mark.parametrize("name", ["reference_test", "ljspeech_v1"])
+def test_pack_gate_fragments(built_lib, name):
+    params = configs.generator_params(name)
+    h = HostHandle(params)
+    sd = synthetic.make_state_dict(params, seed=0)
+    packed = h.pack(sd)
+    assert packed.shape == (h.packed_weight_count,)
+    assert np.isfinite(packed).all()
+    # the first layer's gate fragments start right after the fixed blocks; find them by value
+    wd = sd["conv_layers.0.conv.weight"]
+    wa = sd["conv_layers.0.conv1x1_aux.weight"]
+    G, R = wd.shape[0], wd.shape[1]
+    A = wa.shape[1]
+    KS = wd.shape[2]
+    first = [_ref_pack_gate(wd, wa, G, R, A, KS, lane, 0, 0) for lane in range(64)]
+    # locate the 64-float fragment in the image
+    f = np.asarray(first, np.float32)
+    hits = [i for i in range(0, packed.size - 64, 64) if np.array_equal(packed[i:i + 64], f)]
+    assert len(hits) == 1
+    base = hits[0]
+    GH = G // 2
+    MT = 1 if GH <= 16 else (GH + 31) // 32 * 32 // 16
+    K1pad = (KS * R + A + 15) // 16 * 16
+    for s in range(K1pad // 2):
+        for m in range(MT):
+            frag = packed[base + (s * MT + m) * 64: base + (s * MT + m + 1) * 64]
+            ref = [_ref_pack_gate(wd, wa, G, R, A, KS, lane, s, m) for lane in range(64)]
+            np.testing.assert_array_equal(frag, np.asarray(ref, np.float32))
+
+
+def test_pack_rejects_missing_weights(built_lib):
+    params = configs.generator_params("reference_test")
+    sd = synthetic.make_state_dict(params, seed=0)
+    del sd["conv_layers.3.conv1x1_aux.weight"]
+    with pytest.raises(KeyError):
+        HostHandle(params).pack(sd)
+
+
+def test_weight_norm_state_packs_like_folded(built_lib):
+    params = configs.generator_params("reference_test")
+    wn = synthetic.make_state_dict(params, seed=0, weight_norm=True)
+    from oracle.pwg_numpy import fold_weight_norm
+
+    folded = {k: np.asarray(v, np.float32) for k, v in fold_weight_norm(wn).items()}
+    h = HostHandle(params)
+    np.testing.assert_allclose(h.pack(wn), h.pack(folded), rtol=2e-7, atol=1e-7)
+
+
+def test_config_translation():
+    cfg = make_config(configs.generator_params("libritts_v1"))
+    assert list(cfg.upsample_scales)[: cfg.num_scales] == [4, 5, 3, 5]
+    assert cfg.use_conv_in == 1 and cfg.aux_context_window == 2

@@ -1,0 +1,208 @@
+"""Parity of the HIP path (through the C-ABI) with the reference's golden vectors, the CPU oracle
+and size-independent properties at full size. GPU only.
+
+Tolerance: |d| < 1e-4 absolute on fp32 outputs (BASELINE.json north_star); the reference's own
+fp32-vs-fp64 floor is ~2e-6."""
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_names, golden_params, golden_state, load_golden
+
+pytestmark = pytest.mark.gpu
+
+ATOL = 1e-4
+
+
+def _module(params, sd, device):
+    from parallelwavegan_amd import ParallelWaveGANGenerator
+
+    m = ParallelWaveGANGenerator(**params)
+    if not any(k.endswith("weight_g") for k in sd):
+        m.remove_weight_norm()
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()}, strict=True)
+    return m.eval().to(device)
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_golden_vectors(name, built_lib, cuda_device):
+    g = load_golden(name)
+    params = golden_params(g["meta"])
+    sd = golden_state(g["meta"], params)
+    m = _module(golden_params(g["meta"]), sd, cuda_device)
+    with torch.no_grad():
+        if g["meta"]["mode"] == "inference":
+            if "mean" in g:
+                m.register_buffer("mean", torch.from_numpy(g["mean"]).to(cuda_device))
+                m.register_buffer("scale", torch.from_numpy(g["scale"]).to(cuda_device))
+            y = m.inference(g["mel"], g["noise"], normalize_before="mean" in g)
+        else:
+            y = m(torch.from_numpy(g["z"]).to(cuda_device), torch.from_numpy(g["c"]).to(cuda_device))
+    y = y.cpu().numpy()
+    assert y.shape == g["y"].shape
+    assert np.isfinite(y).all()
+    err = np.abs(y - g["y"]).max()
+    assert err < ATOL, f"{name}: max|d| = {err:.3e}"
+
+
+@pytest.mark.parametrize("cfg, frames", [("ljspeech_v1", 64), ("libritts_v1", 41), ("yesno_debug", 100)])
+def test_against_numpy_oracle(cfg, frames, built_lib, cuda_device):
+    from oracle import pwg_numpy
+    from parallelwavegan_amd import configs, synthetic
+
+    params = configs.generator_params(cfg)
+    sd = synthetic.make_state_dict(params, seed=7)
+    m = _module(configs.generator_params(cfg), sd, cuda_device)
+    H = m.upsample_factor
+    mel = synthetic.make_mel(frames, 80, seed=11)
+    noise = synthetic.make_noise(frames * H, seed=12)
+    with torch.no_grad():
+        y = m.inference(mel, noise).cpu().numpy()
+    ref = pwg_numpy.inference(mel, noise, sd, params)
+    err = np.abs(y - ref).max()
+    assert err < ATOL, f"max|d| = {err:.3e}"
+
+
+def test_full_size_against_torch_cpu(built_lib, cuda_device):
+    """LJ v1 at T'=512 (131,072 samples, 5.9 s of audio) vs the torch-CPU restatement."""
+    from oracle.pwg_torch_cpu import TorchCPUGenerator
+    from parallelwavegan_amd import configs, synthetic
+
+    params = configs.generator_params("ljspeech_v1")
+    sd = synthetic.make_state_dict(params, seed=0)
+    m = _module(configs.generator_params("ljspeech_v1"), sd, cuda_device)
+    mel = synthetic.make_mel(512, 80, seed=1)
+    noise = synthetic.make_noise(512 * 256, seed=2)
+    with torch.no_grad():
+        y = m.inference(mel, noise).cpu().numpy()
+    ref = TorchCPUGenerator(sd, params).inference(mel, noise).numpy()
+    err = np.abs(y - ref).max()
+    assert err < ATOL, f"max|d| = {err:.3e}"
+
+
+def test_ragged_batch_is_bitwise_equal_to_single_utterances(built_lib, cuda_device):
+    """Segment padding isolates utterances: a batch must reproduce solo runs bit for bit."""
+    from parallelwavegan_amd import Engine, configs, synthetic
+
+    params = configs.generator_params("libritts_v1")
+    eng = Engine(params, cuda_device)
+    eng.load_state_dict(synthetic.make_state_dict(params, seed=0))
+    lengths = [1, 3, 17, 80, 5]
+    mels = [torch.from_numpy(synthetic.make_mel(f, 80, seed=20 + i)).to(cuda_device) for i, f in enumerate(lengths)]
+    noises = [torch.from_numpy(synthetic.make_noise(f * 300, seed=40 + i)).to(cuda_device) for i, f in enumerate(lengths)]
+    batch = [y.cpu().numpy() for y in eng.infer(mels, noises)]
+    for i in range(len(lengths)):
+        solo = eng.infer([mels[i]], [noises[i]])[0].cpu().numpy()
+        np.testing.assert_array_equal(batch[i], solo)
+
+
+def test_receptive_field_locality_full_size(built_lib, cuda_device):
+    """Size-independent property at a long utterance (T'=2048 -> 524,288 samples): perturbing
+    one noise sample changes the output only within +-(receptive_field-1)/2 of it."""
+    from parallelwavegan_amd import Engine, configs, synthetic
+
+    params = configs.generator_params("ljspeech_v1")
+    eng = Engine(params, cuda_device)
+    eng.load_state_dict(synthetic.make_state_dict(params, seed=0))
+    F = 2048
+    mel = torch.from_numpy(synthetic.make_mel(F, 80, seed=1)).to(cuda_device)
+    noise = torch.from_numpy(synthetic.make_noise(F * 256, seed=2)).to(cuda_device)
+    y0 = eng.infer([mel], [noise])[0].clone()
+    p = 300_001
+    n2 = noise.clone()
+    n2[p, 0] += 1.0
+    y1 = eng.infer([mel], [n2])[0]
+    diff = (y1 - y0).abs().reshape(-1).cpu().numpy()
+    half = (eng.receptive_field_size - 1) // 2
+    changed = np.nonzero(diff)[0]
+    assert changed.size > 0
+    assert changed.min() >= p - half and changed.max() <= p + half
+    assert diff[p] > 0
+
+
+def test_causal_generator_is_causal(built_lib, cuda_device):
+    """test/test_parallel_wavegan.py:304-358 restated on the GPU path: perturbing the second half
+    of z and c leaves the first half of the output bit-identical."""
+    from parallelwavegan_amd import ParallelWaveGANGenerator, configs
+
+    for w in (0, 1, 2, 3):
+        params = configs.generator_params("reference_test", use_causal_conv=True, aux_context_window=w)
+        torch.manual_seed(0)
+        m = ParallelWaveGANGenerator(**params).eval().to(cuda_device)
+        T = 4096
+        z = torch.randn(1, 1, T)
+        c = torch.randn(1, 10, T // 16)
+        z_, c_ = z.clone(), c.clone()
+        z_[..., T // 2:] = torch.randn(z[..., T // 2:].shape)
+        c_[..., c.size(-1) // 2:] = torch.randn(c[..., c.size(-1) // 2:].shape)
+        c = torch.nn.ConstantPad1d(w, 0.0)(c)
+        c_ = torch.nn.ConstantPad1d(w, 0.0)(c_)
+        with torch.no_grad():
+            y = m(z.to(cuda_device), c.to(cuda_device)).cpu().numpy()
+            y_ = m(z_.to(cuda_device), c_.to(cuda_device)).cpu().numpy()
+        np.testing.assert_array_equal(y[..., : T // 2], y_[..., : T // 2])
+        assert not np.array_equal(y, y_)
+
+
+def test_forward_length_assert(built_lib, cuda_device):
+    from parallelwavegan_amd import ParallelWaveGANGenerator, configs
+
+    m = ParallelWaveGANGenerator(**configs.generator_params("reference_test")).to(cuda_device)
+    z = torch.randn(1, 1, 160, device=cuda_device)
+    c = torch.randn(1, 10, 10 + 4, device=cuda_device)  # 10 frames * 16 = 160 ok
+    m(z, c)
+    with pytest.raises(AssertionError):
+        m(torch.randn(1, 1, 150, device=cuda_device), c)
+
+
+def test_inference_without_noise_uses_cpu_randn(built_lib, cuda_device):
+    """x=None draws torch.randn on the CPU generator then moves it (parallel_wavegan.py:250-253),
+    so a seeded call equals the explicit-noise call with the same draw."""
+    from parallelwavegan_amd import ParallelWaveGANGenerator, configs, synthetic
+
+    m = ParallelWaveGANGenerator(**configs.generator_params("yesno_debug")).eval().to(cuda_device)
+    mel = synthetic.make_mel(12, 80, seed=3)
+    torch.manual_seed(123)
+    y1 = m.inference(mel).cpu().numpy()
+    torch.manual_seed(123)
+    x = torch.randn(1, 1, 12 * 256).view(-1, 1)
+    y2 = m.inference(mel, x).cpu().numpy()
+    np.testing.assert_array_equal(y1, y2)
+
+
+def test_module_repacks_after_weight_update(built_lib, cuda_device):
+    from parallelwavegan_amd import ParallelWaveGANGenerator, configs, synthetic
+
+    m = ParallelWaveGANGenerator(**configs.generator_params("reference_test")).eval().to(cuda_device)
+    mel = synthetic.make_mel(8, 10, seed=3)
+    x = synthetic.make_noise(8 * 16, seed=4)
+    y1 = m.inference(mel, x).cpu().numpy()
+    with torch.no_grad():
+        m.last_conv_layers[3].bias.add_(1.0)
+    y2 = m.inference(mel, x).cpu().numpy()
+    np.testing.assert_allclose(y2 - y1, 1.0, atol=1e-5)
+
+
+def test_engine_timing_buckets(built_lib, cuda_device):
+    from parallelwavegan_amd import Engine, configs, synthetic
+
+    params = configs.generator_params("yesno_debug")
+    eng = Engine(params, cuda_device)
+    eng.load_state_dict(synthetic.make_state_dict(params, seed=0))
+    eng.set_timing(True)
+    mel = torch.from_numpy(synthetic.make_mel(20, 80, seed=1)).to(cuda_device)
+    noise = torch.from_numpy(synthetic.make_noise(20 * 256, seed=2)).to(cuda_device)
+    eng.infer([mel], [noise])
+    t = eng.collect_timing()
+    assert t["residual_layer"][1] == 20
+    assert all(t[k][1] == 1 for k in ("conv_in", "upsample", "first_conv", "head"))
+    assert all(ms >= 0 for ms, _ in t.values())
+
+
+def test_cpu_module_fails_loudly(built_lib):
+    from parallelwavegan_amd import ParallelWaveGANGenerator, configs
+
+    m = ParallelWaveGANGenerator(**configs.generator_params("reference_test"))
+    with pytest.raises(RuntimeError):
+        m.inference(np.zeros((4, 10), np.float32))
