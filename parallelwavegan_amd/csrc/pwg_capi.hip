@@ -47,16 +47,211 @@ struct TimingRecord {
   hipEvent_t start, stop;
 };
 
+// ---------------------------------------------------------------------------------------------
+// Composite upsampler tables (AuxTab). The reference upsampler (layers/upsample.py:112-128) is,
+// per channel, a linear map from T' frames to T = T'*H samples: U[t][f]. Rows whose dependency
+// cone never meets a zero-padded boundary equal the periodic interior kernel; the first TL / last
+// TR rows see the left / right boundary only and depend on t / T-1-t alone once F >= Fmin; shorter
+// utterances get their full matrices. Everything is computed by running the staged upsampler on
+// unit impulses in double precision and then VERIFIED row by row against the exact matrix.
+
+struct AuxStruct {
+  long long H = 1;
+  int J1 = 0, J2 = 0, J = 1, TL = 0, TR = 0, Fmin = 1;
+  int nka = 1, nfwg = 1;
+};
+
+void up_stage(const std::vector<double>& in, int s, const double* h, bool causal, std::vector<double>& out) {
+  const long long n = (long long)in.size() * s;
+  const int P = causal ? 2 * s : s;
+  out.assign(n, 0.0);
+  for (long long t = 0; t < n; ++t) {
+    double v = 0.0;
+    for (int k = 0; k < 2 * s + 1; ++k) {
+      const long long u = t + k - P;
+      if (u >= 0 && u < n) v += h[k] * in[u / s];
+    }
+    out[t] = v;
+  }
+}
+
+// Exact U for F frames, row-major [F*H][F].
+std::vector<double> upsample_matrix(const PwgConfig& c, const std::vector<std::vector<double>>& taps, int F,
+                                    long long H) {
+  std::vector<double> M((size_t)(F * H) * F, 0.0), a, b;
+  for (int f = 0; f < F; ++f) {
+    a.assign(F, 0.0);
+    a[f] = 1.0;
+    for (int i = 0; i < c.num_scales; ++i) {
+      up_stage(a, c.upsample_scales[i], taps[i].data(), c.use_causal_conv != 0, b);
+      a.swap(b);
+    }
+    for (long long t = 0; t < F * H; ++t) M[(size_t)t * F + f] = a[t];
+  }
+  return M;
+}
+
+long long floordiv_h(long long a, long long b) {
+  long long q = a / b;
+  if ((a % b != 0) && (a < 0)) --q;
+  return q;
+}
+
+// Frame window [t/H - J1, t/H + J2] of every output row, from the stage dependency ranges.
+void aux_window(const PwgConfig& c, long long H, int* J1, int* J2) {
+  const long long fm = 64;
+  int j1 = 0, j2 = 0;
+  for (long long p = 0; p < H; ++p) {
+    long long lo = fm * H + p, hi = lo + 1;
+    for (int i = c.num_scales - 1; i >= 0; --i) {
+      const int s = c.upsample_scales[i];
+      const int P = c.use_causal_conv ? 2 * s : s;
+      lo = floordiv_h(lo - P, s);
+      hi = floordiv_h(hi - 1 + 2 * s - P, s) + 1;
+    }
+    j1 = std::max(j1, (int)(fm - lo));
+    j2 = std::max(j2, (int)(hi - 1 - fm));
+  }
+  *J1 = j1;
+  *J2 = j2;
+}
+
+// Row weights as the layer kernel selects them (w has AUX_J4 entries).
+void decomposed_row(const AuxStruct& st, const std::vector<float>& interior, const std::vector<float>& left,
+                    const std::vector<float>& right, const std::vector<float>& small, long long F, long long t,
+                    float* w) {
+  const long long T = F * st.H;
+  const float* row;
+  if (F < st.Fmin) row = small.data() + (st.H * F * (F - 1) / 2 + t) * AUX_J4;
+  else if (t < st.TL) row = left.data() + t * AUX_J4;
+  else if (t >= T - st.TR) row = right.data() + (T - 1 - t) * AUX_J4;
+  else row = interior.data() + (t % st.H) * AUX_J4;
+  for (int j = 0; j < AUX_J4; ++j) w[j] = row[j];
+}
+
+void exact_row(const AuxStruct& st, const std::vector<double>& M, long long F, long long t, double* w) {
+  for (int j = 0; j < AUX_J4; ++j) {
+    const long long f = t / st.H - st.J1 + j;
+    w[j] = (j < st.J && f >= 0 && f < F) ? M[(size_t)t * F + f] : 0.0;
+  }
+}
+
+// Structure (TL, TR, Fmin, window sizes) from generic taps; tables from the real taps.
+int aux_structure(const PwgConfig& c, AuxStruct* st) {
+  long long H = 1;
+  for (int i = 0; i < c.num_scales; ++i) H *= c.upsample_scales[i];
+  st->H = H;
+  if (H < 2 || H > 4096) return fail(PWG_ERR_UNSUPPORTED, "upsample factor must be in [2, 4096]");
+  aux_window(c, H, &st->J1, &st->J2);
+  st->J = st->J1 + st->J2 + 1;
+  if (st->J > AUX_J4) return fail(PWG_ERR_UNSUPPORTED, "composite upsampler spans more than 8 frames");
+  // generic taps: the unclean row set is structural (boundary truncation), not value-dependent
+  std::vector<std::vector<double>> taps(c.num_scales);
+  uint64_t x = 0x9E3779B97F4A7C15ULL;
+  for (int i = 0; i < c.num_scales; ++i)
+    for (int k = 0; k < 2 * c.upsample_scales[i] + 1; ++k) {
+      x = x * 6364136223846793005ULL + 1442695040888963407ULL;
+      taps[i].push_back(0.5 + (double)(x >> 11) / (double)(1ULL << 53));
+    }
+  const int Fb = 24;
+  const std::vector<double> M = upsample_matrix(c, taps, Fb, H);
+  const long long T = Fb * H, fm = Fb / 2;
+  int TL = 0, TR = 0;
+  for (long long t = 0; t < T; ++t) {
+    double w[AUX_J4];
+    exact_row(*st, M, Fb, t, w);
+    bool clean = true;
+    for (int j = 0; j < st->J; ++j)
+      if (std::fabs(w[j] - M[(size_t)(fm * H + t % H) * Fb + fm - st->J1 + j]) > 1e-13) clean = false;
+    if (!clean) {
+      if (t < T / 2) TL = std::max(TL, (int)(t + 1));
+      else TR = std::max(TR, (int)(T - t));
+    }
+  }
+  st->TL = TL;
+  st->TR = TR;
+  st->Fmin = (int)((TL + TR + H - 1) / H) + 1;
+  if (st->Fmin + 4 > Fb) return fail(PWG_ERR_UNSUPPORTED, "upsampler edge region too wide");
+  // aux k-steps per 32-sample wave window and frames per 128-sample workgroup window
+  int cnt = 0, nfwg = 0;
+  for (long long t0 = 0; t0 < 128 * H; t0 += 32)
+    cnt = std::max(cnt, (int)((t0 + 31) / H - t0 / H) + st->J);
+  st->nka = (cnt + 1) / 2;
+  for (long long t0 = 0; t0 < 128 * H; t0 += TILE)
+    for (int w = 0; w < 4; ++w)
+      nfwg = std::max(nfwg, (int)((t0 + 32 * w) / H - t0 / H) + 2 * st->nka);
+  st->nfwg = nfwg;
+  if (nfwg > AUX_MAX_NFWG) return fail(PWG_ERR_UNSUPPORTED, "upsample factor too small for the aux frame window");
+  return PWG_OK;
+}
+
+int aux_tables(const PwgConfig& c, const AuxStruct& st, const std::vector<std::vector<double>>& taps,
+               std::vector<float>& interior, std::vector<float>& left, std::vector<float>& right,
+               std::vector<float>& small) {
+  const long long H = st.H;
+  const int Fb = 24;
+  const long long fm = Fb / 2;
+  const std::vector<double> Mb = upsample_matrix(c, taps, Fb, H);
+  const long long Tb = Fb * H;
+  interior.assign((size_t)H * AUX_J4, 0.f);
+  left.assign((size_t)std::max(st.TL, 1) * AUX_J4, 0.f);
+  right.assign((size_t)std::max(st.TR, 1) * AUX_J4, 0.f);
+  small.assign((size_t)std::max<long long>(H * st.Fmin * (st.Fmin - 1) / 2, 1) * AUX_J4, 0.f);
+  double w[AUX_J4];
+  for (long long p = 0; p < H; ++p) {
+    exact_row(st, Mb, Fb, fm * H + p, w);
+    for (int j = 0; j < AUX_J4; ++j) interior[p * AUX_J4 + j] = (float)w[j];
+  }
+  for (long long t = 0; t < st.TL; ++t) {
+    exact_row(st, Mb, Fb, t, w);
+    for (int j = 0; j < AUX_J4; ++j) left[t * AUX_J4 + j] = (float)w[j];
+  }
+  for (long long q = 0; q < st.TR; ++q) {
+    exact_row(st, Mb, Fb, Tb - 1 - q, w);
+    for (int j = 0; j < AUX_J4; ++j) right[q * AUX_J4 + j] = (float)w[j];
+  }
+  for (int F = 1; F < st.Fmin; ++F) {
+    const std::vector<double> M = upsample_matrix(c, taps, F, H);
+    for (long long t = 0; t < F * H; ++t) {
+      exact_row(st, M, F, t, w);
+      for (int j = 0; j < AUX_J4; ++j) small[(H * F * (F - 1) / 2 + t) * AUX_J4 + j] = (float)w[j];
+    }
+  }
+  // verify the decomposition against exact matrices (every row, every frame)
+  double scale = 0.0;
+  for (double v : Mb) scale = std::max(scale, std::fabs(v));
+  const double tol = 1e-6 * std::max(scale, 1e-30);  // fp32 storage of the weights
+  std::vector<int> Fs;
+  for (int F = 1; F < st.Fmin + 4; ++F) Fs.push_back(F);
+  Fs.push_back(Fb);
+  for (int F : Fs) {
+    const std::vector<double> M = F == Fb ? Mb : upsample_matrix(c, taps, F, H);
+    for (long long t = 0; t < F * H; ++t) {
+      float wd[AUX_J4];
+      decomposed_row(st, interior, left, right, small, F, t, wd);
+      for (int f = 0; f < F; ++f) {
+        const long long j = f - (t / H - st.J1);
+        const double got = (j >= 0 && j < AUX_J4) ? (double)wd[j] : 0.0;
+        if (std::fabs(got - M[(size_t)t * F + f]) > tol)
+          return fail(PWG_ERR_INVALID, "internal: composite upsampler table does not reproduce the reference upsampler");
+      }
+    }
+  }
+  return PWG_OK;
+}
+
 }  // namespace
 
 struct PwgHandle {
   PwgConfig cfg;
   int device;
   // derived shapes
-  int R, G, GH, GHPAD, MT, S, M2T, A, KS, KW, O, L, lps, K1, K1pad, NQ;
+  int R, RP, G, GH, GHPAD, GR, MT, S, M2T, A, KS, KW, O, L, lps, K1, NQ;
   std::vector<int> dil;
+  AuxStruct aux;
   // packed image offsets (floats)
-  size_t off_first_w, off_first_b, off_conv_in, off_taps;
+  size_t off_first_w, off_first_b, off_conv_in, off_waux;
+  size_t off_tab_interior, off_tab_left, off_tab_right, off_tab_small;
   size_t off_layers, layer_stride, lo_wg, lo_bg, lo_w2, lo_b2;
   size_t off_head_w1, off_head_b1, off_head_w2, off_head_b2, packed_total;
   long long ref_total;
@@ -75,7 +270,7 @@ struct PwgPlan {
   UttDesc* d_utts = nullptr;
   int* d_tile_utt = nullptr;
   // workspace offsets (bytes)
-  size_t ws_x0, ws_x1, ws_skip, ws_cup, ws_c1, ws_total;
+  size_t ws_x0, ws_x1, ws_skip, ws_c1, ws_d, ws_total;
 };
 
 extern "C" {
@@ -119,9 +314,10 @@ int pwg_create(const PwgConfig* cfg, int device, PwgHandle** out) {
   h->GHPAD = h->GH <= 16 ? 16 : (h->GH + 31) / 32 * 32;
   h->MT = h->GHPAD <= 16 ? 1 : h->GHPAD / 16;
   h->NQ = h->GHPAD / 2;
+  h->GR = 32 * h->MT;
   h->M2T = (h->S + h->R + 31) / 32;
-  h->K1 = h->KS * h->R + h->A;
-  h->K1pad = (h->K1 + KC - 1) / KC * KC;
+  h->RP = (h->R + KC - 1) / KC * KC;
+  h->K1 = h->KS * h->RP;
   if (!(h->MT == 1 || h->MT == 2 || h->MT == 4) || !(h->M2T == 1 || h->M2T == 2 || h->M2T == 4)) {
     delete h;
     return fail(PWG_ERR_UNSUPPORTED, "gate_channels <= 128 and skip+residual <= 128 supported");
@@ -132,29 +328,23 @@ int pwg_create(const PwgConfig* cfg, int device, PwgHandle** out) {
     if (d > (1LL << 24)) { delete h; return fail(PWG_ERR_UNSUPPORTED, "dilation too large"); }
     h->dil.push_back((int)d);
   }
-  // upsampler LDS widths for one TILE of output: a stage whose output spans W samples reads at
-  // most ceil((W-1)/s)+3 input samples (any alignment, causal or not)
   {
-    long long w = TILE;
-    for (int i = c.num_scales - 1; i >= 0; --i) {
-      const int s = c.upsample_scales[i];
-      w = (w - 1 + s - 1) / s + 3;
-      if (w > UP_MAXW) { delete h; return fail(PWG_ERR_UNSUPPORTED, "upsample stage too wide for LDS"); }
-    }
+    const int rc = aux_structure(c, &h->aux);
+    if (rc != PWG_OK) { delete h; return rc; }
   }
   // packed image layout
   size_t o = 0;
   h->off_first_w = o; o += align64(h->R);
   h->off_first_b = o; o += align64(h->R);
   h->off_conv_in = o; o += align64((size_t)h->A * h->A * h->KW);
-  h->off_taps = o;
-  {
-    size_t nt = 0;
-    for (int i = 0; i < c.num_scales; ++i) nt += 2 * c.upsample_scales[i] + 1;
-    o += align64(nt);
-  }
+  h->off_waux = o; o += align64((size_t)h->L * h->GR * h->A);
+  h->off_tab_interior = o; o += align64((size_t)h->aux.H * AUX_J4);
+  h->off_tab_left = o; o += align64((size_t)std::max(h->aux.TL, 1) * AUX_J4);
+  h->off_tab_right = o; o += align64((size_t)std::max(h->aux.TR, 1) * AUX_J4);
+  h->off_tab_small = o;
+  o += align64((size_t)std::max<long long>(h->aux.H * h->aux.Fmin * (h->aux.Fmin - 1) / 2, 1) * AUX_J4);
   h->lo_wg = 0;
-  h->lo_bg = h->lo_wg + align64((size_t)(h->K1pad / 2) * h->MT * 64);
+  h->lo_bg = h->lo_wg + align64((size_t)(h->K1 / 2) * h->MT * 64);
   h->lo_w2 = h->lo_bg + align64(2 * h->GHPAD);
   h->lo_b2 = h->lo_w2 + align64((size_t)h->NQ * h->M2T * 64);
   h->layer_stride = h->lo_b2 + align64(32 * h->M2T);
@@ -217,9 +407,16 @@ int pwg_pack_weights(const PwgHandle* h, const float* ref, float* pk) {
     pk[h->off_conv_in] = 1.f;  // unused (identity path)
   }
   {
-    size_t t = 0;
+    std::vector<std::vector<double>> taps(c.num_scales);
     for (int i = 0; i < c.num_scales; ++i)
-      for (int k = 0; k < 2 * c.upsample_scales[i] + 1; ++k) pk[h->off_taps + t++] = *p++;
+      for (int k = 0; k < 2 * c.upsample_scales[i] + 1; ++k) taps[i].push_back((double)*p++);
+    std::vector<float> ti, tl, tr, ts;
+    const int rc = aux_tables(c, h->aux, taps, ti, tl, tr, ts);
+    if (rc != PWG_OK) return rc;
+    std::copy(ti.begin(), ti.end(), pk + h->off_tab_interior);
+    std::copy(tl.begin(), tl.end(), pk + h->off_tab_left);
+    std::copy(tr.begin(), tr.end(), pk + h->off_tab_right);
+    std::copy(ts.begin(), ts.end(), pk + h->off_tab_small);
   }
   for (int l = 0; l < h->L; ++l) {
     const float* wd = p; p += (size_t)G * R * KS;   // conv.weight [G][R][KS]
@@ -236,24 +433,23 @@ int pwg_pack_weights(const PwgHandle* h, const float* ref, float* pk) {
       const int q = prow - GHPAD;
       return q < GH ? GH + q : -1;
     };
+    const int RP = h->RP;
     auto wcat = [&](int grow, int k) -> float {
       if (grow < 0) return 0.f;
-      if (k < KS * R) {
-        const int tap = k / R, ch = k % R;
-        return wd[((size_t)grow * R + ch) * KS + tap];
-      }
-      if (k < KS * R + A) return wa[(size_t)grow * A + (k - KS * R)];
-      return 0.f;
+      const int tap = k / RP, ch = k % RP;
+      return ch < R ? wd[((size_t)grow * R + ch) * KS + tap] : 0.f;
     };
     float* wg = L0 + h->lo_wg;
-    for (int s = 0; s < h->K1pad / 2; ++s)
+    for (int s = 0; s < h->K1 / 2; ++s)
       for (int m = 0; m < MT; ++m)
         for (int lane = 0; lane < 64; ++lane)
           wg[((size_t)s * MT + m) * 64 + lane] = wcat(gate_row(32 * m + (lane & 31)), 2 * s + (lane >> 5));
     float* bg = L0 + h->lo_bg;
+    float* waux = pk + h->off_waux + (size_t)l * h->GR * A;
     for (int prow = 0; prow < 2 * GHPAD; ++prow) {
       const int gr = gate_row(prow);
       bg[prow] = gr < 0 ? 0.f : bd[gr];
+      for (int i = 0; i < A; ++i) waux[(size_t)prow * A + i] = gr < 0 ? 0.f : wa[(size_t)gr * A + i];
     }
     float* w2 = L0 + h->lo_w2;
     for (int q = 0; q < h->NQ; ++q)
@@ -329,8 +525,8 @@ int pwg_plan_create(PwgHandle* h, int n_utts, const long long* frames, int layou
   p->ws_x0 = o; o += align_bytes(sizeof(float) * h->R * p->Tpad);
   p->ws_x1 = o; o += align_bytes(sizeof(float) * h->R * p->Tpad);
   p->ws_skip = o; o += align_bytes(sizeof(float) * h->S * p->Tpad);
-  p->ws_cup = o; o += align_bytes(sizeof(float) * h->A * p->Tpad);
   p->ws_c1 = o; o += align_bytes(sizeof(float) * h->A * p->F_total);
+  p->ws_d = o; o += align_bytes(sizeof(float) * h->L * h->GR * p->F_total);
   p->ws_total = o;
 
   DeviceGuard g(h->device);
@@ -388,8 +584,8 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
   float* x0 = (float*)(ws + p->ws_x0);
   float* x1 = (float*)(ws + p->ws_x1);
   float* skip = (float*)(ws + p->ws_skip);
-  float* cup = (float*)(ws + p->ws_cup);
   float* c1 = (float*)(ws + p->ws_c1);
+  float* dproj = (float*)(ws + p->ws_d);
 
   auto timed = [&](int bucket, auto&& launch) -> hipError_t {
     if (!h->timing) return launch();
@@ -412,13 +608,10 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
   e = timed(PWG_KERNEL_CONV_IN, [&] { return launch_conv_in(ca, s); });
   if (e != hipSuccess) return hip_fail(e, "conv_in launch");
 
-  UpsampleArgs ua;
-  ua.c1 = c1; ua.cup = cup; ua.taps = packed + h->off_taps; ua.tile_utt = p->d_tile_utt; ua.utts = p->d_utts;
-  ua.F_total = p->F_total; ua.Tpad = p->Tpad; ua.A = h->A; ua.n_scales = h->cfg.num_scales;
-  for (int i = 0; i < MAX_SCALES; ++i) ua.scales[i] = i < h->cfg.num_scales ? h->cfg.upsample_scales[i] : 1;
-  ua.causal = h->cfg.use_causal_conv;
-  e = timed(PWG_KERNEL_UPSAMPLE, [&] { return launch_upsample(ua, p->n_tiles, s); });
-  if (e != hipSuccess) return hip_fail(e, "upsample launch");
+  AuxProjArgs pa;
+  pa.c1 = c1; pa.waux = packed + h->off_waux; pa.d = dproj; pa.F_total = p->F_total; pa.A = h->A; pa.GR = h->GR;
+  e = timed(PWG_KERNEL_UPSAMPLE, [&] { return launch_aux_proj(pa, h->L, s); });
+  if (e != hipSuccess) return hip_fail(e, "aux projection launch");
 
   FirstConvArgs fa;
   fa.noise = noise; fa.w = packed + h->off_first_w; fa.b = packed + h->off_first_b; fa.x = x0;
@@ -431,10 +624,15 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
   for (int l = 0; l < h->L; ++l) {
     const float* L0 = packed + h->off_layers + h->layer_stride * l;
     LayerArgs la;
-    la.x_in = xin; la.x_out = xout; la.skip = skip; la.cup = cup;
+    la.x_in = xin; la.x_out = xout; la.skip = skip;
+    la.d = dproj + (size_t)l * p->F_total * h->GR;
+    la.tab.interior = packed + h->off_tab_interior; la.tab.left = packed + h->off_tab_left;
+    la.tab.right = packed + h->off_tab_right; la.tab.small = packed + h->off_tab_small;
+    la.tab.H = (int)h->aux.H; la.tab.J1 = h->aux.J1; la.tab.TL = h->aux.TL; la.tab.TR = h->aux.TR;
+    la.tab.Fmin = h->aux.Fmin; la.nka = h->aux.nka; la.nfwg = h->aux.nfwg;
     la.wg = L0 + h->lo_wg; la.bg = L0 + h->lo_bg; la.w2 = L0 + h->lo_w2; la.b2 = L0 + h->lo_b2;
     la.tile_utt = p->d_tile_utt; la.utts = p->d_utts; la.Tpad = p->Tpad;
-    la.R = h->R; la.S = h->S; la.A = h->A; la.KS = h->KS; la.K1pad = h->K1pad; la.dil = h->dil[l];
+    la.R = h->R; la.RP = h->RP; la.S = h->S; la.KS = h->KS; la.dil = h->dil[l];
     la.tap_center = h->cfg.use_causal_conv ? h->KS - 1 : (h->KS - 1) / 2;
     la.first = l == 0;
     e = timed(PWG_KERNEL_RESIDUAL_LAYER, [&] { return launch_layer(la, h->MT, h->M2T, p->n_tiles, s); });

@@ -13,10 +13,11 @@ constexpr int TILE = 128;
 constexpr int SEG = 256;
 // K-chunk of the gate GEMM staged per LDS round.
 constexpr int KC = 16;
-// Upsampler: channels per LDS pass and max staged width per stage.
-constexpr int UP_CG = 16;
-constexpr int UP_MAXW = 192;
 constexpr int MAX_SCALES = 8;
+// Composite-upsampler taps per output sample, padded (J = J1 + J2 + 1 <= 8).
+constexpr int AUX_J4 = 8;
+// Max frames of the per-workgroup frame window of the aux term.
+constexpr int AUX_MAX_NFWG = 16;
 
 // One utterance of a planned batch. All offsets in elements.
 struct UttDesc {
@@ -42,17 +43,28 @@ struct ConvInArgs {
   int use_conv_in;       // 0: identity (UpsampleNetwork)
 };
 
-struct UpsampleArgs {
+// Exact composite of the upsampler (Stretch2d + FIR stages, layers/upsample.py:112-128) as a
+// per-output-sample tap table over mel frames: c_up[:, t] = sum_j w_t[j] * C1[:, t/H - J1 + j].
+// Rows t in [TL, T-TR) of an utterance with F >= Fmin frames use interior[t % H]; the first TL
+// rows use left[t], the last TR rows right[T-1-t]; utterances with F < Fmin use small[] (rows of
+// F frames start at H*F*(F-1)/2). Built and verified against the staged upsampler in double on
+// the host (pwg_capi.hip, build_aux_tables).
+struct AuxTab {
+  const float* interior;
+  const float* left;
+  const float* right;
+  const float* small;
+  int H, J1, TL, TR, Fmin;
+};
+
+// D[l][f][row] = sum_i Waux_l[row][i] * C1[i][f]: the aux 1x1 conv of every layer applied at FRAME
+// rate (it commutes with the per-channel linear upsampler), rows in packed gate-row order.
+struct AuxProjArgs {
   const float* c1;       // [A][F_total]
-  float* cup;            // [A][Tpad]
-  const float* taps;     // concatenated (2s+1) per stage
-  const int* tile_utt;
-  const UttDesc* utts;
-  long long F_total, Tpad;
-  int A;
-  int n_scales;
-  int scales[MAX_SCALES];
-  int causal;
+  const float* waux;     // [L][GR][A]
+  float* d;              // [L][F_total][GR]
+  long long F_total;
+  int A, GR;
 };
 
 struct FirstConvArgs {
@@ -70,17 +82,19 @@ struct LayerArgs {
   const float* x_in;     // [R][Tpad]
   float* x_out;          // [R][Tpad]
   float* skip;           // [S][Tpad]
-  const float* cup;      // [A][Tpad]
-  const float* wg;       // gate GEMM A-fragments [K1pad/2][MT][64]
+  const float* d;        // this layer's frame-rate aux projection [F_total][GR]
+  AuxTab tab;
+  const float* wg;       // gate GEMM A-fragments [K1/2][MT][64], K1 = KS*RP
   const float* bg;       // [2*GHPAD]
   const float* w2;       // skip|out GEMM A-fragments [GHPAD/2][M2T][64]
   const float* b2;       // [32*M2T]
   const int* tile_utt;
   const UttDesc* utts;
   long long Tpad;
-  int R, S, A, KS;
-  int K1pad;
+  int R, RP, S, KS;      // RP = R rounded up to KC (one K chunk never straddles two taps)
   int dil;
+  int nka;               // aux k-steps per wave (frames of a 32-sample window / 2)
+  int nfwg;              // frames staged per workgroup
   int tap_center;        // (KS-1)/2 non-causal, KS-1 causal
   int first;             // layer 0: skip buffer is written, not accumulated
 };
@@ -104,7 +118,7 @@ struct HeadArgs {
 
 // Kernel launchers (pwg_kernels.hip).
 hipError_t launch_conv_in(const ConvInArgs& a, hipStream_t s);
-hipError_t launch_upsample(const UpsampleArgs& a, long long n_tiles, hipStream_t s);
+hipError_t launch_aux_proj(const AuxProjArgs& a, int layers, hipStream_t s);
 hipError_t launch_first_conv(const FirstConvArgs& a, long long n_tiles, hipStream_t s);
 hipError_t launch_layer(const LayerArgs& a, int mt, int m2t, long long n_tiles, hipStream_t s);
 hipError_t launch_head(const HeadArgs& a, long long n_tiles, hipStream_t s);

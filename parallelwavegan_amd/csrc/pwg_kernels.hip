@@ -9,11 +9,14 @@
 // Kernels (reference op each one replaces):
 //   pwg_conv_in_kernel      ReplicationPad1d + (c-mean)/scale + conv_in (Conv1d A->A, k=2w+1, valid)
 //                           models/parallel_wavegan.py:259-262, layers/upsample.py:166-168,192
-//   pwg_upsample_kernel     per scale: Stretch2d nearest xs + Conv2d (1,2s+1) FIR, all stages fused
-//                           through LDS, layers/upsample.py:43-45,97-103,112-128
+//   pwg_aux_proj_kernel     conv1x1_aux of ALL layers at frame rate: D_l = W_aux_l . C1. The aux 1x1
+//                           (residual_block.py:93,126-130) is linear per time step and the upsampler
+//                           (layers/upsample.py:43-45,97-103,112-128) is linear per channel, so
+//                           W_aux . U(C1) == U(W_aux . C1); the layer kernel applies U as an exact
+//                           polyphase tap table over <= 8 frames (AuxTab) inside its MFMA GEMM.
 //   pwg_first_conv_kernel   first_conv 1x1 (1->R), models/parallel_wavegan.py:81,161
 //   pwg_layer_kernel        one WaveNetResidualBlock + skip accumulation, fused:
-//                           dilated conv (K taps) + aux 1x1 as ONE fp32 MFMA GEMM, gate
+//                           dilated conv (K taps) + upsampled aux term as ONE fp32 MFMA GEMM, gate
 //                           tanh*sigmoid in registers, skip|out 1x1 as a second MFMA GEMM whose
 //                           B operand is the gate tile straight out of the accumulators,
 //                           residual*sqrt(.5) and skip += in the epilogue.
@@ -26,6 +29,7 @@
 namespace pwg {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));  // native vector: stays in VGPRs (HIP float4 is a struct)
 
 __device__ __forceinline__ long long floordiv(long long a, long long b) {
   long long q = a / b;
@@ -82,86 +86,42 @@ __global__ void __launch_bounds__(256) pwg_conv_in_kernel(const ConvInArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Upsample network: all nearest-xs + (2s+1)-tap FIR stages of one TILE of output samples,
-// UP_CG channels per LDS pass. Stage i output t reads up[t+k-P], up[v] = in[v//s] for
-// 0 <= v < s*n_i else 0 (Conv2d zero padding, upsample.py:97-102), and stage outputs outside
-// [0, n_{i+1}) are zero for the next stage. Integer t//s replaces torch's float nearest index
-// (identical below 2^24 samples).
-__global__ void __launch_bounds__(256) pwg_upsample_kernel(const UpsampleArgs a) {
-  __shared__ float buf[2][UP_CG * UP_MAXW];
-  const long long tile = blockIdx.x;
-  const UttDesc ud = a.utts[a.tile_utt[tile]];
-  const long long col0 = tile * TILE;
-  const long long t0 = col0 - ud.seg_base;
-  const int tid = threadIdx.x;
-
-  if (t0 >= ud.T) {  // pure padding tile
-    for (int idx = tid; idx < a.A * TILE; idx += 256) {
-      const int c = idx / TILE, j = idx % TILE;
-      a.cup[(size_t)c * a.Tpad + col0 + j] = 0.f;
-    }
-    return;
+// D[l][f][row] = sum_i Waux_l[row][i] C1[i][f]. grid (ceil(F_total/64), L), block GR threads: one
+// gate row per thread, 64 frames per block; C1 tile and the layer's W rows staged in LDS.
+// Output rows are contiguous per frame (coalesced stores), the layout the layer kernel stages.
+__global__ void __launch_bounds__(128) pwg_aux_proj_kernel(const AuxProjArgs a) {
+  extern __shared__ float sm[];
+  const int A = a.A, GR = a.GR;
+  float* cs = sm;                 // [A][64]
+  float* ws = sm + A * 64;        // [GR][A+1]
+  const int l = blockIdx.y;
+  const long long f0 = (long long)blockIdx.x * 64;
+  const int row = threadIdx.x;
+  for (int idx = threadIdx.x; idx < A * 64; idx += GR) {
+    const int i = idx / 64, j = idx % 64;
+    const long long f = f0 + j;
+    cs[idx] = f < a.F_total ? a.c1[(size_t)i * a.F_total + f] : 0.f;
   }
-  const long long t1 = (t0 + TILE < ud.T) ? t0 + TILE : ud.T;
-  const int L = a.n_scales;
-  long long lo[MAX_SCALES + 1], hi[MAX_SCALES + 1], n[MAX_SCALES + 1];
-  lo[L] = t0; hi[L] = t1;
-  for (int i = L - 1; i >= 0; --i) {
-    const int s = a.scales[i];
-    const int P = a.causal ? 2 * s : s;
-    lo[i] = floordiv(lo[i + 1] - P, s);
-    hi[i] = floordiv(hi[i + 1] - 1 + 2 * s - P, s) + 1;
-  }
-  n[0] = ud.frames;
-  for (int i = 0; i < L; ++i) n[i + 1] = n[i] * a.scales[i];
-
-  for (int cg = 0; cg < a.A; cg += UP_CG) {
-    // stage-0 input: conv_in output frames [lo0, hi0), zero outside the utterance
-    {
-      const int W = (int)(hi[0] - lo[0]);
-      for (int idx = tid; idx < UP_CG * W; idx += 256) {
-        const int c = idx / W, j = idx % W;
-        const long long f = lo[0] + j;
-        const int ch = cg + c;
-        float v = 0.f;
-        if (ch < a.A && f >= 0 && f < ud.frames) v = a.c1[(size_t)ch * a.F_total + ud.frame_base + f];
-        buf[0][c * UP_MAXW + j] = v;
-      }
+  const float* w = a.waux + (size_t)l * GR * A;
+  for (int idx = threadIdx.x; idx < GR * A; idx += GR) ws[(idx / A) * (A + 1) + idx % A] = w[idx];
+  __syncthreads();
+  float* d = a.d + (size_t)l * a.F_total * GR;
+  for (int j = 0; j < 64; j += 4) {
+    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
+    for (int i = 0; i < A; ++i) {
+      const float wv = ws[row * (A + 1) + i];
+      const f32x4 c = *reinterpret_cast<const f32x4*>(&cs[i * 64 + j]);
+      acc0 = fmaf(wv, c.x, acc0);
+      acc1 = fmaf(wv, c.y, acc1);
+      acc2 = fmaf(wv, c.z, acc2);
+      acc3 = fmaf(wv, c.w, acc3);
     }
-    __syncthreads();
-    int cur = 0;
-    const float* taps = a.taps;
-    for (int i = 0; i < L; ++i) {
-      const int s = a.scales[i];
-      const int P = a.causal ? 2 * s : s;
-      const int KT = 2 * s + 1;
-      const int W = (int)(hi[i + 1] - lo[i + 1]);
-      const long long nin_up = n[i] * s;
-      for (int idx = tid; idx < UP_CG * W; idx += 256) {
-        const int c = idx / W, j = idx % W;
-        const long long t = lo[i + 1] + j;
-        float v = 0.f;
-        if (t >= 0 && t < n[i + 1]) {
-          const float* bin = &buf[cur][c * UP_MAXW];
-          for (int k = 0; k < KT; ++k) {
-            const long long uu = t + k - P;
-            if (uu >= 0 && uu < nin_up) v = fmaf(taps[k], bin[floordiv(uu, s) - lo[i]], v);
-          }
-        }
-        buf[cur ^ 1][c * UP_MAXW + j] = v;
-      }
-      taps += KT;
-      cur ^= 1;
-      __syncthreads();
+    const float accs[4] = {acc0, acc1, acc2, acc3};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const long long f = f0 + j + q;
+      if (f < a.F_total) d[(size_t)f * GR + row] = accs[q];
     }
-    for (int idx = tid; idx < UP_CG * TILE; idx += 256) {
-      const int c = idx / TILE, j = idx % TILE;
-      const int ch = cg + c;
-      if (ch >= a.A) continue;
-      const long long t = t0 + j;
-      a.cup[(size_t)ch * a.Tpad + col0 + j] = (t < t1) ? buf[cur][c * UP_MAXW + (int)(t - t0)] : 0.f;
-    }
-    __syncthreads();
   }
 }
 
@@ -186,28 +146,119 @@ __global__ void __launch_bounds__(256) pwg_first_conv_kernel(const FirstConvArgs
 // 32-sample column block [32w, 32w+32) and ALL gate rows, so the gate and both GEMMs stay in
 // its registers.
 //
-// GEMM 1 (gate pre-activation, 32*MT rows): Z = Wcat . [x(t-d); x(t); x(t+d); c_up(t)]
-//   K = KS*R + A (272 for LJ/LibriTTS v1), v_mfma_f32_32x32x2_f32, A operand = packed weight
-//   fragments (64 floats per (k-step, m-tile), lane-linear), B operand = staged activation
-//   column. K is streamed through LDS in chunks of KC.
-// gate: g = tanh(Za + ba) * sigmoid(Zb + bb); Za rows [0,GHPAD), Zb rows [GHPAD, 2*GHPAD) —
-//   the two halves sit in the same lane/register of m-tiles m and m+MT/2 (MT==1: regs r, r+8).
+// GEMM 1 (gate pre-activation, GR = 32*MT packed rows):
+//   Z = Wdil . [x(t+(0-c)d); x(t+(1-c)d); ...]   K = KS*RP, streamed through LDS in KC=16 chunks,
+//       one chunk = 16 channels of ONE tap (uniform source offset), double-buffered: the global
+//       loads of chunk i+1 are in flight while chunk i's MFMAs run, one barrier per chunk;
+//     + U(D_l)                                   the aux term at sample rate from frame-rate
+//       projections: a K = 2*nka (<= 16) GEMM whose A operand is the staged D tile [frame][row]
+//       and whose B operand (frame f, sample t) is the composite upsampler tap w_t[f - t/H + J1],
+//       computed per lane from the AuxTab row of its sample.
+//   v_mfma_f32_32x32x2_f32 throughout; A fragments are host-packed lane-linear (64 floats per
+//   (k-step, m-tile)), B fragments one ds_read_b32 per lane.
+// gate: g = tanh(Za + ba) * sigmoid(Zb + bb); Za rows [0,GHPAD), Zb rows [GHPAD, 2*GHPAD) sit in
+//   the same lane/register of m-tiles m and m+MT/2 (MT==1: registers r and r+8).
 // GEMM 2 ([skip; out] rows, 32*M2T): the gate accumulator register (m, r) IS the B fragment of
-//   one k-step (lane l: channel row(m,r,l>>5), column l&31); the host packs W2 in the matching
-//   permuted-k order, so no LDS round trip for g.
+//   one k-step (lane l: channel row(m,r,l>>5), column l&31); the host packs W2 in that permuted-k
+//   order. W2 fragments are read straight from global memory (L1/L2-resident, 32 KB per layer).
 // C/D map of the 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
-template <int MT, int M2T>
-__global__ void __launch_bounds__(256) pwg_layer_kernel(const LayerArgs a) {
+template <int MT>
+struct LayerSmem {
+  static constexpr int GR = 32 * MT;
+  static constexpr int A_CHUNK = (KC / 2) * MT * 64;  // floats of weight fragments per K chunk
+  static constexpr int B_CHUNK = KC * TILE;           // floats of activations per K chunk
+  static constexpr int BUF = A_CHUNK + B_CHUNK;
+  static constexpr int FLOATS = 2 * BUF + AUX_MAX_NFWG * GR;
+};
+
+// Registers carrying one K chunk from global memory to LDS (named fields, not arrays: an array
+// indexed across the unrolled staging loops ends up in scratch).
+// Registers carrying one K chunk from global memory to LDS: raw loads plus a validity mask that
+// is applied only when the chunk is written to LDS, so no instruction touches the loaded values
+// before the MFMAs of the current chunk have been issued (named fields, native vectors: a
+// predicated or struct-typed load is spilled to scratch / forces an early vmcnt(0) in hipcc).
+struct ChunkRegs {
+  f32x4 a0, a1, b0, b1;
+  unsigned mask;  // bit j: element j of b0, bit 4+j: element j of b1
+};
+
+// x[ch][e..e+3] of one utterance from an address clamped into the utterance's padded segment;
+// returns the raw vector and the validity bits (inside [0, T) and ch < R). ALIGNED (every tap
+// offset a multiple of 4, i.e. dilation % 4 == 0) selects one dwordx4 load, else 4 dword loads;
+// it is a template parameter so neither path carries a branch around its loads.
+template <bool ALIGNED>
+__device__ __forceinline__ f32x4 load_x4(const LayerArgs& a, const UttDesc& ud, long long segpad, int ch,
+                                         long long e, unsigned& bits) {
+  const bool chok = ch < a.R;
+  const float* src = a.x_in + (size_t)(chok ? ch : 0) * a.Tpad + ud.seg_base;
+  const long long Tu = ud.T;
+  f32x4 v;
+  if (ALIGNED) {
+    const long long ec = e < 0 ? 0 : (e > segpad - 4 ? segpad - 4 : e);
+    v = *reinterpret_cast<const f32x4*>(src + ec);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const long long ej = e + j;
+      v[j] = src[ej < 0 ? 0 : (ej > segpad - 1 ? segpad - 1 : ej)];
+    }
+  }
+  bits = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bits |= (chok && e + j >= 0 && e + j < Tu) ? (1u << j) : 0u;
+  return v;
+}
+
+// Chunk c = 16 consecutive K rows of ONE tap: A fragments (contiguous in the packed image) and
+// the activation rows x[ch0..ch0+15][t0 + off .. t0 + off + 127], zero outside the utterance.
+template <int MT, bool ALIGNED>
+__device__ __forceinline__ void layer_load_chunk(const LayerArgs& a, int c, const UttDesc& ud, long long t0,
+                                                 int tid, ChunkRegs& r) {
+  constexpr int NA4 = LayerSmem<MT>::A_CHUNK / 4;
+  const f32x4* wsrc = reinterpret_cast<const f32x4*>(a.wg + (size_t)c * LayerSmem<MT>::A_CHUNK);
+  r.a0 = wsrc[NA4 >= 256 ? tid : (tid < NA4 ? tid : 0)];
+  r.a1 = NA4 > 256 ? wsrc[tid + 256] : r.a0;
+  const int k0 = c * KC;
+  const int tap = k0 / a.RP;                 // uniform
+  const int ch0 = k0 - tap * a.RP;
+  const long long off = (long long)(tap - a.tap_center) * a.dil;
+  const int row = tid >> 5, c4 = tid & 31;
+  const long long e = t0 + 4 * c4 + off;
+  const long long segpad = (ud.T + SEG - 1) / SEG * SEG;
+  unsigned m0, m1;
+  r.b0 = load_x4<ALIGNED>(a, ud, segpad, ch0 + row, e, m0);
+  r.b1 = load_x4<ALIGNED>(a, ud, segpad, ch0 + row + 8, e, m1);
+  r.mask = m0 | (m1 << 4);
+}
+
+template <int MT>
+__device__ __forceinline__ void layer_store_chunk(float* buf, int tid, const ChunkRegs& r) {
+  constexpr int NA4 = LayerSmem<MT>::A_CHUNK / 4;
+  f32x4* as = reinterpret_cast<f32x4*>(buf);
+  if (NA4 >= 256 || tid < NA4) as[tid] = r.a0;
+  if (NA4 > 256) as[tid + 256] = r.a1;
+  float* bs = buf + LayerSmem<MT>::A_CHUNK;
+  const int row = tid >> 5, c4 = tid & 31;
+  f32x4 b0, b1;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    b0[j] = (r.mask >> j) & 1u ? r.b0[j] : 0.f;
+    b1[j] = (r.mask >> (4 + j)) & 1u ? r.b1[j] : 0.f;
+  }
+  *reinterpret_cast<f32x4*>(bs + row * TILE + 4 * c4) = b0;
+  *reinterpret_cast<f32x4*>(bs + (row + 8) * TILE + 4 * c4) = b1;
+}
+
+template <int MT, int M2T, bool ALIGNED>
+__global__ void __launch_bounds__(256, 2) pwg_layer_kernel(const LayerArgs a) {
+  using SM = LayerSmem<MT>;
   constexpr int GHPAD = (MT == 1) ? 16 : 16 * MT;
+  constexpr int GR = SM::GR;
   constexpr int NQ = GHPAD / 2;                 // k-steps of GEMM 2
   constexpr int NG = (MT == 1) ? 1 : MT / 2;    // gate register tiles
-  constexpr int A_CHUNK = (KC / 2) * MT * 64;   // floats of weight fragments per K chunk
-  constexpr int B_CHUNK = KC * TILE;
-  constexpr int W2_FLOATS = NQ * M2T * 64;
-  constexpr int LDS_FLOATS = (A_CHUNK + B_CHUNK) > W2_FLOATS ? (A_CHUNK + B_CHUNK) : W2_FLOATS;
-  __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
-  float* As = lds;
-  float* Bs = lds + A_CHUNK;
+  static_assert(SM::A_CHUNK / 4 <= 512, "A chunk staged by at most two float4 per thread");
+  __shared__ __attribute__((aligned(16))) float lds[SM::FLOATS];
+  float* ds = lds + 2 * SM::BUF;                // aux D tile [nfwg][GR]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -217,11 +268,25 @@ __global__ void __launch_bounds__(256) pwg_layer_kernel(const LayerArgs a) {
   const long long tile = blockIdx.x;
   const UttDesc ud = a.utts[a.tile_utt[tile]];
   const long long col0 = tile * TILE;
-  const long long t0 = col0 - ud.seg_base;
+  const long long t0 = col0 - ud.seg_base;      // local sample index of the tile start
   const long long Tu = ud.T;
   const long long P = a.Tpad;
-  const int KSR = a.KS * a.R;
-  const int K1 = KSR + a.A;
+  const int NC = a.KS * a.RP / KC;
+  const int H = a.tab.H;
+
+  // ---- prologue: chunk 0 in flight, aux D tile to LDS
+  ChunkRegs cr;
+  layer_load_chunk<MT, ALIGNED>(a, 0, ud, t0, tid, cr);
+  const long long fwg0 = t0 / H - a.tab.J1;     // first staged frame (utterance-local)
+  for (int idx = tid; idx < a.nfwg * GR; idx += 256) {
+    const int fi = idx / GR, row = idx - fi * GR;
+    const long long f = fwg0 + fi;
+    const long long fc = f < 0 ? 0 : (f >= ud.frames ? ud.frames - 1 : f);
+    const float v = a.d[(size_t)(ud.frame_base + fc) * GR + row];
+    ds[idx] = (f >= 0 && f < ud.frames) ? v : 0.f;
+  }
+  layer_store_chunk<MT>(lds, tid, cr);
+  __syncthreads();
 
   f32x16 acc[MT];
 #pragma unroll
@@ -229,29 +294,12 @@ __global__ void __launch_bounds__(256) pwg_layer_kernel(const LayerArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
 
-  for (int kc = 0; kc < a.K1pad; kc += KC) {
-    {
-      const float4* src = reinterpret_cast<const float4*>(a.wg + (size_t)(kc / 2) * MT * 64);
-      float4* dst = reinterpret_cast<float4*>(As);
-      for (int i = tid; i < A_CHUNK / 4; i += 256) dst[i] = src[i];
-    }
-#pragma unroll
-    for (int i = 0; i < B_CHUNK / 256; ++i) {
-      const int idx = tid + 256 * i;
-      const int row = idx / TILE, c = idx % TILE;
-      const int k = kc + row;
-      float v = 0.f;
-      if (k < KSR) {
-        const int tap = k / a.R;
-        const int ch = k - tap * a.R;
-        const long long src = t0 + c + (long long)(tap - a.tap_center) * a.dil;
-        if (src >= 0 && src < Tu) v = a.x_in[(size_t)ch * P + ud.seg_base + src];
-      } else if (k < K1) {
-        v = a.cup[(size_t)(k - KSR) * P + col0 + c];
-      }
-      Bs[row * TILE + c] = v;
-    }
-    __syncthreads();
+  // ---- GEMM 1 main loop
+  for (int c = 0; c < NC; ++c) {
+    if (c + 1 < NC) layer_load_chunk<MT, ALIGNED>(a, c + 1, ud, t0, tid, cr);
+    const float* buf = lds + (c & 1) * SM::BUF;
+    const float* As = buf;
+    const float* Bs = buf + SM::A_CHUNK;
 #pragma unroll
     for (int s = 0; s < KC / 2; ++s) {
       const float b = Bs[(2 * s + hh) * TILE + wave * 32 + cl];
@@ -261,10 +309,47 @@ __global__ void __launch_bounds__(256) pwg_layer_kernel(const LayerArgs a) {
         acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, b, acc[m], 0, 0, 0);
       }
     }
+    if (c + 1 < NC) layer_store_chunk<MT>(lds + ((c + 1) & 1) * SM::BUF, tid, cr);
     __syncthreads();
   }
 
-  // gate: tanh(Za) * sigmoid(Zb)  (residual_block.py:123-132)
+  // ---- aux term: + sum_f D[f][row] * w_t[f - t/H + J1]
+  {
+    const long long t = t0 + wave * 32 + cl;
+    float wt[AUX_J4];
+    {
+      const long long tc = t < Tu ? t : Tu - 1;  // padding columns: load a valid row, zero it below
+      const float* row;
+      const long long F = ud.frames;
+      if (F < a.tab.Fmin) row = a.tab.small + ((long long)H * F * (F - 1) / 2 + tc) * AUX_J4;
+      else if (tc < a.tab.TL) row = a.tab.left + tc * AUX_J4;
+      else if (tc >= Tu - a.tab.TR) row = a.tab.right + (Tu - 1 - tc) * AUX_J4;
+      else row = a.tab.interior + (tc % H) * AUX_J4;
+      const f32x4 w0 = *reinterpret_cast<const f32x4*>(row);
+      const f32x4 w1 = *reinterpret_cast<const f32x4*>(row + 4);
+      const bool ok = t < Tu;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        wt[j] = ok ? w0[j] : 0.f;
+        wt[j + 4] = ok ? w1[j] : 0.f;
+      }
+    }
+    const long long fb = t / H - a.tab.J1;                       // frame of wt[0]
+    const long long fw0 = (t0 + wave * 32) / H - a.tab.J1;      // wave window start (uniform)
+    const int fo = (int)(fw0 - fwg0);
+    for (int s = 0; s < a.nka; ++s) {
+      const int j = (int)(fw0 + 2 * s + hh - fb);
+      float bw = 0.f;
+#pragma unroll
+      for (int q = 0; q < AUX_J4; ++q) bw = (j == q) ? wt[q] : bw;
+      const float* drow = ds + (fo + 2 * s + hh) * GR + cl;
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(drow[32 * m], bw, acc[m], 0, 0, 0);
+    }
+  }
+
+  // ---- gate: tanh(Za) * sigmoid(Zb)  (residual_block.py:123-132)
   float g[NG][16];
 #pragma unroll
   for (int gm = 0; gm < NG; ++gm) {
@@ -278,30 +363,22 @@ __global__ void __launch_bounds__(256) pwg_layer_kernel(const LayerArgs a) {
     }
   }
 
-  // stage W2 fragments
-  {
-    const float4* src = reinterpret_cast<const float4*>(a.w2);
-    float4* dst = reinterpret_cast<float4*>(lds);
-    for (int i = tid; i < W2_FLOATS / 4; i += 256) dst[i] = src[i];
-  }
-  __syncthreads();
-
+  // ---- GEMM 2: [skip; out] = W2 . g, A fragments from global (L1/L2)
   f32x16 acc2[M2T];
 #pragma unroll
   for (int m = 0; m < M2T; ++m)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc2[m][r] = 0.f;
+  const float* w2 = a.w2 + lane;
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
     const float bq = g[q >> 4][q & 15];
 #pragma unroll
-    for (int m2 = 0; m2 < M2T; ++m2) {
-      const float av = lds[(q * M2T + m2) * 64 + lane];
-      acc2[m2] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bq, acc2[m2], 0, 0, 0);
-    }
+    for (int m2 = 0; m2 < M2T; ++m2)
+      acc2[m2] = __builtin_amdgcn_mfma_f32_32x32x2f32(w2[(q * M2T + m2) * 64], bq, acc2[m2], 0, 0, 0);
   }
 
-  // epilogue: skip += W_s g + b_s ; x = (W_o g + b_o + x) * sqrt(0.5)   (residual_block.py:135-138)
+  // ---- epilogue: skip += W_s g + b_s ; x = (W_o g + b_o + x) * sqrt(0.5)   (residual_block.py:135-138)
   const size_t gt = (size_t)(col0 + wave * 32 + cl);
 #pragma unroll
   for (int m2 = 0; m2 < M2T; ++m2) {
@@ -359,8 +436,10 @@ hipError_t launch_conv_in(const ConvInArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_upsample(const UpsampleArgs& a, long long n_tiles, hipStream_t s) {
-  hipLaunchKernelGGL(pwg_upsample_kernel, dim3((unsigned)n_tiles), dim3(256), 0, s, a);
+hipError_t launch_aux_proj(const AuxProjArgs& a, int layers, hipStream_t s) {
+  const dim3 grid((unsigned)((a.F_total + 63) / 64), (unsigned)layers), block(a.GR);
+  const size_t lds = sizeof(float) * ((size_t)a.A * 64 + (size_t)a.GR * (a.A + 1));
+  hipLaunchKernelGGL(pwg_aux_proj_kernel, grid, block, lds, s, a);
   return hipGetLastError();
 }
 
@@ -371,10 +450,12 @@ hipError_t launch_first_conv(const FirstConvArgs& a, long long n_tiles, hipStrea
 
 hipError_t launch_layer(const LayerArgs& a, int mt, int m2t, long long n_tiles, hipStream_t s) {
   const dim3 grid((unsigned)n_tiles), block(256);
-#define PWG_LAYER_CASE(MT_, M2T_)                                                   \
-  if (mt == MT_ && m2t == M2T_) {                                                   \
-    hipLaunchKernelGGL((pwg_layer_kernel<MT_, M2T_>), grid, block, 0, s, a);        \
-    return hipGetLastError();                                                       \
+  const bool aligned = (a.dil % 4) == 0;
+#define PWG_LAYER_CASE(MT_, M2T_)                                                             \
+  if (mt == MT_ && m2t == M2T_) {                                                             \
+    if (aligned) hipLaunchKernelGGL((pwg_layer_kernel<MT_, M2T_, true>), grid, block, 0, s, a);  \
+    else hipLaunchKernelGGL((pwg_layer_kernel<MT_, M2T_, false>), grid, block, 0, s, a);         \
+    return hipGetLastError();                                                                 \
   }
   PWG_LAYER_CASE(1, 1) PWG_LAYER_CASE(1, 2) PWG_LAYER_CASE(1, 4)
   PWG_LAYER_CASE(2, 1) PWG_LAYER_CASE(2, 2) PWG_LAYER_CASE(2, 4)

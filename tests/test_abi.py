@@ -83,20 +83,19 @@ def test_invalid_configs_raise_reference_exceptions(built_lib, override, exc):
         HostHandle(params)
 
 
-def _ref_pack_gate(wd, wa, G, R, A, KS, lane, s, m):
-    """Independent restatement of the gate A-fragment element (kernel docs in pwg_kernels.hip)."""
+def _ref_pack_gate(wd, G, R, KS, lane, s, m):
+    """Independent restatement of the gate A-fragment element (pwg_kernels.hip, GEMM 1): K rows
+    are tap blocks of RP = ceil(R/16)*16 channels, gate rows packed [Za | pad | Zb | pad]."""
     GH = G // 2
     GHPAD = 16 if GH <= 16 else (GH + 31) // 32 * 32
+    RP = (R + 15) // 16 * 16
     prow = 32 * m + (lane & 31)
     k = 2 * s + (lane >> 5)
     grow = (prow if prow < GH else None) if prow < GHPAD else (GH + prow - GHPAD if prow - GHPAD < GH else None)
-    if grow is None:
+    tap, ch = k // RP, k % RP
+    if grow is None or ch >= R:
         return 0.0
-    if k < KS * R:
-        return wd[grow, k % R, k // R]
-    if k < KS * R + A:
-        return wa[grow, k - KS * R, 0]
-    return 0.0
+    return wd[grow, ch, tap]
 
 
 @pytest.mark.parametrize("name", ["reference_test", "ljspeech_v1"])
@@ -107,25 +106,20 @@ def test_pack_gate_fragments(built_lib, name):
     packed = h.pack(sd)
     assert packed.shape == (h.packed_weight_count,)
     assert np.isfinite(packed).all()
-    # the first layer's gate fragments start right after the fixed blocks; find them by value
     wd = sd["conv_layers.0.conv.weight"]
-    wa = sd["conv_layers.0.conv1x1_aux.weight"]
-    G, R = wd.shape[0], wd.shape[1]
-    A = wa.shape[1]
-    KS = wd.shape[2]
-    first = [_ref_pack_gate(wd, wa, G, R, A, KS, lane, 0, 0) for lane in range(64)]
-    # locate the 64-float fragment in the image
-    f = np.asarray(first, np.float32)
+    G, R, KS = wd.shape
+    GH = G // 2
+    MT = 1 if GH <= 16 else (GH + 31) // 32 * 32 // 16
+    RP = (R + 15) // 16 * 16
+    # locate the first layer's first fragment in the image by value, then check all of them
+    f = np.asarray([_ref_pack_gate(wd, G, R, KS, lane, 0, 0) for lane in range(64)], np.float32)
     hits = [i for i in range(0, packed.size - 64, 64) if np.array_equal(packed[i:i + 64], f)]
     assert len(hits) == 1
     base = hits[0]
-    GH = G // 2
-    MT = 1 if GH <= 16 else (GH + 31) // 32 * 32 // 16
-    K1pad = (KS * R + A + 15) // 16 * 16
-    for s in range(K1pad // 2):
+    for s in range(KS * RP // 2):
         for m in range(MT):
             frag = packed[base + (s * MT + m) * 64: base + (s * MT + m + 1) * 64]
-            ref = [_ref_pack_gate(wd, wa, G, R, A, KS, lane, s, m) for lane in range(64)]
+            ref = [_ref_pack_gate(wd, G, R, KS, lane, s, m) for lane in range(64)]
             np.testing.assert_array_equal(frag, np.asarray(ref, np.float32))
 
 
