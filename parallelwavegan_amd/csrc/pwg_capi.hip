@@ -246,13 +246,13 @@ struct PwgHandle {
   PwgConfig cfg;
   int device;
   // derived shapes
-  int R, RP, G, GH, GHPAD, GR, MT, S, M2T, A, KS, KW, O, L, lps, K1, NQ;
+  int R, RP, RS, G, GH, GHPAD, GR, MT, S, SS, M2T, A, KS, KW, O, L, lps, K1, NQ, NQ4;
   std::vector<int> dil;
   AuxStruct aux;
   // packed image offsets (floats)
   size_t off_first_w, off_first_b, off_conv_in, off_waux;
   size_t off_tab_interior, off_tab_left, off_tab_right, off_tab_small;
-  size_t off_layers, layer_stride, lo_wg, lo_bg, lo_w2, lo_b2;
+  size_t off_layers, layer_stride, lo_wg, lo_bg, lo_w2;
   size_t off_head_w1, off_head_b1, off_head_w2, off_head_b2, packed_total;
   long long ref_total;
   // timing
@@ -317,6 +317,9 @@ int pwg_create(const PwgConfig* cfg, int device, PwgHandle** out) {
   h->GR = 32 * h->MT;
   h->M2T = (h->S + h->R + 31) / 32;
   h->RP = (h->R + KC - 1) / KC * KC;
+  h->RS = (h->R + 3) / 4 * 4;
+  h->SS = (h->S + 3) / 4 * 4;
+  h->NQ4 = (h->NQ + 1 + 3) / 4;
   h->K1 = h->KS * h->RP;
   if (!(h->MT == 1 || h->MT == 2 || h->MT == 4) || !(h->M2T == 1 || h->M2T == 2 || h->M2T == 4)) {
     delete h;
@@ -346,8 +349,7 @@ int pwg_create(const PwgConfig* cfg, int device, PwgHandle** out) {
   h->lo_wg = 0;
   h->lo_bg = h->lo_wg + align64((size_t)(h->K1 / 2) * h->MT * 64);
   h->lo_w2 = h->lo_bg + align64(2 * h->GHPAD);
-  h->lo_b2 = h->lo_w2 + align64((size_t)h->NQ * h->M2T * 64);
-  h->layer_stride = h->lo_b2 + align64(32 * h->M2T);
+  h->layer_stride = h->lo_w2 + align64((size_t)h->NQ4 * h->M2T * 64 * 4);
   h->off_layers = o; o += h->layer_stride * h->L;
   h->off_head_w1 = o; o += align64((size_t)h->S * h->S);
   h->off_head_b1 = o; o += align64(h->S);
@@ -451,23 +453,26 @@ int pwg_pack_weights(const PwgHandle* h, const float* ref, float* pk) {
       bg[prow] = gr < 0 ? 0.f : bd[gr];
       for (int i = 0; i < A; ++i) waux[(size_t)prow * A + i] = gr < 0 ? 0.f : wa[(size_t)gr * A + i];
     }
+    // GEMM 2 A fragments, 4 k-steps per 16-byte lane load: [q/4][m2][lane][q%4]; k-step NQ is
+    // the bias (A[i][0] = b2[row i], B = ones row).
     float* w2 = L0 + h->lo_w2;
-    for (int q = 0; q < h->NQ; ++q)
+    for (int q = 0; q < 4 * h->NQ4; ++q)
       for (int m2 = 0; m2 < M2T; ++m2)
         for (int lane = 0; lane < 64; ++lane) {
           const int row2 = 32 * m2 + (lane & 31);
-          const int r = q & 15, gm = q >> 4;
-          const int ch = 32 * gm + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
           float v = 0.f;
-          if (ch < GH) {
-            if (row2 < S) v = ws[(size_t)row2 * GH + ch];
-            else if (row2 < S + R) v = wo[(size_t)(row2 - S) * GH + ch];
+          if (q < h->NQ) {
+            const int r = q & 15, gm = q >> 4;
+            const int ch = 32 * gm + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            if (ch < GH) {
+              if (row2 < S) v = ws[(size_t)row2 * GH + ch];
+              else if (row2 < S + R) v = wo[(size_t)(row2 - S) * GH + ch];
+            }
+          } else if (q == h->NQ && lane < 32) {
+            v = row2 < S ? bs[row2] : (row2 < S + R ? bo[row2 - S] : 0.f);
           }
-          w2[((size_t)q * M2T + m2) * 64 + lane] = v;
+          w2[(((size_t)(q / 4) * M2T + m2) * 64 + lane) * 4 + (q % 4)] = v;
         }
-    float* b2 = L0 + h->lo_b2;
-    for (int row2 = 0; row2 < 32 * M2T; ++row2)
-      b2[row2] = row2 < S ? bs[row2] : (row2 < S + R ? bo[row2 - S] : 0.f);
   }
   for (size_t i = 0; i < (size_t)S * S; ++i) pk[h->off_head_w1 + i] = *p++;
   for (int i = 0; i < S; ++i) pk[h->off_head_b1 + i] = *p++;
@@ -522,9 +527,9 @@ int pwg_plan_create(PwgHandle* h, int n_utts, const long long* frames, int layou
     for (long long t = b; t < e; ++t) tile_utt[t] = u;
   }
   size_t o = 0;
-  p->ws_x0 = o; o += align_bytes(sizeof(float) * h->R * p->Tpad);
-  p->ws_x1 = o; o += align_bytes(sizeof(float) * h->R * p->Tpad);
-  p->ws_skip = o; o += align_bytes(sizeof(float) * h->S * p->Tpad);
+  p->ws_x0 = o; o += align_bytes(sizeof(float) * h->RS * p->Tpad);
+  p->ws_x1 = o; o += align_bytes(sizeof(float) * h->RS * p->Tpad);
+  p->ws_skip = o; o += align_bytes(sizeof(float) * h->SS * p->Tpad);
   p->ws_c1 = o; o += align_bytes(sizeof(float) * h->A * p->F_total);
   p->ws_d = o; o += align_bytes(sizeof(float) * h->L * h->GR * p->F_total);
   p->ws_total = o;
@@ -615,7 +620,7 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
 
   FirstConvArgs fa;
   fa.noise = noise; fa.w = packed + h->off_first_w; fa.b = packed + h->off_first_b; fa.x = x0;
-  fa.tile_utt = p->d_tile_utt; fa.utts = p->d_utts; fa.Tpad = p->Tpad; fa.R = h->R;
+  fa.tile_utt = p->d_tile_utt; fa.utts = p->d_utts; fa.Tpad = p->Tpad; fa.R = h->R; fa.RS = h->RS;
   e = timed(PWG_KERNEL_FIRST_CONV, [&] { return launch_first_conv(fa, p->n_tiles, s); });
   if (e != hipSuccess) return hip_fail(e, "first_conv launch");
 
@@ -630,9 +635,9 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
     la.tab.right = packed + h->off_tab_right; la.tab.small = packed + h->off_tab_small;
     la.tab.H = (int)h->aux.H; la.tab.J1 = h->aux.J1; la.tab.TL = h->aux.TL; la.tab.TR = h->aux.TR;
     la.tab.Fmin = h->aux.Fmin; la.nka = h->aux.nka; la.nfwg = h->aux.nfwg;
-    la.wg = L0 + h->lo_wg; la.bg = L0 + h->lo_bg; la.w2 = L0 + h->lo_w2; la.b2 = L0 + h->lo_b2;
+    la.wg = L0 + h->lo_wg; la.bg = L0 + h->lo_bg; la.w2 = L0 + h->lo_w2;
     la.tile_utt = p->d_tile_utt; la.utts = p->d_utts; la.Tpad = p->Tpad;
-    la.R = h->R; la.RP = h->RP; la.S = h->S; la.KS = h->KS; la.dil = h->dil[l];
+    la.R = h->R; la.RP = h->RP; la.RS = h->RS; la.S = h->S; la.SS = h->SS; la.KS = h->KS; la.dil = h->dil[l];
     la.tap_center = h->cfg.use_causal_conv ? h->KS - 1 : (h->KS - 1) / 2;
     la.first = l == 0;
     e = timed(PWG_KERNEL_RESIDUAL_LAYER, [&] { return launch_layer(la, h->MT, h->M2T, p->n_tiles, s); });
@@ -643,7 +648,7 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
   HeadArgs ha;
   ha.skip = skip; ha.w1 = packed + h->off_head_w1; ha.b1 = packed + h->off_head_b1;
   ha.w2 = packed + h->off_head_w2; ha.b2 = packed + h->off_head_b2; ha.out = out;
-  ha.tile_utt = p->d_tile_utt; ha.utts = p->d_utts; ha.Tpad = p->Tpad; ha.S = h->S; ha.O = h->O;
+  ha.tile_utt = p->d_tile_utt; ha.utts = p->d_utts; ha.Tpad = p->Tpad; ha.S = h->S; ha.SS = h->SS; ha.O = h->O;
   ha.skip_scale = (float)std::sqrt(1.0 / h->L);
   if (p->layout == PWG_LAYOUT_INFERENCE) { ha.out_stride_t = h->O; ha.out_stride_o = 1; }
   else { ha.out_stride_t = 1; ha.out_stride_o = p->utts[0].T; }

@@ -71,27 +71,29 @@ struct FirstConvArgs {
   const float* noise;    // compact
   const float* w;        // [R]
   const float* b;        // [R]
-  float* x;              // [R][Tpad]
+  float* x;              // [Tpad][RS] time-major
   const int* tile_utt;
   const UttDesc* utts;
   long long Tpad;
-  int R;
+  int R, RS;
 };
 
+// Residual stream x and skip sum are TIME-major ([Tpad][RS], [Tpad][SS], RS/SS = R/S rounded up
+// to 4): the MFMA accumulator holds 4 consecutive channels of one sample per register quad, so
+// the epilogue moves them with one 16-byte access, and a dilation shift moves whole rows.
 struct LayerArgs {
-  const float* x_in;     // [R][Tpad]
-  float* x_out;          // [R][Tpad]
-  float* skip;           // [S][Tpad]
+  const float* x_in;     // [Tpad][RS]
+  float* x_out;          // [Tpad][RS]
+  float* skip;           // [Tpad][SS]
   const float* d;        // this layer's frame-rate aux projection [F_total][GR]
   AuxTab tab;
   const float* wg;       // gate GEMM A-fragments [K1/2][MT][64], K1 = KS*RP
-  const float* bg;       // [2*GHPAD]
-  const float* w2;       // skip|out GEMM A-fragments [GHPAD/2][M2T][64]
-  const float* b2;       // [32*M2T]
+  const float* bg;       // [2*GHPAD]  gate bias, added by an MFMA k-step against a ones row
+  const float* w2;       // skip|out GEMM A-fragments incl. a bias k-step, [NQ4][M2T][64][4]
   const int* tile_utt;
   const UttDesc* utts;
   long long Tpad;
-  int R, RP, S, KS;      // RP = R rounded up to KC (one K chunk never straddles two taps)
+  int R, RP, RS, S, SS, KS;  // RP = R rounded up to KC (one K chunk never straddles two taps)
   int dil;
   int nka;               // aux k-steps per wave (frames of a 32-sample window / 2)
   int nfwg;              // frames staged per workgroup
@@ -100,7 +102,7 @@ struct LayerArgs {
 };
 
 struct HeadArgs {
-  const float* skip;     // [S][Tpad]
+  const float* skip;     // [Tpad][SS] time-major
   const float* w1;       // [S][S]
   const float* b1;       // [S]
   const float* w2;       // [O][S]
@@ -109,7 +111,7 @@ struct HeadArgs {
   const int* tile_utt;
   const UttDesc* utts;
   long long Tpad;
-  int S, O;
+  int S, SS, O;
   float skip_scale;      // sqrt(1/L), models/parallel_wavegan.py:166
   // element strides of the caller's output; utterance u starts at io_off*O in both layouts
   // (inference: (T_u, O) time-major -> t*O + o; forward: (B, O, T) -> o*T + t)

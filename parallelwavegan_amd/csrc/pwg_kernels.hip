@@ -126,18 +126,18 @@ __global__ void __launch_bounds__(128) pwg_aux_proj_kernel(const AuxProjArgs a) 
 }
 
 // ---------------------------------------------------------------------------------------------
-// first_conv (1x1, 1 -> R, bias): writes X0 on the padded axis, zero in segment padding.
+// first_conv (1x1, 1 -> R, bias): writes X0 time-major [Tpad][RS], zero in segment padding.
 __global__ void __launch_bounds__(256) pwg_first_conv_kernel(const FirstConvArgs a) {
   const long long tile = blockIdx.x;
   const UttDesc ud = a.utts[a.tile_utt[tile]];
   const long long col0 = tile * TILE;
   const long long t0 = col0 - ud.seg_base;
-  for (int idx = threadIdx.x; idx < a.R * TILE; idx += 256) {
-    const int c = idx / TILE, j = idx % TILE;
+  for (int idx = threadIdx.x; idx < a.RS * TILE; idx += 256) {
+    const int j = idx / a.RS, c = idx - j * a.RS;
     const long long t = t0 + j;
     float v = 0.f;
-    if (t < ud.T) v = fmaf(a.w[c], a.noise[ud.io_off + t], a.b[c]);
-    a.x[(size_t)c * a.Tpad + col0 + j] = v;
+    if (t < ud.T && c < a.R) v = fmaf(a.w[c], a.noise[ud.io_off + t], a.b[c]);
+    a.x[(size_t)(col0 + j) * a.RS + c] = v;
   }
 }
 
@@ -148,31 +148,35 @@ __global__ void __launch_bounds__(256) pwg_first_conv_kernel(const FirstConvArgs
 //
 // GEMM 1 (gate pre-activation, GR = 32*MT packed rows):
 //   Z = Wdil . [x(t+(0-c)d); x(t+(1-c)d); ...]   K = KS*RP, streamed through LDS in KC=16 chunks,
-//       one chunk = 16 channels of ONE tap (uniform source offset), double-buffered: the global
+//       one chunk = 16 channels of ONE tap (uniform time shift), double-buffered: the global
 //       loads of chunk i+1 are in flight while chunk i's MFMAs run, one barrier per chunk;
 //     + U(D_l)                                   the aux term at sample rate from frame-rate
-//       projections: a K = 2*nka (<= 16) GEMM whose A operand is the staged D tile [frame][row]
-//       and whose B operand (frame f, sample t) is the composite upsampler tap w_t[f - t/H + J1],
-//       computed per lane from the AuxTab row of its sample.
+//       projections: a K = 2*nka GEMM whose A operand is the staged D tile [frame][row] and whose
+//       B operand (frame f, sample t) is the composite upsampler tap w_t[f - t/H + J1], from the
+//       AuxTab row of the lane's sample;
+//     + bias                                     one k-step: A = [bg; 0], B = [1; 0].
 //   v_mfma_f32_32x32x2_f32 throughout; A fragments are host-packed lane-linear (64 floats per
-//   (k-step, m-tile)), B fragments one ds_read_b32 per lane.
-// gate: g = tanh(Za + ba) * sigmoid(Zb + bb); Za rows [0,GHPAD), Zb rows [GHPAD, 2*GHPAD) sit in
-//   the same lane/register of m-tiles m and m+MT/2 (MT==1: registers r and r+8).
+//   (k-step, m-tile)); the activation chunk sits time-major in LDS ([t][KC+1], conflict-free
+//   B-fragment reads).
+// gate: g = tanh(Za) * sigmoid(Zb) on v_exp/v_rcp; Za rows [0,GHPAD), Zb rows [GHPAD, 2*GHPAD)
+//   sit in the same lane/register of m-tiles m and m+MT/2 (MT==1: registers r and r+8).
 // GEMM 2 ([skip; out] rows, 32*M2T): the gate accumulator register (m, r) IS the B fragment of
 //   one k-step (lane l: channel row(m,r,l>>5), column l&31); the host packs W2 in that permuted-k
-//   order. W2 fragments are read straight from global memory (L1/L2-resident, 32 KB per layer).
-// C/D map of the 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+//   order, 4 k-steps per 16-byte load, plus one bias k-step against a ones row. W2 is read from
+//   global memory (L1/L2-resident, 33 KB per layer).
+// C/D map of the 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5): registers
+//   4j..4j+3 are 4 consecutive channels of one sample -> one 16-byte access in the time-major
+//   epilogue.
 template <int MT>
 struct LayerSmem {
   static constexpr int GR = 32 * MT;
+  static constexpr int BSTR = KC + 1;                 // time-major B row stride (floats)
   static constexpr int A_CHUNK = (KC / 2) * MT * 64;  // floats of weight fragments per K chunk
-  static constexpr int B_CHUNK = KC * TILE;           // floats of activations per K chunk
+  static constexpr int B_CHUNK = TILE * BSTR;         // floats of activations per K chunk
   static constexpr int BUF = A_CHUNK + B_CHUNK;
-  static constexpr int FLOATS = 2 * BUF + AUX_MAX_NFWG * GR;
+  static constexpr int FLOATS = 2 * BUF + (AUX_MAX_NFWG + 2) * GR;
 };
 
-// Registers carrying one K chunk from global memory to LDS (named fields, not arrays: an array
-// indexed across the unrolled staging loops ends up in scratch).
 // Registers carrying one K chunk from global memory to LDS: raw loads plus a validity mask that
 // is applied only when the chunk is written to LDS, so no instruction touches the loaded values
 // before the MFMAs of the current chunk have been issued (named fields, native vectors: a
@@ -182,83 +186,70 @@ struct ChunkRegs {
   unsigned mask;  // bit j: element j of b0, bit 4+j: element j of b1
 };
 
-// x[ch][e..e+3] of one utterance from an address clamped into the utterance's padded segment;
-// returns the raw vector and the validity bits (inside [0, T) and ch < R). ALIGNED (every tap
-// offset a multiple of 4, i.e. dilation % 4 == 0) selects one dwordx4 load, else 4 dword loads;
-// it is a template parameter so neither path carries a branch around its loads.
-template <bool ALIGNED>
-__device__ __forceinline__ f32x4 load_x4(const LayerArgs& a, const UttDesc& ud, long long segpad, int ch,
-                                         long long e, unsigned& bits) {
-  const bool chok = ch < a.R;
-  const float* src = a.x_in + (size_t)(chok ? ch : 0) * a.Tpad + ud.seg_base;
-  const long long Tu = ud.T;
-  f32x4 v;
-  if (ALIGNED) {
-    const long long ec = e < 0 ? 0 : (e > segpad - 4 ? segpad - 4 : e);
-    v = *reinterpret_cast<const f32x4*>(src + ec);
-  } else {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const long long ej = e + j;
-      v[j] = src[ej < 0 ? 0 : (ej > segpad - 1 ? segpad - 1 : ej)];
-    }
-  }
-  bits = 0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) bits |= (chok && e + j >= 0 && e + j < Tu) ? (1u << j) : 0u;
-  return v;
-}
-
 // Chunk c = 16 consecutive K rows of ONE tap: A fragments (contiguous in the packed image) and
-// the activation rows x[ch0..ch0+15][t0 + off .. t0 + off + 127], zero outside the utterance.
-template <int MT, bool ALIGNED>
+// the activation rows x[t0 + off + t][ch0 .. ch0+15], t in [0, 128), zero outside the utterance.
+// Thread -> (t = tid/4 + 64 i, channel quad q = tid%4): lanes 4t..4t+3 read one 64-byte row
+// piece. Loads are unconditional from addresses clamped into the utterance's padded segment
+// (a load under a divergent branch makes hipcc wait vmcnt(0) at the merge,
+// cdna_hip_programming.md sec 5 item 4(c)).
+template <int MT>
 __device__ __forceinline__ void layer_load_chunk(const LayerArgs& a, int c, const UttDesc& ud, long long t0,
-                                                 int tid, ChunkRegs& r) {
+                                                 long long segpad, int tid, ChunkRegs& r) {
   constexpr int NA4 = LayerSmem<MT>::A_CHUNK / 4;
   const f32x4* wsrc = reinterpret_cast<const f32x4*>(a.wg + (size_t)c * LayerSmem<MT>::A_CHUNK);
   r.a0 = wsrc[NA4 >= 256 ? tid : (tid < NA4 ? tid : 0)];
   r.a1 = NA4 > 256 ? wsrc[tid + 256] : r.a0;
   const int k0 = c * KC;
   const int tap = k0 / a.RP;                 // uniform
-  const int ch0 = k0 - tap * a.RP;
+  const int ch = k0 - tap * a.RP + 4 * (tid & 3);
   const long long off = (long long)(tap - a.tap_center) * a.dil;
-  const int row = tid >> 5, c4 = tid & 31;
-  const long long e = t0 + 4 * c4 + off;
-  const long long segpad = (ud.T + SEG - 1) / SEG * SEG;
-  unsigned m0, m1;
-  r.b0 = load_x4<ALIGNED>(a, ud, segpad, ch0 + row, e, m0);
-  r.b1 = load_x4<ALIGNED>(a, ud, segpad, ch0 + row + 8, e, m1);
-  r.mask = m0 | (m1 << 4);
+  const float* base = a.x_in + (size_t)ud.seg_base * a.RS + (ch < a.RS ? ch : 0);
+  unsigned m = 0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const long long e = t0 + (tid >> 2) + 64 * i + off;
+    const long long ec = e < 0 ? 0 : (e > segpad - 1 ? segpad - 1 : e);
+    const f32x4 v = *reinterpret_cast<const f32x4*>(base + ec * a.RS);
+    if (i == 0) r.b0 = v; else r.b1 = v;
+    const bool tok = e >= 0 && e < ud.T;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) m |= (tok && ch + j < a.R) ? (1u << (4 * i + j)) : 0u;
+  }
+  r.mask = m;
 }
 
 template <int MT>
 __device__ __forceinline__ void layer_store_chunk(float* buf, int tid, const ChunkRegs& r) {
   constexpr int NA4 = LayerSmem<MT>::A_CHUNK / 4;
+  constexpr int BSTR = LayerSmem<MT>::BSTR;
   f32x4* as = reinterpret_cast<f32x4*>(buf);
   if (NA4 >= 256 || tid < NA4) as[tid] = r.a0;
   if (NA4 > 256) as[tid + 256] = r.a1;
-  float* bs = buf + LayerSmem<MT>::A_CHUNK;
-  const int row = tid >> 5, c4 = tid & 31;
-  f32x4 b0, b1;
+  float* bs = buf + LayerSmem<MT>::A_CHUNK + (tid >> 2) * BSTR + 4 * (tid & 3);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    b0[j] = (r.mask >> j) & 1u ? r.b0[j] : 0.f;
-    b1[j] = (r.mask >> (4 + j)) & 1u ? r.b1[j] : 0.f;
+    bs[j] = (r.mask >> j) & 1u ? r.b0[j] : 0.f;
+    bs[64 * BSTR + j] = (r.mask >> (4 + j)) & 1u ? r.b1[j] : 0.f;
   }
-  *reinterpret_cast<f32x4*>(bs + row * TILE + 4 * c4) = b0;
-  *reinterpret_cast<f32x4*>(bs + (row + 8) * TILE + 4 * c4) = b1;
 }
 
-template <int MT, int M2T, bool ALIGNED>
+// tanh(x) = 2 sigmoid(2x) - 1 and sigmoid(x) = 1 / (1 + e^-x) on v_exp_f32 / v_rcp_f32
+// (~1e-7 absolute error; the reference uses torch.tanh / torch.sigmoid, residual_block.py:132).
+__device__ __forceinline__ float fast_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+__device__ __forceinline__ float fast_tanh(float x) { return 2.f * __builtin_amdgcn_rcpf(1.f + __expf(-2.f * x)) - 1.f; }
+
+template <int MT, int M2T>
 __global__ void __launch_bounds__(256, 2) pwg_layer_kernel(const LayerArgs a) {
   using SM = LayerSmem<MT>;
   constexpr int GHPAD = (MT == 1) ? 16 : 16 * MT;
   constexpr int GR = SM::GR;
-  constexpr int NQ = GHPAD / 2;                 // k-steps of GEMM 2
+  constexpr int BSTR = SM::BSTR;
+  constexpr int NQ = GHPAD / 2;                 // k-steps of GEMM 2 (+1 bias step)
+  constexpr int NQ4 = (NQ + 1 + 3) / 4;         // 16-byte W2 fragment groups
   constexpr int NG = (MT == 1) ? 1 : MT / 2;    // gate register tiles
   static_assert(SM::A_CHUNK / 4 <= 512, "A chunk staged by at most two float4 per thread");
   __shared__ __attribute__((aligned(16))) float lds[SM::FLOATS];
-  float* ds = lds + 2 * SM::BUF;                // aux D tile [nfwg][GR]
+  float* ds = lds + 2 * SM::BUF;                // aux D tile [nfwg][GR], then bias rows [bg; 0]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -270,13 +261,13 @@ __global__ void __launch_bounds__(256, 2) pwg_layer_kernel(const LayerArgs a) {
   const long long col0 = tile * TILE;
   const long long t0 = col0 - ud.seg_base;      // local sample index of the tile start
   const long long Tu = ud.T;
-  const long long P = a.Tpad;
+  const long long segpad = (Tu + SEG - 1) / SEG * SEG;
   const int NC = a.KS * a.RP / KC;
   const int H = a.tab.H;
 
-  // ---- prologue: chunk 0 in flight, aux D tile to LDS
+  // ---- prologue: chunk 0 in flight, aux D tile + gate bias to LDS
   ChunkRegs cr;
-  layer_load_chunk<MT, ALIGNED>(a, 0, ud, t0, tid, cr);
+  layer_load_chunk<MT>(a, 0, ud, t0, segpad, tid, cr);
   const long long fwg0 = t0 / H - a.tab.J1;     // first staged frame (utterance-local)
   for (int idx = tid; idx < a.nfwg * GR; idx += 256) {
     const int fi = idx / GR, row = idx - fi * GR;
@@ -284,6 +275,10 @@ __global__ void __launch_bounds__(256, 2) pwg_layer_kernel(const LayerArgs a) {
     const long long fc = f < 0 ? 0 : (f >= ud.frames ? ud.frames - 1 : f);
     const float v = a.d[(size_t)(ud.frame_base + fc) * GR + row];
     ds[idx] = (f >= 0 && f < ud.frames) ? v : 0.f;
+  }
+  if (tid < GR) {
+    ds[a.nfwg * GR + tid] = a.bg[tid];
+    ds[(a.nfwg + 1) * GR + tid] = 0.f;
   }
   layer_store_chunk<MT>(lds, tid, cr);
   __syncthreads();
@@ -296,13 +291,13 @@ __global__ void __launch_bounds__(256, 2) pwg_layer_kernel(const LayerArgs a) {
 
   // ---- GEMM 1 main loop
   for (int c = 0; c < NC; ++c) {
-    if (c + 1 < NC) layer_load_chunk<MT, ALIGNED>(a, c + 1, ud, t0, tid, cr);
+    if (c + 1 < NC) layer_load_chunk<MT>(a, c + 1, ud, t0, segpad, tid, cr);
     const float* buf = lds + (c & 1) * SM::BUF;
     const float* As = buf;
-    const float* Bs = buf + SM::A_CHUNK;
+    const float* Bs = buf + SM::A_CHUNK + (wave * 32 + cl) * BSTR + hh;
 #pragma unroll
     for (int s = 0; s < KC / 2; ++s) {
-      const float b = Bs[(2 * s + hh) * TILE + wave * 32 + cl];
+      const float b = Bs[2 * s];
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
         const float av = As[(s * MT + m) * 64 + lane];
@@ -313,7 +308,7 @@ __global__ void __launch_bounds__(256, 2) pwg_layer_kernel(const LayerArgs a) {
     __syncthreads();
   }
 
-  // ---- aux term: + sum_f D[f][row] * w_t[f - t/H + J1]
+  // ---- aux term: + sum_f D[f][row] * w_t[f - t/H + J1]  and the gate bias
   {
     const long long t = t0 + wave * 32 + cl;
     float wt[AUX_J4];
@@ -347,6 +342,10 @@ __global__ void __launch_bounds__(256, 2) pwg_layer_kernel(const LayerArgs a) {
       for (int m = 0; m < MT; ++m)
         acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(drow[32 * m], bw, acc[m], 0, 0, 0);
     }
+    const float* brow = ds + (a.nfwg + hh) * GR + cl;
+    const float one = hh == 0 ? 1.f : 0.f;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(brow[32 * m], one, acc[m], 0, 0, 0);
   }
 
   // ---- gate: tanh(Za) * sigmoid(Zb)  (residual_block.py:123-132)
@@ -356,26 +355,32 @@ __global__ void __launch_bounds__(256, 2) pwg_layer_kernel(const LayerArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       if (MT == 1 && r >= 8) { g[gm][r] = 0.f; continue; }
-      const int row = 32 * gm + (r & 3) + 8 * (r >> 2) + 4 * hh;
-      const float za = acc[gm][r] + a.bg[row];
-      const float zb = (MT == 1 ? acc[0][r + 8] : acc[gm + MT / 2][r]) + a.bg[row + GHPAD];
-      g[gm][r] = tanhf(za) * (1.0f / (1.0f + expf(-zb)));
+      const float za = acc[gm][r];
+      const float zb = MT == 1 ? acc[0][r + 8] : acc[gm + MT / 2][r];
+      g[gm][r] = fast_tanh(za) * fast_sigmoid(zb);
     }
   }
 
-  // ---- GEMM 2: [skip; out] = W2 . g, A fragments from global (L1/L2)
+  // ---- GEMM 2: [skip; out] = W2 . g + b2 (bias = k-step NQ against a ones row)
   f32x16 acc2[M2T];
 #pragma unroll
   for (int m = 0; m < M2T; ++m)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc2[m][r] = 0.f;
-  const float* w2 = a.w2 + lane;
+  const f32x4* w2 = reinterpret_cast<const f32x4*>(a.w2) + lane;
 #pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    const float bq = g[q >> 4][q & 15];
+  for (int q4 = 0; q4 < NQ4; ++q4) {
 #pragma unroll
-    for (int m2 = 0; m2 < M2T; ++m2)
-      acc2[m2] = __builtin_amdgcn_mfma_f32_32x32x2f32(w2[(q * M2T + m2) * 64], bq, acc2[m2], 0, 0, 0);
+    for (int m2 = 0; m2 < M2T; ++m2) {
+      const f32x4 wv = w2[(q4 * M2T + m2) * 64];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int q = 4 * q4 + i;
+        if (q > NQ) continue;
+        const float bq = q < NQ ? g[q >> 4][q & 15] : (hh == 0 ? 1.f : 0.f);
+        acc2[m2] = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[i], bq, acc2[m2], 0, 0, 0);
+      }
+    }
   }
 
   // ---- epilogue: skip += W_s g + b_s ; x = (W_o g + b_o + x) * sqrt(0.5)   (residual_block.py:135-138)
@@ -383,15 +388,18 @@ __global__ void __launch_bounds__(256, 2) pwg_layer_kernel(const LayerArgs a) {
 #pragma unroll
   for (int m2 = 0; m2 < M2T; ++m2) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = 32 * m2 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-      const float v = acc2[m2][r] + a.b2[row];
+    for (int j4 = 0; j4 < 4; ++j4) {
+      const int row = 32 * m2 + 8 * j4 + 4 * hh;  // 4 consecutive channels row..row+3
+      f32x4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = acc2[m2][4 * j4 + i];
       if (row < a.S) {
-        float* p = a.skip + (size_t)row * P + gt;
+        f32x4* p = reinterpret_cast<f32x4*>(a.skip + gt * a.SS + row);
         *p = a.first ? v : (*p + v);
       } else if (row < a.S + a.R) {
-        const size_t off = (size_t)(row - a.S) * P + gt;
-        a.x_out[off] = (v + a.x_in[off]) * 0.70710677f;
+        const size_t off = gt * a.RS + (row - a.S);
+        const f32x4 xin = *reinterpret_cast<const f32x4*>(a.x_in + off);
+        *reinterpret_cast<f32x4*>(a.x_out + off) = (v + xin) * 0.70710677f;
       }
     }
   }
@@ -411,7 +419,7 @@ __global__ void __launch_bounds__(TILE) pwg_head_kernel(const HeadArgs a) {
 #pragma unroll
   for (int i = 0; i < SMAX; ++i) {
     float v = 0.f;
-    if (i < a.S) v = fmaxf(a.skip[(size_t)i * a.Tpad + gt] * a.skip_scale, 0.f);
+    if (i < a.S) v = fmaxf(a.skip[gt * a.SS + i] * a.skip_scale, 0.f);
     hv[i] = v;
   }
   float* out = a.out + ud.io_off * a.O + t * a.out_stride_t;
@@ -450,12 +458,10 @@ hipError_t launch_first_conv(const FirstConvArgs& a, long long n_tiles, hipStrea
 
 hipError_t launch_layer(const LayerArgs& a, int mt, int m2t, long long n_tiles, hipStream_t s) {
   const dim3 grid((unsigned)n_tiles), block(256);
-  const bool aligned = (a.dil % 4) == 0;
-#define PWG_LAYER_CASE(MT_, M2T_)                                                             \
-  if (mt == MT_ && m2t == M2T_) {                                                             \
-    if (aligned) hipLaunchKernelGGL((pwg_layer_kernel<MT_, M2T_, true>), grid, block, 0, s, a);  \
-    else hipLaunchKernelGGL((pwg_layer_kernel<MT_, M2T_, false>), grid, block, 0, s, a);         \
-    return hipGetLastError();                                                                 \
+#define PWG_LAYER_CASE(MT_, M2T_)                                                   \
+  if (mt == MT_ && m2t == M2T_) {                                                   \
+    hipLaunchKernelGGL((pwg_layer_kernel<MT_, M2T_>), grid, block, 0, s, a);        \
+    return hipGetLastError();                                                       \
   }
   PWG_LAYER_CASE(1, 1) PWG_LAYER_CASE(1, 2) PWG_LAYER_CASE(1, 4)
   PWG_LAYER_CASE(2, 1) PWG_LAYER_CASE(2, 2) PWG_LAYER_CASE(2, 4)
