@@ -74,10 +74,10 @@ enum {
 /* Timing buckets reported by pwg_timing_collect. */
 enum {
   PWG_KERNEL_CONV_IN = 0,
-  PWG_KERNEL_UPSAMPLE = 1,
+  PWG_KERNEL_UPSAMPLE = 1,        /* frame-rate aux projection (the upsampler is folded into the layers) */
   PWG_KERNEL_FIRST_CONV = 2,
   PWG_KERNEL_RESIDUAL_LAYER = 3,
-  PWG_KERNEL_HEAD = 4,
+  PWG_KERNEL_HEAD = 4,            /* fused into the last residual layer: always 0 launches */
   PWG_NUM_KERNELS = 5
 };
 

@@ -253,7 +253,8 @@ struct PwgHandle {
   size_t off_first_w, off_first_b, off_conv_in, off_waux;
   size_t off_tab_interior, off_tab_left, off_tab_right, off_tab_small;
   size_t off_layers, layer_stride, lo_wg, lo_bg, lo_w2;
-  size_t off_head_w1, off_head_b1, off_head_w2, off_head_b2, packed_total;
+  size_t off_head_w1, off_head_w2, off_head_b2, packed_total;
+  int M3T;
   long long ref_total;
   // timing
   bool timing = false;
@@ -326,6 +327,7 @@ int pwg_create(const PwgConfig* cfg, int device, PwgHandle** out) {
     return fail(PWG_ERR_UNSUPPORTED, "gate_channels <= 128 and skip+residual <= 128 supported");
   }
   if (h->S > 128) { delete h; return fail(PWG_ERR_UNSUPPORTED, "skip_channels <= 128 supported"); }
+  if (h->A > 128) { delete h; return fail(PWG_ERR_UNSUPPORTED, "aux_channels <= 128 supported"); }
   for (int l = 0; l < h->L; ++l) {
     long long d = 1LL << (l % h->lps);
     if (d > (1LL << 24)) { delete h; return fail(PWG_ERR_UNSUPPORTED, "dilation too large"); }
@@ -340,7 +342,7 @@ int pwg_create(const PwgConfig* cfg, int device, PwgHandle** out) {
   h->off_first_w = o; o += align64(h->R);
   h->off_first_b = o; o += align64(h->R);
   h->off_conv_in = o; o += align64((size_t)h->A * h->A * h->KW);
-  h->off_waux = o; o += align64((size_t)h->L * h->GR * h->A);
+  h->off_waux = o; o += align64((size_t)h->L * ((h->A + 1) / 2) * h->MT * 64);
   h->off_tab_interior = o; o += align64((size_t)h->aux.H * AUX_J4);
   h->off_tab_left = o; o += align64((size_t)std::max(h->aux.TL, 1) * AUX_J4);
   h->off_tab_right = o; o += align64((size_t)std::max(h->aux.TR, 1) * AUX_J4);
@@ -351,9 +353,9 @@ int pwg_create(const PwgConfig* cfg, int device, PwgHandle** out) {
   h->lo_w2 = h->lo_bg + align64(2 * h->GHPAD);
   h->layer_stride = h->lo_w2 + align64((size_t)h->NQ4 * h->M2T * 64 * 4);
   h->off_layers = o; o += h->layer_stride * h->L;
-  h->off_head_w1 = o; o += align64((size_t)h->S * h->S);
-  h->off_head_b1 = o; o += align64(h->S);
-  h->off_head_w2 = o; o += align64((size_t)h->O * h->S);
+  h->M3T = (h->S + 31) / 32;
+  h->off_head_w1 = o; o += align64((size_t)(16 * h->M3T + 1 + 3) / 4 * h->M3T * 64 * 4);
+  h->off_head_w2 = o; o += align64((size_t)h->O * h->M3T * 32);
   h->off_head_b2 = o; o += align64(h->O);
   h->packed_total = o;
 
@@ -447,12 +449,20 @@ int pwg_pack_weights(const PwgHandle* h, const float* ref, float* pk) {
         for (int lane = 0; lane < 64; ++lane)
           wg[((size_t)s * MT + m) * 64 + lane] = wcat(gate_row(32 * m + (lane & 31)), 2 * s + (lane >> 5));
     float* bg = L0 + h->lo_bg;
-    float* waux = pk + h->off_waux + (size_t)l * h->GR * A;
     for (int prow = 0; prow < 2 * GHPAD; ++prow) {
       const int gr = gate_row(prow);
       bg[prow] = gr < 0 ? 0.f : bd[gr];
-      for (int i = 0; i < A; ++i) waux[(size_t)prow * A + i] = gr < 0 ? 0.f : wa[(size_t)gr * A + i];
     }
+    // aux projection A-fragments: (k-step s, m-tile m, lane) -> Waux[gate_row(32m + lane%32)][2s + lane/32]
+    const int nks = (A + 1) / 2;
+    float* waux = pk + h->off_waux + (size_t)l * nks * MT * 64;
+    for (int s = 0; s < nks; ++s)
+      for (int m = 0; m < MT; ++m)
+        for (int lane = 0; lane < 64; ++lane) {
+          const int gr = gate_row(32 * m + (lane & 31));
+          const int i = 2 * s + (lane >> 5);
+          waux[((size_t)s * MT + m) * 64 + lane] = (gr < 0 || i >= A) ? 0.f : wa[(size_t)gr * A + i];
+        }
     // GEMM 2 A fragments, 4 k-steps per 16-byte lane load: [q/4][m2][lane][q%4]; k-step NQ is
     // the bias (A[i][0] = b2[row i], B = ones row).
     float* w2 = L0 + h->lo_w2;
@@ -474,10 +484,41 @@ int pwg_pack_weights(const PwgHandle* h, const float* ref, float* pk) {
           w2[(((size_t)(q / 4) * M2T + m2) * 64 + lane) * 4 + (q % 4)] = v;
         }
   }
-  for (size_t i = 0; i < (size_t)S * S; ++i) pk[h->off_head_w1 + i] = *p++;
-  for (int i = 0; i < S; ++i) pk[h->off_head_b1 + i] = *p++;
-  for (size_t i = 0; i < (size_t)O * S; ++i) pk[h->off_head_w2 + i] = *p++;
-  for (int i = 0; i < O; ++i) pk[h->off_head_b2 + i] = *p++;
+  // output head (fused into the last layer): W1h A-fragments over skip channels in the same
+  // permuted-k order as GEMM 2, bias as k-step NQH; W2h per lane half in accumulator row order.
+  {
+    const float* w1 = p; p += (size_t)S * S;
+    const float* b1 = p; p += S;
+    const float* w2h = p; p += (size_t)O * S;
+    const float* b2h = p; p += O;
+    const int M3T = h->M3T, NQH = 16 * M3T, NQH4 = (NQH + 1 + 3) / 4;
+    float* hw1 = pk + h->off_head_w1;
+    for (int q = 0; q < 4 * NQH4; ++q)
+      for (int m3 = 0; m3 < M3T; ++m3)
+        for (int lane = 0; lane < 64; ++lane) {
+          const int row = 32 * m3 + (lane & 31);
+          float v = 0.f;
+          if (row < S) {
+            if (q < NQH) {
+              const int r = q & 15, gm = q >> 4;
+              const int ch = 32 * gm + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+              if (ch < S) v = w1[(size_t)row * S + ch];
+            } else if (q == NQH && lane < 32) {
+              v = b1[row];
+            }
+          }
+          hw1[(((size_t)(q / 4) * M3T + m3) * 64 + lane) * 4 + (q % 4)] = v;
+        }
+    float* hw2 = pk + h->off_head_w2;
+    for (int oc = 0; oc < O; ++oc)
+      for (int m3 = 0; m3 < M3T; ++m3)
+        for (int half = 0; half < 2; ++half)
+          for (int r = 0; r < 16; ++r) {
+            const int row = 32 * m3 + (r & 3) + 8 * (r >> 2) + 4 * half;
+            hw2[(((size_t)oc * M3T + m3) * 2 + half) * 16 + r] = row < S ? w2h[(size_t)oc * S + row] : 0.f;
+          }
+    for (int i = 0; i < O; ++i) pk[h->off_head_b2 + i] = b2h[i];
+  }
   if ((long long)(p - ref) != h->ref_total) return fail(PWG_ERR_INVALID, "internal: weight count mismatch");
   return PWG_OK;
 }
@@ -640,20 +681,16 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
     la.R = h->R; la.RP = h->RP; la.RS = h->RS; la.S = h->S; la.SS = h->SS; la.KS = h->KS; la.dil = h->dil[l];
     la.tap_center = h->cfg.use_causal_conv ? h->KS - 1 : (h->KS - 1) / 2;
     la.first = l == 0;
-    e = timed(PWG_KERNEL_RESIDUAL_LAYER, [&] { return launch_layer(la, h->MT, h->M2T, p->n_tiles, s); });
+    const bool last = l == h->L - 1;
+    la.hw1 = packed + h->off_head_w1; la.hw2 = packed + h->off_head_w2; la.hb2 = packed + h->off_head_b2;
+    la.out = out; la.O = h->O; la.skip_scale = (float)std::sqrt(1.0 / h->L);
+    if (p->layout == PWG_LAYOUT_INFERENCE) { la.out_stride_t = h->O; la.out_stride_o = 1; }
+    else { la.out_stride_t = 1; la.out_stride_o = p->utts[0].T; }
+    e = timed(PWG_KERNEL_RESIDUAL_LAYER,
+              [&] { return launch_layer(la, h->MT, h->M2T, last, p->n_tiles, s); });
     if (e != hipSuccess) return hip_fail(e, "residual layer launch");
     std::swap(xin, xout);
   }
-
-  HeadArgs ha;
-  ha.skip = skip; ha.w1 = packed + h->off_head_w1; ha.b1 = packed + h->off_head_b1;
-  ha.w2 = packed + h->off_head_w2; ha.b2 = packed + h->off_head_b2; ha.out = out;
-  ha.tile_utt = p->d_tile_utt; ha.utts = p->d_utts; ha.Tpad = p->Tpad; ha.S = h->S; ha.SS = h->SS; ha.O = h->O;
-  ha.skip_scale = (float)std::sqrt(1.0 / h->L);
-  if (p->layout == PWG_LAYOUT_INFERENCE) { ha.out_stride_t = h->O; ha.out_stride_o = 1; }
-  else { ha.out_stride_t = 1; ha.out_stride_o = p->utts[0].T; }
-  e = timed(PWG_KERNEL_HEAD, [&] { return launch_head(ha, p->n_tiles, s); });
-  if (e != hipSuccess) return hip_fail(e, "head launch");
   return PWG_OK;
 }
 

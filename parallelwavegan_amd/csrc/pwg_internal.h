@@ -61,7 +61,7 @@ struct AuxTab {
 // rate (it commutes with the per-channel linear upsampler), rows in packed gate-row order.
 struct AuxProjArgs {
   const float* c1;       // [A][F_total]
-  const float* waux;     // [L][GR][A]
+  const float* waux;     // A-fragments [L][ceil(A/2)][MT][64] (packed gate rows x aux channels)
   float* d;              // [L][F_total][GR]
   long long F_total;
   int A, GR;
@@ -99,30 +99,21 @@ struct LayerArgs {
   int nfwg;              // frames staged per workgroup
   int tap_center;        // (KS-1)/2 non-causal, KS-1 causal
   int first;             // layer 0: skip buffer is written, not accumulated
-};
-
-struct HeadArgs {
-  const float* skip;     // [Tpad][SS] time-major
-  const float* w1;       // [S][S]
-  const float* b1;       // [S]
-  const float* w2;       // [O][S]
-  const float* b2;       // [O]
+  // last layer only: the output head (models/parallel_wavegan.py:131-138,166-171) is fused into
+  // the epilogue: y = W2h . relu(W1h . relu(skip * sqrt(1/L)) + b1h) + b2h
+  const float* hw1;      // W1h A-fragments incl. bias k-step, [NQH4][M3T][64][4]
+  const float* hw2;      // W2h per lane half, [O][M3T][2][16]
+  const float* hb2;      // [O]
   float* out;
-  const int* tile_utt;
-  const UttDesc* utts;
-  long long Tpad;
-  int S, SS, O;
-  float skip_scale;      // sqrt(1/L), models/parallel_wavegan.py:166
-  // element strides of the caller's output; utterance u starts at io_off*O in both layouts
-  // (inference: (T_u, O) time-major -> t*O + o; forward: (B, O, T) -> o*T + t)
-  long long out_stride_t, out_stride_o;
+  long long out_stride_t, out_stride_o;  // caller output strides (base io_off * O)
+  int O;
+  float skip_scale;
 };
 
 // Kernel launchers (pwg_kernels.hip).
 hipError_t launch_conv_in(const ConvInArgs& a, hipStream_t s);
 hipError_t launch_aux_proj(const AuxProjArgs& a, int layers, hipStream_t s);
 hipError_t launch_first_conv(const FirstConvArgs& a, long long n_tiles, hipStream_t s);
-hipError_t launch_layer(const LayerArgs& a, int mt, int m2t, long long n_tiles, hipStream_t s);
-hipError_t launch_head(const HeadArgs& a, long long n_tiles, hipStream_t s);
+hipError_t launch_layer(const LayerArgs& a, int mt, int m2t, bool last, long long n_tiles, hipStream_t s);
 
 }  // namespace pwg

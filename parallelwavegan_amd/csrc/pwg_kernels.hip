@@ -21,8 +21,9 @@
 //                           B operand is the gate tile straight out of the accumulators,
 //                           residual*sqrt(.5) and skip += in the epilogue.
 //                           layers/residual_block.py:102-140, models/parallel_wavegan.py:163-165
-//   pwg_head_kernel         skips*sqrt(1/L) -> ReLU -> 1x1 -> ReLU -> 1x1,
-//                           models/parallel_wavegan.py:131-138,166-171
+//                           The LAST layer's epilogue also runs the output head, skips*sqrt(1/L) ->
+//                           ReLU -> 1x1 -> ReLU -> 1x1 (models/parallel_wavegan.py:131-138,166-171),
+//                           as a third MFMA GEMM on the skip tile held in registers.
 #include "pwg_internal.h"
 #include "../../include/pwg.h"
 
@@ -48,18 +49,24 @@ __device__ __forceinline__ int find_utt_by_frame(const UttDesc* utts, int n, lon
 }
 
 // ---------------------------------------------------------------------------------------------
-// conv_in at frame rate. grid (ceil(F_total/256), A), one output (channel o, frame g) per thread.
-// 2w+1 taps x A inputs = 400 MAC per output at A=80, w=2: 125 MAC per audio sample, <0.1 % of
-// the forward; the input gather is served by L1/L2.
+// conv_in at frame rate. grid ceil(F_total/64), 256 threads = 4 waves; lane = frame, wave w =
+// output channels [w*OG, (w+1)*OG) (OG = ceil(A/4) <= 32): each thread reads its (2w+1)-frame
+// input window once and accumulates OG outputs; the weights are wave-uniform (scalar loads).
+// 2w+1 taps x A inputs = 400 MAC per output at A=80, w=2: 125 MAC per audio sample.
+template <int OGMAX>
 __global__ void __launch_bounds__(256) pwg_conv_in_kernel(const ConvInArgs a) {
-  const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (g >= a.F_total) return;
-  const int o = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int grp = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const long long g0 = (long long)blockIdx.x * 64 + lane;
+  const bool valid = g0 < a.F_total;
+  const long long g = valid ? g0 : a.F_total - 1;
   const int u = find_utt_by_frame(a.utts, a.n_utts, g);
   const UttDesc ud = a.utts[u];
   const long long f = g - ud.frame_base;
   const long long Tf = ud.frames;
   const long long Tin = Tf + 2 * a.ctx;  // padded input length (forward layout)
+  const int OG = (a.A + 3) / 4;
+  const int o0 = grp * OG;
 
   auto cin = [&](int i, long long fp) -> float {
     float v;
@@ -74,55 +81,71 @@ __global__ void __launch_bounds__(256) pwg_conv_in_kernel(const ConvInArgs a) {
     return v;
   };
 
-  float acc = 0.f;
+  float acc[OGMAX];
+#pragma unroll
+  for (int j = 0; j < OGMAX; ++j) acc[j] = 0.f;
   if (a.use_conv_in) {
-    const float* w = a.w + (size_t)o * a.A * a.KW;
-    for (int i = 0; i < a.A; ++i)
-      for (int k = 0; k < a.KW; ++k) acc = fmaf(w[i * a.KW + k], cin(i, f + k), acc);
+    for (int i = 0; i < a.A; ++i) {
+      for (int k = 0; k < a.KW; ++k) {
+        const float x = cin(i, f + k);
+        const float* w = a.w + ((size_t)o0 * a.A + i) * a.KW + k;  // W[o][i][k], o = o0 + j
+#pragma unroll
+        for (int j = 0; j < OGMAX; ++j)
+          if (j < OG && o0 + j < a.A) acc[j] = fmaf(w[(size_t)j * a.A * a.KW], x, acc[j]);
+      }
+    }
   } else {
-    acc = cin(o, f);
+#pragma unroll
+    for (int j = 0; j < OGMAX; ++j)
+      if (j < OG && o0 + j < a.A) acc[j] = cin(o0 + j, f);
   }
-  a.c1[(size_t)o * a.F_total + g] = acc;
+  if (!valid) return;
+#pragma unroll
+  for (int j = 0; j < OGMAX; ++j)
+    if (j < OG && o0 + j < a.A) a.c1[(size_t)(o0 + j) * a.F_total + g] = acc[j];
 }
 
 // ---------------------------------------------------------------------------------------------
-// D[l][f][row] = sum_i Waux_l[row][i] C1[i][f]. grid (ceil(F_total/64), L), block GR threads: one
-// gate row per thread, 64 frames per block; C1 tile and the layer's W rows staged in LDS.
-// Output rows are contiguous per frame (coalesced stores), the layout the layer kernel stages.
-__global__ void __launch_bounds__(128) pwg_aux_proj_kernel(const AuxProjArgs a) {
-  extern __shared__ float sm[];
-  const int A = a.A, GR = a.GR;
-  float* cs = sm;                 // [A][64]
-  float* ws = sm + A * 64;        // [GR][A+1]
+// D[l][f][row] = sum_i Waux_l[row][i] C1[i][f] as an fp32 MFMA GEMM per layer: M = GR gate rows
+// (A fragments host-packed like the layer weights), N = 32 frames per wave (B fragment = C1 row
+// segment, 2 x 128-B reads), K = A. The accumulator's register quads are 4 consecutive rows of one
+// frame -> 16-byte stores into the frame-major D the layer kernel stages.
+// grid (ceil(F_total/128), L), 256 threads: wave w owns frames [128*bx + 32w, +32).
+template <int MT>
+__global__ void __launch_bounds__(256) pwg_aux_proj_kernel(const AuxProjArgs a) {
+  constexpr int GR = 32 * MT;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int hh = lane >> 5, cl = lane & 31;
   const int l = blockIdx.y;
-  const long long f0 = (long long)blockIdx.x * 64;
-  const int row = threadIdx.x;
-  for (int idx = threadIdx.x; idx < A * 64; idx += GR) {
-    const int i = idx / 64, j = idx % 64;
-    const long long f = f0 + j;
-    cs[idx] = f < a.F_total ? a.c1[(size_t)i * a.F_total + f] : 0.f;
-  }
-  const float* w = a.waux + (size_t)l * GR * A;
-  for (int idx = threadIdx.x; idx < GR * A; idx += GR) ws[(idx / A) * (A + 1) + idx % A] = w[idx];
-  __syncthreads();
-  float* d = a.d + (size_t)l * a.F_total * GR;
-  for (int j = 0; j < 64; j += 4) {
-    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
-    for (int i = 0; i < A; ++i) {
-      const float wv = ws[row * (A + 1) + i];
-      const f32x4 c = *reinterpret_cast<const f32x4*>(&cs[i * 64 + j]);
-      acc0 = fmaf(wv, c.x, acc0);
-      acc1 = fmaf(wv, c.y, acc1);
-      acc2 = fmaf(wv, c.z, acc2);
-      acc3 = fmaf(wv, c.w, acc3);
-    }
-    const float accs[4] = {acc0, acc1, acc2, acc3};
+  const long long f = (long long)blockIdx.x * 128 + wave * 32 + cl;
+  const long long fc = f < a.F_total ? f : a.F_total - 1;
+  const int nks = (a.A + 1) / 2;
+  const float* w = a.waux + (size_t)l * nks * MT * 64 + lane;
+  f32x16 acc[MT];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const long long f = f0 + j + q;
-      if (f < a.F_total) d[(size_t)f * GR + row] = accs[q];
-    }
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
+  for (int s = 0; s < nks; ++s) {
+    const int i = 2 * s + hh;
+    const float bv = a.c1[(size_t)(i < a.A ? i : 0) * a.F_total + fc];
+    const float b = i < a.A ? bv : 0.f;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+      acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(w[(s * MT + m) * 64], b, acc[m], 0, 0, 0);
   }
+  if (f >= a.F_total) return;
+  float* d = a.d + ((size_t)l * a.F_total + f) * GR;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int j4 = 0; j4 < 4; ++j4) {
+      f32x4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = acc[m][4 * j4 + i];
+      *reinterpret_cast<f32x4*>(d + 32 * m + 8 * j4 + 4 * hh) = v;
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -238,8 +261,10 @@ __device__ __forceinline__ void layer_store_chunk(float* buf, int tid, const Chu
 __device__ __forceinline__ float fast_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 __device__ __forceinline__ float fast_tanh(float x) { return 2.f * __builtin_amdgcn_rcpf(1.f + __expf(-2.f * x)) - 1.f; }
 
-template <int MT, int M2T>
+// M3T = 0: a middle layer. M3T = ceil(S/32) > 0: the last layer, with the output head fused.
+template <int MT, int M2T, int M3T>
 __global__ void __launch_bounds__(256, 2) pwg_layer_kernel(const LayerArgs a) {
+  constexpr bool LAST = M3T > 0;
   using SM = LayerSmem<MT>;
   constexpr int GHPAD = (MT == 1) ? 16 : 16 * MT;
   constexpr int GR = SM::GR;
@@ -385,69 +410,110 @@ __global__ void __launch_bounds__(256, 2) pwg_layer_kernel(const LayerArgs a) {
 
   // ---- epilogue: skip += W_s g + b_s ; x = (W_o g + b_o + x) * sqrt(0.5)   (residual_block.py:135-138)
   const size_t gt = (size_t)(col0 + wave * 32 + cl);
+  if (!LAST) {
+#pragma unroll
+    for (int m2 = 0; m2 < M2T; ++m2) {
+#pragma unroll
+      for (int j4 = 0; j4 < 4; ++j4) {
+        const int row = 32 * m2 + 8 * j4 + 4 * hh;  // 4 consecutive channels row..row+3
+        f32x4 v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = acc2[m2][4 * j4 + i];
+        if (row < a.S) {
+          f32x4* p = reinterpret_cast<f32x4*>(a.skip + gt * a.SS + row);
+          *p = a.first ? v : (*p + v);
+        } else if (row < a.S + a.R) {
+          const size_t off = gt * a.RS + (row - a.S);
+          const f32x4 xin = *reinterpret_cast<const f32x4*>(a.x_in + off);
+          *reinterpret_cast<f32x4*>(a.x_out + off) = (v + xin) * 0.70710677f;
+        }
+      }
+    }
+    return;
+  }
+
+  // ---- last layer: output head on the final skip sum, no x / skip stores
+  //   hs = relu(skip * sqrt(1/L)) stays in the accumulator layout and is the B operand of
+  //   h1 = W1h . hs + b1h (M3T = ceil(S/32) tiles); y = W2h . relu(h1) + b2h is a per-lane dot
+  //   over the lane's 32 rows plus the partner half (lane ^ 32) of the same sample.
+  float hs[M2T][16];
 #pragma unroll
   for (int m2 = 0; m2 < M2T; ++m2) {
 #pragma unroll
     for (int j4 = 0; j4 < 4; ++j4) {
-      const int row = 32 * m2 + 8 * j4 + 4 * hh;  // 4 consecutive channels row..row+3
+      const int row = 32 * m2 + 8 * j4 + 4 * hh;
       f32x4 v;
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] = acc2[m2][4 * j4 + i];
       if (row < a.S) {
-        f32x4* p = reinterpret_cast<f32x4*>(a.skip + gt * a.SS + row);
-        *p = a.first ? v : (*p + v);
-      } else if (row < a.S + a.R) {
-        const size_t off = gt * a.RS + (row - a.S);
-        const f32x4 xin = *reinterpret_cast<const f32x4*>(a.x_in + off);
-        *reinterpret_cast<f32x4*>(a.x_out + off) = (v + xin) * 0.70710677f;
+        if (!a.first) v += *reinterpret_cast<const f32x4*>(a.skip + gt * a.SS + row);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) hs[m2][4 * j4 + i] = fmaxf(v[i] * a.skip_scale, 0.f);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) hs[m2][4 * j4 + i] = 0.f;
       }
     }
   }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Output head, one sample per thread.
-template <int SMAX>
-__global__ void __launch_bounds__(TILE) pwg_head_kernel(const HeadArgs a) {
-  const long long tile = blockIdx.x;
-  const UttDesc ud = a.utts[a.tile_utt[tile]];
-  const long long col0 = tile * TILE;
-  const long long t = col0 - ud.seg_base + threadIdx.x;
-  if (t >= ud.T) return;
-  const size_t gt = (size_t)(col0 + threadIdx.x);
-  float hv[SMAX];
+  constexpr int NQH = 16 * (LAST ? M3T : 1);  // k-steps over skip rows [0, 32*M3T)
+  constexpr int NQH4 = (NQH + 1 + 3) / 4;
+  constexpr int M3 = LAST ? M3T : 1;
+  f32x16 acc3[M3];
 #pragma unroll
-  for (int i = 0; i < SMAX; ++i) {
-    float v = 0.f;
-    if (i < a.S) v = fmaxf(a.skip[gt * a.SS + i] * a.skip_scale, 0.f);
-    hv[i] = v;
+  for (int m = 0; m < M3; ++m)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc3[m][r] = 0.f;
+  const f32x4* hw1 = reinterpret_cast<const f32x4*>(a.hw1) + lane;
+#pragma unroll
+  for (int q4 = 0; q4 < NQH4; ++q4) {
+#pragma unroll
+    for (int m3 = 0; m3 < M3; ++m3) {
+      const f32x4 wv = hw1[(q4 * M3 + m3) * 64];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int q = 4 * q4 + i;
+        if (q > NQH) continue;
+        const float bq = q < NQH ? hs[q >> 4][q & 15] : (hh == 0 ? 1.f : 0.f);
+        acc3[m3] = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[i], bq, acc3[m3], 0, 0, 0);
+      }
+    }
   }
+  const long long t = t0 + wave * 32 + cl;
   float* out = a.out + ud.io_off * a.O + t * a.out_stride_t;
   for (int oc = 0; oc < a.O; ++oc) {
-    float y = a.b2[oc];
-    for (int o = 0; o < a.S; ++o) {
-      float z = a.b1[o];
-      const float* w1 = a.w1 + (size_t)o * a.S;
+    float part = 0.f;
 #pragma unroll
-      for (int i = 0; i < SMAX; ++i)
-        if (i < a.S) z = fmaf(w1[i], hv[i], z);
-      y = fmaf(a.w2[(size_t)oc * a.S + o], fmaxf(z, 0.f), y);
+    for (int m3 = 0; m3 < M3; ++m3) {
+      const f32x4* w = reinterpret_cast<const f32x4*>(a.hw2 + ((size_t)(oc * M3 + m3) * 2 + hh) * 16);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 wq = w[q];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) part = fmaf(wq[i], fmaxf(acc3[m3][4 * q + i], 0.f), part);
+      }
     }
-    out[oc * a.out_stride_o] = y;
+    const float y = part + __shfl_xor(part, 32) + a.hb2[oc];
+    if (hh == 0 && t < Tu) out[oc * a.out_stride_o] = y;
   }
 }
 
 // ---------------------------------------------------------------------------------------------
 hipError_t launch_conv_in(const ConvInArgs& a, hipStream_t s) {
-  dim3 grid((unsigned)((a.F_total + 255) / 256), (unsigned)a.A);
-  hipLaunchKernelGGL(pwg_conv_in_kernel, grid, dim3(256), 0, s, a);
+  const dim3 grid((unsigned)((a.F_total + 63) / 64));
+  const int og = (a.A + 3) / 4;
+  if (og <= 8) hipLaunchKernelGGL(pwg_conv_in_kernel<8>, grid, dim3(256), 0, s, a);
+  else if (og <= 20) hipLaunchKernelGGL(pwg_conv_in_kernel<20>, grid, dim3(256), 0, s, a);
+  else if (og <= 32) hipLaunchKernelGGL(pwg_conv_in_kernel<32>, grid, dim3(256), 0, s, a);
+  else return hipErrorInvalidValue;
   return hipGetLastError();
 }
 
 hipError_t launch_aux_proj(const AuxProjArgs& a, int layers, hipStream_t s) {
-  const dim3 grid((unsigned)((a.F_total + 63) / 64), (unsigned)layers), block(a.GR);
-  const size_t lds = sizeof(float) * ((size_t)a.A * 64 + (size_t)a.GR * (a.A + 1));
-  hipLaunchKernelGGL(pwg_aux_proj_kernel, grid, block, lds, s, a);
+  const dim3 grid((unsigned)((a.F_total + 127) / 128), (unsigned)layers), block(256);
+  if (a.GR == 32) hipLaunchKernelGGL(pwg_aux_proj_kernel<1>, grid, block, 0, s, a);
+  else if (a.GR == 64) hipLaunchKernelGGL(pwg_aux_proj_kernel<2>, grid, block, 0, s, a);
+  else if (a.GR == 128) hipLaunchKernelGGL(pwg_aux_proj_kernel<4>, grid, block, 0, s, a);
+  else return hipErrorInvalidValue;
   return hipGetLastError();
 }
 
@@ -456,28 +522,23 @@ hipError_t launch_first_conv(const FirstConvArgs& a, long long n_tiles, hipStrea
   return hipGetLastError();
 }
 
-hipError_t launch_layer(const LayerArgs& a, int mt, int m2t, long long n_tiles, hipStream_t s) {
+hipError_t launch_layer(const LayerArgs& a, int mt, int m2t, bool last, long long n_tiles, hipStream_t s) {
   const dim3 grid((unsigned)n_tiles), block(256);
-#define PWG_LAYER_CASE(MT_, M2T_)                                                   \
-  if (mt == MT_ && m2t == M2T_) {                                                   \
-    hipLaunchKernelGGL((pwg_layer_kernel<MT_, M2T_>), grid, block, 0, s, a);        \
-    return hipGetLastError();                                                       \
+  const int m3t = (a.S + 31) / 32;
+#define PWG_LAYER_CASE(MT_, M2T_)                                                                  \
+  if (mt == MT_ && m2t == M2T_) {                                                                  \
+    if (!last) hipLaunchKernelGGL((pwg_layer_kernel<MT_, M2T_, 0>), grid, block, 0, s, a);          \
+    else if (m3t == 1) hipLaunchKernelGGL((pwg_layer_kernel<MT_, M2T_, 1>), grid, block, 0, s, a);  \
+    else if (m3t == 2 && M2T_ >= 2) hipLaunchKernelGGL((pwg_layer_kernel<MT_, M2T_, (M2T_ >= 2 ? 2 : 1)>), grid, block, 0, s, a); \
+    else if (M2T_ >= 4) hipLaunchKernelGGL((pwg_layer_kernel<MT_, M2T_, (M2T_ >= 4 ? 4 : 1)>), grid, block, 0, s, a); \
+    else return hipErrorInvalidValue;                                                              \
+    return hipGetLastError();                                                                      \
   }
   PWG_LAYER_CASE(1, 1) PWG_LAYER_CASE(1, 2) PWG_LAYER_CASE(1, 4)
   PWG_LAYER_CASE(2, 1) PWG_LAYER_CASE(2, 2) PWG_LAYER_CASE(2, 4)
   PWG_LAYER_CASE(4, 1) PWG_LAYER_CASE(4, 2) PWG_LAYER_CASE(4, 4)
 #undef PWG_LAYER_CASE
   return hipErrorInvalidValue;
-}
-
-hipError_t launch_head(const HeadArgs& a, long long n_tiles, hipStream_t s) {
-  const dim3 grid((unsigned)n_tiles), block(TILE);
-  if (a.S <= 16) hipLaunchKernelGGL(pwg_head_kernel<16>, grid, block, 0, s, a);
-  else if (a.S <= 32) hipLaunchKernelGGL(pwg_head_kernel<32>, grid, block, 0, s, a);
-  else if (a.S <= 64) hipLaunchKernelGGL(pwg_head_kernel<64>, grid, block, 0, s, a);
-  else if (a.S <= 128) hipLaunchKernelGGL(pwg_head_kernel<128>, grid, block, 0, s, a);
-  else return hipErrorInvalidValue;
-  return hipGetLastError();
 }
 
 }  // namespace pwg

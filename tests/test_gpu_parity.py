@@ -196,7 +196,8 @@ def test_engine_timing_buckets(built_lib, cuda_device):
     eng.infer([mel], [noise])
     t = eng.collect_timing()
     assert t["residual_layer"][1] == 20
-    assert all(t[k][1] == 1 for k in ("conv_in", "upsample", "first_conv", "head"))
+    assert all(t[k][1] == 1 for k in ("conv_in", "upsample", "first_conv"))
+    assert t["head"][1] == 0  # fused into the last residual layer
     assert all(ms >= 0 for ms, _ in t.values())
 
 
