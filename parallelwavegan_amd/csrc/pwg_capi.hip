@@ -246,7 +246,8 @@ struct PwgHandle {
   PwgConfig cfg;
   int device;
   // derived shapes
-  int R, RP, RS, G, GH, GHPAD, GR, MT, S, SS, M2T, A, KS, KW, O, L, lps, K1, NQ, NQ4;
+  int R, RS, G, GH, GHPAD, GR, MT, S, SS, M2T, A, KS, KW, O, L, lps, K1, NQ, NQ4;
+  long long gap;  // zero columns between utterance segments (>= the largest tap offset)
   std::vector<int> dil;
   AuxStruct aux;
   // packed image offsets (floats)
@@ -267,9 +268,10 @@ struct PwgPlan {
   int layout;
   int n_utts;
   std::vector<UttDesc> utts;
-  long long n_tiles, Tpad, F_total, T_total;
+  long long n_tiles, n_gap_tiles, Tpad, F_total, T_total;
   UttDesc* d_utts = nullptr;
   int* d_tile_utt = nullptr;
+  long long* d_gap_col0 = nullptr;
   // workspace offsets (bytes)
   size_t ws_x0, ws_x1, ws_skip, ws_c1, ws_d, ws_total;
 };
@@ -317,21 +319,27 @@ int pwg_create(const PwgConfig* cfg, int device, PwgHandle** out) {
   h->NQ = h->GHPAD / 2;
   h->GR = 32 * h->MT;
   h->M2T = (h->S + h->R + 31) / 32;
-  h->RP = (h->R + KC - 1) / KC * KC;
-  h->RS = (h->R + 3) / 4 * 4;
+  h->RS = (h->R + KC - 1) / KC * KC;
   h->SS = (h->S + 3) / 4 * 4;
   h->NQ4 = (h->NQ + 1 + 3) / 4;
-  h->K1 = h->KS * h->RP;
+  h->K1 = h->KS * h->RS;
   if (!(h->MT == 1 || h->MT == 2 || h->MT == 4) || !(h->M2T == 1 || h->M2T == 2 || h->M2T == 4)) {
     delete h;
     return fail(PWG_ERR_UNSUPPORTED, "gate_channels <= 128 and skip+residual <= 128 supported");
   }
   if (h->S > 128) { delete h; return fail(PWG_ERR_UNSUPPORTED, "skip_channels <= 128 supported"); }
   if (h->A > 128) { delete h; return fail(PWG_ERR_UNSUPPORTED, "aux_channels <= 128 supported"); }
+  long long dmax = 1;
   for (int l = 0; l < h->L; ++l) {
     long long d = 1LL << (l % h->lps);
-    if (d > (1LL << 24)) { delete h; return fail(PWG_ERR_UNSUPPORTED, "dilation too large"); }
+    if (d > (1LL << 20)) { delete h; return fail(PWG_ERR_UNSUPPORTED, "dilation too large"); }
     h->dil.push_back((int)d);
+    dmax = std::max(dmax, d);
+  }
+  {
+    const long long center = c.use_causal_conv ? h->KS - 1 : (h->KS - 1) / 2;
+    const long long halo = std::max(center, (long long)h->KS - 1 - center) * dmax;
+    h->gap = (halo + TILE - 1) / TILE * TILE;
   }
   {
     const int rc = aux_structure(c, &h->aux);
@@ -437,10 +445,10 @@ int pwg_pack_weights(const PwgHandle* h, const float* ref, float* pk) {
       const int q = prow - GHPAD;
       return q < GH ? GH + q : -1;
     };
-    const int RP = h->RP;
+    const int RS = h->RS;
     auto wcat = [&](int grow, int k) -> float {
       if (grow < 0) return 0.f;
-      const int tap = k / RP, ch = k % RP;
+      const int tap = k / RS, ch = k % RS;
       return ch < R ? wd[((size_t)grow * R + ch) * KS + tap] : 0.f;
     };
     float* wg = L0 + h->lo_wg;
@@ -536,7 +544,10 @@ int pwg_plan_create(PwgHandle* h, int n_utts, const long long* frames, int layou
   p->h = h;
   p->layout = layout;
   p->n_utts = n_utts;
-  long long seg = 0, fb = 0, io = 0, mel = 0;
+  // time axis: [gap][utt 0 padded to TILE][gap][utt 1]...[gap]
+  long long seg = h->gap, fb = 0, io = 0, mel = 0, tiles = 0;
+  std::vector<long long> gap_col0;
+  for (long long c0 = 0; c0 < h->gap; c0 += TILE) gap_col0.push_back(c0);
   for (int u = 0; u < n_utts; ++u) {
     const long long f = frames[u];
     if (f < 1) { delete p; return fail(PWG_ERR_INVALID, "every utterance needs >= 1 mel frame"); }
@@ -546,13 +557,18 @@ int pwg_plan_create(PwgHandle* h, int n_utts, const long long* frames, int layou
     }
     UttDesc d;
     d.seg_base = seg;
+    d.first_tile = tiles;
     d.T = f * H;
     d.frame_base = fb;
     d.frames = f;
     d.mel_off = mel;
     d.io_off = io;
     p->utts.push_back(d);
-    seg += (d.T + SEG - 1) / SEG * SEG;
+    const long long padded = (d.T + TILE - 1) / TILE * TILE;
+    tiles += padded / TILE;
+    seg += padded;
+    for (long long c0 = 0; c0 < h->gap; c0 += TILE) gap_col0.push_back(seg + c0);
+    seg += h->gap;
     fb += f;
     io += d.T;
     mel += layout == PWG_LAYOUT_INFERENCE ? f * h->A : (f + 2 * w) * h->A;
@@ -560,12 +576,12 @@ int pwg_plan_create(PwgHandle* h, int n_utts, const long long* frames, int layou
   p->Tpad = seg;
   p->F_total = fb;
   p->T_total = io;
-  p->n_tiles = seg / TILE;
+  p->n_tiles = tiles;
+  p->n_gap_tiles = (long long)gap_col0.size();
   std::vector<int> tile_utt(p->n_tiles);
   for (int u = 0; u < n_utts; ++u) {
-    const long long b = p->utts[u].seg_base / TILE;
-    const long long e = (p->utts[u].seg_base + (p->utts[u].T + SEG - 1) / SEG * SEG) / TILE;
-    for (long long t = b; t < e; ++t) tile_utt[t] = u;
+    const long long n = (p->utts[u].T + TILE - 1) / TILE;
+    for (long long t = 0; t < n; ++t) tile_utt[p->utts[u].first_tile + t] = u;
   }
   size_t o = 0;
   p->ws_x0 = o; o += align_bytes(sizeof(float) * h->RS * p->Tpad);
@@ -579,6 +595,9 @@ int pwg_plan_create(PwgHandle* h, int n_utts, const long long* frames, int layou
   if (!g.ok) { delete p; return fail(PWG_ERR_HIP, "hipSetDevice failed"); }
   hipError_t e = hipMalloc(&p->d_utts, sizeof(UttDesc) * n_utts);
   if (e == hipSuccess) e = hipMalloc(&p->d_tile_utt, sizeof(int) * p->n_tiles);
+  if (e == hipSuccess) e = hipMalloc(&p->d_gap_col0, sizeof(long long) * std::max<long long>(p->n_gap_tiles, 1));
+  if (e == hipSuccess && p->n_gap_tiles > 0)
+    e = hipMemcpy(p->d_gap_col0, gap_col0.data(), sizeof(long long) * p->n_gap_tiles, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(p->d_utts, p->utts.data(), sizeof(UttDesc) * n_utts, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(p->d_tile_utt, tile_utt.data(), sizeof(int) * p->n_tiles, hipMemcpyHostToDevice);
   if (e != hipSuccess) {
@@ -596,6 +615,7 @@ void pwg_plan_destroy(PwgPlan* p) {
     DeviceGuard g(p->h->device);
     if (p->d_utts) (void)hipFree(p->d_utts);
     if (p->d_tile_utt) (void)hipFree(p->d_tile_utt);
+    if (p->d_gap_col0) (void)hipFree(p->d_gap_col0);
   }
   delete p;
 }
@@ -660,9 +680,10 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
   if (e != hipSuccess) return hip_fail(e, "aux projection launch");
 
   FirstConvArgs fa;
-  fa.noise = noise; fa.w = packed + h->off_first_w; fa.b = packed + h->off_first_b; fa.x = x0;
-  fa.tile_utt = p->d_tile_utt; fa.utts = p->d_utts; fa.Tpad = p->Tpad; fa.R = h->R; fa.RS = h->RS;
-  e = timed(PWG_KERNEL_FIRST_CONV, [&] { return launch_first_conv(fa, p->n_tiles, s); });
+  fa.noise = noise; fa.w = packed + h->off_first_w; fa.b = packed + h->off_first_b; fa.x = x0; fa.x1 = x1;
+  fa.tile_utt = p->d_tile_utt; fa.utts = p->d_utts; fa.gap_col0 = p->d_gap_col0; fa.n_work = p->n_tiles;
+  fa.Tpad = p->Tpad; fa.R = h->R; fa.RS = h->RS;
+  e = timed(PWG_KERNEL_FIRST_CONV, [&] { return launch_first_conv(fa, p->n_tiles + p->n_gap_tiles, s); });
   if (e != hipSuccess) return hip_fail(e, "first_conv launch");
 
   float* xin = x0;
@@ -678,7 +699,7 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
     la.tab.Fmin = h->aux.Fmin; la.nka = h->aux.nka; la.nfwg = h->aux.nfwg;
     la.wg = L0 + h->lo_wg; la.bg = L0 + h->lo_bg; la.w2 = L0 + h->lo_w2;
     la.tile_utt = p->d_tile_utt; la.utts = p->d_utts; la.Tpad = p->Tpad;
-    la.R = h->R; la.RP = h->RP; la.RS = h->RS; la.S = h->S; la.SS = h->SS; la.KS = h->KS; la.dil = h->dil[l];
+    la.R = h->R; la.RS = h->RS; la.S = h->S; la.SS = h->SS; la.KS = h->KS; la.dil = h->dil[l];
     la.tap_center = h->cfg.use_causal_conv ? h->KS - 1 : (h->KS - 1) / 2;
     la.first = l == 0;
     const bool last = l == h->L - 1;

@@ -7,10 +7,10 @@ namespace pwg {
 
 // Time tile of one residual-layer workgroup: 4 waves x 32 samples (one 32x32 MFMA column block each).
 constexpr int TILE = 128;
-// Utterance segments on the HBM time axis are padded to this multiple so no tile straddles two
-// utterances (per-layer zero padding at utterance edges, residual_block.py:82-89, is then a
-// per-tile bounds check).
-constexpr int SEG = 256;
+// HBM time axis of a planned batch: [gap][utt 0, padded to TILE][gap][utt 1 ...][gap]. The gaps
+// are >= the largest dilated-conv tap offset and hold zeros in both residual buffers, and the
+// padding columns of every utterance are written as zeros, so the per-layer zero padding at
+// utterance edges (residual_block.py:82-89) costs no masking: a shifted tap simply reads zeros.
 // K-chunk of the gate GEMM staged per LDS round.
 constexpr int KC = 16;
 constexpr int MAX_SCALES = 8;
@@ -22,6 +22,7 @@ constexpr int AUX_MAX_NFWG = 16;
 // One utterance of a planned batch. All offsets in elements.
 struct UttDesc {
   long long seg_base;    // first sample of the utterance on the padded HBM time axis
+  long long first_tile;  // index of its first work tile
   long long T;           // samples = frames * upsample_factor
   long long frame_base;  // first frame in the compact conv_in output C1 [A][F_total]
   long long frames;      // T'
@@ -67,13 +68,18 @@ struct AuxProjArgs {
   int A, GR;
 };
 
+// Writes X0 and zeroes everything of X0/X1 the layers read but never write (gaps, padding
+// channels). Blocks [0, n_work) are work tiles, the rest gap tiles (gap_col0).
 struct FirstConvArgs {
   const float* noise;    // compact
   const float* w;        // [R]
   const float* b;        // [R]
   float* x;              // [Tpad][RS] time-major
+  float* x1;             // the other residual buffer
   const int* tile_utt;
   const UttDesc* utts;
+  const long long* gap_col0;
+  long long n_work;
   long long Tpad;
   int R, RS;
 };
@@ -87,13 +93,13 @@ struct LayerArgs {
   float* skip;           // [Tpad][SS]
   const float* d;        // this layer's frame-rate aux projection [F_total][GR]
   AuxTab tab;
-  const float* wg;       // gate GEMM A-fragments [K1/2][MT][64], K1 = KS*RP
+  const float* wg;       // gate GEMM A-fragments [K1/2][MT][64], K1 = KS*RS
   const float* bg;       // [2*GHPAD]  gate bias, added by an MFMA k-step against a ones row
   const float* w2;       // skip|out GEMM A-fragments incl. a bias k-step, [NQ4][M2T][64][4]
   const int* tile_utt;
   const UttDesc* utts;
   long long Tpad;
-  int R, RP, RS, S, SS, KS;  // RP = R rounded up to KC (one K chunk never straddles two taps)
+  int R, RS, S, SS, KS;  // RS = R rounded up to KC: the row stride of x, channels [R, RS) are zero
   int dil;
   int nka;               // aux k-steps per wave (frames of a 32-sample window / 2)
   int nfwg;              // frames staged per workgroup

@@ -1,10 +1,10 @@
 // HIP kernels of the PWG generator forward for gfx950 (MI355X, CDNA4).
 //
-// Data layout in HBM (see DESIGN.md "Data layout"): every activation is channel-major
-// [channels][Tpad] on one padded time axis that concatenates the batch's utterances, each
-// utterance segment padded to a multiple of SEG samples. A time tile of TILE samples therefore
-// belongs to exactly one utterance (tile_utt[]), and the per-layer zero padding at utterance
-// edges (layers/residual_block.py:82-89) is a bounds check on the staged operand.
+// Data layout in HBM (see DESIGN.md "Data layout"): the residual stream and the skip sum are
+// time-major [Tpad][channels] on one padded time axis that concatenates the batch's utterances,
+// each padded to a multiple of TILE and separated by zero gaps wider than any dilated-conv tap
+// offset. A time tile belongs to exactly one utterance (tile_utt[]), and the per-layer zero
+// padding at utterance edges (layers/residual_block.py:82-89) is free: shifted taps read zeros.
 //
 // Kernels (reference op each one replaces):
 //   pwg_conv_in_kernel      ReplicationPad1d + (c-mean)/scale + conv_in (Conv1d A->A, k=2w+1, valid)
@@ -149,11 +149,20 @@ __global__ void __launch_bounds__(256) pwg_aux_proj_kernel(const AuxProjArgs a) 
 }
 
 // ---------------------------------------------------------------------------------------------
-// first_conv (1x1, 1 -> R, bias): writes X0 time-major [Tpad][RS], zero in segment padding.
+// first_conv (1x1, 1 -> R, bias): writes X0 time-major [Tpad][RS] (zero in utterance padding and
+// padding channels), zeroes the padding channels of X1 and, in gap blocks, both buffers.
 __global__ void __launch_bounds__(256) pwg_first_conv_kernel(const FirstConvArgs a) {
   const long long tile = blockIdx.x;
+  if (tile >= a.n_work) {
+    const long long col0 = a.gap_col0[tile - a.n_work];
+    for (int idx = threadIdx.x; idx < a.RS * TILE; idx += 256) {
+      a.x[(size_t)col0 * a.RS + idx] = 0.f;
+      a.x1[(size_t)col0 * a.RS + idx] = 0.f;
+    }
+    return;
+  }
   const UttDesc ud = a.utts[a.tile_utt[tile]];
-  const long long col0 = tile * TILE;
+  const long long col0 = ud.seg_base + (tile - ud.first_tile) * TILE;
   const long long t0 = col0 - ud.seg_base;
   for (int idx = threadIdx.x; idx < a.RS * TILE; idx += 256) {
     const int j = idx / a.RS, c = idx - j * a.RS;
@@ -161,6 +170,7 @@ __global__ void __launch_bounds__(256) pwg_first_conv_kernel(const FirstConvArgs
     float v = 0.f;
     if (t < ud.T && c < a.R) v = fmaf(a.w[c], a.noise[ud.io_off + t], a.b[c]);
     a.x[(size_t)(col0 + j) * a.RS + c] = v;
+    if (c >= a.R) a.x1[(size_t)(col0 + j) * a.RS + c] = 0.f;
   }
 }
 
@@ -170,7 +180,7 @@ __global__ void __launch_bounds__(256) pwg_first_conv_kernel(const FirstConvArgs
 // its registers.
 //
 // GEMM 1 (gate pre-activation, GR = 32*MT packed rows):
-//   Z = Wdil . [x(t+(0-c)d); x(t+(1-c)d); ...]   K = KS*RP, streamed through LDS in KC=16 chunks,
+//   Z = Wdil . [x(t+(0-c)d); x(t+(1-c)d); ...]   K = KS*RS, streamed through LDS in KC=16 chunks,
 //       one chunk = 16 channels of ONE tap (uniform time shift), double-buffered: the global
 //       loads of chunk i+1 are in flight while chunk i's MFMAs run, one barrier per chunk;
 //     + U(D_l)                                   the aux term at sample rate from frame-rate
@@ -200,45 +210,30 @@ struct LayerSmem {
   static constexpr int FLOATS = 2 * BUF + (AUX_MAX_NFWG + 2) * GR;
 };
 
-// Registers carrying one K chunk from global memory to LDS: raw loads plus a validity mask that
-// is applied only when the chunk is written to LDS, so no instruction touches the loaded values
-// before the MFMAs of the current chunk have been issued (named fields, native vectors: a
-// predicated or struct-typed load is spilled to scratch / forces an early vmcnt(0) in hipcc).
+// Registers carrying one K chunk from global memory to LDS (named fields, native vectors: an
+// array or struct-typed load is spilled to scratch by hipcc).
 struct ChunkRegs {
   f32x4 a0, a1, b0, b1;
-  unsigned mask;  // bit j: element j of b0, bit 4+j: element j of b1
 };
 
 // Chunk c = 16 consecutive K rows of ONE tap: A fragments (contiguous in the packed image) and
-// the activation rows x[t0 + off + t][ch0 .. ch0+15], t in [0, 128), zero outside the utterance.
-// Thread -> (t = tid/4 + 64 i, channel quad q = tid%4): lanes 4t..4t+3 read one 64-byte row
-// piece. Loads are unconditional from addresses clamped into the utterance's padded segment
-// (a load under a divergent branch makes hipcc wait vmcnt(0) at the merge,
-// cdna_hip_programming.md sec 5 item 4(c)).
+// the activation rows x[col0 + off + t][ch0 .. ch0+15], t in [0, 128). Thread -> (t = tid/4 + 64 i,
+// channel quad q = tid%4): lanes 4t..4t+3 read one 64-byte row piece. No masks or clamps: the
+// zero gaps / padding make every shifted read either valid data or the reference's zero pad.
 template <int MT>
-__device__ __forceinline__ void layer_load_chunk(const LayerArgs& a, int c, const UttDesc& ud, long long t0,
-                                                 long long segpad, int tid, ChunkRegs& r) {
+__device__ __forceinline__ void layer_load_chunk(const LayerArgs& a, int c, const float* xcol, int tid,
+                                                 ChunkRegs& r) {
   constexpr int NA4 = LayerSmem<MT>::A_CHUNK / 4;
   const f32x4* wsrc = reinterpret_cast<const f32x4*>(a.wg + (size_t)c * LayerSmem<MT>::A_CHUNK);
   r.a0 = wsrc[NA4 >= 256 ? tid : (tid < NA4 ? tid : 0)];
   r.a1 = NA4 > 256 ? wsrc[tid + 256] : r.a0;
   const int k0 = c * KC;
-  const int tap = k0 / a.RP;                 // uniform
-  const int ch = k0 - tap * a.RP + 4 * (tid & 3);
+  const int tap = k0 / a.RS;                 // uniform
+  const int ch0 = k0 - tap * a.RS;
   const long long off = (long long)(tap - a.tap_center) * a.dil;
-  const float* base = a.x_in + (size_t)ud.seg_base * a.RS + (ch < a.RS ? ch : 0);
-  unsigned m = 0;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const long long e = t0 + (tid >> 2) + 64 * i + off;
-    const long long ec = e < 0 ? 0 : (e > segpad - 1 ? segpad - 1 : e);
-    const f32x4 v = *reinterpret_cast<const f32x4*>(base + ec * a.RS);
-    if (i == 0) r.b0 = v; else r.b1 = v;
-    const bool tok = e >= 0 && e < ud.T;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) m |= (tok && ch + j < a.R) ? (1u << (4 * i + j)) : 0u;
-  }
-  r.mask = m;
+  const float* p = xcol + (off * a.RS + ch0);
+  r.b0 = *reinterpret_cast<const f32x4*>(p);
+  r.b1 = *reinterpret_cast<const f32x4*>(p + 64 * a.RS);
 }
 
 template <int MT>
@@ -251,8 +246,8 @@ __device__ __forceinline__ void layer_store_chunk(float* buf, int tid, const Chu
   float* bs = buf + LayerSmem<MT>::A_CHUNK + (tid >> 2) * BSTR + 4 * (tid & 3);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    bs[j] = (r.mask >> j) & 1u ? r.b0[j] : 0.f;
-    bs[64 * BSTR + j] = (r.mask >> (4 + j)) & 1u ? r.b1[j] : 0.f;
+    bs[j] = r.b0[j];
+    bs[64 * BSTR + j] = r.b1[j];
   }
 }
 
@@ -283,16 +278,16 @@ __global__ void __launch_bounds__(256, 2) pwg_layer_kernel(const LayerArgs a) {
   const int cl = lane & 31;
   const long long tile = blockIdx.x;
   const UttDesc ud = a.utts[a.tile_utt[tile]];
-  const long long col0 = tile * TILE;
-  const long long t0 = col0 - ud.seg_base;      // local sample index of the tile start
+  const long long t0 = (tile - ud.first_tile) * TILE;  // local sample index of the tile start
+  const long long col0 = ud.seg_base + t0;
   const long long Tu = ud.T;
-  const long long segpad = (Tu + SEG - 1) / SEG * SEG;
-  const int NC = a.KS * a.RP / KC;
+  const int NC = a.KS * a.RS / KC;
+  const float* xcol = a.x_in + (size_t)(col0 + (tid >> 2)) * a.RS + 4 * (tid & 3);
   const int H = a.tab.H;
 
   // ---- prologue: chunk 0 in flight, aux D tile + gate bias to LDS
   ChunkRegs cr;
-  layer_load_chunk<MT>(a, 0, ud, t0, segpad, tid, cr);
+  layer_load_chunk<MT>(a, 0, xcol, tid, cr);
   const long long fwg0 = t0 / H - a.tab.J1;     // first staged frame (utterance-local)
   for (int idx = tid; idx < a.nfwg * GR; idx += 256) {
     const int fi = idx / GR, row = idx - fi * GR;
@@ -316,7 +311,7 @@ __global__ void __launch_bounds__(256, 2) pwg_layer_kernel(const LayerArgs a) {
 
   // ---- GEMM 1 main loop
   for (int c = 0; c < NC; ++c) {
-    if (c + 1 < NC) layer_load_chunk<MT>(a, c + 1, ud, t0, segpad, tid, cr);
+    if (c + 1 < NC) layer_load_chunk<MT>(a, c + 1, xcol, tid, cr);
     const float* buf = lds + (c & 1) * SM::BUF;
     const float* As = buf;
     const float* Bs = buf + SM::A_CHUNK + (wave * 32 + cl) * BSTR + hh;
@@ -410,6 +405,7 @@ __global__ void __launch_bounds__(256, 2) pwg_layer_kernel(const LayerArgs a) {
 
   // ---- epilogue: skip += W_s g + b_s ; x = (W_o g + b_o + x) * sqrt(0.5)   (residual_block.py:135-138)
   const size_t gt = (size_t)(col0 + wave * 32 + cl);
+  const bool live = t0 + wave * 32 + cl < Tu;
   if (!LAST) {
 #pragma unroll
     for (int m2 = 0; m2 < M2T; ++m2) {
@@ -425,7 +421,9 @@ __global__ void __launch_bounds__(256, 2) pwg_layer_kernel(const LayerArgs a) {
         } else if (row < a.S + a.R) {
           const size_t off = gt * a.RS + (row - a.S);
           const f32x4 xin = *reinterpret_cast<const f32x4*>(a.x_in + off);
-          *reinterpret_cast<f32x4*>(a.x_out + off) = (v + xin) * 0.70710677f;
+          const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+          // padding columns stay zero: they are the next layers' right-edge zero pad
+          *reinterpret_cast<f32x4*>(a.x_out + off) = live ? (v + xin) * 0.70710677f : z;
         }
       }
     }
