@@ -114,6 +114,9 @@ def main():
     ap.add_argument("--utts", type=int, default=32, help="utterances per GPU per step")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "layer_traffic.json"))
+    ap.add_argument("--layer-kernel", default="persistent", choices=["persistent", "tiled"])
+    ap.add_argument("--waves-per-wg", type=int, default=None)
+    ap.add_argument("--wg-per-cu", type=int, default=None)
     args = ap.parse_args()
 
     rank, world, dev = dist_setup(args.gpus)
@@ -121,6 +124,11 @@ def main():
     params = configs.generator_params(args.config)
     fs = configs.SAMPLING_RATE[args.config]
     eng = Engine(params, dev)
+    eng.set_option("layer_kernel", args.layer_kernel)
+    if args.waves_per_wg:
+        eng.set_option("waves_per_wg", args.waves_per_wg)
+    if args.wg_per_cu:
+        eng.set_option("wg_per_cu", args.wg_per_cu)
     H = eng.upsample_factor
     A = params["aux_channels"]
 
@@ -217,7 +225,7 @@ def main():
         "rtf_per_gpu": per_gpu and fs / per_gpu,
         "kernel_ms_per_step": {k: round(ms / args.steps, 3) for k, (ms, _) in timing.items()},
         "roofline": {
-            "kernel": "pwg_layer_kernel<4,4> (one fused WaveNet residual layer)",
+            "kernel": f"residual layer ({args.layer_kernel} kernel, one fused WaveNet residual block)",
             "bound": "mfma",
             "achieved": round(achieved_tflops, 3),
             "peak": FP32_PEAK_TFLOPS,

@@ -149,6 +149,15 @@ PWG_API long long pwg_plan_workspace_bytes(const PwgPlan* p);
 PWG_API int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* noise,
             const float* mean, const float* scale, float* out, void* workspace, void* stream);
 
+/* Engine options (pwg_set_option). Defaults are the tuned values; the others exist for A/B
+ * measurement (bench.py --layer-kernel ...). */
+enum {
+  PWG_OPT_LAYER_KERNEL = 0,   /* 0: persistent, weights resident in LDS (default); 1: tiled */
+  PWG_OPT_WAVES_PER_WG = 1,   /* persistent kernel: waves per workgroup (1..8, default 8) */
+  PWG_OPT_WG_PER_CU = 2       /* persistent kernel: workgroups per CU in the grid (default 1) */
+};
+PWG_API int pwg_set_option(PwgHandle* h, int option, long long value);
+
 /* Per-kernel HIP-event timing of pwg_run (off by default). collect synchronises
  * on the recorded events, adds ms and launch counts per PWG_KERNEL_* bucket into
  * the caller's arrays and clears the records. */

@@ -17,7 +17,7 @@ import threading
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_DIR = os.path.join(PKG_DIR, "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libpwg_hip.so")
+LIB_PATH = os.environ.get("PWG_LIB_PATH") or os.path.join(LIB_DIR, "libpwg_hip.so")
 CSRC = [
     os.path.join(PKG_DIR, "csrc", "pwg_kernels.hip"),
     os.path.join(PKG_DIR, "csrc", "pwg_capi.hip"),
@@ -57,9 +57,14 @@ EXPORTED_SYMBOLS = (
     "pwg_plan_padded_samples",
     "pwg_plan_workspace_bytes",
     "pwg_run",
+    "pwg_set_option",
     "pwg_set_timing",
     "pwg_timing_collect",
 )
+
+PWG_OPT_LAYER_KERNEL = 0
+PWG_OPT_WAVES_PER_WG = 1
+PWG_OPT_WG_PER_CU = 2
 
 
 class PwgConfig(ctypes.Structure):
@@ -154,6 +159,7 @@ def load():
             getattr(lib, name).restype = ll
         lib.pwg_run.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp]
         lib.pwg_set_timing.argtypes = [vp, ctypes.c_int]
+        lib.pwg_set_option.argtypes = [vp, ctypes.c_int, ctypes.c_longlong]
         lib.pwg_timing_collect.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ll)]
         if lib.pwg_abi_version() != 1:
             raise RuntimeError("libpwg_hip ABI version mismatch")

@@ -257,6 +257,10 @@ struct PwgHandle {
   size_t off_head_w1, off_head_w2, off_head_b2, packed_total;
   int M3T;
   long long ref_total;
+  size_t lo_wgp;
+  // options
+  int layer_kernel = 0, waves_per_wg = 8, wg_per_cu = 1;
+  int n_cu = 0;
   // timing
   bool timing = false;
   std::vector<TimingRecord> records;
@@ -295,6 +299,8 @@ int pwg_create(const PwgConfig* cfg, int device, PwgHandle** out) {
     return fail(PWG_ERR_INVALID, "gate_channels must be even (split into tanh/sigmoid halves)");
   if (c.residual_channels < 1 || c.skip_channels < 1 || c.aux_channels < 1)
     return fail(PWG_ERR_UNSUPPORTED, "residual/skip/aux channels must be >= 1");
+  if (c.residual_channels % 8 != 0 || c.skip_channels % 8 != 0)
+    return fail(PWG_ERR_UNSUPPORTED, "residual_channels and skip_channels must be multiples of 8");
   if (c.aux_context_window < 0) return fail(PWG_ERR_INVALID, "aux_context_window must be >= 0");
   if (c.num_scales < 1 || c.num_scales > PWG_MAX_SCALES)
     return fail(PWG_ERR_UNSUPPORTED, "1..8 upsample scales supported");
@@ -357,7 +363,8 @@ int pwg_create(const PwgConfig* cfg, int device, PwgHandle** out) {
   h->off_tab_small = o;
   o += align64((size_t)std::max<long long>(h->aux.H * h->aux.Fmin * (h->aux.Fmin - 1) / 2, 1) * AUX_J4);
   h->lo_wg = 0;
-  h->lo_bg = h->lo_wg + align64((size_t)(h->K1 / 2) * h->MT * 64);
+  h->lo_wgp = h->lo_wg + align64((size_t)(h->K1 / 2) * h->MT * 64);
+  h->lo_bg = h->lo_wgp + align64((size_t)(h->K1 / 2) * h->MT * 64);
   h->lo_w2 = h->lo_bg + align64(2 * h->GHPAD);
   h->layer_stride = h->lo_w2 + align64((size_t)h->NQ4 * h->M2T * 64 * 4);
   h->off_layers = o; o += h->layer_stride * h->L;
@@ -456,6 +463,25 @@ int pwg_pack_weights(const PwgHandle* h, const float* ref, float* pk) {
       for (int m = 0; m < MT; ++m)
         for (int lane = 0; lane < 64; ++lane)
           wg[((size_t)s * MT + m) * 64 + lane] = wcat(gate_row(32 * m + (lane & 31)), 2 * s + (lane >> 5));
+    // persistent-kernel grouping: group g = 2*GK channels c0.. of one tap (GK = 16 when RS % 32 == 0,
+    // else 8); k-step i of the group pairs channels c0+i (lane half 0) and c0+GK+i (lane half 1).
+    // Stored in 4-k-step slices: [g][i/4][m][lane][i%4].
+    float* wgp = L0 + h->lo_wgp;
+    {
+      const int GK = RS % 32 == 0 ? 16 : 8;
+      const int NB = GK / 4;
+      for (int g = 0; g < h->K1 / (2 * GK); ++g) {
+        const int tap = (2 * GK * g) / RS, c0 = (2 * GK * g) % RS;
+        for (int i = 0; i < GK; ++i)
+          for (int m = 0; m < MT; ++m)
+            for (int lane = 0; lane < 64; ++lane) {
+              const int grow = gate_row(32 * m + (lane & 31));
+              const int ch = c0 + i + GK * (lane >> 5);
+              wgp[((((size_t)g * NB + i / 4) * MT + m) * 64 + lane) * 4 + (i % 4)] =
+                  (grow < 0 || ch >= R) ? 0.f : wd[((size_t)grow * R + ch) * KS + tap];
+            }
+      }
+    }
     float* bg = L0 + h->lo_bg;
     for (int prow = 0; prow < 2 * GHPAD; ++prow) {
       const int gr = gate_row(prow);
@@ -645,6 +671,12 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
   PwgHandle* h = p->h;
   DeviceGuard g(h->device);
   if (!g.ok) return fail(PWG_ERR_HIP, "hipSetDevice failed");
+  if (h->n_cu == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || n < 1)
+      return fail(PWG_ERR_HIP, "cannot query the CU count");
+    h->n_cu = n;
+  }
   hipStream_t s = (hipStream_t)stream;
   char* ws = (char*)workspace;
   float* x0 = (float*)(ws + p->ws_x0);
@@ -697,7 +729,8 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
     la.tab.right = packed + h->off_tab_right; la.tab.small = packed + h->off_tab_small;
     la.tab.H = (int)h->aux.H; la.tab.J1 = h->aux.J1; la.tab.TL = h->aux.TL; la.tab.TR = h->aux.TR;
     la.tab.Fmin = h->aux.Fmin; la.nka = h->aux.nka; la.nfwg = h->aux.nfwg;
-    la.wg = L0 + h->lo_wg; la.bg = L0 + h->lo_bg; la.w2 = L0 + h->lo_w2;
+    la.wg = L0 + h->lo_wg; la.wgp = L0 + h->lo_wgp; la.bg = L0 + h->lo_bg; la.w2 = L0 + h->lo_w2;
+    la.n_blocks = p->n_tiles * (TILE / 32);
     la.tile_utt = p->d_tile_utt; la.utts = p->d_utts; la.Tpad = p->Tpad;
     la.R = h->R; la.RS = h->RS; la.S = h->S; la.SS = h->SS; la.KS = h->KS; la.dil = h->dil[l];
     la.tap_center = h->cfg.use_causal_conv ? h->KS - 1 : (h->KS - 1) / 2;
@@ -707,12 +740,39 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
     la.out = out; la.O = h->O; la.skip_scale = (float)std::sqrt(1.0 / h->L);
     if (p->layout == PWG_LAYOUT_INFERENCE) { la.out_stride_t = h->O; la.out_stride_o = 1; }
     else { la.out_stride_t = 1; la.out_stride_o = p->utts[0].T; }
-    e = timed(PWG_KERNEL_RESIDUAL_LAYER,
-              [&] { return launch_layer(la, h->MT, h->M2T, last, p->n_tiles, s); });
+    if (h->layer_kernel == 0) {
+      const int nwg = h->n_cu * h->wg_per_cu;
+      e = timed(PWG_KERNEL_RESIDUAL_LAYER, [&] {
+        return launch_layer_persistent(la, h->MT, h->M2T, last, h->waves_per_wg, nwg, s);
+      });
+    } else {
+      e = timed(PWG_KERNEL_RESIDUAL_LAYER,
+                [&] { return launch_layer(la, h->MT, h->M2T, last, p->n_tiles, s); });
+    }
     if (e != hipSuccess) return hip_fail(e, "residual layer launch");
     std::swap(xin, xout);
   }
   return PWG_OK;
+}
+
+int pwg_set_option(PwgHandle* h, int option, long long value) {
+  if (!h) return fail(PWG_ERR_INVALID, "null handle");
+  switch (option) {
+    case PWG_OPT_LAYER_KERNEL:
+      if (value != 0 && value != 1) return fail(PWG_ERR_INVALID, "layer kernel must be 0 or 1");
+      h->layer_kernel = (int)value;
+      return PWG_OK;
+    case PWG_OPT_WAVES_PER_WG:
+      if (value < 1 || value > 8) return fail(PWG_ERR_INVALID, "waves per workgroup must be in [1, 8]");
+      h->waves_per_wg = (int)value;
+      return PWG_OK;
+    case PWG_OPT_WG_PER_CU:
+      if (value < 1 || value > 64) return fail(PWG_ERR_INVALID, "workgroups per CU must be in [1, 64]");
+      h->wg_per_cu = (int)value;
+      return PWG_OK;
+    default:
+      return fail(PWG_ERR_INVALID, "unknown option");
+  }
 }
 
 int pwg_set_timing(PwgHandle* h, int enable) {

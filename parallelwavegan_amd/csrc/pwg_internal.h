@@ -93,7 +93,9 @@ struct LayerArgs {
   float* skip;           // [Tpad][SS]
   const float* d;        // this layer's frame-rate aux projection [F_total][GR]
   AuxTab tab;
-  const float* wg;       // gate GEMM A-fragments [K1/2][MT][64], K1 = KS*RS
+  const float* wg;       // gate GEMM A-fragments [K1/2][MT][64], K1 = KS*RS (tiled kernel)
+  const float* wgp;      // the same, grouped for the persistent kernel [K1/8][MT][64][4]
+  long long n_blocks;    // 32-sample blocks (4 per tile)
   const float* bg;       // [2*GHPAD]  gate bias, added by an MFMA k-step against a ones row
   const float* w2;       // skip|out GEMM A-fragments incl. a bias k-step, [NQ4][M2T][64][4]
   const int* tile_utt;
@@ -121,5 +123,7 @@ hipError_t launch_conv_in(const ConvInArgs& a, hipStream_t s);
 hipError_t launch_aux_proj(const AuxProjArgs& a, int layers, hipStream_t s);
 hipError_t launch_first_conv(const FirstConvArgs& a, long long n_tiles, hipStream_t s);
 hipError_t launch_layer(const LayerArgs& a, int mt, int m2t, bool last, long long n_tiles, hipStream_t s);
+hipError_t launch_layer_persistent(const LayerArgs& a, int mt, int m2t, bool last, int waves_per_wg, int n_wg,
+                                   hipStream_t s);
 
 }  // namespace pwg

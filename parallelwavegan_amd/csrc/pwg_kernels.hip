@@ -411,14 +411,15 @@ __global__ void __launch_bounds__(256, 2) pwg_layer_kernel(const LayerArgs a) {
     for (int m2 = 0; m2 < M2T; ++m2) {
 #pragma unroll
       for (int j4 = 0; j4 < 4; ++j4) {
-        const int row = 32 * m2 + 8 * j4 + 4 * hh;  // 4 consecutive channels row..row+3
+        const int rowu = 32 * m2 + 8 * j4;  // S, R multiples of 8: wave-uniform branch
+        const int row = rowu + 4 * hh;       // 4 consecutive channels row..row+3
         f32x4 v;
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = acc2[m2][4 * j4 + i];
-        if (row < a.S) {
+        if (rowu < a.S) {
           f32x4* p = reinterpret_cast<f32x4*>(a.skip + gt * a.SS + row);
           *p = a.first ? v : (*p + v);
-        } else if (row < a.S + a.R) {
+        } else if (rowu < a.S + a.R) {
           const size_t off = gt * a.RS + (row - a.S);
           const f32x4 xin = *reinterpret_cast<const f32x4*>(a.x_in + off);
           const f32x4 z = {0.f, 0.f, 0.f, 0.f};
@@ -439,11 +440,12 @@ __global__ void __launch_bounds__(256, 2) pwg_layer_kernel(const LayerArgs a) {
   for (int m2 = 0; m2 < M2T; ++m2) {
 #pragma unroll
     for (int j4 = 0; j4 < 4; ++j4) {
-      const int row = 32 * m2 + 8 * j4 + 4 * hh;
+      const int rowu = 32 * m2 + 8 * j4;
+      const int row = rowu + 4 * hh;
       f32x4 v;
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] = acc2[m2][4 * j4 + i];
-      if (row < a.S) {
+      if (rowu < a.S) {
         if (!a.first) v += *reinterpret_cast<const f32x4*>(a.skip + gt * a.SS + row);
 #pragma unroll
         for (int i = 0; i < 4; ++i) hs[m2][4 * j4 + i] = fmaxf(v[i] * a.skip_scale, 0.f);
@@ -496,6 +498,326 @@ __global__ void __launch_bounds__(256, 2) pwg_layer_kernel(const LayerArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Persistent residual layer: the layer's weights live in LDS for the whole launch, every wave
+// streams its own 32-sample blocks from HBM/L2 with register prefetch, no barrier after the
+// one-time weight load.
+//
+// LDS (floats): gate fragments [K1/4][MT][64][4] (96 KB for PWG v1) | W2 fragments (incl. bias)
+// [NQ4][M2T][64][4] (36 KB) | gate bias [GR] | last layer: head W1 fragments [NQH4][M3T][64][4].
+// GEMM 1 runs in groups of GK k-steps = 2*GK channels of one tap: lane (t, h) loads
+// x[t+off][c0 + GK*h .. c0 + GK*h + GK-1] (GK*4 contiguous bytes; the two lane halves read one
+// whole 128-byte line per row when GK = 16), the B operand of all GK k-steps (k-step i pairs
+// channels c0+i and c0+GK+i; the host packs the weights in that order). One ds_read_b128 per
+// m-tile gives 4 k-steps of A. Blocks are assigned statically: block b -> wave (b mod waves).
+template <int MT, int M2T, int M3T>
+struct PersistSmem {
+  static constexpr int GR = 32 * MT;
+  static constexpr int GHPAD = (MT == 1) ? 16 : 16 * MT;
+  static constexpr int NQ4 = (GHPAD / 2 + 1 + 3) / 4;
+  static constexpr int NQH4 = (16 * (M3T > 0 ? M3T : 1) + 1 + 3) / 4;
+  static constexpr int W2 = NQ4 * M2T * 256;
+  static constexpr int HW1 = M3T > 0 ? NQH4 * M3T * 256 : 0;
+  __host__ __device__ static constexpr int floats(int k1) { return k1 / 8 * MT * 256 + W2 + GR + HW1; }
+};
+
+template <int MT, int M2T, int M3T, int GK>
+__global__ void __launch_bounds__(512, 1) pwg_layer_persistent_kernel(const LayerArgs a) {
+  using SM = PersistSmem<MT, M2T, M3T>;
+  constexpr int NB = GK / 4;                     // 16-byte B loads per lane per group
+  typedef float bvec __attribute__((ext_vector_type(GK)));  // one lane's B operands of a group
+  constexpr bool LAST = M3T > 0;
+  constexpr int GHPAD = SM::GHPAD;
+  constexpr int GR = SM::GR;
+  constexpr int NQ = GHPAD / 2;
+  constexpr int NQ4 = SM::NQ4;
+  constexpr int NG = (MT == 1) ? 1 : MT / 2;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int K1 = a.KS * a.RS;
+  const int NGRP = K1 / (2 * GK);                // GEMM-1 groups of GK k-steps
+  float* s_wg = smem;
+  float* s_w2 = s_wg + K1 / 8 * MT * 256;
+  float* s_bg = s_w2 + SM::W2;
+  float* s_hw1 = s_bg + GR;
+
+  // ---- one-time: this layer's weights into LDS
+  {
+    const int nthr = blockDim.x;
+    const f32x4* src = reinterpret_cast<const f32x4*>(a.wgp);
+    f32x4* dst = reinterpret_cast<f32x4*>(s_wg);
+    for (int i = threadIdx.x; i < K1 / 8 * MT * 64; i += nthr) dst[i] = src[i];
+    src = reinterpret_cast<const f32x4*>(a.w2);
+    dst = reinterpret_cast<f32x4*>(s_w2);
+    for (int i = threadIdx.x; i < SM::W2 / 4; i += nthr) dst[i] = src[i];
+    for (int i = threadIdx.x; i < GR; i += nthr) s_bg[i] = a.bg[i];
+    if (LAST) {
+      src = reinterpret_cast<const f32x4*>(a.hw1);
+      dst = reinterpret_cast<f32x4*>(s_hw1);
+      for (int i = threadIdx.x; i < SM::HW1 / 4; i += nthr) dst[i] = src[i];
+    }
+    __syncthreads();
+  }
+
+  const int lane = threadIdx.x & 63;
+  const int hh = lane >> 5;
+  const int cl = lane & 31;
+  const int nw = blockDim.x >> 6;
+  const long long total_waves = (long long)gridDim.x * nw;
+  const int H = a.tab.H;
+  const int gpt = a.RS / (2 * GK);               // groups per tap
+  const f32x4* wgl = reinterpret_cast<const f32x4*>(s_wg) + lane;
+  const f32x4* w2l = reinterpret_cast<const f32x4*>(s_w2) + lane;
+
+  // B operand of group g for the lane whose x row is xl (GK*4 contiguous, aligned bytes)
+  auto bptr = [&](const float* xl, int g) -> const bvec* {
+    const int tap = g / gpt;
+    const int c0 = (g - tap * gpt) * 2 * GK;
+    const long long off = (long long)(tap - a.tap_center) * a.dil;
+    return reinterpret_cast<const bvec*>(xl + off * a.RS + c0);
+  };
+  auto block_col = [&](long long blk, UttDesc& ud, long long& t0w) -> long long {
+    const long long tile = blk >> 2;
+    ud = a.utts[a.tile_utt[tile]];
+    t0w = (tile - ud.first_tile) * TILE + (blk & 3) * 32;
+    return ud.seg_base + t0w + cl;
+  };
+
+  long long blk = (long long)blockIdx.x * nw + (threadIdx.x >> 6);
+  if (blk >= a.n_blocks) return;
+  UttDesc ud;
+  long long t0w;
+  long long col = block_col(blk, ud, t0w);
+  bvec bn = *bptr(a.x_in + (size_t)col * a.RS + GK * hh, 0);  // B operand of the next group (prefetched)
+
+  while (true) {
+    const long long Tu = ud.T;
+    const float* xl = a.x_in + (size_t)col * a.RS + GK * hh;
+    const long long nblk = blk + total_waves;
+    UttDesc ud_n = ud;
+    long long t0w_n = 0, col_n = 0;
+    if (nblk < a.n_blocks) col_n = block_col(nblk, ud_n, t0w_n);
+
+    // aux inputs of this block, in flight during GEMM 1
+    const long long t = t0w + cl;
+    float wt[AUX_J4];
+    float dv[8][MT];
+    const long long fw0 = t0w / H - a.tab.J1;  // uniform
+    {
+      const long long tc = t < Tu ? t : Tu - 1;
+      const float* row;
+      const long long F = ud.frames;
+      if (F < a.tab.Fmin) row = a.tab.small + ((long long)H * F * (F - 1) / 2 + tc) * AUX_J4;
+      else if (tc < a.tab.TL) row = a.tab.left + tc * AUX_J4;
+      else if (tc >= Tu - a.tab.TR) row = a.tab.right + (Tu - 1 - tc) * AUX_J4;
+      else row = a.tab.interior + (tc % H) * AUX_J4;
+      const f32x4 w0 = *reinterpret_cast<const f32x4*>(row);
+      const f32x4 w1 = *reinterpret_cast<const f32x4*>(row + 4);
+      const bool ok = t < Tu;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        wt[j] = ok ? w0[j] : 0.f;
+        wt[j + 4] = ok ? w1[j] : 0.f;
+      }
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        if (s >= a.nka) break;
+        long long f = fw0 + 2 * s + hh;
+        f = f < 0 ? 0 : (f >= ud.frames ? ud.frames - 1 : f);  // out-of-range frames carry weight 0
+        const float* drow = a.d + (size_t)(ud.frame_base + f) * GR + cl;
+#pragma unroll
+        for (int m = 0; m < MT; ++m) dv[s][m] = drow[32 * m];
+      }
+    }
+
+    f32x16 acc[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
+
+    // ---- GEMM 1: B prefetched one group ahead, across the block boundary for the last group
+    for (int g = 0; g < NGRP; ++g) {
+      const bvec bc = bn;
+      bn = *(g + 1 < NGRP ? bptr(xl, g + 1)
+                          : bptr(a.x_in + (size_t)(nblk < a.n_blocks ? col_n : col) * a.RS + GK * hh, 0));
+#pragma unroll
+      for (int sub = 0; sub < NB; ++sub) {
+        f32x4 av[MT];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) av[m] = wgl[((g * NB + sub) * MT + m) * 64];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int m = 0; m < MT; ++m)
+            acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m][i], bc[4 * sub + i], acc[m], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+
+    // ---- GEMM 2 in two passes of MP m-tiles (pass 0: skip rows, pass 1: residual rows for PWG v1),
+    //      accumulators initialised with [skip_old; x_in]: the MFMA performs the skip sum and the
+    //      residual add (residual_block.py:138, parallel_wavegan.py:164). Init loads are issued one
+    //      phase ahead (pass 0 before aux + gate, pass 1 before pass 0).
+    constexpr int NP = M2T >= 2 ? 2 : 1;
+    constexpr int MP = M2T / NP;
+    constexpr int NPASS = LAST ? 1 : NP;  // the last layer needs only the skip rows (S <= 32*MP)
+    auto init_pass = [&](int pass, f32x16 (&acc2)[MP]) {
+#pragma unroll
+      for (int mm = 0; mm < MP; ++mm)
+#pragma unroll
+        for (int j4 = 0; j4 < 4; ++j4) {
+          const int rowu = 32 * (pass * MP + mm) + 8 * j4;  // S, R multiples of 8: wave-uniform branch
+          const int row = rowu + 4 * hh;
+          f32x4 v = {0.f, 0.f, 0.f, 0.f};
+          if (rowu < a.S) {
+            if (!a.first) v = *reinterpret_cast<const f32x4*>(a.skip + (size_t)col * a.SS + row);
+          } else if (rowu < a.S + a.R) {
+            v = *reinterpret_cast<const f32x4*>(a.x_in + (size_t)col * a.RS + (row - a.S));
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc2[mm][4 * j4 + i] = v[i];
+        }
+    };
+    f32x16 accp0[MP], accp1[MP];
+    init_pass(0, accp0);
+
+    // ---- aux term + gate bias
+    {
+      const long long fb = t / H - a.tab.J1;
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+        if (s >= a.nka) break;
+        const int j = (int)(fw0 + 2 * s + hh - fb);
+        float bw = 0.f;
+#pragma unroll
+        for (int q = 0; q < AUX_J4; ++q) bw = (j == q) ? wt[q] : bw;
+#pragma unroll
+        for (int m = 0; m < MT; ++m) acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(dv[s][m], bw, acc[m], 0, 0, 0);
+      }
+      const float one = hh == 0 ? 1.f : 0.f;
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(hh == 0 ? s_bg[32 * m + cl] : 0.f, one, acc[m], 0, 0, 0);
+    }
+
+    // ---- gate
+    float gt[NG][16];
+#pragma unroll
+    for (int gm = 0; gm < NG; ++gm)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (MT == 1 && r >= 8) { gt[gm][r] = 0.f; continue; }
+        const float za = acc[gm][r];
+        const float zb = MT == 1 ? acc[0][r + 8] : acc[gm + MT / 2][r];
+        gt[gm][r] = fast_tanh(za) * fast_sigmoid(zb);
+      }
+
+    if (NPASS > 1) init_pass(1, accp1);
+
+    const bool live = t < Tu;
+    auto gemm2_pass = [&](int pass, f32x16 (&acc2)[MP]) {
+#pragma unroll
+      for (int q4 = 0; q4 < NQ4; ++q4) {
+#pragma unroll
+        for (int mm = 0; mm < MP; ++mm) {
+          const f32x4 wv = w2l[(q4 * M2T + pass * MP + mm) * 64];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int q = 4 * q4 + i;
+            if (q > NQ) continue;
+            const float bq = q < NQ ? gt[q >> 4][q & 15] : (hh == 0 ? 1.f : 0.f);
+            acc2[mm] = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[i], bq, acc2[mm], 0, 0, 0);
+          }
+        }
+        // keep the LDS fragment reads next to their MFMAs (hoisting them all costs ~140 VGPRs)
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    auto store_pass = [&](int pass, const f32x16 (&acc2)[MP]) {
+#pragma unroll
+      for (int mm = 0; mm < MP; ++mm)
+#pragma unroll
+        for (int j4 = 0; j4 < 4; ++j4) {
+          const int rowu = 32 * (pass * MP + mm) + 8 * j4;
+          const int row = rowu + 4 * hh;
+          f32x4 v;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = acc2[mm][4 * j4 + i];
+          if (rowu < a.S) {
+            *reinterpret_cast<f32x4*>(a.skip + (size_t)col * a.SS + row) = v;
+          } else if (rowu < a.S + a.R) {
+            const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+            *reinterpret_cast<f32x4*>(a.x_out + (size_t)col * a.RS + (row - a.S)) = live ? v * 0.70710677f : z;
+          }
+        }
+    };
+
+    gemm2_pass(0, accp0);
+    if (!LAST) {
+      store_pass(0, accp0);
+      if (NPASS > 1) {
+        gemm2_pass(1, accp1);
+        store_pass(1, accp1);
+      }
+    } else {
+      // ---- last layer: fused output head on the final skip sum (skip rows all in pass 0)
+      constexpr int M3 = LAST ? M3T : 1;
+      constexpr int NQH = 16 * M3;
+      constexpr int NQH4 = SM::NQH4;
+      float hs[MP][16];
+#pragma unroll
+      for (int mm = 0; mm < MP; ++mm)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = 32 * mm + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          hs[mm][r] = row < a.S ? fmaxf(accp0[mm][r] * a.skip_scale, 0.f) : 0.f;
+        }
+      f32x16 acc3[M3];
+#pragma unroll
+      for (int m = 0; m < M3; ++m)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc3[m][r] = 0.f;
+      const f32x4* hw1 = reinterpret_cast<const f32x4*>(s_hw1) + lane;
+#pragma unroll
+      for (int q4 = 0; q4 < NQH4; ++q4)
+#pragma unroll
+        for (int m3 = 0; m3 < M3; ++m3) {
+          const f32x4 wv = hw1[(q4 * M3 + m3) * 64];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int q = 4 * q4 + i;
+            if (q > NQH || (q < NQH && (q >> 4) >= MP)) continue;
+            const float bq = q < NQH ? hs[q >> 4][q & 15] : (hh == 0 ? 1.f : 0.f);
+            acc3[m3] = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[i], bq, acc3[m3], 0, 0, 0);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      float* out = a.out + ud.io_off * a.O + t * a.out_stride_t;
+      for (int oc = 0; oc < a.O; ++oc) {
+        float part = 0.f;
+#pragma unroll
+        for (int m3 = 0; m3 < M3; ++m3) {
+          const f32x4* w = reinterpret_cast<const f32x4*>(a.hw2 + ((size_t)(oc * M3 + m3) * 2 + hh) * 16);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const f32x4 wq = w[q];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) part = fmaf(wq[i], fmaxf(acc3[m3][4 * q + i], 0.f), part);
+          }
+        }
+        const float y = part + __shfl_xor(part, 32) + a.hb2[oc];
+        if (hh == 0 && live) out[oc * a.out_stride_o] = y;
+      }
+    }
+
+    if (nblk >= a.n_blocks) break;
+    blk = nblk;
+    ud = ud_n;
+    t0w = t0w_n;
+    col = col_n;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 hipError_t launch_conv_in(const ConvInArgs& a, hipStream_t s) {
   const dim3 grid((unsigned)((a.F_total + 63) / 64));
   const int og = (a.A + 3) / 4;
@@ -536,6 +858,42 @@ hipError_t launch_layer(const LayerArgs& a, int mt, int m2t, bool last, long lon
   PWG_LAYER_CASE(2, 1) PWG_LAYER_CASE(2, 2) PWG_LAYER_CASE(2, 4)
   PWG_LAYER_CASE(4, 1) PWG_LAYER_CASE(4, 2) PWG_LAYER_CASE(4, 4)
 #undef PWG_LAYER_CASE
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_layer_persistent(const LayerArgs& a, int mt, int m2t, bool last, int waves_per_wg, int n_wg,
+                                   hipStream_t s) {
+  const dim3 grid((unsigned)n_wg), block((unsigned)(64 * waves_per_wg));
+  const int k1 = a.KS * a.RS;
+  const int m3t = (a.S + 31) / 32;
+  const bool gk16 = a.RS % 32 == 0;  // 32-channel groups when every tap block holds whole groups
+#define PWG_PERS_LAUNCH2(MT_, M2T_, M3T_, GK_)                                                             \
+  {                                                                                                        \
+    const size_t lds = sizeof(float) * PersistSmem<MT_, M2T_, M3T_>::floats(k1);                           \
+    if (lds > 160 * 1024) return hipErrorInvalidValue;                                                     \
+    auto kfn = &pwg_layer_persistent_kernel<MT_, M2T_, M3T_, GK_>;                                         \
+    hipError_t e_ = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),                                \
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);              \
+    if (e_ != hipSuccess) return e_;                                                                       \
+    hipLaunchKernelGGL(kfn, grid, block, lds, s, a);                                                       \
+    return hipGetLastError();                                                                              \
+  }
+#define PWG_PERS_LAUNCH(MT_, M2T_, M3T_) \
+  { if (gk16) PWG_PERS_LAUNCH2(MT_, M2T_, M3T_, 16) else PWG_PERS_LAUNCH2(MT_, M2T_, M3T_, 8) }
+#define PWG_PERS_CASE(MT_, M2T_)                                                    \
+  if (mt == MT_ && m2t == M2T_) {                                                   \
+    if (!last) PWG_PERS_LAUNCH(MT_, M2T_, 0)                                        \
+    if (m3t == 1) PWG_PERS_LAUNCH(MT_, M2T_, 1)                                     \
+    if (m3t == 2 && M2T_ >= 2) PWG_PERS_LAUNCH(MT_, M2T_, (M2T_ >= 2 ? 2 : 1))      \
+    if (M2T_ >= 4) PWG_PERS_LAUNCH(MT_, M2T_, (M2T_ >= 4 ? 4 : 1))                  \
+    return hipErrorInvalidValue;                                                    \
+  }
+  PWG_PERS_CASE(1, 1) PWG_PERS_CASE(1, 2) PWG_PERS_CASE(1, 4)
+  PWG_PERS_CASE(2, 1) PWG_PERS_CASE(2, 2) PWG_PERS_CASE(2, 4)
+  PWG_PERS_CASE(4, 1) PWG_PERS_CASE(4, 2) PWG_PERS_CASE(4, 4)
+#undef PWG_PERS_CASE
+#undef PWG_PERS_LAUNCH
+#undef PWG_PERS_LAUNCH2
   return hipErrorInvalidValue;
 }
 

@@ -256,6 +256,17 @@ class Engine:
             self._workspace = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=self.device)
         return self._workspace
 
+    # ---------------------------------------------------------------- options
+    LAYER_KERNELS = {"persistent": 0, "tiled": 1}
+
+    def set_option(self, option, value):
+        """pwg_set_option: option in {"layer_kernel", "waves_per_wg", "wg_per_cu"}."""
+        opts = {"layer_kernel": _lib.PWG_OPT_LAYER_KERNEL, "waves_per_wg": _lib.PWG_OPT_WAVES_PER_WG,
+                "wg_per_cu": _lib.PWG_OPT_WG_PER_CU}
+        if option == "layer_kernel" and isinstance(value, str):
+            value = self.LAYER_KERNELS[value]
+        _lib.check(self._lib.pwg_set_option(self._h, opts[option], int(value)))
+
     # ---------------------------------------------------------------- timing
     def set_timing(self, enable):
         self.timing_enabled = bool(enable)
