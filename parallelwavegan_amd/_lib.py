@@ -93,13 +93,15 @@ def _needs_build():
     return any(os.path.getmtime(p) > t for p in CSRC + HEADERS)
 
 
-def build(force=False, verbose=False):
-    """Compile the HIP kernels + C-ABI into parallelwavegan_amd/lib/libpwg_hip.so (gfx950)."""
-    if not force and not _needs_build():
+def build(force=False, verbose=False, extra_flags=(), out_path=None):
+    """Compile the HIP kernels + C-ABI into parallelwavegan_amd/lib/libpwg_hip.so (gfx950).
+    extra_flags/out_path build A/B measurement variants (e.g. -DPWG_STORE_SC1=0) elsewhere."""
+    target = out_path or LIB_PATH
+    if not force and out_path is None and not _needs_build():
         return LIB_PATH
-    os.makedirs(LIB_DIR, exist_ok=True)
+    os.makedirs(os.path.dirname(target), exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    tmp = LIB_PATH + ".tmp.%d" % os.getpid()
+    tmp = target + ".tmp.%d" % os.getpid()
     cmd = [
         hipcc,
         f"--offload-arch={OFFLOAD_ARCH}",
@@ -112,14 +114,14 @@ def build(force=False, verbose=False):
         "-Wall",
         "-o",
         tmp,
-    ] + CSRC
+    ] + list(extra_flags) + CSRC
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError("hipcc failed:\n" + " ".join(cmd) + "\n" + res.stdout + res.stderr)
     if verbose and (res.stdout or res.stderr):
         print(res.stdout + res.stderr)
-    os.replace(tmp, LIB_PATH)
-    return LIB_PATH
+    os.replace(tmp, target)
+    return target
 
 
 _lib = None

@@ -276,6 +276,8 @@ struct PwgPlan {
   UttDesc* d_utts = nullptr;
   int* d_tile_utt = nullptr;
   long long* d_gap_col0 = nullptr;
+  BlockDesc* d_blocks = nullptr;
+  UttInfo* d_uttinfo = nullptr;
   // workspace offsets (bytes)
   size_t ws_x0, ws_x1, ws_skip, ws_c1, ws_d, ws_total;
 };
@@ -604,10 +606,30 @@ int pwg_plan_create(PwgHandle* h, int n_utts, const long long* frames, int layou
   p->T_total = io;
   p->n_tiles = tiles;
   p->n_gap_tiles = (long long)gap_col0.size();
+  if (p->Tpad + h->gap >= (1LL << 31) || p->F_total >= (1LL << 31) || p->T_total * h->O >= (1LL << 31)) {
+    delete p;
+    return fail(PWG_ERR_UNSUPPORTED, "batch too large for one plan (2^31 samples); split it");
+  }
   std::vector<int> tile_utt(p->n_tiles);
+  std::vector<BlockDesc> blocks((size_t)p->n_tiles * (TILE / 32));
+  std::vector<UttInfo> uinfo(n_utts);
   for (int u = 0; u < n_utts; ++u) {
-    const long long n = (p->utts[u].T + TILE - 1) / TILE;
-    for (long long t = 0; t < n; ++t) tile_utt[p->utts[u].first_tile + t] = u;
+    const UttDesc& d = p->utts[u];
+    const long long n = (d.T + TILE - 1) / TILE;
+    for (long long t = 0; t < n; ++t) {
+      tile_utt[d.first_tile + t] = u;
+      for (int b = 0; b < TILE / 32; ++b) {
+        BlockDesc& bd = blocks[(size_t)(d.first_tile + t) * (TILE / 32) + b];
+        bd.t0 = (int)(t * TILE + 32 * b);
+        bd.col = (int)(d.seg_base + bd.t0);
+        bd.utt = u;
+        bd.pad = 0;
+      }
+    }
+    uinfo[u].T = (int)d.T;
+    uinfo[u].frames = (int)d.frames;
+    uinfo[u].frame_base = (int)d.frame_base;
+    uinfo[u].io_off = (int)d.io_off;
   }
   size_t o = 0;
   p->ws_x0 = o; o += align_bytes(sizeof(float) * h->RS * p->Tpad);
@@ -624,6 +646,12 @@ int pwg_plan_create(PwgHandle* h, int n_utts, const long long* frames, int layou
   if (e == hipSuccess) e = hipMalloc(&p->d_gap_col0, sizeof(long long) * std::max<long long>(p->n_gap_tiles, 1));
   if (e == hipSuccess && p->n_gap_tiles > 0)
     e = hipMemcpy(p->d_gap_col0, gap_col0.data(), sizeof(long long) * p->n_gap_tiles, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMalloc(&p->d_blocks, sizeof(BlockDesc) * blocks.size());
+  if (e == hipSuccess) e = hipMalloc(&p->d_uttinfo, sizeof(UttInfo) * uinfo.size());
+  if (e == hipSuccess)
+    e = hipMemcpy(p->d_blocks, blocks.data(), sizeof(BlockDesc) * blocks.size(), hipMemcpyHostToDevice);
+  if (e == hipSuccess)
+    e = hipMemcpy(p->d_uttinfo, uinfo.data(), sizeof(UttInfo) * uinfo.size(), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(p->d_utts, p->utts.data(), sizeof(UttDesc) * n_utts, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(p->d_tile_utt, tile_utt.data(), sizeof(int) * p->n_tiles, hipMemcpyHostToDevice);
   if (e != hipSuccess) {
@@ -642,6 +670,8 @@ void pwg_plan_destroy(PwgPlan* p) {
     if (p->d_utts) (void)hipFree(p->d_utts);
     if (p->d_tile_utt) (void)hipFree(p->d_tile_utt);
     if (p->d_gap_col0) (void)hipFree(p->d_gap_col0);
+    if (p->d_blocks) (void)hipFree(p->d_blocks);
+    if (p->d_uttinfo) (void)hipFree(p->d_uttinfo);
   }
   delete p;
 }
@@ -740,10 +770,26 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
     la.out = out; la.O = h->O; la.skip_scale = (float)std::sqrt(1.0 / h->L);
     if (p->layout == PWG_LAYOUT_INFERENCE) { la.out_stride_t = h->O; la.out_stride_o = 1; }
     else { la.out_stride_t = 1; la.out_stride_o = p->utts[0].T; }
-    if (h->layer_kernel == 0) {
+    if (h->layer_kernel == 0 && h->aux.nka <= 4) {
+      PersistArgs pa2;
+      pa2.x_in = xin; pa2.x_out = xout; pa2.skip = skip; pa2.d = la.d;
+      pa2.tab = packed + h->off_tab_interior;
+      pa2.tab_left = (int)(h->off_tab_left - h->off_tab_interior);
+      pa2.tab_right = (int)(h->off_tab_right - h->off_tab_interior);
+      pa2.tab_small = (int)(h->off_tab_small - h->off_tab_interior);
+      pa2.blocks = p->d_blocks; pa2.utts = p->d_uttinfo;
+      pa2.wgp = la.wgp; pa2.w2 = la.w2; pa2.bg = la.bg;
+      pa2.hw1 = la.hw1; pa2.hw2 = la.hw2; pa2.hb2 = la.hb2; pa2.out = out;
+      pa2.H = (int)h->aux.H; pa2.J1 = h->aux.J1; pa2.TL = h->aux.TL; pa2.TR = h->aux.TR;
+      pa2.Fmin = h->aux.Fmin; pa2.nka = h->aux.nka;
+      pa2.n_blocks = (int)la.n_blocks;
+      pa2.R = h->R; pa2.RS = h->RS; pa2.S = h->S; pa2.SS = h->SS; pa2.KS = h->KS; pa2.dil = h->dil[l];
+      pa2.tap_center = la.tap_center; pa2.first = la.first; pa2.O = h->O;
+      pa2.out_stride_t = (int)la.out_stride_t; pa2.out_stride_o = (int)la.out_stride_o;
+      pa2.skip_scale = la.skip_scale;
       const int nwg = h->n_cu * h->wg_per_cu;
       e = timed(PWG_KERNEL_RESIDUAL_LAYER, [&] {
-        return launch_layer_persistent(la, h->MT, h->M2T, last, h->waves_per_wg, nwg, s);
+        return launch_layer_persistent(pa2, h->MT, h->M2T, last, h->waves_per_wg, nwg, s);
       });
     } else {
       e = timed(PWG_KERNEL_RESIDUAL_LAYER,

@@ -118,12 +118,51 @@ struct LayerArgs {
   float skip_scale;
 };
 
+// Compact descriptors for the persistent layer kernel (32-bit: the plan guarantees every column
+// and frame index fits). BlockDesc: one 32-sample block; UttInfo: one utterance.
+struct BlockDesc {
+  int col;    // global column (padded time axis) of the block's first sample
+  int t0;     // utterance-local index of the block's first sample
+  int utt;
+  int pad;
+};
+struct UttInfo {
+  int T;           // samples
+  int frames;      // T'
+  int frame_base;  // first frame in C1 / D
+  int io_off;      // first sample in the caller's noise/output arrays
+};
+
+// Slim argument block of the persistent layer kernel (fewer live scalars than LayerArgs).
+struct PersistArgs {
+  const float* x_in;     // [Tpad][RS]
+  float* x_out;
+  float* skip;           // [Tpad][SS]
+  const float* d;        // this layer's aux projection [F_total][GR]
+  const float* tab;      // AuxTab base; the four tables at 32-bit offsets below
+  const BlockDesc* blocks;
+  const UttInfo* utts;
+  const float* wgp;      // [K1/4][MT][64][4]
+  const float* w2;       // [NQ4][M2T][64][4]
+  const float* bg;       // [GR]
+  const float* hw1;      // last layer only
+  const float* hw2;
+  const float* hb2;
+  float* out;
+  int tab_left, tab_right, tab_small;  // offsets (floats) from tab; interior at 0
+  int H, J1, TL, TR, Fmin, nka;
+  int n_blocks;
+  int R, RS, S, SS, KS, dil, tap_center, first, O;
+  int out_stride_t, out_stride_o;
+  float skip_scale;
+};
+
 // Kernel launchers (pwg_kernels.hip).
 hipError_t launch_conv_in(const ConvInArgs& a, hipStream_t s);
 hipError_t launch_aux_proj(const AuxProjArgs& a, int layers, hipStream_t s);
 hipError_t launch_first_conv(const FirstConvArgs& a, long long n_tiles, hipStream_t s);
 hipError_t launch_layer(const LayerArgs& a, int mt, int m2t, bool last, long long n_tiles, hipStream_t s);
-hipError_t launch_layer_persistent(const LayerArgs& a, int mt, int m2t, bool last, int waves_per_wg, int n_wg,
+hipError_t launch_layer_persistent(const PersistArgs& a, int mt, int m2t, bool last, int waves_per_wg, int n_wg,
                                    hipStream_t s);
 
 }  // namespace pwg

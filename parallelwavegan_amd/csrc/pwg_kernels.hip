@@ -520,20 +520,56 @@ struct PersistSmem {
   __host__ __device__ static constexpr int floats(int k1) { return k1 / 8 * MT * 256 + W2 + GR + HW1; }
 };
 
-template <int MT, int M2T, int M3T, int GK>
-__global__ void __launch_bounds__(512, 1) pwg_layer_persistent_kernel(const LayerArgs a) {
+// tanh(a) * sigmoid(b) with 2 v_exp + 1 v_rcp: (1 - e^-2a) / ((1 + e^-2a)(1 + e^-b)). Inputs are
+// clamped where the result is already saturated in fp32 (|a| > 15: tanh = +-1; b < -30: sigmoid
+// < 1e-13) so no intermediate overflows.
+__device__ __forceinline__ float fast_gate(float a, float b) {
+  a = __builtin_amdgcn_fmed3f(a, -15.f, 15.f);
+  b = __builtin_amdgcn_fmed3f(b, -30.f, 88.f);
+  const float e1 = __builtin_amdgcn_exp2f(a * -2.8853900817779268f);  // e^{-2a}
+  const float e2 = __builtin_amdgcn_exp2f(b * -1.4426950408889634f);  // e^{-b}
+  return (1.f - e1) * __builtin_amdgcn_rcpf((1.f + e1) * (1.f + e2));
+}
+
+// Stores of the streamed outputs (x_out, skip). PWG_STORE_SC1=1 selects write-through sc1 stores
+// (cache policy 16), which drop the line from the XCD's L2; measured 11 % SLOWER than plain stores
+// on the LibriTTS bench (4.55 vs 4.10 ms per layer), so plain stores are the default.
+#ifndef PWG_STORE_SC1
+#define PWG_STORE_SC1 0
+#endif
+__device__ __forceinline__ void store_stream(float* wave_base, int byte_off, f32x4 v) {
+#if PWG_STORE_SC1
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(wave_base, 0, 0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
+                                         rsrc, byte_off, 0, 16);
+#else
+  *reinterpret_cast<f32x4*>(reinterpret_cast<char*>(wave_base) + byte_off) = v;
+#endif
+}
+
+// RC / SC: compile-time residual / skip channels for the production shapes (0 = runtime).
+// 8 waves per CU (2 per SIMD): measured faster than 12 with the XCD-local schedule (L2 footprint).
+template <int MT, int M2T, int M3T, int GK, int RC, int SC>
+__global__ void __launch_bounds__(512, 1) pwg_layer_persistent_kernel(const PersistArgs a) {
   using SM = PersistSmem<MT, M2T, M3T>;
-  constexpr int NB = GK / 4;                     // 16-byte B loads per lane per group
-  typedef float bvec __attribute__((ext_vector_type(GK)));  // one lane's B operands of a group
+  constexpr int NB = GK / 4;                                   // 4-k-step slices per group
+  typedef float bvec __attribute__((ext_vector_type(GK)));   // one lane's B operands of a group
   constexpr bool LAST = M3T > 0;
   constexpr int GHPAD = SM::GHPAD;
   constexpr int GR = SM::GR;
   constexpr int NQ = GHPAD / 2;
   constexpr int NQ4 = SM::NQ4;
   constexpr int NG = (MT == 1) ? 1 : MT / 2;
+  constexpr int NP = M2T >= 2 ? 2 : 1;       // GEMM-2 passes (pass 0: skip rows for PWG v1)
+  constexpr int MP = M2T / NP;
+  constexpr int NPASS = LAST ? 1 : NP;       // the last layer needs the skip rows only (S <= 32*MP)
+  const int R = RC ? RC : a.R;
+  const int S = SC ? SC : a.S;
+  const int RS = RC ? (RC + KC - 1) / KC * KC : a.RS;
+  const int SS = SC ? (SC + 3) / 4 * 4 : a.SS;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int K1 = a.KS * a.RS;
-  const int NGRP = K1 / (2 * GK);                // GEMM-1 groups of GK k-steps
+  const int K1 = a.KS * RS;
+  const int NGRP = K1 / (2 * GK);
   float* s_wg = smem;
   float* s_w2 = s_wg + K1 / 8 * MT * 256;
   float* s_bg = s_w2 + SM::W2;
@@ -561,105 +597,105 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_persistent_kernel(const Laye
   const int hh = lane >> 5;
   const int cl = lane & 31;
   const int nw = blockDim.x >> 6;
-  const long long total_waves = (long long)gridDim.x * nw;
-  const int H = a.tab.H;
-  const int gpt = a.RS / (2 * GK);               // groups per tap
+  // XCD-aware static schedule (speed only, never correctness): workgroups are dealt round-robin
+  // over the 8 XCDs, so workgroup i runs on XCD i % 8; XCD x sweeps the x-th contiguous eighth of
+  // the blocks with all its waves side by side, so the dilated taps of a block re-read rows that
+  // neighbouring waves of the same XCD just loaded (its 4 MB L2) instead of HBM.
+  const int xcd = blockIdx.x & 7;
+  const int nwg_x = ((int)gridDim.x - xcd + 7) >> 3;
+  const int stride = nwg_x * nw;
+  const int blk_end = (int)((long long)a.n_blocks * (xcd + 1) / 8);
+  const int gpt = RS / (2 * GK);  // groups per tap
   const f32x4* wgl = reinterpret_cast<const f32x4*>(s_wg) + lane;
   const f32x4* w2l = reinterpret_cast<const f32x4*>(s_w2) + lane;
 
-  // B operand of group g for the lane whose x row is xl (GK*4 contiguous, aligned bytes)
-  auto bptr = [&](const float* xl, int g) -> const bvec* {
+  // lane's B operand (GK channels) of group g for the block starting at column c
+  auto bload = [&](int c, int g) -> bvec {
     const int tap = g / gpt;
     const int c0 = (g - tap * gpt) * 2 * GK;
-    const long long off = (long long)(tap - a.tap_center) * a.dil;
-    return reinterpret_cast<const bvec*>(xl + off * a.RS + c0);
+    const int off = (tap - a.tap_center) * a.dil;
+    return *reinterpret_cast<const bvec*>(a.x_in + (size_t)(c + cl + off) * RS + c0 + GK * hh);
   };
-  auto block_col = [&](long long blk, UttDesc& ud, long long& t0w) -> long long {
-    const long long tile = blk >> 2;
-    ud = a.utts[a.tile_utt[tile]];
-    t0w = (tile - ud.first_tile) * TILE + (blk & 3) * 32;
-    return ud.seg_base + t0w + cl;
+  // 4*GK-byte group of k-steps: 16 MFMAs per 4-k-step slice, A from LDS
+  auto group_mfma = [&](f32x16 (&acc)[MT], const bvec& b, int g) {
+#pragma unroll
+    for (int sub = 0; sub < NB; ++sub) {
+      f32x4 av[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) av[m] = wgl[((g * NB + sub) * MT + m) * 64];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+          acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m][i], b[4 * sub + i], acc[m], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   };
 
-  long long blk = (long long)blockIdx.x * nw + (threadIdx.x >> 6);
-  if (blk >= a.n_blocks) return;
-  UttDesc ud;
-  long long t0w;
-  long long col = block_col(blk, ud, t0w);
-  bvec bn = *bptr(a.x_in + (size_t)col * a.RS + GK * hh, 0);  // B operand of the next group (prefetched)
+  int blk = (int)((long long)a.n_blocks * xcd / 8) + (blockIdx.x >> 3) * nw + (threadIdx.x >> 6);
+  if (blk >= blk_end) return;
+  BlockDesc bd = a.blocks[blk];
+  bvec b0 = bload(bd.col, 0);  // B operand of the next group (prefetched, across blocks)
 
   while (true) {
-    const long long Tu = ud.T;
-    const float* xl = a.x_in + (size_t)col * a.RS + GK * hh;
-    const long long nblk = blk + total_waves;
-    UttDesc ud_n = ud;
-    long long t0w_n = 0, col_n = 0;
-    if (nblk < a.n_blocks) col_n = block_col(nblk, ud_n, t0w_n);
+    const UttInfo ui = a.utts[bd.utt];
+    const int col = bd.col + cl;  // this lane's column
+    const int t = bd.t0 + cl;     // this lane's utterance-local sample
+    const bool live = t < ui.T;
+    const int nblk = blk + stride;
+    const int col_next = nblk < blk_end ? a.blocks[nblk].col : bd.col;
 
-    // aux inputs of this block, in flight during GEMM 1
-    const long long t = t0w + cl;
-    float wt[AUX_J4];
-    float dv[8][MT];
-    const long long fw0 = t0w / H - a.tab.J1;  // uniform
+    // aux inputs, in flight during GEMM 1: B weights bw[s] = w_t[f - t/H + J1] of frame
+    // f = fw0 + 2s + h (a table load per k-step), A = D rows of those frames
+    float bw[4];
+    float dv[4][MT];
     {
-      const long long tc = t < Tu ? t : Tu - 1;
-      const float* row;
-      const long long F = ud.frames;
-      if (F < a.tab.Fmin) row = a.tab.small + ((long long)H * F * (F - 1) / 2 + tc) * AUX_J4;
-      else if (tc < a.tab.TL) row = a.tab.left + tc * AUX_J4;
-      else if (tc >= Tu - a.tab.TR) row = a.tab.right + (Tu - 1 - tc) * AUX_J4;
-      else row = a.tab.interior + (tc % H) * AUX_J4;
-      const f32x4 w0 = *reinterpret_cast<const f32x4*>(row);
-      const f32x4 w1 = *reinterpret_cast<const f32x4*>(row + 4);
-      const bool ok = t < Tu;
+      const int fw0 = bd.t0 / a.H - a.J1;  // wave window (uniform)
+      const int tc = live ? t : ui.T - 1;
+      int roff;
+      if (ui.frames < a.Fmin) roff = a.tab_small + (a.H * ui.frames * (ui.frames - 1) / 2 + tc) * AUX_J4;
+      else if (tc < a.TL) roff = a.tab_left + tc * AUX_J4;
+      else if (tc >= ui.T - a.TR) roff = a.tab_right + (ui.T - 1 - tc) * AUX_J4;
+      else roff = (tc % a.H) * AUX_J4;
+      const int fb = t / a.H - a.J1;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        wt[j] = ok ? w0[j] : 0.f;
-        wt[j + 4] = ok ? w1[j] : 0.f;
-      }
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        if (s >= a.nka) break;
-        long long f = fw0 + 2 * s + hh;
-        f = f < 0 ? 0 : (f >= ud.frames ? ud.frames - 1 : f);  // out-of-range frames carry weight 0
-        const float* drow = a.d + (size_t)(ud.frame_base + f) * GR + cl;
+      for (int s = 0; s < 4; ++s) {
+        const int f = fw0 + 2 * s + hh;
+        const int j = f - fb;
+        const bool ok = live && j >= 0 && j < AUX_J4 && s < a.nka;
+        const float w = a.tab[roff + (j < 0 ? 0 : (j >= AUX_J4 ? AUX_J4 - 1 : j))];
+        bw[s] = ok ? w : 0.f;
+        const int fc = f < 0 ? 0 : (f >= ui.frames ? ui.frames - 1 : f);  // weight 0 outside
+        const float* drow = a.d + (size_t)(ui.frame_base + fc) * GR + cl;
 #pragma unroll
         for (int m = 0; m < MT; ++m) dv[s][m] = drow[32 * m];
       }
     }
 
+    // ---- GEMM 1. acc starts from the gate bias (k-step against a ones row, zero C), B operands
+    //      ping-pong between two register groups, the last group prefetching the next block's first
     f32x16 acc[MT];
+    {
+      const float one = hh == 0 ? 1.f : 0.f;
+      const f32x16 zero = {};
 #pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
-
-    // ---- GEMM 1: B prefetched one group ahead, across the block boundary for the last group
-    for (int g = 0; g < NGRP; ++g) {
-      const bvec bc = bn;
-      bn = *(g + 1 < NGRP ? bptr(xl, g + 1)
-                          : bptr(a.x_in + (size_t)(nblk < a.n_blocks ? col_n : col) * a.RS + GK * hh, 0));
-#pragma unroll
-      for (int sub = 0; sub < NB; ++sub) {
-        f32x4 av[MT];
-#pragma unroll
-        for (int m = 0; m < MT; ++m) av[m] = wgl[((g * NB + sub) * MT + m) * 64];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int m = 0; m < MT; ++m)
-            acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m][i], bc[4 * sub + i], acc[m], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
+      for (int m = 0; m < MT; ++m)
+        acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(hh == 0 ? s_bg[32 * m + cl] : 0.f, one, zero, 0, 0, 0);
+    }
+    for (int g = 0; g < NGRP; g += 2) {
+      const bvec b1 = bload(bd.col, g + 1 < NGRP ? g + 1 : g);
+      group_mfma(acc, b0, g);
+      if (g + 1 >= NGRP) {  // odd group count: b0 takes the next block's first group
+        b0 = bload(col_next, 0);
+        break;
       }
+      b0 = g + 2 < NGRP ? bload(bd.col, g + 2) : bload(col_next, 0);
+      group_mfma(acc, b1, g + 1);
     }
 
-    // ---- GEMM 2 in two passes of MP m-tiles (pass 0: skip rows, pass 1: residual rows for PWG v1),
-    //      accumulators initialised with [skip_old; x_in]: the MFMA performs the skip sum and the
-    //      residual add (residual_block.py:138, parallel_wavegan.py:164). Init loads are issued one
-    //      phase ahead (pass 0 before aux + gate, pass 1 before pass 0).
-    constexpr int NP = M2T >= 2 ? 2 : 1;
-    constexpr int MP = M2T / NP;
-    constexpr int NPASS = LAST ? 1 : NP;  // the last layer needs only the skip rows (S <= 32*MP)
+    // ---- GEMM 2 accumulators seeded with [skip_old; x_in]: the MFMA performs the skip sum and
+    //      the residual add (residual_block.py:138, parallel_wavegan.py:164); pass-0 loads in flight
+    //      during aux + gate, pass-1 loads during pass 0.
     auto init_pass = [&](int pass, f32x16 (&acc2)[MP]) {
 #pragma unroll
       for (int mm = 0; mm < MP; ++mm)
@@ -668,10 +704,10 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_persistent_kernel(const Laye
           const int rowu = 32 * (pass * MP + mm) + 8 * j4;  // S, R multiples of 8: wave-uniform branch
           const int row = rowu + 4 * hh;
           f32x4 v = {0.f, 0.f, 0.f, 0.f};
-          if (rowu < a.S) {
-            if (!a.first) v = *reinterpret_cast<const f32x4*>(a.skip + (size_t)col * a.SS + row);
-          } else if (rowu < a.S + a.R) {
-            v = *reinterpret_cast<const f32x4*>(a.x_in + (size_t)col * a.RS + (row - a.S));
+          if (rowu < S) {
+            if (!a.first) v = *reinterpret_cast<const f32x4*>(a.skip + (size_t)col * SS + row);
+          } else if (rowu < S + R) {
+            v = *reinterpret_cast<const f32x4*>(a.x_in + (size_t)col * RS + (row - S));
           }
 #pragma unroll
           for (int i = 0; i < 4; ++i) acc2[mm][4 * j4 + i] = v[i];
@@ -680,40 +716,25 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_persistent_kernel(const Laye
     f32x16 accp0[MP], accp1[MP];
     init_pass(0, accp0);
 
-    // ---- aux term + gate bias
-    {
-      const long long fb = t / H - a.tab.J1;
+    // ---- aux term: + sum_f D[f][row] * w_t[f - t/H + J1]
 #pragma unroll
-      for (int s = 0; s < 8; ++s) {
-        if (s >= a.nka) break;
-        const int j = (int)(fw0 + 2 * s + hh - fb);
-        float bw = 0.f;
+    for (int s = 0; s < 4; ++s) {
+      if (s >= a.nka) break;
 #pragma unroll
-        for (int q = 0; q < AUX_J4; ++q) bw = (j == q) ? wt[q] : bw;
-#pragma unroll
-        for (int m = 0; m < MT; ++m) acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(dv[s][m], bw, acc[m], 0, 0, 0);
-      }
-      const float one = hh == 0 ? 1.f : 0.f;
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
-        acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(hh == 0 ? s_bg[32 * m + cl] : 0.f, one, acc[m], 0, 0, 0);
+      for (int m = 0; m < MT; ++m) acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(dv[s][m], bw[s], acc[m], 0, 0, 0);
     }
 
-    // ---- gate
+    // ---- gate: tanh(Za) * sigmoid(Zb)  (residual_block.py:123-132)
     float gt[NG][16];
 #pragma unroll
     for (int gm = 0; gm < NG; ++gm)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         if (MT == 1 && r >= 8) { gt[gm][r] = 0.f; continue; }
-        const float za = acc[gm][r];
-        const float zb = MT == 1 ? acc[0][r + 8] : acc[gm + MT / 2][r];
-        gt[gm][r] = fast_tanh(za) * fast_sigmoid(zb);
+        gt[gm][r] = fast_gate(acc[gm][r], MT == 1 ? acc[0][r + 8] : acc[gm + MT / 2][r]);
       }
-
     if (NPASS > 1) init_pass(1, accp1);
 
-    const bool live = t < Tu;
     auto gemm2_pass = [&](int pass, f32x16 (&acc2)[MP]) {
 #pragma unroll
       for (int q4 = 0; q4 < NQ4; ++q4) {
@@ -728,8 +749,7 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_persistent_kernel(const Laye
             acc2[mm] = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[i], bq, acc2[mm], 0, 0, 0);
           }
         }
-        // keep the LDS fragment reads next to their MFMAs (hoisting them all costs ~140 VGPRs)
-        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_sched_barrier(0);  // keep LDS fragment reads next to their MFMAs
       }
     };
     auto store_pass = [&](int pass, const f32x16 (&acc2)[MP]) {
@@ -742,11 +762,12 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_persistent_kernel(const Laye
           f32x4 v;
 #pragma unroll
           for (int i = 0; i < 4; ++i) v[i] = acc2[mm][4 * j4 + i];
-          if (rowu < a.S) {
-            *reinterpret_cast<f32x4*>(a.skip + (size_t)col * a.SS + row) = v;
-          } else if (rowu < a.S + a.R) {
+          if (rowu < S) {
+            store_stream(a.skip + (size_t)bd.col * SS, (cl * SS + row) * 4, v);
+          } else if (rowu < S + R) {
             const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-            *reinterpret_cast<f32x4*>(a.x_out + (size_t)col * a.RS + (row - a.S)) = live ? v * 0.70710677f : z;
+            // padding columns stay zero: they are the next layers' right-edge zero pad
+            store_stream(a.x_out + (size_t)bd.col * RS, (cl * RS + row - S) * 4, live ? v * 0.70710677f : z);
           }
         }
     };
@@ -759,7 +780,10 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_persistent_kernel(const Laye
         store_pass(1, accp1);
       }
     } else {
-      // ---- last layer: fused output head on the final skip sum (skip rows all in pass 0)
+      // ---- last layer: fused output head (models/parallel_wavegan.py:131-138,166-171) on the
+      //      final skip sum: h1 = W1h . relu(skip * sqrt(1/L)) + b1h as a third MFMA GEMM whose B
+      //      operand is the skip tile in registers; y = W2h . relu(h1) + b2h as a per-lane dot
+      //      plus the partner lane half.
       constexpr int M3 = LAST ? M3T : 1;
       constexpr int NQH = 16 * M3;
       constexpr int NQH4 = SM::NQH4;
@@ -769,7 +793,7 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_persistent_kernel(const Laye
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int row = 32 * mm + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          hs[mm][r] = row < a.S ? fmaxf(accp0[mm][r] * a.skip_scale, 0.f) : 0.f;
+          hs[mm][r] = row < S ? fmaxf(accp0[mm][r] * a.skip_scale, 0.f) : 0.f;
         }
       f32x16 acc3[M3];
 #pragma unroll
@@ -791,7 +815,7 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_persistent_kernel(const Laye
           }
           __builtin_amdgcn_sched_barrier(0);
         }
-      float* out = a.out + ud.io_off * a.O + t * a.out_stride_t;
+      float* out = a.out + (size_t)ui.io_off * a.O + (size_t)t * a.out_stride_t;
       for (int oc = 0; oc < a.O; ++oc) {
         float part = 0.f;
 #pragma unroll
@@ -805,15 +829,13 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_persistent_kernel(const Laye
           }
         }
         const float y = part + __shfl_xor(part, 32) + a.hb2[oc];
-        if (hh == 0 && live) out[oc * a.out_stride_o] = y;
+        if (hh == 0 && live) out[(size_t)oc * a.out_stride_o] = y;
       }
     }
 
-    if (nblk >= a.n_blocks) break;
+    if (nblk >= blk_end) break;
     blk = nblk;
-    ud = ud_n;
-    t0w = t0w_n;
-    col = col_n;
+    bd = a.blocks[blk];
   }
 }
 
@@ -861,22 +883,30 @@ hipError_t launch_layer(const LayerArgs& a, int mt, int m2t, bool last, long lon
   return hipErrorInvalidValue;
 }
 
-hipError_t launch_layer_persistent(const LayerArgs& a, int mt, int m2t, bool last, int waves_per_wg, int n_wg,
+hipError_t launch_layer_persistent(const PersistArgs& a, int mt, int m2t, bool last, int waves_per_wg, int n_wg,
                                    hipStream_t s) {
+  if (waves_per_wg > 8) waves_per_wg = 8;
   const dim3 grid((unsigned)n_wg), block((unsigned)(64 * waves_per_wg));
   const int k1 = a.KS * a.RS;
   const int m3t = (a.S + 31) / 32;
   const bool gk16 = a.RS % 32 == 0;  // 32-channel groups when every tap block holds whole groups
-#define PWG_PERS_LAUNCH2(MT_, M2T_, M3T_, GK_)                                                             \
+#define PWG_PERS_LAUNCH3(MT_, M2T_, M3T_, GK_, RC_, SC_)                                                   \
   {                                                                                                        \
     const size_t lds = sizeof(float) * PersistSmem<MT_, M2T_, M3T_>::floats(k1);                           \
     if (lds > 160 * 1024) return hipErrorInvalidValue;                                                     \
-    auto kfn = &pwg_layer_persistent_kernel<MT_, M2T_, M3T_, GK_>;                                         \
+    auto kfn = &pwg_layer_persistent_kernel<MT_, M2T_, M3T_, GK_, RC_, SC_>;                               \
     hipError_t e_ = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),                                \
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);              \
     if (e_ != hipSuccess) return e_;                                                                       \
     hipLaunchKernelGGL(kfn, grid, block, lds, s, a);                                                       \
     return hipGetLastError();                                                                              \
+  }
+// PWG v1 (R = S = 64) gets compile-time channel counts; other shapes the runtime kernel.
+#define PWG_PERS_LAUNCH2(MT_, M2T_, M3T_, GK_)                                          \
+  {                                                                                     \
+    if (MT_ == 4 && M2T_ == 4 && a.R == 64 && a.S == 64)                                \
+      PWG_PERS_LAUNCH3(MT_, M2T_, M3T_, GK_, 64, 64)                                    \
+    else PWG_PERS_LAUNCH3(MT_, M2T_, M3T_, GK_, 0, 0)                                   \
   }
 #define PWG_PERS_LAUNCH(MT_, M2T_, M3T_) \
   { if (gk16) PWG_PERS_LAUNCH2(MT_, M2T_, M3T_, 16) else PWG_PERS_LAUNCH2(MT_, M2T_, M3T_, 8) }
@@ -894,6 +924,7 @@ hipError_t launch_layer_persistent(const LayerArgs& a, int mt, int m2t, bool las
 #undef PWG_PERS_CASE
 #undef PWG_PERS_LAUNCH
 #undef PWG_PERS_LAUNCH2
+#undef PWG_PERS_LAUNCH3
   return hipErrorInvalidValue;
 }
 
