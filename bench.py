@@ -172,6 +172,24 @@ def main():
     if not torch.isfinite(out).all():
         raise RuntimeError("non-finite generator output")
 
+    # PCIe-inclusive rate (never `value`): host mel + noise in pinned memory -> H2D -> forward ->
+    # D2H of the audio, like inference() called on host arrays (models/parallel_wavegan.py:244-263)
+    mel_h, noise_h = mel.cpu().pin_memory(), noise.cpu().pin_memory()
+    out_h = torch.empty(out.numel(), dtype=torch.float32).pin_memory()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        mel.copy_(mel_h, non_blocking=True)
+        noise.copy_(noise_h, non_blocking=True)
+        eng.run(plan, mel, noise, out)
+        out_h.copy_(out, non_blocking=True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    e2e = max_over_ranks(time.perf_counter() - t0, dev)
+
     samples_per_step = plan.total_samples * world
     value = samples_per_step * args.steps / elapsed
     per_gpu = value / world
@@ -179,12 +197,13 @@ def main():
     layer_avg_s = layer_ms / 1e3 / max(layer_n, 1)
     flops_launch = layer_flops_per_sample(params) * plan.total_samples
     achieved_tflops = flops_launch / layer_avg_s / 1e12
-    traffic = None
+    traffic = mfma_insts = None
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
             if tj.get("config") == args.config and tj.get("utts") == args.utts:
                 traffic = tj.get("hbm_bytes_per_launch")
+                mfma_insts = tj.get("mfma_insts_per_launch")
         except (OSError, ValueError):
             traffic = None
 
@@ -236,9 +255,15 @@ def main():
             "algorithmic_bytes_per_launch": int(layer_bytes_per_sample(params) * plan.total_samples),
             "avg_launch_ms": round(layer_avg_s * 1e3, 4),
             "launches_timed": layer_n,
+            # FLOPs the MFMAs actually execute (rocprofv3 SQ_INSTS_MFMA x 4096 per 32x32x2 f32 MFMA):
+            # below the reference count because the aux 1x1 runs at frame rate
+            "executed_flop_per_launch": mfma_insts and int(mfma_insts * 4096),
+            "executed_frac": mfma_insts and round(mfma_insts * 4096 / layer_avg_s / 1e12 / FP32_PEAK_TFLOPS, 4),
+            "hbm_GBs": traffic and round(traffic / layer_avg_s / 1e9, 1),
         },
         "model_flop_per_sample": round(model_flops_per_sample(params), 1),
         "model_tflops": round(value / world * model_flops_per_sample(params) / 1e12, 3),
+        "pcie_inclusive_value": round(samples_per_step * args.steps / e2e, 1),
         "cpu_baseline": cpu,
     }
     print(json.dumps(res), flush=True)

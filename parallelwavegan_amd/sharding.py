@@ -63,3 +63,50 @@ def sum_over_ranks(value, device=None):
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
+
+
+def shard_for_rank(lengths, rank, world):
+    """Utterance indices this rank decodes (LPT over frame counts, identical on every rank)."""
+    if not 0 <= rank < world:
+        raise ValueError(f"rank {rank} outside world of {world}")
+    return lpt_partition(lengths, world)[rank]
+
+
+def decode_sharded(lengths, decode_fn, rank=None, world=None):
+    """Decode this rank's share of a fixed utterance list.
+
+    ``decode_fn(indices) -> list of per-utterance outputs`` runs the local batch (on a GPU rank:
+    ``Engine.infer`` over the selected mels/noises, one ragged plan). Returns {index: output} for
+    this rank's utterances only; no data-path collective is involved."""
+    if rank is None or world is None:
+        init = dist.is_available() and dist.is_initialized()
+        rank = dist.get_rank() if init else 0
+        world = dist.get_world_size() if init else 1
+    mine = shard_for_rank(lengths, rank, world)
+    outs = decode_fn(mine) if mine else []
+    if len(outs) != len(mine):
+        raise RuntimeError(f"decode_fn returned {len(outs)} outputs for {len(mine)} utterances")
+    return dict(zip(mine, outs))
+
+
+def gather_outputs(local, n_utts, dst=0):
+    """Collect every rank's {index: output} on ``dst`` as a list in utterance order (host
+    objects, e.g. CPU tensors / arrays). Other ranks get None. Off the timed path: the reference's
+    decode writes each utterance to disk from the process that produced it (bin/decode.py:262-266),
+    so this exists for callers that want one list."""
+    if not dist.is_available() or not dist.is_initialized():
+        return [local[i] for i in range(n_utts)]
+    world = dist.get_world_size()
+    parts = [None] * world if dist.get_rank() == dst else None
+    dist.gather_object(local, parts, dst=dst)
+    if dist.get_rank() != dst:
+        return None
+    merged = {}
+    for p in parts:
+        overlap = merged.keys() & p.keys()
+        if overlap:
+            raise RuntimeError(f"utterances decoded twice: {sorted(overlap)[:5]}")
+        merged.update(p)
+    if len(merged) != n_utts:
+        raise RuntimeError(f"gathered {len(merged)} of {n_utts} utterances")
+    return [merged[i] for i in range(n_utts)]

@@ -17,6 +17,7 @@ def main(summary, out, config="libritts_v1", utts=32):
         "fetch_bytes_per_launch": v["FETCH_BYTES_corrected"],
         "write_bytes_per_launch": v["WRITE_BYTES"],
         "hbm_bytes_per_launch": v["FETCH_BYTES_corrected"] + v["WRITE_BYTES"],
+        "mfma_insts_per_launch": v["SQ_INSTS_MFMA"],
         "mfma_busy": v["SQ_VALU_MFMA_BUSY_CYCLES"] / (v["GRBM_GUI_ACTIVE"] / 8 * 1024),
         "l2_hit": v["TCC_HIT_sum"] / (v["TCC_HIT_sum"] + v["TCC_MISS_sum"]),
         "source": summary,
