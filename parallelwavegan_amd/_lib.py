@@ -97,7 +97,7 @@ def build(force=False, verbose=False, extra_flags=(), out_path=None):
     """Compile the HIP kernels + C-ABI into parallelwavegan_amd/lib/libpwg_hip.so (gfx950).
     extra_flags/out_path build A/B measurement variants (e.g. -DPWG_STORE_SC1=0) elsewhere."""
     target = out_path or LIB_PATH
-    if not force and out_path is None and not _needs_build():
+    if not force and out_path is None and (os.environ.get("PWG_NO_BUILD") == "1" or not _needs_build()):
         return LIB_PATH
     os.makedirs(os.path.dirname(target), exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -111,6 +111,10 @@ def build(force=False, verbose=False, extra_flags=(), out_path=None):
         "-shared",
         "-fvisibility=hidden",
         "-mcode-object-version=5",
+        # keep the work-queue atomic a plain per-lane op: the optimizer's wave-reduction form
+        # waits for the returned value right after issue, which defeats the claim-ahead
+        "-mllvm",
+        "-amdgpu-atomic-optimizer-strategy=None",
         "-Wall",
         "-o",
         tmp,

@@ -4,6 +4,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -277,9 +279,8 @@ struct PwgPlan {
   int* d_tile_utt = nullptr;
   long long* d_gap_col0 = nullptr;
   BlockDesc* d_blocks = nullptr;
-  UttInfo* d_uttinfo = nullptr;
   // workspace offsets (bytes)
-  size_t ws_x0, ws_x1, ws_skip, ws_c1, ws_d, ws_total;
+  size_t ws_x0, ws_x1, ws_skip, ws_c1, ws_d, ws_ctr, ws_total;
 };
 
 extern "C" {
@@ -612,7 +613,6 @@ int pwg_plan_create(PwgHandle* h, int n_utts, const long long* frames, int layou
   }
   std::vector<int> tile_utt(p->n_tiles);
   std::vector<BlockDesc> blocks((size_t)p->n_tiles * (TILE / 32));
-  std::vector<UttInfo> uinfo(n_utts);
   for (int u = 0; u < n_utts; ++u) {
     const UttDesc& d = p->utts[u];
     const long long n = (d.T + TILE - 1) / TILE;
@@ -622,14 +622,14 @@ int pwg_plan_create(PwgHandle* h, int n_utts, const long long* frames, int layou
         BlockDesc& bd = blocks[(size_t)(d.first_tile + t) * (TILE / 32) + b];
         bd.t0 = (int)(t * TILE + 32 * b);
         bd.col = (int)(d.seg_base + bd.t0);
+        bd.T = (int)d.T;
+        bd.frames = (int)d.frames;
+        bd.frame_base = (int)d.frame_base;
+        bd.io_off = (int)d.io_off;
         bd.utt = u;
         bd.pad = 0;
       }
     }
-    uinfo[u].T = (int)d.T;
-    uinfo[u].frames = (int)d.frames;
-    uinfo[u].frame_base = (int)d.frame_base;
-    uinfo[u].io_off = (int)d.io_off;
   }
   size_t o = 0;
   p->ws_x0 = o; o += align_bytes(sizeof(float) * h->RS * p->Tpad);
@@ -637,6 +637,7 @@ int pwg_plan_create(PwgHandle* h, int n_utts, const long long* frames, int layou
   p->ws_skip = o; o += align_bytes(sizeof(float) * h->SS * p->Tpad);
   p->ws_c1 = o; o += align_bytes(sizeof(float) * h->A * p->F_total);
   p->ws_d = o; o += align_bytes(sizeof(float) * h->L * h->GR * p->F_total);
+  p->ws_ctr = o; o += align_bytes(sizeof(int) * h->L * SCHED_CTR_STRIDE * 8);
   p->ws_total = o;
 
   DeviceGuard g(h->device);
@@ -647,11 +648,8 @@ int pwg_plan_create(PwgHandle* h, int n_utts, const long long* frames, int layou
   if (e == hipSuccess && p->n_gap_tiles > 0)
     e = hipMemcpy(p->d_gap_col0, gap_col0.data(), sizeof(long long) * p->n_gap_tiles, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMalloc(&p->d_blocks, sizeof(BlockDesc) * blocks.size());
-  if (e == hipSuccess) e = hipMalloc(&p->d_uttinfo, sizeof(UttInfo) * uinfo.size());
   if (e == hipSuccess)
     e = hipMemcpy(p->d_blocks, blocks.data(), sizeof(BlockDesc) * blocks.size(), hipMemcpyHostToDevice);
-  if (e == hipSuccess)
-    e = hipMemcpy(p->d_uttinfo, uinfo.data(), sizeof(UttInfo) * uinfo.size(), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(p->d_utts, p->utts.data(), sizeof(UttDesc) * n_utts, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(p->d_tile_utt, tile_utt.data(), sizeof(int) * p->n_tiles, hipMemcpyHostToDevice);
   if (e != hipSuccess) {
@@ -671,7 +669,6 @@ void pwg_plan_destroy(PwgPlan* p) {
     if (p->d_tile_utt) (void)hipFree(p->d_tile_utt);
     if (p->d_gap_col0) (void)hipFree(p->d_gap_col0);
     if (p->d_blocks) (void)hipFree(p->d_blocks);
-    if (p->d_uttinfo) (void)hipFree(p->d_uttinfo);
   }
   delete p;
 }
@@ -714,6 +711,7 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
   float* skip = (float*)(ws + p->ws_skip);
   float* c1 = (float*)(ws + p->ws_c1);
   float* dproj = (float*)(ws + p->ws_d);
+  int* sched_ctr = (int*)(ws + p->ws_ctr);
 
   auto timed = [&](int bucket, auto&& launch) -> hipError_t {
     if (!h->timing) return launch();
@@ -728,7 +726,8 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
     return e;
   };
 
-  hipError_t e;
+  hipError_t e = hipMemsetAsync(sched_ctr, 0, sizeof(int) * h->L * SCHED_CTR_STRIDE * 8, s);
+  if (e != hipSuccess) return hip_fail(e, "work-queue reset");
   ConvInArgs ca;
   ca.mel = mel; ca.mean = mean; ca.scale = scale; ca.w = packed + h->off_conv_in; ca.c1 = c1;
   ca.utts = p->d_utts; ca.n_utts = p->n_utts; ca.F_total = p->F_total; ca.A = h->A; ca.KW = h->KW;
@@ -777,7 +776,7 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
       pa2.tab_left = (int)(h->off_tab_left - h->off_tab_interior);
       pa2.tab_right = (int)(h->off_tab_right - h->off_tab_interior);
       pa2.tab_small = (int)(h->off_tab_small - h->off_tab_interior);
-      pa2.blocks = p->d_blocks; pa2.utts = p->d_uttinfo;
+      pa2.blocks = p->d_blocks;
       pa2.wgp = la.wgp; pa2.w2 = la.w2; pa2.bg = la.bg;
       pa2.hw1 = la.hw1; pa2.hw2 = la.hw2; pa2.hb2 = la.hb2; pa2.out = out;
       pa2.H = (int)h->aux.H; pa2.J1 = h->aux.J1; pa2.TL = h->aux.TL; pa2.TR = h->aux.TR;
@@ -788,6 +787,41 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
       pa2.out_stride_t = (int)la.out_stride_t; pa2.out_stride_o = (int)la.out_stride_o;
       pa2.skip_scale = la.skip_scale;
       const int nwg = h->n_cu * h->wg_per_cu;
+      pa2.trace = nullptr;
+      pa2.ctr = sched_ctr + (size_t)l * SCHED_CTR_STRIDE * 8;
+#if PWG_TRACE
+      // diagnostic build: every layer's per-wave records, dumped after the run (PWG_TRACE_FILE)
+      static unsigned long long* d_trace = nullptr;
+      const size_t per_layer = (size_t)nwg * 8 * 8;
+      if (!d_trace && hipMalloc((void**)&d_trace, per_layer * 64 * sizeof(unsigned long long)) != hipSuccess)
+        return fail(PWG_ERR_HIP, "trace buffer");
+      pa2.trace = d_trace + per_layer * (l % 64);
+      if (last) {
+        const int wpw = h->waves_per_wg;
+        auto kick = [=, &e]() {
+          std::vector<unsigned long long> host(per_layer * h->L);
+          e = hipStreamSynchronize(s);
+          if (e == hipSuccess) e = hipMemcpy(host.data(), d_trace, host.size() * 8, hipMemcpyDeviceToHost);
+          const char* fn = getenv("PWG_TRACE_FILE");
+          if (e == hipSuccess && fn) {
+            FILE* f = fopen(fn, "wb");
+            if (f) {
+              const long long hdr[4] = {h->L, nwg, wpw, 8};
+              fwrite(hdr, sizeof(hdr), 1, f);
+              fwrite(host.data(), 8, host.size(), f);
+              fclose(f);
+            }
+          }
+        };
+        e = timed(PWG_KERNEL_RESIDUAL_LAYER, [&] {
+          return launch_layer_persistent(pa2, h->MT, h->M2T, last, h->waves_per_wg, nwg, s);
+        });
+        if (e == hipSuccess) kick();
+        if (e != hipSuccess) return hip_fail(e, "residual layer launch (trace)");
+        std::swap(xin, xout);
+        continue;
+      }
+#endif
       e = timed(PWG_KERNEL_RESIDUAL_LAYER, [&] {
         return launch_layer_persistent(pa2, h->MT, h->M2T, last, h->waves_per_wg, nwg, s);
       });

@@ -118,19 +118,18 @@ struct LayerArgs {
   float skip_scale;
 };
 
-// Compact descriptors for the persistent layer kernel (32-bit: the plan guarantees every column
-// and frame index fits). BlockDesc: one 32-sample block; UttInfo: one utterance.
+// Descriptor of one 32-sample block for the persistent layer kernel, with its utterance's fields
+// folded in so a wave fetches everything about its next block in ONE 32-byte load issued a whole
+// block ahead (32-bit: the plan guarantees every column and frame index fits).
 struct BlockDesc {
-  int col;    // global column (padded time axis) of the block's first sample
-  int t0;     // utterance-local index of the block's first sample
+  int col;         // global column (padded time axis) of the block's first sample
+  int t0;          // utterance-local index of the block's first sample
+  int T;           // the utterance's samples
+  int frames;      // its T'
+  int frame_base;  // its first frame in C1 / D
+  int io_off;      // its first sample in the caller's noise/output arrays
   int utt;
   int pad;
-};
-struct UttInfo {
-  int T;           // samples
-  int frames;      // T'
-  int frame_base;  // first frame in C1 / D
-  int io_off;      // first sample in the caller's noise/output arrays
 };
 
 // Slim argument block of the persistent layer kernel (fewer live scalars than LayerArgs).
@@ -141,7 +140,6 @@ struct PersistArgs {
   const float* d;        // this layer's aux projection [F_total][GR]
   const float* tab;      // AuxTab base; the four tables at 32-bit offsets below
   const BlockDesc* blocks;
-  const UttInfo* utts;
   const float* wgp;      // [K1/4][MT][64][4]
   const float* w2;       // [NQ4][M2T][64][4]
   const float* bg;       // [GR]
@@ -155,7 +153,12 @@ struct PersistArgs {
   int R, RS, S, SS, KS, dil, tap_center, first, O;
   int out_stride_t, out_stride_o;
   float skip_scale;
+  int* ctr;                   // this layer's 8 per-XCD work-queue heads, SCHED_CTR_STRIDE ints apart (zeroed per run)
+  unsigned long long* trace;  // PWG_TRACE builds only: per-wave timestamps (tools/trace_layer.py)
 };
+
+// Persistent-kernel work queues: one head per XCD, each on its own 128-byte line.
+constexpr int SCHED_CTR_STRIDE = 32;
 
 // Kernel launchers (pwg_kernels.hip).
 hipError_t launch_conv_in(const ConvInArgs& a, hipStream_t s);

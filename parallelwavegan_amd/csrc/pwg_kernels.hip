@@ -597,14 +597,42 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_persistent_kernel(const Pers
   const int hh = lane >> 5;
   const int cl = lane & 31;
   const int nw = blockDim.x >> 6;
-  // XCD-aware static schedule (speed only, never correctness): workgroups are dealt round-robin
-  // over the 8 XCDs, so workgroup i runs on XCD i % 8; XCD x sweeps the x-th contiguous eighth of
-  // the blocks with all its waves side by side, so the dilated taps of a block re-read rows that
-  // neighbouring waves of the same XCD just loaded (its 4 MB L2) instead of HBM.
+  // XCD-local work queues (speed only, never correctness): workgroups are dealt round-robin over
+  // the 8 XCDs, so workgroup i runs on XCD i % 8. XCD x owns the x-th contiguous eighth of the
+  // blocks; its waves take rounds 0 and 1 statically and then claim blocks in order from the XCD's
+  // queue head, so all waves of an XCD sweep its range side by side and the dilated taps of a block
+  // re-read rows that neighbouring waves just loaded into the same 4 MB L2. Dynamic claiming
+  // balances the two waves sharing a SIMD (arbitration makes one of them up to 30 % slower) and
+  // the XCDs (a wave whose own range is drained steals from the next XCDs' queues). Claims run two
+  // blocks ahead so the atomic's latency hides behind a whole block.
   const int xcd = blockIdx.x & 7;
-  const int nwg_x = ((int)gridDim.x - xcd + 7) >> 3;
-  const int stride = nwg_x * nw;
-  const int blk_end = (int)((long long)a.n_blocks * (xcd + 1) / 8);
+  const int wave = threadIdx.x >> 6;
+  auto xcd_waves = [&](int y) { return (((int)gridDim.x - y + 7) >> 3) * nw; };
+  auto xcd_first = [&](int y) { return (int)((long long)a.n_blocks * y / 8); };
+  const int x_first = xcd_first(xcd), x_end = xcd_first(xcd + 1), x_waves = xcd_waves(xcd);
+  int victim = 0;  // XCD offset being claimed from: 0 = own queue
+  auto ticket_issue = [&]() -> int {  // non-blocking claim on the own queue (lane 0's value)
+    int v = 0;
+    if (victim == 0 && lane == 0)
+      v = __hip_atomic_fetch_add(a.ctr + xcd * SCHED_CTR_STRIDE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return v;
+  };
+  auto ticket_resolve = [&](int v) -> int {  // block index of an issued ticket, or steal, or -1
+    if (victim == 0) {
+      const int i = x_first + 2 * x_waves + __builtin_amdgcn_readfirstlane(v);
+      if (i < x_end) return i;
+      victim = 1;
+    }
+    for (; victim < 8; ++victim) {
+      const int y = (xcd + victim) & 7;
+      int tk = 0;
+      if (lane == 0)
+        tk = __hip_atomic_fetch_add(a.ctr + y * SCHED_CTR_STRIDE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int i = xcd_first(y) + 2 * xcd_waves(y) + __builtin_amdgcn_readfirstlane(tk);
+      if (i < xcd_first(y + 1)) return i;
+    }
+    return -1;
+  };
   const int gpt = RS / (2 * GK);  // groups per tap
   const f32x4* wgl = reinterpret_cast<const f32x4*>(s_wg) + lane;
   const f32x4* w2l = reinterpret_cast<const f32x4*>(s_w2) + lane;
@@ -632,18 +660,43 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_persistent_kernel(const Pers
     }
   };
 
-  int blk = (int)((long long)a.n_blocks * xcd / 8) + (blockIdx.x >> 3) * nw + (threadIdx.x >> 6);
-  if (blk >= blk_end) return;
-  BlockDesc bd = a.blocks[blk];
-  bvec b0 = bload(bd.col, 0);  // B operand of the next group (prefetched, across blocks)
+  int blk = x_first + (blockIdx.x >> 3) * nw + wave;  // static round 0
+  int nblk = blk + x_waves;                           // static round 1
+  if (blk >= x_end) blk = -1;
+  if (nblk >= x_end) nblk = -1;
+#if PWG_SETPRIO
+  if (wave >= nw / 2) __builtin_amdgcn_s_setprio(1);  // younger half wins arbitration
+#endif
+#if PWG_TRACE
+  // diagnostic build: [start_rt, end_rt, blocks, gemm1_cyc, gate_cyc, gemm2_cyc, start_clk, end_clk]
+  unsigned long long* trw = a.trace + ((size_t)blockIdx.x * nw + wave) * 8;
+  const unsigned long long tr_rt0 = wall_clock64(), tr_c0 = clock64();
+  unsigned long long tr_g1 = 0, tr_gt = 0, tr_g2 = 0, tr_n = 0;
+  auto tr_done = [&] {
+    if (lane == 0) {
+      trw[0] = tr_rt0; trw[1] = wall_clock64(); trw[2] = tr_n; trw[3] = tr_g1; trw[4] = tr_gt;
+      trw[5] = tr_g2; trw[6] = tr_c0; trw[7] = clock64();
+    }
+  };
+#define PWG_TR(x) x
+#else
+#define PWG_TR(x)
+#endif
+  if (blk < 0) {
+    PWG_TR(tr_done());
+    return;
+  }
+  BlockDesc bdn = a.blocks[blk];  // descriptor of the block processed next (loaded a block ahead)
+  bvec b0 = bload(bdn.col, 0);     // B operand of the next group (prefetched, across blocks)
 
   while (true) {
-    const UttInfo ui = a.utts[bd.utt];
+    const BlockDesc bd = bdn;
+    bdn = a.blocks[nblk >= 0 ? nblk : blk];  // unconditional: a branch here would force a wait
+    const BlockDesc& ui = bd;
     const int col = bd.col + cl;  // this lane's column
     const int t = bd.t0 + cl;     // this lane's utterance-local sample
     const bool live = t < ui.T;
-    const int nblk = blk + stride;
-    const int col_next = nblk < blk_end ? a.blocks[nblk].col : bd.col;
+    const int col_next = nblk >= 0 ? bdn.col : bd.col;
 
     // aux inputs, in flight during GEMM 1: B weights bw[s] = w_t[f - t/H + J1] of frame
     // f = fw0 + 2s + h (a table load per k-step), A = D rows of those frames
@@ -672,27 +725,6 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_persistent_kernel(const Pers
       }
     }
 
-    // ---- GEMM 1. acc starts from the gate bias (k-step against a ones row, zero C), B operands
-    //      ping-pong between two register groups, the last group prefetching the next block's first
-    f32x16 acc[MT];
-    {
-      const float one = hh == 0 ? 1.f : 0.f;
-      const f32x16 zero = {};
-#pragma unroll
-      for (int m = 0; m < MT; ++m)
-        acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(hh == 0 ? s_bg[32 * m + cl] : 0.f, one, zero, 0, 0, 0);
-    }
-    for (int g = 0; g < NGRP; g += 2) {
-      const bvec b1 = bload(bd.col, g + 1 < NGRP ? g + 1 : g);
-      group_mfma(acc, b0, g);
-      if (g + 1 >= NGRP) {  // odd group count: b0 takes the next block's first group
-        b0 = bload(col_next, 0);
-        break;
-      }
-      b0 = g + 2 < NGRP ? bload(bd.col, g + 2) : bload(col_next, 0);
-      group_mfma(acc, b1, g + 1);
-    }
-
     // ---- GEMM 2 accumulators seeded with [skip_old; x_in]: the MFMA performs the skip sum and
     //      the residual add (residual_block.py:138, parallel_wavegan.py:164); pass-0 loads in flight
     //      during aux + gate, pass-1 loads during pass 0.
@@ -705,7 +737,9 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_persistent_kernel(const Pers
           const int row = rowu + 4 * hh;
           f32x4 v = {0.f, 0.f, 0.f, 0.f};
           if (rowu < S) {
-            if (!a.first) v = *reinterpret_cast<const f32x4*>(a.skip + (size_t)col * SS + row);
+            // unconditional load + select: a branch around the load would make its join wait for it
+            v = *reinterpret_cast<const f32x4*>(a.skip + (size_t)col * SS + row);
+            if (a.first) v = f32x4{0.f, 0.f, 0.f, 0.f};  // layer 0: no skip sum yet (buffer unset)
           } else if (rowu < S + R) {
             v = *reinterpret_cast<const f32x4*>(a.x_in + (size_t)col * RS + (row - S));
           }
@@ -713,8 +747,41 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_persistent_kernel(const Pers
           for (int i = 0; i < 4; ++i) acc2[mm][4 * j4 + i] = v[i];
         }
     };
+    PWG_TR(const unsigned long long tr_a = clock64());
+    int ticket = 0;  // claim for the block after next, issued once GEMM 1's loads are out
     f32x16 accp0[MP], accp1[MP];
+#if PWG_EARLY_SKIP
+    init_pass(0, accp0);  // skip_old rows stream from HBM: issue them before GEMM 1
+#endif
+    // ---- GEMM 1. acc starts from the gate bias (k-step against a ones row, zero C), B operands
+    //      ping-pong between two register groups, the last group prefetching the next block's first
+    f32x16 acc[MT];
+    {
+      const float one = hh == 0 ? 1.f : 0.f;
+      const f32x16 zero = {};
+      float bgv[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) bgv[m] = s_bg[32 * m + cl];  // all reads in flight, one wait
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(hh == 0 ? bgv[m] : 0.f, one, zero, 0, 0, 0);
+    }
+    for (int g = 0; g < NGRP; g += 2) {
+      const bvec b1 = bload(bd.col, g + 1 < NGRP ? g + 1 : g);
+      group_mfma(acc, b0, g);
+      if (g + 1 >= NGRP) {  // odd group count: b0 takes the next block's first group
+        b0 = bload(col_next, 0);
+        break;
+      }
+      b0 = g + 2 < NGRP ? bload(bd.col, g + 2) : bload(col_next, 0);
+      group_mfma(acc, b1, g + 1);
+    }
+
+    PWG_TR(const unsigned long long tr_b = clock64());
+#if !PWG_EARLY_SKIP
     init_pass(0, accp0);
+#endif
+    if (nblk >= 0) ticket = ticket_issue();
 
     // ---- aux term: + sum_f D[f][row] * w_t[f - t/H + J1]
 #pragma unroll
@@ -734,6 +801,7 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_persistent_kernel(const Pers
         gt[gm][r] = fast_gate(acc[gm][r], MT == 1 ? acc[0][r + 8] : acc[gm + MT / 2][r]);
       }
     if (NPASS > 1) init_pass(1, accp1);
+    PWG_TR(const unsigned long long tr_c = clock64());
 
     auto gemm2_pass = [&](int pass, f32x16 (&acc2)[MP]) {
 #pragma unroll
@@ -833,10 +901,14 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_persistent_kernel(const Pers
       }
     }
 
-    if (nblk >= blk_end) break;
+    PWG_TR(const unsigned long long tr_d = clock64(); tr_g1 += tr_b - tr_a; tr_gt += tr_c - tr_b;
+           tr_g2 += tr_d - tr_c; ++tr_n);
+    if (nblk < 0) break;
     blk = nblk;
-    bd = a.blocks[blk];
+    nblk = ticket_resolve(ticket);
   }
+  PWG_TR(tr_done());
+#undef PWG_TR
 }
 
 // ---------------------------------------------------------------------------------------------
