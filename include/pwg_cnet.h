@@ -1,0 +1,103 @@
+/*
+ * pwg_cnet.h — C-ABI of the MI355X conv-network executor behind the MelGAN-family drop-ins
+ * (MelGANGenerator incl. multi-band + PQMF synthesis, HiFiGANGenerator).
+ *
+ * The reference builds these generators as torch.nn.Sequential / ModuleList stacks of
+ * Conv1d, ConvTranspose1d, LeakyReLU, ReflectionPad1d, Tanh and residual sums
+ * (parallel_wavegan/models/melgan.py:17-257, layers/residual_stack.py:13-85,
+ *  models/hifigan.py:23-265, layers/residual_block.py:143-258, layers/pqmf.py:51-149).
+ * Here a generator is a PROGRAM of fused conv ops that the Python drop-in builds from its
+ * constructor arguments (parallelwavegan_amd/melgan.py, hifigan.py); this library packs the
+ * weights for the MFMA kernels, plans ragged utterance batches and runs the program on the
+ * caller's HIP stream. Every op is one launch of a generic fp32 MFMA implicit-GEMM kernel:
+ *
+ *   y[o, t] = post( ( sum_src sum_{i<C_src, k<K_src} W_src[o, i, k] *
+ *                     pre_src( x_src[i, t - pad_src + k * dil_src] ) + b[o] + b2[o]
+ *                     + res[o, t] + (accumulate ? y_old[o, t] : 0) ) / out_div )
+ *
+ * pre = optional (x - mean)/scale (first op) then LeakyReLU(pre_slope) (slope 1 = identity);
+ * taps outside an utterance read zeros (PWG_PAD_ZERO, Conv1d padding=) or the mirrored sample
+ * (PWG_PAD_REFLECT, ReflectionPad1d); post = none | LeakyReLU | tanh.
+ * PWG_CNET_CONVT is ConvTranspose1d(kernel 2*stride): split into `stride` output phases, each a
+ * 2-tap conv of the input (models/melgan.py:86-100, models/hifigan.py:96-107).
+ * PWG_CNET_PQMF is PQMF.synthesis (layers/pqmf.py:133-149) with host-supplied filters.
+ *
+ * Buffers are time-major [rows][ld] fp32 (ld = channels rounded up to 16); buffer b of a plan
+ * holds frames[u] * rate[b] rows per utterance u, utterances back to back. Buffer 0 is the input
+ * (mel frames-major, exactly inference()'s c), the op writing the last buffer makes the output.
+ *
+ * Errors: int status codes as in pwg.h (pwg_last_error() gives the message).
+ */
+#ifndef PWG_CNET_H_
+#define PWG_CNET_H_
+
+#include "pwg.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PWG_CNET_ABI_VERSION 1
+
+enum { PWG_CNET_CONV = 0, PWG_CNET_CONVT = 1, PWG_CNET_PQMF = 2 };
+enum { PWG_PAD_ZERO = 0, PWG_PAD_REFLECT = 1 };
+enum { PWG_ACT_NONE = 0, PWG_ACT_LRELU = 1, PWG_ACT_TANH = 2 };
+
+typedef struct PwgCnetSrc {
+  int buf;          /* buffer id; -1 = source unused */
+  int channels;     /* input channels (C_src) */
+  int taps;         /* kernel size K_src */
+  int dilation;
+  int pad;          /* tap k reads row t - pad + k*dilation */
+  int pad_mode;     /* PWG_PAD_* */
+  int normalize;    /* apply (x - mean) / scale from pwg_cnet_run (inference normalize_before) */
+  float pre_slope;  /* LeakyReLU negative slope applied on load; 1.0 = identity */
+  long long w_off;  /* floats into the reference-order weights: Conv1d (out, C_src, K_src);
+                       CONVT: ConvTranspose1d (C_src, out, 2*stride) */
+} PwgCnetSrc;
+
+typedef struct PwgCnetOp {
+  int kind;           /* PWG_CNET_* */
+  int dst;            /* output buffer id */
+  int out_channels;
+  PwgCnetSrc src[2];  /* CONVT and PQMF use src[0] only */
+  long long b_off;    /* bias (out_channels floats) or -1 */
+  long long b2_off;   /* second bias summed with the first (two-source ops) or -1 */
+  int res;            /* buffer added after the bias, -1 = none */
+  int accumulate;     /* add the destination's previous value */
+  float out_div;      /* result divided by this (1.0 = none) */
+  int post_act;       /* PWG_ACT_* */
+  float post_slope;
+  int stride;         /* CONVT: stride (rate[dst] = stride * rate[src]); PQMF: subbands */
+  int padding;        /* CONVT: padding; PQMF: filter taps (odd, = taps+1 of PQMF) */
+  int output_padding; /* CONVT */
+} PwgCnetOp;
+
+typedef struct PwgCnet PwgCnet;
+typedef struct PwgCnetPlan PwgCnetPlan;
+
+PWG_API int pwg_cnet_abi_version(void);
+/* n_bufs buffers with `channels[b]` channels and `rate[b]` rows per input frame. */
+PWG_API int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* channels, const int* rate,
+                    long long ref_weight_count, int device, PwgCnet** out);
+PWG_API void pwg_cnet_destroy(PwgCnet* n);
+PWG_API long long pwg_cnet_packed_weight_count(const PwgCnet* n);
+/* Host -> host packing of the reference-order weight vector into the kernel image. */
+PWG_API int pwg_cnet_pack_weights(const PwgCnet* n, const float* ref_host, float* packed_host);
+PWG_API int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCnetPlan** out);
+PWG_API void pwg_cnet_plan_destroy(PwgCnetPlan* p);
+PWG_API long long pwg_cnet_plan_rows(const PwgCnetPlan* p, int buf); /* sum_u frames[u]*rate[buf] */
+PWG_API long long pwg_cnet_plan_workspace_bytes(const PwgCnetPlan* p);
+/* mel: buffer 0 contents (device, rows x channels[0], frames-major = time-major);
+ * out: the last buffer's first channels[last] channels, time-major (device);
+ * mean/scale: device or NULL (ops with normalize=1 need them). */
+PWG_API int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const float* mean,
+                 const float* scale, float* out, void* workspace, void* stream);
+PWG_API int pwg_cnet_set_timing(PwgCnet* n, int enable);
+/* Adds per-op milliseconds and launch counts (arrays of n_ops) and clears the records. */
+PWG_API int pwg_cnet_timing_collect(PwgCnet* n, double* ms, long long* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PWG_CNET_H_ */

@@ -21,9 +21,11 @@ LIB_PATH = os.environ.get("PWG_LIB_PATH") or os.path.join(LIB_DIR, "libpwg_hip.s
 CSRC = [
     os.path.join(PKG_DIR, "csrc", "pwg_kernels.hip"),
     os.path.join(PKG_DIR, "csrc", "pwg_capi.hip"),
+    os.path.join(PKG_DIR, "csrc", "pwg_cnet.hip"),
 ]
 HEADERS = [
     os.path.join(REPO_DIR, "include", "pwg.h"),
+    os.path.join(REPO_DIR, "include", "pwg_cnet.h"),
     os.path.join(PKG_DIR, "csrc", "pwg_internal.h"),
 ]
 OFFLOAD_ARCH = "gfx950"
@@ -40,7 +42,7 @@ PWG_LAYOUT_FORWARD = 1
 KERNEL_BUCKETS = ("conv_in", "upsample", "first_conv", "residual_layer", "head")
 PWG_MAX_SCALES = 8
 
-# Every symbol include/pwg.h declares (checked by tests/test_abi.py).
+# Every symbol include/*.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = (
     "pwg_abi_version",
     "pwg_last_error",
@@ -60,6 +62,19 @@ EXPORTED_SYMBOLS = (
     "pwg_set_option",
     "pwg_set_timing",
     "pwg_timing_collect",
+    # include/pwg_cnet.h: conv-network executor (MelGAN family)
+    "pwg_cnet_abi_version",
+    "pwg_cnet_create",
+    "pwg_cnet_destroy",
+    "pwg_cnet_packed_weight_count",
+    "pwg_cnet_pack_weights",
+    "pwg_cnet_plan_create",
+    "pwg_cnet_plan_destroy",
+    "pwg_cnet_plan_rows",
+    "pwg_cnet_plan_workspace_bytes",
+    "pwg_cnet_run",
+    "pwg_cnet_set_timing",
+    "pwg_cnet_timing_collect",
 )
 
 PWG_OPT_LAYER_KERNEL = 0

@@ -1,0 +1,334 @@
+"""ctypes binding of the conv-network executor (include/pwg_cnet.h) and the program builder the
+MelGAN-family drop-ins use.
+
+A ``Program`` is a list of fused conv ops over numbered time-major buffers (buffer 0 = the mel
+input, the last buffer = the output) plus the reference-order flat weight layout: every op names
+its weights by state-dict key, and ``CnetEngine.pack`` flattens a (weight-norm folded) state dict
+in that order before the library packs it into MFMA fragments. Nothing here computes: the forward
+runs in libpwg_hip.so, and a missing library or a CPU device raises.
+"""
+
+import ctypes
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from . import _lib
+from .engine import fold_weight_norm
+
+CONV, CONVT, PQMF = 0, 1, 2
+PAD_ZERO, PAD_REFLECT = 0, 1
+ACT_NONE, ACT_LRELU, ACT_TANH = 0, 1, 2
+
+CNET_SYMBOLS = tuple(n for n in _lib.EXPORTED_SYMBOLS if n.startswith("pwg_cnet_"))
+
+
+class PwgCnetSrc(ctypes.Structure):
+    _fields_ = [
+        ("buf", ctypes.c_int),
+        ("channels", ctypes.c_int),
+        ("taps", ctypes.c_int),
+        ("dilation", ctypes.c_int),
+        ("pad", ctypes.c_int),
+        ("pad_mode", ctypes.c_int),
+        ("normalize", ctypes.c_int),
+        ("pre_slope", ctypes.c_float),
+        ("w_off", ctypes.c_longlong),
+    ]
+
+
+class PwgCnetOp(ctypes.Structure):
+    _fields_ = [
+        ("kind", ctypes.c_int),
+        ("dst", ctypes.c_int),
+        ("out_channels", ctypes.c_int),
+        ("src", PwgCnetSrc * 2),
+        ("b_off", ctypes.c_longlong),
+        ("b2_off", ctypes.c_longlong),
+        ("res", ctypes.c_int),
+        ("accumulate", ctypes.c_int),
+        ("out_div", ctypes.c_float),
+        ("post_act", ctypes.c_int),
+        ("post_slope", ctypes.c_float),
+        ("stride", ctypes.c_int),
+        ("padding", ctypes.c_int),
+        ("output_padding", ctypes.c_int),
+    ]
+
+
+_bound = False
+
+
+def lib():
+    """The loaded library with the cnet prototypes declared."""
+    global _bound
+    L = _lib.load()
+    if not _bound:
+        vp, ll = ctypes.c_void_p, ctypes.c_longlong
+        L.pwg_cnet_abi_version.restype = ctypes.c_int
+        L.pwg_cnet_create.argtypes = [ctypes.POINTER(PwgCnetOp), ctypes.c_int, ctypes.c_int,
+                                      ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int), ll,
+                                      ctypes.c_int, ctypes.POINTER(vp)]
+        L.pwg_cnet_destroy.argtypes = [vp]
+        L.pwg_cnet_destroy.restype = None
+        L.pwg_cnet_packed_weight_count.argtypes = [vp]
+        L.pwg_cnet_packed_weight_count.restype = ll
+        L.pwg_cnet_pack_weights.argtypes = [vp, vp, vp]
+        L.pwg_cnet_plan_create.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ll), ctypes.POINTER(vp)]
+        L.pwg_cnet_plan_destroy.argtypes = [vp]
+        L.pwg_cnet_plan_destroy.restype = None
+        L.pwg_cnet_plan_rows.argtypes = [vp, ctypes.c_int]
+        L.pwg_cnet_plan_rows.restype = ll
+        L.pwg_cnet_plan_workspace_bytes.argtypes = [vp]
+        L.pwg_cnet_plan_workspace_bytes.restype = ll
+        L.pwg_cnet_run.argtypes = [vp] * 8
+        L.pwg_cnet_set_timing.argtypes = [vp, ctypes.c_int]
+        L.pwg_cnet_timing_collect.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ll)]
+        if L.pwg_cnet_abi_version() != 1:
+            raise RuntimeError("libpwg_hip cnet ABI version mismatch")
+        _bound = True
+    return L
+
+
+class Program:
+    """Builder of a conv-network program. Weights are referenced by state-dict key; ``weights``
+    keeps the reference order (first use) and sizes."""
+
+    def __init__(self, in_channels):
+        self.channels = [int(in_channels)]
+        self.rate = [1]
+        self.ops = []
+        self.names = []
+        self.weights = OrderedDict()  # key -> number of floats
+
+    def buffer(self, channels, rate):
+        self.channels.append(int(channels))
+        self.rate.append(int(rate))
+        return len(self.channels) - 1
+
+    def _w(self, key, count):
+        if key is None:
+            return -1
+        if key in self.weights:
+            if self.weights[key] != count:
+                raise ValueError(f"weight {key} used with two sizes")
+        else:
+            self.weights[key] = int(count)
+        return key
+
+    @staticmethod
+    def src(buf, channels, taps=1, dilation=1, pad=0, pad_mode=PAD_ZERO, pre_slope=1.0, weight=None,
+            normalize=False):
+        return dict(buf=buf, channels=channels, taps=taps, dilation=dilation, pad=pad, pad_mode=pad_mode,
+                    pre_slope=pre_slope, weight=weight, normalize=normalize)
+
+    def conv(self, name, dst, out_channels, srcs, bias=None, bias2=None, res=-1, accumulate=False, out_div=1.0,
+             post_act=ACT_NONE, post_slope=1.0):
+        for s in srcs:
+            self._w(s["weight"], out_channels * s["channels"] * s["taps"])
+        self._w(bias, out_channels)
+        self._w(bias2, out_channels)
+        self.ops.append(dict(kind=CONV, dst=dst, out_channels=out_channels, srcs=srcs, bias=bias, bias2=bias2,
+                             res=res, accumulate=accumulate, out_div=out_div, post_act=post_act,
+                             post_slope=post_slope, stride=1, padding=0, output_padding=0))
+        self.names.append(name)
+
+    def convt(self, name, dst, out_channels, src, stride, padding, output_padding, bias=None):
+        self._w(src["weight"], src["channels"] * out_channels * 2 * stride)
+        self._w(bias, out_channels)
+        self.ops.append(dict(kind=CONVT, dst=dst, out_channels=out_channels, srcs=[src], bias=bias, bias2=None,
+                             res=-1, accumulate=False, out_div=1.0, post_act=ACT_NONE, post_slope=1.0,
+                             stride=stride, padding=padding, output_padding=output_padding))
+        self.names.append(name)
+
+    def pqmf(self, name, dst, src_buf, subbands, filt_key, filt_taps):
+        self._w(filt_key, subbands * filt_taps)
+        src = self.src(src_buf, subbands, weight=filt_key)
+        self.ops.append(dict(kind=PQMF, dst=dst, out_channels=1, srcs=[src], bias=None, bias2=None, res=-1,
+                             accumulate=False, out_div=1.0, post_act=ACT_NONE, post_slope=1.0, stride=subbands,
+                             padding=filt_taps, output_padding=0))
+        self.names.append(name)
+
+    # ------------------------------------------------------------------ lowering
+    def offsets(self):
+        off, o = {}, 0
+        for k, n in self.weights.items():
+            off[k] = o
+            o += n
+        return off, o
+
+    def c_ops(self):
+        off, _ = self.offsets()
+        arr = (PwgCnetOp * len(self.ops))()
+        for i, op in enumerate(self.ops):
+            c = arr[i]
+            c.kind, c.dst, c.out_channels = op["kind"], op["dst"], op["out_channels"]
+            for j in range(2):
+                s = c.src[j]
+                if j < len(op["srcs"]):
+                    d = op["srcs"][j]
+                    s.buf, s.channels, s.taps, s.dilation = d["buf"], d["channels"], d["taps"], d["dilation"]
+                    s.pad, s.pad_mode, s.normalize = d["pad"], d["pad_mode"], int(bool(d["normalize"]))
+                    s.pre_slope = d["pre_slope"]
+                    s.w_off = off[d["weight"]] if d["weight"] is not None else -1
+                else:
+                    s.buf = -1
+            c.b_off = off[op["bias"]] if op["bias"] is not None else -1
+            c.b2_off = off[op["bias2"]] if op["bias2"] is not None else -1
+            c.res, c.accumulate, c.out_div = op["res"], int(op["accumulate"]), op["out_div"]
+            c.post_act, c.post_slope = op["post_act"], op["post_slope"]
+            c.stride, c.padding, c.output_padding = op["stride"], op["padding"], op["output_padding"]
+        return arr
+
+    def flatten(self, state, extra=None):
+        """Reference-order flat float32 vector from a state dict (+ host-side constants such as
+        the PQMF filters in ``extra``)."""
+        folded = fold_weight_norm(state)
+        if extra:
+            folded.update(extra)
+        parts = []
+        for k, n in self.weights.items():
+            if k not in folded:
+                raise KeyError(f"missing generator weight {k!r}")
+            v = np.ascontiguousarray(folded[k], dtype=np.float32).reshape(-1)
+            if v.size != n:
+                raise ValueError(f"weight {k!r} has {v.size} values, expected {n}")
+            parts.append(v)
+        return np.concatenate(parts).astype(np.float32)
+
+
+class CnetPlan:
+    def __init__(self, eng, frames):
+        self.eng = eng
+        self.frames = tuple(int(f) for f in frames)
+        arr = (ctypes.c_longlong * len(self.frames))(*self.frames)
+        p = ctypes.c_void_p()
+        _lib.check(eng._lib.pwg_cnet_plan_create(eng._h, len(self.frames), arr, ctypes.byref(p)))
+        self._p = p
+        nb = len(eng.program.channels)
+        self.out_rows = eng._lib.pwg_cnet_plan_rows(p, nb - 1)
+        self.workspace_bytes = eng._lib.pwg_cnet_plan_workspace_bytes(p)
+
+    def __del__(self):
+        p = getattr(self, "_p", None)
+        if p is not None and p.value:
+            self.eng._lib.pwg_cnet_plan_destroy(p)
+            self._p = None
+
+
+class CnetEngine:
+    """One program on one device: weights packed once, plans cached per utterance-length tuple."""
+
+    def __init__(self, program, device, host_only=False):
+        self.program = program
+        self.device = torch.device(device) if device is not None else None
+        if not host_only and (self.device is None or self.device.type != "cuda"):
+            raise RuntimeError("the conv-network engine runs on a ROCm GPU only (no CPU fallback)")
+        L = lib()
+        self._lib = L
+        ops = program.c_ops()
+        nb = len(program.channels)
+        ch = (ctypes.c_int * nb)(*program.channels)
+        rt = (ctypes.c_int * nb)(*program.rate)
+        _, n_ref = program.offsets()
+        idx = 0
+        if not host_only:
+            idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        h = ctypes.c_void_p()
+        _lib.check(L.pwg_cnet_create(ops, len(program.ops), nb, ch, rt, n_ref, idx, ctypes.byref(h)))
+        self._h = h
+        self.packed_weight_count = L.pwg_cnet_packed_weight_count(h)
+        self.packed = None
+        self._plans = OrderedDict()
+        self._workspace = None
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            self._plans = OrderedDict()
+            self._lib.pwg_cnet_destroy(h)
+            self._h = None
+
+    def pack(self, state, extra=None):
+        flat = self.program.flatten(state, extra)
+        packed = np.empty(self.packed_weight_count, np.float32)
+        _lib.check(self._lib.pwg_cnet_pack_weights(self._h, flat.ctypes.data, packed.ctypes.data))
+        return packed
+
+    def load_state_dict(self, state, extra=None):
+        self.packed = torch.from_numpy(self.pack(state, extra)).to(self.device)
+        return self.packed
+
+    def plan(self, frames):
+        key = tuple(int(f) for f in frames)
+        p = self._plans.get(key)
+        if p is None:
+            p = CnetPlan(self, key)
+            self._plans[key] = p
+            while len(self._plans) > 16:
+                self._plans.popitem(last=False)
+        else:
+            self._plans.move_to_end(key)
+        return p
+
+    def workspace(self, nbytes):
+        if self._workspace is None or self._workspace.numel() < nbytes:
+            self._workspace = None
+            self._workspace = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=self.device)
+        return self._workspace
+
+    @property
+    def out_channels(self):
+        return self.program.channels[-1]
+
+    @property
+    def hop(self):
+        return self.program.rate[-1]
+
+    def run(self, plan, mel, out, mean=None, scale=None, stream=None):
+        if self.packed is None:
+            raise RuntimeError("no weights loaded")
+        for name, t in (("mel", mel), ("out", out)):
+            if t.device != self.device or t.dtype != torch.float32 or not t.is_contiguous():
+                raise ValueError(f"{name} must be a contiguous float32 tensor on {self.device}")
+        if mel.numel() != sum(plan.frames) * self.program.channels[0]:
+            raise ValueError("mel has the wrong size for the plan")
+        if out.numel() != plan.out_rows * self.out_channels:
+            raise ValueError("output buffer has the wrong size")
+        mp = sp = None
+        if mean is not None:
+            mean = mean.to(self.device, torch.float32).contiguous()
+            scale = scale.to(self.device, torch.float32).contiguous()
+            mp, sp = mean.data_ptr(), scale.data_ptr()
+        ws = self.workspace(plan.workspace_bytes)
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device)
+        _lib.check(self._lib.pwg_cnet_run(plan._p, self.packed.data_ptr(), mel.data_ptr(), mp, sp, out.data_ptr(),
+                                          ws.data_ptr(), stream.cuda_stream))
+        return out
+
+    def infer(self, mels, mean=None, scale=None):
+        """Ragged batch: list of (T'_u, in_channels) device tensors -> list of (T'_u*hop, out)."""
+        frames = [int(m.shape[0]) for m in mels]
+        plan = self.plan(frames)
+        mel = torch.cat([m.reshape(-1) for m in mels]) if len(mels) > 1 else mels[0].reshape(-1).contiguous()
+        O = self.out_channels
+        out = torch.empty(plan.out_rows * O, dtype=torch.float32, device=self.device)
+        self.run(plan, mel, out, mean, scale)
+        res, off = [], 0
+        for f in frames:
+            T = f * self.hop
+            res.append(out[off * O:(off + T) * O].view(T, O))
+            off += T
+        return res
+
+    def set_timing(self, enable):
+        _lib.check(self._lib.pwg_cnet_set_timing(self._h, int(enable)))
+
+    def collect_timing(self):
+        n = len(self.program.ops)
+        ms = (ctypes.c_double * n)()
+        cnt = (ctypes.c_longlong * n)()
+        _lib.check(self._lib.pwg_cnet_timing_collect(self._h, ms, cnt))
+        return [(self.program.names[i], ms[i], cnt[i]) for i in range(n)]

@@ -73,3 +73,57 @@ def generator_params(name, **overrides):
     p = copy.deepcopy(GENERATOR_PARAMS[name])
     p.update(copy.deepcopy(overrides))
     return p
+
+
+# MelGAN-family generators, executed by the conv-network engine.
+#   melgan_v1     egs/ljspeech/voc1/conf/melgan.v1.yaml (generator_params)
+#   mb_melgan_v2  egs/ljspeech/voc1/conf/multi_band_melgan.v2.yaml:38-48, + PQMF(4) synthesis
+#   hifigan_v1    egs/ljspeech/voc1/conf/hifigan.v1.yaml:32-50
+# ``*_test`` are reduced shapes for parity fixtures (same code paths, seconds on the oracle).
+VOCODER_PARAMS = {
+    "melgan_v1": ("MelGANGenerator", dict(in_channels=80, out_channels=1, kernel_size=7, channels=512,
+                                          upsample_scales=[8, 8, 2, 2], stack_kernel_size=3, stacks=3,
+                                          use_weight_norm=True, use_causal_conv=False)),
+    "mb_melgan_v2": ("MelGANGenerator", dict(in_channels=80, out_channels=4, kernel_size=7, channels=384,
+                                             upsample_scales=[8, 4, 2], stack_kernel_size=3, stacks=4,
+                                             use_weight_norm=True, use_causal_conv=False)),
+    "hifigan_v1": ("HiFiGANGenerator", dict(in_channels=80, out_channels=1, channels=512, kernel_size=7,
+                                            upsample_scales=[8, 8, 2, 2], upsample_kernel_sizes=[16, 16, 4, 4],
+                                            resblock_kernel_sizes=[3, 7, 11],
+                                            resblock_dilations=[[1, 3, 5], [1, 3, 5], [1, 3, 5]],
+                                            use_additional_convs=True, bias=True,
+                                            nonlinear_activation="LeakyReLU",
+                                            nonlinear_activation_params={"negative_slope": 0.1},
+                                            use_weight_norm=True)),
+    "mb_melgan_test": ("MelGANGenerator", dict(in_channels=80, out_channels=4, kernel_size=7, channels=64,
+                                               upsample_scales=[4, 2], stack_kernel_size=3, stacks=3,
+                                               use_weight_norm=True, use_causal_conv=False)),
+    "melgan_test": ("MelGANGenerator", dict(in_channels=80, out_channels=1, kernel_size=7, channels=96,
+                                            upsample_scales=[3, 2, 2], stack_kernel_size=3, stacks=2,
+                                            use_weight_norm=True, use_causal_conv=False)),
+    "hifigan_test": ("HiFiGANGenerator", dict(in_channels=80, out_channels=1, channels=64, kernel_size=7,
+                                              upsample_scales=[4, 2], upsample_kernel_sizes=[8, 4],
+                                              resblock_kernel_sizes=[3, 5], resblock_dilations=[[1, 3], [1, 2]],
+                                              use_additional_convs=True, bias=True,
+                                              nonlinear_activation="LeakyReLU",
+                                              nonlinear_activation_params={"negative_slope": 0.1},
+                                              use_weight_norm=True)),
+    "hifigan_noadd_test": ("HiFiGANGenerator", dict(in_channels=80, out_channels=1, channels=32, kernel_size=5,
+                                                    upsample_scales=[3], upsample_kernel_sizes=[6],
+                                                    resblock_kernel_sizes=[3, 5, 7],
+                                                    resblock_dilations=[[1, 3], [1, 2], [2, 1]],
+                                                    use_additional_convs=False, bias=True,
+                                                    nonlinear_activation="LeakyReLU",
+                                                    nonlinear_activation_params={"negative_slope": 0.1},
+                                                    use_weight_norm=True)),
+}
+VOCODER_PQMF = {"mb_melgan_v2": dict(subbands=4), "mb_melgan_test": dict(subbands=4)}
+SAMPLING_RATE.update(melgan_v1=22050, mb_melgan_v2=22050, hifigan_v1=22050)
+
+
+def vocoder_params(name, **overrides):
+    """(generator class name, deep-copied generator_params) of a MelGAN-family recipe."""
+    cls, p = VOCODER_PARAMS[name]
+    p = copy.deepcopy(p)
+    p.update(copy.deepcopy(overrides))
+    return cls, p

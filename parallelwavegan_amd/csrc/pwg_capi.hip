@@ -879,3 +879,8 @@ int pwg_timing_collect(PwgHandle* h, double* ms, long long* launches) {
 }
 
 }  // extern "C"
+
+namespace pwg {
+// shared with pwg_cnet.hip: one thread-local last-error message for the whole library
+int set_error(int code, const char* msg) { return fail(code, msg); }
+}  // namespace pwg

@@ -1,0 +1,784 @@
+// Conv-network executor (include/pwg_cnet.h): the MelGAN / multi-band MelGAN + PQMF / HiFiGAN
+// generators as programs of fused fp32 MFMA implicit-GEMM conv ops, for gfx950.
+//
+// One op = one launch of pwg_cnet_conv_kernel<MT>:
+//   * workgroup = 4 waves x 32 output columns (one 128-column block of ONE utterance) x 32*MT
+//     output rows; grid = (blocks, row tiles);
+//   * K = sum over sources, taps and 16-channel chunks; a chunk is 8 k-steps of
+//     v_mfma_f32_32x32x2_f32 in which k-step i pairs channels c0+i (lane half 0) and c0+8+i (lane
+//     half 1), so a lane's B operand of a chunk is 8 contiguous channels (32 bytes) of one
+//     time-major row, loaded with the op's pre-activation (normalize, LeakyReLU) and edge mode
+//     (zero / reflect) applied, one chunk ahead in registers;
+//   * the chunk's A fragments (host-packed lane-linear, MT x 2 KB) are staged in LDS by the whole
+//     workgroup, double-buffered, one barrier per chunk;
+//   * epilogue: + bias (+ second bias) + residual (+ old value) then / out_div then post
+//     activation, 16-byte stores of 4 consecutive channels of one time row.
+// ConvTranspose1d(kernel 2s, stride s) runs as s phase launches: outputs t = q*s + r are a 2-tap
+// conv of input rows q + floor((r+p)/s) - {0, 1} with taps k_a = (r+p) mod s and k_a + s.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/pwg_cnet.h"
+#include "pwg_internal.h"
+
+namespace pwg {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef float f32x8v __attribute__((ext_vector_type(8)));
+
+constexpr int CN_COLS = 128;       // output columns per workgroup (4 waves x 32)
+constexpr int CN_CHUNK = 16;       // input channels per K chunk
+constexpr int CN_MAX_CHUNKS = 4096;
+
+struct ChunkDesc {   // one K chunk of an op (uniform per launch)
+  int src;           // 0 / 1
+  int row_off;       // -pad + tap*dil
+  int c0;            // first input channel
+  int pad;
+};
+
+struct CnSrc {
+  const float* x;
+  const int* seg;    // [n_utts][2]: first row, rows of this buffer
+  int ld;
+  int pad_mode;
+  int normalize;
+  float slope;
+};
+
+struct CnConvArgs {
+  CnSrc src[2];
+  const ChunkDesc* chunks;
+  int n_chunks;
+  const float* wfrag;     // [chunk][MTtot][2][64][4]
+  int mt_total;
+  const float* bias;      // MTtot*32 floats (both biases summed host-side, zero padded)
+  const float* res;
+  const int* seg_res;
+  int ld_res;
+  float* y;
+  const int* seg_dst;
+  int ld_dst;
+  int M;
+  int accumulate;
+  float out_div;
+  int post_act;
+  float post_slope;
+  const int2* blocks;     // (utt, q0)
+  const int* ncols;       // [n_utts] columns of this phase
+  int ostride, ophase;
+  const float* mean;
+  const float* scale;
+};
+
+__device__ __forceinline__ int reflect_row(int p, int T) {
+  p = p < 0 ? -p : p;
+  p = p >= T ? 2 * (T - 1) - p : p;
+  return p < 0 ? 0 : (p >= T ? T - 1 : p);  // masked columns / tiny T: stay in bounds
+}
+
+template <int MT>
+__global__ void __launch_bounds__(256) pwg_cnet_conv_kernel(const CnConvArgs a) {
+  __shared__ __attribute__((aligned(16))) float s_a[2][MT * 512];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int hh = lane >> 5;
+  const int cl = lane & 31;
+  const int2 blk = a.blocks[blockIdx.x];
+  const int u = blk.x;
+  const int q = blk.y + wave * 32 + cl;   // this lane's output column (phase index space)
+  const int nq = a.ncols[u];
+  const bool live = q < nq;
+  const int m0 = blockIdx.y * MT;         // first m-tile of this workgroup
+
+  // B operand of chunk c: 8 channels of one input row, pre-activation applied
+  auto bload = [&](int c) -> f32x8v {
+    const ChunkDesc cd = a.chunks[c];
+    const CnSrc& s = a.src[cd.src];
+    const int2 sg = *reinterpret_cast<const int2*>(s.seg + 2 * u);
+    int p = q + cd.row_off;
+    bool ok = true;
+    if (s.pad_mode == PWG_PAD_REFLECT) p = reflect_row(p, sg.y);
+    else {
+      ok = p >= 0 && p < sg.y;
+      p = p < 0 ? 0 : (p >= sg.y ? sg.y - 1 : p);
+    }
+    const int ch = cd.c0 + 8 * hh;
+    const float* src = s.x + (size_t)(sg.x + p) * s.ld + ch;
+    f32x8v v = *reinterpret_cast<const f32x8v*>(src);
+    if (s.normalize) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = (v[i] - a.mean[ch + i]) / a.scale[ch + i];
+    }
+    if (s.slope != 1.f) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = v[i] > 0.f ? v[i] : v[i] * s.slope;
+    }
+    if (!ok) v = f32x8v{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    return v;
+  };
+  // A fragments of chunk c for this workgroup's MT m-tiles: MT*512 floats, 2*MT float4 per thread
+  // pair of the 256 threads (MT*128 float4 in all)
+  auto aload = [&](int c, f32x4v (&r)[(MT + 1) / 2]) {
+    const f32x4v* g = reinterpret_cast<const f32x4v*>(a.wfrag + ((size_t)c * a.mt_total + m0) * 512);
+#pragma unroll
+    for (int i = 0; i < (MT + 1) / 2; ++i) {
+      const int idx = threadIdx.x + 256 * i;
+      r[i] = idx < MT * 128 ? g[idx] : f32x4v{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto astore = [&](int buf, const f32x4v (&r)[(MT + 1) / 2]) {
+    f32x4v* d = reinterpret_cast<f32x4v*>(s_a[buf]);
+#pragma unroll
+    for (int i = 0; i < (MT + 1) / 2; ++i) {
+      const int idx = threadIdx.x + 256 * i;
+      if (idx < MT * 128) d[idx] = r[i];
+    }
+  };
+
+  f32x16 acc[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
+
+  f32x4v ar[(MT + 1) / 2];
+  aload(0, ar);
+  astore(0, ar);
+  f32x8v bcur = bload(0);
+  __syncthreads();
+  for (int c = 0; c < a.n_chunks; ++c) {
+    const bool more = c + 1 < a.n_chunks;
+    f32x8v bnext = bcur;
+    if (more) {
+      aload(c + 1, ar);
+      bnext = bload(c + 1);
+    }
+    const f32x4v* sa = reinterpret_cast<const f32x4v*>(s_a[c & 1]) + lane;
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      f32x4v av[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) av[m] = sa[(m * 2 + sub) * 64];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+          acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m][e], bcur[4 * sub + e], acc[m], 0, 0, 0);
+    }
+    if (more) astore((c + 1) & 1, ar);
+    __syncthreads();
+    bcur = bnext;
+  }
+
+  // epilogue
+  if (!live) return;
+  const int t = q * a.ostride + a.ophase;
+  const int2 sd = *reinterpret_cast<const int2*>(a.seg_dst + 2 * u);
+  float* yrow = a.y + (size_t)(sd.x + t) * a.ld_dst;
+  const float* rrow = nullptr;
+  if (a.res) {
+    const int2 sr = *reinterpret_cast<const int2*>(a.seg_res + 2 * u);
+    rrow = a.res + (size_t)(sr.x + t) * a.ld_res;
+  }
+  const bool quad = (a.ld_dst & 3) == 0;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int j4 = 0; j4 < 4; ++j4) {
+      const int row = 32 * (m0 + m) + 8 * j4 + 4 * hh;
+      if (row >= a.M) {
+        // padding channels of a padded buffer are written as zeros: later ops read whole chunks
+        if (quad && row < a.ld_dst) *reinterpret_cast<f32x4v*>(yrow + row) = f32x4v{0.f, 0.f, 0.f, 0.f};
+        continue;
+      }
+      const f32x4v b = *reinterpret_cast<const f32x4v*>(a.bias + row);
+      f32x4v v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = acc[m][4 * j4 + i] + b[i];
+      if (quad) {
+        if (rrow) v += *reinterpret_cast<const f32x4v*>(rrow + row);
+        if (a.accumulate) v = *reinterpret_cast<const f32x4v*>(yrow + row) + v;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (row + i >= a.M) continue;
+          if (rrow) v[i] += rrow[row + i];
+          if (a.accumulate) v[i] = yrow[row + i] + v[i];
+        }
+      }
+      if (a.out_div != 1.f) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = v[i] / a.out_div;
+      }
+      if (a.post_act == PWG_ACT_LRELU) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = v[i] > 0.f ? v[i] : v[i] * a.post_slope;
+      } else if (a.post_act == PWG_ACT_TANH) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = tanhf(v[i]);
+      }
+      if (quad) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (row + i >= a.M) v[i] = 0.f;
+        *reinterpret_cast<f32x4v*>(yrow + row) = v;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (row + i < a.M) yrow[row + i] = v[i];
+      }
+    }
+}
+
+// PQMF synthesis (layers/pqmf.py:133-149): y[t] = sum_m sum_k h[m][k] * S * x[(t+k-P)/S][m] over
+// the k with (t+k-P) divisible by S and inside the utterance. One thread per output sample.
+struct CnPqmfArgs {
+  const float* x;
+  const int* seg_src;
+  int ld_src;
+  const float* h;     // [S][NT] synthesis filters
+  float* y;
+  const int* seg_dst;
+  int ld_dst;
+  const int* utt_of_row;  // dst row -> utterance
+  long long rows;
+  int S, NT;
+};
+
+__global__ void __launch_bounds__(256) pwg_cnet_pqmf_kernel(const CnPqmfArgs a) {
+  const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (g >= a.rows) return;
+  const int u = a.utt_of_row[g];
+  const int2 sd = *reinterpret_cast<const int2*>(a.seg_dst + 2 * u);
+  const int2 ss = *reinterpret_cast<const int2*>(a.seg_src + 2 * u);
+  const int t = (int)(g - sd.x);
+  const int P = a.NT / 2;
+  float acc = 0.f;
+  // k with (t + k - P) % S == 0: k = k0, k0 + S, ...
+  const int r = ((P - t) % a.S + a.S) % a.S;
+  for (int k = r; k < a.NT; k += a.S) {
+    const int n = t + k - P;
+    if (n < 0) continue;
+    const int j = n / a.S;
+    if (j >= ss.y) break;
+    const float* xr = a.x + (size_t)(ss.x + j) * a.ld_src;
+    for (int m = 0; m < a.S; ++m) acc = fmaf(a.h[m * a.NT + k], (float)a.S * xr[m], acc);
+  }
+  a.y[(size_t)g * a.ld_dst] = acc;
+}
+
+// ---------------------------------------------------------------------------------------------
+struct OpPhase {          // one launch
+  int op;
+  int phase;              // CONVT phase r, else 0
+  int MT, mt_total;
+  long long frag_off;     // floats into the packed image
+  long long bias_off;
+  std::vector<ChunkDesc> chunks;
+  ChunkDesc* d_chunks = nullptr;
+  int ostride, ophase;
+  int k_a, off_a;         // CONVT
+};
+
+}  // namespace
+}  // namespace pwg
+
+using namespace pwg;
+
+struct PwgCnet {
+  int device = 0;
+  std::vector<PwgCnetOp> ops;
+  std::vector<int> channels, rate, ld;
+  long long ref_count = 0;
+  std::vector<OpPhase> phases;
+  long long packed_count = 0;
+  bool timing = false;
+  struct Rec { int op; hipEvent_t a, b; };
+  std::vector<Rec> records;
+  std::vector<hipEvent_t> pool;
+};
+
+struct PwgCnetPlan {
+  PwgCnet* n = nullptr;
+  int n_utts = 0;
+  std::vector<long long> frames;
+  std::vector<long long> rows;               // per buffer
+  std::vector<size_t> buf_off;               // workspace offsets (SIZE_MAX: external)
+  size_t ws_bytes = 0;
+  int* d_seg = nullptr;                      // [n_bufs][n_utts][2]
+  std::vector<int2*> d_blocks;               // per phase
+  std::vector<int> n_blocks;
+  std::vector<int*> d_ncols;                 // per phase
+  std::vector<int*> d_uttrow;                // per op (PQMF): dst row -> utt
+};
+
+namespace {
+
+int fail(int code, const std::string& m) { return set_error(code, m.c_str()); }
+int hipf(hipError_t e, const char* what) {
+  return fail(PWG_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+struct Guard {
+  int prev = -1;
+  bool ok = true;
+  explicit Guard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) { ok = false; return; }
+    if (prev != dev && hipSetDevice(dev) != hipSuccess) ok = false;
+  }
+  ~Guard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+int pick_mt(int mt_total) {
+  if (mt_total <= 4) return mt_total;
+  if (mt_total % 4 == 0) return 4;
+  if (mt_total % 3 == 0) return 3;
+  if (mt_total % 2 == 0) return 2;
+  return 4;
+}
+
+// weight of (op, phase) at (output o, source s, channel i, tap k) in reference order, 0 outside
+float ref_weight(const PwgCnetOp& op, const OpPhase& ph, const float* ref, int s, int o, int i, int k) {
+  const PwgCnetSrc& src = op.src[s];
+  if (o >= op.out_channels || i >= src.channels) return 0.f;
+  if (op.kind == PWG_CNET_CONVT) {
+    // ConvTranspose1d weight (C_in, C_out, 2*stride); phase tap k=0 -> k_a, k=1 -> k_a + stride
+    const int kk = ph.k_a + k * op.stride;
+    return ref[src.w_off + ((long long)i * op.out_channels + o) * (2 * op.stride) + kk];
+  }
+  return ref[src.w_off + ((long long)o * src.channels + i) * src.taps + k];
+}
+
+}  // namespace
+
+extern "C" {
+
+int pwg_cnet_abi_version(void) { return PWG_CNET_ABI_VERSION; }
+
+int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* channels, const int* rate,
+                    long long ref_weight_count, int device, PwgCnet** out) {
+  if (!ops || n_ops < 1 || n_bufs < 2 || !channels || !rate || !out) return fail(PWG_ERR_INVALID, "bad arguments");
+  *out = nullptr;
+  PwgCnet* n = new PwgCnet();
+  n->device = device;
+  n->ops.assign(ops, ops + n_ops);
+  n->channels.assign(channels, channels + n_bufs);
+  n->rate.assign(rate, rate + n_bufs);
+  n->ref_count = ref_weight_count;
+  for (int b = 0; b < n_bufs; ++b) {
+    if (channels[b] < 1 || rate[b] < 1) { delete n; return fail(PWG_ERR_INVALID, "buffer channels/rate must be >= 1"); }
+    n->ld.push_back(b == n_bufs - 1 ? channels[b] : (channels[b] + 15) / 16 * 16);
+  }
+  if (n->ld[0] != channels[0] || channels[0] % 16) {
+    delete n;
+    return fail(PWG_ERR_UNSUPPORTED, "input channels must be a multiple of 16");
+  }
+  long long off = 0;
+  auto check_w = [&](long long o, long long cnt) { return o >= 0 && o + cnt <= ref_weight_count; };
+  for (int oi = 0; oi < n_ops; ++oi) {
+    const PwgCnetOp& op = n->ops[oi];
+    std::string where = "op " + std::to_string(oi) + ": ";
+    if (op.dst < 1 || op.dst >= n_bufs) { delete n; return fail(PWG_ERR_INVALID, where + "bad dst"); }
+    if (op.out_channels != channels[op.dst]) { delete n; return fail(PWG_ERR_INVALID, where + "out_channels != dst channels"); }
+    if (op.kind == PWG_CNET_PQMF) {
+      const PwgCnetSrc& s = op.src[0];
+      if (s.buf < 0 || s.buf >= n_bufs || op.stride < 1 || channels[s.buf] < op.stride ||
+          rate[op.dst] != op.stride * rate[s.buf] || op.out_channels != 1 || op.padding < 1 || op.padding % 2 == 0 ||
+          !check_w(s.w_off, (long long)op.stride * op.padding)) {
+        delete n;
+        return fail(PWG_ERR_INVALID, where + "bad PQMF op");
+      }
+      OpPhase ph;
+      ph.op = oi; ph.phase = 0; ph.MT = 0; ph.mt_total = 0; ph.frag_off = off; ph.bias_off = -1;
+      ph.ostride = 1; ph.ophase = 0;
+      off += (long long)op.stride * op.padding;
+      n->phases.push_back(ph);
+      continue;
+    }
+    if (op.kind != PWG_CNET_CONV && op.kind != PWG_CNET_CONVT) { delete n; return fail(PWG_ERR_INVALID, where + "bad kind"); }
+    const int nsrc = (op.src[1].buf >= 0 && op.kind == PWG_CNET_CONV) ? 2 : 1;
+    for (int s = 0; s < nsrc; ++s) {
+      const PwgCnetSrc& src = op.src[s];
+      if (src.buf < 0 || src.buf >= n_bufs || src.channels < 1 || src.channels > channels[src.buf] || src.taps < 1 ||
+          (op.kind == PWG_CNET_CONV && src.dilation < 1)) {
+        delete n;
+        return fail(PWG_ERR_INVALID, where + "bad source");
+      }
+      if (src.buf == n_bufs - 1) { delete n; return fail(PWG_ERR_INVALID, where + "the output buffer cannot be read"); }
+      if (op.kind == PWG_CNET_CONV && rate[src.buf] != rate[op.dst]) {
+        delete n;
+        return fail(PWG_ERR_INVALID, where + "conv source and destination rates differ");
+      }
+      if (src.normalize && src.buf != 0) { delete n; return fail(PWG_ERR_INVALID, where + "normalize on a non-input buffer"); }
+    }
+    if (op.res >= 0 && (op.res >= n_bufs || rate[op.res] != rate[op.dst] || channels[op.res] < op.out_channels ||
+                        op.res == n_bufs - 1)) {
+      delete n;
+      return fail(PWG_ERR_INVALID, where + "bad residual buffer");
+    }
+    if (op.out_div == 0.f) { delete n; return fail(PWG_ERR_INVALID, where + "out_div must be non-zero"); }
+    const int mt_total0 = (op.out_channels + 31) / 32;
+    const int MT = pick_mt(mt_total0);
+    const int mt_total = (mt_total0 + MT - 1) / MT * MT;
+    int n_phase = 1;
+    if (op.kind == PWG_CNET_CONVT) {
+      const int s = op.stride;
+      if (s < 1 || rate[op.dst] != s * rate[op.src[0].buf] || s - 2 * op.padding + op.output_padding != 0) {
+        delete n;
+        return fail(PWG_ERR_UNSUPPORTED, where + "ConvTranspose1d must map T -> stride*T (kernel 2*stride)");
+      }
+      if (!check_w(op.src[0].w_off, (long long)op.src[0].channels * op.out_channels * 2 * s)) {
+        delete n;
+        return fail(PWG_ERR_INVALID, where + "weights out of range");
+      }
+      n_phase = s;
+    } else {
+      for (int s = 0; s < nsrc; ++s)
+        if (!check_w(op.src[s].w_off, (long long)op.out_channels * op.src[s].channels * op.src[s].taps)) {
+          delete n;
+          return fail(PWG_ERR_INVALID, where + "weights out of range");
+        }
+    }
+    if ((op.b_off >= 0 && !check_w(op.b_off, op.out_channels)) || (op.b2_off >= 0 && !check_w(op.b2_off, op.out_channels))) {
+      delete n;
+      return fail(PWG_ERR_INVALID, where + "bias out of range");
+    }
+    for (int r = 0; r < n_phase; ++r) {
+      OpPhase ph;
+      ph.op = oi; ph.phase = r; ph.MT = MT; ph.mt_total = mt_total;
+      ph.ostride = op.kind == PWG_CNET_CONVT ? op.stride : 1;
+      ph.ophase = r;
+      if (op.kind == PWG_CNET_CONVT) {
+        ph.k_a = (r + op.padding) % op.stride;
+        ph.off_a = (r + op.padding) / op.stride;
+        const int cs = (op.src[0].channels + CN_CHUNK - 1) / CN_CHUNK;
+        for (int k = 0; k < 2; ++k)
+          for (int c = 0; c < cs; ++c) ph.chunks.push_back({0, ph.off_a - k, c * CN_CHUNK, 0});
+      } else {
+        ph.k_a = ph.off_a = 0;
+        for (int s = 0; s < nsrc; ++s) {
+          const PwgCnetSrc& src = op.src[s];
+          const int cs = (src.channels + CN_CHUNK - 1) / CN_CHUNK;
+          for (int k = 0; k < src.taps; ++k)
+            for (int c = 0; c < cs; ++c) ph.chunks.push_back({s, -src.pad + k * src.dilation, c * CN_CHUNK, 0});
+        }
+      }
+      if (ph.chunks.size() > (size_t)CN_MAX_CHUNKS) { delete n; return fail(PWG_ERR_UNSUPPORTED, where + "K too large"); }
+      for (const ChunkDesc& cd : ph.chunks)
+        if (cd.c0 + CN_CHUNK > n->ld[op.src[cd.src].buf]) {
+          delete n;
+          return fail(PWG_ERR_UNSUPPORTED, where + "source channel padding too small");
+        }
+      ph.frag_off = off;
+      off += (long long)ph.chunks.size() * mt_total * 512;
+      ph.bias_off = off;
+      off += (long long)mt_total * 32;
+      n->phases.push_back(ph);
+    }
+  }
+  n->packed_count = off;
+  *out = n;  // device tables are uploaded by the first plan: packing needs no GPU
+  return PWG_OK;
+}
+
+void pwg_cnet_destroy(PwgCnet* n) {
+  if (!n) return;
+  Guard g(n->device);
+  for (OpPhase& ph : n->phases)
+    if (ph.d_chunks) (void)hipFree(ph.d_chunks);
+  for (auto& r : n->records) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+  for (hipEvent_t e : n->pool) (void)hipEventDestroy(e);
+  delete n;
+}
+
+long long pwg_cnet_packed_weight_count(const PwgCnet* n) { return n ? n->packed_count : -1; }
+
+int pwg_cnet_pack_weights(const PwgCnet* n, const float* ref, float* packed) {
+  if (!n || !ref || !packed) return fail(PWG_ERR_INVALID, "null argument");
+  std::memset(packed, 0, sizeof(float) * n->packed_count);
+  for (const OpPhase& ph : n->phases) {
+    const PwgCnetOp& op = n->ops[ph.op];
+    if (op.kind == PWG_CNET_PQMF) {
+      std::memcpy(packed + ph.frag_off, ref + op.src[0].w_off, sizeof(float) * op.stride * op.padding);
+      continue;
+    }
+    // A fragments: [chunk][m][sub][lane][e], k-step i = 4 sub + e pairs channels c0+i / c0+8+i
+    for (size_t c = 0; c < ph.chunks.size(); ++c) {
+      const ChunkDesc& cd = ph.chunks[c];
+      const PwgCnetSrc& src = op.src[cd.src];
+      const int tap = op.kind == PWG_CNET_CONVT ? ph.off_a - cd.row_off   // 0 or 1
+                                                : (cd.row_off + src.pad) / src.dilation;
+      for (int m = 0; m < ph.mt_total; ++m)
+        for (int sub = 0; sub < 2; ++sub)
+          for (int l = 0; l < 64; ++l)
+            for (int e = 0; e < 4; ++e) {
+              const int i = 4 * sub + e;
+              const int o = 32 * m + (l & 31);
+              const int ch = cd.c0 + i + 8 * (l >> 5);
+              packed[ph.frag_off + (((size_t)c * ph.mt_total + m) * 2 + sub) * 256 + l * 4 + e] =
+                  ref_weight(op, ph, ref, cd.src, o, ch, tap);
+            }
+    }
+    for (int o = 0; o < op.out_channels; ++o) {
+      float b = op.b_off >= 0 ? ref[op.b_off + o] : 0.f;
+      if (op.b2_off >= 0) b += ref[op.b2_off + o];
+      packed[ph.bias_off + o] = b;
+    }
+  }
+  return PWG_OK;
+}
+
+int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCnetPlan** out) {
+  if (!n || n_utts < 1 || !frames || !out) return fail(PWG_ERR_INVALID, "bad arguments");
+  *out = nullptr;
+  const int nb = (int)n->channels.size();
+  PwgCnetPlan* p = new PwgCnetPlan();
+  p->n = n;
+  p->n_utts = n_utts;
+  p->frames.assign(frames, frames + n_utts);
+  std::vector<int> seg((size_t)nb * n_utts * 2);
+  p->rows.assign(nb, 0);
+  for (int b = 0; b < nb; ++b) {
+    long long base = 0;
+    for (int u = 0; u < n_utts; ++u) {
+      if (frames[u] < 1) { delete p; return fail(PWG_ERR_INVALID, "every utterance needs >= 1 frame"); }
+      const long long r = frames[u] * n->rate[b];
+      seg[((size_t)b * n_utts + u) * 2] = (int)base;
+      seg[((size_t)b * n_utts + u) * 2 + 1] = (int)r;
+      base += r;
+    }
+    if (base >= (1LL << 31) / std::max(1, n->ld[b])) { delete p; return fail(PWG_ERR_UNSUPPORTED, "batch too large for one plan"); }
+    p->rows[b] = base;
+  }
+  // reflect padding needs pad < T (torch.nn.ReflectionPad1d raises otherwise)
+  for (const PwgCnetOp& op : n->ops)
+    for (int s = 0; s < 2; ++s) {
+      const PwgCnetSrc& src = op.src[s];
+      if (src.buf < 0 || op.kind != PWG_CNET_CONV || src.pad_mode != PWG_PAD_REFLECT) continue;
+      const long long reach = std::max<long long>(src.pad, (long long)(src.taps - 1) * src.dilation - src.pad);
+      for (int u = 0; u < n_utts; ++u)
+        if (reach >= frames[u] * n->rate[src.buf]) {
+          delete p;
+          return fail(PWG_ERR_INVALID, "reflection padding wider than an utterance (ReflectionPad1d)");
+        }
+    }
+  // Workspace: internal buffers (1 .. nb-2) share storage slots when their live ranges (first
+  // write .. last read, in op order) do not overlap and their sizes match; an op never gets a
+  // destination that aliases one of its own inputs.
+  const int nops = (int)n->ops.size();
+  std::vector<int> first_def(nb, nops), last_use(nb, -1);
+  for (int oi = 0; oi < nops; ++oi) {
+    const PwgCnetOp& op = n->ops[oi];
+    first_def[op.dst] = std::min(first_def[op.dst], oi);
+    last_use[op.dst] = std::max(last_use[op.dst], oi);
+    for (int s2 = 0; s2 < 2; ++s2)
+      if (op.src[s2].buf >= 0) last_use[op.src[s2].buf] = std::max(last_use[op.src[s2].buf], oi);
+    if (op.res >= 0) last_use[op.res] = std::max(last_use[op.res], oi);
+  }
+  struct Slot { size_t off, bytes; int free_after; };
+  std::vector<Slot> slots;
+  size_t o = 0;
+  p->buf_off.assign(nb, SIZE_MAX);
+  std::vector<int> order;
+  for (int b = 1; b < nb - 1; ++b) order.push_back(b);
+  std::sort(order.begin(), order.end(), [&](int x, int y) { return first_def[x] < first_def[y]; });
+  for (int b : order) {
+    const size_t bytes = ((size_t)p->rows[b] * n->ld[b] * sizeof(float) + 255) / 256 * 256;
+    int pick = -1;
+    for (size_t si = 0; si < slots.size(); ++si)
+      if (slots[si].bytes == bytes && slots[si].free_after < first_def[b]) { pick = (int)si; break; }
+    if (pick < 0) {
+      slots.push_back({o, bytes, -1});
+      o += bytes;
+      pick = (int)slots.size() - 1;
+    }
+    p->buf_off[b] = slots[pick].off;
+    slots[pick].free_after = std::max(last_use[b], first_def[b]);
+  }
+  p->ws_bytes = std::max<size_t>(o, 256);
+  Guard g(n->device);
+  if (!g.ok) { delete p; return fail(PWG_ERR_HIP, "hipSetDevice failed"); }
+  hipError_t e = hipSuccess;
+  for (OpPhase& ph : n->phases) {
+    if (ph.chunks.empty() || ph.d_chunks) continue;
+    e = hipMalloc(&ph.d_chunks, sizeof(ChunkDesc) * ph.chunks.size());
+    if (e == hipSuccess)
+      e = hipMemcpy(ph.d_chunks, ph.chunks.data(), sizeof(ChunkDesc) * ph.chunks.size(), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      if (ph.d_chunks) (void)hipFree(ph.d_chunks);
+      ph.d_chunks = nullptr;
+      delete p;
+      return hipf(e, "chunk table upload");
+    }
+  }
+  e = hipMalloc(&p->d_seg, sizeof(int) * seg.size());
+  if (e == hipSuccess) e = hipMemcpy(p->d_seg, seg.data(), sizeof(int) * seg.size(), hipMemcpyHostToDevice);
+  for (const OpPhase& ph : n->phases) {
+    const PwgCnetOp& op = n->ops[ph.op];
+    std::vector<int2> blocks;
+    std::vector<int> ncols(n_utts);
+    std::vector<int> uttrow;
+    if (op.kind == PWG_CNET_PQMF) {
+      uttrow.resize(p->rows[op.dst]);
+      for (int u = 0; u < n_utts; ++u) {
+        const int base = seg[((size_t)op.dst * n_utts + u) * 2], r = seg[((size_t)op.dst * n_utts + u) * 2 + 1];
+        for (int i = 0; i < r; ++i) uttrow[base + i] = u;
+      }
+    } else {
+      for (int u = 0; u < n_utts; ++u) {
+        const long long T = frames[u] * n->rate[op.dst];
+        const int nq = (int)((T - ph.ophase + ph.ostride - 1) / ph.ostride);
+        ncols[u] = nq;
+        for (int q0 = 0; q0 < nq; q0 += CN_COLS) blocks.push_back(make_int2(u, q0));
+      }
+    }
+    int2* db = nullptr;
+    int* dn = nullptr;
+    int* dr = nullptr;
+    if (e == hipSuccess && !blocks.empty()) {
+      e = hipMalloc(&db, sizeof(int2) * blocks.size());
+      if (e == hipSuccess) e = hipMemcpy(db, blocks.data(), sizeof(int2) * blocks.size(), hipMemcpyHostToDevice);
+      if (e == hipSuccess) e = hipMalloc(&dn, sizeof(int) * n_utts);
+      if (e == hipSuccess) e = hipMemcpy(dn, ncols.data(), sizeof(int) * n_utts, hipMemcpyHostToDevice);
+    }
+    if (e == hipSuccess && !uttrow.empty()) {
+      e = hipMalloc(&dr, sizeof(int) * uttrow.size());
+      if (e == hipSuccess) e = hipMemcpy(dr, uttrow.data(), sizeof(int) * uttrow.size(), hipMemcpyHostToDevice);
+    }
+    p->d_blocks.push_back(db);
+    p->n_blocks.push_back((int)blocks.size());
+    p->d_ncols.push_back(dn);
+    p->d_uttrow.push_back(dr);
+  }
+  if (e != hipSuccess) {
+    const int rc = hipf(e, "cnet plan upload");
+    pwg_cnet_plan_destroy(p);
+    return rc;
+  }
+  *out = p;
+  return PWG_OK;
+}
+
+void pwg_cnet_plan_destroy(PwgCnetPlan* p) {
+  if (!p) return;
+  Guard g(p->n->device);
+  if (p->d_seg) (void)hipFree(p->d_seg);
+  for (auto* x : p->d_blocks) if (x) (void)hipFree(x);
+  for (auto* x : p->d_ncols) if (x) (void)hipFree(x);
+  for (auto* x : p->d_uttrow) if (x) (void)hipFree(x);
+  delete p;
+}
+
+long long pwg_cnet_plan_rows(const PwgCnetPlan* p, int buf) {
+  if (!p || buf < 0 || buf >= (int)p->rows.size()) return -1;
+  return p->rows[buf];
+}
+
+long long pwg_cnet_plan_workspace_bytes(const PwgCnetPlan* p) { return p ? (long long)p->ws_bytes : -1; }
+
+int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const float* mean, const float* scale,
+                 float* out, void* workspace, void* stream) {
+  if (!p || !packed || !mel || !out || !workspace) return fail(PWG_ERR_INVALID, "null argument");
+  PwgCnet* n = p->n;
+  const int nb = (int)n->channels.size();
+  Guard g(n->device);
+  if (!g.ok) return fail(PWG_ERR_HIP, "hipSetDevice failed");
+  hipStream_t s = (hipStream_t)stream;
+  std::vector<float*> bufs(nb);
+  bufs[0] = const_cast<float*>(mel);
+  bufs[nb - 1] = out;
+  for (int b = 1; b < nb - 1; ++b) bufs[b] = (float*)((char*)workspace + p->buf_off[b]);
+  auto seg_of = [&](int b) -> const int* { return p->d_seg + (size_t)b * p->n_utts * 2; };
+  for (size_t pi = 0; pi < n->phases.size(); ++pi) {
+    const OpPhase& ph = n->phases[pi];
+    const PwgCnetOp& op = n->ops[ph.op];
+    hipEvent_t ea = nullptr, eb = nullptr;
+    if (n->timing) {
+      for (hipEvent_t* ev : {&ea, &eb}) {
+        if (!n->pool.empty()) { *ev = n->pool.back(); n->pool.pop_back(); }
+        else if (hipEventCreate(ev) != hipSuccess) return fail(PWG_ERR_HIP, "event create");
+      }
+      (void)hipEventRecord(ea, s);
+    }
+    if (op.kind == PWG_CNET_PQMF) {
+      CnPqmfArgs a;
+      a.x = bufs[op.src[0].buf]; a.seg_src = seg_of(op.src[0].buf); a.ld_src = n->ld[op.src[0].buf];
+      a.h = packed + ph.frag_off; a.y = bufs[op.dst]; a.seg_dst = seg_of(op.dst); a.ld_dst = n->ld[op.dst];
+      a.utt_of_row = p->d_uttrow[pi]; a.rows = p->rows[op.dst]; a.S = op.stride; a.NT = op.padding;
+      hipLaunchKernelGGL(pwg_cnet_pqmf_kernel, dim3((unsigned)((a.rows + 255) / 256)), dim3(256), 0, s, a);
+    } else if (p->n_blocks[pi] > 0) {
+      CnConvArgs a;
+      const int nsrc = (op.src[1].buf >= 0 && op.kind == PWG_CNET_CONV) ? 2 : 1;
+      for (int si = 0; si < 2; ++si) {
+        const PwgCnetSrc& src = op.src[si];
+        CnSrc& d = a.src[si];
+        if (si < nsrc) {
+          d.x = bufs[src.buf]; d.seg = seg_of(src.buf); d.ld = n->ld[src.buf];
+          d.pad_mode = op.kind == PWG_CNET_CONVT ? PWG_PAD_ZERO : src.pad_mode;
+          d.normalize = src.normalize && mean && scale;  // normalize_before: caller passes stats
+          d.slope = src.pre_slope;
+        } else {
+          d = a.src[0];
+        }
+      }
+      a.chunks = ph.d_chunks; a.n_chunks = (int)ph.chunks.size();
+      a.wfrag = packed + ph.frag_off; a.mt_total = ph.mt_total; a.bias = packed + ph.bias_off;
+      a.res = op.res >= 0 ? bufs[op.res] : nullptr; a.seg_res = op.res >= 0 ? seg_of(op.res) : nullptr;
+      a.ld_res = op.res >= 0 ? n->ld[op.res] : 0;
+      a.y = bufs[op.dst]; a.seg_dst = seg_of(op.dst); a.ld_dst = n->ld[op.dst]; a.M = op.out_channels;
+      a.accumulate = op.accumulate; a.out_div = op.out_div; a.post_act = op.post_act; a.post_slope = op.post_slope;
+      a.blocks = p->d_blocks[pi]; a.ncols = p->d_ncols[pi]; a.ostride = ph.ostride; a.ophase = ph.ophase;
+      a.mean = mean; a.scale = scale;
+      const dim3 grid((unsigned)p->n_blocks[pi], (unsigned)(ph.mt_total / ph.MT)), block(256);
+      switch (ph.MT) {
+        case 1: hipLaunchKernelGGL(pwg_cnet_conv_kernel<1>, grid, block, 0, s, a); break;
+        case 2: hipLaunchKernelGGL(pwg_cnet_conv_kernel<2>, grid, block, 0, s, a); break;
+        case 3: hipLaunchKernelGGL(pwg_cnet_conv_kernel<3>, grid, block, 0, s, a); break;
+        default: hipLaunchKernelGGL(pwg_cnet_conv_kernel<4>, grid, block, 0, s, a); break;
+      }
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hipf(e, "cnet op launch");
+    if (n->timing) {
+      (void)hipEventRecord(eb, s);
+      n->records.push_back({ph.op, ea, eb});
+    }
+  }
+  return PWG_OK;
+}
+
+int pwg_cnet_set_timing(PwgCnet* n, int enable) {
+  if (!n) return fail(PWG_ERR_INVALID, "null handle");
+  n->timing = enable != 0;
+  return PWG_OK;
+}
+
+int pwg_cnet_timing_collect(PwgCnet* n, double* ms, long long* launches) {
+  if (!n || !ms || !launches) return fail(PWG_ERR_INVALID, "null argument");
+  Guard g(n->device);
+  for (auto& r : n->records) {
+    hipError_t e = hipEventSynchronize(r.b);
+    float t = 0.f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&t, r.a, r.b);
+    if (e != hipSuccess) return hipf(e, "cnet timing");
+    ms[r.op] += t;
+    launches[r.op] += 1;
+    n->pool.push_back(r.a);
+    n->pool.push_back(r.b);
+  }
+  n->records.clear();
+  return PWG_OK;
+}
+
+}  // extern "C"

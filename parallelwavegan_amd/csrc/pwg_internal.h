@@ -160,6 +160,9 @@ struct PersistArgs {
 // Persistent-kernel work queues: one head per XCD, each on its own 128-byte line.
 constexpr int SCHED_CTR_STRIDE = 32;
 
+// Sets the message pwg_last_error() returns and passes `code` through (pwg_capi.hip).
+int set_error(int code, const char* msg);
+
 // Kernel launchers (pwg_kernels.hip).
 hipError_t launch_conv_in(const ConvInArgs& a, hipStream_t s);
 hipError_t launch_aux_proj(const AuxProjArgs& a, int layers, hipStream_t s);

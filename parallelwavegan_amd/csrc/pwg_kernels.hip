@@ -645,6 +645,33 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_persistent_kernel(const Pers
     return *reinterpret_cast<const bvec*>(a.x_in + (size_t)(c + cl + off) * RS + c0 + GK * hh);
   };
   // 4*GK-byte group of k-steps: 16 MFMAs per 4-k-step slice, A from LDS
+#if PWG_APREFETCH
+  // A fragments one 4-k-step slice ahead: av holds the slice about to run; the read of the next
+  // one (wrapping to slice 0, the next block's first: the weights are the same) is in flight
+  // during its 16 MFMAs.
+  const int n_slices = NGRP * NB;
+  f32x4 av[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) av[m] = wgl[m * 64];
+  auto group_mfma = [&](f32x16 (&acc)[MT], const bvec& b, int g) {
+#pragma unroll
+    for (int sub = 0; sub < NB; ++sub) {
+      int nxt = g * NB + sub + 1;
+      nxt = nxt == n_slices ? 0 : nxt;
+      f32x4 an[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) an[m] = wgl[(nxt * MT + m) * 64];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+          acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m][i], b[4 * sub + i], acc[m], 0, 0, 0);
+#pragma unroll
+      for (int m = 0; m < MT; ++m) av[m] = an[m];
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+#else
   auto group_mfma = [&](f32x16 (&acc)[MT], const bvec& b, int g) {
 #pragma unroll
     for (int sub = 0; sub < NB; ++sub) {
@@ -659,6 +686,7 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_persistent_kernel(const Pers
       __builtin_amdgcn_sched_barrier(0);
     }
   };
+#endif
 
   int blk = x_first + (blockIdx.x >> 3) * nw + wave;  // static round 0
   int nblk = blk + x_waves;                           // static round 1

