@@ -105,12 +105,157 @@ def cpu_baseline(params, sd, lengths, H, seconds_budget):
     return done_samples / t_total, threads, desc
 
 
+VOCODERS = ["mb_melgan_v2", "hifigan_v1", "melgan_v1"]
+
+
+def program_flops_per_frame(P):
+    """Algorithmic FLOP per input frame of a conv program (each op: 2 * out * K per output row)."""
+    from parallelwavegan_amd import cnet
+
+    fl = 0.0
+    for op in P.ops:
+        rows = P.rate[op["dst"]]
+        if op["kind"] == cnet.CONV:
+            k = sum(s["channels"] * s["taps"] for s in op["srcs"])
+        elif op["kind"] == cnet.CONVT:
+            k = op["srcs"][0]["channels"] * 2
+        else:  # PQMF: (taps / S) taps x S bands per output sample
+            k = op["padding"]
+        fl += 2.0 * op["out_channels"] * k * rows
+    return fl
+
+
+def program_bytes_per_frame(P):
+    """Algorithmic HBM bytes per input frame: every op reads its sources / residual once and
+    writes its destination once (fp32, unpadded channels)."""
+    b = 0.0
+    for op in P.ops:
+        rows = P.rate[op["dst"]]
+        for s in op["srcs"]:
+            b += 4.0 * s["channels"] * P.rate[s["buf"]]
+        if op["res"] >= 0:
+            b += 4.0 * op["out_channels"] * rows
+        b += 4.0 * op["out_channels"] * rows * (2 if op["accumulate"] else 1)
+    return b
+
+
+def bench_vocoder(args, rank, world, dev):
+    """MelGAN-family generator inference (BASELINE configs[2] multi_band_melgan.v2 and [3]
+    hifigan.v1) on the conv-network executor: same ragged-batch workload shape
+    as the PWG bench, weak scaling, utterance sharding, RCCL weight broadcast."""
+    from oracle.melgan_torch_cpu import TorchCPUVocoder  # cpu_baseline leg only
+    from parallelwavegan_amd.engine import fold_weight_norm
+    from parallelwavegan_amd.hifigan import HiFiGANGenerator
+    from parallelwavegan_amd.melgan import PQMF, MelGANGenerator
+
+    cls_name, params = configs.vocoder_params(args.config)
+    m = {"MelGANGenerator": MelGANGenerator, "HiFiGANGenerator": HiFiGANGenerator}[cls_name](**params)
+    sd = synthetic.make_module_state_dict(m, seed=0)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    syn = None
+    if args.config in configs.VOCODER_PQMF:
+        m.pqmf = PQMF(**configs.VOCODER_PQMF[args.config])
+        syn = m.pqmf.synthesis_taps()
+    m = m.to(dev)
+    eng = m.engine()
+    if world > 1:
+        broadcast_packed_weights(eng.packed, src=0)
+    P = eng.program
+    hop = eng.hop
+    fs = configs.SAMPLING_RATE[args.config]
+    lengths = synthetic.libritts_lengths(args.utts, seed=3)
+    plan = eng.plan(lengths.tolist())
+    rs = np.random.RandomState(100 + rank)
+    mel = torch.from_numpy(rs.standard_normal(int(lengths.sum()) * 80).astype(np.float32)).to(dev)
+    out = torch.empty(plan.out_rows * eng.out_channels, dtype=torch.float32, device=dev)
+    for _ in range(args.warmup):
+        eng.run(plan, mel, out)
+    torch.cuda.synchronize(dev)
+    eng.set_timing(True)
+    eng.collect_timing()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.run(plan, mel, out)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0, dev)
+    eng.set_timing(False)
+    timing = eng.collect_timing()
+    if not torch.isfinite(out).all():
+        raise RuntimeError("non-finite generator output")
+    samples = int(lengths.sum()) * hop
+    value = samples * world * args.steps / elapsed
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    fl_frame = program_flops_per_frame(P)
+    by_frame = program_bytes_per_frame(P)
+    kern_ms = sum(ms for _, ms, _ in timing) / args.steps
+    frames = int(lengths.sum())
+    achieved = fl_frame * frames / (kern_ms * 1e-3) / 1e12
+    top = sorted(timing, key=lambda r: -r[1])[:5]
+    cpu = None
+    if args.cpu_seconds > 0 and world == 1:
+        threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+        torch.set_num_threads(threads)
+        gen = TorchCPUVocoder(cls_name, fold_weight_norm(sd), params, syn)
+        gen.inference(synthetic.make_mel(40, 80, seed=99))
+        done, tt, used = 0, 0.0, 0
+        for i, f in enumerate(lengths):
+            c = synthetic.make_mel(int(f), 80, seed=1000 + i)
+            t1 = time.perf_counter()
+            gen.inference(c)
+            tt += time.perf_counter() - t1
+            done += int(f) * hop
+            used += 1
+            if tt >= args.cpu_seconds:
+                break
+        cpu = {"value": round(done / tt, 1), "unit": "audio samples/s", "cores": threads, "kind": "port",
+               "sample": f"{used} utterances ({done} samples, first of the bench batch), B=1, torch-CPU restatement "
+                         f"of the reference op sequence"}
+    res = {
+        "metric": f"audio samples/sec/GPU ({fs / 1000:g} kHz {args.config}, 80-band mel)",
+        "value": round(value, 1),
+        "unit": "audio samples/s (whole job, all GPUs)",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (seeded N(0,1) mel, seeded N(0, 1/fan_in) weights)",
+        "config": {"workload": f"{args.config} generator inference, {args.utts} ragged utterances per GPU per step",
+                   "model": cls_name, "sampling_rate": fs, "hop": hop, "global_batch": args.utts * world,
+                   "frames_per_gpu": frames, "samples_per_step_per_gpu": samples,
+                   "parallelism": f"utterance-sharded x{world}"},
+        "x_realtime_per_gpu": round(value / world / fs, 1),
+        "kernel_ms_per_step": round(kern_ms, 3),
+        "top_ops_ms_per_step": {n: round(ms / args.steps, 3) for n, ms, _ in top},
+        "roofline": {"kernel": "all conv ops (fp32 MFMA implicit GEMM), whole program", "bound": "mfma",
+                     "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                     "flop_per_sample": round(fl_frame / hop, 1),
+                     "algorithmic_bytes_per_sample": round(by_frame / hop, 1)},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="libritts_v1", choices=["libritts_v1", "ljspeech_v1", "yesno_debug"])
+    ap.add_argument("--config", default="libritts_v1",
+                    choices=["libritts_v1", "ljspeech_v1", "yesno_debug"] + VOCODERS)
     ap.add_argument("--utts", type=int, default=32, help="utterances per GPU per step")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "layer_traffic.json"))
@@ -121,6 +266,8 @@ def main():
 
     rank, world, dev = dist_setup(args.gpus)
     _lib.build()
+    if args.config in VOCODERS:
+        return bench_vocoder(args, rank, world, dev)
     params = configs.generator_params(args.config)
     fs = configs.SAMPLING_RATE[args.config]
     eng = Engine(params, dev)

@@ -101,3 +101,19 @@ def test_pqmf_filters_match_scipy_kaiser():
 
     for m, beta in ((63, 9.0), (31, 5.0), (64, 8.6)):
         np.testing.assert_allclose(_kaiser(m, beta), scipy.signal.windows.kaiser(m, beta), rtol=0, atol=1e-13)
+
+
+@pytest.mark.parametrize("name", vocoder_golden_names())
+def test_vocoder_torch_cpu_restatement_matches_golden(name):
+    """oracle/melgan_torch_cpu.py (the vocoder CPU baseline) reproduces the reference outputs."""
+    from oracle.melgan_torch_cpu import TorchCPUVocoder
+
+    g = load_golden(name)
+    meta = g["meta"]
+    if meta["options"].get("forward") or meta["options"].get("normalize"):
+        pytest.skip("inference() without normalization only")
+    m, params, folded = vocoder_holder(meta)
+    syn = m.pqmf.synthesis_taps() if getattr(m, "pqmf", None) is not None else None
+    y = TorchCPUVocoder(type(m).__name__, folded, params, syn).inference(g["mel"]).numpy()
+    err = np.abs(y - g["y"]).max()
+    assert err < 1e-5, f"{name}: max|d| = {err:.3e}"

@@ -1,0 +1,65 @@
+"""Per-op time and MFMA rate of a MelGAN-family program on the GPU (diagnostic).
+Usage: python tools/cnet_profile.py mb_melgan_v2 [--utts 32] [--steps 3]"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from parallelwavegan_amd import cnet, configs, synthetic  # noqa: E402
+from parallelwavegan_amd.hifigan import HiFiGANGenerator  # noqa: E402
+from parallelwavegan_amd.melgan import PQMF, MelGANGenerator  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("config")
+    ap.add_argument("--utts", type=int, default=32)
+    ap.add_argument("--steps", type=int, default=3)
+    a = ap.parse_args()
+    cls, p = configs.vocoder_params(a.config)
+    m = {"MelGANGenerator": MelGANGenerator, "HiFiGANGenerator": HiFiGANGenerator}[cls](**p)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic.make_module_state_dict(m, seed=0).items()})
+    if a.config in configs.VOCODER_PQMF:
+        m.pqmf = PQMF(**configs.VOCODER_PQMF[a.config])
+    dev = torch.device("cuda", 0)
+    m = m.to(dev)
+    eng = m.engine()
+    P = eng.program
+    lengths = synthetic.libritts_lengths(a.utts, seed=3)
+    frames = int(lengths.sum())
+    plan = eng.plan(lengths.tolist())
+    mel = torch.randn(frames * 80, device=dev)
+    out = torch.empty(plan.out_rows * eng.out_channels, device=dev)
+    eng.run(plan, mel, out)
+    torch.cuda.synchronize()
+    eng.set_timing(True)
+    eng.collect_timing()
+    for _ in range(a.steps):
+        eng.run(plan, mel, out)
+    t = eng.collect_timing()
+    tot = 0.0
+    rows = []
+    for i, (name, ms, n) in enumerate(t):
+        op = P.ops[i]
+        r = P.rate[op["dst"]]
+        if op["kind"] == cnet.CONV:
+            k = sum(s["channels"] * s["taps"] for s in op["srcs"])
+        elif op["kind"] == cnet.CONVT:
+            k = op["srcs"][0]["channels"] * 2
+        else:
+            k = op["padding"]
+        fl = 2.0 * op["out_channels"] * k * r * frames
+        ms /= a.steps
+        tot += ms
+        rows.append((name, op["out_channels"], k, r, ms, fl / (ms * 1e-3) / 1e12))
+    for name, M, K, r, ms, tf in rows:
+        print(f"{name:28s} M {M:4d} K {K:5d} rate {r:4d}  {ms:7.3f} ms  {tf:6.1f} TF")
+    print(f"total {tot:.3f} ms")
+
+
+if __name__ == "__main__":
+    main()
