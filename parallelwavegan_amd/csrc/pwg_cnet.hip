@@ -51,6 +51,10 @@ struct CnSrc {
   int pad_mode;
   int normalize;
   float slope;
+  int taps, nc;      // thin kernel: taps, 16-channel blocks
+  int chunk_base;    // first chunk of this source (chunks: tap-major, then channel block)
+  int off_min;       // smallest tap row offset
+  int span;          // rows a 128-column block reads: 128 + off_max - off_min
 };
 
 struct CnConvArgs {
@@ -84,7 +88,7 @@ __device__ __forceinline__ int reflect_row(int p, int T) {
   return p < 0 ? 0 : (p >= T ? T - 1 : p);  // masked columns / tiny T: stay in bounds
 }
 
-template <int MT>
+template <int MT, int NT>
 __global__ void __launch_bounds__(256) pwg_cnet_conv_kernel(const CnConvArgs a) {
   __shared__ __attribute__((aligned(16))) float s_a[2][MT * 512];
   const int lane = threadIdx.x & 63;
@@ -93,39 +97,38 @@ __global__ void __launch_bounds__(256) pwg_cnet_conv_kernel(const CnConvArgs a) 
   const int cl = lane & 31;
   const int2 blk = a.blocks[blockIdx.x];
   const int u = blk.x;
-  const int q = blk.y + wave * 32 + cl;   // this lane's output column (phase index space)
+  const int qb = blk.y + wave * 32 * NT + cl;  // this lane's column in n-tile 0 (phase index space)
   const int nq = a.ncols[u];
-  const bool live = q < nq;
-  const int m0 = blockIdx.y * MT;         // first m-tile of this workgroup
+  const int m0 = blockIdx.y * MT;              // first m-tile of this workgroup
 
-  // B operand of chunk c: 8 channels of one input row, pre-activation applied
-  auto bload = [&](int c) -> f32x8v {
+  // B operands of chunk c for the NT column tiles: 8 channels of one input row each
+  auto bload = [&](int c, f32x8v (&v)[NT]) {
     const ChunkDesc cd = a.chunks[c];
     const CnSrc& s = a.src[cd.src];
     const int2 sg = *reinterpret_cast<const int2*>(s.seg + 2 * u);
-    int p = q + cd.row_off;
-    bool ok = true;
-    if (s.pad_mode == PWG_PAD_REFLECT) p = reflect_row(p, sg.y);
-    else {
-      ok = p >= 0 && p < sg.y;
-      p = p < 0 ? 0 : (p >= sg.y ? sg.y - 1 : p);
-    }
     const int ch = cd.c0 + 8 * hh;
-    const float* src = s.x + (size_t)(sg.x + p) * s.ld + ch;
-    f32x8v v = *reinterpret_cast<const f32x8v*>(src);
-    if (s.normalize) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = (v[i] - a.mean[ch + i]) / a.scale[ch + i];
-    }
-    if (s.slope != 1.f) {
+    for (int n = 0; n < NT; ++n) {
+      int p = qb + 32 * n + cd.row_off;
+      bool ok = true;
+      if (s.pad_mode == PWG_PAD_REFLECT) p = reflect_row(p, sg.y);
+      else {
+        ok = p >= 0 && p < sg.y;
+        p = p < 0 ? 0 : (p >= sg.y ? sg.y - 1 : p);
+      }
+      f32x8v x = *reinterpret_cast<const f32x8v*>(s.x + (size_t)(sg.x + p) * s.ld + ch);
+      if (s.normalize) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = v[i] > 0.f ? v[i] : v[i] * s.slope;
+        for (int i = 0; i < 8; ++i) x[i] = (x[i] - a.mean[ch + i]) / a.scale[ch + i];
+      }
+      if (s.slope != 1.f) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[i] = x[i] > 0.f ? x[i] : x[i] * s.slope;
+      }
+      v[n] = ok ? x : f32x8v{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     }
-    if (!ok) v = f32x8v{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    return v;
   };
-  // A fragments of chunk c for this workgroup's MT m-tiles: MT*512 floats, 2*MT float4 per thread
-  // pair of the 256 threads (MT*128 float4 in all)
+  // A fragments of chunk c for this workgroup's MT m-tiles: MT*128 float4, spread over 256 threads
   auto aload = [&](int c, f32x4v (&r)[(MT + 1) / 2]) {
     const f32x4v* g = reinterpret_cast<const f32x4v*>(a.wfrag + ((size_t)c * a.mt_total + m0) * 512);
 #pragma unroll
@@ -143,23 +146,25 @@ __global__ void __launch_bounds__(256) pwg_cnet_conv_kernel(const CnConvArgs a) 
     }
   };
 
-  f32x16 acc[MT];
+  f32x16 acc[MT][NT];
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
+    for (int n = 0; n < NT; ++n)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[m][n][r] = 0.f;
 
   f32x4v ar[(MT + 1) / 2];
   aload(0, ar);
   astore(0, ar);
-  f32x8v bcur = bload(0);
+  f32x8v bcur[NT], bnext[NT];
+  bload(0, bcur);
   __syncthreads();
   for (int c = 0; c < a.n_chunks; ++c) {
     const bool more = c + 1 < a.n_chunks;
-    f32x8v bnext = bcur;
     if (more) {
       aload(c + 1, ar);
-      bnext = bload(c + 1);
+      bload(c + 1, bnext);
     }
     const f32x4v* sa = reinterpret_cast<const f32x4v*>(s_a[c & 1]) + lane;
 #pragma unroll
@@ -171,14 +176,144 @@ __global__ void __launch_bounds__(256) pwg_cnet_conv_kernel(const CnConvArgs a) 
       for (int e = 0; e < 4; ++e)
 #pragma unroll
         for (int m = 0; m < MT; ++m)
-          acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m][e], bcur[4 * sub + e], acc[m], 0, 0, 0);
+#pragma unroll
+          for (int n = 0; n < NT; ++n)
+            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m][e], bcur[n][4 * sub + e], acc[m][n], 0, 0, 0);
     }
     if (more) astore((c + 1) & 1, ar);
     __syncthreads();
-    bcur = bnext;
+#pragma unroll
+    for (int n = 0; n < NT; ++n) bcur[n] = bnext[n];
   }
 
   // epilogue
+  const int2 sd = *reinterpret_cast<const int2*>(a.seg_dst + 2 * u);
+  const int2 sr = a.res ? *reinterpret_cast<const int2*>(a.seg_res + 2 * u) : make_int2(0, 0);
+  const bool quad = (a.ld_dst & 3) == 0;
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    const int q = qb + 32 * n;
+    if (q >= nq) continue;
+    const int t = q * a.ostride + a.ophase;
+    float* yrow = a.y + (size_t)(sd.x + t) * a.ld_dst;
+    const float* rrow = a.res ? a.res + (size_t)(sr.x + t) * a.ld_res : nullptr;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int j4 = 0; j4 < 4; ++j4) {
+        const int row = 32 * (m0 + m) + 8 * j4 + 4 * hh;
+        if (row >= a.M) {
+          // padding channels of a padded buffer are written as zeros: later ops read whole chunks
+          if (quad && row < a.ld_dst) *reinterpret_cast<f32x4v*>(yrow + row) = f32x4v{0.f, 0.f, 0.f, 0.f};
+          continue;
+        }
+        const f32x4v b = *reinterpret_cast<const f32x4v*>(a.bias + row);
+        f32x4v v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = acc[m][n][4 * j4 + i] + b[i];
+        if (quad) {
+          if (rrow) v += *reinterpret_cast<const f32x4v*>(rrow + row);
+          if (a.accumulate) v = *reinterpret_cast<const f32x4v*>(yrow + row) + v;
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if (row + i >= a.M) continue;
+            if (rrow) v[i] += rrow[row + i];
+            if (a.accumulate) v[i] = yrow[row + i] + v[i];
+          }
+        }
+        if (a.out_div != 1.f) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = v[i] / a.out_div;
+        }
+        if (a.post_act == PWG_ACT_LRELU) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = v[i] > 0.f ? v[i] : v[i] * a.post_slope;
+        } else if (a.post_act == PWG_ACT_TANH) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = tanhf(v[i]);
+        }
+        if (quad) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (row + i >= a.M) v[i] = 0.f;
+          *reinterpret_cast<f32x4v*>(yrow + row) = v;
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (row + i < a.M) yrow[row + i] = v[i];
+        }
+      }
+  }
+}
+
+// Thin outputs (M <= 8: the last conv of a generator, 1 or 4 channels). A 32-row MFMA tile would
+// be >= 75 % zero rows, so one THREAD computes all M outputs of one column on the VALU: per K
+// chunk it loads its 16 input channels (pre-activation and edge mode as in the MFMA kernel) and
+// FMAs them with the M x 16 weights, which are wave-uniform scalar loads from the same packed
+// fragments (chunk c, m-tile 0: output o / channel c0+8h+i sit at lane o+32h, k-step i).
+constexpr int THIN_MAX_SPAN = 128 + 512;
+template <int M>
+__global__ void __launch_bounds__(128) pwg_cnet_thin_kernel(const CnConvArgs a, int nsrc) {
+  __shared__ __attribute__((aligned(16))) float s_x[THIN_MAX_SPAN * 16];
+  const int2 blk = a.blocks[blockIdx.x];
+  const int u = blk.x;
+  const int q = blk.y + threadIdx.x;
+  const bool live = q < a.ncols[u];
+  float acc[M];
+#pragma unroll
+  for (int o = 0; o < M; ++o) acc[o] = 0.f;
+  for (int si = 0; si < nsrc; ++si) {
+    const CnSrc& s = a.src[si];
+    const int2 sg = *reinterpret_cast<const int2*>(s.seg + 2 * u);
+    for (int cb = 0; cb < s.nc; ++cb) {
+      // stage rows [q0 + off_min, q0 + off_min + span) x 16 channels, pre-activation applied once
+      __syncthreads();
+      for (int i = threadIdx.x; i < s.span * 4; i += 128) {
+        const int r = i >> 2, qd = i & 3;
+        int p = blk.y + s.off_min + r;
+        bool ok = true;
+        if (s.pad_mode == PWG_PAD_REFLECT) p = reflect_row(p, sg.y);
+        else {
+          ok = p >= 0 && p < sg.y;
+          p = p < 0 ? 0 : (p >= sg.y ? sg.y - 1 : p);
+        }
+        const int ch = 16 * cb + 4 * qd;
+        f32x4v v = *reinterpret_cast<const f32x4v*>(s.x + (size_t)(sg.x + p) * s.ld + ch);
+        if (s.normalize) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = (v[e] - a.mean[ch + e]) / a.scale[ch + e];
+        }
+        if (s.slope != 1.f) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * s.slope;
+        }
+        *reinterpret_cast<f32x4v*>(s_x + 16 * r + 4 * qd) = ok ? v : f32x4v{0.f, 0.f, 0.f, 0.f};
+      }
+      __syncthreads();
+      for (int k = 0; k < s.taps; ++k) {
+        const int c = s.chunk_base + k * s.nc + cb;
+        const int r = threadIdx.x + a.chunks[c].row_off - s.off_min;
+        const float* xr = s_x + 16 * r;
+        const float* wf = a.wfrag + (size_t)c * a.mt_total * 512;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f32x4v x0 = *reinterpret_cast<const f32x4v*>(xr + 8 * h);
+          const f32x4v x1 = *reinterpret_cast<const f32x4v*>(xr + 8 * h + 4);
+#pragma unroll
+          for (int o = 0; o < M; ++o) {
+            // k-step i = 4 sub + e of lane o + 32 h: W[o][16 cb + 8 h + i][k]
+            const f32x4v w0 = *reinterpret_cast<const f32x4v*>(wf + (o + 32 * h) * 4);
+            const f32x4v w1 = *reinterpret_cast<const f32x4v*>(wf + 256 + (o + 32 * h) * 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[o] = fmaf(w0[e], x0[e], acc[o]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[o] = fmaf(w1[e], x1[e], acc[o]);
+          }
+        }
+      }
+    }
+  }
   if (!live) return;
   const int t = q * a.ostride + a.ophase;
   const int2 sd = *reinterpret_cast<const int2*>(a.seg_dst + 2 * u);
@@ -188,54 +323,18 @@ __global__ void __launch_bounds__(256) pwg_cnet_conv_kernel(const CnConvArgs a) 
     const int2 sr = *reinterpret_cast<const int2*>(a.seg_res + 2 * u);
     rrow = a.res + (size_t)(sr.x + t) * a.ld_res;
   }
-  const bool quad = (a.ld_dst & 3) == 0;
 #pragma unroll
-  for (int m = 0; m < MT; ++m)
-#pragma unroll
-    for (int j4 = 0; j4 < 4; ++j4) {
-      const int row = 32 * (m0 + m) + 8 * j4 + 4 * hh;
-      if (row >= a.M) {
-        // padding channels of a padded buffer are written as zeros: later ops read whole chunks
-        if (quad && row < a.ld_dst) *reinterpret_cast<f32x4v*>(yrow + row) = f32x4v{0.f, 0.f, 0.f, 0.f};
-        continue;
-      }
-      const f32x4v b = *reinterpret_cast<const f32x4v*>(a.bias + row);
-      f32x4v v;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = acc[m][4 * j4 + i] + b[i];
-      if (quad) {
-        if (rrow) v += *reinterpret_cast<const f32x4v*>(rrow + row);
-        if (a.accumulate) v = *reinterpret_cast<const f32x4v*>(yrow + row) + v;
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          if (row + i >= a.M) continue;
-          if (rrow) v[i] += rrow[row + i];
-          if (a.accumulate) v[i] = yrow[row + i] + v[i];
-        }
-      }
-      if (a.out_div != 1.f) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = v[i] / a.out_div;
-      }
-      if (a.post_act == PWG_ACT_LRELU) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = v[i] > 0.f ? v[i] : v[i] * a.post_slope;
-      } else if (a.post_act == PWG_ACT_TANH) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = tanhf(v[i]);
-      }
-      if (quad) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (row + i >= a.M) v[i] = 0.f;
-        *reinterpret_cast<f32x4v*>(yrow + row) = v;
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (row + i < a.M) yrow[row + i] = v[i];
-      }
-    }
+  for (int o = 0; o < M; ++o) {
+    if (o >= a.M) break;
+    float v = acc[o] + a.bias[o];
+    if (rrow) v += rrow[o];
+    if (a.accumulate) v = yrow[o] + v;
+    if (a.out_div != 1.f) v = v / a.out_div;
+    if (a.post_act == PWG_ACT_LRELU) v = v > 0.f ? v : v * a.post_slope;
+    else if (a.post_act == PWG_ACT_TANH) v = tanhf(v);
+    yrow[o] = v;
+  }
+  for (int o = a.M; o < a.ld_dst; ++o) yrow[o] = 0.f;  // padding channels stay zero
 }
 
 // PQMF synthesis (layers/pqmf.py:133-149): y[t] = sum_m sum_k h[m][k] * S * x[(t+k-P)/S][m] over
@@ -248,31 +347,42 @@ struct CnPqmfArgs {
   float* y;
   const int* seg_dst;
   int ld_dst;
-  const int* utt_of_row;  // dst row -> utterance
-  long long rows;
+  const int2* blocks; // (utt, first output sample) per 256-sample block
   int S, NT;
 };
 
+// One workgroup = 256 consecutive output samples of one utterance. The subband rows it needs
+// (256/S + NT/S + 1 rows x S bands) and the S x NT filter bank are staged in LDS once; each thread
+// then sums its ~NT/S taps x S bands from LDS.
+constexpr int PQ_MAX_S = 8, PQ_MAX_NT = 128, PQ_ROWS = 256 + PQ_MAX_NT;
 __global__ void __launch_bounds__(256) pwg_cnet_pqmf_kernel(const CnPqmfArgs a) {
-  const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (g >= a.rows) return;
-  const int u = a.utt_of_row[g];
+  __shared__ float s_x[PQ_ROWS * PQ_MAX_S];
+  __shared__ float s_h[PQ_MAX_S * PQ_MAX_NT];
+  const int2 blk = a.blocks[blockIdx.x];
+  const int u = blk.x;
   const int2 sd = *reinterpret_cast<const int2*>(a.seg_dst + 2 * u);
   const int2 ss = *reinterpret_cast<const int2*>(a.seg_src + 2 * u);
-  const int t = (int)(g - sd.x);
-  const int P = a.NT / 2;
-  float acc = 0.f;
-  // k with (t + k - P) % S == 0: k = k0, k0 + S, ...
-  const int r = ((P - t) % a.S + a.S) % a.S;
-  for (int k = r; k < a.NT; k += a.S) {
-    const int n = t + k - P;
-    if (n < 0) continue;
-    const int j = n / a.S;
-    if (j >= ss.y) break;
-    const float* xr = a.x + (size_t)(ss.x + j) * a.ld_src;
-    for (int m = 0; m < a.S; ++m) acc = fmaf(a.h[m * a.NT + k], (float)a.S * xr[m], acc);
+  const int S = a.S, NT = a.NT, P = NT / 2;
+  const int t0 = blk.y;
+  // subband rows j with S*j in [t0 - P, t0 + 255 + NT - 1 - P]
+  const int j0 = (t0 - P) >= 0 ? (t0 - P) / S : -((P - t0 + S - 1) / S);
+  const int nrow = (t0 + 255 + NT - 1 - P) / S - j0 + 1;
+  for (int i = threadIdx.x; i < nrow * S; i += 256) {
+    const int r = i / S, m = i - r * S;
+    const int j = j0 + r;
+    s_x[i] = (j >= 0 && j < ss.y) ? (float)S * a.x[(size_t)(ss.x + j) * a.ld_src + m] : 0.f;
   }
-  a.y[(size_t)g * a.ld_dst] = acc;
+  for (int i = threadIdx.x; i < S * NT; i += 256) s_h[i] = a.h[i];
+  __syncthreads();
+  const int t = t0 + threadIdx.x;
+  if (t >= sd.y) return;
+  float acc = 0.f;
+  const int r0 = ((P - t) % S + S) % S;  // first tap k with (t + k - P) % S == 0
+  for (int k = r0; k < NT; k += S) {
+    const int rr = (t + k - P) / S - j0;  // exact division
+    for (int m = 0; m < S; ++m) acc = fmaf(s_h[m * NT + k], s_x[rr * S + m], acc);
+  }
+  a.y[(size_t)(sd.x + t) * a.ld_dst] = acc;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -286,6 +396,10 @@ struct OpPhase {          // one launch
   ChunkDesc* d_chunks = nullptr;
   int ostride, ophase;
   int k_a, off_a;         // CONVT
+  int NT;                 // column tiles per wave (workgroup = 4 waves x NT x 32 columns)
+  bool thin = false;      // M <= 8: VALU kernel with an LDS-staged input tile
+  int thin_taps[2] = {0, 0}, thin_nc[2] = {0, 0}, thin_base[2] = {0, 0}, thin_off_min[2] = {0, 0},
+      thin_span[2] = {0, 0};
 };
 
 }  // namespace
@@ -317,7 +431,6 @@ struct PwgCnetPlan {
   std::vector<int2*> d_blocks;               // per phase
   std::vector<int> n_blocks;
   std::vector<int*> d_ncols;                 // per phase
-  std::vector<int*> d_uttrow;                // per op (PQMF): dst row -> utt
 };
 
 namespace {
@@ -395,12 +508,13 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
       const PwgCnetSrc& s = op.src[0];
       if (s.buf < 0 || s.buf >= n_bufs || op.stride < 1 || channels[s.buf] < op.stride ||
           rate[op.dst] != op.stride * rate[s.buf] || op.out_channels != 1 || op.padding < 1 || op.padding % 2 == 0 ||
+          op.stride > PQ_MAX_S || op.padding > PQ_MAX_NT ||
           !check_w(s.w_off, (long long)op.stride * op.padding)) {
         delete n;
         return fail(PWG_ERR_INVALID, where + "bad PQMF op");
       }
       OpPhase ph;
-      ph.op = oi; ph.phase = 0; ph.MT = 0; ph.mt_total = 0; ph.frag_off = off; ph.bias_off = -1;
+      ph.op = oi; ph.phase = 0; ph.MT = 0; ph.mt_total = 0; ph.frag_off = off; ph.bias_off = -1; ph.NT = 1;
       ph.ostride = 1; ph.ophase = 0;
       off += (long long)op.stride * op.padding;
       n->phases.push_back(ph);
@@ -457,6 +571,7 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
     for (int r = 0; r < n_phase; ++r) {
       OpPhase ph;
       ph.op = oi; ph.phase = r; ph.MT = MT; ph.mt_total = mt_total;
+      ph.NT = 1;  // NT 2/4 for thin row tiles measured SLOWER (fewer workgroups in flight)
       ph.ostride = op.kind == PWG_CNET_CONVT ? op.stride : 1;
       ph.ophase = r;
       if (op.kind == PWG_CNET_CONVT) {
@@ -475,6 +590,22 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
         }
       }
       if (ph.chunks.size() > (size_t)CN_MAX_CHUNKS) { delete n; return fail(PWG_ERR_UNSUPPORTED, where + "K too large"); }
+      if (op.kind == PWG_CNET_CONV && op.out_channels <= 8 && n->ld[op.dst] <= 16) {
+        ph.thin = true;
+        int base = 0;
+        for (int s2 = 0; s2 < nsrc; ++s2) {
+          const PwgCnetSrc& src = op.src[s2];
+          const int lo = std::min(-src.pad, -src.pad + (src.taps - 1) * src.dilation);
+          const int hi = std::max(-src.pad, -src.pad + (src.taps - 1) * src.dilation);
+          ph.thin_taps[s2] = src.taps;
+          ph.thin_nc[s2] = (src.channels + CN_CHUNK - 1) / CN_CHUNK;
+          ph.thin_base[s2] = base;
+          ph.thin_off_min[s2] = lo;
+          ph.thin_span[s2] = CN_COLS + hi - lo;
+          base += src.taps * ph.thin_nc[s2];
+          if (ph.thin_span[s2] > THIN_MAX_SPAN) ph.thin = false;
+        }
+      }
       for (const ChunkDesc& cd : ph.chunks)
         if (cd.c0 + CN_CHUNK > n->ld[op.src[cd.src].buf]) {
           delete n;
@@ -628,38 +759,31 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
     const PwgCnetOp& op = n->ops[ph.op];
     std::vector<int2> blocks;
     std::vector<int> ncols(n_utts);
-    std::vector<int> uttrow;
     if (op.kind == PWG_CNET_PQMF) {
-      uttrow.resize(p->rows[op.dst]);
       for (int u = 0; u < n_utts; ++u) {
-        const int base = seg[((size_t)op.dst * n_utts + u) * 2], r = seg[((size_t)op.dst * n_utts + u) * 2 + 1];
-        for (int i = 0; i < r; ++i) uttrow[base + i] = u;
+        const long long T = frames[u] * n->rate[op.dst];
+        for (long long t0 = 0; t0 < T; t0 += 256) blocks.push_back(make_int2(u, (int)t0));
       }
     } else {
       for (int u = 0; u < n_utts; ++u) {
         const long long T = frames[u] * n->rate[op.dst];
         const int nq = (int)((T - ph.ophase + ph.ostride - 1) / ph.ostride);
         ncols[u] = nq;
-        for (int q0 = 0; q0 < nq; q0 += CN_COLS) blocks.push_back(make_int2(u, q0));
+        const int cols = ph.thin ? CN_COLS : CN_COLS * ph.NT;
+        for (int q0 = 0; q0 < nq; q0 += cols) blocks.push_back(make_int2(u, q0));
       }
     }
     int2* db = nullptr;
     int* dn = nullptr;
-    int* dr = nullptr;
     if (e == hipSuccess && !blocks.empty()) {
       e = hipMalloc(&db, sizeof(int2) * blocks.size());
       if (e == hipSuccess) e = hipMemcpy(db, blocks.data(), sizeof(int2) * blocks.size(), hipMemcpyHostToDevice);
       if (e == hipSuccess) e = hipMalloc(&dn, sizeof(int) * n_utts);
       if (e == hipSuccess) e = hipMemcpy(dn, ncols.data(), sizeof(int) * n_utts, hipMemcpyHostToDevice);
     }
-    if (e == hipSuccess && !uttrow.empty()) {
-      e = hipMalloc(&dr, sizeof(int) * uttrow.size());
-      if (e == hipSuccess) e = hipMemcpy(dr, uttrow.data(), sizeof(int) * uttrow.size(), hipMemcpyHostToDevice);
-    }
     p->d_blocks.push_back(db);
     p->n_blocks.push_back((int)blocks.size());
     p->d_ncols.push_back(dn);
-    p->d_uttrow.push_back(dr);
   }
   if (e != hipSuccess) {
     const int rc = hipf(e, "cnet plan upload");
@@ -676,7 +800,6 @@ void pwg_cnet_plan_destroy(PwgCnetPlan* p) {
   if (p->d_seg) (void)hipFree(p->d_seg);
   for (auto* x : p->d_blocks) if (x) (void)hipFree(x);
   for (auto* x : p->d_ncols) if (x) (void)hipFree(x);
-  for (auto* x : p->d_uttrow) if (x) (void)hipFree(x);
   delete p;
 }
 
@@ -715,8 +838,8 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
       CnPqmfArgs a;
       a.x = bufs[op.src[0].buf]; a.seg_src = seg_of(op.src[0].buf); a.ld_src = n->ld[op.src[0].buf];
       a.h = packed + ph.frag_off; a.y = bufs[op.dst]; a.seg_dst = seg_of(op.dst); a.ld_dst = n->ld[op.dst];
-      a.utt_of_row = p->d_uttrow[pi]; a.rows = p->rows[op.dst]; a.S = op.stride; a.NT = op.padding;
-      hipLaunchKernelGGL(pwg_cnet_pqmf_kernel, dim3((unsigned)((a.rows + 255) / 256)), dim3(256), 0, s, a);
+      a.blocks = p->d_blocks[pi]; a.S = op.stride; a.NT = op.padding;
+      hipLaunchKernelGGL(pwg_cnet_pqmf_kernel, dim3((unsigned)p->n_blocks[pi]), dim3(256), 0, s, a);
     } else if (p->n_blocks[pi] > 0) {
       CnConvArgs a;
       const int nsrc = (op.src[1].buf >= 0 && op.kind == PWG_CNET_CONV) ? 2 : 1;
@@ -728,6 +851,8 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
           d.pad_mode = op.kind == PWG_CNET_CONVT ? PWG_PAD_ZERO : src.pad_mode;
           d.normalize = src.normalize && mean && scale;  // normalize_before: caller passes stats
           d.slope = src.pre_slope;
+          d.taps = ph.thin_taps[si]; d.nc = ph.thin_nc[si]; d.chunk_base = ph.thin_base[si];
+          d.off_min = ph.thin_off_min[si]; d.span = ph.thin_span[si];
         } else {
           d = a.src[0];
         }
@@ -741,11 +866,17 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
       a.blocks = p->d_blocks[pi]; a.ncols = p->d_ncols[pi]; a.ostride = ph.ostride; a.ophase = ph.ophase;
       a.mean = mean; a.scale = scale;
       const dim3 grid((unsigned)p->n_blocks[pi], (unsigned)(ph.mt_total / ph.MT)), block(256);
+      if (ph.thin) {
+        const dim3 tgrid((unsigned)p->n_blocks[pi]), tblock(CN_COLS);
+        if (op.out_channels <= 1) hipLaunchKernelGGL(pwg_cnet_thin_kernel<1>, tgrid, tblock, 0, s, a, nsrc);
+        else if (op.out_channels <= 4) hipLaunchKernelGGL(pwg_cnet_thin_kernel<4>, tgrid, tblock, 0, s, a, nsrc);
+        else hipLaunchKernelGGL(pwg_cnet_thin_kernel<8>, tgrid, tblock, 0, s, a, nsrc);
+      } else
       switch (ph.MT) {
-        case 1: hipLaunchKernelGGL(pwg_cnet_conv_kernel<1>, grid, block, 0, s, a); break;
-        case 2: hipLaunchKernelGGL(pwg_cnet_conv_kernel<2>, grid, block, 0, s, a); break;
-        case 3: hipLaunchKernelGGL(pwg_cnet_conv_kernel<3>, grid, block, 0, s, a); break;
-        default: hipLaunchKernelGGL(pwg_cnet_conv_kernel<4>, grid, block, 0, s, a); break;
+        case 1: hipLaunchKernelGGL((pwg_cnet_conv_kernel<1, 1>), grid, block, 0, s, a); break;
+        case 2: hipLaunchKernelGGL((pwg_cnet_conv_kernel<2, 1>), grid, block, 0, s, a); break;
+        case 3: hipLaunchKernelGGL((pwg_cnet_conv_kernel<3, 1>), grid, block, 0, s, a); break;
+        default: hipLaunchKernelGGL((pwg_cnet_conv_kernel<4, 1>), grid, block, 0, s, a); break;
       }
     }
     hipError_t e = hipGetLastError();
