@@ -36,6 +36,10 @@ typedef float f32x8v __attribute__((ext_vector_type(8)));
 constexpr int CN_COLS = 128;       // output columns per workgroup (4 waves x 32)
 constexpr int CN_CHUNK = 16;       // input channels per K chunk
 constexpr int CN_MAX_CHUNKS = 4096;
+#ifndef PWG_CNET_G
+#define PWG_CNET_G 1  // 2 (two chunks per barrier) measured 9 % slower on HiFiGAN v1
+#endif
+constexpr int CN_G = PWG_CNET_G;   // 16-channel chunks staged per barrier
 
 struct ChunkDesc {   // one K chunk of an op (uniform per launch)
   int src;           // 0 / 1
@@ -88,9 +92,9 @@ __device__ __forceinline__ int reflect_row(int p, int T) {
   return p < 0 ? 0 : (p >= T ? T - 1 : p);  // masked columns / tiny T: stay in bounds
 }
 
-template <int MT, int NT>
+template <int MT, int NT, int G>
 __global__ void __launch_bounds__(256) pwg_cnet_conv_kernel(const CnConvArgs a) {
-  __shared__ __attribute__((aligned(16))) float s_a[2][MT * 512];
+  __shared__ __attribute__((aligned(16))) float s_a[2][G * MT * 512];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int hh = lane >> 5;
@@ -101,12 +105,20 @@ __global__ void __launch_bounds__(256) pwg_cnet_conv_kernel(const CnConvArgs a) 
   const int nq = a.ncols[u];
   const int m0 = blockIdx.y * MT;              // first m-tile of this workgroup
 
-  // B operands of chunk c for the NT column tiles: 8 channels of one input row each
-  auto bload = [&](int c, f32x8v (&v)[NT]) {
+  // B operands of chunk c for the NT column tiles: 8 channels of one input row each. The load
+  // (braw) and the pre-activation (bprep) are split so the raw loads of chunk c+1 stay in flight
+  // during chunk c's MFMAs: processing them right after issue would wait for them there.
+  struct BRaw {
+    f32x8v v[NT];
+    bool ok[NT];
+    int c;
+  };
+  auto braw = [&](int c, BRaw& r) {
     const ChunkDesc cd = a.chunks[c];
     const CnSrc& s = a.src[cd.src];
     const int2 sg = *reinterpret_cast<const int2*>(s.seg + 2 * u);
     const int ch = cd.c0 + 8 * hh;
+    r.c = c;
 #pragma unroll
     for (int n = 0; n < NT; ++n) {
       int p = qb + 32 * n + cd.row_off;
@@ -116,7 +128,17 @@ __global__ void __launch_bounds__(256) pwg_cnet_conv_kernel(const CnConvArgs a) 
         ok = p >= 0 && p < sg.y;
         p = p < 0 ? 0 : (p >= sg.y ? sg.y - 1 : p);
       }
-      f32x8v x = *reinterpret_cast<const f32x8v*>(s.x + (size_t)(sg.x + p) * s.ld + ch);
+      r.v[n] = *reinterpret_cast<const f32x8v*>(s.x + (size_t)(sg.x + p) * s.ld + ch);
+      r.ok[n] = ok;
+    }
+  };
+  auto bprep = [&](const BRaw& r, f32x8v (&v)[NT]) {
+    const ChunkDesc cd = a.chunks[r.c];
+    const CnSrc& s = a.src[cd.src];
+    const int ch = cd.c0 + 8 * hh;
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+      f32x8v x = r.v[n];
       if (s.normalize) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) x[i] = (x[i] - a.mean[ch + i]) / a.scale[ch + i];
@@ -125,24 +147,31 @@ __global__ void __launch_bounds__(256) pwg_cnet_conv_kernel(const CnConvArgs a) 
 #pragma unroll
         for (int i = 0; i < 8; ++i) x[i] = x[i] > 0.f ? x[i] : x[i] * s.slope;
       }
-      v[n] = ok ? x : f32x8v{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      v[n] = r.ok[n] ? x : f32x8v{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     }
   };
-  // A fragments of chunk c for this workgroup's MT m-tiles: MT*128 float4, spread over 256 threads
-  auto aload = [&](int c, f32x4v (&r)[(MT + 1) / 2]) {
-    const f32x4v* g = reinterpret_cast<const f32x4v*>(a.wfrag + ((size_t)c * a.mt_total + m0) * 512);
+  // (G chunks are staged per barrier; the host pads the chunk list to a multiple of G with
+  // zero-weight chunks)
+  auto aload = [&](int cg, f32x4v (&r)[G][(MT + 1) / 2]) {
 #pragma unroll
-    for (int i = 0; i < (MT + 1) / 2; ++i) {
-      const int idx = threadIdx.x + 256 * i;
-      r[i] = idx < MT * 128 ? g[idx] : f32x4v{0.f, 0.f, 0.f, 0.f};
+    for (int g2 = 0; g2 < G; ++g2) {
+      const f32x4v* gp = reinterpret_cast<const f32x4v*>(a.wfrag + ((size_t)(cg * G + g2) * a.mt_total + m0) * 512);
+#pragma unroll
+      for (int i = 0; i < (MT + 1) / 2; ++i) {
+        const int idx = threadIdx.x + 256 * i;
+        r[g2][i] = idx < MT * 128 ? gp[idx] : f32x4v{0.f, 0.f, 0.f, 0.f};
+      }
     }
   };
-  auto astore = [&](int buf, const f32x4v (&r)[(MT + 1) / 2]) {
-    f32x4v* d = reinterpret_cast<f32x4v*>(s_a[buf]);
+  auto astore = [&](int buf, const f32x4v (&r)[G][(MT + 1) / 2]) {
 #pragma unroll
-    for (int i = 0; i < (MT + 1) / 2; ++i) {
-      const int idx = threadIdx.x + 256 * i;
-      if (idx < MT * 128) d[idx] = r[i];
+    for (int g2 = 0; g2 < G; ++g2) {
+      f32x4v* d = reinterpret_cast<f32x4v*>(s_a[buf] + g2 * MT * 512);
+#pragma unroll
+      for (int i = 0; i < (MT + 1) / 2; ++i) {
+        const int idx = threadIdx.x + 256 * i;
+        if (idx < MT * 128) d[idx] = r[g2][i];
+      }
     }
   };
 
@@ -154,36 +183,50 @@ __global__ void __launch_bounds__(256) pwg_cnet_conv_kernel(const CnConvArgs a) 
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[m][n][r] = 0.f;
 
-  f32x4v ar[(MT + 1) / 2];
+  f32x4v ar[G][(MT + 1) / 2];
   aload(0, ar);
   astore(0, ar);
-  f32x8v bcur[NT], bnext[NT];
-  bload(0, bcur);
+  f32x8v bcur[G][NT];
+  BRaw bnext[G];
+#pragma unroll
+  for (int g2 = 0; g2 < G; ++g2) {
+    braw(g2, bnext[g2]);
+    bprep(bnext[g2], bcur[g2]);
+  }
   __syncthreads();
-  for (int c = 0; c < a.n_chunks; ++c) {
-    const bool more = c + 1 < a.n_chunks;
+  const int n_groups = a.n_chunks / G;
+  for (int cg = 0; cg < n_groups; ++cg) {
+    const bool more = cg + 1 < n_groups;
     if (more) {
-      aload(c + 1, ar);
-      bload(c + 1, bnext);
+      aload(cg + 1, ar);
+#pragma unroll
+      for (int g2 = 0; g2 < G; ++g2) braw((cg + 1) * G + g2, bnext[g2]);
     }
-    const f32x4v* sa = reinterpret_cast<const f32x4v*>(s_a[c & 1]) + lane;
+    __builtin_amdgcn_sched_barrier(0);  // keep the loads issued before the MFMAs below
 #pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
-      f32x4v av[MT];
+    for (int g2 = 0; g2 < G; ++g2) {
+      const f32x4v* sa = reinterpret_cast<const f32x4v*>(s_a[cg & 1] + g2 * MT * 512) + lane;
 #pragma unroll
-      for (int m = 0; m < MT; ++m) av[m] = sa[(m * 2 + sub) * 64];
+      for (int sub = 0; sub < 2; ++sub) {
+        f32x4v av[MT];
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
+        for (int m = 0; m < MT; ++m) av[m] = sa[(m * 2 + sub) * 64];
 #pragma unroll
-        for (int m = 0; m < MT; ++m)
+        for (int e = 0; e < 4; ++e)
 #pragma unroll
-          for (int n = 0; n < NT; ++n)
-            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m][e], bcur[n][4 * sub + e], acc[m][n], 0, 0, 0);
+          for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int n = 0; n < NT; ++n)
+              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m][e], bcur[g2][n][4 * sub + e], acc[m][n], 0, 0, 0);
+      }
     }
-    if (more) astore((c + 1) & 1, ar);
+    __builtin_amdgcn_sched_barrier(0);  // ... and their consumers after them
+    if (more) astore((cg + 1) & 1, ar);
     __syncthreads();
+    if (more) {
 #pragma unroll
-    for (int n = 0; n < NT; ++n) bcur[n] = bnext[n];
+      for (int g2 = 0; g2 < G; ++g2) bprep(bnext[g2], bcur[g2]);
+    }
   }
 
   // epilogue
@@ -397,6 +440,7 @@ struct OpPhase {          // one launch
   int ostride, ophase;
   int k_a, off_a;         // CONVT
   int NT;                 // column tiles per wave (workgroup = 4 waves x NT x 32 columns)
+  int n_real_chunks = 0;  // chunks before padding to a multiple of CN_G (the rest pack as zeros)
   bool thin = false;      // M <= 8: VALU kernel with an LDS-staged input tile
   int thin_taps[2] = {0, 0}, thin_nc[2] = {0, 0}, thin_base[2] = {0, 0}, thin_off_min[2] = {0, 0},
       thin_span[2] = {0, 0};
@@ -589,6 +633,8 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
             for (int c = 0; c < cs; ++c) ph.chunks.push_back({s, -src.pad + k * src.dilation, c * CN_CHUNK, 0});
         }
       }
+      ph.n_real_chunks = (int)ph.chunks.size();
+      while (ph.chunks.size() % CN_G) ph.chunks.push_back(ph.chunks.back());  // zero-weight padding
       if (ph.chunks.size() > (size_t)CN_MAX_CHUNKS) { delete n; return fail(PWG_ERR_UNSUPPORTED, where + "K too large"); }
       if (op.kind == PWG_CNET_CONV && op.out_channels <= 8 && n->ld[op.dst] <= 16) {
         ph.thin = true;
@@ -645,7 +691,7 @@ int pwg_cnet_pack_weights(const PwgCnet* n, const float* ref, float* packed) {
       continue;
     }
     // A fragments: [chunk][m][sub][lane][e], k-step i = 4 sub + e pairs channels c0+i / c0+8+i
-    for (size_t c = 0; c < ph.chunks.size(); ++c) {
+    for (size_t c = 0; c < (size_t)ph.n_real_chunks; ++c) {
       const ChunkDesc& cd = ph.chunks[c];
       const PwgCnetSrc& src = op.src[cd.src];
       const int tap = op.kind == PWG_CNET_CONVT ? ph.off_a - cd.row_off   // 0 or 1
@@ -873,10 +919,10 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         else hipLaunchKernelGGL(pwg_cnet_thin_kernel<8>, tgrid, tblock, 0, s, a, nsrc);
       } else
       switch (ph.MT) {
-        case 1: hipLaunchKernelGGL((pwg_cnet_conv_kernel<1, 1>), grid, block, 0, s, a); break;
-        case 2: hipLaunchKernelGGL((pwg_cnet_conv_kernel<2, 1>), grid, block, 0, s, a); break;
-        case 3: hipLaunchKernelGGL((pwg_cnet_conv_kernel<3, 1>), grid, block, 0, s, a); break;
-        default: hipLaunchKernelGGL((pwg_cnet_conv_kernel<4, 1>), grid, block, 0, s, a); break;
+        case 1: hipLaunchKernelGGL((pwg_cnet_conv_kernel<1, 1, CN_G>), grid, block, 0, s, a); break;
+        case 2: hipLaunchKernelGGL((pwg_cnet_conv_kernel<2, 1, CN_G>), grid, block, 0, s, a); break;
+        case 3: hipLaunchKernelGGL((pwg_cnet_conv_kernel<3, 1, CN_G>), grid, block, 0, s, a); break;
+        default: hipLaunchKernelGGL((pwg_cnet_conv_kernel<4, 1, CN_G>), grid, block, 0, s, a); break;
       }
     }
     hipError_t e = hipGetLastError();
