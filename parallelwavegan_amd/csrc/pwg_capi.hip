@@ -843,7 +843,7 @@ int pwg_set_option(PwgHandle* h, int option, long long value) {
       h->layer_kernel = (int)value;
       return PWG_OK;
     case PWG_OPT_WAVES_PER_WG:
-      if (value < 1 || value > 8) return fail(PWG_ERR_INVALID, "waves per workgroup must be in [1, 8]");
+      if (value < 1 || value > 16) return fail(PWG_ERR_INVALID, "waves per workgroup must be in [1, 16]");
       h->waves_per_wg = (int)value;
       return PWG_OK;
     case PWG_OPT_WG_PER_CU:

@@ -547,10 +547,16 @@ __device__ __forceinline__ void store_stream(float* wave_base, int byte_off, f32
 #endif
 }
 
+#ifndef PWG_PERSIST_THREADS
+#define PWG_PERSIST_THREADS 512
+#endif
 // RC / SC: compile-time residual / skip channels for the production shapes (0 = runtime).
 // 8 waves per CU (2 per SIMD): measured faster than 12 with the XCD-local schedule (L2 footprint).
-template <int MT, int M2T, int M3T, int GK, int RC, int SC>
-__global__ void __launch_bounds__(512, 1) pwg_layer_persistent_kernel(const PersistArgs a) {
+#ifndef PWG_BPF
+#define PWG_BPF 2  // B groups in flight ahead of the MFMAs (compile-time-K instances)
+#endif
+template <int MT, int M2T, int M3T, int GK, int RC, int SC, int KSC>
+__global__ void __launch_bounds__(PWG_PERSIST_THREADS, 1) pwg_layer_persistent_kernel(const PersistArgs a) {
   using SM = PersistSmem<MT, M2T, M3T>;
   constexpr int NB = GK / 4;                                   // 4-k-step slices per group
   typedef float bvec __attribute__((ext_vector_type(GK)));   // one lane's B operands of a group
@@ -568,8 +574,21 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_persistent_kernel(const Pers
   const int RS = RC ? (RC + KC - 1) / KC * KC : a.RS;
   const int SS = SC ? (SC + 3) / 4 * 4 : a.SS;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int K1 = a.KS * RS;
+  const int KS = KSC ? KSC : a.KS;
+  const int K1 = KS * RS;
   const int NGRP = K1 / (2 * GK);
+  // compile-time K (KSC, RC): GEMM 1 fully unrolled with a PF-deep B register ring
+#ifndef PWG_NO_UNROLL
+#define PWG_NO_UNROLL 1  // the unrolled PF-deep ring measured equal (3.87-3.88 ms) at +30-50 VGPRs
+#endif
+#if PWG_NO_UNROLL
+  constexpr int NGRP_C = 0;
+#else
+  constexpr int NGRP_C = (KSC && RC) ? KSC * ((RC + KC - 1) / KC * KC) / (2 * GK) : 0;
+#endif
+  constexpr int PF = PWG_BPF;
+  constexpr int RING = PF + 1;
+  static_assert(NGRP_C == 0 || NGRP_C % RING == 0, "ring size must divide the group count");
   float* s_wg = smem;
   float* s_w2 = s_wg + K1 / 8 * MT * 256;
   float* s_bg = s_w2 + SM::W2;
@@ -716,6 +735,12 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_persistent_kernel(const Pers
   }
   BlockDesc bdn = a.blocks[blk];  // descriptor of the block processed next (loaded a block ahead)
   bvec b0 = bload(bdn.col, 0);     // B operand of the next group (prefetched, across blocks)
+  bvec bq[RING];                   // compile-time-K path: groups g .. g+PF-1 in flight
+  if constexpr (NGRP_C > 0) {
+    bq[0] = b0;
+#pragma unroll
+    for (int i = 1; i < PF; ++i) bq[i] = bload(bdn.col, i);
+  }
 
   while (true) {
     const BlockDesc bd = bdn;
@@ -730,8 +755,18 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_persistent_kernel(const Pers
     // f = fw0 + 2s + h (a table load per k-step), A = D rows of those frames
     float bw[4];
     float dv[4][MT];
+    const int fw0 = bd.t0 / a.H - a.J1;  // wave window (uniform)
+    auto load_dv = [&]() {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int f = fw0 + 2 * s + hh;
+        const int fc = f < 0 ? 0 : (f >= ui.frames ? ui.frames - 1 : f);  // weight 0 outside
+        const float* drow = a.d + (size_t)(ui.frame_base + fc) * GR + cl;
+#pragma unroll
+        for (int m = 0; m < MT; ++m) dv[s][m] = drow[32 * m];
+      }
+    };
     {
-      const int fw0 = bd.t0 / a.H - a.J1;  // wave window (uniform)
       const int tc = live ? t : ui.T - 1;
       int roff;
       if (ui.frames < a.Fmin) roff = a.tab_small + (a.H * ui.frames * (ui.frames - 1) / 2 + tc) * AUX_J4;
@@ -746,12 +781,11 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_persistent_kernel(const Pers
         const bool ok = live && j >= 0 && j < AUX_J4 && s < a.nka;
         const float w = a.tab[roff + (j < 0 ? 0 : (j >= AUX_J4 ? AUX_J4 - 1 : j))];
         bw[s] = ok ? w : 0.f;
-        const int fc = f < 0 ? 0 : (f >= ui.frames ? ui.frames - 1 : f);  // weight 0 outside
-        const float* drow = a.d + (size_t)(ui.frame_base + fc) * GR + cl;
-#pragma unroll
-        for (int m = 0; m < MT; ++m) dv[s][m] = drow[32 * m];
       }
     }
+#if !PWG_LATE_AUX
+    load_dv();  // in flight during GEMM 1
+#endif
 
     // ---- GEMM 2 accumulators seeded with [skip_old; x_in]: the MFMA performs the skip sum and
     //      the residual add (residual_block.py:138, parallel_wavegan.py:164); pass-0 loads in flight
@@ -794,18 +828,30 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_persistent_kernel(const Pers
       for (int m = 0; m < MT; ++m)
         acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(hh == 0 ? bgv[m] : 0.f, one, zero, 0, 0, 0);
     }
-    for (int g = 0; g < NGRP; g += 2) {
-      const bvec b1 = bload(bd.col, g + 1 < NGRP ? g + 1 : g);
-      group_mfma(acc, b0, g);
-      if (g + 1 >= NGRP) {  // odd group count: b0 takes the next block's first group
-        b0 = bload(col_next, 0);
-        break;
+    if constexpr (NGRP_C > 0) {
+#pragma unroll
+      for (int g = 0; g < NGRP_C; ++g) {
+        const int gn = g + PF;  // issue group g+PF (the next block's first groups at the end)
+        bq[gn % RING] = gn < NGRP_C ? bload(bd.col, gn) : bload(col_next, gn - NGRP_C);
+        group_mfma(acc, bq[g % RING], g);
       }
-      b0 = g + 2 < NGRP ? bload(bd.col, g + 2) : bload(col_next, 0);
-      group_mfma(acc, b1, g + 1);
+    } else {
+      for (int g = 0; g < NGRP; g += 2) {
+        const bvec b1 = bload(bd.col, g + 1 < NGRP ? g + 1 : g);
+        group_mfma(acc, b0, g);
+        if (g + 1 >= NGRP) {  // odd group count: b0 takes the next block's first group
+          b0 = bload(col_next, 0);
+          break;
+        }
+        b0 = g + 2 < NGRP ? bload(bd.col, g + 2) : bload(col_next, 0);
+        group_mfma(acc, b1, g + 1);
+      }
     }
 
     PWG_TR(const unsigned long long tr_b = clock64());
+#if PWG_LATE_AUX
+    load_dv();  // 16 VGPRs fewer across GEMM 1 (3 waves/SIMD fit); latency covered by the others
+#endif
 #if !PWG_EARLY_SKIP
     init_pass(0, accp0);
 #endif
@@ -828,7 +874,9 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_persistent_kernel(const Pers
         if (MT == 1 && r >= 8) { gt[gm][r] = 0.f; continue; }
         gt[gm][r] = fast_gate(acc[gm][r], MT == 1 ? acc[0][r + 8] : acc[gm + MT / 2][r]);
       }
+#if !PWG_SEQ_PASS
     if (NPASS > 1) init_pass(1, accp1);
+#endif
     PWG_TR(const unsigned long long tr_c = clock64());
 
     auto gemm2_pass = [&](int pass, f32x16 (&acc2)[MP]) {
@@ -868,6 +916,9 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_persistent_kernel(const Pers
         }
     };
 
+#if PWG_SEQ_PASS
+    if (!LAST && NPASS > 1) init_pass(1, accp1);  // x_in rows: L2 hits, in flight during pass 0
+#endif
     gemm2_pass(0, accp0);
     if (!LAST) {
       store_pass(0, accp0);
@@ -985,16 +1036,16 @@ hipError_t launch_layer(const LayerArgs& a, int mt, int m2t, bool last, long lon
 
 hipError_t launch_layer_persistent(const PersistArgs& a, int mt, int m2t, bool last, int waves_per_wg, int n_wg,
                                    hipStream_t s) {
-  if (waves_per_wg > 8) waves_per_wg = 8;
+  if (waves_per_wg > PWG_PERSIST_THREADS / 64) waves_per_wg = PWG_PERSIST_THREADS / 64;
   const dim3 grid((unsigned)n_wg), block((unsigned)(64 * waves_per_wg));
   const int k1 = a.KS * a.RS;
   const int m3t = (a.S + 31) / 32;
   const bool gk16 = a.RS % 32 == 0;  // 32-channel groups when every tap block holds whole groups
-#define PWG_PERS_LAUNCH3(MT_, M2T_, M3T_, GK_, RC_, SC_)                                                   \
+#define PWG_PERS_LAUNCH3(MT_, M2T_, M3T_, GK_, RC_, SC_, KSC_)                                             \
   {                                                                                                        \
     const size_t lds = sizeof(float) * PersistSmem<MT_, M2T_, M3T_>::floats(k1);                           \
     if (lds > 160 * 1024) return hipErrorInvalidValue;                                                     \
-    auto kfn = &pwg_layer_persistent_kernel<MT_, M2T_, M3T_, GK_, RC_, SC_>;                               \
+    auto kfn = &pwg_layer_persistent_kernel<MT_, M2T_, M3T_, GK_, RC_, SC_, KSC_>;                         \
     hipError_t e_ = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),                                \
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);              \
     if (e_ != hipSuccess) return e_;                                                                       \
@@ -1004,9 +1055,9 @@ hipError_t launch_layer_persistent(const PersistArgs& a, int mt, int m2t, bool l
 // PWG v1 (R = S = 64) gets compile-time channel counts; other shapes the runtime kernel.
 #define PWG_PERS_LAUNCH2(MT_, M2T_, M3T_, GK_)                                          \
   {                                                                                     \
-    if (MT_ == 4 && M2T_ == 4 && a.R == 64 && a.S == 64)                                \
-      PWG_PERS_LAUNCH3(MT_, M2T_, M3T_, GK_, 64, 64)                                    \
-    else PWG_PERS_LAUNCH3(MT_, M2T_, M3T_, GK_, 0, 0)                                   \
+    if (MT_ == 4 && M2T_ == 4 && a.R == 64 && a.S == 64 && a.KS == 3)                   \
+      PWG_PERS_LAUNCH3(MT_, M2T_, M3T_, GK_, 64, 64, 3)                                 \
+    else PWG_PERS_LAUNCH3(MT_, M2T_, M3T_, GK_, 0, 0, 0)                                \
   }
 #define PWG_PERS_LAUNCH(MT_, M2T_, M3T_) \
   { if (gk16) PWG_PERS_LAUNCH2(MT_, M2T_, M3T_, 16) else PWG_PERS_LAUNCH2(MT_, M2T_, M3T_, 8) }
