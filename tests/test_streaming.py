@@ -1,0 +1,71 @@
+"""Chunked and causal-streaming inference (parallelwavegan_amd/streaming.py) reproduce the
+whole-utterance engine output BIT FOR BIT (SURVEY.md sec 8(e) long-utterance split, sec 8(f) row 3)."""
+
+import numpy as np
+import pytest
+import torch
+
+from parallelwavegan_amd import streaming
+
+
+def test_chunk_ranges_cover_exactly():
+    for causal in (False, True):
+        r = streaming.chunk_ranges(1000, 64, 17, causal)
+        assert r[0][1] == 0 and r[-1][2] == 1000
+        for (lo, s, e, hi), nxt in zip(r, r[1:] + [None]):
+            assert lo == max(0, s - 17) and (hi == e if causal else hi == min(1000, e + 17))
+            if nxt:
+                assert nxt[1] == e
+
+
+def _engine(name, cuda_device, **over):
+    from parallelwavegan_amd import Engine, configs, synthetic
+
+    params = configs.generator_params(name, **over)
+    eng = Engine(params, cuda_device)
+    eng.load_state_dict(synthetic.make_state_dict(params, seed=0))
+    return eng
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name, frames, chunk", [("ljspeech_v1", 300, 64), ("libritts_v1", 161, 40)])
+def test_chunked_equals_whole_utterance(name, frames, chunk, built_lib, cuda_device):
+    from parallelwavegan_amd import synthetic
+
+    eng = _engine(name, cuda_device)
+    H = eng.upsample_factor
+    mel = torch.from_numpy(synthetic.make_mel(frames, 80, seed=3)).to(cuda_device)
+    noise = torch.from_numpy(synthetic.make_noise(frames * H, seed=4)).to(cuda_device)
+    full = eng.infer([mel], [noise])[0].cpu().numpy()
+    y = streaming.infer_chunked(eng, mel, noise, chunk).cpu().numpy()
+    np.testing.assert_array_equal(y, full)
+    # a halo that is too short must show (the test has teeth)
+    y_bad = streaming.infer_chunked(eng, mel, noise, chunk, halo=1).cpu().numpy()
+    assert not np.array_equal(y_bad, full)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["reference_test", "ljspeech_v1"])
+def test_causal_stream_equals_whole_utterance(name, built_lib, cuda_device):
+    from parallelwavegan_amd import synthetic
+
+    eng = _engine(name, cuda_device, use_causal_conv=True)
+    A, H = eng.config.aux_channels, eng.upsample_factor
+    frames = 150
+    mel = torch.from_numpy(synthetic.make_mel(frames, A, seed=5)).to(cuda_device)
+    noise = torch.from_numpy(synthetic.make_noise(frames * H, seed=6)).to(cuda_device).reshape(-1)
+    full = eng.infer([mel], [noise])[0].cpu().numpy()
+    st = streaming.CausalStream(eng)
+    outs, f = [], 0
+    for n in (1, 7, 30, 2, 50, 60):
+        outs.append(st.push(mel[f:f + n], noise[f * H:(f + n) * H]).cpu().numpy())
+        f += n
+    assert f == frames
+    np.testing.assert_array_equal(np.concatenate(outs, 0), full)
+
+
+@pytest.mark.gpu
+def test_causal_stream_rejects_noncausal(built_lib, cuda_device):
+    eng = _engine("reference_test", cuda_device)
+    with pytest.raises(ValueError):
+        streaming.CausalStream(eng)
