@@ -70,9 +70,17 @@ def dist_setup(n_gpus):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
         local = int(os.environ.get("LOCAL_RANK", "0"))
+        # one process per GPU; PWG_BENCH_BACKEND=gloo (with ranks sharing a GPU when there are
+        # fewer GPUs than ranks) only rehearses the multi-rank path on a 1-GPU box
+        backend = os.environ.get("PWG_BENCH_BACKEND", "nccl")
+        ndev = torch.cuda.device_count()
+        local = local if backend == "nccl" else local % max(ndev, 1)
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
         return dist.get_rank(), world, dev
     if n_gpus != 1:
         print(f"[bench] --gpus {n_gpus} without torch.distributed.run: running 1 process", file=sys.stderr)
