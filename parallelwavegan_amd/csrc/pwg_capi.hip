@@ -253,7 +253,7 @@ struct PwgHandle {
   std::vector<int> dil;
   AuxStruct aux;
   // packed image offsets (floats)
-  size_t off_first_w, off_first_b, off_conv_in, off_waux;
+  size_t off_first_w, off_first_b, off_conv_in, off_conv_in_frag, off_waux;
   size_t off_tab_interior, off_tab_left, off_tab_right, off_tab_small;
   size_t off_layers, layer_stride, lo_wg, lo_bg, lo_w2;
   size_t off_head_w1, off_head_w2, off_head_b2, packed_total;
@@ -359,6 +359,7 @@ int pwg_create(const PwgConfig* cfg, int device, PwgHandle** out) {
   h->off_first_w = o; o += align64(h->R);
   h->off_first_b = o; o += align64(h->R);
   h->off_conv_in = o; o += align64((size_t)h->A * h->A * h->KW);
+  h->off_conv_in_frag = o; o += align64((size_t)(h->A * h->KW + 1) / 2 * ((h->A + 31) / 32) * 64);
   h->off_waux = o; o += align64((size_t)h->L * ((h->A + 1) / 2) * h->MT * 64);
   h->off_tab_interior = o; o += align64((size_t)h->aux.H * AUX_J4);
   h->off_tab_left = o; o += align64((size_t)std::max(h->aux.TL, 1) * AUX_J4);
@@ -424,7 +425,17 @@ int pwg_pack_weights(const PwgHandle* h, const float* ref, float* pk) {
   for (int i = 0; i < R; ++i) pk[h->off_first_w + i] = *p++;
   for (int i = 0; i < R; ++i) pk[h->off_first_b + i] = *p++;
   if (c.use_conv_in) {
-    for (size_t i = 0; i < (size_t)A * A * KW; ++i) pk[h->off_conv_in + i] = *p++;
+    for (size_t i = 0; i < (size_t)A * A * KW; ++i) pk[h->off_conv_in + i] = p[i];
+    // MFMA fragments: k-step s, lane l -> W[o = 32 m + (l & 31)][k = 2 s + (l >> 5)], k = i*KW + kk
+    const int nks = (A * KW + 1) / 2, mti = (A + 31) / 32;
+    for (int s2 = 0; s2 < nks; ++s2)
+      for (int m = 0; m < mti; ++m)
+        for (int l = 0; l < 64; ++l) {
+          const int o2 = 32 * m + (l & 31), k = 2 * s2 + (l >> 5);
+          pk[h->off_conv_in_frag + ((size_t)s2 * mti + m) * 64 + l] =
+              (o2 < A && k < A * KW) ? p[(size_t)o2 * A * KW + k] : 0.f;
+        }
+    p += (size_t)A * A * KW;
   } else {
     pk[h->off_conv_in] = 1.f;  // unused (identity path)
   }
@@ -730,6 +741,7 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
   if (e != hipSuccess) return hip_fail(e, "work-queue reset");
   ConvInArgs ca;
   ca.mel = mel; ca.mean = mean; ca.scale = scale; ca.w = packed + h->off_conv_in; ca.c1 = c1;
+  ca.wfrag = packed + h->off_conv_in_frag;
   ca.utts = p->d_utts; ca.n_utts = p->n_utts; ca.F_total = p->F_total; ca.A = h->A; ca.KW = h->KW;
   ca.ctx = h->cfg.aux_context_window; ca.layout = p->layout; ca.use_conv_in = h->cfg.use_conv_in;
   e = timed(PWG_KERNEL_CONV_IN, [&] { return launch_conv_in(ca, s); });

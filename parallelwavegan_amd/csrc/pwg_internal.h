@@ -35,6 +35,7 @@ struct ConvInArgs {
   const float* mean;     // nullable
   const float* scale;    // nullable
   const float* w;        // [A][A][KW]
+  const float* wfrag;    // MFMA A fragments [ceil(A*KW/2)][ceil(A/32)][64]: row o, k = i*KW + kk
   float* c1;             // [A][F_total]
   const UttDesc* utts;
   int n_utts;

@@ -106,6 +106,61 @@ __global__ void __launch_bounds__(256) pwg_conv_in_kernel(const ConvInArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// conv_in as an fp32 MFMA GEMM: C1[o][f] = sum_k W[o][k] X[k][f], k = i*KW + kk, X[i*KW+kk][f] =
+// the (replication-padded, normalized) input channel i at frame f + kk. M = A rows (MT m-tiles),
+// N = 32 frames per wave, K = A*KW in k-steps of 2 (lane half h takes k = 2s + h). The B operand
+// is one input value per lane and k-step (L1-resident: the mel tile is 5 frames wide).
+template <int MT>
+__global__ void __launch_bounds__(256) pwg_conv_in_mfma_kernel(const ConvInArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int hh = lane >> 5, cl = lane & 31;
+  const long long g0 = (long long)blockIdx.x * 128 + wave * 32 + cl;
+  const bool valid = g0 < a.F_total;
+  const long long g = valid ? g0 : a.F_total - 1;
+  const int u = find_utt_by_frame(a.utts, a.n_utts, g);
+  const UttDesc ud = a.utts[u];
+  const long long f = g - ud.frame_base;
+  const long long Tf = ud.frames;
+  const long long Tin = Tf + 2 * a.ctx;
+  const int K = a.A * a.KW;
+  const int nks = (K + 1) / 2;
+  f32x16 acc[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
+  int i = hh / a.KW, kk = hh - i * a.KW;  // k = 2s + hh = i*KW + kk
+  const float* wl = a.wfrag + lane;
+  for (int s = 0; s < nks; ++s) {
+    float x = 0.f;
+    if (i < a.A) {
+      const long long fp = f + kk;
+      if (a.layout == PWG_LAYOUT_INFERENCE) {
+        long long src = fp - a.ctx;
+        src = src < 0 ? 0 : (src >= Tf ? Tf - 1 : src);  // ReplicationPad1d
+        x = a.mel[ud.mel_off + src * a.A + i];
+        if (a.mean != nullptr) x = (x - a.mean[i]) / a.scale[i];
+      } else {
+        x = a.mel[ud.mel_off + (long long)i * Tin + fp];
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(wl[(s * MT + m) * 64], x, acc[m], 0, 0, 0);
+    kk += 2;
+    while (kk >= a.KW) { kk -= a.KW; ++i; }
+  }
+  if (!valid) return;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int o = 32 * m + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      if (o < a.A) a.c1[(size_t)o * a.F_total + g] = acc[m][r];
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // D[l][f][row] = sum_i Waux_l[row][i] C1[i][f] as an fp32 MFMA GEMM per layer: M = GR gate rows
 // (A fragments host-packed like the layer weights), N = 32 frames per wave (B fragment = C1 row
 // segment, 2 x 128-B reads), K = A. The accumulator's register quads are 4 consecutive rows of one
@@ -164,6 +219,8 @@ __global__ void __launch_bounds__(256) pwg_first_conv_kernel(const FirstConvArgs
   const UttDesc ud = a.utts[a.tile_utt[tile]];
   const long long col0 = ud.seg_base + (tile - ud.first_tile) * TILE;
   const long long t0 = col0 - ud.seg_base;
+  // (4-byte stores, 256 contiguous bytes per wave instruction: a 16-byte-per-lane variant measured
+  // slower, 0.87 vs 0.65 ms for the LibriTTS batch)
   for (int idx = threadIdx.x; idx < a.RS * TILE; idx += 256) {
     const int j = idx / a.RS, c = idx - j * a.RS;
     const long long t = t0 + j;
@@ -992,6 +1049,16 @@ __global__ void __launch_bounds__(PWG_PERSIST_THREADS, 1) pwg_layer_persistent_k
 
 // ---------------------------------------------------------------------------------------------
 hipError_t launch_conv_in(const ConvInArgs& a, hipStream_t s) {
+  if (a.use_conv_in && a.A <= 128) {
+    const dim3 grid((unsigned)((a.F_total + 127) / 128));
+    switch ((a.A + 31) / 32) {
+      case 1: hipLaunchKernelGGL(pwg_conv_in_mfma_kernel<1>, grid, dim3(256), 0, s, a); break;
+      case 2: hipLaunchKernelGGL(pwg_conv_in_mfma_kernel<2>, grid, dim3(256), 0, s, a); break;
+      case 3: hipLaunchKernelGGL(pwg_conv_in_mfma_kernel<3>, grid, dim3(256), 0, s, a); break;
+      default: hipLaunchKernelGGL(pwg_conv_in_mfma_kernel<4>, grid, dim3(256), 0, s, a); break;
+    }
+    return hipGetLastError();
+  }
   const dim3 grid((unsigned)((a.F_total + 63) / 64));
   const int og = (a.A + 3) / 4;
   if (og <= 8) hipLaunchKernelGGL(pwg_conv_in_kernel<8>, grid, dim3(256), 0, s, a);
