@@ -1,0 +1,15 @@
+#!/bin/bash
+# One GPU verification pass (GPU box): parity suite, smoke, default bench, rocprofv3 kernel stats.
+# Usage: bash tools/gpu_check.sh OUTDIR
+set -e
+OUT=${1:-gpurun_out/check}
+mkdir -p "$OUT"
+export TMPDIR=/tmp PWG_NO_BUILD=1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
+tail -3 "$OUT/pytest_gpu.log"
+timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
+cat "$OUT/smoke.log" | tail -1
+timeout -k 10 300 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
+cat "$OUT/bench.json"
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --cpu-seconds 0 > "$GRAFT_REPO_ROOT/$OUT/bench_prof.json" 2> "$GRAFT_REPO_ROOT/$OUT/prof.err"
+echo done
