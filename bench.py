@@ -267,7 +267,8 @@ def main():
     ap.add_argument("--utts", type=int, default=32, help="utterances per GPU per step")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "layer_traffic.json"))
-    ap.add_argument("--layer-kernel", default="persistent", choices=["persistent", "tiled"])
+    ap.add_argument("--layer-kernel", default=None, choices=["split", "persistent", "tiled"],
+                    help="default: split where the shape allows, else persistent (the engine default)")
     ap.add_argument("--waves-per-wg", type=int, default=None)
     ap.add_argument("--wg-per-cu", type=int, default=None)
     args = ap.parse_args()
@@ -279,6 +280,12 @@ def main():
     params = configs.generator_params(args.config)
     fs = configs.SAMPLING_RATE[args.config]
     eng = Engine(params, dev)
+    if args.layer_kernel is None:
+        try:
+            eng.set_option("layer_kernel", "split")
+            args.layer_kernel = "split"
+        except NotImplementedError:
+            args.layer_kernel = "persistent"
     eng.set_option("layer_kernel", args.layer_kernel)
     if args.waves_per_wg:
         eng.set_option("waves_per_wg", args.waves_per_wg)

@@ -152,7 +152,10 @@ PWG_API int pwg_run(PwgPlan* p, const float* packed, const float* mel, const flo
 /* Engine options (pwg_set_option). Defaults are the tuned values; the others exist for A/B
  * measurement (bench.py --layer-kernel ...). */
 enum {
-  PWG_OPT_LAYER_KERNEL = 0,   /* 0: persistent, weights resident in LDS (default); 1: tiled */
+  PWG_OPT_LAYER_KERNEL = 0,   /* 0: persistent fp32 MFMA, weights resident in LDS (default for shapes
+                                    the split kernel does not cover); 1: tiled fp32; 2: persistent
+                                    split-f16 (fp32 operands as fp16 hi+lo pairs, 3 f16 MFMAs per
+                                    product; default for R = S = 64, gate 128, kernel 3) */
   PWG_OPT_WAVES_PER_WG = 1,   /* persistent kernel: waves per workgroup (1..8, default 8) */
   PWG_OPT_WG_PER_CU = 2       /* persistent kernel: workgroups per CU in the grid (default 1) */
 };

@@ -22,6 +22,7 @@ CSRC = [
     os.path.join(PKG_DIR, "csrc", "pwg_kernels.hip"),
     os.path.join(PKG_DIR, "csrc", "pwg_capi.hip"),
     os.path.join(PKG_DIR, "csrc", "pwg_cnet.hip"),
+    os.path.join(PKG_DIR, "csrc", "pwg_split.hip"),
 ]
 HEADERS = [
     os.path.join(REPO_DIR, "include", "pwg.h"),

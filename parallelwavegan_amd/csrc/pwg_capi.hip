@@ -44,6 +44,43 @@ struct DeviceGuard {
   }
 };
 
+// fp16 round-to-nearest-even on the host (split-f16 weight packing); h2f is its exact inverse.
+uint16_t f2h(float f) {
+  uint32_t x;
+  std::memcpy(&x, &f, 4);
+  const uint32_t sign = (x >> 16) & 0x8000u, ax = x & 0x7fffffffu;
+  if (ax >= 0x7f800000u) return (uint16_t)(sign | (ax > 0x7f800000u ? 0x7e00u : 0x7c00u));
+  if (ax >= 0x477ff000u) return (uint16_t)(sign | 0x7c00u);  // rounds to infinity
+  if (ax < 0x38800000u) {                                     // half subnormal: units of 2^-24
+    float v;
+    std::memcpy(&v, &ax, 4);
+    return (uint16_t)(sign | (uint32_t)std::nearbyint(v * 16777216.0f));
+  }
+  uint32_t h = (((ax >> 23) - 112u) << 10) | ((ax & 0x7fffffu) >> 13);
+  const uint32_t rem = ax & 0x1fffu;
+  if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) ++h;
+  return (uint16_t)(sign | h);
+}
+
+float h2f(uint16_t h) {
+  const uint32_t e = (h >> 10) & 0x1fu, m = h & 0x3ffu;
+  float v;
+  if (e == 0) v = std::ldexp((float)m, -24);
+  else if (e == 31) v = m ? NAN : INFINITY;
+  else v = std::ldexp((float)(m | 0x400u), (int)e - 25);
+  return (h & 0x8000u) ? -v : v;
+}
+
+// v ~= hi + lo as fp16 (hi = rne(v), lo = rne(v - hi)); returns hi | lo << 16
+uint32_t split_pair(float v) {
+  const uint16_t hi = f2h(v);
+  const uint16_t lo = f2h(v - h2f(hi));
+  return (uint32_t)hi | ((uint32_t)lo << 16);
+}
+
+// Channel held by slot p = 8s + j of lane half hh in the split layout (pwg_split.hip header).
+int split_chan(int s, int hh, int j) { return 32 * (s >> 1) + 16 * (s & 1) + 8 * (j >> 2) + 4 * hh + (j & 3); }
+
 struct TimingRecord {
   int bucket;
   hipEvent_t start, stop;
@@ -260,6 +297,9 @@ struct PwgHandle {
   int M3T;
   long long ref_total;
   size_t lo_wgp;
+  // split-f16 layer kernel (R = S = 64, 128 gate rows, kernel 3): per-layer image + skip-bias sum
+  int split_ok = 0;
+  size_t lo_split = 0, off_skip0 = 0;
   // options
   int layer_kernel = 0, waves_per_wg = 8, wg_per_cu = 1;
   int n_cu = 0;
@@ -370,12 +410,16 @@ int pwg_create(const PwgConfig* cfg, int device, PwgHandle** out) {
   h->lo_wgp = h->lo_wg + align64((size_t)(h->K1 / 2) * h->MT * 64);
   h->lo_bg = h->lo_wgp + align64((size_t)(h->K1 / 2) * h->MT * 64);
   h->lo_w2 = h->lo_bg + align64(2 * h->GHPAD);
-  h->layer_stride = h->lo_w2 + align64((size_t)h->NQ4 * h->M2T * 64 * 4);
+  h->lo_split = h->lo_w2 + align64((size_t)h->NQ4 * h->M2T * 64 * 4);
+  h->split_ok = h->R == 64 && h->S == 64 && h->G == 128 && h->KS == 3 && h->aux.nka <= 4;
+  h->layer_kernel = h->split_ok ? 2 : 0;
+  h->layer_stride = h->lo_split + (h->split_ok ? align64(SPLIT_LAYER_DWORDS) : 0);
   h->off_layers = o; o += h->layer_stride * h->L;
   h->M3T = (h->S + 31) / 32;
   h->off_head_w1 = o; o += align64((size_t)(16 * h->M3T + 1 + 3) / 4 * h->M3T * 64 * 4);
   h->off_head_w2 = o; o += align64((size_t)h->O * h->M3T * 32);
   h->off_head_b2 = o; o += align64(h->O);
+  h->off_skip0 = o; o += align64(64);
   h->packed_total = o;
 
   long long rt = 0;
@@ -531,6 +575,62 @@ int pwg_pack_weights(const PwgHandle* h, const float* ref, float* pk) {
           }
           w2[(((size_t)(q / 4) * M2T + m2) * 64 + lane) * 4 + (q % 4)] = v;
         }
+    if (h->split_ok) {
+      // split-f16 image (pwg_split.hip SplitSmem): gate A fragments [tap][s][m][hi/lo][lane][4]
+      // (row gate_row(32m + lane%32), k = 8hh + j <-> x channel split_chan(s, hh, j)), GEMM-2 A
+      // fragments [s][m][hi/lo][lane][4] (rows: skip 0..63, then out 0..63 pre-scaled by sqrt(.5);
+      // k <-> gate channel split_chan(s, hh, j)), gate-bias pairs [lane 32][m 4], sqrt(.5) b_out
+      // [hh][slot].
+      uint32_t* sp = reinterpret_cast<uint32_t*>(L0 + h->lo_split);
+      const double rh = std::sqrt(0.5);
+      for (int tap = 0; tap < 3; ++tap)
+        for (int s4 = 0; s4 < 4; ++s4)
+          for (int m = 0; m < 4; ++m)
+            for (int lane = 0; lane < 64; ++lane)
+              for (int j = 0; j < 8; j += 2) {
+                const int grow = gate_row(32 * m + (lane & 31));
+                uint32_t hv = 0, lv = 0;
+                for (int e = 0; e < 2; ++e) {
+                  const int ch = split_chan(s4, lane >> 5, j + e);
+                  const uint32_t pr = grow < 0 ? 0u : split_pair(wd[((size_t)grow * R + ch) * KS + tap]);
+                  hv |= (pr & 0xffffu) << (16 * e);
+                  lv |= (pr >> 16) << (16 * e);
+                }
+                const size_t base = ((((size_t)tap * 4 + s4) * 4 + m) * 2) * 256 + (size_t)lane * 4 + j / 2;
+                sp[base] = hv;
+                sp[base + 256] = lv;
+              }
+      uint32_t* s2 = sp + 3 * 4 * 4 * 2 * 256;
+      for (int s4 = 0; s4 < 4; ++s4)
+        for (int m = 0; m < 4; ++m)
+          for (int lane = 0; lane < 64; ++lane)
+            for (int j = 0; j < 8; j += 2) {
+              const int row = 32 * (m & 1) + (lane & 31);
+              uint32_t hv = 0, lv = 0;
+              for (int e = 0; e < 2; ++e) {
+                const int ch = split_chan(s4, lane >> 5, j + e);
+                const float v = m < 2 ? ws[(size_t)row * GH + ch] : (float)(rh * wo[(size_t)row * GH + ch]);
+                const uint32_t pr = split_pair(v);
+                hv |= (pr & 0xffffu) << (16 * e);
+                lv |= (pr >> 16) << (16 * e);
+              }
+              const size_t base = (((size_t)s4 * 4 + m) * 2) * 256 + (size_t)lane * 4 + j / 2;
+              s2[base] = hv;
+              s2[base + 256] = lv;
+            }
+      uint32_t* sbg = s2 + 4 * 4 * 2 * 256;
+      for (int cl = 0; cl < 32; ++cl)
+        for (int m = 0; m < 4; ++m) {
+          const int gr = gate_row(32 * m + cl);
+          sbg[cl * 4 + m] = gr < 0 ? 0u : split_pair(bd[gr]);
+        }
+      float* sbo = reinterpret_cast<float*>(sbg + 128);
+      for (int hh = 0; hh < 2; ++hh)
+        for (int p2 = 0; p2 < 32; ++p2) sbo[hh * 32 + p2] = (float)(rh * bo[split_chan(p2 >> 3, hh, p2 & 7)]);
+      float* s0 = pk + h->off_skip0;
+      for (int hh = 0; hh < 2; ++hh)
+        for (int p2 = 0; p2 < 32; ++p2) s0[hh * 32 + p2] += bs[split_chan(p2 >> 3, hh, p2 & 7)];
+    }
   }
   // output head (fused into the last layer): W1h A-fragments over skip channels in the same
   // permuted-k order as GEMM 2, bias as k-step NQH; W2h per lane half in accumulator row order.
@@ -748,7 +848,9 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
   if (e != hipSuccess) return hip_fail(e, "conv_in launch");
 
   AuxProjArgs pa;
+  const bool split = h->layer_kernel == 2;
   pa.c1 = c1; pa.waux = packed + h->off_waux; pa.d = dproj; pa.F_total = p->F_total; pa.A = h->A; pa.GR = h->GR;
+  pa.split = split ? 1 : 0;
   e = timed(PWG_KERNEL_UPSAMPLE, [&] { return launch_aux_proj(pa, h->L, s); });
   if (e != hipSuccess) return hip_fail(e, "aux projection launch");
 
@@ -756,7 +858,10 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
   fa.noise = noise; fa.w = packed + h->off_first_w; fa.b = packed + h->off_first_b; fa.x = x0; fa.x1 = x1;
   fa.tile_utt = p->d_tile_utt; fa.utts = p->d_utts; fa.gap_col0 = p->d_gap_col0; fa.n_work = p->n_tiles;
   fa.Tpad = p->Tpad; fa.R = h->R; fa.RS = h->RS;
-  e = timed(PWG_KERNEL_FIRST_CONV, [&] { return launch_first_conv(fa, p->n_tiles + p->n_gap_tiles, s); });
+  e = timed(PWG_KERNEL_FIRST_CONV, [&] {
+    return split ? launch_first_conv_split(fa, p->n_tiles + p->n_gap_tiles, s)
+                 : launch_first_conv(fa, p->n_tiles + p->n_gap_tiles, s);
+  });
   if (e != hipSuccess) return hip_fail(e, "first_conv launch");
 
   float* xin = x0;
@@ -781,7 +886,28 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
     la.out = out; la.O = h->O; la.skip_scale = (float)std::sqrt(1.0 / h->L);
     if (p->layout == PWG_LAYOUT_INFERENCE) { la.out_stride_t = h->O; la.out_stride_o = 1; }
     else { la.out_stride_t = 1; la.out_stride_o = p->utts[0].T; }
-    if (h->layer_kernel == 0 && h->aux.nka <= 4) {
+    if (split) {
+      SplitArgs sa;
+      sa.x_in = reinterpret_cast<const unsigned*>(xin); sa.x_out = reinterpret_cast<unsigned*>(xout);
+      sa.skip = skip; sa.skip0 = packed + h->off_skip0;
+      sa.d = reinterpret_cast<const unsigned*>(la.d);
+      sa.tab = packed + h->off_tab_interior;
+      sa.tab_left = (int)(h->off_tab_left - h->off_tab_interior);
+      sa.tab_right = (int)(h->off_tab_right - h->off_tab_interior);
+      sa.tab_small = (int)(h->off_tab_small - h->off_tab_interior);
+      sa.blocks = p->d_blocks;
+      sa.wg = reinterpret_cast<const unsigned*>(L0 + h->lo_split);
+      sa.hw1 = la.hw1; sa.hw2 = la.hw2; sa.hb2 = la.hb2; sa.out = out;
+      sa.H = (int)h->aux.H; sa.J1 = h->aux.J1; sa.TL = h->aux.TL; sa.TR = h->aux.TR; sa.Fmin = h->aux.Fmin;
+      sa.n_blocks = (int)la.n_blocks; sa.dil = h->dil[l]; sa.first = la.first; sa.O = h->O;
+      sa.out_stride_t = (int)la.out_stride_t; sa.out_stride_o = (int)la.out_stride_o;
+      sa.skip_scale = la.skip_scale;
+      sa.ctr = sched_ctr + (size_t)l * SCHED_CTR_STRIDE * 8;
+      const int nwg = h->n_cu * h->wg_per_cu;
+      e = timed(PWG_KERNEL_RESIDUAL_LAYER, [&] {
+        return launch_layer_split(sa, last, la.tap_center, h->waves_per_wg, nwg, s);
+      });
+    } else if (h->layer_kernel == 0 && h->aux.nka <= 4) {
       PersistArgs pa2;
       pa2.x_in = xin; pa2.x_out = xout; pa2.skip = skip; pa2.d = la.d;
       pa2.tab = packed + h->off_tab_interior;
@@ -851,7 +977,9 @@ int pwg_set_option(PwgHandle* h, int option, long long value) {
   if (!h) return fail(PWG_ERR_INVALID, "null handle");
   switch (option) {
     case PWG_OPT_LAYER_KERNEL:
-      if (value != 0 && value != 1) return fail(PWG_ERR_INVALID, "layer kernel must be 0 or 1");
+      if (value != 0 && value != 1 && value != 2) return fail(PWG_ERR_INVALID, "layer kernel must be 0, 1 or 2");
+      if (value == 2 && !h->split_ok)
+        return fail(PWG_ERR_UNSUPPORTED, "split-f16 layer kernel needs R = S = 64, gate_channels = 128, kernel_size = 3");
       h->layer_kernel = (int)value;
       return PWG_OK;
     case PWG_OPT_WAVES_PER_WG:

@@ -67,6 +67,7 @@ struct AuxProjArgs {
   float* d;              // [L][F_total][GR]
   long long F_total;
   int A, GR;
+  int split;             // 1: store (hi | lo << 16) fp16 pairs for the split-f16 layer kernel
 };
 
 // Writes X0 and zeroes everything of X0/X1 the layers read but never write (gaps, padding
@@ -158,6 +159,30 @@ struct PersistArgs {
   unsigned long long* trace;  // PWG_TRACE builds only: per-wave timestamps (tools/trace_layer.py)
 };
 
+// Split-f16 layer kernel (pwg_split.hip), PWG v1 shape: R = S = 64, 128 gate rows, kernel 3.
+struct SplitArgs {
+  const unsigned* x_in;  // [Tpad][64] fp16-pair slots (pwg_split.hip header)
+  unsigned* x_out;
+  float* skip;           // [Tpad][64] fp32, slot order
+  const float* skip0;    // [2][32]: sum over layers of the skip biases (layer 0's seed)
+  const unsigned* d;     // this layer's aux projection [F_total][128] pairs
+  const float* tab;      // AuxTab base (interior at 0)
+  const BlockDesc* blocks;
+  const unsigned* wg;    // the layer's LDS image: gate frags | W2 frags | gate bias | sqrt(.5) b_out
+  const float* hw1;      // last layer: head (as the fp32 kernel)
+  const float* hw2;
+  const float* hb2;
+  float* out;
+  int tab_left, tab_right, tab_small;
+  int H, J1, TL, TR, Fmin;
+  int n_blocks, dil, first, O;
+  int out_stride_t, out_stride_o;
+  float skip_scale;
+  int* ctr;
+};
+// dwords of one layer's split image (SplitSmem in pwg_split.hip without the head)
+constexpr int SPLIT_LAYER_DWORDS = 3 * 4 * 4 * 2 * 64 * 4 + 4 * 4 * 2 * 64 * 4 + 32 * 4 + 64;
+
 // Persistent-kernel work queues: one head per XCD, each on its own 128-byte line.
 constexpr int SCHED_CTR_STRIDE = 32;
 
@@ -169,6 +194,9 @@ hipError_t launch_conv_in(const ConvInArgs& a, hipStream_t s);
 hipError_t launch_aux_proj(const AuxProjArgs& a, int layers, hipStream_t s);
 hipError_t launch_first_conv(const FirstConvArgs& a, long long n_tiles, hipStream_t s);
 hipError_t launch_layer(const LayerArgs& a, int mt, int m2t, bool last, long long n_tiles, hipStream_t s);
+hipError_t launch_first_conv_split(const FirstConvArgs& a, long long n_tiles, hipStream_t s);
+hipError_t launch_layer_split(const SplitArgs& a, bool last, int tap_center, int waves_per_wg, int n_wg,
+                              hipStream_t s);
 hipError_t launch_layer_persistent(const PersistArgs& a, int mt, int m2t, bool last, int waves_per_wg, int n_wg,
                                    hipStream_t s);
 

@@ -199,7 +199,20 @@ __global__ void __launch_bounds__(256) pwg_aux_proj_kernel(const AuxProjArgs a) 
       f32x4 v;
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] = acc[m][4 * j4 + i];
-      *reinterpret_cast<f32x4*>(d + 32 * m + 8 * j4 + 4 * hh) = v;
+      if (a.split) {
+        // fp16 pair (hi | lo << 16) per value for the split-f16 layer kernel
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+        u32x4 u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const _Float16 hi = (_Float16)v[i];
+          u[i] = __builtin_bit_cast(unsigned, f16x2{hi, (_Float16)(v[i] - (float)hi)});
+        }
+        *reinterpret_cast<u32x4*>(d + 32 * m + 8 * j4 + 4 * hh) = u;
+      } else {
+        *reinterpret_cast<f32x4*>(d + 32 * m + 8 * j4 + 4 * hh) = v;
+      }
     }
 }
 
