@@ -904,9 +904,34 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
       sa.skip_scale = la.skip_scale;
       sa.ctr = sched_ctr + (size_t)l * SCHED_CTR_STRIDE * 8;
       const int nwg = h->n_cu * h->wg_per_cu;
+      sa.trace = nullptr;
+#if PWG_TRACE
+      static unsigned long long* d_trace_s = nullptr;
+      const size_t per_layer_s = (size_t)nwg * 8 * 8;
+      if (!d_trace_s && hipMalloc((void**)&d_trace_s, per_layer_s * 64 * sizeof(unsigned long long)) != hipSuccess)
+        return fail(PWG_ERR_HIP, "trace buffer");
+      sa.trace = d_trace_s + per_layer_s * (l % 64);
+#endif
       e = timed(PWG_KERNEL_RESIDUAL_LAYER, [&] {
         return launch_layer_split(sa, last, la.tap_center, h->waves_per_wg, nwg, s);
       });
+#if PWG_TRACE
+      if (e == hipSuccess && last) {
+        std::vector<unsigned long long> host(per_layer_s * h->L);
+        e = hipStreamSynchronize(s);
+        if (e == hipSuccess) e = hipMemcpy(host.data(), d_trace_s, host.size() * 8, hipMemcpyDeviceToHost);
+        const char* fn = getenv("PWG_TRACE_FILE");
+        if (e == hipSuccess && fn) {
+          FILE* f = fopen(fn, "wb");
+          if (f) {
+            const long long hdr[4] = {h->L, nwg, h->waves_per_wg, 8};
+            fwrite(hdr, sizeof(hdr), 1, f);
+            fwrite(host.data(), 8, host.size(), f);
+            fclose(f);
+          }
+        }
+      }
+#endif
     } else if (h->layer_kernel == 0 && h->aux.nka <= 4) {
       PersistArgs pa2;
       pa2.x_in = xin; pa2.x_out = xout; pa2.skip = skip; pa2.d = la.d;

@@ -179,6 +179,7 @@ struct SplitArgs {
   int out_stride_t, out_stride_o;
   float skip_scale;
   int* ctr;
+  unsigned long long* trace;  // PWG_TRACE builds only (tools/trace_layer.py)
 };
 // dwords of one layer's split image (SplitSmem in pwg_split.hip without the head)
 constexpr int SPLIT_LAYER_DWORDS = 3 * 4 * 4 * 2 * 64 * 4 + 4 * 4 * 2 * 64 * 4 + 32 * 4 + 64;

@@ -10,16 +10,20 @@
 // reference's |d| < 1e-4 (BASELINE north star); measured end to end it stays at the plain-fp32
 // engine's error level (tests/test_gpu_parity.py).
 //
-// Data layout (all per padded time column, 256 B, the same bytes as the fp32 engine):
-//   x   [Tpad][64 dwords]: lane half hh owns dwords [32hh, 32hh+32): 16 dwords of hi halves then
-//       16 dwords of lo halves for its 32 channel SLOTS p = 0..31. Slot p of half hh holds channel
+// Data layout (256 B per padded time column, as the fp32 engine, but TILED): columns are grouped
+// in 32-column tiles of 8 KB, [hh 2][piece 8][column 32][16 B]. Piece i < 4 of half hh holds the hi
+// halves of slots 8i..8i+7, piece 4 + i their lo halves. So the 32 lanes of one half reading piece
+// i of 32 consecutive columns read 512 contiguous bytes: a wave's 16-byte load touches 8 cache
+// lines, not 64 (1.83 vs 2.67 ms per layer with per-column rows).
+//   x   lane half hh owns 32 channel SLOTS p = 0..31 (16 dwords of hi halves, 16 of lo). Slot p of half hh holds channel
 //           chan(s = p>>3, hh, j = p&7) = 32(s>>1) + 16(s&1) + 8(j>>2) + 4hh + (j&3)
 //       which is at once (a) k-element j of k-step s of the GEMM-1 B operand of lane half hh
 //       (B[k = 8hh + j][col]) and (b) accumulator register r = 16(s>>1)... of the GEMM-2 out rows:
 //       acc[2+mo][r] holds channel 32mo + 8(r>>2) + 4hh + (r&3) = slot 16mo + r. So a lane's
 //       128 contiguous bytes per tap row ARE its MFMA operand, and its epilogue writes exactly the
 //       bytes it will read as the next layer's center tap.
-//   skip [Tpad][64 floats]: the same slot order, fp32 (it is never an MFMA operand).
+//   skip the same tiles and slot order, fp32 (it is never an MFMA operand): piece i of half hh =
+//       slots 4i..4i+3.
 //   D    [F][128 dwords]: the aux projection of this layer at frame rate as (hi | lo << 16).
 //
 // Per block of 32 samples (one wave): GEMM 1 = 3 taps x 4 k-steps x 4 m-tiles x 3 = 144 MFMA,
@@ -79,6 +83,19 @@ struct SplitSmem {
   static constexpr int HW1 = 9 * 2 * 256;
   static constexpr int dwords(bool last) { return WG + W2 + BG + BO + (last ? HW1 : 0); }
 };
+
+// Diagnostic builds only (timing experiments, wrong results): PWG_SPLIT_L2ONLY folds every
+// x / skip access into a small window that stays L2-resident; PWG_SPLIT_NOGATE replaces the gate
+// by a product.
+#if PWG_SPLIT_L2ONLY
+#define PWG_COL(c) (((c) & 8191) + 1024)
+#else
+#define PWG_COL(c) (c)
+#endif
+// dword offset of piece 0 of column c, lane half hh, in the tiled x / skip layout (header);
+// piece i is PWG_PIECE dwords further
+#define PWG_ROW(c, hh) ((size_t)(PWG_COL(c) >> 5) * 2048 + (size_t)(hh) * 1024 + (size_t)(PWG_COL(c) & 31) * 4)
+#define PWG_PIECE 128
 
 #ifndef PWG_SPLIT_SEED_RELOAD
 #define PWG_SPLIT_SEED_RELOAD 1  // reloading the center row (L2 hit) avoids spills at 256 VGPRs
@@ -143,9 +160,9 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
   // a lane's 128 B of tap row (block column c + lane column + tap offset): [0..3] hi k-steps,
   // [4..7] lo k-steps
   auto bload = [&](int c, int tap, u32x4 (&b)[8]) {
-    const u32x4* p = reinterpret_cast<const u32x4*>(a.x_in + (size_t)(c + cl + (tap - TC) * a.dil) * 64 + 32 * hh);
+    const u32x4* p = reinterpret_cast<const u32x4*>(a.x_in + PWG_ROW(c + cl + (tap - TC) * a.dil, hh));
 #pragma unroll
-    for (int i = 0; i < 8; ++i) b[i] = p[i];
+    for (int i = 0; i < 8; ++i) b[i] = p[i * (PWG_PIECE / 4)];
   };
   const u32x4* wgl = reinterpret_cast<const u32x4*>(s_wg) + lane;
   auto mma_tap = [&](f32x16 (&acc)[4], const u32x4 (&b)[8], int tap) {
@@ -187,7 +204,25 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
   int nblk = blk + x_waves;
   if (blk >= x_end) blk = -1;
   if (nblk >= x_end) nblk = -1;
-  if (blk < 0) return;
+#if PWG_TRACE
+  // diagnostic build: [start_rt, end_rt, blocks, gemm1_cyc, aux+gate_cyc, gemm2_cyc, start_clk, end_clk]
+  unsigned long long* trw = a.trace + ((size_t)blockIdx.x * nw + wave) * 8;
+  const unsigned long long tr_rt0 = wall_clock64(), tr_c0 = clock64();
+  unsigned long long tr_g1 = 0, tr_gt = 0, tr_g2 = 0, tr_n = 0;
+  auto tr_done = [&] {
+    if (lane == 0) {
+      trw[0] = tr_rt0; trw[1] = wall_clock64(); trw[2] = tr_n; trw[3] = tr_g1; trw[4] = tr_gt;
+      trw[5] = tr_g2; trw[6] = tr_c0; trw[7] = clock64();
+    }
+  };
+#define PWG_TR(x) x
+#else
+#define PWG_TR(x)
+#endif
+  if (blk < 0) {
+    PWG_TR(tr_done());
+    return;
+  }
   BlockDesc bdn = a.blocks[blk];
   u32x4 b0[8], b1[8];
   bload(bdn.col, 0, b0);
@@ -239,6 +274,7 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
     f32x16 seed[2];
+    PWG_TR(const unsigned long long tr_a = clock64());
     bload(bd.col, 1, b1);
     mma_tap(acc, b0, 0);
     load_dv();  // in flight during taps 1 and 2
@@ -253,16 +289,17 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
     if (TC == 2) x_seed(b0, seed);
 #endif
 
+    PWG_TR(const unsigned long long tr_b = clock64());
     int ticket = 0;
     if (nblk >= 0) ticket = ticket_issue();
     // skip seeds (old skip sum; layer 0: the sum of all layers' skip biases)
     f32x16 acc2[4];
     {
       const f32x4* sp = reinterpret_cast<const f32x4*>(
-          a.first ? a.skip0 + 32 * hh : a.skip + (size_t)(bd.col + cl) * 64 + 32 * hh);
+          a.first ? a.skip0 + 32 * hh : a.skip + PWG_ROW(bd.col + cl, hh));
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        const f32x4 v = sp[k];
+        const f32x4 v = sp[a.first ? k : k * (PWG_PIECE / 4)];
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc2[k >> 2][4 * (k & 3) + i] = v[i];
       }
@@ -306,8 +343,13 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int gm = s >> 1, r = 8 * (s & 1) + 2 * k;
+#if PWG_SPLIT_NOGATE
+        const float g0 = acc[gm][r] * acc[gm + 2][r];
+        const float g1 = acc[gm][r + 1] * acc[gm + 2][r + 1];
+#else
         const float g0 = gate(acc[gm][r], acc[gm + 2][r]);
         const float g1 = gate(acc[gm][r + 1], acc[gm + 2][r + 1]);
+#endif
         const Pair2 pr = split2(g0, g1);
         gh[s][k] = pr.hi;
         gl[s][k] = pr.lo;
@@ -322,6 +364,7 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
       acc2[3] = seed[1];
     }
 
+    PWG_TR(const unsigned long long tr_c = clock64());
     // ---- GEMM 2: [skip; out] rows
     constexpr int M2 = LAST ? 2 : 4;
     const u32x4* w2l = reinterpret_cast<const u32x4*>(s_w2) + lane;
@@ -344,15 +387,15 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
 
     if (!LAST) {
       // skip sum (fp32) and the next residual stream (fp16 pairs; padding columns stay zero)
-      f32x4* sp = reinterpret_cast<f32x4*>(a.skip + (size_t)(bd.col + cl) * 64 + 32 * hh);
+      f32x4* sp = reinterpret_cast<f32x4*>(a.skip + PWG_ROW(bd.col + cl, hh));
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         f32x4 v;
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = acc2[k >> 2][4 * (k & 3) + i];
-        sp[k] = v;
+        sp[k * (PWG_PIECE / 4)] = v;
       }
-      u32x4* xp = reinterpret_cast<u32x4*>(a.x_out + (size_t)(bd.col + cl) * 64 + 32 * hh);
+      u32x4* xp = reinterpret_cast<u32x4*>(a.x_out + PWG_ROW(bd.col + cl, hh));
 #pragma unroll
       for (int k4 = 0; k4 < 4; ++k4) {
         u32x4 vh, vl;
@@ -363,8 +406,8 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
           vh[k] = live ? pr.hi : 0u;
           vl[k] = live ? pr.lo : 0u;
         }
-        xp[k4] = vh;
-        xp[4 + k4] = vl;
+        xp[k4 * (PWG_PIECE / 4)] = vh;
+        xp[(4 + k4) * (PWG_PIECE / 4)] = vl;
       }
     } else {
       // ---- fused output head on the final skip sum (models/parallel_wavegan.py:131-138,166-171):
@@ -414,12 +457,16 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
       }
     }
 
+    PWG_TR(const unsigned long long tr_d = clock64(); tr_g1 += tr_b - tr_a; tr_gt += tr_c - tr_b;
+           tr_g2 += tr_d - tr_c; ++tr_n);
     if (nblk < 0) break;
     blk = nblk;
     nblk = ticket_resolve(ticket);
 #pragma unroll
     for (int i = 0; i < 8; ++i) b0[i] = b1[i];
   }
+  PWG_TR(tr_done());
+#undef PWG_TR
 }
 
 // first_conv (1x1, 1 -> 64, bias) into the split x layout; gap tiles zero both buffers.
@@ -438,9 +485,13 @@ __global__ void __launch_bounds__(256) pwg_first_conv_split_kernel(const FirstCo
   const UttDesc ud = a.utts[a.tile_utt[tile]];
   const long long col0 = ud.seg_base + (tile - ud.first_tile) * TILE;
   const long long t0 = col0 - ud.seg_base;
+  // the 128 columns are 4 whole 32-column tiles = 8192 contiguous dwords: idx walks them in
+  // memory order (coalesced stores)
   for (int idx = threadIdx.x; idx < 64 * TILE; idx += 256) {
-    const int jcol = idx >> 6, dw = idx & 63;
-    const int hh = dw >> 5, k = dw & 31, lo = k >> 4, p = 2 * (k & 15);
+    const int sub = idx >> 11, rem = idx & 2047;
+    const int hh = rem >> 10, piece = (rem >> 7) & 7, jc = (rem >> 2) & 31, dw = rem & 3;
+    const int jcol = 32 * sub + jc;
+    const int s = piece & 3, p = 8 * s + 2 * dw;  // slots p, p+1
     const long long t = t0 + jcol;
     unsigned v = 0u;
     if (t < ud.T) {
@@ -448,14 +499,14 @@ __global__ void __launch_bounds__(256) pwg_first_conv_split_kernel(const FirstCo
       float y[2];
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
-        const int s = (p + e) >> 3, j = (p + e) & 7;
+        const int j = (p + e) & 7;
         const int c = 32 * (s >> 1) + 16 * (s & 1) + 8 * (j >> 2) + 4 * hh + (j & 3);
         y[e] = fmaf(a.w[c], z, a.b[c]);
       }
       const Pair2 pr = split2(y[0], y[1]);
-      v = lo ? pr.lo : pr.hi;
+      v = piece >= 4 ? pr.lo : pr.hi;
     }
-    x[(size_t)(col0 + jcol) * 64 + dw] = v;
+    x[(size_t)col0 * 64 + idx] = v;
   }
 }
 

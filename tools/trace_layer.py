@@ -27,7 +27,8 @@ def main():
     ap.add_argument("--out", default=os.path.join(REPO, "gpurun_out", "layer_trace.bin"))
     ap.add_argument("--flags", default="", help="extra hipcc flags for the variant")
     args = ap.parse_args()
-    _lib.build(force=True, extra_flags=["-DPWG_TRACE=1"] + args.flags.split(), out_path=VARIANT)
+    if not (os.environ.get("PWG_NO_BUILD") == "1" and os.path.exists(VARIANT)):
+        _lib.build(force=True, extra_flags=["-DPWG_TRACE=1"] + args.flags.split(), out_path=VARIANT)
     os.environ["PWG_TRACE_FILE"] = args.out
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     params = configs.generator_params(args.config)
