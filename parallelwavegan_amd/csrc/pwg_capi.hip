@@ -589,10 +589,12 @@ int pwg_pack_weights(const PwgHandle* h, const float* ref, float* pk) {
             for (int lane = 0; lane < 64; ++lane)
               for (int j = 0; j < 8; j += 2) {
                 const int grow = gate_row(32 * m + (lane & 31));
+                const double gsc = m < 2 ? SPLIT_GATE_SCALE_TANH : SPLIT_GATE_SCALE_SIGM;
                 uint32_t hv = 0, lv = 0;
                 for (int e = 0; e < 2; ++e) {
                   const int ch = split_chan(s4, lane >> 5, j + e);
-                  const uint32_t pr = grow < 0 ? 0u : split_pair(wd[((size_t)grow * R + ch) * KS + tap]);
+                  const uint32_t pr =
+                      grow < 0 ? 0u : split_pair((float)(gsc * wd[((size_t)grow * R + ch) * KS + tap]));
                   hv |= (pr & 0xffffu) << (16 * e);
                   lv |= (pr >> 16) << (16 * e);
                 }
@@ -622,7 +624,8 @@ int pwg_pack_weights(const PwgHandle* h, const float* ref, float* pk) {
       for (int cl = 0; cl < 32; ++cl)
         for (int m = 0; m < 4; ++m) {
           const int gr = gate_row(32 * m + cl);
-          sbg[cl * 4 + m] = gr < 0 ? 0u : split_pair(bd[gr]);
+          const double gsc = m < 2 ? SPLIT_GATE_SCALE_TANH : SPLIT_GATE_SCALE_SIGM;
+          sbg[cl * 4 + m] = gr < 0 ? 0u : split_pair((float)(gsc * bd[gr]));
         }
       float* sbo = reinterpret_cast<float*>(sbg + 128);
       for (int hh = 0; hh < 2; ++hh)
@@ -851,6 +854,8 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
   const bool split = h->layer_kernel == 2;
   pa.c1 = c1; pa.waux = packed + h->off_waux; pa.d = dproj; pa.F_total = p->F_total; pa.A = h->A; pa.GR = h->GR;
   pa.split = split ? 1 : 0;
+  pa.split_scale_a = (float)SPLIT_GATE_SCALE_TANH;
+  pa.split_scale_b = (float)SPLIT_GATE_SCALE_SIGM;
   e = timed(PWG_KERNEL_UPSAMPLE, [&] { return launch_aux_proj(pa, h->L, s); });
   if (e != hipSuccess) return hip_fail(e, "aux projection launch");
 

@@ -67,8 +67,14 @@ struct AuxProjArgs {
   float* d;              // [L][F_total][GR]
   long long F_total;
   int A, GR;
-  int split;             // 1: store (hi | lo << 16) fp16 pairs for the split-f16 layer kernel
+  int split;             // 1: store (hi | lo << 16) fp16 pairs for the split-f16 layer kernel,
+                         // rows [0, GR/2) scaled by split_scale_a, the rest by split_scale_b
+  float split_scale_a, split_scale_b;
 };
+// Pre-scaling of the split kernel's gate rows (pwg_split.hip gate()): tanh rows by -2 log2(e),
+// sigmoid rows by -log2(e).
+constexpr double SPLIT_GATE_SCALE_TANH = -2.8853900817779268;
+constexpr double SPLIT_GATE_SCALE_SIGM = -1.4426950408889634;
 
 // Writes X0 and zeroes everything of X0/X1 the layers read but never write (gaps, padding
 // channels). Blocks [0, n_work) are work tiles, the rest gap tiles (gap_col0).

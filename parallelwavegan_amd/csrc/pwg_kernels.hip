@@ -204,10 +204,12 @@ __global__ void __launch_bounds__(256) pwg_aux_proj_kernel(const AuxProjArgs a) 
         typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
         typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
         u32x4 u;
+        const float sc = 32 * m + 8 * j4 < GR / 2 ? a.split_scale_a : a.split_scale_b;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const _Float16 hi = (_Float16)v[i];
-          u[i] = __builtin_bit_cast(unsigned, f16x2{hi, (_Float16)(v[i] - (float)hi)});
+          const float x = v[i] * sc;
+          const _Float16 hi = (_Float16)x;
+          u[i] = __builtin_bit_cast(unsigned, f16x2{hi, (_Float16)(x - (float)hi)});
         }
         *reinterpret_cast<u32x4*>(d + 32 * m + 8 * j4 + 4 * hh) = u;
       } else {

@@ -51,23 +51,52 @@ struct Pair2 {
 };
 __device__ __forceinline__ Pair2 split2(float v0, float v1) {
   const _Float16 h0 = (_Float16)v0, h1 = (_Float16)v1;
-  const _Float16 l0 = (_Float16)(v0 - (float)h0), l1 = (_Float16)(v1 - (float)h1);
+  // v - hi as one v_fma_mix_f32 each (f16 source widened inside the FMA)
+  const _Float16 l0 = (_Float16)__builtin_fmaf((float)h0, -1.f, v0), l1 = (_Float16)__builtin_fmaf((float)h1, -1.f, v1);
   return {__builtin_bit_cast(unsigned, f16x2{h0, h1}), __builtin_bit_cast(unsigned, f16x2{l0, l1})};
 }
 
-__device__ __forceinline__ float pair_value(_Float16 hi, _Float16 lo) { return (float)hi + (float)lo; }
 
 __device__ __forceinline__ f32x16 mma(u32x4 a, u32x4 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(h8(a), h8(b), c, 0, 0, 0);
 }
 
-// tanh(a) * sigmoid(b) with 2 v_exp + 1 v_rcp (same formulation as the fp32 kernel)
-__device__ __forceinline__ float gate(float a, float b) {
-  a = __builtin_amdgcn_fmed3f(a, -15.f, 15.f);
-  b = __builtin_amdgcn_fmed3f(b, -30.f, 88.f);
-  const float e1 = __builtin_amdgcn_exp2f(a * -2.8853900817779268f);
-  const float e2 = __builtin_amdgcn_exp2f(b * -1.4426950408889634f);
+// tanh(a) * sigmoid(b) = (1 - e^-2a) / ((1 + e^-2a)(1 + e^-b)) with 2 v_exp + 1 v_rcp. The gate
+// rows arrive PRE-SCALED (host packing and the aux projection): u = -2 log2(e) a, v = -log2(e) b,
+// so e^-2a = 2^u and e^-b = 2^v. Clamps where fp32 is already saturated (|a| > 15: tanh = +-1;
+// b < -30: sigmoid < 1e-13) keep every intermediate finite.
+constexpr float GATE_SCALE_TANH = -2.8853900817779268f;  // -2 log2(e)
+constexpr float GATE_SCALE_SIGM = -1.4426950408889634f;  // -log2(e)
+__device__ __forceinline__ float gate(float u, float v) {
+  u = __builtin_amdgcn_fmed3f(u, -43.28085123f, 43.28085123f);
+  v = __builtin_amdgcn_fmed3f(v, -126.95716359f, 43.28085123f);
+  const float e1 = __builtin_amdgcn_exp2f(u);
+  const float e2 = __builtin_amdgcn_exp2f(v);
   return (1.f - e1) * __builtin_amdgcn_rcpf((1.f + e1) * (1.f + e2));
+}
+
+// Four split pairs in one statement: hi = cvt_pk (RNE), lo = rne16(v - hi) by v_fma_mix{lo,hi}
+// (one instruction per value; the compiler's own form is 2 conversions + a packed f32 add).
+// Only for VALU-produced inputs; the trailing s_nop 1 covers a VALU write -> MFMA operand read
+// (cdna_hip_programming.md 5.7 item 2).
+__device__ __forceinline__ void split8(const float (&v)[8], unsigned (&hi)[4], unsigned (&lo)[4]) {
+  asm volatile(
+      "v_cvt_pk_f16_f32 %0, %8, %9\n\t"
+      "v_cvt_pk_f16_f32 %1, %10, %11\n\t"
+      "v_cvt_pk_f16_f32 %2, %12, %13\n\t"
+      "v_cvt_pk_f16_f32 %3, %14, %15\n\t"
+      "v_fma_mixlo_f16 %4, %0, -1.0, %8 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixlo_f16 %5, %1, -1.0, %10 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixlo_f16 %6, %2, -1.0, %12 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixlo_f16 %7, %3, -1.0, %14 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %4, %0, -1.0, %9 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %5, %1, -1.0, %11 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %6, %2, -1.0, %13 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %7, %3, -1.0, %15 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "s_nop 1"
+      : "=&v"(hi[0]), "=&v"(hi[1]), "=&v"(hi[2]), "=&v"(hi[3]), "=&v"(lo[0]), "=&v"(lo[1]), "=&v"(lo[2]),
+        "=&v"(lo[3])
+      : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]));
 }
 
 }  // namespace
@@ -171,15 +200,22 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
       u32x4 ah[4], al[4];
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
+#if PWG_SPLIT_DIAG_LDS1  // diagnostic: one A fragment pair for every k-step (wrong results)
+        ah[m] = wgl[(m * 2) * 64];
+        al[m] = wgl[(m * 2 + 1) * 64];
+#else
         ah[m] = wgl[(((tap * 4 + s) * 4 + m) * 2) * 64];
         al[m] = wgl[(((tap * 4 + s) * 4 + m) * 2 + 1) * 64];
+#endif
       }
 #pragma unroll
       for (int m = 0; m < 4; ++m) acc[m] = mma(ah[m], b[s], acc[m]);
+#if !PWG_SPLIT_DIAG_1PASS  // diagnostic: hi*hi only (wrong results)
 #pragma unroll
       for (int m = 0; m < 4; ++m) acc[m] = mma(ah[m], b[4 + s], acc[m]);
 #pragma unroll
       for (int m = 0; m < 4; ++m) acc[m] = mma(al[m], b[s], acc[m]);
+#endif
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -194,8 +230,9 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int r = 4 * q + i, s = 2 * mo + (r >> 3), j = r & 7;
-          const float xv = pair_value(h8(b[s])[j], h8(b[4 + s])[j]);
-          seed[mo][r] = fmaf(xv, 0.70710677f, bv[i]);
+          // sqrt(.5) * (hi + lo) + b' as two v_fma_mix_f32
+          seed[mo][r] = __builtin_fmaf((float)h8(b[s])[j], 0.70710677f,
+                                       __builtin_fmaf((float)h8(b[4 + s])[j], 0.70710677f, bv[i]));
         }
       }
   };
@@ -232,6 +269,7 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
     bdn = a.blocks[nblk >= 0 ? nblk : blk];
     const int t = bd.t0 + cl;
     const bool live = t < bd.T;
+    const bool full = bd.t0 + 32 <= bd.T;  // wave-uniform: no padding column in this block
     const int col_next = nblk >= 0 ? bdn.col : bd.col;
 
     // aux operands, in flight during GEMM 1. Window frames fw0 + 4hh + j (j < 4) hold K slots
@@ -275,6 +313,11 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
       for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
     f32x16 seed[2];
     PWG_TR(const unsigned long long tr_a = clock64());
+#if PWG_SPLIT_PRIO == 1
+    __builtin_amdgcn_s_setprio(1);  // GEMM 1 (MFMA phase) wins issue arbitration
+#elif PWG_SPLIT_PRIO == 2
+    __builtin_amdgcn_s_setprio(0);
+#endif
     bload(bd.col, 1, b1);
     mma_tap(acc, b0, 0);
     load_dv();  // in flight during taps 1 and 2
@@ -290,6 +333,11 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
 #endif
 
     PWG_TR(const unsigned long long tr_b = clock64());
+#if PWG_SPLIT_PRIO == 1
+    __builtin_amdgcn_s_setprio(0);
+#elif PWG_SPLIT_PRIO == 2
+    __builtin_amdgcn_s_setprio(1);  // aux + gate (VALU phase) wins issue arbitration
+#endif
     int ticket = 0;
     if (nblk >= 0) ticket = ticket_issue();
     // skip seeds (old skip sum; layer 0: the sum of all layers' skip biases)
@@ -339,21 +387,25 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
     //      element r & 7
     u32x4 gh[4], gl[4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s)
+    for (int s = 0; s < 4; ++s) {
+      const int gm = s >> 1, r0 = 8 * (s & 1);
+      float gv[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+#if PWG_SPLIT_NOGATE
+        gv[k] = acc[gm][r0 + k] * acc[gm + 2][r0 + k];
+#else
+        gv[k] = gate(acc[gm][r0 + k], acc[gm + 2][r0 + k]);
+#endif
+      }
+      unsigned hv[4], lv[4];
+      split8(gv, hv, lv);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const int gm = s >> 1, r = 8 * (s & 1) + 2 * k;
-#if PWG_SPLIT_NOGATE
-        const float g0 = acc[gm][r] * acc[gm + 2][r];
-        const float g1 = acc[gm][r + 1] * acc[gm + 2][r + 1];
-#else
-        const float g0 = gate(acc[gm][r], acc[gm + 2][r]);
-        const float g1 = gate(acc[gm][r + 1], acc[gm + 2][r + 1]);
-#endif
-        const Pair2 pr = split2(g0, g1);
-        gh[s][k] = pr.hi;
-        gl[s][k] = pr.lo;
+        gh[s][k] = hv[k];
+        gl[s][k] = lv[k];
       }
+    }
     if (!LAST) {
 #if PWG_SPLIT_SEED_RELOAD
       u32x4 bc[8];
@@ -365,6 +417,11 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
     }
 
     PWG_TR(const unsigned long long tr_c = clock64());
+#if PWG_SPLIT_PRIO == 2
+    __builtin_amdgcn_s_setprio(0);
+#elif PWG_SPLIT_PRIO == 3
+    __builtin_amdgcn_s_setprio(1);  // GEMM 2 + stores
+#endif
     // ---- GEMM 2: [skip; out] rows
     constexpr int M2 = LAST ? 2 : 4;
     const u32x4* w2l = reinterpret_cast<const u32x4*>(s_w2) + lane;
@@ -403,8 +460,8 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
         for (int k = 0; k < 4; ++k) {
           const int p = 2 * (4 * k4 + k);  // slot pair p, p+1 -> mo = p >> 4, r = p & 15
           const Pair2 pr = split2(acc2[2 + (p >> 4)][p & 15], acc2[2 + (p >> 4)][(p & 15) + 1]);
-          vh[k] = live ? pr.hi : 0u;
-          vl[k] = live ? pr.lo : 0u;
+          vh[k] = full || live ? pr.hi : 0u;  // padding columns stay zero
+          vl[k] = full || live ? pr.lo : 0u;
         }
         xp[k4 * (PWG_PIECE / 4)] = vh;
         xp[(4 + k4) * (PWG_PIECE / 4)] = vl;
@@ -457,6 +514,9 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
       }
     }
 
+#if PWG_SPLIT_PRIO == 3
+    __builtin_amdgcn_s_setprio(0);
+#endif
     PWG_TR(const unsigned long long tr_d = clock64(); tr_g1 += tr_b - tr_a; tr_gt += tr_c - tr_b;
            tr_g2 += tr_d - tr_c; ++tr_n);
     if (nblk < 0) break;
