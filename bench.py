@@ -33,6 +33,26 @@ from parallelwavegan_amd.sharding import broadcast_packed_weights, max_over_rank
 
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: Peak FP32 (matrix) = vector, spec
 HBM_PEAK_GBS = 8000.0
+F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/F16 dense (no sparsity)
+
+
+def split_layer_bytes_per_sample(params, H, L):
+    """Algorithmic HBM bytes per sample of the split engine's residual layer, averaged over the L
+    launches: x read + write (4 B per channel as an fp16 pair) and skip read + write (fp32); layer 0
+    reads no skip, the last layer writes neither x nor skip but the output; plus the frame-rate aux
+    rows (GR pairs per frame). DESIGN.md sec 3.6."""
+    R, S, G, O = (params[k] for k in ("residual_channels", "skip_channels", "gate_channels", "out_channels"))
+    mid = 4 * (2 * R + 2 * S)
+    first = 4 * (2 * R + S)
+    last = 4 * (R + S) + 4 * O
+    return (first + (L - 2) * mid + last) / L + 4 * G / H
+
+
+def split_executed_flop_per_block(L):
+    """f16 MFMA FLOP one 32-sample block executes, averaged over the L launches: 144 GEMM-1 +
+    12 aux/bias + 48 GEMM-2 v_mfma_f32_32x32x16_f16 (32,768 FLOP each); the last layer runs 24
+    GEMM-2 MFMAs and its head as fp32 MFMA (not counted)."""
+    return 32768 * ((L - 1) * 204 + (144 + 12 + 24)) / L
 
 
 def layer_flops_per_sample(params):
@@ -363,11 +383,60 @@ def main():
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            if tj.get("config") == args.config and tj.get("utts") == args.utts:
+            if (tj.get("config") == args.config and tj.get("utts") == args.utts
+                    and tj.get("layer_kernel", "persistent") == args.layer_kernel):
                 traffic = tj.get("hbm_bytes_per_launch")
                 mfma_insts = tj.get("mfma_insts_per_launch")
         except (OSError, ValueError):
             traffic = None
+    L = params["layers"]
+    if args.layer_kernel == "split":
+        # HBM-bound: algorithmic bytes of the engine's layer per launch / launch time
+        bytes_launch = split_layer_bytes_per_sample(params, H, L) * plan.total_samples
+        n_blocks = int(sum(-(-int(f) * H // 128) * 4 for f in lengths))
+        exec_flop = split_executed_flop_per_block(L) * n_blocks
+        achieved_gbs = bytes_launch / layer_avg_s / 1e9
+        roofline = {
+            "kernel": "residual layer (split-f16 persistent kernel, one fused WaveNet residual block)",
+            "bound": "hbm",
+            "achieved": round(achieved_gbs, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "algorithmic_bytes_per_launch": int(bytes_launch),
+            "avg_launch_ms": round(layer_avg_s * 1e3, 4),
+            "launches_timed": layer_n,
+            "mfma": {
+                "executed_f16_flop_per_launch": int(exec_flop),
+                "achieved_tflops": round(exec_flop / layer_avg_s / 1e12, 1),
+                "peak_tflops": F16_MFMA_PEAK_TFLOPS,
+                "frac": round(exec_flop / layer_avg_s / 1e12 / F16_MFMA_PEAK_TFLOPS, 4),
+            },
+            # the reference formulation's fp32 FLOPs per launch over the same time
+            "reference_flop_per_launch": int(flops_launch),
+            "reference_tflops": round(achieved_tflops, 1),
+            "hbm_GBs_measured": traffic and round(traffic / layer_avg_s / 1e9, 1),
+        }
+    else:
+        roofline = {
+            "kernel": f"residual layer ({args.layer_kernel} kernel, one fused WaveNet residual block)",
+            "bound": "mfma",
+            "achieved": round(achieved_tflops, 3),
+            "peak": FP32_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 4),
+            "traffic": traffic,
+            "flop_per_launch": int(flops_launch),
+            "algorithmic_bytes_per_launch": int(layer_bytes_per_sample(params) * plan.total_samples),
+            "avg_launch_ms": round(layer_avg_s * 1e3, 4),
+            "launches_timed": layer_n,
+            # FLOPs the MFMAs actually execute (rocprofv3 SQ_INSTS_MFMA x 4096 per 32x32x2 f32 MFMA):
+            # below the reference count because the aux 1x1 runs at frame rate (DESIGN.md)
+            "executed_flop_per_launch": mfma_insts and int(mfma_insts * 4096),
+            "executed_frac": mfma_insts and round(mfma_insts * 4096 / layer_avg_s / 1e12 / FP32_PEAK_TFLOPS, 4),
+            "hbm_GBs": traffic and round(traffic / layer_avg_s / 1e9, 1),
+        }
 
     if rank != 0:
         dist.destroy_process_group()
@@ -389,7 +458,8 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": "f32 (fp16 hi+lo pair operands, 3 f16 MFMAs per product, fp32 accumulate)"
+                 if args.layer_kernel == "split" else "f32",
         "data": "synthetic (seeded N(0,1) mel + noise, seeded kaiming-init weights)",
         "config": {
             "workload": f"{args.config} generator inference, {args.utts} ragged utterances per GPU per step",
@@ -405,24 +475,7 @@ def main():
         "x_realtime_per_gpu": round(per_gpu / fs, 1),
         "rtf_per_gpu": per_gpu and fs / per_gpu,
         "kernel_ms_per_step": {k: round(ms / args.steps, 3) for k, (ms, _) in timing.items()},
-        "roofline": {
-            "kernel": f"residual layer ({args.layer_kernel} kernel, one fused WaveNet residual block)",
-            "bound": "mfma",
-            "achieved": round(achieved_tflops, 3),
-            "peak": FP32_PEAK_TFLOPS,
-            "unit": "TFLOP/s",
-            "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 4),
-            "traffic": traffic,
-            "flop_per_launch": int(flops_launch),
-            "algorithmic_bytes_per_launch": int(layer_bytes_per_sample(params) * plan.total_samples),
-            "avg_launch_ms": round(layer_avg_s * 1e3, 4),
-            "launches_timed": layer_n,
-            # FLOPs the MFMAs actually execute (rocprofv3 SQ_INSTS_MFMA x 4096 per 32x32x2 f32 MFMA):
-            # below the reference count because the aux 1x1 runs at frame rate (DESIGN.md)
-            "executed_flop_per_launch": mfma_insts and int(mfma_insts * 4096),
-            "executed_frac": mfma_insts and round(mfma_insts * 4096 / layer_avg_s / 1e12 / FP32_PEAK_TFLOPS, 4),
-            "hbm_GBs": traffic and round(traffic / layer_avg_s / 1e9, 1),
-        },
+        "roofline": roofline,
         "model_flop_per_sample": round(model_flops_per_sample(params), 1),
         "model_tflops": round(value / world * model_flops_per_sample(params) / 1e12, 3),
         "pcie_inclusive_value": round(samples_per_step * args.steps / e2e, 1),

@@ -94,6 +94,34 @@ def test_full_size_against_torch_cpu(built_lib, cuda_device):
     assert err < ATOL, f"max|d| = {err:.3e}"
 
 
+@pytest.mark.parametrize("wscale", [1.0, 2.0])
+def test_split_kernel_matches_fp32_kernel_full_batch(wscale, built_lib, cuda_device):
+    """The bench workload's shape (LibriTTS v1, ragged utterances, 1.4 M samples) through the
+    split-f16 kernel and the exact-fp32 persistent kernel: |d| < 1e-4 at full size. wscale=2
+    doubles every residual-block conv weight (larger activations than the kaiming init gives)."""
+    from parallelwavegan_amd import Engine, configs, synthetic
+
+    params = configs.generator_params("libritts_v1")
+    sd = synthetic.make_state_dict(params, seed=5)
+    for k in sd:
+        if k.startswith("conv_layers.") and k.endswith("conv.weight"):
+            sd[k] = sd[k] * wscale
+    lengths = synthetic.libritts_lengths(6, seed=3).tolist()
+    rs = np.random.RandomState(9)
+    mels = [torch.from_numpy(rs.standard_normal((f, 80)).astype(np.float32)).to(cuda_device) for f in lengths]
+    noises = [torch.from_numpy(rs.standard_normal((f * 300, 1)).astype(np.float32)).to(cuda_device) for f in lengths]
+    outs = {}
+    for kernel in ("split", "persistent"):
+        eng = Engine(params, cuda_device)
+        eng.load_state_dict(sd)
+        eng.set_option("layer_kernel", kernel)
+        outs[kernel] = torch.cat([y.reshape(-1) for y in eng.infer(mels, noises)]).cpu().numpy()
+    err = np.abs(outs["split"] - outs["persistent"]).max()
+    scale = np.abs(outs["persistent"]).max()
+    assert np.isfinite(outs["split"]).all()
+    assert err < ATOL, f"max|d| = {err:.3e} (max|y| = {scale:.2f})"
+
+
 def test_ragged_batch_is_bitwise_equal_to_single_utterances(built_lib, cuda_device):
     """Segment padding isolates utterances: a batch must reproduce solo runs bit for bit."""
     from parallelwavegan_amd import Engine, configs, synthetic

@@ -12,4 +12,8 @@ cat "$OUT/smoke.log" | tail -1
 timeout -k 10 300 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
 cat "$OUT/bench.json"
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --cpu-seconds 0 > "$GRAFT_REPO_ROOT/$OUT/bench_prof.json" 2> "$GRAFT_REPO_ROOT/$OUT/prof.err"
+
+cd "$GRAFT_REPO_ROOT"
+# PMC passes (separate rocprofv3 runs) -> HBM traffic per split-layer launch
+bash tools/profile_pmc.sh "$OUT/pmc" && python tools/pmc_summary.py "$OUT/pmc" "$OUT/pmc_summary.json" > /dev/null && python tools/make_traffic_json.py "$OUT/pmc_summary.json" "$OUT/layer_traffic.json" split
 echo done

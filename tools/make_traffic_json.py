@@ -6,13 +6,17 @@ import json
 import sys
 
 
-def main(summary, out, config="libritts_v1", utts=32):
+def main(summary, out, config="libritts_v1", utts=32, layer_kernel="split"):
     d = json.load(open(summary))
-    rows = {k: v for k, v in d.items() if "layer" in k and ("0, 16" in k or "4, 4, 0" in k)}
+    if layer_kernel == "split":
+        rows = {k: v for k, v in d.items() if "layer_split_kernel<false" in k}
+    else:
+        rows = {k: v for k, v in d.items() if "layer" in k and ("0, 16" in k or "4, 4, 0" in k)}
     k, v = max(rows.items(), key=lambda kv: kv[1].get("SQ_WAVES", 0))
     res = {
         "config": config,
         "utts": utts,
+        "layer_kernel": layer_kernel,
         "kernel": k,
         "fetch_bytes_per_launch": v["FETCH_BYTES_corrected"],
         "write_bytes_per_launch": v["WRITE_BYTES"],
@@ -27,4 +31,4 @@ def main(summary, out, config="libritts_v1", utts=32):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:3])
+    main(sys.argv[1], sys.argv[2], layer_kernel=sys.argv[3] if len(sys.argv) > 3 else "split")
