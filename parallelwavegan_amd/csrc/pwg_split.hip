@@ -67,9 +67,10 @@ __device__ __forceinline__ f32x16 mma(u32x4 a, u32x4 b, f32x16 c) {
 // b < -30: sigmoid < 1e-13) keep every intermediate finite.
 constexpr float GATE_SCALE_TANH = -2.8853900817779268f;  // -2 log2(e)
 constexpr float GATE_SCALE_SIGM = -1.4426950408889634f;  // -log2(e)
+// Only u needs a clamp: 2^u must stay finite (u <= 64: tanh is -1 to fp32 precision long
+// before). 2^v may overflow to +inf: rcp(inf) = 0 gives the sigmoid's limit 0, and 2^v -> 0 its 1.
 __device__ __forceinline__ float gate(float u, float v) {
-  u = __builtin_amdgcn_fmed3f(u, -43.28085123f, 43.28085123f);
-  v = __builtin_amdgcn_fmed3f(v, -126.95716359f, 43.28085123f);
+  u = fminf(u, 64.f);
   const float e1 = __builtin_amdgcn_exp2f(u);
   const float e2 = __builtin_amdgcn_exp2f(v);
   return (1.f - e1) * __builtin_amdgcn_rcpf((1.f + e1) * (1.f + e2));
@@ -77,10 +78,12 @@ __device__ __forceinline__ float gate(float u, float v) {
 
 // Four split pairs in one statement: hi = cvt_pk (RNE), lo = rne16(v - hi) by v_fma_mix{lo,hi}
 // (one instruction per value; the compiler's own form is 2 conversions + a packed f32 add).
-// Only for VALU-produced inputs; the trailing s_nop 1 covers a VALU write -> MFMA operand read
-// (cdna_hip_programming.md 5.7 item 2).
+// The trailing s_nop 1 covers a VALU write -> MFMA operand read; NOPS leading wait states cover
+// inputs fresh from an MFMA (12 for an 8-pass 32x32x16; cdna_hip_programming.md 5.7 item 2).
+template <int NOPS>
 __device__ __forceinline__ void split8(const float (&v)[8], unsigned (&hi)[4], unsigned (&lo)[4]) {
   asm volatile(
+      "s_nop %16\n\t"
       "v_cvt_pk_f16_f32 %0, %8, %9\n\t"
       "v_cvt_pk_f16_f32 %1, %10, %11\n\t"
       "v_cvt_pk_f16_f32 %2, %12, %13\n\t"
@@ -96,7 +99,35 @@ __device__ __forceinline__ void split8(const float (&v)[8], unsigned (&hi)[4], u
       "s_nop 1"
       : "=&v"(hi[0]), "=&v"(hi[1]), "=&v"(hi[2]), "=&v"(hi[3]), "=&v"(lo[0]), "=&v"(lo[1]), "=&v"(lo[2]),
         "=&v"(lo[3])
-      : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]));
+      : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]), "i"(NOPS));
+}
+
+// GEMM-2 out-row seeds of 8 slots: c * (hi + lo) + b for the fp16 pairs of one k-step (hi halves
+// in dwords h, lo halves in l), two v_fma_mix_f32 per value; trailing s_nop 1: the results are
+// MFMA accumulator inputs.
+__device__ __forceinline__ void seed8(const u32x4 h, const u32x4 l, const f32x4 b0, const f32x4 b1, float c,
+                                      float (&o)[8]) {
+  asm volatile(
+      "v_fma_mix_f32 %0, %8, %16, %12 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %1, %8, %16, %13 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %2, %9, %16, %14 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %3, %9, %16, %15 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %4, %10, %16, %17 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %5, %10, %16, %18 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %6, %11, %16, %19 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %7, %11, %16, %20 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %0, %21, %16, %0 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %1, %21, %16, %1 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %2, %22, %16, %2 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %3, %22, %16, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %4, %23, %16, %4 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %5, %23, %16, %5 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %6, %24, %16, %6 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %7, %24, %16, %7 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "s_nop 1"
+      : "=&v"(o[0]), "=&v"(o[1]), "=&v"(o[2]), "=&v"(o[3]), "=&v"(o[4]), "=&v"(o[5]), "=&v"(o[6]), "=&v"(o[7])
+      : "v"(l[0]), "v"(l[1]), "v"(l[2]), "v"(l[3]), "v"(b0[0]), "v"(b0[1]), "v"(b0[2]), "v"(b0[3]), "v"(c),
+        "v"(b1[0]), "v"(b1[1]), "v"(b1[2]), "v"(b1[3]), "v"(h[0]), "v"(h[1]), "v"(h[2]), "v"(h[3]));
 }
 
 }  // namespace
@@ -240,18 +271,12 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
   auto x_seed = [&](const u32x4 (&b)[8], f32x16 (&seed)[2]) {
     const f32x4* bo = reinterpret_cast<const f32x4*>(s_bo + 32 * hh);
 #pragma unroll
-    for (int mo = 0; mo < 2; ++mo)
+    for (int s = 0; s < 4; ++s) {  // k-step s = slots 8s..8s+7 = seed[s >> 1][8(s & 1) + 0..7]
+      float o[8];
+      seed8(b[s], b[4 + s], bo[2 * s], bo[2 * s + 1], 0.70710677f, o);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4 bv = bo[4 * mo + q];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int r = 4 * q + i, s = 2 * mo + (r >> 3), j = r & 7;
-          // sqrt(.5) * (hi + lo) + b' as two v_fma_mix_f32
-          seed[mo][r] = __builtin_fmaf((float)h8(b[s])[j], 0.70710677f,
-                                       __builtin_fmaf((float)h8(b[4 + s])[j], 0.70710677f, bv[i]));
-        }
-      }
+      for (int j = 0; j < 8; ++j) seed[s >> 1][8 * (s & 1) + j] = o[j];
+    }
   };
 
   int blk = x_first + (blockIdx.x >> 3) * nw + wave;
@@ -422,7 +447,7 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
 #endif
       }
       unsigned hv[4], lv[4];
-      split8(gv, hv, lv);
+      split8<0>(gv, hv, lv);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         gh[s][k] = hv[k];
@@ -477,14 +502,19 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
       }
       u32x4* xp = reinterpret_cast<u32x4*>(a.x_out + PWG_ROW(bd.col + cl, hh));
 #pragma unroll
-      for (int k4 = 0; k4 < 4; ++k4) {
-        u32x4 vh, vl;
+      for (int k4 = 0; k4 < 4; ++k4) {  // k-step k4 = slots 8k4..8k4+7 = acc2[2 + (k4 >> 1)][8(k4 & 1) + j]
+        float v[8];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int p = 2 * (4 * k4 + k);  // slot pair p, p+1 -> mo = p >> 4, r = p & 15
-          const Pair2 pr = split2(acc2[2 + (p >> 4)][p & 15], acc2[2 + (p >> 4)][(p & 15) + 1]);
-          vh[k] = full || live ? pr.hi : 0u;  // padding columns stay zero
-          vl[k] = full || live ? pr.lo : 0u;
+        for (int j = 0; j < 8; ++j) v[j] = acc2[2 + (k4 >> 1)][8 * (k4 & 1) + j];
+        unsigned hv[4], lv[4];
+        split8<11>(v, hv, lv);  // inputs straight from the GEMM-2 MFMAs
+        u32x4 vh = {hv[0], hv[1], hv[2], hv[3]}, vl = {lv[0], lv[1], lv[2], lv[3]};
+        if (!full) {  // wave-uniform: only a block holding padding columns masks (they stay zero)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            vh[k] = live ? vh[k] : 0u;
+            vl[k] = live ? vl[k] : 0u;
+          }
         }
         PWG_ST_STREAM(xp + k4 * (PWG_PIECE / 4), vh);
         PWG_ST_STREAM(xp + (4 + k4) * (PWG_PIECE / 4), vl);

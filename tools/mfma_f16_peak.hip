@@ -12,6 +12,7 @@
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
 
@@ -67,6 +68,49 @@ __global__ void __launch_bounds__(512, 1) kern(const unsigned* in, float* out, i
   out[blockIdx.x * blockDim.x + threadIdx.x] = sum;
 }
 
+// kind 3: the same work on v_mfma_f32_16x16x32_f16 -- 8 m-tiles x 2 n-tiles of 16x16 per wave (the
+// same 128 x 32 output tile), per k-step 16 ds_read_b128 (A hi/lo) and 48 MFMAs
+__device__ __forceinline__ f32x4 mma16(u32x4 a, u32x4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+__global__ void __launch_bounds__(512, 1) kern16(const unsigned* in, float* out, int iters) {
+  extern __shared__ u32x4 lds[];
+  for (int i = threadIdx.x; i < 16 * 8 * 64; i += blockDim.x) {
+    u32x4 v = {in[i & 255], in[(i + 7) & 255], in[(i + 13) & 255], in[(i + 29) & 255]};
+    lds[i] = v;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  u32x4 b[2][2];
+  for (int n = 0; n < 2; ++n)
+    for (int h = 0; h < 2; ++h) b[n][h] = u32x4{in[lane], in[lane + 64 + n], in[lane + 128 + h], in[(lane + 192) & 255]};
+  f32x4 acc[8][2] = {};
+  const u32x4* al = lds + lane;
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int ks = (it * 4 + s) & 7;
+      u32x4 ah[8], alo[8];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) { ah[m] = al[((ks * 8 + m) * 2) * 64]; alo[m] = al[((ks * 8 + m) * 2 + 1) * 64]; }
+#pragma unroll
+      for (int m = 0; m < 8; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+          acc[m][n] = mma16(ah[m], b[n][0], acc[m][n]);
+          acc[m][n] = mma16(ah[m], b[n][1], acc[m][n]);
+          acc[m][n] = mma16(alo[m], b[n][0], acc[m][n]);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  float sum = 0.f;
+  for (int m = 0; m < 8; ++m)
+    for (int n = 0; n < 2; ++n)
+      for (int r = 0; r < 4; ++r) sum += acc[m][n][r];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = sum;
+}
+
 int main() {
   int dev = 0, ncu = 0;
   CHECK(hipGetDevice(&dev));
@@ -91,20 +135,22 @@ int main() {
   CHECK(hipFuncSetAttribute((const void*)kern<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   CHECK(hipFuncSetAttribute((const void*)kern<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   CHECK(hipFuncSetAttribute((const void*)kern<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  CHECK(hipFuncSetAttribute((const void*)kern16, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   for (int waves : {4, 8}) {
-    for (int kind = 0; kind < 3; ++kind) {
+    for (int kind = 0; kind < 4; ++kind) {
       const dim3 grid(ncu), block(64 * waves);
       for (int rep = 0; rep < 3; ++rep) {
         CHECK(hipEventRecord(e0));
         if (kind == 0) hipLaunchKernelGGL(kern<0>, grid, block, lds, 0, in, out, iters);
         else if (kind == 1) hipLaunchKernelGGL(kern<1>, grid, block, lds, 0, in, out, iters);
-        else hipLaunchKernelGGL(kern<2>, grid, block, lds, 0, in, out, iters);
+        else if (kind == 2) hipLaunchKernelGGL(kern<2>, grid, block, lds, 0, in, out, iters);
+        else hipLaunchKernelGGL(kern16, grid, block, lds, 0, in, out, iters);
         CHECK(hipEventRecord(e1));
         CHECK(hipEventSynchronize(e1));
         float ms = 0;
         CHECK(hipEventElapsedTime(&ms, e0, e1));
         const double mfmas = (double)ncu * waves * iters * 4 * 12;
-        const double tf = mfmas * 32 * 32 * 16 * 2 / (ms * 1e-3) / 1e12;
+        const double tf = mfmas * 32 * 32 * 16 * 2 * (kind == 3 ? 2 : 1) / (ms * 1e-3) / 1e12;  // kind 3: K=32 steps
         if (rep == 2)
           printf("kind %d waves/CU=%d: %.3f ms  %.1f TFLOP/s f16  (%.1f cyc/MFMA/SIMD at 2.4 GHz)\n", kind, waves, ms, tf,
                  ms * 1e-3 * 2.4e9 / (mfmas / (ncu * 4)));
