@@ -174,8 +174,12 @@ struct SplitSmem {
 #define PWG_LD_SKIP(p) (*(p))
 #endif
 
+#ifndef PWG_SPLIT_DIAG_NOTAP
+#define PWG_SPLIT_DIAG_NOTAP 0  // diagnostic: every tap reads the center row (wrong results)
+#endif
+
 #ifndef PWG_SPLIT_SEED_RELOAD
-#define PWG_SPLIT_SEED_RELOAD 1  // reloading the center row (L2 hit) avoids spills at 256 VGPRs
+#define PWG_SPLIT_SEED_RELOAD 0  // 1: re-load the center row for the seeds (diagnostic)
 #endif
 
 template <bool LAST, int TC>
@@ -237,7 +241,7 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
   // a lane's 128 B of tap row (block column c + lane column + tap offset): [0..3] hi k-steps,
   // [4..7] lo k-steps
   auto bload = [&](int c, int tap, u32x4 (&b)[8]) {
-    const u32x4* p = reinterpret_cast<const u32x4*>(a.x_in + PWG_ROW(c + cl + (tap - TC) * a.dil, hh));
+    const u32x4* p = reinterpret_cast<const u32x4*>(a.x_in + PWG_ROW(c + cl + (PWG_SPLIT_DIAG_NOTAP ? 0 : (tap - TC) * a.dil), hh));
 #pragma unroll
     for (int i = 0; i < 8; ++i) b[i] = p[i * (PWG_PIECE / 4)];
   };
@@ -366,18 +370,19 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
 #elif PWG_SPLIT_PRIO == 2
     __builtin_amdgcn_s_setprio(0);
 #endif
-    bload(bd.col, 1, b1);
+    // taps in the order 0, the other, the center: the center row is in registers at the end of
+    // GEMM 1 and becomes the GEMM-2 out-row seeds right there (re-loading it later missed L2 for
+    // ~half the blocks: +1.05 GB of HBM reads per launch)
+    constexpr int T1 = TC == 1 ? 2 : 1;
+    bload(bd.col, T1, b1);
     mma_tap(acc, b0, 0);
-    load_dv();  // in flight during taps 1 and 2
-    bload(bd.col, 2, b0);
-    mma_tap(acc, b1, 1);
-#if !PWG_SPLIT_SEED_RELOAD
-    if (TC == 1) x_seed(b1, seed);
-#endif
+    load_dv();  // in flight during the other two taps
+    bload(bd.col, TC, b0);
+    mma_tap(acc, b1, T1);
     bload(col_next, 0, b1);
-    mma_tap(acc, b0, 2);
+    mma_tap(acc, b0, TC);
 #if !PWG_SPLIT_SEED_RELOAD
-    if (TC == 2) x_seed(b0, seed);
+    x_seed(b0, seed);
 #endif
 
     PWG_TR(const unsigned long long tr_b = clock64());
@@ -457,7 +462,11 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
     if (!LAST) {
 #if PWG_SPLIT_SEED_RELOAD
       u32x4 bc[8];
+#if PWG_SPLIT_DIAG_NORELOAD  // diagnostic: no center reload (wrong results)
+      for (int i = 0; i < 8; ++i) bc[i] = b1[i];
+#else
       bload(bd.col, TC, bc);  // the center tap row again (an L2 hit): fewer registers live in GEMM 1
+#endif
       x_seed(bc, seed);
 #endif
       acc2[2] = seed[0];

@@ -1,0 +1,26 @@
+#!/bin/bash
+# FETCH_SIZE / WRITE_SIZE per split-layer launch for prebuilt variants (GPU box).
+# Usage: bash tools/fetch_ab.sh OUT name1 name2 ...   ("base" = default library)
+set -e
+OUT=$1; shift
+mkdir -p "$OUT"
+export TMPDIR=/tmp PWG_NO_BUILD=1
+for v in "$@"; do
+  if [ "$v" = base ]; then lib=parallelwavegan_amd/lib/libpwg_hip.so; else lib=parallelwavegan_amd/lib/variants/libpwg_$v.so; fi
+  mkdir -p "$OUT/$v"
+  for c in FETCH_SIZE WRITE_SIZE; do
+    PWG_LIB_PATH=$lib timeout -k 10 120 rocprofv3 --pmc $c --output-format csv -d "$OUT/$v/$c" -o pmc -- python bench.py --steps 1 --warmup 1 --cpu-seconds 0 > "$OUT/$v/$c.log" 2>&1
+  done
+  python - "$OUT/$v" "$v" <<'PY'
+import csv, glob, sys, collections
+root, name = sys.argv[1], sys.argv[2]
+tot = collections.defaultdict(lambda: collections.defaultdict(float)); n = collections.defaultdict(set)
+for p in glob.glob(root + "/**/*counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(p)):
+        k = r["Kernel_Name"]
+        if "layer_split_kernel<false" not in k: continue
+        tot[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
+f = tot["FETCH_SIZE"]; w = tot["WRITE_SIZE"]
+print(name, "fetch GB/launch (x2)", round(sum(f.values()) / max(len(f), 1) * 2048 / 1e9, 3), "write GB/launch", round(sum(w.values()) / max(len(w), 1) * 1024 / 1e9, 3))
+PY
+done
