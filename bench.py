@@ -48,11 +48,14 @@ def split_layer_bytes_per_sample(params, H, L):
     return (first + (L - 2) * mid + last) / L + 4 * G / H
 
 
-def split_executed_flop_per_block(L):
-    """f16 MFMA FLOP one 32-sample block executes, averaged over the L launches: 144 GEMM-1 +
-    12 aux/bias + 48 GEMM-2 v_mfma_f32_32x32x16_f16 (32,768 FLOP each); the last layer runs 24
-    GEMM-2 MFMAs and its head as fp32 MFMA (not counted)."""
-    return 32768 * ((L - 1) * 204 + (144 + 12 + 24)) / L
+def split_executed_flop_per_block(L, kernel="split16"):
+    """f16 MFMA FLOP one 32-sample block executes, averaged over the L launches. split: 144 GEMM-1
+    + 12 aux/bias + 48 GEMM-2 v_mfma_f32_32x32x16_f16 (32,768 FLOP each), the last layer 24 GEMM-2;
+    split16: 288 + 16 + 96 v_mfma_f32_16x16x32_f16 (16,384 FLOP each), the last layer 48
+    GEMM-2. The last layer's head runs as fp32 MFMA (not counted)."""
+    if kernel == "split":
+        return 32768 * ((L - 1) * 204 + (144 + 12 + 24)) / L
+    return 16384 * ((L - 1) * 400 + (288 + 16 + 48)) / L
 
 
 def layer_flops_per_sample(params):
@@ -287,7 +290,7 @@ def main():
     ap.add_argument("--utts", type=int, default=32, help="utterances per GPU per step")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "layer_traffic.json"))
-    ap.add_argument("--layer-kernel", default=None, choices=["split", "persistent", "tiled"],
+    ap.add_argument("--layer-kernel", default=None, choices=["split", "split16", "persistent", "tiled"],
                     help="default: split where the shape allows, else persistent (the engine default)")
     ap.add_argument("--waves-per-wg", type=int, default=None)
     ap.add_argument("--wg-per-cu", type=int, default=None)
@@ -302,8 +305,8 @@ def main():
     eng = Engine(params, dev)
     if args.layer_kernel is None:
         try:
-            eng.set_option("layer_kernel", "split")
-            args.layer_kernel = "split"
+            eng.set_option("layer_kernel", "split16")
+            args.layer_kernel = "split16"
         except NotImplementedError:
             args.layer_kernel = "persistent"
     eng.set_option("layer_kernel", args.layer_kernel)
@@ -390,14 +393,14 @@ def main():
         except (OSError, ValueError):
             traffic = None
     L = params["layers"]
-    if args.layer_kernel == "split":
+    if args.layer_kernel in ("split", "split16"):
         # HBM-bound: algorithmic bytes of the engine's layer per launch / launch time
         bytes_launch = split_layer_bytes_per_sample(params, H, L) * plan.total_samples
         n_blocks = int(sum(-(-int(f) * H // 128) * 4 for f in lengths))
-        exec_flop = split_executed_flop_per_block(L) * n_blocks
+        exec_flop = split_executed_flop_per_block(L, args.layer_kernel) * n_blocks
         achieved_gbs = bytes_launch / layer_avg_s / 1e9
         roofline = {
-            "kernel": "residual layer (split-f16 persistent kernel, one fused WaveNet residual block)",
+            "kernel": f"residual layer ({args.layer_kernel} persistent kernel, one fused WaveNet residual block)",
             "bound": "hbm",
             "achieved": round(achieved_gbs, 1),
             "peak": HBM_PEAK_GBS,
@@ -459,7 +462,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32 (fp16 hi+lo pair operands, 3 f16 MFMAs per product, fp32 accumulate)"
-                 if args.layer_kernel == "split" else "f32",
+                 if args.layer_kernel in ("split", "split16") else "f32",
         "data": "synthetic (seeded N(0,1) mel + noise, seeded kaiming-init weights)",
         "config": {
             "workload": f"{args.config} generator inference, {args.utts} ragged utterances per GPU per step",

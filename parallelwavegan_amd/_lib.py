@@ -23,6 +23,7 @@ CSRC = [
     os.path.join(PKG_DIR, "csrc", "pwg_capi.hip"),
     os.path.join(PKG_DIR, "csrc", "pwg_cnet.hip"),
     os.path.join(PKG_DIR, "csrc", "pwg_split.hip"),
+    os.path.join(PKG_DIR, "csrc", "pwg_split16.hip"),
 ]
 HEADERS = [
     os.path.join(REPO_DIR, "include", "pwg.h"),

@@ -202,6 +202,9 @@ hipError_t launch_aux_proj(const AuxProjArgs& a, int layers, hipStream_t s);
 hipError_t launch_first_conv(const FirstConvArgs& a, long long n_tiles, hipStream_t s);
 hipError_t launch_layer(const LayerArgs& a, int mt, int m2t, bool last, long long n_tiles, hipStream_t s);
 hipError_t launch_first_conv_split(const FirstConvArgs& a, long long n_tiles, hipStream_t s);
+hipError_t launch_first_conv_split16(const FirstConvArgs& a, long long n_tiles, hipStream_t s);
+hipError_t launch_layer_split16(const SplitArgs& a, bool last, int tap_center, int waves_per_wg, int n_wg,
+                                hipStream_t s);
 hipError_t launch_layer_split(const SplitArgs& a, bool last, int tap_center, int waves_per_wg, int n_wg,
                               hipStream_t s);
 hipError_t launch_layer_persistent(const PersistArgs& a, int mt, int m2t, bool last, int waves_per_wg, int n_wg,

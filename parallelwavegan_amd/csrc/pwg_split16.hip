@@ -1,0 +1,528 @@
+// Split-f16 residual layer on v_mfma_f32_16x16x32_f16 (PWG_OPT_LAYER_KERNEL = 3).
+//
+// Same arithmetic as pwg_split.hip (fp32 operands as fp16 hi+lo pairs, three MFMAs per product,
+// fp32 accumulate) on the 16x16x32 shape: per wave a 128-row x 32-column block is
+// 8 m-tiles x 2 n-tiles of 16x16. On this power-limited chip the 16x16x32 loop delivered 11 % more
+// f16 FLOP/s than the 32x32x16 loop at the same tile (tools/mfma_f16_peak.hip, kind 3 vs 1), and
+// its K = 32 packs the whole aux term (three products of two frames plus the bias) into one MFMA.
+//
+// Lane l: c = l & 15 (A row / B column inside a 16-tile), g = l >> 4 (k group: k = 8g + j).
+// Accumulator: column c, rows 4g + i.
+// Channel of k element (k-step ks, group g, element j), for x (GEMM-1 B) and for the gate values
+// (GEMM-2 B) alike:  chan16(ks, g, j) = 16 (2ks + (j >> 2)) + 4g + (j & 3)
+// which is exactly the accumulator position (m-tile 2ks + (j >> 2), register j & 3) of lane
+// group g: a lane's x pieces are its GEMM-2 out rows and its gate values its GEMM-2 B operand.
+//
+// Tiled layout (32 columns, 8 KB per tile, 16-B pieces, lane (c, g) of n-tile nt):
+//   x     [nt 2][ks 2][hi/lo 2][g 4][c 16][16 B]   piece = 8 fp16 halves of chan16(ks, g, 0..7)
+//   skip  [nt 2][ms 4][g 4][c 16][16 B]           piece = fp32 rows 16ms + 4g + 0..3
+// so one wave-instruction reads or writes 1 KB contiguous.
+// Reference: layers/residual_block.py:102-140, models/parallel_wavegan.py:131-138,160-171.
+#include "pwg_internal.h"
+
+namespace pwg {
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mma16(u32x4 a, u32x4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
+                                                0);
+}
+
+// rows pre-scaled into exp2 arguments (see pwg_split.hip gate())
+__device__ __forceinline__ float gate16(float u, float v) {
+  u = fminf(u, 64.f);
+  const float e1 = __builtin_amdgcn_exp2f(u);
+  const float e2 = __builtin_amdgcn_exp2f(v);
+  return (1.f - e1) * __builtin_amdgcn_rcpf((1.f + e1) * (1.f + e2));
+}
+
+// 8 values -> 4 hi dwords + 4 lo dwords (v_cvt_pk_f16_f32 + v_fma_mix{lo,hi}_f16). NOPS leading
+// wait states for MFMA-fresh inputs, trailing s_nop 1 for MFMA consumers (cdna_hip_programming.md
+// 5.7 item 2).
+template <int NOPS>
+__device__ __forceinline__ void split8x(const float (&v)[8], u32x4& hi, u32x4& lo) {
+  unsigned h0, h1, h2, h3, l0, l1, l2, l3;
+  asm volatile(
+      "s_nop %16\n\t"
+      "v_cvt_pk_f16_f32 %0, %8, %9\n\t"
+      "v_cvt_pk_f16_f32 %1, %10, %11\n\t"
+      "v_cvt_pk_f16_f32 %2, %12, %13\n\t"
+      "v_cvt_pk_f16_f32 %3, %14, %15\n\t"
+      "v_fma_mixlo_f16 %4, %0, -1.0, %8 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixlo_f16 %5, %1, -1.0, %10 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixlo_f16 %6, %2, -1.0, %12 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixlo_f16 %7, %3, -1.0, %14 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %4, %0, -1.0, %9 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %5, %1, -1.0, %11 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %6, %2, -1.0, %13 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %7, %3, -1.0, %15 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "s_nop 1"
+      : "=&v"(h0), "=&v"(h1), "=&v"(h2), "=&v"(h3), "=&v"(l0), "=&v"(l1), "=&v"(l2), "=&v"(l3)
+      : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]), "i"(NOPS));
+  hi = u32x4{h0, h1, h2, h3};
+  lo = u32x4{l0, l1, l2, l3};
+}
+
+// c * (hi + lo) + b for the 8 fp16 pairs of one piece pair, two v_fma_mix_f32 each; trailing
+// s_nop 1: the results seed MFMA accumulators.
+__device__ __forceinline__ void seed8x(const u32x4 h, const u32x4 l, const f32x4 b0, const f32x4 b1, float c,
+                                       float (&o)[8]) {
+  asm volatile(
+      "v_fma_mix_f32 %0, %8, %16, %12 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %1, %8, %16, %13 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %2, %9, %16, %14 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %3, %9, %16, %15 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %4, %10, %16, %17 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %5, %10, %16, %18 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %6, %11, %16, %19 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %7, %11, %16, %20 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %0, %21, %16, %0 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %1, %21, %16, %1 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %2, %22, %16, %2 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %3, %22, %16, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %4, %23, %16, %4 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %5, %23, %16, %5 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %6, %24, %16, %6 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %7, %24, %16, %7 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "s_nop 1"
+      : "=&v"(o[0]), "=&v"(o[1]), "=&v"(o[2]), "=&v"(o[3]), "=&v"(o[4]), "=&v"(o[5]), "=&v"(o[6]), "=&v"(o[7])
+      : "v"(l[0]), "v"(l[1]), "v"(l[2]), "v"(l[3]), "v"(b0[0]), "v"(b0[1]), "v"(b0[2]), "v"(b0[3]), "v"(c),
+        "v"(b1[0]), "v"(b1[1]), "v"(b1[2]), "v"(b1[3]), "v"(h[0]), "v"(h[1]), "v"(h[2]), "v"(h[3]));
+}
+
+struct Pair16 {
+  unsigned hi, lo;
+};
+__device__ __forceinline__ Pair16 split_pair16(float v0, float v1) {
+  typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+  const _Float16 h0 = (_Float16)v0, h1 = (_Float16)v1;
+  const _Float16 l0 = (_Float16)(v0 - (float)h0), l1 = (_Float16)(v1 - (float)h1);
+  return {__builtin_bit_cast(unsigned, f16x2{h0, h1}), __builtin_bit_cast(unsigned, f16x2{l0, l1})};
+}
+
+}  // namespace
+
+// dword offset of piece q of column c (n-tile from c) for lane group g; pieces of one n-tile are
+// 256 dwords (1 KB) apart
+__device__ __forceinline__ size_t row16(int c, int g) {
+  return (size_t)(c >> 5) * 2048 + (size_t)((c >> 4) & 1) * 1024 + (size_t)g * 64 + (size_t)(c & 15) * 4;
+}
+
+// LDS image of one layer (dwords): GEMM-1 A fragments [tap 3][ks 2][m 8][hi/lo 2][lane 64][4]
+// | GEMM-2 [ks 2][m 8][hi/lo 2][lane 64][4] | gate bias pairs [m 8][c 16] | sqrt(.5) b_out [g 4][16]
+// | last layer: head W1 [ms 4][m3 4][lane 64][4] fp32 + b1 [g 4][16].
+struct Split16Smem {
+  static constexpr int WG = 3 * 2 * 8 * 2 * 64 * 4;
+  static constexpr int W2 = 2 * 8 * 2 * 64 * 4;
+  static constexpr int BG = 8 * 16;
+  static constexpr int BO = 64;
+  static constexpr int HW1 = 4 * 4 * 64 * 4 + 64;
+  static constexpr int dwords(bool last) { return WG + W2 + BG + BO + (last ? HW1 : 0); }
+};
+static_assert(Split16Smem::WG + Split16Smem::W2 + Split16Smem::BG + Split16Smem::BO == SPLIT_LAYER_DWORDS,
+              "split16 layer image size");
+
+template <bool LAST, int TC>
+__global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned smem16[];
+  unsigned* s_wg = smem16;
+  unsigned* s_w2 = s_wg + Split16Smem::WG;
+  unsigned* s_bg = s_w2 + Split16Smem::W2;
+  float* s_bo = reinterpret_cast<float*>(s_bg + Split16Smem::BG);
+  float* s_hw1 = s_bo + Split16Smem::BO;
+  {
+    const int nthr = blockDim.x;
+    const u32x4* src = reinterpret_cast<const u32x4*>(a.wg);
+    u32x4* dst = reinterpret_cast<u32x4*>(s_wg);
+    for (int i = threadIdx.x; i < SPLIT_LAYER_DWORDS / 4; i += nthr) dst[i] = src[i];
+    if (LAST) {
+      src = reinterpret_cast<const u32x4*>(a.hw1);
+      dst = reinterpret_cast<u32x4*>(s_hw1);
+      for (int i = threadIdx.x; i < Split16Smem::HW1 / 4; i += nthr) dst[i] = src[i];
+    }
+    __syncthreads();
+  }
+
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4;
+  const int c = lane & 15;
+  const int nw = blockDim.x >> 6;
+  const int xcd = blockIdx.x & 7;
+  const int wave = threadIdx.x >> 6;
+  auto xcd_waves = [&](int y) { return (((int)gridDim.x - y + 7) >> 3) * nw; };
+  auto xcd_first = [&](int y) { return (int)((long long)a.n_blocks * y / 8); };
+  const int x_first = xcd_first(xcd), x_end = xcd_first(xcd + 1), x_waves = xcd_waves(xcd);
+  int victim = 0;
+  auto ticket_issue = [&]() -> int {
+    int v = 0;
+    if (victim == 0 && lane == 0)
+      v = __hip_atomic_fetch_add(a.ctr + xcd * SCHED_CTR_STRIDE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return v;
+  };
+  auto ticket_resolve = [&](int v) -> int {
+    if (victim == 0) {
+      const int i = x_first + 2 * x_waves + __builtin_amdgcn_readfirstlane(v);
+      if (i < x_end) return i;
+      victim = 1;
+    }
+    for (; victim < 8; ++victim) {
+      const int y = (xcd + victim) & 7;
+      int tk = 0;
+      if (lane == 0)
+        tk = __hip_atomic_fetch_add(a.ctr + y * SCHED_CTR_STRIDE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int i = xcd_first(y) + 2 * xcd_waves(y) + __builtin_amdgcn_readfirstlane(tk);
+      if (i < xcd_first(y + 1)) return i;
+    }
+    return -1;
+  };
+
+  // a lane's tap row pieces for both n-tiles: b[nt*4 + ks*2 + hl]
+  auto bload = [&](int col, int tap, u32x4 (&b)[8]) {
+    const int cc = col + (tap - TC) * a.dil;
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const u32x4* p = reinterpret_cast<const u32x4*>(a.x_in + row16(cc + 16 * nt + c, g));
+#pragma unroll
+      for (int q = 0; q < 4; ++q) b[nt * 4 + q] = p[q * 64];
+    }
+  };
+  const u32x4* wgl = reinterpret_cast<const u32x4*>(s_wg) + lane;
+  auto mma_tap = [&](f32x4 (&acc)[8][2], const u32x4 (&b)[8], int tap) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int mh = 0; mh < 2; ++mh) {  // 4 m-tiles per group: fragments of 4 read ahead
+        u32x4 ah[4], al[4];
+#pragma unroll
+        for (int mm = 0; mm < 4; ++mm) {
+          const int m = 4 * mh + mm;
+          ah[mm] = wgl[(((tap * 2 + ks) * 8 + m) * 2) * 64];
+          al[mm] = wgl[(((tap * 2 + ks) * 8 + m) * 2 + 1) * 64];
+        }
+#pragma unroll
+        for (int mm = 0; mm < 4; ++mm)
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) {
+            f32x4& ac = acc[4 * mh + mm][nt];
+            ac = mma16(ah[mm], b[nt * 4 + ks * 2], ac);
+            ac = mma16(ah[mm], b[nt * 4 + ks * 2 + 1], ac);
+            ac = mma16(al[mm], b[nt * 4 + ks * 2], ac);
+          }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+  // GEMM-2 out-row seeds sqrt(.5)(x + b_out) from the center tap's pieces: acc2[4 + 2ks + (j>>2)][nt][j&3]
+  const f32x4* bo_l = reinterpret_cast<const f32x4*>(s_bo + 16 * g);
+  auto x_seed = [&](const u32x4 (&b)[8], f32x4 (&acc2)[8][2]) {
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        float o[8];
+        seed8x(b[nt * 4 + ks * 2], b[nt * 4 + ks * 2 + 1], bo_l[2 * ks], bo_l[2 * ks + 1], 0.70710677f, o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc2[4 + 2 * ks + (j >> 2)][nt][j & 3] = o[j];
+      }
+  };
+
+  int blk = x_first + (blockIdx.x >> 3) * nw + wave;
+  int nblk = blk + x_waves;
+  if (blk >= x_end) blk = -1;
+  if (nblk >= x_end) nblk = -1;
+  if (blk < 0) return;
+  BlockDesc bdn = a.blocks[blk];
+  u32x4 b0[8], b1[8];
+  bload(bdn.col, 0, b0);
+
+  while (true) {
+    const BlockDesc bd = bdn;
+    bdn = a.blocks[nblk >= 0 ? nblk : blk];
+    const int col_next = nblk >= 0 ? bdn.col : bd.col;
+    const bool full = bd.t0 + 32 <= bd.T;
+
+    // aux operands: lane group g covers window frames fw0 + 2g, fw0 + 2g + 1; K slots
+    // [Dh0 Dh1 Dl0 Dl1 Dh0 Dh1 bh bl] x [wh0 wh1 wh0 wh1 wl0 wl1 1 1] (bias in group 0 only)
+    const int fw0 = bd.t0 / a.H - a.J1;
+    unsigned dv[2][8];  // [frame][m]
+    auto load_dv = [&]() {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int f = fw0 + 2 * g + j;
+        const int fc = f < 0 ? 0 : (f >= bd.frames ? bd.frames - 1 : f);  // weight 0 there
+        const unsigned* drow = a.d + (size_t)(bd.frame_base + fc) * 128 + c;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) dv[j][m] = drow[16 * m];
+      }
+    };
+    float bw[2][2];  // [nt][frame]
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const int t = bd.t0 + 16 * nt + c;
+      const bool live = t < bd.T;
+      const int tc = live ? t : bd.T - 1;
+      int roff;
+      if (bd.frames < a.Fmin) roff = a.tab_small + (a.H * bd.frames * (bd.frames - 1) / 2 + tc) * AUX_J4;
+      else if (tc < a.TL) roff = a.tab_left + tc * AUX_J4;
+      else if (tc >= bd.T - a.TR) roff = a.tab_right + (bd.T - 1 - tc) * AUX_J4;
+      else roff = (tc % a.H) * AUX_J4;
+      const int shift = t / a.H - bd.t0 / a.H;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int idx = 2 * g + j - shift;
+        const bool ok = live && idx >= 0 && idx < AUX_J4;
+        const float w = a.tab[roff + (idx < 0 ? 0 : (idx >= AUX_J4 ? AUX_J4 - 1 : idx))];
+        bw[nt][j] = ok ? w : 0.f;
+      }
+    }
+
+    // ---- GEMM 1: taps 0, other, center (the center row becomes the GEMM-2 seeds at the end)
+    f32x4 acc[8][2];
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) acc[m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 acc2[8][2];
+    constexpr int T1 = TC == 1 ? 2 : 1;
+    bload(bd.col, T1, b1);
+    mma_tap(acc, b0, 0);
+    load_dv();
+    bload(bd.col, TC, b0);
+    mma_tap(acc, b1, T1);
+    bload(col_next, 0, b1);
+    mma_tap(acc, b0, TC);
+    if (!LAST) x_seed(b0, acc2);
+
+    int ticket = 0;
+    if (nblk >= 0) ticket = ticket_issue();
+    // skip seeds: old skip sum (layer 0: the sum of all layers' skip biases, [g][16] layout)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int ms = 0; ms < 4; ++ms) {
+        if (a.first) {
+          acc2[ms][nt] = reinterpret_cast<const f32x4*>(a.skip0 + 16 * g)[ms];
+        } else {
+          const f32x4* sp = reinterpret_cast<const f32x4*>(a.skip + row16(bd.col + 16 * nt + c, g));
+          acc2[ms][nt] = __builtin_nontemporal_load(sp + ms * 64);
+        }
+      }
+
+    // ---- aux term + gate bias: one MFMA per (m, nt)
+    {
+      const Pair16 bias_one = split_pair16(g == 0 ? 1.f : 0.f, g == 0 ? 1.f : 0.f);
+      u32x4 bB[2];
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const Pair16 w = split_pair16(bw[nt][0], bw[nt][1]);
+        // [wh0 wh1 | wh0 wh1 | wl0 wl1 | 1 1]
+        bB[nt] = u32x4{w.hi, w.hi, w.lo, bias_one.hi};
+      }
+      const unsigned* bgl = s_bg + c;
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const unsigned bgp = g == 0 ? bgl[16 * m] : 0u;  // (bias hi | bias lo << 16)
+        const unsigned dh = __builtin_amdgcn_perm(dv[1][m], dv[0][m], 0x05040100u);
+        const unsigned dl = __builtin_amdgcn_perm(dv[1][m], dv[0][m], 0x07060302u);
+        // [Dh0 Dh1 | Dl0 Dl1 | Dh0 Dh1 | bh bl]
+        const u32x4 aA = {dh, dl, dh, bgp};
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) acc[m][nt] = mma16(aA, bB[nt], acc[m][nt]);
+      }
+    }
+
+    // ---- gate -> GEMM-2 B pairs: k-step ks element j = channel chan16(ks, g, j) = acc row
+    u32x4 gh[2][2], gl[2][2];  // [nt][ks]
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        float gv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int m = 2 * ks + (j >> 2), i = j & 3;
+          gv[j] = gate16(acc[m][nt][i], acc[m + 4][nt][i]);
+        }
+        split8x<0>(gv, gh[nt][ks], gl[nt][ks]);
+      }
+
+    // ---- GEMM 2: [skip; out] rows, 8 m-tiles (last layer: the 4 skip tiles)
+    constexpr int M2 = LAST ? 4 : 8;
+    const u32x4* w2l = reinterpret_cast<const u32x4*>(s_w2) + lane;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int mh = 0; mh < M2 / 4; ++mh) {
+        u32x4 ah[4], al[4];
+#pragma unroll
+        for (int mm = 0; mm < 4; ++mm) {
+          ah[mm] = w2l[((ks * 8 + 4 * mh + mm) * 2) * 64];
+          al[mm] = w2l[((ks * 8 + 4 * mh + mm) * 2 + 1) * 64];
+        }
+#pragma unroll
+        for (int mm = 0; mm < 4; ++mm)
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) {
+            f32x4& ac = acc2[4 * mh + mm][nt];
+            ac = mma16(ah[mm], gh[nt][ks], ac);
+            ac = mma16(ah[mm], gl[nt][ks], ac);
+            ac = mma16(al[mm], gh[nt][ks], ac);
+          }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+
+    if (!LAST) {
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const int col = bd.col + 16 * nt + c;
+        const bool live = bd.t0 + 16 * nt + c < bd.T;
+        f32x4* sp = reinterpret_cast<f32x4*>(a.skip + row16(col, g));
+#pragma unroll
+        for (int ms = 0; ms < 4; ++ms) __builtin_nontemporal_store(acc2[ms][nt], sp + ms * 64);
+        u32x4* xp = reinterpret_cast<u32x4*>(a.x_out + row16(col, g));
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          float v[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = acc2[4 + 2 * ks + (j >> 2)][nt][j & 3];
+          u32x4 vh, vl;
+          split8x<11>(v, vh, vl);  // inputs straight from the GEMM-2 MFMAs
+          if (!full) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              vh[k] = live ? vh[k] : 0u;
+              vl[k] = live ? vl[k] : 0u;
+            }
+          }
+          __builtin_nontemporal_store(vh, xp + (ks * 2) * 64);
+          __builtin_nontemporal_store(vl, xp + (ks * 2 + 1) * 64);
+        }
+      }
+    } else {
+      // ---- fused output head (models/parallel_wavegan.py:131-138,166-171) on v_mfma_f32_16x16x4f32:
+      //      h1 = W1h . relu(skip * sqrt(1/L)) + b1h, k-step (ms, i): lane group g supplies skip row
+      //      16ms + 4g + i; then y = W2h . relu(h1) + b2h across the 4 lane groups
+      const f32x4* hw1 = reinterpret_cast<const f32x4*>(s_hw1) + lane;
+      const f32x4* hb1 = reinterpret_cast<const f32x4*>(s_hw1 + 4 * 4 * 64 * 4 + 16 * g);
+      f32x4 acc3[4][2];
+#pragma unroll
+      for (int m3 = 0; m3 < 4; ++m3)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) acc3[m3][nt] = hb1[m3];
+#pragma unroll
+      for (int ms = 0; ms < 4; ++ms)
+#pragma unroll
+        for (int m3 = 0; m3 < 4; ++m3) {
+          const f32x4 wv = hw1[(ms * 4 + m3) * 64];
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) {
+              const float hs = fmaxf(acc2[ms][nt][i] * a.skip_scale, 0.f);
+              acc3[m3][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[i], hs, acc3[m3][nt], 0, 0, 0);
+            }
+        }
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const int t = bd.t0 + 16 * nt + c;
+        const bool live = t < bd.T;
+        float* out = a.out + (size_t)bd.io_off * a.O + (size_t)t * a.out_stride_t;
+        for (int oc = 0; oc < a.O; ++oc) {
+          const f32x4* w = reinterpret_cast<const f32x4*>(a.hw2 + ((size_t)oc * 4 + g) * 16);
+          float part = 0.f;
+#pragma unroll
+          for (int m3 = 0; m3 < 4; ++m3) {
+            const f32x4 wq = w[m3];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) part = fmaf(wq[i], fmaxf(acc3[m3][nt][i], 0.f), part);
+          }
+          part += __shfl_xor(part, 16);
+          part += __shfl_xor(part, 32);
+          if (g == 0 && live) out[(size_t)oc * a.out_stride_o] = part + a.hb2[oc];
+        }
+      }
+    }
+
+    if (nblk < 0) break;
+    blk = nblk;
+    nblk = ticket_resolve(ticket);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) b0[i] = b1[i];
+  }
+}
+
+// first_conv (1x1, 1 -> 64, bias) into the split16 x layout; gap tiles zero both buffers.
+__global__ void __launch_bounds__(256) pwg_first_conv_split16_kernel(const FirstConvArgs a) {
+  const long long tile = blockIdx.x;
+  unsigned* x = reinterpret_cast<unsigned*>(a.x);
+  unsigned* x1 = reinterpret_cast<unsigned*>(a.x1);
+  if (tile >= a.n_work) {
+    const long long col0 = a.gap_col0[tile - a.n_work];
+    for (int idx = threadIdx.x; idx < 64 * TILE; idx += 256) {
+      x[(size_t)col0 * 64 + idx] = 0u;
+      x1[(size_t)col0 * 64 + idx] = 0u;
+    }
+    return;
+  }
+  const UttDesc ud = a.utts[a.tile_utt[tile]];
+  const long long col0 = ud.seg_base + (tile - ud.first_tile) * TILE;
+  const long long t0 = col0 - ud.seg_base;
+  // 128 columns = 4 tiles of 2048 dwords, walked in memory order:
+  // [sub 4][nt 2][ks 2][hl 2][g 4][c 16][dw 4]
+  for (int idx = threadIdx.x; idx < 64 * TILE; idx += 256) {
+    const int sub = idx >> 11, rem = idx & 2047;
+    const int nt = rem >> 10, ks = (rem >> 9) & 1, hl = (rem >> 8) & 1, g = (rem >> 6) & 3, cc = (rem >> 2) & 15,
+              dw = rem & 3;
+    const int jcol = 32 * sub + 16 * nt + cc;
+    const long long t = t0 + jcol;
+    unsigned v = 0u;
+    if (t < ud.T) {
+      const float z = a.noise[ud.io_off + t];
+      float y[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int j = 2 * dw + e;
+        const int ch = 16 * (2 * ks + (j >> 2)) + 4 * g + (j & 3);
+        y[e] = fmaf(a.w[ch], z, a.b[ch]);
+      }
+      const Pair16 pr = split_pair16(y[0], y[1]);
+      v = hl ? pr.lo : pr.hi;
+    }
+    x[(size_t)col0 * 64 + idx] = v;
+  }
+}
+
+hipError_t launch_first_conv_split16(const FirstConvArgs& a, long long n_tiles, hipStream_t s) {
+  hipLaunchKernelGGL(pwg_first_conv_split16_kernel, dim3((unsigned)n_tiles), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_layer_split16(const SplitArgs& a, bool last, int tap_center, int waves_per_wg, int n_wg,
+                                hipStream_t s) {
+  if (waves_per_wg > 8) waves_per_wg = 8;
+  const dim3 grid((unsigned)n_wg), block((unsigned)(64 * waves_per_wg));
+#define PWG_SPLIT16_LAUNCH(LAST_, TC_)                                                                  \
+  {                                                                                                     \
+    const size_t lds = sizeof(unsigned) * Split16Smem::dwords(LAST_);                                   \
+    auto kfn = &pwg_layer_split16_kernel<LAST_, TC_>;                                                   \
+    hipError_t e_ = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),                             \
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);           \
+    if (e_ != hipSuccess) return e_;                                                                    \
+    hipLaunchKernelGGL(kfn, grid, block, lds, s, a);                                                    \
+    return hipGetLastError();                                                                           \
+  }
+  if (tap_center == 1) {
+    if (last) PWG_SPLIT16_LAUNCH(true, 1) else PWG_SPLIT16_LAUNCH(false, 1)
+  } else if (tap_center == 2) {
+    if (last) PWG_SPLIT16_LAUNCH(true, 2) else PWG_SPLIT16_LAUNCH(false, 2)
+  }
+#undef PWG_SPLIT16_LAUNCH
+  return hipErrorInvalidValue;
+}
+
+}  // namespace pwg

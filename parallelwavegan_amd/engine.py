@@ -257,7 +257,7 @@ class Engine:
         return self._workspace
 
     # ---------------------------------------------------------------- options
-    LAYER_KERNELS = {"persistent": 0, "tiled": 1, "split": 2}
+    LAYER_KERNELS = {"persistent": 0, "tiled": 1, "split": 2, "split16": 3}
 
     def set_option(self, option, value):
         """pwg_set_option: option in {"layer_kernel", "waves_per_wg", "wg_per_cu"}."""

@@ -18,7 +18,7 @@ tot = collections.defaultdict(lambda: collections.defaultdict(float)); n = colle
 for p in glob.glob(root + "/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(p)):
         k = r["Kernel_Name"]
-        if "layer_split_kernel<false" not in k: continue
+        if "_kernel<false" not in k or "layer_split" not in k: continue
         tot[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
 f = tot["FETCH_SIZE"]; w = tot["WRITE_SIZE"]
 print(name, "fetch GB/launch (x2)", round(sum(f.values()) / max(len(f), 1) * 2048 / 1e9, 3), "write GB/launch", round(sum(w.values()) / max(len(w), 1) * 1024 / 1e9, 3))

@@ -15,5 +15,5 @@ cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_RO
 
 cd "$GRAFT_REPO_ROOT"
 # PMC passes (separate rocprofv3 runs) -> HBM traffic per split-layer launch
-bash tools/profile_pmc.sh "$OUT/pmc" && python tools/pmc_summary.py "$OUT/pmc" "$OUT/pmc_summary.json" > /dev/null && python tools/make_traffic_json.py "$OUT/pmc_summary.json" "$OUT/layer_traffic.json" split
+bash tools/profile_pmc.sh "$OUT/pmc" && python tools/pmc_summary.py "$OUT/pmc" "$OUT/pmc_summary.json" > /dev/null && python tools/make_traffic_json.py "$OUT/pmc_summary.json" "$OUT/layer_traffic.json" split16
 echo done
