@@ -93,6 +93,10 @@ PWG_API long long pwg_cnet_plan_workspace_bytes(const PwgCnetPlan* p);
  * mean/scale: device or NULL (ops with normalize=1 need them). */
 PWG_API int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const float* mean,
                  const float* scale, float* out, void* workspace, void* stream);
+/* Options. PWG_CNET_OPT_SPLIT_F16 (default 1): fp32 operands as fp16 hi+lo pairs on the f16
+ * MFMA (three products, fp32 accumulate; error class of fp32); 0: fp32 MFMA. */
+enum { PWG_CNET_OPT_SPLIT_F16 = 0 };
+PWG_API int pwg_cnet_set_option(PwgCnet* n, int option, long long value);
 PWG_API int pwg_cnet_set_timing(PwgCnet* n, int enable);
 /* Adds per-op milliseconds and launch counts (arrays of n_ops) and clears the records. */
 PWG_API int pwg_cnet_timing_collect(PwgCnet* n, double* ms, long long* launches);

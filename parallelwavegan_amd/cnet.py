@@ -84,6 +84,7 @@ def lib():
         L.pwg_cnet_plan_workspace_bytes.restype = ll
         L.pwg_cnet_run.argtypes = [vp] * 8
         L.pwg_cnet_set_timing.argtypes = [vp, ctypes.c_int]
+        L.pwg_cnet_set_option.argtypes = [vp, ctypes.c_int, ctypes.c_longlong]
         L.pwg_cnet_timing_collect.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ll)]
         if L.pwg_cnet_abi_version() != 1:
             raise RuntimeError("libpwg_hip cnet ABI version mismatch")
@@ -325,6 +326,11 @@ class CnetEngine:
 
     def set_timing(self, enable):
         _lib.check(self._lib.pwg_cnet_set_timing(self._h, int(enable)))
+
+    def set_split_f16(self, enable):
+        """pwg_cnet_set_option(PWG_CNET_OPT_SPLIT_F16): fp16-pair operands on the f16 MFMA
+        (default) or exact fp32 MFMA."""
+        _lib.check(self._lib.pwg_cnet_set_option(self._h, 0, int(bool(enable))))
 
     def collect_timing(self):
         n = len(self.program.ops)

@@ -13,9 +13,16 @@
 //     workgroup, double-buffered, one barrier per chunk;
 //   * epilogue: + bias (+ second bias) + residual (+ old value) then / out_div then post
 //     activation, 16-byte stores of 4 consecutive channels of one time row.
+// Split-f16 mode (pwg_cnet_set_option PWG_CNET_OPT_SPLIT_F16, default on): the same kernel with
+// every operand an fp16 pair v = hi + lo and ONE v_mfma_f32_32x32x16_f16 k-step per chunk run
+// three times (hi*hi, hi*lo, lo*hi), fp32 accumulate, as the PWG layer: a lane's
+// 8 channels of a chunk are exactly its 32x32x16 B fragment (k = 8*hh + j), and the A fragments
+// ([chunk][m][hi/lo][lane][8 halves]) take the fp32 fragments' bytes.
 // ConvTranspose1d(kernel 2s, stride s) runs as s phase launches: outputs t = q*s + r are a 2-tap
 // conv of input rows q + floor((r+p)/s) - {0, 1} with taps k_a = (r+p) mod s and k_a + s.
 #include <hip/hip_runtime.h>
+
+#include <stdint.h>
 
 #include <algorithm>
 #include <cmath>
@@ -92,7 +99,21 @@ __device__ __forceinline__ int reflect_row(int p, int T) {
   return p < 0 ? 0 : (p >= T ? T - 1 : p);  // masked columns / tiny T: stay in bounds
 }
 
-template <int MT, int NT, int G>
+typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8v __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
+
+// 8 fp32 -> fp16 pairs: hi = rne16(v), lo = rne16(v - hi)
+__device__ __forceinline__ void cn_split8(const f32x8v& v, u32x4v& hi, u32x4v& lo) {
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const _Float16 h0 = (_Float16)v[2 * d], h1 = (_Float16)v[2 * d + 1];
+    hi[d] = __builtin_bit_cast(unsigned, f16x2v{h0, h1});
+    lo[d] = __builtin_bit_cast(unsigned, f16x2v{(_Float16)(v[2 * d] - (float)h0), (_Float16)(v[2 * d + 1] - (float)h1)});
+  }
+}
+
+template <int MT, int NT, int G, bool SPLIT = false>
 __global__ void __launch_bounds__(256) pwg_cnet_conv_kernel(const CnConvArgs a) {
   __shared__ __attribute__((aligned(16))) float s_a[2][G * MT * 512];
   const int lane = threadIdx.x & 63;
@@ -205,19 +226,43 @@ __global__ void __launch_bounds__(256) pwg_cnet_conv_kernel(const CnConvArgs a) 
     __builtin_amdgcn_sched_barrier(0);  // keep the loads issued before the MFMAs below
 #pragma unroll
     for (int g2 = 0; g2 < G; ++g2) {
-      const f32x4v* sa = reinterpret_cast<const f32x4v*>(s_a[cg & 1] + g2 * MT * 512) + lane;
+      if constexpr (SPLIT) {
+        const u32x4v* sa = reinterpret_cast<const u32x4v*>(s_a[cg & 1] + g2 * MT * 512) + lane;
+        u32x4v bh[NT], bl[NT];
 #pragma unroll
-      for (int sub = 0; sub < 2; ++sub) {
-        f32x4v av[MT];
+        for (int n = 0; n < NT; ++n) cn_split8(bcur[g2][n], bh[n], bl[n]);
+        u32x4v ah[MT], al[MT];
 #pragma unroll
-        for (int m = 0; m < MT; ++m) av[m] = sa[(m * 2 + sub) * 64];
+        for (int m = 0; m < MT; ++m) {
+          ah[m] = sa[(m * 2) * 64];
+          al[m] = sa[(m * 2 + 1) * 64];
+        }
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
+        for (int m = 0; m < MT; ++m)
 #pragma unroll
-          for (int m = 0; m < MT; ++m)
+          for (int n = 0; n < NT; ++n) {
+            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, ah[m]),
+                                                               __builtin_bit_cast(f16x8v, bh[n]), acc[m][n], 0, 0, 0);
+            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, ah[m]),
+                                                               __builtin_bit_cast(f16x8v, bl[n]), acc[m][n], 0, 0, 0);
+            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, al[m]),
+                                                               __builtin_bit_cast(f16x8v, bh[n]), acc[m][n], 0, 0, 0);
+          }
+      } else {
+        const f32x4v* sa = reinterpret_cast<const f32x4v*>(s_a[cg & 1] + g2 * MT * 512) + lane;
 #pragma unroll
-            for (int n = 0; n < NT; ++n)
-              acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m][e], bcur[g2][n][4 * sub + e], acc[m][n], 0, 0, 0);
+        for (int sub = 0; sub < 2; ++sub) {
+          f32x4v av[MT];
+#pragma unroll
+          for (int m = 0; m < MT; ++m) av[m] = sa[(m * 2 + sub) * 64];
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int m = 0; m < MT; ++m)
+#pragma unroll
+              for (int n = 0; n < NT; ++n)
+                acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m][e], bcur[g2][n][4 * sub + e], acc[m][n], 0, 0, 0);
+        }
       }
     }
     __builtin_amdgcn_sched_barrier(0);  // ... and their consumers after them
@@ -434,6 +479,7 @@ struct OpPhase {          // one launch
   int phase;              // CONVT phase r, else 0
   int MT, mt_total;
   long long frag_off;     // floats into the packed image
+  long long frag16_off = -1;  // split-f16 A fragments (same size), MFMA phases only
   long long bias_off;
   std::vector<ChunkDesc> chunks;
   ChunkDesc* d_chunks = nullptr;
@@ -453,6 +499,7 @@ using namespace pwg;
 
 struct PwgCnet {
   int device = 0;
+  int split_f16 = 1;  // PWG_CNET_OPT_SPLIT_F16
   std::vector<PwgCnetOp> ops;
   std::vector<int> channels, rate, ld;
   long long ref_count = 0;
@@ -496,6 +543,32 @@ struct Guard {
     if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
   }
 };
+
+// host fp16 round-to-nearest-even and its exact inverse (split-f16 packing)
+uint16_t cn_f2h(float f) {
+  uint32_t x;
+  std::memcpy(&x, &f, 4);
+  const uint32_t sign = (x >> 16) & 0x8000u, ax = x & 0x7fffffffu;
+  if (ax >= 0x7f800000u) return (uint16_t)(sign | (ax > 0x7f800000u ? 0x7e00u : 0x7c00u));
+  if (ax >= 0x477ff000u) return (uint16_t)(sign | 0x7c00u);
+  if (ax < 0x38800000u) {
+    float v;
+    std::memcpy(&v, &ax, 4);
+    return (uint16_t)(sign | (uint32_t)std::nearbyint(v * 16777216.0f));
+  }
+  uint32_t h = (((ax >> 23) - 112u) << 10) | ((ax & 0x7fffffu) >> 13);
+  const uint32_t rem = ax & 0x1fffu;
+  if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) ++h;
+  return (uint16_t)(sign | h);
+}
+float cn_h2f(uint16_t h) {
+  const uint32_t e = (h >> 10) & 0x1fu, m = h & 0x3ffu;
+  float v;
+  if (e == 0) v = std::ldexp((float)m, -24);
+  else if (e == 31) v = m ? NAN : INFINITY;
+  else v = std::ldexp((float)(m | 0x400u), (int)e - 25);
+  return (h & 0x8000u) ? -v : v;
+}
 
 int pick_mt(int mt_total) {
   if (mt_total <= 4) return mt_total;
@@ -659,6 +732,8 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
         }
       ph.frag_off = off;
       off += (long long)ph.chunks.size() * mt_total * 512;
+      ph.frag16_off = off;
+      off += (long long)ph.chunks.size() * mt_total * 512;
       ph.bias_off = off;
       off += (long long)mt_total * 32;
       n->phases.push_back(ph);
@@ -706,6 +781,26 @@ int pwg_cnet_pack_weights(const PwgCnet* n, const float* ref, float* packed) {
               packed[ph.frag_off + (((size_t)c * ph.mt_total + m) * 2 + sub) * 256 + l * 4 + e] =
                   ref_weight(op, ph, ref, cd.src, o, ch, tap);
             }
+      // split-f16 fragments: [chunk][m][hi/lo][lane][4 dwords], lane (cl, hh) dword d = halves of
+      // channels c0 + 8hh + 2d, +1 of output row 32m + cl
+      uint32_t* p16 = reinterpret_cast<uint32_t*>(packed + ph.frag16_off);
+      for (int m = 0; m < ph.mt_total; ++m)
+        for (int l = 0; l < 64; ++l)
+          for (int d = 0; d < 4; ++d) {
+            uint32_t hv = 0, lv = 0;
+            for (int e2 = 0; e2 < 2; ++e2) {
+              const int o = 32 * m + (l & 31);
+              const int ch = cd.c0 + 8 * (l >> 5) + 2 * d + e2;
+              const float w = ref_weight(op, ph, ref, cd.src, o, ch, tap);
+              const uint16_t h = cn_f2h(w);
+              const uint16_t lo = cn_f2h(w - cn_h2f(h));
+              hv |= (uint32_t)h << (16 * e2);
+              lv |= (uint32_t)lo << (16 * e2);
+            }
+            const size_t base = (((size_t)c * ph.mt_total + m) * 2) * 256 + (size_t)l * 4 + d;
+            p16[base] = hv;
+            p16[base + 256] = lv;
+          }
     }
     for (int o = 0; o < op.out_channels; ++o) {
       float b = op.b_off >= 0 ? ref[op.b_off + o] : 0.f;
@@ -904,7 +999,8 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         }
       }
       a.chunks = ph.d_chunks; a.n_chunks = (int)ph.chunks.size();
-      a.wfrag = packed + ph.frag_off; a.mt_total = ph.mt_total; a.bias = packed + ph.bias_off;
+      const bool split = n->split_f16 && !ph.thin;
+      a.wfrag = packed + (split ? ph.frag16_off : ph.frag_off); a.mt_total = ph.mt_total; a.bias = packed + ph.bias_off;
       a.res = op.res >= 0 ? bufs[op.res] : nullptr; a.seg_res = op.res >= 0 ? seg_of(op.res) : nullptr;
       a.ld_res = op.res >= 0 ? n->ld[op.res] : 0;
       a.y = bufs[op.dst]; a.seg_dst = seg_of(op.dst); a.ld_dst = n->ld[op.dst]; a.M = op.out_channels;
@@ -918,11 +1014,20 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         else if (op.out_channels <= 4) hipLaunchKernelGGL(pwg_cnet_thin_kernel<4>, tgrid, tblock, 0, s, a, nsrc);
         else hipLaunchKernelGGL(pwg_cnet_thin_kernel<8>, tgrid, tblock, 0, s, a, nsrc);
       } else
-      switch (ph.MT) {
-        case 1: hipLaunchKernelGGL((pwg_cnet_conv_kernel<1, 1, CN_G>), grid, block, 0, s, a); break;
-        case 2: hipLaunchKernelGGL((pwg_cnet_conv_kernel<2, 1, CN_G>), grid, block, 0, s, a); break;
-        case 3: hipLaunchKernelGGL((pwg_cnet_conv_kernel<3, 1, CN_G>), grid, block, 0, s, a); break;
-        default: hipLaunchKernelGGL((pwg_cnet_conv_kernel<4, 1, CN_G>), grid, block, 0, s, a); break;
+      if (split) {
+        switch (ph.MT) {
+          case 1: hipLaunchKernelGGL((pwg_cnet_conv_kernel<1, 1, CN_G, true>), grid, block, 0, s, a); break;
+          case 2: hipLaunchKernelGGL((pwg_cnet_conv_kernel<2, 1, CN_G, true>), grid, block, 0, s, a); break;
+          case 3: hipLaunchKernelGGL((pwg_cnet_conv_kernel<3, 1, CN_G, true>), grid, block, 0, s, a); break;
+          default: hipLaunchKernelGGL((pwg_cnet_conv_kernel<4, 1, CN_G, true>), grid, block, 0, s, a); break;
+        }
+      } else {
+        switch (ph.MT) {
+          case 1: hipLaunchKernelGGL((pwg_cnet_conv_kernel<1, 1, CN_G>), grid, block, 0, s, a); break;
+          case 2: hipLaunchKernelGGL((pwg_cnet_conv_kernel<2, 1, CN_G>), grid, block, 0, s, a); break;
+          case 3: hipLaunchKernelGGL((pwg_cnet_conv_kernel<3, 1, CN_G>), grid, block, 0, s, a); break;
+          default: hipLaunchKernelGGL((pwg_cnet_conv_kernel<4, 1, CN_G>), grid, block, 0, s, a); break;
+        }
       }
     }
     hipError_t e = hipGetLastError();
@@ -932,6 +1037,14 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
       n->records.push_back({ph.op, ea, eb});
     }
   }
+  return PWG_OK;
+}
+
+int pwg_cnet_set_option(PwgCnet* n, int option, long long value) {
+  if (!n) return fail(PWG_ERR_INVALID, "null handle");
+  if (option != PWG_CNET_OPT_SPLIT_F16) return fail(PWG_ERR_INVALID, "unknown option");
+  if (value != 0 && value != 1) return fail(PWG_ERR_INVALID, "split_f16 must be 0 or 1");
+  n->split_f16 = (int)value;
   return PWG_OK;
 }
 

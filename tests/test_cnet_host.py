@@ -56,7 +56,8 @@ def test_convt_fragment_layout(built_lib):
     b = rs.standard_normal(32).astype(np.float32)
     eng = cnet.CnetEngine(P, None, host_only=True)
     packed = eng.pack({"w": w, "b": b})
-    per_phase = 2 * 1 * 512 + 32  # 2 chunks (taps) x 1 m-tile x 512 floats + bias
+    # 2 chunks (taps) x 1 m-tile x 512 floats, fp32 fragments then split-f16 fragments, + bias
+    per_phase = 2 * 2 * 1 * 512 + 32
     assert eng.packed_weight_count == 4 * per_phase
     for r in range(4):
         base = r * per_phase
@@ -69,7 +70,16 @@ def test_convt_fragment_layout(built_lib):
                     o = lane & 31
                     ch = i + 8 * (lane >> 5)
                     assert frag[sub, lane, e] == w[ch, o, ka + tap * 4]
-        np.testing.assert_array_equal(packed[base + 1024: base + 1056], b)
+            # split-f16 fragment of the same chunk: [hi/lo][lane][8 halves], channel 8*(lane>>5) + j
+            f16 = packed[base + 1024 + tap * 512: base + 1024 + (tap + 1) * 512].view(np.float16).reshape(2, 64, 8)
+            for lane in (0, 5, 33, 63):
+                for j in range(8):
+                    want = w[8 * (lane >> 5) + j, lane & 31, ka + tap * 4]
+                    hi, lo = f16[0, lane, j], f16[1, lane, j]
+                    assert hi == np.float16(want)
+                    # ~22 significant bits; an fp16-subnormal lo still resolves 2^-25 absolute
+                    assert abs(float(hi) + float(lo) - float(want)) <= max(2.0 ** -21 * abs(float(want)), 2.0 ** -25)
+        np.testing.assert_array_equal(packed[base + 2048: base + 2080], b)
 
 
 @pytest.mark.parametrize("bad", ["rate", "channels", "dst", "convt_pad"])

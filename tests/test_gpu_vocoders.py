@@ -15,12 +15,14 @@ pytestmark = pytest.mark.gpu
 ATOL = 1e-4
 
 
+@pytest.mark.parametrize("split", [True, False], ids=["split_f16", "fp32"])
 @pytest.mark.parametrize("name", vocoder_golden_names())
-def test_vocoder_golden_vectors(name, built_lib, cuda_device):
+def test_vocoder_golden_vectors(name, split, built_lib, cuda_device):
     g = load_golden(name)
     meta = g["meta"]
     m, params, _ = vocoder_holder(meta)
     m = m.to(cuda_device)
+    m.engine().set_split_f16(split)
     with torch.no_grad():
         if meta["options"].get("forward"):
             y = m(torch.from_numpy(g["c"]).to(cuda_device))
@@ -37,8 +39,9 @@ def test_vocoder_golden_vectors(name, built_lib, cuda_device):
     assert err < ATOL, f"{name}: max|d| = {err:.3e}"
 
 
+@pytest.mark.parametrize("split", [True, False], ids=["split_f16", "fp32"])
 @pytest.mark.parametrize("cfg, frames", [("mb_melgan_v2", 40), ("hifigan_v1", 12), ("melgan_v1", 16)])
-def test_full_size_configs_against_oracle(cfg, frames, built_lib, cuda_device):
+def test_full_size_configs_against_oracle(cfg, frames, split, built_lib, cuda_device):
     from oracle import melgan_numpy
     from parallelwavegan_amd import configs, synthetic
     from parallelwavegan_amd.engine import fold_weight_norm
@@ -54,6 +57,7 @@ def test_full_size_configs_against_oracle(cfg, frames, built_lib, cuda_device):
         m.pqmf = PQMF(**configs.VOCODER_PQMF[cfg])
         syn = m.pqmf.synthesis_taps()
     m = m.to(cuda_device)
+    m.engine().set_split_f16(split)
     mel = synthetic.make_mel(frames, 80, seed=9)
     with torch.no_grad():
         y = m.inference(mel).cpu().numpy()
