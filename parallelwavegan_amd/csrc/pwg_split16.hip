@@ -20,6 +20,30 @@
 // Reference: layers/residual_block.py:102-140, models/parallel_wavegan.py:131-138,160-171.
 #include "pwg_internal.h"
 
+#ifndef PWG_SPLIT16_EARLY_SKIP
+#define PWG_SPLIT16_EARLY_SKIP 0
+#endif
+// streams touched once per layer: non-temporal (PWG_SPLIT16_NT bit 0: stores, bit 1: skip loads)
+#ifndef PWG_SPLIT16_NT
+#define PWG_SPLIT16_NT 3
+#endif
+#if PWG_SPLIT16_NT & 1
+#define PWG16_ST(p, v) __builtin_nontemporal_store((v), (p))
+#else
+#define PWG16_ST(p, v) (*(p) = (v))
+#endif
+#if PWG_SPLIT16_NT & 2
+#define PWG16_LD_SKIP(p) __builtin_nontemporal_load(p)
+#else
+#define PWG16_LD_SKIP(p) (*(p))
+#endif
+#ifndef PWG_SPLIT16_DIAG_NOTAP
+#define PWG_SPLIT16_DIAG_NOTAP 0
+#endif
+#ifndef PWG_SPLIT16_MG
+#define PWG_SPLIT16_MG 4  // GEMM-1 m-tiles whose A fragments are read per group
+#endif
+
 namespace pwg {
 
 namespace {
@@ -129,6 +153,7 @@ static_assert(Split16Smem::WG + Split16Smem::W2 + Split16Smem::BG + Split16Smem:
 
 template <bool LAST, int TC>
 __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitArgs a) {
+  constexpr int MG = PWG_SPLIT16_MG;
   extern __shared__ __attribute__((aligned(16))) unsigned smem16[];
   unsigned* s_wg = smem16;
   unsigned* s_w2 = s_wg + Split16Smem::WG;
@@ -183,7 +208,7 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
 
   // a lane's tap row pieces for both n-tiles: b[nt*4 + ks*2 + hl]
   auto bload = [&](int col, int tap, u32x4 (&b)[8]) {
-    const int cc = col + (tap - TC) * a.dil;
+    const int cc = col + (PWG_SPLIT16_DIAG_NOTAP ? 0 : (tap - TC) * a.dil);  // NOTAP: diagnostic only
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {
       const u32x4* p = reinterpret_cast<const u32x4*>(a.x_in + row16(cc + 16 * nt + c, g));
@@ -196,19 +221,19 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
 #pragma unroll
-      for (int mh = 0; mh < 2; ++mh) {  // 4 m-tiles per group: fragments of 4 read ahead
-        u32x4 ah[4], al[4];
+      for (int mh = 0; mh < 8 / MG; ++mh) {  // MG m-tiles per group: their fragments read ahead
+        u32x4 ah[MG], al[MG];
 #pragma unroll
-        for (int mm = 0; mm < 4; ++mm) {
-          const int m = 4 * mh + mm;
+        for (int mm = 0; mm < MG; ++mm) {
+          const int m = MG * mh + mm;
           ah[mm] = wgl[(((tap * 2 + ks) * 8 + m) * 2) * 64];
           al[mm] = wgl[(((tap * 2 + ks) * 8 + m) * 2 + 1) * 64];
         }
 #pragma unroll
-        for (int mm = 0; mm < 4; ++mm)
+        for (int mm = 0; mm < MG; ++mm)
 #pragma unroll
           for (int nt = 0; nt < 2; ++nt) {
-            f32x4& ac = acc[4 * mh + mm][nt];
+            f32x4& ac = acc[MG * mh + mm][nt];
             ac = mma16(ah[mm], b[nt * 4 + ks * 2], ac);
             ac = mma16(ah[mm], b[nt * 4 + ks * 2 + 1], ac);
             ac = mma16(al[mm], b[nt * 4 + ks * 2], ac);
@@ -257,7 +282,11 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
         const int fc = f < 0 ? 0 : (f >= bd.frames ? bd.frames - 1 : f);  // weight 0 there
         const unsigned* drow = a.d + (size_t)(bd.frame_base + fc) * 128 + c;
 #pragma unroll
+#if PWG_SPLIT16_DIAG_NOD  // diagnostic: no D loads (wrong results)
+        for (int m = 0; m < 8; ++m) dv[j][m] = (unsigned)(fc + m);
+#else
         for (int m = 0; m < 8; ++m) dv[j][m] = drow[16 * m];
+#endif
       }
     };
     float bw[2][2];  // [nt][frame]
@@ -288,6 +317,21 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) acc[m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
     f32x4 acc2[8][2];
+#if PWG_SPLIT16_EARLY_SKIP
+    // skip seeds first: the old skip sum streams from HBM, its latency hides behind GEMM 1
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int ms = 0; ms < 4; ++ms) {
+        if (a.first) {
+          acc2[ms][nt] = reinterpret_cast<const f32x4*>(a.skip0 + 16 * g)[ms];
+        } else {
+          const f32x4* sp = reinterpret_cast<const f32x4*>(a.skip + row16(bd.col + 16 * nt + c, g));
+          acc2[ms][nt] = PWG16_LD_SKIP(sp + ms * 64);
+        }
+      }
+
+#endif
     constexpr int T1 = TC == 1 ? 2 : 1;
     bload(bd.col, T1, b1);
     mma_tap(acc, b0, 0);
@@ -300,6 +344,7 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
 
     int ticket = 0;
     if (nblk >= 0) ticket = ticket_issue();
+#if !PWG_SPLIT16_EARLY_SKIP
     // skip seeds: old skip sum (layer 0: the sum of all layers' skip biases, [g][16] layout)
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
@@ -309,10 +354,11 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
           acc2[ms][nt] = reinterpret_cast<const f32x4*>(a.skip0 + 16 * g)[ms];
         } else {
           const f32x4* sp = reinterpret_cast<const f32x4*>(a.skip + row16(bd.col + 16 * nt + c, g));
-          acc2[ms][nt] = __builtin_nontemporal_load(sp + ms * 64);
+          acc2[ms][nt] = PWG16_LD_SKIP(sp + ms * 64);
         }
       }
 
+#endif
     // ---- aux term + gate bias: one MFMA per (m, nt)
     {
       const Pair16 bias_one = split_pair16(g == 0 ? 1.f : 0.f, g == 0 ? 1.f : 0.f);
@@ -383,7 +429,7 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
         const bool live = bd.t0 + 16 * nt + c < bd.T;
         f32x4* sp = reinterpret_cast<f32x4*>(a.skip + row16(col, g));
 #pragma unroll
-        for (int ms = 0; ms < 4; ++ms) __builtin_nontemporal_store(acc2[ms][nt], sp + ms * 64);
+        for (int ms = 0; ms < 4; ++ms) PWG16_ST(sp + ms * 64, acc2[ms][nt]);
         u32x4* xp = reinterpret_cast<u32x4*>(a.x_out + row16(col, g));
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
@@ -399,8 +445,8 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
               vl[k] = live ? vl[k] : 0u;
             }
           }
-          __builtin_nontemporal_store(vh, xp + (ks * 2) * 64);
-          __builtin_nontemporal_store(vl, xp + (ks * 2 + 1) * 64);
+          PWG16_ST(xp + (ks * 2) * 64, vh);
+          PWG16_ST(xp + (ks * 2 + 1) * 64, vl);
         }
       }
     } else {
