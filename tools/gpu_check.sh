@@ -17,6 +17,7 @@ cd "$GRAFT_REPO_ROOT"
 # PMC passes (separate rocprofv3 runs) -> HBM traffic per split-layer launch
 bash tools/profile_pmc.sh "$OUT/pmc" && python tools/pmc_summary.py "$OUT/pmc" "$OUT/pmc_summary.json" > /dev/null && python tools/make_traffic_json.py "$OUT/pmc_summary.json" "$OUT/layer_traffic.json" split16
 echo done
+timeout -k 10 300 python bench.py --config ljspeech_v1 --cpu-seconds 8 > "$OUT/ljspeech_v1.json" 2> "$OUT/ljspeech_v1.err"
 # vocoder configs (BASELINE configs 3-4 and MelGAN v1) and the HiFiGAN per-op profile
 for c in mb_melgan_v2 hifigan_v1 melgan_v1; do
   timeout -k 10 300 python bench.py --config $c --cpu-seconds 8 > "$OUT/$c.json" 2> "$OUT/$c.err"
