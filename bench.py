@@ -190,6 +190,9 @@ def bench_vocoder(args, rank, world, dev):
     m = m.to(dev)
     eng = m.engine()
     eng.set_split_f16(not args.cnet_fp32)
+    eng.set_fuse_pairs(not args.cnet_nofuse)
+    if args.pair_steps:
+        eng.set_pair_steps(args.pair_steps)
     if world > 1:
         broadcast_packed_weights(eng.packed, src=0)
     P = eng.program
@@ -265,7 +268,8 @@ def bench_vocoder(args, rank, world, dev):
         "config": {"workload": f"{args.config} generator inference, {args.utts} ragged utterances per GPU per step",
                    "model": cls_name, "sampling_rate": fs, "hop": hop, "global_batch": args.utts * world,
                    "frames_per_gpu": frames, "samples_per_step_per_gpu": samples,
-                   "parallelism": f"utterance-sharded x{world}"},
+                   "parallelism": f"utterance-sharded x{world}",
+                   "fused_conv_pairs": sum(1 for _, _, n in timing if n == 0)},
         "x_realtime_per_gpu": round(value / world / fs, 1),
         "kernel_ms_per_step": round(kern_ms, 3),
         "top_ops_ms_per_step": {n: round(ms / args.steps, 3) for n, ms, _ in top},
@@ -304,6 +308,8 @@ def main():
     ap.add_argument("--waves-per-wg", type=int, default=None)
     ap.add_argument("--wg-per-cu", type=int, default=None)
     ap.add_argument("--cnet-fp32", action="store_true", help="vocoder configs: exact fp32 MFMA instead of split-f16")
+    ap.add_argument("--cnet-nofuse", action="store_true", help="vocoder configs: run fusable conv pairs unfused")
+    ap.add_argument("--pair-steps", type=int, default=None, help="vocoder configs: 128-column tiles per fused-pair strip")
     args = ap.parse_args()
 
     rank, world, dev = dist_setup(args.gpus)

@@ -94,8 +94,14 @@ PWG_API long long pwg_cnet_plan_workspace_bytes(const PwgCnetPlan* p);
 PWG_API int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const float* mean,
                  const float* scale, float* out, void* workspace, void* stream);
 /* Options. PWG_CNET_OPT_SPLIT_F16 (default 1): fp32 operands as fp16 hi+lo pairs on the f16
- * MFMA (three products, fp32 accumulate; error class of fp32); 0: fp32 MFMA. */
-enum { PWG_CNET_OPT_SPLIT_F16 = 0 };
+ * MFMA (three products, fp32 accumulate; error class of fp32); 0: fp32 MFMA.
+ * PWG_CNET_OPT_FUSE_PAIRS (default 1, split-f16 mode): run "conv A -> t -> conv B" pairs whose
+ * intermediate t has no other reader (HiFiGAN ResBlock steps, layers/residual_block.py:231-237)
+ * as one kernel with t kept in LDS; bit-identical to the unfused ops. Applies to 32-channel
+ * zero-padded pairs whose weights fit in LDS (HiFiGAN v1's last stage).
+ * PWG_CNET_OPT_PAIR_STEPS (default 16): 128-column tiles per fused-pair workgroup, for plans
+ * created afterwards. */
+enum { PWG_CNET_OPT_SPLIT_F16 = 0, PWG_CNET_OPT_FUSE_PAIRS = 1, PWG_CNET_OPT_PAIR_STEPS = 2 };
 PWG_API int pwg_cnet_set_option(PwgCnet* n, int option, long long value);
 PWG_API int pwg_cnet_set_timing(PwgCnet* n, int enable);
 /* Adds per-op milliseconds and launch counts (arrays of n_ops) and clears the records. */

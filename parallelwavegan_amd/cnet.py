@@ -332,6 +332,18 @@ class CnetEngine:
         (default) or exact fp32 MFMA."""
         _lib.check(self._lib.pwg_cnet_set_option(self._h, 0, int(bool(enable))))
 
+    def set_fuse_pairs(self, enable):
+        """pwg_cnet_set_option(PWG_CNET_OPT_FUSE_PAIRS): run conv pairs whose intermediate has no
+        other reader (HiFiGAN ResBlock steps) as one kernel, intermediate in LDS (default on,
+        split-f16 mode only; bit-identical to the unfused ops)."""
+        _lib.check(self._lib.pwg_cnet_set_option(self._h, 1, int(bool(enable))))
+
+    def set_pair_steps(self, steps):
+        """pwg_cnet_set_option(PWG_CNET_OPT_PAIR_STEPS): 128-column tiles per fused-pair
+        workgroup, for plans created afterwards (cached plans are dropped)."""
+        _lib.check(self._lib.pwg_cnet_set_option(self._h, 2, int(steps)))
+        self._plans.clear()
+
     def collect_timing(self):
         n = len(self.program.ops)
         ms = (ctypes.c_double * n)()

@@ -102,6 +102,7 @@ __device__ __forceinline__ int reflect_row(int p, int T) {
 typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x8v __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x4v __attribute__((ext_vector_type(4)));
 
 // 8 fp32 -> fp16 pairs: hi = rne16(v), lo = rne16(v - hi)
 __device__ __forceinline__ void cn_split8(const f32x8v& v, u32x4v& hi, u32x4v& lo) {
@@ -335,6 +336,279 @@ __global__ void __launch_bounds__(256) pwg_cnet_conv_kernel(const CnConvArgs a) 
   }
 }
 
+// Fused conv pair (split-f16 mode): y = post((conv2(pre2(conv1(pre1(x)) + b1)) + b2 + res [+ y_old]) / div)
+// with conv2's intermediate never leaving the chip. This is HiFiGAN's ResBlock step
+// (layers/residual_block.py:231-237: xt = c1(lrelu(x)); xt = c2(lrelu(xt)); x = xt + x) and any other
+// program pair "op A writes t, op B is the only reader of t" (PwgCnet::pair_of).
+//   * one workgroup = 4 waves sweeping a STRIP of `steps` 128-column tiles of one utterance;
+//   * step s: stage 1 computes the intermediate h (C channels) for columns [base + 128s - 16,
+//     base + 128s + 112) (wave w: 32 of them) into LDS slot s & 1, with conv2's pre-activation
+//     applied, zeros outside the utterance (conv2's zero padding), split into fp16 hi/lo;
+//     stage 2 computes output columns [base + 128(s-1), base + 128s), whose conv2 taps (offsets
+//     within +-16) read slots (s-1) & 1 and s & 1. Each h column is computed once per strip
+//     (plus one 128-column tile of warm-up per strip).
+//   * A fragments of both convs stream through the same double-buffered LDS staging as
+//     pwg_cnet_conv_kernel (one barrier per 16-channel chunk); stage-1 B rows come from HBM one
+//     chunk ahead, stage-2 B rows from LDS.
+// The arithmetic (chunk order, pair split, fp32 accumulate, epilogue order) is the unfused ops'
+// exactly, so the fused result is bit-identical to running op A then op B in split mode.
+constexpr int PR_HALO = 16;
+constexpr int PR_MAX_XS = 128 + 2 * 64;        // x tile columns (stage-1 tap reach +-64 - PR_HALO)
+constexpr int PR_XQ = PR_MAX_XS * 8 / 256;     // 16-byte x quads per thread
+constexpr int PR_MAX_LDS = 160 * 1024;
+struct CnPairArgs {
+  const float* x;
+  const int* seg_x;
+  int ld_x;
+  float slope1, slope2;
+  const ChunkDesc* ch1;
+  int n1;
+  const float* w1;        // split-f16 fragments [chunk][MT][hi/lo][lane][4 dwords]
+  const float* b1;
+  const ChunkDesc* ch2;
+  int n2;
+  const float* w2;
+  const float* b2;
+  const float* res;
+  const int* seg_res;
+  int ld_res;
+  float* y;
+  const int* seg_y;
+  int ld_y;
+  int accumulate;
+  float out_div;
+  int post_act;
+  float post_slope;
+  const int2* strips;     // (utt, first output column)
+  const int* ncols;       // [n_utts]
+  int steps;              // 128-column tiles per strip
+  int x_min_off, xs;      // stage-1 x tile: first column offset (vs the h tile start) and width
+  int off1, dil1, off2, dil2;  // chunk c reads row offset off + (c >> 1) * dil (2 chunks per tap)
+};
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
+// global loads/stores in flight (__syncthreads' release fence would drain those too).
+__device__ __forceinline__ void pr_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// C = 32 channels (MT = 1). Dynamic LDS: [A fragments of all n1 + n2 chunks, 2 KB each]
+// [x tile: xs columns x HROW halves] [h ring: 2 x 128 columns x HROW halves].
+__global__ void __launch_bounds__(256) pwg_cnet_pair_kernel(const CnPairArgs a) {
+  constexpr int C = 32;
+  constexpr int HROW = 2 * C + 8;  // halves per LDS column: [hi C][lo C][16 B pad]
+  extern __shared__ __attribute__((aligned(16))) unsigned char pr_smem[];
+  const int n1 = a.n1, n2 = a.n2;
+  unsigned* s_w = reinterpret_cast<unsigned*>(pr_smem);                      // [(n1+n2)][2][64][4]
+  _Float16* s_x = reinterpret_cast<_Float16*>(pr_smem + (size_t)(n1 + n2) * 2048);
+  _Float16* s_h = s_x + (size_t)a.xs * HROW;                                    // [2][128][HROW]
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int hh = lane >> 5;
+  const int cl = lane & 31;
+  const int2 st = a.strips[blockIdx.x];
+  const int u = st.x, base = st.y;
+  const int T = a.ncols[u];
+  const int nsteps = min(a.steps, (T - base + 127) / 128);
+  const int2 sx = *reinterpret_cast<const int2*>(a.seg_x + 2 * u);
+  const int sd_x = a.seg_y[2 * u];
+  const int sr_x = a.res ? a.seg_res[2 * u] : 0;
+
+  // weights of both convs, resident for the whole strip
+  {
+    const u32x4v* g1 = reinterpret_cast<const u32x4v*>(a.w1);
+    const u32x4v* g2 = reinterpret_cast<const u32x4v*>(a.w2);
+    u32x4v* d = reinterpret_cast<u32x4v*>(s_w);
+    for (int i = threadIdx.x; i < n1 * 128; i += 256) d[i] = g1[i];
+    for (int i = threadIdx.x; i < n2 * 128; i += 256) d[n1 * 128 + i] = g2[i];
+  }
+  // x tile of step s: columns x0(s) + [0, xs), x0(s) = base + 128 s - PR_HALO + x_min_off; each
+  // thread moves up to PR_XQ 16-byte quads (column = q >> 3, channels 4 (q & 7) .. +3)
+  f32x4v xq[PR_XQ];
+  auto xfetch = [&](int s) {
+    const int x0 = base + 128 * s - PR_HALO + a.x_min_off;
+#pragma unroll
+    for (int i = 0; i < PR_XQ; ++i) {
+      // unconditional (clamped) loads: a predicated load makes the compiler wait for the
+      // previous ones first
+      const int q = threadIdx.x + 256 * i;
+      int p = x0 + (q >> 3);
+      p = p < 0 ? 0 : (p >= T ? T - 1 : p);
+      xq[i] = *reinterpret_cast<const f32x4v*>(a.x + (size_t)(sx.x + p) * a.ld_x + 4 * (q & 7));
+    }
+  };
+  auto xstore = [&](int s) {  // LeakyReLU(slope1), zeros outside the utterance, fp16 pair split
+    const int x0 = base + 128 * s - PR_HALO + a.x_min_off;
+#pragma unroll
+    for (int i = 0; i < PR_XQ; ++i) {
+      const int q = threadIdx.x + 256 * i;
+      if (q >= a.xs * 8) continue;
+      const int p = x0 + (q >> 3);
+      f32x4v v = xq[i];
+      if (a.slope1 != 1.f) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * a.slope1;
+      }
+      if (p < 0 || p >= T) v = f32x4v{0.f, 0.f, 0.f, 0.f};
+      f16x4v vh, vl;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        vh[e] = (_Float16)v[e];
+        vl[e] = (_Float16)(v[e] - (float)vh[e]);
+      }
+      _Float16* r = s_x + (q >> 3) * HROW + 4 * (q & 7);
+      *reinterpret_cast<f16x4v*>(r) = vh;
+      *reinterpret_cast<f16x4v*>(r + C) = vl;
+    }
+  };
+  auto mfma3 = [&](const u32x4v& ah, const u32x4v& al, const u32x4v& bh, const u32x4v& bl, f32x16& acc) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, ah), __builtin_bit_cast(f16x8v, bh), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, ah), __builtin_bit_cast(f16x8v, bl), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, al), __builtin_bit_cast(f16x8v, bh), acc, 0, 0, 0);
+  };
+  struct Ops { u32x4v ah, al, bh, bl; };
+  // stage-1 operands of chunk c: A from s_w, B = x tile column (32 wave + cl + row_off - x_min_off)
+  auto op1 = [&](int c, Ops& o) {
+    const u32x4v* w = reinterpret_cast<const u32x4v*>(s_w) + (size_t)c * 128 + lane;
+    o.ah = w[0];
+    o.al = w[64];
+    // chunk c = (tap c >> 1, channels 16 (c & 1) ..): the op's chunk order (pwg_cnet_create)
+    const int row_off = a.off1 + (c >> 1) * a.dil1;
+    const _Float16* r = s_x + (32 * wave + cl + row_off - a.x_min_off) * HROW + 16 * (c & 1) + 8 * hh;
+    o.bh = *reinterpret_cast<const u32x4v*>(r);
+    o.bl = *reinterpret_cast<const u32x4v*>(r + C);
+  };
+  // stage-2 operands of chunk c at step s: B = h columns of tiles s-1 / s
+  auto op2 = [&](int s, int c, Ops& o) {
+    const u32x4v* w = reinterpret_cast<const u32x4v*>(s_w) + (size_t)(n1 + c) * 128 + lane;
+    o.ah = w[0];
+    o.al = w[64];
+    const int p = 32 * wave + cl + PR_HALO + a.off2 + (c >> 1) * a.dil2;  // 0 .. 159 within tiles s-1, s
+    const _Float16* r = s_h + ((p < 128 ? ((s - 1) & 1) : (s & 1)) * 128 + (p & 127)) * HROW + 16 * (c & 1) + 8 * hh;
+    o.bh = *reinterpret_cast<const u32x4v*>(r);
+    o.bl = *reinterpret_cast<const u32x4v*>(r + C);
+  };
+
+  f32x4v rb1[4], rb2[4];  // biases of this lane's rows 8 j4 + 4 hh .. +3 (read once)
+#pragma unroll
+  for (int j4 = 0; j4 < 4; ++j4) {
+    rb1[j4] = *reinterpret_cast<const f32x4v*>(a.b1 + 8 * j4 + 4 * hh);
+    rb2[j4] = *reinterpret_cast<const f32x4v*>(a.b2 + 8 * j4 + 4 * hh);
+  }
+  // Output rows are stored one step late (after the next stage 1): a store's data registers
+  // cannot be rewritten before the store completes, and the next step's first LDS reads would
+  // otherwise wait for that at once.
+  f32x4v pend[4];
+  float* pend_row = nullptr;
+  auto flush = [&]() {
+    if (pend_row) {
+#pragma unroll
+      for (int j4 = 0; j4 < 4; ++j4) *reinterpret_cast<f32x4v*>(pend_row + 8 * j4 + 4 * hh) = pend[j4];
+    }
+  };
+  xfetch(0);
+  xstore(0);
+  pr_barrier();
+  for (int s = 0; s <= nsteps; ++s) {
+    // ---------------- stage 1: h columns j of tile s
+    const int j = base + 128 * s - PR_HALO + 32 * wave + cl;
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    {
+      Ops cur, nxt;
+      op1(0, cur);
+      for (int c = 0; c < n1; ++c) {
+        if (c + 1 < n1) op1(c + 1, nxt);
+        mfma3(cur.ah, cur.al, cur.bh, cur.bl, acc);
+        cur = nxt;
+      }
+    }
+    flush();
+    pend_row = nullptr;
+    // x tile s+1: in flight during epilogue 1 and stage 2, stored to LDS after stage 2 (issued
+    // after stage 1 so that no wait of stage 1 covers it)
+    if (s < nsteps) xfetch(s + 1);
+    // epilogue 1: + b1, conv2's pre-activation, zero outside [0, T), fp16 pair split -> h slot s & 1
+    // (its previous tile was last read by stage 2 of step s-1, before the barrier ending that step)
+    {
+      _Float16* hrow = s_h + ((s & 1) * 128 + 32 * wave + cl) * HROW;
+      const bool inside = j >= 0 && j < T;
+#pragma unroll
+      for (int j4 = 0; j4 < 4; ++j4) {
+        const int row = 8 * j4 + 4 * hh;
+        const f32x4v b = rb1[j4];
+        f16x4v vh, vl;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = acc[4 * j4 + e] + b[e];
+          if (a.slope2 != 1.f) v = v > 0.f ? v : v * a.slope2;
+          v = inside ? v : 0.f;
+          vh[e] = (_Float16)v;
+          vl[e] = (_Float16)(v - (float)vh[e]);
+        }
+        *reinterpret_cast<f16x4v*>(hrow + row) = vh;
+        *reinterpret_cast<f16x4v*>(hrow + C + row) = vl;
+      }
+    }
+    pr_barrier();  // h tile s visible; every wave is done with x tile s
+    if (s >= 1) {
+      // ---------------- stage 2: output columns q of tile s-1
+      const int q = base + 128 * (s - 1) + 32 * wave + cl;
+      const bool live = q < T;
+      const int qc = live ? q : 0;
+      float* yrow = a.y + (size_t)(sd_x + qc) * a.ld_y;
+      // residual and old value, loaded unconditionally (a predicated load waits for all earlier
+      // ones) before the MFMAs; without a residual buffer the y row stands in and is not used
+      const float* rrow = a.res ? a.res + (size_t)(sr_x + qc) * a.ld_res : yrow;
+      f32x4v rv[4], ov[4];
+#pragma unroll
+      for (int j4 = 0; j4 < 4; ++j4) {
+        const int row = 8 * j4 + 4 * hh;
+        rv[j4] = *reinterpret_cast<const f32x4v*>(rrow + row);
+        ov[j4] = *reinterpret_cast<const f32x4v*>(yrow + row);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+      {
+        Ops cur, nxt;
+        op2(s, 0, cur);
+        for (int c = 0; c < n2; ++c) {
+          if (c + 1 < n2) op2(s, c + 1, nxt);
+          mfma3(cur.ah, cur.al, cur.bh, cur.bl, acc);
+          cur = nxt;
+        }
+      }
+      if (live) {
+#pragma unroll
+        for (int j4 = 0; j4 < 4; ++j4) {
+          const int row = 8 * j4 + 4 * hh;
+          const f32x4v b = rb2[j4];
+          f32x4v v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = acc[4 * j4 + e] + b[e];
+          if (a.res) v += rv[j4];
+          if (a.accumulate) v = ov[j4] + v;
+          if (a.out_div != 1.f) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = v[e] / a.out_div;
+          }
+          if (a.post_act == PWG_ACT_LRELU) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * a.post_slope;
+          } else if (a.post_act == PWG_ACT_TANH) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = tanhf(v[e]);
+          }
+          pend[j4] = v;
+        }
+        pend_row = yrow;
+      }
+    }
+    if (s < nsteps) xstore(s + 1);
+    pr_barrier();  // x tile s+1 visible; h slot (s+1) & 1 free
+  }
+  flush();
+}
+
 // Thin outputs (M <= 8: the last conv of a generator, 1 or 4 channels). A 32-row MFMA tile would
 // be >= 75 % zero rows, so one THREAD computes all M outputs of one column on the VALU: per K
 // chunk it loads its 16 input channels (pre-activation and edge mode as in the MFMA kernel) and
@@ -490,6 +764,8 @@ struct OpPhase {          // one launch
   bool thin = false;      // M <= 8: VALU kernel with an LDS-staged input tile
   int thin_taps[2] = {0, 0}, thin_nc[2] = {0, 0}, thin_base[2] = {0, 0}, thin_off_min[2] = {0, 0},
       thin_span[2] = {0, 0};
+  int pair_b = -1;        // phase index of the op this one fuses with (pwg_cnet_pair_kernel), -1 = none
+  int pair_xmin = 0, pair_xs = 0, pair_lds = 0;  // its x tile offset / width and dynamic LDS bytes
 };
 
 }  // namespace
@@ -500,6 +776,9 @@ using namespace pwg;
 struct PwgCnet {
   int device = 0;
   int split_f16 = 1;  // PWG_CNET_OPT_SPLIT_F16
+  int fuse_pairs = 1; // PWG_CNET_OPT_FUSE_PAIRS (split-f16 mode only)
+  int pair_steps = 16; // PWG_CNET_OPT_PAIR_STEPS: 128-column tiles per fused-pair strip (plan time)
+  bool pair_attr_set = false;
   std::vector<PwgCnetOp> ops;
   std::vector<int> channels, rate, ld;
   long long ref_count = 0;
@@ -522,6 +801,9 @@ struct PwgCnetPlan {
   std::vector<int2*> d_blocks;               // per phase
   std::vector<int> n_blocks;
   std::vector<int*> d_ncols;                 // per phase
+  std::vector<int2*> d_strips;               // per phase: fused-pair strips (utt, q0), or null
+  std::vector<int> n_strips;
+  int pair_steps = 16;
 };
 
 namespace {
@@ -740,6 +1022,49 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
     }
   }
   n->packed_count = off;
+  // Fusable pairs (pwg_cnet_pair_kernel): op A = single-source zero-padded conv C_in -> C writing t
+  // with no residual / accumulate / division / post activation; the next op B = single-source
+  // zero-padded conv C -> C reading t, taps within +-PR_HALO; nobody else reads t.
+  for (size_t i = 0; i + 1 < n->phases.size(); ++i) {
+    const OpPhase& pa = n->phases[i];
+    const OpPhase& pb = n->phases[i + 1];
+    if (pb.op != pa.op + 1) continue;
+    const PwgCnetOp& A = n->ops[pa.op];
+    const PwgCnetOp& B = n->ops[pb.op];
+    const int C = A.out_channels;
+    if (A.kind != PWG_CNET_CONV || B.kind != PWG_CNET_CONV || pa.thin || pb.thin) continue;
+    if (A.src[1].buf >= 0 || B.src[1].buf >= 0 || B.src[0].buf != A.dst) continue;
+    if (A.res >= 0 || A.accumulate || A.out_div != 1.f || A.post_act != PWG_ACT_NONE) continue;
+    if (A.src[0].pad_mode != PWG_PAD_ZERO || A.src[0].normalize || B.src[0].pad_mode != PWG_PAD_ZERO) continue;
+    if (C != 32 || A.src[0].channels != C || n->ld[A.src[0].buf] != C || B.out_channels != C ||
+        B.src[0].channels != C || n->ld[A.dst] != C)
+      continue;
+    if (pa.mt_total != 1 || pb.mt_total != 1 || pa.MT != 1 || pb.MT != 1) continue;
+    bool ok = true;
+    int mn = 1 << 30, mx = -(1 << 30);
+    for (const ChunkDesc& cd : pa.chunks) { mn = std::min(mn, cd.row_off); mx = std::max(mx, cd.row_off); }
+    for (size_t c = 0; c < pa.chunks.size(); ++c)
+      ok = ok && pa.chunks[c].row_off == -A.src[0].pad + (int)(c >> 1) * A.src[0].dilation && pa.chunks[c].c0 == 16 * (int)(c & 1);
+    for (size_t c = 0; c < pb.chunks.size(); ++c)
+      ok = ok && pb.chunks[c].row_off == -B.src[0].pad + (int)(c >> 1) * B.src[0].dilation && pb.chunks[c].c0 == 16 * (int)(c & 1);
+    const int xs = 128 + mx - mn;
+    const long long lds = (long long)(pa.chunks.size() + pb.chunks.size()) * 2048 + (long long)(xs + 256) * (2 * C + 8) * 2;
+    if (xs > PR_MAX_XS || lds > PR_MAX_LDS) continue;
+    if (B.dst != n_bufs - 1 && n->ld[B.dst] != C) continue;
+    ok = ok && n->ld[B.dst] % 4 == 0 && (B.res < 0 || n->ld[B.res] % 4 == 0);
+    for (const ChunkDesc& cd : pb.chunks) ok = ok && cd.row_off >= -PR_HALO && cd.row_off <= PR_HALO;
+    for (int k = 0; k < n_ops && ok; ++k) {
+      if (k == pb.op) continue;
+      const PwgCnetOp& o2 = n->ops[k];
+      ok = o2.src[0].buf != A.dst && o2.src[1].buf != A.dst && o2.res != A.dst && (k == pa.op || o2.dst != A.dst);
+    }
+    if (ok) {
+      n->phases[i].pair_b = (int)i + 1;
+      n->phases[i].pair_xmin = mn;
+      n->phases[i].pair_xs = xs;
+      n->phases[i].pair_lds = (int)lds;
+    }
+  }
   *out = n;  // device tables are uploaded by the first plan: packing needs no GPU
   return PWG_OK;
 }
@@ -818,6 +1143,7 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
   PwgCnetPlan* p = new PwgCnetPlan();
   p->n = n;
   p->n_utts = n_utts;
+  p->pair_steps = n->pair_steps;
   p->frames.assign(frames, frames + n_utts);
   std::vector<int> seg((size_t)nb * n_utts * 2);
   p->rows.assign(nb, 0);
@@ -925,6 +1251,17 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
     p->d_blocks.push_back(db);
     p->n_blocks.push_back((int)blocks.size());
     p->d_ncols.push_back(dn);
+    std::vector<int2> strips;
+    if (ph.pair_b >= 0)
+      for (int u = 0; u < n_utts; ++u)
+        for (int q0 = 0; q0 < ncols[u]; q0 += 128 * p->pair_steps) strips.push_back(make_int2(u, q0));
+    int2* dstr = nullptr;
+    if (e == hipSuccess && !strips.empty()) {
+      e = hipMalloc(&dstr, sizeof(int2) * strips.size());
+      if (e == hipSuccess) e = hipMemcpy(dstr, strips.data(), sizeof(int2) * strips.size(), hipMemcpyHostToDevice);
+    }
+    p->d_strips.push_back(dstr);
+    p->n_strips.push_back((int)strips.size());
   }
   if (e != hipSuccess) {
     const int rc = hipf(e, "cnet plan upload");
@@ -941,6 +1278,7 @@ void pwg_cnet_plan_destroy(PwgCnetPlan* p) {
   if (p->d_seg) (void)hipFree(p->d_seg);
   for (auto* x : p->d_blocks) if (x) (void)hipFree(x);
   for (auto* x : p->d_ncols) if (x) (void)hipFree(x);
+  for (auto* x : p->d_strips) if (x) (void)hipFree(x);
   delete p;
 }
 
@@ -964,9 +1302,11 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
   bufs[nb - 1] = out;
   for (int b = 1; b < nb - 1; ++b) bufs[b] = (float*)((char*)workspace + p->buf_off[b]);
   auto seg_of = [&](int b) -> const int* { return p->d_seg + (size_t)b * p->n_utts * 2; };
+  const bool fuse = n->fuse_pairs && n->split_f16;
   for (size_t pi = 0; pi < n->phases.size(); ++pi) {
     const OpPhase& ph = n->phases[pi];
     const PwgCnetOp& op = n->ops[ph.op];
+    if (fuse && pi > 0 && n->phases[pi - 1].pair_b == (int)pi) continue;  // ran inside the pair
     hipEvent_t ea = nullptr, eb = nullptr;
     if (n->timing) {
       for (hipEvent_t* ev : {&ea, &eb}) {
@@ -975,7 +1315,31 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
       }
       (void)hipEventRecord(ea, s);
     }
-    if (op.kind == PWG_CNET_PQMF) {
+    if (fuse && ph.pair_b >= 0) {
+      if (p->n_strips[pi] > 0) {
+        const OpPhase& pb = n->phases[ph.pair_b];
+        const PwgCnetOp& opb = n->ops[pb.op];
+        CnPairArgs a;
+        a.x = bufs[op.src[0].buf]; a.seg_x = seg_of(op.src[0].buf); a.ld_x = n->ld[op.src[0].buf];
+        a.slope1 = op.src[0].pre_slope; a.slope2 = opb.src[0].pre_slope;
+        a.ch1 = ph.d_chunks; a.n1 = (int)ph.chunks.size(); a.w1 = packed + ph.frag16_off; a.b1 = packed + ph.bias_off;
+        a.ch2 = pb.d_chunks; a.n2 = (int)pb.chunks.size(); a.w2 = packed + pb.frag16_off; a.b2 = packed + pb.bias_off;
+        a.res = opb.res >= 0 ? bufs[opb.res] : nullptr; a.seg_res = opb.res >= 0 ? seg_of(opb.res) : nullptr;
+        a.ld_res = opb.res >= 0 ? n->ld[opb.res] : 0;
+        a.y = bufs[opb.dst]; a.seg_y = seg_of(opb.dst); a.ld_y = n->ld[opb.dst];
+        a.accumulate = opb.accumulate; a.out_div = opb.out_div; a.post_act = opb.post_act; a.post_slope = opb.post_slope;
+        a.strips = p->d_strips[pi]; a.ncols = p->d_ncols[pi]; a.steps = p->pair_steps;
+        a.x_min_off = ph.pair_xmin; a.xs = ph.pair_xs;
+        a.off1 = -op.src[0].pad; a.dil1 = op.src[0].dilation; a.off2 = -opb.src[0].pad; a.dil2 = opb.src[0].dilation;
+        if (!n->pair_attr_set) {
+          const hipError_t ea2 = hipFuncSetAttribute(reinterpret_cast<const void*>(pwg_cnet_pair_kernel),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, PR_MAX_LDS);
+          if (ea2 != hipSuccess) return hipf(ea2, "pair kernel LDS attribute");
+          n->pair_attr_set = true;
+        }
+        hipLaunchKernelGGL(pwg_cnet_pair_kernel, dim3((unsigned)p->n_strips[pi]), dim3(256), (size_t)ph.pair_lds, s, a);
+      }
+    } else if (op.kind == PWG_CNET_PQMF) {
       CnPqmfArgs a;
       a.x = bufs[op.src[0].buf]; a.seg_src = seg_of(op.src[0].buf); a.ld_src = n->ld[op.src[0].buf];
       a.h = packed + ph.frag_off; a.y = bufs[op.dst]; a.seg_dst = seg_of(op.dst); a.ld_dst = n->ld[op.dst];
@@ -1042,9 +1406,14 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
 
 int pwg_cnet_set_option(PwgCnet* n, int option, long long value) {
   if (!n) return fail(PWG_ERR_INVALID, "null handle");
-  if (option != PWG_CNET_OPT_SPLIT_F16) return fail(PWG_ERR_INVALID, "unknown option");
-  if (value != 0 && value != 1) return fail(PWG_ERR_INVALID, "split_f16 must be 0 or 1");
-  n->split_f16 = (int)value;
+  if (option == PWG_CNET_OPT_PAIR_STEPS) {
+    if (value < 1 || value > 4096) return fail(PWG_ERR_INVALID, "pair_steps must be in [1, 4096]");
+    n->pair_steps = (int)value;
+    return PWG_OK;
+  }
+  if (option != PWG_CNET_OPT_SPLIT_F16 && option != PWG_CNET_OPT_FUSE_PAIRS) return fail(PWG_ERR_INVALID, "unknown option");
+  if (value != 0 && value != 1) return fail(PWG_ERR_INVALID, "option value must be 0 or 1");
+  (option == PWG_CNET_OPT_SPLIT_F16 ? n->split_f16 : n->fuse_pairs) = (int)value;
   return PWG_OK;
 }
 

@@ -109,3 +109,33 @@ def test_vocoder_timing_and_weight_update(built_lib, cuda_device):
         m.output_conv[1].bias.add_(0.25)  # re-packed on the next call
         y2 = m.inference(mel).cpu().numpy()
     assert np.abs(y2 - y1).max() > 1e-3
+
+
+@pytest.mark.parametrize("steps", [1, 3, 8])
+def test_fused_conv_pairs_bitwise_equal_to_unfused(steps, built_lib, cuda_device):
+    """pwg_cnet_pair_kernel (ResBlock conv pairs with the intermediate in LDS) against the two
+    unfused split-f16 ops: same chunk order, pair split and epilogue order, so bit-identical.
+    Ragged utterances (1..14 frames -> 256..3584 columns at the 32-channel stage) with strips of
+    1, 3 and 8 tiles exercise strip starts, partial last strips and utterance edges."""
+    from parallelwavegan_amd import configs, synthetic
+    from parallelwavegan_amd.hifigan import HiFiGANGenerator
+
+    _, params = configs.vocoder_params("hifigan_v1")
+    m = HiFiGANGenerator(**params)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic.make_module_state_dict(m, seed=4).items()})
+    m = m.to(cuda_device)
+    eng = m.engine()
+    eng.set_pair_steps(steps)
+    mels = [synthetic.make_mel(f, 80, seed=60 + i) for i, f in enumerate([3, 1, 14, 5])]
+    with torch.no_grad():
+        eng.set_fuse_pairs(False)
+        ref = [y.cpu().numpy() for y in m.inference_batch(mels)]
+        eng.set_fuse_pairs(True)
+        eng.set_timing(True)
+        got = [y.cpu().numpy() for y in m.inference_batch(mels)]
+        t = eng.collect_timing()
+        eng.set_timing(False)
+    # the 32-channel stage's 3 ResBlocks x 3 (conv1, conv2) pairs run fused
+    assert sum(1 for _, _, n in t if n == 0) == 9
+    for a, b in zip(got, ref):
+        np.testing.assert_array_equal(a, b)

@@ -19,6 +19,8 @@ def main():
     ap.add_argument("config")
     ap.add_argument("--utts", type=int, default=32)
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--nofuse", action="store_true")
+    ap.add_argument("--pair-steps", type=int, default=None)
     a = ap.parse_args()
     cls, p = configs.vocoder_params(a.config)
     m = {"MelGANGenerator": MelGANGenerator, "HiFiGANGenerator": HiFiGANGenerator}[cls](**p)
@@ -28,6 +30,9 @@ def main():
     dev = torch.device("cuda", 0)
     m = m.to(dev)
     eng = m.engine()
+    eng.set_fuse_pairs(not a.nofuse)
+    if a.pair_steps:
+        eng.set_pair_steps(a.pair_steps)
     P = eng.program
     lengths = synthetic.libritts_lengths(a.utts, seed=3)
     frames = int(lengths.sum())
@@ -55,9 +60,13 @@ def main():
         fl = 2.0 * op["out_channels"] * k * r * frames
         ms /= a.steps
         tot += ms
-        rows.append((name, op["out_channels"], k, r, ms, fl / (ms * 1e-3) / 1e12))
-    for name, M, K, r, ms, tf in rows:
-        print(f"{name:28s} M {M:4d} K {K:5d} rate {r:4d}  {ms:7.3f} ms  {tf:6.1f} TF")
+        if n == 0 and rows:  # fused into the previous op's launch (pwg_cnet_pair_kernel)
+            prev = rows[-1]
+            rows[-1] = (prev[0] + "+", prev[1], prev[2] + k, r, prev[4], prev[5] + fl)
+            continue
+        rows.append((name, op["out_channels"], k, r, ms, fl))
+    for name, M, K, r, ms, fl in rows:
+        print(f"{name:28s} M {M:4d} K {K:5d} rate {r:4d}  {ms:7.3f} ms  {fl / (ms * 1e-3) / 1e12:6.1f} TF")
     print(f"total {tot:.3f} ms")
 
 
