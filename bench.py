@@ -36,14 +36,15 @@ HBM_PEAK_GBS = 8000.0
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/F16 dense (no sparsity)
 
 
-def split_layer_bytes_per_sample(params, H, L):
+def split_layer_bytes_per_sample(params, H, L, fuse_first=False):
     """Algorithmic HBM bytes per sample of the split engine's residual layer, averaged over the L
     launches: x read + write (4 B per channel as an fp16 pair) and skip read + write (fp32); layer 0
-    reads no skip, the last layer writes neither x nor skip but the output; plus the frame-rate aux
-    rows (GR pairs per frame). DESIGN.md sec 3.6."""
+    reads no skip (and, with the fused first_conv, the 4-byte noise instead of x), the last layer
+    writes neither x nor skip but the output; plus the frame-rate aux rows (GR pairs per frame).
+    DESIGN.md sec 3.0."""
     R, S, G, O = (params[k] for k in ("residual_channels", "skip_channels", "gate_channels", "out_channels"))
     mid = 4 * (2 * R + 2 * S)
-    first = 4 * (2 * R + S)
+    first = 4 * (R + S) + 4 if fuse_first else 4 * (2 * R + S)
     last = 4 * (R + S) + 4 * O
     return (first + (L - 2) * mid + last) / L + 4 * G / H
 
@@ -307,6 +308,7 @@ def main():
                     help="default: split where the shape allows, else persistent (the engine default)")
     ap.add_argument("--waves-per-wg", type=int, default=None)
     ap.add_argument("--wg-per-cu", type=int, default=None)
+    ap.add_argument("--no-fuse-first", action="store_true", help="split16: standalone first_conv kernel (A/B)")
     ap.add_argument("--cnet-fp32", action="store_true", help="vocoder configs: exact fp32 MFMA instead of split-f16")
     ap.add_argument("--cnet-nofuse", action="store_true", help="vocoder configs: run fusable conv pairs unfused")
     ap.add_argument("--pair-steps", type=int, default=None, help="vocoder configs: 128-column tiles per fused-pair strip")
@@ -330,6 +332,8 @@ def main():
         eng.set_option("waves_per_wg", args.waves_per_wg)
     if args.wg_per_cu:
         eng.set_option("wg_per_cu", args.wg_per_cu)
+    fuse_first = args.layer_kernel == "split16" and not args.no_fuse_first and params["layers"] > 1
+    eng.set_option("fuse_first_conv", 0 if args.no_fuse_first else 1)
     H = eng.upsample_factor
     A = params["aux_channels"]
 
@@ -411,7 +415,7 @@ def main():
     L = params["layers"]
     if args.layer_kernel in ("split", "split16"):
         # HBM-bound: algorithmic bytes of the engine's layer per launch / launch time
-        bytes_launch = split_layer_bytes_per_sample(params, H, L) * plan.total_samples
+        bytes_launch = split_layer_bytes_per_sample(params, H, L, fuse_first) * plan.total_samples
         n_blocks = int(sum(-(-int(f) * H // 128) * 4 for f in lengths))
         exec_flop = split_executed_flop_per_block(L, args.layer_kernel) * n_blocks
         achieved_gbs = bytes_launch / layer_avg_s / 1e9

@@ -157,7 +157,9 @@ enum {
                                     split-f16 (fp32 operands as fp16 hi+lo pairs, 3 f16 MFMAs per
                                     product; default for R = S = 64, gate 128, kernel 3) */
   PWG_OPT_WAVES_PER_WG = 1,   /* persistent kernel: waves per workgroup (1..8, default 8) */
-  PWG_OPT_WG_PER_CU = 2       /* persistent kernel: workgroups per CU in the grid (default 1) */
+  PWG_OPT_WG_PER_CU = 2,      /* persistent kernel: workgroups per CU in the grid (default 1) */
+  PWG_OPT_FUSE_FIRST_CONV = 3 /* split16 layer kernel: first_conv evaluated inside layer 0 from the
+                                    noise, x0 never stored (default 1; bit-identical to 0) */
 };
 PWG_API int pwg_set_option(PwgHandle* h, int option, long long value);
 

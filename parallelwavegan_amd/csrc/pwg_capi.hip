@@ -304,6 +304,7 @@ struct PwgHandle {
   size_t lo_split16 = 0, off_skip0_16 = 0, off_head16_w1 = 0, off_head16_w2 = 0;
   // options
   int layer_kernel = 0, waves_per_wg = 8, wg_per_cu = 1;
+  int fuse_first = 1;  // PWG_OPT_FUSE_FIRST_CONV
   int n_cu = 0;
   // timing
   bool timing = false;
@@ -946,7 +947,12 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
   fa.noise = noise; fa.w = packed + h->off_first_w; fa.b = packed + h->off_first_b; fa.x = x0; fa.x1 = x1;
   fa.tile_utt = p->d_tile_utt; fa.utts = p->d_utts; fa.gap_col0 = p->d_gap_col0; fa.n_work = p->n_tiles;
   fa.Tpad = p->Tpad; fa.R = h->R; fa.RS = h->RS;
+  // split16 with the fused first_conv: layer 0 builds x0 itself; only the gap tiles of both
+  // residual buffers are zeroed here (the work-tile branch is skipped: n_work = 0)
+  const bool fuse_first = split16 && h->fuse_first && h->L > 1;
+  if (fuse_first) fa.n_work = 0;
   e = timed(PWG_KERNEL_FIRST_CONV, [&] {
+    if (fuse_first) return p->n_gap_tiles > 0 ? launch_first_conv_split16(fa, p->n_gap_tiles, s) : hipSuccess;
     return split16 ? launch_first_conv_split16(fa, p->n_tiles + p->n_gap_tiles, s)
            : split ? launch_first_conv_split(fa, p->n_tiles + p->n_gap_tiles, s)
                    : launch_first_conv(fa, p->n_tiles + p->n_gap_tiles, s);
@@ -999,6 +1005,10 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
       sa.ctr = sched_ctr + (size_t)l * SCHED_CTR_STRIDE * 8;
       const int nwg = h->n_cu * h->wg_per_cu;
       sa.trace = nullptr;
+      sa.noise = nullptr; sa.fw = sa.fb = nullptr;
+      if (fuse_first && l == 0) {
+        sa.noise = noise; sa.fw = packed + h->off_first_w; sa.fb = packed + h->off_first_b;
+      }
 #if PWG_TRACE
       static unsigned long long* d_trace_s = nullptr;
       const size_t per_layer_s = (size_t)nwg * 8 * 8;
@@ -1105,6 +1115,10 @@ int pwg_set_option(PwgHandle* h, int option, long long value) {
     case PWG_OPT_WAVES_PER_WG:
       if (value < 1 || value > 16) return fail(PWG_ERR_INVALID, "waves per workgroup must be in [1, 16]");
       h->waves_per_wg = (int)value;
+      return PWG_OK;
+    case PWG_OPT_FUSE_FIRST_CONV:
+      if (value != 0 && value != 1) return fail(PWG_ERR_INVALID, "fuse_first_conv must be 0 or 1");
+      h->fuse_first = (int)value;
       return PWG_OK;
     case PWG_OPT_WG_PER_CU:
       if (value < 1 || value > 64) return fail(PWG_ERR_INVALID, "workgroups per CU must be in [1, 64]");

@@ -186,6 +186,9 @@ struct SplitArgs {
   float skip_scale;
   int* ctr;
   unsigned long long* trace;  // PWG_TRACE builds only (tools/trace_layer.py)
+  const float* noise;         // split16 layer 0 with first_conv fused (else null): caller noise
+  const float* fw;            // first_conv weight [64] and bias [64]
+  const float* fb;
 };
 // dwords of one layer's split image (SplitSmem in pwg_split.hip without the head)
 constexpr int SPLIT_LAYER_DWORDS = 3 * 4 * 4 * 2 * 64 * 4 + 4 * 4 * 2 * 64 * 4 + 32 * 4 + 64;

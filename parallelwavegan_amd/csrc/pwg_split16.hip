@@ -151,7 +151,11 @@ struct Split16Smem {
 static_assert(Split16Smem::WG + Split16Smem::W2 + Split16Smem::BG + Split16Smem::BO == SPLIT_LAYER_DWORDS,
               "split16 layer image size");
 
-template <bool LAST, int TC>
+// FIRST (layer 0 with PWG_OPT_FUSE_FIRST_CONV): first_conv (models/parallel_wavegan.py:81,161,
+// x0 = w z + b, zero outside the utterance) is evaluated on the fly from the 4-byte noise while
+// the tap pieces are built, with the same fmaf and pair split as pwg_first_conv_split16_kernel
+// (bit-identical), so x0 is never written to or read from HBM. w, b sit in LDS after the image.
+template <bool LAST, int TC, bool FIRST>
 __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitArgs a) {
   constexpr int MG = PWG_SPLIT16_MG;
   extern __shared__ __attribute__((aligned(16))) unsigned smem16[];
@@ -160,6 +164,7 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
   unsigned* s_bg = s_w2 + Split16Smem::W2;
   float* s_bo = reinterpret_cast<float*>(s_bg + Split16Smem::BG);
   float* s_hw1 = s_bo + Split16Smem::BO;
+  float* s_fwb = reinterpret_cast<float*>(smem16 + Split16Smem::dwords(LAST));  // FIRST: w[64] | b[64]
   {
     const int nthr = blockDim.x;
     const u32x4* src = reinterpret_cast<const u32x4*>(a.wg);
@@ -170,6 +175,7 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
       dst = reinterpret_cast<u32x4*>(s_hw1);
       for (int i = threadIdx.x; i < Split16Smem::HW1 / 4; i += nthr) dst[i] = src[i];
     }
+    if (FIRST && threadIdx.x < 128) s_fwb[threadIdx.x] = threadIdx.x < 64 ? a.fw[threadIdx.x] : a.fb[threadIdx.x - 64];
     __syncthreads();
   }
 
@@ -207,13 +213,36 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
   };
 
   // a lane's tap row pieces for both n-tiles: b[nt*4 + ks*2 + hl]
-  auto bload = [&](int col, int tap, u32x4 (&b)[8]) {
-    const int cc = col + (PWG_SPLIT16_DIAG_NOTAP ? 0 : (tap - TC) * a.dil);  // NOTAP: diagnostic only
+  auto bload = [&](const BlockDesc& d, int tap, u32x4 (&b)[8]) {
+    if constexpr (FIRST) {
+      // piece (ks, hl) = channels chan16(ks, g, 0..7) of x0 = w z + b at sample t
+      const f32x4* fw4 = reinterpret_cast<const f32x4*>(s_fwb) + g;
+      const f32x4* fb4 = reinterpret_cast<const f32x4*>(s_fwb + 64) + g;
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-      const u32x4* p = reinterpret_cast<const u32x4*>(a.x_in + row16(cc + 16 * nt + c, g));
+      for (int nt = 0; nt < 2; ++nt) {
+        const int t = d.t0 + 16 * nt + c + (tap - TC) * a.dil;
+        const bool inside = t >= 0 && t < d.T;
+        const float z = a.noise[d.io_off + (t < 0 ? 0 : (t >= d.T ? d.T - 1 : t))];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) b[nt * 4 + q] = p[q * 64];
+        for (int ks = 0; ks < 2; ++ks) {
+          float v[8];
+#pragma unroll
+          for (int jh = 0; jh < 2; ++jh) {
+            const f32x4 w = fw4[4 * (2 * ks + jh)], bb = fb4[4 * (2 * ks + jh)];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[4 * jh + i] = inside ? fmaf(w[i], z, bb[i]) : 0.f;
+          }
+          split8x<0>(v, b[nt * 4 + ks * 2], b[nt * 4 + ks * 2 + 1]);
+        }
+      }
+    } else {
+      const int cc = d.col + (PWG_SPLIT16_DIAG_NOTAP ? 0 : (tap - TC) * a.dil);  // NOTAP: diagnostic only
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const u32x4* p = reinterpret_cast<const u32x4*>(a.x_in + row16(cc + 16 * nt + c, g));
+#pragma unroll
+        for (int q = 0; q < 4; ++q) b[nt * 4 + q] = p[q * 64];
+      }
     }
   };
   const u32x4* wgl = reinterpret_cast<const u32x4*>(s_wg) + lane;
@@ -263,12 +292,11 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
   if (blk < 0) return;
   BlockDesc bdn = a.blocks[blk];
   u32x4 b0[8], b1[8];
-  bload(bdn.col, 0, b0);
+  bload(bdn, 0, b0);
 
   while (true) {
     const BlockDesc bd = bdn;
     bdn = a.blocks[nblk >= 0 ? nblk : blk];
-    const int col_next = nblk >= 0 ? bdn.col : bd.col;
     const bool full = bd.t0 + 32 <= bd.T;
 
     // aux operands: lane group g covers window frames fw0 + 2g, fw0 + 2g + 1; K slots
@@ -333,12 +361,12 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
 
 #endif
     constexpr int T1 = TC == 1 ? 2 : 1;
-    bload(bd.col, T1, b1);
+    bload(bd, T1, b1);
     mma_tap(acc, b0, 0);
     load_dv();
-    bload(bd.col, TC, b0);
+    bload(bd, TC, b0);
     mma_tap(acc, b1, T1);
-    bload(col_next, 0, b1);
+    bload(bdn, 0, b1);  // the next block's (bdn = bd when there is none)
     mma_tap(acc, b0, TC);
     if (!LAST) x_seed(b0, acc2);
 
@@ -552,20 +580,24 @@ hipError_t launch_layer_split16(const SplitArgs& a, bool last, int tap_center, i
                                 hipStream_t s) {
   if (waves_per_wg > 8) waves_per_wg = 8;
   const dim3 grid((unsigned)n_wg), block((unsigned)(64 * waves_per_wg));
-#define PWG_SPLIT16_LAUNCH(LAST_, TC_)                                                                  \
+#define PWG_SPLIT16_LAUNCH(LAST_, TC_, FIRST_)                                                          \
   {                                                                                                     \
-    const size_t lds = sizeof(unsigned) * Split16Smem::dwords(LAST_);                                   \
-    auto kfn = &pwg_layer_split16_kernel<LAST_, TC_>;                                                   \
+    const size_t lds = sizeof(unsigned) * (Split16Smem::dwords(LAST_) + (FIRST_ ? 128 : 0));            \
+    auto kfn = &pwg_layer_split16_kernel<LAST_, TC_, FIRST_>;                                           \
     hipError_t e_ = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),                             \
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);           \
     if (e_ != hipSuccess) return e_;                                                                    \
     hipLaunchKernelGGL(kfn, grid, block, lds, s, a);                                                    \
     return hipGetLastError();                                                                           \
   }
+  const bool first = a.noise != nullptr;  // fused first_conv (never together with last: L > 1)
+  if (first && last) return hipErrorInvalidValue;
   if (tap_center == 1) {
-    if (last) PWG_SPLIT16_LAUNCH(true, 1) else PWG_SPLIT16_LAUNCH(false, 1)
+    if (first) PWG_SPLIT16_LAUNCH(false, 1, true)
+    if (last) PWG_SPLIT16_LAUNCH(true, 1, false) else PWG_SPLIT16_LAUNCH(false, 1, false)
   } else if (tap_center == 2) {
-    if (last) PWG_SPLIT16_LAUNCH(true, 2) else PWG_SPLIT16_LAUNCH(false, 2)
+    if (first) PWG_SPLIT16_LAUNCH(false, 2, true)
+    if (last) PWG_SPLIT16_LAUNCH(true, 2, false) else PWG_SPLIT16_LAUNCH(false, 2, false)
   }
 #undef PWG_SPLIT16_LAUNCH
   return hipErrorInvalidValue;

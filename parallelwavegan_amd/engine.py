@@ -260,9 +260,9 @@ class Engine:
     LAYER_KERNELS = {"persistent": 0, "tiled": 1, "split": 2, "split16": 3}
 
     def set_option(self, option, value):
-        """pwg_set_option: option in {"layer_kernel", "waves_per_wg", "wg_per_cu"}."""
+        """pwg_set_option: option in {"layer_kernel", "waves_per_wg", "wg_per_cu", "fuse_first_conv"}."""
         opts = {"layer_kernel": _lib.PWG_OPT_LAYER_KERNEL, "waves_per_wg": _lib.PWG_OPT_WAVES_PER_WG,
-                "wg_per_cu": _lib.PWG_OPT_WG_PER_CU}
+                "wg_per_cu": _lib.PWG_OPT_WG_PER_CU, "fuse_first_conv": _lib.PWG_OPT_FUSE_FIRST_CONV}
         if option == "layer_kernel" and isinstance(value, str):
             value = self.LAYER_KERNELS[value]
         _lib.check(self._lib.pwg_set_option(self._h, opts[option], int(value)))

@@ -249,3 +249,40 @@ def test_cpu_module_fails_loudly(built_lib):
     m = ParallelWaveGANGenerator(**configs.generator_params("reference_test"))
     with pytest.raises(RuntimeError):
         m.inference(np.zeros((4, 10), np.float32))
+
+
+@pytest.mark.parametrize("causal", [False, True], ids=["noncausal", "causal"])
+def test_fused_first_conv_bitwise_equal(causal, built_lib, cuda_device):
+    """PWG_OPT_FUSE_FIRST_CONV: layer 0 of the split16 kernel evaluates first_conv from the noise
+    (same fmaf and pair split as the standalone kernel), so the output is bit-identical to the
+    unfused path, for ragged inference batches and for the batched forward(z, c) layout."""
+    from parallelwavegan_amd import Engine, ParallelWaveGANGenerator, configs, synthetic
+
+    params = dict(configs.generator_params("libritts_v1"), use_causal_conv=causal)
+    sd = synthetic.make_state_dict(params, seed=6)
+    lengths = [2, 9, 1, 33]
+    mels = [torch.from_numpy(synthetic.make_mel(f, 80, seed=70 + i)).to(cuda_device) for i, f in enumerate(lengths)]
+    noises = [torch.from_numpy(synthetic.make_noise(f * 300, seed=80 + i)).to(cuda_device) for i, f in enumerate(lengths)]
+    outs = []
+    for fuse in (0, 1):
+        eng = Engine(params, cuda_device)
+        eng.load_state_dict(sd)
+        eng.set_option("layer_kernel", "split16")
+        eng.set_option("fuse_first_conv", fuse)
+        outs.append([y.cpu().numpy() for y in eng.infer(mels, noises)])
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a, b)
+
+    m = ParallelWaveGANGenerator(**params)
+    m.remove_weight_norm()
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+    m = m.eval().to(cuda_device)
+    w = params["aux_context_window"]
+    c = torch.from_numpy(np.stack([synthetic.make_mel(12 + 2 * w, 80, seed=90 + b).T for b in range(2)])).to(cuda_device)
+    z = torch.from_numpy(np.stack([synthetic.make_noise(12 * 300, seed=95 + b).T for b in range(2)])).to(cuda_device)
+    ys = []
+    with torch.no_grad():
+        for fuse in (0, 1):
+            m.engine().set_option("fuse_first_conv", fuse)
+            ys.append(m(z, c).cpu().numpy())
+    np.testing.assert_array_equal(ys[0], ys[1])

@@ -9,7 +9,8 @@ import sys
 def main(summary, out, config="libritts_v1", utts=32, layer_kernel="split"):
     d = json.load(open(summary))
     if layer_kernel.startswith("split"):
-        rows = {k: v for k, v in d.items() if ("layer_%s_kernel<false" % layer_kernel) in k}
+        # middle layers: not last, and not layer 0 with the fused first_conv (<false, TC, true>)
+        rows = {k: v for k, v in d.items() if ("layer_%s_kernel<false" % layer_kernel) in k and ", true>" not in k}
     else:
         rows = {k: v for k, v in d.items() if "layer" in k and ("0, 16" in k or "4, 4, 0" in k)}
     k, v = max(rows.items(), key=lambda kv: kv[1].get("SQ_WAVES", 0))
