@@ -734,15 +734,27 @@ int pwg_pack_weights(const PwgHandle* h, const float* ref, float* pk) {
           }
     for (int i = 0; i < O; ++i) pk[h->off_head_b2 + i] = b2h[i];
     if (h->split_ok) {
-      // 16x16x4 f32 head of the split16 kernel: W1h [ms][m3][lane (c, g)][i] = W1h[16m3 + c][16ms + 4g + i],
-      // then b1 [g][4m3 + i] = b1[16m3 + 4g + i]; W2h [oc][g][4m3 + i] = W2h[oc][16m3 + 4g + i]
+      // split-f16 head of the split16 kernel (v_mfma_f32_16x16x32_f16, 3 products): W1h pairs
+      // [ks 2][m3 4][hi/lo 2][lane (c, g) 64][4 dwords], lane's k = 8g + j <-> skip row
+      // chan16(ks, g, j) (its accumulator rows), A row 16m3 + c; then b1 [g][4m3 + i] =
+      // b1[16m3 + 4g + i]; W2h [oc][g][4m3 + i] = W2h[oc][16m3 + 4g + i]
       float* w16 = pk + h->off_head16_w1;
-      for (int ms = 0; ms < 4; ++ms)
+      uint32_t* w16u = reinterpret_cast<uint32_t*>(w16);
+      auto hchan = [](int ks, int g, int j) { return 16 * (2 * ks + (j >> 2)) + 4 * g + (j & 3); };
+      for (int ks = 0; ks < 2; ++ks)
         for (int m3 = 0; m3 < 4; ++m3)
           for (int lane = 0; lane < 64; ++lane)
-            for (int i = 0; i < 4; ++i)
-              w16[(((size_t)ms * 4 + m3) * 64 + lane) * 4 + i] =
-                  w1[(size_t)(16 * m3 + (lane & 15)) * S + 16 * ms + 4 * (lane >> 4) + i];
+            for (int j = 0; j < 8; j += 2) {
+              uint32_t hv = 0, lv = 0;
+              for (int e = 0; e < 2; ++e) {
+                const uint32_t pr = split_pair(w1[(size_t)(16 * m3 + (lane & 15)) * S + hchan(ks, lane >> 4, j + e)]);
+                hv |= (pr & 0xffffu) << (16 * e);
+                lv |= (pr >> 16) << (16 * e);
+              }
+              const size_t base = (((size_t)ks * 4 + m3) * 2) * 256 + (size_t)lane * 4 + j / 2;
+              w16u[base] = hv;
+              w16u[base + 256] = lv;
+            }
       for (int g = 0; g < 4; ++g)
         for (int m3 = 0; m3 < 4; ++m3)
           for (int i = 0; i < 4; ++i) w16[4096 + 16 * g + 4 * m3 + i] = b1[16 * m3 + 4 * g + i];

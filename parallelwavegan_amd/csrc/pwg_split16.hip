@@ -478,28 +478,39 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
         }
       }
     } else {
-      // ---- fused output head (models/parallel_wavegan.py:131-138,166-171) on v_mfma_f32_16x16x4f32:
-      //      h1 = W1h . relu(skip * sqrt(1/L)) + b1h, k-step (ms, i): lane group g supplies skip row
-      //      16ms + 4g + i; then y = W2h . relu(h1) + b2h across the 4 lane groups
-      const f32x4* hw1 = reinterpret_cast<const f32x4*>(s_hw1) + lane;
+      // ---- fused output head (models/parallel_wavegan.py:131-138,166-171), split-f16 on
+      //      v_mfma_f32_16x16x32_f16 like the layer: h1 = W1h . relu(skip * sqrt(1/L)) + b1h with
+      //      k-step ks element j = skip row chan16(ks, g, j) = acc2[2ks + (j >> 2)][nt][j & 3]
+      //      (the W1h image is packed in that k order); then y = W2h . relu(h1) + b2h across the 4
+      //      lane groups. (The fp32 v_mfma_f32_16x16x4f32 head took 128 MFMAs of twice the cycles.)
+      const u32x4* hw1 = reinterpret_cast<const u32x4*>(s_hw1) + lane;
       const f32x4* hb1 = reinterpret_cast<const f32x4*>(s_hw1 + 4 * 4 * 64 * 4 + 16 * g);
       f32x4 acc3[4][2];
 #pragma unroll
       for (int m3 = 0; m3 < 4; ++m3)
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) acc3[m3][nt] = hb1[m3];
+      u32x4 sh[2][2], sl[2][2];  // [nt][ks]
 #pragma unroll
-      for (int ms = 0; ms < 4; ++ms)
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          float hv[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) hv[j] = fmaxf(acc2[2 * ks + (j >> 2)][nt][j & 3] * a.skip_scale, 0.f);
+          split8x<0>(hv, sh[nt][ks], sl[nt][ks]);
+        }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int m3 = 0; m3 < 4; ++m3) {
-          const f32x4 wv = hw1[(ms * 4 + m3) * 64];
+          const u32x4 ah = hw1[((ks * 4 + m3) * 2) * 64], al = hw1[((ks * 4 + m3) * 2 + 1) * 64];
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int nt = 0; nt < 2; ++nt) {
-              const float hs = fmaxf(acc2[ms][nt][i] * a.skip_scale, 0.f);
-              acc3[m3][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[i], hs, acc3[m3][nt], 0, 0, 0);
-            }
+          for (int nt = 0; nt < 2; ++nt) {
+            acc3[m3][nt] = mma16(ah, sh[nt][ks], acc3[m3][nt]);
+            acc3[m3][nt] = mma16(ah, sl[nt][ks], acc3[m3][nt]);
+            acc3[m3][nt] = mma16(al, sh[nt][ks], acc3[m3][nt]);
+          }
         }
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
