@@ -47,6 +47,9 @@ constexpr int CN_MAX_CHUNKS = 4096;
 #define PWG_CNET_G 1  // 2 (two chunks per barrier) measured 9 % slower on HiFiGAN v1
 #endif
 constexpr int CN_G = PWG_CNET_G;   // 16-channel chunks staged per barrier
+#ifndef PWG_CNET_DEPTH2
+#define PWG_CNET_DEPTH2 0  // 1: loads two chunk groups ahead (A/B variant)
+#endif
 
 struct ChunkDesc {   // one K chunk of an op (uniform per launch)
   int src;           // 0 / 1
@@ -205,33 +208,15 @@ __global__ void __launch_bounds__(256) pwg_cnet_conv_kernel(const CnConvArgs a) 
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[m][n][r] = 0.f;
 
-  f32x4v ar[G][(MT + 1) / 2];
-  aload(0, ar);
-  astore(0, ar);
-  f32x8v bcur[G][NT];
-  BRaw bnext[G];
-#pragma unroll
-  for (int g2 = 0; g2 < G; ++g2) {
-    braw(g2, bnext[g2]);
-    bprep(bnext[g2], bcur[g2]);
-  }
-  __syncthreads();
-  const int n_groups = a.n_chunks / G;
-  for (int cg = 0; cg < n_groups; ++cg) {
-    const bool more = cg + 1 < n_groups;
-    if (more) {
-      aload(cg + 1, ar);
-#pragma unroll
-      for (int g2 = 0; g2 < G; ++g2) braw((cg + 1) * G + g2, bnext[g2]);
-    }
-    __builtin_amdgcn_sched_barrier(0);  // keep the loads issued before the MFMAs below
+  // one chunk group's MFMAs from LDS buffer buf and the prepared B operands
+  auto compute = [&](int buf, const f32x8v (&bc)[G][NT]) {
 #pragma unroll
     for (int g2 = 0; g2 < G; ++g2) {
       if constexpr (SPLIT) {
-        const u32x4v* sa = reinterpret_cast<const u32x4v*>(s_a[cg & 1] + g2 * MT * 512) + lane;
+        const u32x4v* sa = reinterpret_cast<const u32x4v*>(s_a[buf] + g2 * MT * 512) + lane;
         u32x4v bh[NT], bl[NT];
 #pragma unroll
-        for (int n = 0; n < NT; ++n) cn_split8(bcur[g2][n], bh[n], bl[n]);
+        for (int n = 0; n < NT; ++n) cn_split8(bc[g2][n], bh[n], bl[n]);
         u32x4v ah[MT], al[MT];
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
@@ -250,7 +235,7 @@ __global__ void __launch_bounds__(256) pwg_cnet_conv_kernel(const CnConvArgs a) 
                                                                __builtin_bit_cast(f16x8v, bh[n]), acc[m][n], 0, 0, 0);
           }
       } else {
-        const f32x4v* sa = reinterpret_cast<const f32x4v*>(s_a[cg & 1] + g2 * MT * 512) + lane;
+        const f32x4v* sa = reinterpret_cast<const f32x4v*>(s_a[buf] + g2 * MT * 512) + lane;
 #pragma unroll
         for (int sub = 0; sub < 2; ++sub) {
           f32x4v av[MT];
@@ -262,10 +247,75 @@ __global__ void __launch_bounds__(256) pwg_cnet_conv_kernel(const CnConvArgs a) 
             for (int m = 0; m < MT; ++m)
 #pragma unroll
               for (int n = 0; n < NT; ++n)
-                acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m][e], bcur[g2][n][4 * sub + e], acc[m][n], 0, 0, 0);
+                acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m][e], bc[g2][n][4 * sub + e], acc[m][n], 0, 0, 0);
         }
       }
     }
+  };
+
+  const int n_groups = a.n_chunks / G;
+  f32x8v bcur[G][NT];
+#if PWG_CNET_DEPTH2
+  // Loads run TWO chunk groups ahead (register ring of 2): chunk c+2's A fragments and raw B rows
+  // are issued before chunk c's MFMAs; chunk c+1's (issued one step earlier) are staged / prepared
+  // after them.
+  f32x4v ar0[G][(MT + 1) / 2], ar1[G][(MT + 1) / 2];
+  BRaw br0[G], br1[G];
+  aload(0, ar0);
+  astore(0, ar0);
+#pragma unroll
+  for (int g2 = 0; g2 < G; ++g2) {
+    braw(g2, br0[g2]);
+    bprep(br0[g2], bcur[g2]);
+  }
+  if (n_groups > 1) {
+    aload(1, ar1);
+#pragma unroll
+    for (int g2 = 0; g2 < G; ++g2) braw(G + g2, br1[g2]);
+  }
+  __syncthreads();
+  auto step = [&](int cg, f32x4v (&rl)[G][(MT + 1) / 2], BRaw (&bl2)[G], f32x4v (&rs)[G][(MT + 1) / 2],
+                  BRaw (&bs)[G]) {
+    if (cg + 2 < n_groups) {
+      aload(cg + 2, rl);
+#pragma unroll
+      for (int g2 = 0; g2 < G; ++g2) braw((cg + 2) * G + g2, bl2[g2]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    compute(cg & 1, bcur);
+    __builtin_amdgcn_sched_barrier(0);
+    const bool more = cg + 1 < n_groups;
+    if (more) astore((cg + 1) & 1, rs);
+    __syncthreads();
+    if (more) {
+#pragma unroll
+      for (int g2 = 0; g2 < G; ++g2) bprep(bs[g2], bcur[g2]);
+    }
+  };
+  for (int cg = 0; cg < n_groups; cg += 2) {
+    step(cg, ar0, br0, ar1, br1);
+    if (cg + 1 < n_groups) step(cg + 1, ar1, br1, ar0, br0);
+  }
+#else
+  f32x4v ar[G][(MT + 1) / 2];
+  aload(0, ar);
+  astore(0, ar);
+  BRaw bnext[G];
+#pragma unroll
+  for (int g2 = 0; g2 < G; ++g2) {
+    braw(g2, bnext[g2]);
+    bprep(bnext[g2], bcur[g2]);
+  }
+  __syncthreads();
+  for (int cg = 0; cg < n_groups; ++cg) {
+    const bool more = cg + 1 < n_groups;
+    if (more) {
+      aload(cg + 1, ar);
+#pragma unroll
+      for (int g2 = 0; g2 < G; ++g2) braw((cg + 1) * G + g2, bnext[g2]);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep the loads issued before the MFMAs below
+    compute(cg & 1, bcur);
     __builtin_amdgcn_sched_barrier(0);  // ... and their consumers after them
     if (more) astore((cg + 1) & 1, ar);
     __syncthreads();
@@ -274,6 +324,7 @@ __global__ void __launch_bounds__(256) pwg_cnet_conv_kernel(const CnConvArgs a) 
       for (int g2 = 0; g2 < G; ++g2) bprep(bnext[g2], bcur[g2]);
     }
   }
+#endif
 
   // epilogue
   const int2 sd = *reinterpret_cast<const int2*>(a.seg_dst + 2 * u);
