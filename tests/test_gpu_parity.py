@@ -286,3 +286,28 @@ def test_fused_first_conv_bitwise_equal(causal, built_lib, cuda_device):
             m.engine().set_option("fuse_first_conv", fuse)
             ys.append(m(z, c).cpu().numpy())
     np.testing.assert_array_equal(ys[0], ys[1])
+
+
+def test_maximum_size_utterance(built_lib, cuda_device):
+    """One 12.5-minute utterance (LibriTTS v1, T' = 60,000 frames -> 18 M samples, ~15 GB of plan
+    workspace) in one plan: finite, bit-identical to the same utterance decoded as overlapping
+    chunks (a size-independent property: chunk halos cover the receptive field), and plans past
+    the 2^31-sample limit are refused with ValueError/RuntimeError, not mis-indexed."""
+    from parallelwavegan_amd import Engine, configs, streaming, synthetic
+
+    params = configs.generator_params("libritts_v1")
+    eng = Engine(params, cuda_device)
+    eng.load_state_dict(synthetic.make_state_dict(params, seed=11))
+    F = 60_000
+    mel = torch.from_numpy(synthetic.make_mel(F, 80, seed=12)).to(cuda_device)
+    noise = torch.from_numpy(synthetic.make_noise(F * 300, seed=13)).to(cuda_device)
+    with torch.no_grad():
+        y = eng.infer([mel], [noise])[0]
+        assert y.shape == (F * 300, 1)
+        assert bool(torch.isfinite(y).all())
+        yc = streaming.infer_chunked(eng, mel, noise, 7_000)
+    assert torch.equal(y, yc)
+    del y, yc
+    torch.cuda.empty_cache()
+    with pytest.raises((ValueError, RuntimeError, NotImplementedError)):
+        eng.plan([(1 << 31) // 300 + 1])
