@@ -98,7 +98,8 @@ PWG_API int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, 
  * PWG_CNET_OPT_FUSE_PAIRS (default 1, split-f16 mode): run "conv A -> t -> conv B" pairs whose
  * intermediate t has no other reader (HiFiGAN ResBlock steps, layers/residual_block.py:231-237)
  * as one kernel with t kept in LDS; bit-identical to the unfused ops. Applies to 32-channel
- * zero-padded pairs whose weights fit in LDS (HiFiGAN v1's last stage).
+ * (weights resident in LDS) and 64-channel (weights streamed) zero-padded pairs (HiFiGAN v1's
+ * last two stages).
  * PWG_CNET_OPT_PAIR_STEPS (default 16): 128-column tiles per fused-pair workgroup, for plans
  * created afterwards. */
 enum { PWG_CNET_OPT_SPLIT_F16 = 0, PWG_CNET_OPT_FUSE_PAIRS = 1, PWG_CNET_OPT_PAIR_STEPS = 2 };

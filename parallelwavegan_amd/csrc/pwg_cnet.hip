@@ -407,6 +407,9 @@ constexpr int PR_HALO = 16;
 constexpr int PR_MAX_XS = 128 + 2 * 64;        // x tile columns (stage-1 tap reach +-64 - PR_HALO)
 constexpr int PR_XQ = PR_MAX_XS * 8 / 256;     // 16-byte x quads per thread
 constexpr int PR_MAX_LDS = 160 * 1024;
+#ifndef PWG_PAIR_STREAM_C
+#define PWG_PAIR_STREAM_C 64  // channels of the streamed-weight pair kernel (0: off)
+#endif
 struct CnPairArgs {
   const float* x;
   const int* seg_x;
@@ -660,6 +663,234 @@ __global__ void __launch_bounds__(256) pwg_cnet_pair_kernel(const CnPairArgs a) 
   flush();
 }
 
+// C = 32 MT channels with the weights STREAMED (they do not fit in LDS next to the tiles, e.g.
+// HiFiGAN's 64-channel stage): same strip / x tile / h ring scheme as pwg_cnet_pair_kernel, the A
+// fragments of PR_SG chunks at a time staged in a double-buffered LDS area, the next group's
+// loaded into registers while the current group computes (across stage and step boundaries).
+// Dynamic LDS: [x tile: xs x HROW halves] [h ring: 2 x 128 x HROW] [A: 2 x PR_SG x MT x 2 KB].
+constexpr int PR_SG = 4;
+template <int MT>
+__global__ void __launch_bounds__(256) pwg_cnet_pair_stream_kernel(const CnPairArgs a) {
+  constexpr int C = 32 * MT;
+  constexpr int CS = C / 16;        // 16-channel chunks per tap
+  constexpr int HROW = 2 * C + 8;   // halves per LDS column: [hi C][lo C][16 B pad]
+  constexpr int AQ = PR_SG * MT * 128 / 256;  // 16-byte A quads per thread per group
+  constexpr int XQ = PR_MAX_XS * (C / 4) / 256;
+  extern __shared__ __attribute__((aligned(16))) unsigned char pr_smem[];
+  const int n1 = a.n1, n2 = a.n2;   // multiples of PR_SG (host check)
+  _Float16* s_x = reinterpret_cast<_Float16*>(pr_smem);
+  _Float16* s_h = s_x + (size_t)a.xs * HROW;
+  u32x4v* s_a = reinterpret_cast<u32x4v*>(s_h + 2 * 128 * HROW);  // [2][PR_SG][MT][2][64]
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int hh = lane >> 5;
+  const int cl = lane & 31;
+  const int2 st = a.strips[blockIdx.x];
+  const int u = st.x, base = st.y;
+  const int T = a.ncols[u];
+  const int nsteps = min(a.steps, (T - base + 127) / 128);
+  const int2 sx = *reinterpret_cast<const int2*>(a.seg_x + 2 * u);
+  const int sd_x = a.seg_y[2 * u];
+  const int sr_x = a.res ? a.seg_res[2 * u] : 0;
+
+  f32x4v rb1[MT][4], rb2[MT][4];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int j4 = 0; j4 < 4; ++j4) {
+      rb1[m][j4] = *reinterpret_cast<const f32x4v*>(a.b1 + 32 * m + 8 * j4 + 4 * hh);
+      rb2[m][j4] = *reinterpret_cast<const f32x4v*>(a.b2 + 32 * m + 8 * j4 + 4 * hh);
+    }
+  // A group (stage st, first chunk c0): PR_SG chunks x MT x 2 KB, contiguous in the packed image
+  u32x4v aq[AQ];
+  auto agload = [&](int stg, int c0) {
+    const u32x4v* g = reinterpret_cast<const u32x4v*>(stg == 0 ? a.w1 : a.w2) + (size_t)c0 * MT * 128;
+#pragma unroll
+    for (int i = 0; i < AQ; ++i) aq[i] = g[threadIdx.x + 256 * i];
+  };
+  auto agstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < AQ; ++i) s_a[(size_t)buf * PR_SG * MT * 128 + threadIdx.x + 256 * i] = aq[i];
+  };
+  f32x4v xq[XQ];
+  auto xfetch = [&](int s) {
+    const int x0 = base + 128 * s - PR_HALO + a.x_min_off;
+#pragma unroll
+    for (int i = 0; i < XQ; ++i) {
+      const int q = threadIdx.x + 256 * i;
+      int p = x0 + q / (C / 4);
+      p = p < 0 ? 0 : (p >= T ? T - 1 : p);
+      xq[i] = *reinterpret_cast<const f32x4v*>(a.x + (size_t)(sx.x + p) * a.ld_x + 4 * (q % (C / 4)));
+    }
+  };
+  auto xstore = [&](int s) {
+    const int x0 = base + 128 * s - PR_HALO + a.x_min_off;
+#pragma unroll
+    for (int i = 0; i < XQ; ++i) {
+      const int q = threadIdx.x + 256 * i;
+      if (q >= a.xs * (C / 4)) continue;
+      const int col = q / (C / 4), ch = 4 * (q % (C / 4));
+      const int p = x0 + col;
+      f32x4v v = xq[i];
+      if (a.slope1 != 1.f) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * a.slope1;
+      }
+      if (p < 0 || p >= T) v = f32x4v{0.f, 0.f, 0.f, 0.f};
+      f16x4v vh, vl;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        vh[e] = (_Float16)v[e];
+        vl[e] = (_Float16)(v[e] - (float)vh[e]);
+      }
+      _Float16* r = s_x + col * HROW + ch;
+      *reinterpret_cast<f16x4v*>(r) = vh;
+      *reinterpret_cast<f16x4v*>(r + C) = vl;
+    }
+  };
+  f32x16 acc[MT];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
+  };
+  // one chunk: A of group slot k from s_a[buf], B = 8 channels (hi, lo) of an LDS column row
+  auto chunk = [&](int buf, int k, const _Float16* brow) {
+    const u32x4v bh = *reinterpret_cast<const u32x4v*>(brow);
+    const u32x4v bl = *reinterpret_cast<const u32x4v*>(brow + C);
+    const u32x4v* sa = s_a + ((size_t)buf * PR_SG + k) * MT * 128 + lane;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const u32x4v ah = sa[(m * 2) * 64], al = sa[(m * 2 + 1) * 64];
+      acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, ah), __builtin_bit_cast(f16x8v, bh), acc[m], 0, 0, 0);
+      acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, ah), __builtin_bit_cast(f16x8v, bl), acc[m], 0, 0, 0);
+      acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, al), __builtin_bit_cast(f16x8v, bh), acc[m], 0, 0, 0);
+    }
+  };
+  f32x4v pend[MT][4];
+  float* pend_row = nullptr;
+  auto flush = [&]() {
+    if (pend_row) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int j4 = 0; j4 < 4; ++j4) *reinterpret_cast<f32x4v*>(pend_row + 32 * m + 8 * j4 + 4 * hh) = pend[m][j4];
+    }
+  };
+
+  int buf = 0;
+  agload(0, 0);
+  agstore(0);
+  xfetch(0);
+  xstore(0);
+  pr_barrier();
+  for (int s = 0; s <= nsteps; ++s) {
+    // ---------------- stage 1: h columns j of tile s
+    const int j = base + 128 * s - PR_HALO + 32 * wave + cl;
+    zero_acc();
+    for (int c0 = 0; c0 < n1; c0 += PR_SG) {
+      // next group: stage 1's, else stage 2's first (s >= 1) or the next step's stage 1 (s == 0)
+      if (c0 + PR_SG < n1) agload(0, c0 + PR_SG);
+      else agload(s >= 1 ? 1 : 0, 0);
+#pragma unroll
+      for (int k = 0; k < PR_SG; ++k) {
+        const int c = c0 + k;
+        const int row_off = a.off1 + (c / CS) * a.dil1;
+        chunk(buf, k, s_x + (32 * wave + cl + row_off - a.x_min_off) * HROW + 16 * (c % CS) + 8 * hh);
+      }
+      agstore(buf ^ 1);
+      pr_barrier();
+      buf ^= 1;
+    }
+    flush();
+    pend_row = nullptr;
+    if (s < nsteps) xfetch(s + 1);
+    {
+      _Float16* hrow = s_h + ((s & 1) * 128 + 32 * wave + cl) * HROW;
+      const bool inside = j >= 0 && j < T;
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int j4 = 0; j4 < 4; ++j4) {
+          const int row = 32 * m + 8 * j4 + 4 * hh;
+          f16x4v vh, vl;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float v = acc[m][4 * j4 + e] + rb1[m][j4][e];
+            if (a.slope2 != 1.f) v = v > 0.f ? v : v * a.slope2;
+            v = inside ? v : 0.f;
+            vh[e] = (_Float16)v;
+            vl[e] = (_Float16)(v - (float)vh[e]);
+          }
+          *reinterpret_cast<f16x4v*>(hrow + row) = vh;
+          *reinterpret_cast<f16x4v*>(hrow + C + row) = vl;
+        }
+    }
+    pr_barrier();  // h tile s visible; every wave is done with x tile s
+    if (s < nsteps) xstore(s + 1);  // visible after stage 2's first group barrier (or below)
+    if (s >= 1) {
+      // ---------------- stage 2: output columns q of tile s-1
+      const int q = base + 128 * (s - 1) + 32 * wave + cl;
+      const bool live = q < T;
+      const int qc = live ? q : 0;
+      float* yrow = a.y + (size_t)(sd_x + qc) * a.ld_y;
+      const float* rrow = a.res ? a.res + (size_t)(sr_x + qc) * a.ld_res : yrow;
+      f32x4v rv[MT][4], ov[MT][4];
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int j4 = 0; j4 < 4; ++j4) {
+          const int row = 32 * m + 8 * j4 + 4 * hh;
+          rv[m][j4] = *reinterpret_cast<const f32x4v*>(rrow + row);
+          ov[m][j4] = *reinterpret_cast<const f32x4v*>(yrow + row);
+        }
+      zero_acc();
+      for (int c0 = 0; c0 < n2; c0 += PR_SG) {
+        const bool last = c0 + PR_SG >= n2 && s == nsteps;
+        if (c0 + PR_SG < n2) agload(1, c0 + PR_SG);
+        else if (!last) agload(0, 0);
+#pragma unroll
+        for (int k = 0; k < PR_SG; ++k) {
+          const int c = c0 + k;
+          const int p = 32 * wave + cl + PR_HALO + a.off2 + (c / CS) * a.dil2;  // 0 .. 159
+          chunk(buf, k, s_h + ((p < 128 ? ((s - 1) & 1) : (s & 1)) * 128 + (p & 127)) * HROW + 16 * (c % CS) + 8 * hh);
+        }
+        if (!last) agstore(buf ^ 1);
+        pr_barrier();
+        buf ^= 1;
+      }
+      if (live) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+          for (int j4 = 0; j4 < 4; ++j4) {
+            f32x4v v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = acc[m][4 * j4 + e] + rb2[m][j4][e];
+            if (a.res) v += rv[m][j4];
+            if (a.accumulate) v = ov[m][j4] + v;
+            if (a.out_div != 1.f) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = v[e] / a.out_div;
+            }
+            if (a.post_act == PWG_ACT_LRELU) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * a.post_slope;
+            } else if (a.post_act == PWG_ACT_TANH) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = tanhf(v[e]);
+            }
+            pend[m][j4] = v;
+          }
+        pend_row = yrow;
+      }
+    }
+    pr_barrier();  // x tile s+1 visible; h slot (s+1) & 1 free
+  }
+  flush();
+}
+
 // Thin outputs (M <= 8: the last conv of a generator, 1 or 4 channels). A 32-row MFMA tile would
 // be >= 75 % zero rows, so one THREAD computes all M outputs of one column on the VALU: per K
 // chunk it loads its 16 input channels (pre-activation and edge mode as in the MFMA kernel) and
@@ -817,6 +1048,7 @@ struct OpPhase {          // one launch
       thin_span[2] = {0, 0};
   int pair_b = -1;        // phase index of the op this one fuses with (pwg_cnet_pair_kernel), -1 = none
   int pair_xmin = 0, pair_xs = 0, pair_lds = 0;  // its x tile offset / width and dynamic LDS bytes
+  bool pair_resident = true;  // weights resident (pwg_cnet_pair_kernel) or streamed (_stream_kernel)
 };
 
 }  // namespace
@@ -1087,19 +1319,25 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
     if (A.src[1].buf >= 0 || B.src[1].buf >= 0 || B.src[0].buf != A.dst) continue;
     if (A.res >= 0 || A.accumulate || A.out_div != 1.f || A.post_act != PWG_ACT_NONE) continue;
     if (A.src[0].pad_mode != PWG_PAD_ZERO || A.src[0].normalize || B.src[0].pad_mode != PWG_PAD_ZERO) continue;
-    if (C != 32 || A.src[0].channels != C || n->ld[A.src[0].buf] != C || B.out_channels != C ||
-        B.src[0].channels != C || n->ld[A.dst] != C)
+    // 32 channels: both convs' weights resident in LDS; 64: weights streamed in PR_SG-chunk groups
+    if ((C != 32 && C != PWG_PAIR_STREAM_C) || A.src[0].channels != C || n->ld[A.src[0].buf] != C ||
+        B.out_channels != C || B.src[0].channels != C || n->ld[A.dst] != C)
       continue;
-    if (pa.mt_total != 1 || pb.mt_total != 1 || pa.MT != 1 || pb.MT != 1) continue;
+    const int MT = C / 32, cs = C / 16;
+    const bool resident = C == 32;
+    if (pa.mt_total != MT || pb.mt_total != MT || pa.MT != MT || pb.MT != MT) continue;
     bool ok = true;
     int mn = 1 << 30, mx = -(1 << 30);
     for (const ChunkDesc& cd : pa.chunks) { mn = std::min(mn, cd.row_off); mx = std::max(mx, cd.row_off); }
     for (size_t c = 0; c < pa.chunks.size(); ++c)
-      ok = ok && pa.chunks[c].row_off == -A.src[0].pad + (int)(c >> 1) * A.src[0].dilation && pa.chunks[c].c0 == 16 * (int)(c & 1);
+      ok = ok && pa.chunks[c].row_off == -A.src[0].pad + (int)(c / cs) * A.src[0].dilation && pa.chunks[c].c0 == 16 * (int)(c % cs);
     for (size_t c = 0; c < pb.chunks.size(); ++c)
-      ok = ok && pb.chunks[c].row_off == -B.src[0].pad + (int)(c >> 1) * B.src[0].dilation && pb.chunks[c].c0 == 16 * (int)(c & 1);
+      ok = ok && pb.chunks[c].row_off == -B.src[0].pad + (int)(c / cs) * B.src[0].dilation && pb.chunks[c].c0 == 16 * (int)(c % cs);
+    if (!resident) ok = ok && pa.chunks.size() % PR_SG == 0 && pb.chunks.size() % PR_SG == 0;
     const int xs = 128 + mx - mn;
-    const long long lds = (long long)(pa.chunks.size() + pb.chunks.size()) * 2048 + (long long)(xs + 256) * (2 * C + 8) * 2;
+    const long long tiles = (long long)(xs + 256) * (2 * C + 8) * 2;
+    const long long lds = resident ? (long long)(pa.chunks.size() + pb.chunks.size()) * 2048 + tiles
+                                   : tiles + 2LL * PR_SG * MT * 2048;
     if (xs > PR_MAX_XS || lds > PR_MAX_LDS) continue;
     if (B.dst != n_bufs - 1 && n->ld[B.dst] != C) continue;
     ok = ok && n->ld[B.dst] % 4 == 0 && (B.res < 0 || n->ld[B.res] % 4 == 0);
@@ -1114,6 +1352,7 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
       n->phases[i].pair_xmin = mn;
       n->phases[i].pair_xs = xs;
       n->phases[i].pair_lds = (int)lds;
+      n->phases[i].pair_resident = resident;
     }
   }
   *out = n;  // device tables are uploaded by the first plan: packing needs no GPU
@@ -1383,12 +1622,18 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         a.x_min_off = ph.pair_xmin; a.xs = ph.pair_xs;
         a.off1 = -op.src[0].pad; a.dil1 = op.src[0].dilation; a.off2 = -opb.src[0].pad; a.dil2 = opb.src[0].dilation;
         if (!n->pair_attr_set) {
-          const hipError_t ea2 = hipFuncSetAttribute(reinterpret_cast<const void*>(pwg_cnet_pair_kernel),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, PR_MAX_LDS);
-          if (ea2 != hipSuccess) return hipf(ea2, "pair kernel LDS attribute");
+          for (const void* kf : {reinterpret_cast<const void*>(pwg_cnet_pair_kernel),
+                                 reinterpret_cast<const void*>(pwg_cnet_pair_stream_kernel<2>)}) {
+            const hipError_t ea2 = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, PR_MAX_LDS);
+            if (ea2 != hipSuccess) return hipf(ea2, "pair kernel LDS attribute");
+          }
           n->pair_attr_set = true;
         }
-        hipLaunchKernelGGL(pwg_cnet_pair_kernel, dim3((unsigned)p->n_strips[pi]), dim3(256), (size_t)ph.pair_lds, s, a);
+        const dim3 pgrid((unsigned)p->n_strips[pi]);
+        if (ph.pair_resident)
+          hipLaunchKernelGGL(pwg_cnet_pair_kernel, pgrid, dim3(256), (size_t)ph.pair_lds, s, a);
+        else
+          hipLaunchKernelGGL(pwg_cnet_pair_stream_kernel<2>, pgrid, dim3(256), (size_t)ph.pair_lds, s, a);
       }
     } else if (op.kind == PWG_CNET_PQMF) {
       CnPqmfArgs a;
