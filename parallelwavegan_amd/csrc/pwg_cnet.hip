@@ -47,6 +47,9 @@ constexpr int CN_MAX_CHUNKS = 4096;
 #define PWG_CNET_G 1  // 2 (two chunks per barrier) measured 9 % slower on HiFiGAN v1
 #endif
 constexpr int CN_G = PWG_CNET_G;   // 16-channel chunks staged per barrier
+#ifndef PWG_CNET_NT2_MT
+#define PWG_CNET_NT2_MT 0  // > 0: split-mode conv ops with MT >= this use 2 column tiles per wave (A/B)
+#endif
 #ifndef PWG_CNET_DEPTH2
 #define PWG_CNET_DEPTH2 0  // 1: loads two chunk groups ahead (A/B variant)
 #endif
@@ -409,6 +412,9 @@ constexpr int PR_XQ = PR_MAX_XS * 8 / 256;     // 16-byte x quads per thread
 constexpr int PR_MAX_LDS = 160 * 1024;
 #ifndef PWG_PAIR_STREAM_C
 #define PWG_PAIR_STREAM_C 64  // channels of the streamed-weight pair kernel (0: off)
+#endif
+#ifndef PWG_PAIR_RESIDENT32
+#define PWG_PAIR_RESIDENT32 1  // 0: 32-channel pairs use the streamed kernel too (A/B)
 #endif
 struct CnPairArgs {
   const float* x;
@@ -1254,6 +1260,7 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
       OpPhase ph;
       ph.op = oi; ph.phase = r; ph.MT = MT; ph.mt_total = mt_total;
       ph.NT = 1;  // NT 2/4 for thin row tiles measured SLOWER (fewer workgroups in flight)
+      if (PWG_CNET_NT2_MT > 0 && MT >= PWG_CNET_NT2_MT && op.kind == PWG_CNET_CONV) ph.NT = 2;  // A/B
       ph.ostride = op.kind == PWG_CNET_CONVT ? op.stride : 1;
       ph.ophase = r;
       if (op.kind == PWG_CNET_CONVT) {
@@ -1324,7 +1331,7 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
         B.out_channels != C || B.src[0].channels != C || n->ld[A.dst] != C)
       continue;
     const int MT = C / 32, cs = C / 16;
-    const bool resident = C == 32;
+    const bool resident = C == 32 && PWG_PAIR_RESIDENT32;
     if (pa.mt_total != MT || pb.mt_total != MT || pa.MT != MT || pb.MT != MT) continue;
     bool ok = true;
     int mn = 1 << 30, mx = -(1 << 30);
@@ -1623,6 +1630,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         a.off1 = -op.src[0].pad; a.dil1 = op.src[0].dilation; a.off2 = -opb.src[0].pad; a.dil2 = opb.src[0].dilation;
         if (!n->pair_attr_set) {
           for (const void* kf : {reinterpret_cast<const void*>(pwg_cnet_pair_kernel),
+                                 reinterpret_cast<const void*>(pwg_cnet_pair_stream_kernel<1>),
                                  reinterpret_cast<const void*>(pwg_cnet_pair_stream_kernel<2>)}) {
             const hipError_t ea2 = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, PR_MAX_LDS);
             if (ea2 != hipSuccess) return hipf(ea2, "pair kernel LDS attribute");
@@ -1632,6 +1640,8 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         const dim3 pgrid((unsigned)p->n_strips[pi]);
         if (ph.pair_resident)
           hipLaunchKernelGGL(pwg_cnet_pair_kernel, pgrid, dim3(256), (size_t)ph.pair_lds, s, a);
+        else if (ph.mt_total == 1)
+          hipLaunchKernelGGL(pwg_cnet_pair_stream_kernel<1>, pgrid, dim3(256), (size_t)ph.pair_lds, s, a);
         else
           hipLaunchKernelGGL(pwg_cnet_pair_stream_kernel<2>, pgrid, dim3(256), (size_t)ph.pair_lds, s, a);
       }
@@ -1679,14 +1689,20 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
           case 1: hipLaunchKernelGGL((pwg_cnet_conv_kernel<1, 1, CN_G, true>), grid, block, 0, s, a); break;
           case 2: hipLaunchKernelGGL((pwg_cnet_conv_kernel<2, 1, CN_G, true>), grid, block, 0, s, a); break;
           case 3: hipLaunchKernelGGL((pwg_cnet_conv_kernel<3, 1, CN_G, true>), grid, block, 0, s, a); break;
-          default: hipLaunchKernelGGL((pwg_cnet_conv_kernel<4, 1, CN_G, true>), grid, block, 0, s, a); break;
+          default:
+            if (ph.NT == 2) hipLaunchKernelGGL((pwg_cnet_conv_kernel<4, 2, CN_G, true>), grid, block, 0, s, a);
+            else hipLaunchKernelGGL((pwg_cnet_conv_kernel<4, 1, CN_G, true>), grid, block, 0, s, a);
+            break;
         }
       } else {
         switch (ph.MT) {
           case 1: hipLaunchKernelGGL((pwg_cnet_conv_kernel<1, 1, CN_G>), grid, block, 0, s, a); break;
           case 2: hipLaunchKernelGGL((pwg_cnet_conv_kernel<2, 1, CN_G>), grid, block, 0, s, a); break;
           case 3: hipLaunchKernelGGL((pwg_cnet_conv_kernel<3, 1, CN_G>), grid, block, 0, s, a); break;
-          default: hipLaunchKernelGGL((pwg_cnet_conv_kernel<4, 1, CN_G>), grid, block, 0, s, a); break;
+          default:
+            if (ph.NT == 2) hipLaunchKernelGGL((pwg_cnet_conv_kernel<4, 2, CN_G>), grid, block, 0, s, a);
+            else hipLaunchKernelGGL((pwg_cnet_conv_kernel<4, 1, CN_G>), grid, block, 0, s, a);
+            break;
         }
       }
     }
