@@ -949,7 +949,7 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
   const bool split = h->layer_kernel == 2 || h->layer_kernel == 3;
   const bool split16 = h->layer_kernel == 3;
   pa.c1 = c1; pa.waux = packed + h->off_waux; pa.d = dproj; pa.F_total = p->F_total; pa.A = h->A; pa.GR = h->GR;
-  pa.split = split ? 1 : 0;
+  pa.split = split16 ? 2 : split ? 1 : 0;
   pa.split_scale_a = (float)SPLIT_GATE_SCALE_TANH;
   pa.split_scale_b = (float)SPLIT_GATE_SCALE_SIGM;
   e = timed(PWG_KERNEL_UPSAMPLE, [&] { return launch_aux_proj(pa, h->L, s); });

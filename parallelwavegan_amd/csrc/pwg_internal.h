@@ -68,7 +68,8 @@ struct AuxProjArgs {
   long long F_total;
   int A, GR;
   int split;             // 1: store (hi | lo << 16) fp16 pairs for the split-f16 layer kernel,
-                         // rows [0, GR/2) scaled by split_scale_a, the rest by split_scale_b
+                         // rows [0, GR/2) scaled by split_scale_a, the rest by split_scale_b;
+                         // 2: the same in the split16 row order (row 16m + c at c * 8 + m)
   float split_scale_a, split_scale_b;
 };
 // Pre-scaling of the split kernel's gate rows (pwg_split.hip gate()): tanh rows by -2 log2(e),

@@ -190,6 +190,38 @@ __global__ void __launch_bounds__(256) pwg_aux_proj_kernel(const AuxProjArgs a) 
     for (int m = 0; m < MT; ++m)
       acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(w[(s * MT + m) * 64], b, acc[m], 0, 0, 0);
   }
+  if constexpr (GR == 128) if (a.split == 2) {
+    // split16 layout: row r = 16 m16 + c16 of a frame at dword c16 * 8 + m16, so a layer-kernel
+    // lane (c16) reads its 8 m-tiles' rows as two 16-byte loads. Transposed through LDS (row
+    // stride 129 dwords: conflict-free column writes), then stored as whole 512-byte frame rows.
+    __shared__ unsigned s_d[4][32][129];
+    typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int j4 = 0; j4 < 4; ++j4) {
+        const float sc = 32 * m + 8 * j4 < GR / 2 ? a.split_scale_a : a.split_scale_b;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 32 * m + 8 * j4 + 4 * hh + i;
+          const float x = acc[m][4 * j4 + i] * sc;
+          const _Float16 hi = (_Float16)x;
+          s_d[wave][cl][(r & 15) * 8 + (r >> 4)] = __builtin_bit_cast(unsigned, f16x2{hi, (_Float16)(x - (float)hi)});
+        }
+      }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes done (wave-private rows)
+    __builtin_amdgcn_wave_barrier();
+    const long long f0 = (long long)blockIdx.x * 128 + wave * 32;
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int k = it * 64 + lane, fr = k >> 5, ch = k & 31;
+      if (f0 + fr >= a.F_total) continue;
+      const unsigned* src = &s_d[wave][fr][4 * ch];
+      *reinterpret_cast<u32x4*>(a.d + ((size_t)l * a.F_total + f0 + fr) * GR + 4 * ch) = u32x4{src[0], src[1], src[2], src[3]};
+    }
+    return;
+  }
   if (f >= a.F_total) return;
   float* d = a.d + ((size_t)l * a.F_total + f) * GR;
 #pragma unroll

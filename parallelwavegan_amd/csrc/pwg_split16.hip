@@ -308,12 +308,18 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
       for (int j = 0; j < 2; ++j) {
         const int f = fw0 + 2 * g + j;
         const int fc = f < 0 ? 0 : (f >= bd.frames ? bd.frames - 1 : f);  // weight 0 there
-        const unsigned* drow = a.d + (size_t)(bd.frame_base + fc) * 128 + c;
-#pragma unroll
+        // D row (frame) in the split16 layout [c 16][m 8] (pwg_aux_proj_kernel, split == 2)
+        const u32x4* drow = reinterpret_cast<const u32x4*>(a.d + (size_t)(bd.frame_base + fc) * 128 + 8 * c);
 #if PWG_SPLIT16_DIAG_NOD  // diagnostic: no D loads (wrong results)
+#pragma unroll
         for (int m = 0; m < 8; ++m) dv[j][m] = (unsigned)(fc + m);
 #else
-        for (int m = 0; m < 8; ++m) dv[j][m] = drow[16 * m];
+        const u32x4 d0 = drow[0], d1 = drow[1];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          dv[j][m] = d0[m];
+          dv[j][m + 4] = d1[m];
+        }
 #endif
       }
     };
