@@ -155,7 +155,9 @@ enum {
   PWG_OPT_LAYER_KERNEL = 0,   /* 0: persistent fp32 MFMA, weights resident in LDS (default for shapes
                                     the split kernel does not cover); 1: tiled fp32; 2: persistent
                                     split-f16 (fp32 operands as fp16 hi+lo pairs, 3 f16 MFMAs per
-                                    product; default for R = S = 64, gate 128, kernel 3) */
+                                    product) on v_mfma_f32_32x32x16_f16; 3: the same on
+                                    v_mfma_f32_16x16x32_f16 (default for R = S = 64, gate 128,
+                                    kernel 3) */
   PWG_OPT_WAVES_PER_WG = 1,   /* persistent kernel: waves per workgroup (1..8, default 8) */
   PWG_OPT_WG_PER_CU = 2,      /* persistent kernel: workgroups per CU in the grid (default 1) */
   PWG_OPT_FUSE_FIRST_CONV = 3 /* split16 layer kernel: first_conv evaluated inside layer 0 from the
