@@ -413,6 +413,9 @@ constexpr int PR_MAX_LDS = 160 * 1024;
 #ifndef PWG_PAIR_STREAM_C
 #define PWG_PAIR_STREAM_C 64  // channels of the streamed-weight pair kernel (0: off)
 #endif
+#ifndef PWG_PAIR_STREAM128
+#define PWG_PAIR_STREAM128 0  // 1: 128-channel pairs on the streamed kernel, 64-column steps (A/B: slower)
+#endif
 #ifndef PWG_PAIR_RESIDENT32
 #define PWG_PAIR_RESIDENT32 1  // 0: 32-channel pairs use the streamed kernel too (A/B)
 #endif
@@ -674,40 +677,47 @@ __global__ void __launch_bounds__(256) pwg_cnet_pair_kernel(const CnPairArgs a) 
 // fragments of PR_SG chunks at a time staged in a double-buffered LDS area, the next group's
 // loaded into registers while the current group computes (across stage and step boundaries).
 // Dynamic LDS: [x tile: xs x HROW halves] [h ring: 2 x 128 x HROW] [A: 2 x PR_SG x MT x 2 KB].
+// WN waves along time: a step covers STEP = 32 WN columns; wave w owns column tile w % WN and the
+// MTW = MT WN / 4 m-tiles of group w / WN (C = 64: WN 4, all 2 m-tiles per wave, 128-column
+// steps; C = 128: WN 2, 2 of the 4 m-tiles per wave, 64-column steps so the tiles fit in LDS).
 constexpr int PR_SG = 4;
-template <int MT>
+template <int MT, int WN, int SG>
 __global__ void __launch_bounds__(256) pwg_cnet_pair_stream_kernel(const CnPairArgs a) {
   constexpr int C = 32 * MT;
   constexpr int CS = C / 16;        // 16-channel chunks per tap
   constexpr int HROW = 2 * C + 8;   // halves per LDS column: [hi C][lo C][16 B pad]
-  constexpr int AQ = PR_SG * MT * 128 / 256;  // 16-byte A quads per thread per group
-  constexpr int XQ = PR_MAX_XS * (C / 4) / 256;
+  constexpr int STEP = 32 * WN;     // columns per step
+  constexpr int MTW = MT * WN / 4;  // m-tiles per wave
+  constexpr int AQ = SG * MT * 128 / 256;  // 16-byte A quads per thread per group
+  constexpr int XQ = (STEP + PR_MAX_XS - 128) * (C / 4) / 256;  // x tile <= STEP + 128 columns
   extern __shared__ __attribute__((aligned(16))) unsigned char pr_smem[];
-  const int n1 = a.n1, n2 = a.n2;   // multiples of PR_SG (host check)
+  const int n1 = a.n1, n2 = a.n2;   // multiples of SG (host check)
   _Float16* s_x = reinterpret_cast<_Float16*>(pr_smem);
   _Float16* s_h = s_x + (size_t)a.xs * HROW;
-  u32x4v* s_a = reinterpret_cast<u32x4v*>(s_h + 2 * 128 * HROW);  // [2][PR_SG][MT][2][64]
+  u32x4v* s_a = reinterpret_cast<u32x4v*>(s_h + 2 * STEP * HROW);  // [2][SG][MT][2][64]
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int hh = lane >> 5;
   const int cl = lane & 31;
+  const int nt = wave % WN;          // column tile
+  const int m0 = (wave / WN) * MTW;  // first m-tile
   const int2 st = a.strips[blockIdx.x];
   const int u = st.x, base = st.y;
   const int T = a.ncols[u];
-  const int nsteps = min(a.steps, (T - base + 127) / 128);
+  const int nsteps = min(a.steps, (T - base + STEP - 1) / STEP);
   const int2 sx = *reinterpret_cast<const int2*>(a.seg_x + 2 * u);
   const int sd_x = a.seg_y[2 * u];
   const int sr_x = a.res ? a.seg_res[2 * u] : 0;
 
-  f32x4v rb1[MT][4], rb2[MT][4];
+  f32x4v rb1[MTW][4], rb2[MTW][4];
 #pragma unroll
-  for (int m = 0; m < MT; ++m)
+  for (int m = 0; m < MTW; ++m)
 #pragma unroll
     for (int j4 = 0; j4 < 4; ++j4) {
-      rb1[m][j4] = *reinterpret_cast<const f32x4v*>(a.b1 + 32 * m + 8 * j4 + 4 * hh);
-      rb2[m][j4] = *reinterpret_cast<const f32x4v*>(a.b2 + 32 * m + 8 * j4 + 4 * hh);
+      rb1[m][j4] = *reinterpret_cast<const f32x4v*>(a.b1 + 32 * (m0 + m) + 8 * j4 + 4 * hh);
+      rb2[m][j4] = *reinterpret_cast<const f32x4v*>(a.b2 + 32 * (m0 + m) + 8 * j4 + 4 * hh);
     }
-  // A group (stage st, first chunk c0): PR_SG chunks x MT x 2 KB, contiguous in the packed image
+  // A group (stage st, first chunk c0): SG chunks x MT x 2 KB, contiguous in the packed image
   u32x4v aq[AQ];
   auto agload = [&](int stg, int c0) {
     const u32x4v* g = reinterpret_cast<const u32x4v*>(stg == 0 ? a.w1 : a.w2) + (size_t)c0 * MT * 128;
@@ -716,11 +726,11 @@ __global__ void __launch_bounds__(256) pwg_cnet_pair_stream_kernel(const CnPairA
   };
   auto agstore = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < AQ; ++i) s_a[(size_t)buf * PR_SG * MT * 128 + threadIdx.x + 256 * i] = aq[i];
+    for (int i = 0; i < AQ; ++i) s_a[(size_t)buf * SG * MT * 128 + threadIdx.x + 256 * i] = aq[i];
   };
   f32x4v xq[XQ];
   auto xfetch = [&](int s) {
-    const int x0 = base + 128 * s - PR_HALO + a.x_min_off;
+    const int x0 = base + STEP * s - PR_HALO + a.x_min_off;
 #pragma unroll
     for (int i = 0; i < XQ; ++i) {
       const int q = threadIdx.x + 256 * i;
@@ -730,7 +740,7 @@ __global__ void __launch_bounds__(256) pwg_cnet_pair_stream_kernel(const CnPairA
     }
   };
   auto xstore = [&](int s) {
-    const int x0 = base + 128 * s - PR_HALO + a.x_min_off;
+    const int x0 = base + STEP * s - PR_HALO + a.x_min_off;
 #pragma unroll
     for (int i = 0; i < XQ; ++i) {
       const int q = threadIdx.x + 256 * i;
@@ -754,10 +764,10 @@ __global__ void __launch_bounds__(256) pwg_cnet_pair_stream_kernel(const CnPairA
       *reinterpret_cast<f16x4v*>(r + C) = vl;
     }
   };
-  f32x16 acc[MT];
+  f32x16 acc[MTW];
   auto zero_acc = [&]() {
 #pragma unroll
-    for (int m = 0; m < MT; ++m)
+    for (int m = 0; m < MTW; ++m)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
   };
@@ -765,23 +775,23 @@ __global__ void __launch_bounds__(256) pwg_cnet_pair_stream_kernel(const CnPairA
   auto chunk = [&](int buf, int k, const _Float16* brow) {
     const u32x4v bh = *reinterpret_cast<const u32x4v*>(brow);
     const u32x4v bl = *reinterpret_cast<const u32x4v*>(brow + C);
-    const u32x4v* sa = s_a + ((size_t)buf * PR_SG + k) * MT * 128 + lane;
+    const u32x4v* sa = s_a + ((size_t)buf * SG + k) * MT * 128 + lane;
 #pragma unroll
-    for (int m = 0; m < MT; ++m) {
-      const u32x4v ah = sa[(m * 2) * 64], al = sa[(m * 2 + 1) * 64];
+    for (int m = 0; m < MTW; ++m) {
+      const u32x4v ah = sa[((m0 + m) * 2) * 64], al = sa[((m0 + m) * 2 + 1) * 64];
       acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, ah), __builtin_bit_cast(f16x8v, bh), acc[m], 0, 0, 0);
       acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, ah), __builtin_bit_cast(f16x8v, bl), acc[m], 0, 0, 0);
       acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, al), __builtin_bit_cast(f16x8v, bh), acc[m], 0, 0, 0);
     }
   };
-  f32x4v pend[MT][4];
+  f32x4v pend[MTW][4];
   float* pend_row = nullptr;
   auto flush = [&]() {
     if (pend_row) {
 #pragma unroll
-      for (int m = 0; m < MT; ++m)
+      for (int m = 0; m < MTW; ++m)
 #pragma unroll
-        for (int j4 = 0; j4 < 4; ++j4) *reinterpret_cast<f32x4v*>(pend_row + 32 * m + 8 * j4 + 4 * hh) = pend[m][j4];
+        for (int j4 = 0; j4 < 4; ++j4) *reinterpret_cast<f32x4v*>(pend_row + 32 * (m0 + m) + 8 * j4 + 4 * hh) = pend[m][j4];
     }
   };
 
@@ -793,17 +803,17 @@ __global__ void __launch_bounds__(256) pwg_cnet_pair_stream_kernel(const CnPairA
   pr_barrier();
   for (int s = 0; s <= nsteps; ++s) {
     // ---------------- stage 1: h columns j of tile s
-    const int j = base + 128 * s - PR_HALO + 32 * wave + cl;
+    const int j = base + STEP * s - PR_HALO + 32 * nt + cl;
     zero_acc();
-    for (int c0 = 0; c0 < n1; c0 += PR_SG) {
+    for (int c0 = 0; c0 < n1; c0 += SG) {
       // next group: stage 1's, else stage 2's first (s >= 1) or the next step's stage 1 (s == 0)
-      if (c0 + PR_SG < n1) agload(0, c0 + PR_SG);
+      if (c0 + SG < n1) agload(0, c0 + SG);
       else agload(s >= 1 ? 1 : 0, 0);
 #pragma unroll
-      for (int k = 0; k < PR_SG; ++k) {
+      for (int k = 0; k < SG; ++k) {
         const int c = c0 + k;
         const int row_off = a.off1 + (c / CS) * a.dil1;
-        chunk(buf, k, s_x + (32 * wave + cl + row_off - a.x_min_off) * HROW + 16 * (c % CS) + 8 * hh);
+        chunk(buf, k, s_x + (32 * nt + cl + row_off - a.x_min_off) * HROW + 16 * (c % CS) + 8 * hh);
       }
       agstore(buf ^ 1);
       pr_barrier();
@@ -813,13 +823,13 @@ __global__ void __launch_bounds__(256) pwg_cnet_pair_stream_kernel(const CnPairA
     pend_row = nullptr;
     if (s < nsteps) xfetch(s + 1);
     {
-      _Float16* hrow = s_h + ((s & 1) * 128 + 32 * wave + cl) * HROW;
+      _Float16* hrow = s_h + ((s & 1) * STEP + 32 * nt + cl) * HROW;
       const bool inside = j >= 0 && j < T;
 #pragma unroll
-      for (int m = 0; m < MT; ++m)
+      for (int m = 0; m < MTW; ++m)
 #pragma unroll
         for (int j4 = 0; j4 < 4; ++j4) {
-          const int row = 32 * m + 8 * j4 + 4 * hh;
+          const int row = 32 * (m0 + m) + 8 * j4 + 4 * hh;
           f16x4v vh, vl;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -837,30 +847,30 @@ __global__ void __launch_bounds__(256) pwg_cnet_pair_stream_kernel(const CnPairA
     if (s < nsteps) xstore(s + 1);  // visible after stage 2's first group barrier (or below)
     if (s >= 1) {
       // ---------------- stage 2: output columns q of tile s-1
-      const int q = base + 128 * (s - 1) + 32 * wave + cl;
+      const int q = base + STEP * (s - 1) + 32 * nt + cl;
       const bool live = q < T;
       const int qc = live ? q : 0;
       float* yrow = a.y + (size_t)(sd_x + qc) * a.ld_y;
       const float* rrow = a.res ? a.res + (size_t)(sr_x + qc) * a.ld_res : yrow;
-      f32x4v rv[MT][4], ov[MT][4];
+      f32x4v rv[MTW][4], ov[MTW][4];
 #pragma unroll
-      for (int m = 0; m < MT; ++m)
+      for (int m = 0; m < MTW; ++m)
 #pragma unroll
         for (int j4 = 0; j4 < 4; ++j4) {
-          const int row = 32 * m + 8 * j4 + 4 * hh;
+          const int row = 32 * (m0 + m) + 8 * j4 + 4 * hh;
           rv[m][j4] = *reinterpret_cast<const f32x4v*>(rrow + row);
           ov[m][j4] = *reinterpret_cast<const f32x4v*>(yrow + row);
         }
       zero_acc();
-      for (int c0 = 0; c0 < n2; c0 += PR_SG) {
-        const bool last = c0 + PR_SG >= n2 && s == nsteps;
-        if (c0 + PR_SG < n2) agload(1, c0 + PR_SG);
+      for (int c0 = 0; c0 < n2; c0 += SG) {
+        const bool last = c0 + SG >= n2 && s == nsteps;
+        if (c0 + SG < n2) agload(1, c0 + SG);
         else if (!last) agload(0, 0);
 #pragma unroll
-        for (int k = 0; k < PR_SG; ++k) {
+        for (int k = 0; k < SG; ++k) {
           const int c = c0 + k;
-          const int p = 32 * wave + cl + PR_HALO + a.off2 + (c / CS) * a.dil2;  // 0 .. 159
-          chunk(buf, k, s_h + ((p < 128 ? ((s - 1) & 1) : (s & 1)) * 128 + (p & 127)) * HROW + 16 * (c % CS) + 8 * hh);
+          const int p = 32 * nt + cl + PR_HALO + a.off2 + (c / CS) * a.dil2;  // 0 .. STEP + 31
+          chunk(buf, k, s_h + ((p < STEP ? ((s - 1) & 1) : (s & 1)) * STEP + (p < STEP ? p : p - STEP)) * HROW + 16 * (c % CS) + 8 * hh);
         }
         if (!last) agstore(buf ^ 1);
         pr_barrier();
@@ -868,7 +878,7 @@ __global__ void __launch_bounds__(256) pwg_cnet_pair_stream_kernel(const CnPairA
       }
       if (live) {
 #pragma unroll
-        for (int m = 0; m < MT; ++m)
+        for (int m = 0; m < MTW; ++m)
 #pragma unroll
           for (int j4 = 0; j4 < 4; ++j4) {
             f32x4v v;
@@ -1055,6 +1065,7 @@ struct OpPhase {          // one launch
   int pair_b = -1;        // phase index of the op this one fuses with (pwg_cnet_pair_kernel), -1 = none
   int pair_xmin = 0, pair_xs = 0, pair_lds = 0;  // its x tile offset / width and dynamic LDS bytes
   bool pair_resident = true;  // weights resident (pwg_cnet_pair_kernel) or streamed (_stream_kernel)
+  int pair_step = 128;        // columns per kernel step (streamed 128-channel pairs: 64)
 };
 
 }  // namespace
@@ -1327,11 +1338,12 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
     if (A.res >= 0 || A.accumulate || A.out_div != 1.f || A.post_act != PWG_ACT_NONE) continue;
     if (A.src[0].pad_mode != PWG_PAD_ZERO || A.src[0].normalize || B.src[0].pad_mode != PWG_PAD_ZERO) continue;
     // 32 channels: both convs' weights resident in LDS; 64: weights streamed in PR_SG-chunk groups
-    if ((C != 32 && C != PWG_PAIR_STREAM_C) || A.src[0].channels != C || n->ld[A.src[0].buf] != C ||
-        B.out_channels != C || B.src[0].channels != C || n->ld[A.dst] != C)
+    if ((C != 32 && C != PWG_PAIR_STREAM_C && !(C == 128 && PWG_PAIR_STREAM128)) || A.src[0].channels != C ||
+        n->ld[A.src[0].buf] != C || B.out_channels != C || B.src[0].channels != C || n->ld[A.dst] != C)
       continue;
     const int MT = C / 32, cs = C / 16;
     const bool resident = C == 32 && PWG_PAIR_RESIDENT32;
+    const int step = C == 128 ? 64 : 128, sg = C == 128 ? 2 : PR_SG;  // streamed kernel geometry
     if (pa.mt_total != MT || pb.mt_total != MT || pa.MT != MT || pb.MT != MT) continue;
     bool ok = true;
     int mn = 1 << 30, mx = -(1 << 30);
@@ -1340,12 +1352,12 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
       ok = ok && pa.chunks[c].row_off == -A.src[0].pad + (int)(c / cs) * A.src[0].dilation && pa.chunks[c].c0 == 16 * (int)(c % cs);
     for (size_t c = 0; c < pb.chunks.size(); ++c)
       ok = ok && pb.chunks[c].row_off == -B.src[0].pad + (int)(c / cs) * B.src[0].dilation && pb.chunks[c].c0 == 16 * (int)(c % cs);
-    if (!resident) ok = ok && pa.chunks.size() % PR_SG == 0 && pb.chunks.size() % PR_SG == 0;
-    const int xs = 128 + mx - mn;
-    const long long tiles = (long long)(xs + 256) * (2 * C + 8) * 2;
+    if (!resident) ok = ok && pa.chunks.size() % sg == 0 && pb.chunks.size() % sg == 0;
+    const int xs = step + mx - mn;
+    const long long tiles = (long long)(xs + 2 * step) * (2 * C + 8) * 2;
     const long long lds = resident ? (long long)(pa.chunks.size() + pb.chunks.size()) * 2048 + tiles
-                                   : tiles + 2LL * PR_SG * MT * 2048;
-    if (xs > PR_MAX_XS || lds > PR_MAX_LDS) continue;
+                                   : tiles + 2LL * sg * MT * 2048;
+    if (xs - step > PR_MAX_XS - 128 || lds > PR_MAX_LDS) continue;
     if (B.dst != n_bufs - 1 && n->ld[B.dst] != C) continue;
     ok = ok && n->ld[B.dst] % 4 == 0 && (B.res < 0 || n->ld[B.res] % 4 == 0);
     for (const ChunkDesc& cd : pb.chunks) ok = ok && cd.row_off >= -PR_HALO && cd.row_off <= PR_HALO;
@@ -1360,6 +1372,7 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
       n->phases[i].pair_xs = xs;
       n->phases[i].pair_lds = (int)lds;
       n->phases[i].pair_resident = resident;
+      n->phases[i].pair_step = step;
     }
   }
   *out = n;  // device tables are uploaded by the first plan: packing needs no GPU
@@ -1625,13 +1638,14 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         a.ld_res = opb.res >= 0 ? n->ld[opb.res] : 0;
         a.y = bufs[opb.dst]; a.seg_y = seg_of(opb.dst); a.ld_y = n->ld[opb.dst];
         a.accumulate = opb.accumulate; a.out_div = opb.out_div; a.post_act = opb.post_act; a.post_slope = opb.post_slope;
-        a.strips = p->d_strips[pi]; a.ncols = p->d_ncols[pi]; a.steps = p->pair_steps;
+        a.strips = p->d_strips[pi]; a.ncols = p->d_ncols[pi]; a.steps = p->pair_steps * 128 / ph.pair_step;
         a.x_min_off = ph.pair_xmin; a.xs = ph.pair_xs;
         a.off1 = -op.src[0].pad; a.dil1 = op.src[0].dilation; a.off2 = -opb.src[0].pad; a.dil2 = opb.src[0].dilation;
         if (!n->pair_attr_set) {
           for (const void* kf : {reinterpret_cast<const void*>(pwg_cnet_pair_kernel),
-                                 reinterpret_cast<const void*>(pwg_cnet_pair_stream_kernel<1>),
-                                 reinterpret_cast<const void*>(pwg_cnet_pair_stream_kernel<2>)}) {
+                                 reinterpret_cast<const void*>(pwg_cnet_pair_stream_kernel<1, 4, PR_SG>),
+                                 reinterpret_cast<const void*>(pwg_cnet_pair_stream_kernel<2, 4, PR_SG>),
+                                 reinterpret_cast<const void*>(pwg_cnet_pair_stream_kernel<4, 2, 2>)}) {
             const hipError_t ea2 = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, PR_MAX_LDS);
             if (ea2 != hipSuccess) return hipf(ea2, "pair kernel LDS attribute");
           }
@@ -1641,9 +1655,11 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         if (ph.pair_resident)
           hipLaunchKernelGGL(pwg_cnet_pair_kernel, pgrid, dim3(256), (size_t)ph.pair_lds, s, a);
         else if (ph.mt_total == 1)
-          hipLaunchKernelGGL(pwg_cnet_pair_stream_kernel<1>, pgrid, dim3(256), (size_t)ph.pair_lds, s, a);
+          hipLaunchKernelGGL((pwg_cnet_pair_stream_kernel<1, 4, PR_SG>), pgrid, dim3(256), (size_t)ph.pair_lds, s, a);
+        else if (ph.mt_total == 2)
+          hipLaunchKernelGGL((pwg_cnet_pair_stream_kernel<2, 4, PR_SG>), pgrid, dim3(256), (size_t)ph.pair_lds, s, a);
         else
-          hipLaunchKernelGGL(pwg_cnet_pair_stream_kernel<2>, pgrid, dim3(256), (size_t)ph.pair_lds, s, a);
+          hipLaunchKernelGGL((pwg_cnet_pair_stream_kernel<4, 2, 2>), pgrid, dim3(256), (size_t)ph.pair_lds, s, a);
       }
     } else if (op.kind == PWG_CNET_PQMF) {
       CnPqmfArgs a;

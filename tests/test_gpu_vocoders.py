@@ -136,7 +136,7 @@ def test_fused_conv_pairs_bitwise_equal_to_unfused(steps, built_lib, cuda_device
         t = eng.collect_timing()
         eng.set_timing(False)
     # the 64- (streamed weights) and 32-channel (resident weights) stages' 3 ResBlocks x 3
-    # (conv1, conv2) pairs run fused
+    # (conv1, conv2) pairs run fused (128 channels: PWG_PAIR_STREAM128, off)
     assert sum(1 for _, _, n in t if n == 0) == 18
     for a, b in zip(got, ref):
         np.testing.assert_array_equal(a, b)
