@@ -8,8 +8,12 @@ mel frames (1-15 s of audio each). One "step" = one generator forward over the w
 (every kernel of the hot path), inputs resident in HBM before the timed region.
 
 Multi-GPU: one process per GPU (torch.distributed.run), utterances are independent so the data
-path has no collective; rank 0's packed weights are RCCL-broadcast once at start-up.
-Weak scaling: every rank runs the same per-GPU batch shape.
+path has no collective; rank 0's packed weights are RCCL-broadcast once at start-up through the
+C-ABI (pwg_broadcast_weights). Default: weak scaling, every rank runs the same per-GPU batch shape.
+--strong: SURVEY.md sec 8(d)(5), the fixed 512-utterance list LPT-sharded over the ranks.
+
+At N=1 the line also carries the reference's own call pattern (B=1 inference() latency rows, LJ v1,
+bin/decode.py:236-268) and a CPU baseline on a bounded sample.
 
 Prints ONE JSON line (rank 0) with the contract fields plus "roofline" and "cpu_baseline".
 """
@@ -29,7 +33,8 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 from parallelwavegan_amd import Engine, _lib, configs, synthetic  # noqa: E402
-from parallelwavegan_amd.sharding import broadcast_packed_weights, max_over_ranks  # noqa: E402
+from parallelwavegan_amd.sharding import (  # noqa: E402
+    broadcast_packed_weights, broadcast_weights_rccl, lpt_partition, max_over_ranks, shard_loads)
 
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: Peak FP32 (matrix) = vector, spec
 HBM_PEAK_GBS = 8000.0
@@ -111,30 +116,70 @@ def dist_setup(n_gpus):
     return 0, 1, torch.device("cuda", 0)
 
 
-def cpu_baseline(params, sd, lengths, H, seconds_budget):
-    """Time the torch-CPU restatement of the reference (oracle/pwg_torch_cpu.py, same aten op
-    sequence as the reference) on a bounded sample of the same workload, B=1 per utterance like
-    bin/decode.py. Returns (samples/s, threads, description)."""
+def host_cpus():
+    """CPUs this process may use and how that was decided: the scheduler affinity mask capped by a
+    cgroup v2 CPU quota when one is set (on the GPU box os.cpu_count() reports the whole host,
+    while the job's share is smaller), plus os.cpu_count() and the lscpu model name for the
+    record."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        quota = None
+    threads = min(aff, quota) if quota else aff
+    model = "?"
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        model = next((ln.split(":", 1)[1].strip() for ln in out.splitlines() if ln.startswith("Model name")), "?")
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return threads, {"os_cpu_count": os.cpu_count(), "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+                     "cpu_model": model}
+
+
+def cpu_subset(n_total=512, n_pick=16, seed=3):
+    """BASELINE.md sec 4's fixed CPU subset of the 512-utterance LibriTTS list
+    (RandomState(3).randint(80, 1200)): n_pick utterances at evenly spaced length ranks, so the
+    sample spans the length distribution. Returns (indices, lengths)."""
+    lengths = synthetic.libritts_lengths(n_total, seed=seed)
+    order = np.argsort(lengths, kind="stable")
+    idx = [int(order[int((k + 0.5) * n_total / n_pick)]) for k in range(n_pick)]
+    return idx, lengths[idx]
+
+
+def cpu_baseline(params, sd, config, n_utts):
+    """Time the torch-CPU restatement of the reference (oracle/pwg_torch_cpu.py, the reference's
+    aten op sequence; within 2-9 % of the imported reference on the same 8 cores,
+    profiles/r02_cpu/cpu_crosscheck.json) on a bounded sample of the workload, B=1 per utterance
+    like bin/decode.py, one warm-up call. Returns the cpu_baseline object of the JSON line."""
     from oracle.pwg_torch_cpu import TorchCPUGenerator
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    threads, info = host_cpus()
     torch.set_num_threads(threads)
     gen = TorchCPUGenerator(sd, params)
     A = params["aux_channels"]
+    H = int(np.prod(params["upsample_params"]["upsample_scales"]))
     gen.inference(synthetic.make_mel(40, A, seed=99), synthetic.make_noise(40 * H, seed=98))  # warm-up
-    done_samples, t_total, used = 0, 0.0, 0
-    for i, f in enumerate(lengths):
+    idx, lengths = cpu_subset(n_pick=n_utts)
+    done, t_total = 0, 0.0
+    for i, f in zip(idx, lengths):
         mel = synthetic.make_mel(int(f), A, seed=1000 + i)
         noise = synthetic.make_noise(int(f) * H, seed=2000 + i)
         t0 = time.perf_counter()
         gen.inference(mel, noise)
         t_total += time.perf_counter() - t0
-        done_samples += int(f) * H
-        used += 1
-        if t_total >= seconds_budget:
-            break
-    desc = f"{used} LibriTTS-v1 utterances ({done_samples} samples, first of the bench batch), B=1, torch-CPU aten restatement"
-    return done_samples / t_total, threads, desc
+        done += int(f) * H
+    desc = (f"{config}: {len(idx)} utterances of the 512-utterance RandomState(3) list at evenly spaced length "
+            f"ranks (T' = {', '.join(str(int(f)) for f in lengths)}; {done} samples), B=1 each, torch-CPU aten "
+            f"restatement of the reference op sequence, {threads} threads")
+    return dict({"value": round(done / t_total, 1), "unit": "audio samples/s", "cores": threads, "kind": "port",
+                 "sample": desc, "seconds": round(t_total, 2)}, **info)
 
 
 VOCODERS = ["mb_melgan_v2", "hifigan_v1", "melgan_v1"]
@@ -236,7 +281,7 @@ def bench_vocoder(args, rank, world, dev):
     top = sorted(timing, key=lambda r: -r[1])[:5]
     cpu = None
     if args.cpu_seconds > 0 and world == 1:
-        threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+        threads, info = host_cpus()
         torch.set_num_threads(threads)
         gen = TorchCPUVocoder(cls_name, fold_weight_norm(sd), params, syn)
         gen.inference(synthetic.make_mel(40, 80, seed=99))
@@ -250,9 +295,9 @@ def bench_vocoder(args, rank, world, dev):
             used += 1
             if tt >= args.cpu_seconds:
                 break
-        cpu = {"value": round(done / tt, 1), "unit": "audio samples/s", "cores": threads, "kind": "port",
-               "sample": f"{used} utterances ({done} samples, first of the bench batch), B=1, torch-CPU restatement "
-                         f"of the reference op sequence"}
+        cpu = dict({"value": round(done / tt, 1), "unit": "audio samples/s", "cores": threads, "kind": "port",
+                    "sample": f"{args.config}: {used} utterances ({done} samples, first of the bench batch), B=1, "
+                              f"torch-CPU restatement of the reference op sequence, {threads} threads"}, **info)
     res = {
         "metric": f"audio samples/sec/GPU ({fs / 1000:g} kHz {args.config}, 80-band mel)",
         "value": round(value, 1),
@@ -294,6 +339,65 @@ def bench_vocoder(args, rank, world, dev):
         dist.destroy_process_group()
 
 
+def latency_rows(dev, reps=20):
+    """The reference's own call pattern (bin/decode.py:236-268: one utterance per inference()
+    call, B=1) through the drop-in module, SURVEY.md sec 8(d)(2): LJ v1 at T' in {64, 512, 2048},
+    B=1 and B=16 equal-length (inference_batch). Per call: wall ms of the first call at a new
+    length (plan build included), median / min wall ms of repeated calls with device-resident
+    inputs (synchronised, range check included), host-to-host ms (numpy mel/noise in, .cpu() out,
+    like decode.py), and the kernels' own ms (HIP events, summed over the call's launches)."""
+    from parallelwavegan_amd import ParallelWaveGANGenerator
+
+    params = configs.generator_params("ljspeech_v1")
+    m = ParallelWaveGANGenerator(**params)
+    m.remove_weight_norm()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic.make_state_dict(params, seed=0).items()})
+    m = m.eval().to(dev)
+    H = m.upsample_factor
+    rows = []
+
+    def timed(fn):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) * 1e3
+
+    with torch.no_grad():
+        for F in (64, 512, 2048):
+            for B in (1, 16):
+                mels_h = [synthetic.make_mel(F, 80, seed=30 + b) for b in range(B)]
+                noises_h = [synthetic.make_noise(F * H, seed=60 + b) for b in range(B)]
+                mels = [torch.from_numpy(x).to(dev) for x in mels_h]
+                noises = [torch.from_numpy(x).to(dev) for x in noises_h]
+                if B == 1:
+                    call = lambda: m.inference(mels[0], noises[0])  # noqa: E731
+                    call_host = lambda: m.inference(mels_h[0], noises_h[0]).cpu()  # noqa: E731
+                else:
+                    call = lambda: m.inference_batch(mels, noises)  # noqa: E731
+                    call_host = lambda: [y.cpu() for y in m.inference_batch(mels_h, noises_h)]  # noqa: E731
+                first = timed(call)
+                for _ in range(3):
+                    call()
+                dev_ms = sorted(timed(call) for _ in range(reps))
+                host_ms = sorted(timed(call_host) for _ in range(max(3, reps // 4)))
+                eng = m.engine()
+                eng.set_timing(True)
+                eng.collect_timing()
+                call()
+                torch.cuda.synchronize(dev)
+                eng.set_timing(False)
+                kern = sum(ms for ms, _ in eng.collect_timing().values())
+                med = dev_ms[len(dev_ms) // 2]
+                rows.append({"frames": F, "batch": B, "samples_per_call": F * H * B,
+                             "first_call_ms": round(first, 3), "median_ms": round(med, 3),
+                             "min_ms": round(dev_ms[0], 3), "host_to_host_median_ms": round(host_ms[len(host_ms) // 2], 3),
+                             "kernel_ms": round(kern, 3), "overhead_ms": round(med - kern, 3),
+                             "samples_per_s": round(F * H * B / (med * 1e-3), 1)})
+    return {"model": "ljspeech_v1 ParallelWaveGANGenerator.inference / inference_batch (drop-in)",
+            "rows": rows}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -301,8 +405,14 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="libritts_v1",
                     choices=["libritts_v1", "ljspeech_v1", "yesno_debug"] + VOCODERS)
-    ap.add_argument("--utts", type=int, default=32, help="utterances per GPU per step")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (0 = skip)")
+    ap.add_argument("--utts", type=int, default=32, help="utterances per GPU per step (weak scaling)")
+    ap.add_argument("--strong", action="store_true",
+                    help="SURVEY.md sec 8(d)(5): the fixed 512-utterance RandomState(3) list, LPT-sharded over "
+                         "the ranks (strong scaling); one step = the whole list")
+    ap.add_argument("--cpu-seconds", type=float, default=None, help="0 = skip the CPU baseline (other values: legacy)")
+    ap.add_argument("--cpu-utts", type=int, default=4,
+                    help="CPU baseline sample: utterances of BASELINE.md sec 4's stratified subset (16 = all of it)")
+    ap.add_argument("--no-latency", action="store_true", help="skip the B=1 / B=16 latency rows")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "layer_traffic.json"))
     ap.add_argument("--layer-kernel", default=None, choices=["split", "split16", "persistent", "tiled"],
                     help="default: split where the shape allows, else persistent (the engine default)")
@@ -313,6 +423,10 @@ def main():
     ap.add_argument("--cnet-nofuse", action="store_true", help="vocoder configs: run fusable conv pairs unfused")
     ap.add_argument("--pair-steps", type=int, default=None, help="vocoder configs: 128-column tiles per fused-pair strip")
     args = ap.parse_args()
+    if args.cpu_seconds is None:
+        args.cpu_seconds = 12.0
+    if args.cpu_seconds == 0:
+        args.cpu_utts = 0
 
     rank, world, dev = dist_setup(args.gpus)
     _lib.build()
@@ -337,17 +451,35 @@ def main():
     H = eng.upsample_factor
     A = params["aux_channels"]
 
-    # weights: packed on rank 0, RCCL-broadcast to the other ranks (one collective, start-up only)
+    # weights: packed on rank 0 and broadcast to the other ranks, the design's one collective
+    # (start-up only): the C-ABI's RCCL path (pwg_broadcast_weights) on the nccl backend
     sd = synthetic.make_state_dict(params, seed=0)
     if rank == 0:
         packed = torch.from_numpy(eng.pack(sd)).to(dev)
     else:
         packed = torch.empty(eng.packed_weight_count, dtype=torch.float32, device=dev)
-    broadcast_packed_weights(packed, src=0)
+    broadcast = "none (one process)"
+    if world > 1:
+        if os.environ.get("PWG_BENCH_BACKEND", "nccl") == "nccl":
+            broadcast_weights_rccl(eng, packed, src=0)
+            broadcast = "pwg_broadcast_weights (C-ABI, RCCL over xGMI)"
+        else:
+            broadcast_packed_weights(packed, src=0)
+            broadcast = "torch.distributed.broadcast (gloo rehearsal)"
     eng.set_packed(packed)
 
-    # this rank's utterances: same lengths on every rank (weak scaling), rank-specific content
-    lengths = synthetic.libritts_lengths(args.utts, seed=3)
+    if args.strong:
+        all_lengths = synthetic.libritts_lengths(512, seed=3)
+        shards = lpt_partition(all_lengths, world)
+        mine = shards[rank]
+        lengths = all_lengths[mine]
+        loads = shard_loads(all_lengths, shards)
+        workload = (f"{args.config} generator inference, the fixed 512-utterance RandomState(3) list "
+                    f"({int(all_lengths.sum())} frames) LPT-sharded over {world} rank(s); one step = the whole list")
+    else:
+        # weak scaling: the same lengths on every rank, rank-specific content
+        lengths = synthetic.libritts_lengths(args.utts, seed=3)
+        workload = f"{args.config} generator inference, {args.utts} ragged utterances per GPU per step"
     plan = eng.plan(lengths.tolist())
     rs = np.random.RandomState(100 + rank)
     mel = torch.from_numpy(rs.standard_normal(int(lengths.sum()) * A).astype(np.float32)).to(dev)
@@ -356,7 +488,7 @@ def main():
     torch.cuda.synchronize(dev)
 
     for _ in range(args.warmup):
-        eng.run(plan, mel, noise, out)
+        eng.run(plan, mel, noise, out, check=False)
     torch.cuda.synchronize(dev)
 
     eng.set_timing(True)
@@ -366,14 +498,17 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        eng.run(plan, mel, noise, out)
+        eng.run(plan, mel, noise, out, check=False)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
+    local_elapsed = time.perf_counter() - t0
     eng.set_timing(False)
     timing = eng.collect_timing()
-    elapsed = max_over_ranks(elapsed, dev)
+    elapsed = max_over_ranks(local_elapsed, dev)
+    # the split-f16 range flag of the last timed run (pwg_run_status; raises on a flagged run)
+    if args.layer_kernel in ("split", "split16"):
+        eng.run_status(plan)
     if not torch.isfinite(out).all():
         raise RuntimeError("non-finite generator output")
 
@@ -388,14 +523,17 @@ def main():
     for _ in range(args.steps):
         mel.copy_(mel_h, non_blocking=True)
         noise.copy_(noise_h, non_blocking=True)
-        eng.run(plan, mel, noise, out)
+        eng.run(plan, mel, noise, out, check=False)
         out_h.copy_(out, non_blocking=True)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     e2e = max_over_ranks(time.perf_counter() - t0, dev)
 
-    samples_per_step = plan.total_samples * world
+    if args.strong:
+        samples_per_step = int(all_lengths.sum()) * H
+    else:
+        samples_per_step = plan.total_samples * world
     value = samples_per_step * args.steps / elapsed
     per_gpu = value / world
     layer_ms, layer_n = timing["residual_layer"]
@@ -403,18 +541,22 @@ def main():
     flops_launch = layer_flops_per_sample(params) * plan.total_samples
     achieved_tflops = flops_launch / layer_avg_s / 1e12
     traffic = mfma_insts = None
+    traffic_source = None
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            if (tj.get("config") == args.config and tj.get("utts") == args.utts
+            if (tj.get("config") == args.config and tj.get("utts") == args.utts and not args.strong
                     and tj.get("layer_kernel", "persistent") == args.layer_kernel):
                 traffic = tj.get("hbm_bytes_per_launch")
                 mfma_insts = tj.get("mfma_insts_per_launch")
+                traffic_source = (f"{os.path.relpath(args.traffic_json, REPO)} (rocprofv3 --pmc FETCH_SIZE x2 + "
+                                  f"WRITE_SIZE of this workload, {tj.get('source', 'committed profile')}; "
+                                  f"not measured in this run)")
         except (OSError, ValueError):
             traffic = None
     L = params["layers"]
     if args.layer_kernel in ("split", "split16"):
-        # HBM-bound (DESIGN.md 3.6): algorithmic bytes of the engine's layer per launch / launch time
+        # HBM-bound (DESIGN.md 3.0): algorithmic bytes of the engine's layer per launch / launch time
         bytes_launch = split_layer_bytes_per_sample(params, H, L, fuse_first) * plan.total_samples
         n_blocks = int(sum(-(-int(f) * H // 128) * 4 for f in lengths))
         exec_flop = split_executed_flop_per_block(L, args.layer_kernel) * n_blocks
@@ -427,6 +569,7 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
             "traffic": traffic,
+            "traffic_source": traffic_source,
             "algorithmic_bytes_per_launch": int(bytes_launch),
             "avg_launch_ms": round(layer_avg_s * 1e3, 4),
             "launches_timed": layer_n,
@@ -450,6 +593,7 @@ def main():
             "unit": "TFLOP/s",
             "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 4),
             "traffic": traffic,
+            "traffic_source": traffic_source,
             "flop_per_launch": int(flops_launch),
             "algorithmic_bytes_per_launch": int(layer_bytes_per_sample(params) * plan.total_samples),
             "avg_launch_ms": round(layer_avg_s * 1e3, 4),
@@ -460,16 +604,31 @@ def main():
             "executed_frac": mfma_insts and round(mfma_insts * 4096 / layer_avg_s / 1e12 / FP32_PEAK_TFLOPS, 4),
             "hbm_GBs": traffic and round(traffic / layer_avg_s / 1e9, 1),
         }
+    busy = {"local_s": local_elapsed}
+    if args.strong:
+        # per-rank compute time next to the max: load imbalance of the LPT partition
+        gloo = dist.is_initialized() and dist.get_backend() == "gloo"
+        t = torch.tensor([local_elapsed], dtype=torch.float64, device="cpu" if gloo else dev)
+        if world > 1:
+            ts = [torch.zeros_like(t) for _ in range(world)]
+            dist.all_gather(ts, t)
+            busy["per_rank_s"] = [float(x.item()) for x in ts]
+        else:
+            busy["per_rank_s"] = [local_elapsed]
 
     if rank != 0:
         dist.destroy_process_group()
         return
 
     cpu = None
-    if args.cpu_seconds > 0 and world == 1:
-        v, cores, desc = cpu_baseline(params, sd, lengths, H, args.cpu_seconds)
-        cpu = {"value": round(v, 1), "unit": "audio samples/s", "cores": cores, "kind": "port", "sample": desc}
+    if args.cpu_utts > 0 and world == 1:
+        cpu = cpu_baseline(params, sd, args.config, args.cpu_utts)
+    lat = None
+    if not args.no_latency and world == 1:
+        lat = latency_rows(dev)
 
+    parallelism = (f"utterance-sharded x{world} (no data-path collective; weights broadcast once: {broadcast})"
+                   if world > 1 else "1 process, 1 GPU (no collective)")
     res = {
         "metric": "audio samples/sec/GPU (24 kHz PWG, 80-band mel) + RTF at 1/2/4/8 MI355X",
         "value": round(value, 1),
@@ -479,31 +638,39 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,
         "dtype": "f32 (fp16 hi+lo pair operands, 3 f16 MFMAs per product, fp32 accumulate)"
                  if args.layer_kernel in ("split", "split16") else "f32",
         "data": "synthetic (seeded N(0,1) mel + noise, seeded kaiming-init weights)",
         "config": {
-            "workload": f"{args.config} generator inference, {args.utts} ragged utterances per GPU per step",
+            "workload": workload,
             "model": "ParallelWaveGANGenerator",
             "sampling_rate": fs,
             "hop": H,
-            "global_batch": args.utts * world,
+            "global_batch": 512 if args.strong else args.utts * world,
             "frames_per_gpu": int(lengths.sum()),
             "samples_per_step_per_gpu": int(plan.total_samples),
-            "parallelism": f"utterance-sharded x{world} (no data-path collective; RCCL weight broadcast at start)",
+            "parallelism": parallelism,
         },
         "value_per_gpu": round(per_gpu, 1),
         "x_realtime_per_gpu": round(per_gpu / fs, 1),
         "rtf_per_gpu": per_gpu and fs / per_gpu,
         "kernel_ms_per_step": {k: round(ms / args.steps, 3) for k, (ms, _) in timing.items()},
+        "range_check": "ok (pwg_run_status after the timed steps)" if args.layer_kernel in ("split", "split16")
+                       else "n/a (exact fp32)",
         "roofline": roofline,
         "model_flop_per_sample": round(model_flops_per_sample(params), 1),
         "model_tflops": round(value / world * model_flops_per_sample(params) / 1e12, 3),
         "pcie_inclusive_value": round(samples_per_step * args.steps / e2e, 1),
         "cpu_baseline": cpu,
+        "latency": lat,
     }
+    if args.strong:
+        per = busy["per_rank_s"]
+        res["strong"] = {"shard_frames": loads, "frame_imbalance": round(max(loads) / (sum(loads) / world), 4),
+                         "rank_seconds": [round(x, 4) for x in per],
+                         "time_imbalance": round(max(per) / (sum(per) / world), 4)}
     print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

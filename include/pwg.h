@@ -29,8 +29,11 @@
  * pwg_last_error() returns a thread-local message for the last failure.
  *
  * Threading: a handle/plan is not thread-safe; work is enqueued on the caller's
- * HIP stream (hipStream_t passed as void*), nothing synchronises the host except
- * pwg_plan_create (descriptor upload) and pwg_timing_collect.
+ * HIP stream (hipStream_t passed as void*); only pwg_run_status and
+ * pwg_timing_collect synchronise the host. Plans are host-only objects (no device
+ * allocation): pwg_run rebuilds the plan's block descriptors inside the caller's
+ * workspace with one small kernel per 48 utterances, so a new utterance length costs
+ * no hipMalloc / blocking copy and a run is capturable in a HIP graph.
  */
 #ifndef PWG_H_
 #define PWG_H_
@@ -54,7 +57,10 @@ enum {
   PWG_ERR_INVALID = 1,     /* ValueError */
   PWG_ERR_ASSERT = 2,      /* AssertionError */
   PWG_ERR_HIP = 3,         /* RuntimeError (HIP runtime failure) */
-  PWG_ERR_UNSUPPORTED = 4  /* NotImplementedError */
+  PWG_ERR_UNSUPPORTED = 4, /* NotImplementedError */
+  PWG_ERR_RANGE = 5        /* a value left the fp16 pair range of the split-f16 kernels (no reference
+                              counterpart: the reference computes in fp32; the drop-in reruns on the
+                              exact-fp32 kernel, see pwg_run_status) */
 };
 
 /* Input layouts accepted by pwg_plan_create / pwg_run. */
@@ -128,7 +134,10 @@ PWG_API long long pwg_ref_weight_count(const PwgHandle* h);
 /* Number of floats of the kernel-ready packed weight image (fp32). */
 PWG_API long long pwg_packed_weight_count(const PwgHandle* h);
 /* Host -> host: pack reference-order weights into the kernel image. The caller
- * uploads the image to device memory (and may RCCL-broadcast it). */
+ * uploads the image to device memory (and may RCCL-broadcast it, pwg_broadcast_weights).
+ * Returns PWG_ERR_RANGE (image still fully written) when a weight of the split-f16
+ * images exceeds the fp16 range: the image is then valid for the exact-fp32 layer
+ * kernels (PWG_OPT_LAYER_KERNEL 0/1) only. */
 PWG_API int pwg_pack_weights(const PwgHandle* h, const float* ref_host, float* packed_host);
 
 /* Plan a batch of n_utts utterances with frames[u] mel frames each. */
@@ -149,6 +158,14 @@ PWG_API long long pwg_plan_workspace_bytes(const PwgPlan* p);
 PWG_API int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* noise,
             const float* mean, const float* scale, float* out, void* workspace, void* stream);
 
+/* Range check of the last pwg_run on `workspace` (split-f16 layer kernels, which carry
+ * fp32 operands as fp16 hi+lo pairs): synchronises `stream` and returns PWG_ERR_RANGE
+ * if any live column's final skip sum was not finite, i.e. some x / D / first_conv value
+ * exceeded the fp16 range (|v| >= 65520) or the input itself was not finite. The output of
+ * such a run is not valid; rerun it with PWG_OPT_LAYER_KERNEL 0 (exact fp32), which is
+ * what the Python drop-in does. The exact-fp32 kernels never set the flag. */
+PWG_API int pwg_run_status(PwgPlan* p, const void* workspace, void* stream);
+
 /* Engine options (pwg_set_option). Defaults are the tuned values; the others exist for A/B
  * measurement (bench.py --layer-kernel ...). */
 enum {
@@ -164,12 +181,31 @@ enum {
                                     noise, x0 never stored (default 1; bit-identical to 0) */
 };
 PWG_API int pwg_set_option(PwgHandle* h, int option, long long value);
+/* Current value of an option (the layer kernel the handle picked for its shape, ...). */
+PWG_API int pwg_get_option(const PwgHandle* h, int option, long long* value);
 
 /* Per-kernel HIP-event timing of pwg_run (off by default). collect synchronises
  * on the recorded events, adds ms and launch counts per PWG_KERNEL_* bucket into
  * the caller's arrays and clears the records. */
 PWG_API int pwg_set_timing(PwgHandle* h, int enable);
 PWG_API int pwg_timing_collect(PwgHandle* h, double* ms, long long* launches);
+
+/* ---- Multi-GPU: the one collective of the design -----------------
+ * Utterances shard across GPUs with no data-path exchange; the only collective is a broadcast of
+ * the packed weight image from a root rank over RCCL/xGMI at start-up. librccl is resolved at first
+ * use (dlopen of librccl.so.1: inside a torch process that is torch's own RCCL); these return
+ * PWG_ERR_UNSUPPORTED when it is absent. comm is an ncclComm_t passed as void*. A host that already
+ * owns an RCCL communicator passes it straight to pwg_broadcast_weights; one that does not creates
+ * one with the two helpers (rank 0 makes the id and ships its 128 bytes to the other ranks by any
+ * out-of-band channel, every rank then calls pwg_rccl_comm_create). Replaces the reference's
+ * per-process checkpoint load (bin/decode.py:131-155), which each decode process repeats. */
+#define PWG_RCCL_UNIQUE_ID_BYTES 128
+PWG_API int pwg_rccl_unique_id(void* id_out /* PWG_RCCL_UNIQUE_ID_BYTES */);
+PWG_API int pwg_rccl_comm_create(int nranks, const void* id, int rank, int device, void** comm_out);
+PWG_API int pwg_rccl_comm_destroy(void* comm);
+/* In-place ncclBroadcast of pwg_packed_weight_count(h) floats at `packed` (device) from `root`,
+ * enqueued on `stream`. */
+PWG_API int pwg_broadcast_weights(const PwgHandle* h, void* comm, int root, float* packed, void* stream);
 
 #ifdef __cplusplus
 }

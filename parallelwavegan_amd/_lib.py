@@ -24,6 +24,7 @@ CSRC = [
     os.path.join(PKG_DIR, "csrc", "pwg_cnet.hip"),
     os.path.join(PKG_DIR, "csrc", "pwg_split.hip"),
     os.path.join(PKG_DIR, "csrc", "pwg_split16.hip"),
+    os.path.join(PKG_DIR, "csrc", "pwg_rccl.hip"),
 ]
 HEADERS = [
     os.path.join(REPO_DIR, "include", "pwg.h"),
@@ -37,6 +38,8 @@ PWG_ERR_INVALID = 1
 PWG_ERR_ASSERT = 2
 PWG_ERR_HIP = 3
 PWG_ERR_UNSUPPORTED = 4
+PWG_ERR_RANGE = 5
+PWG_RCCL_UNIQUE_ID_BYTES = 128
 
 PWG_LAYOUT_INFERENCE = 0
 PWG_LAYOUT_FORWARD = 1
@@ -61,9 +64,15 @@ EXPORTED_SYMBOLS = (
     "pwg_plan_padded_samples",
     "pwg_plan_workspace_bytes",
     "pwg_run",
+    "pwg_run_status",
     "pwg_set_option",
+    "pwg_get_option",
     "pwg_set_timing",
     "pwg_timing_collect",
+    "pwg_rccl_unique_id",
+    "pwg_rccl_comm_create",
+    "pwg_rccl_comm_destroy",
+    "pwg_broadcast_weights",
     # include/pwg_cnet.h: conv-network executor (MelGAN family)
     "pwg_cnet_abi_version",
     "pwg_cnet_create",
@@ -112,22 +121,13 @@ def _needs_build():
     return any(os.path.getmtime(p) > t for p in CSRC + HEADERS)
 
 
-def build(force=False, verbose=False, extra_flags=(), out_path=None):
-    """Compile the HIP kernels + C-ABI into parallelwavegan_amd/lib/libpwg_hip.so (gfx950).
-    extra_flags/out_path build A/B measurement variants (e.g. -DPWG_STORE_SC1=0) elsewhere."""
-    target = out_path or LIB_PATH
-    if not force and out_path is None and (os.environ.get("PWG_NO_BUILD") == "1" or not _needs_build()):
-        return LIB_PATH
-    os.makedirs(os.path.dirname(target), exist_ok=True)
-    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    tmp = target + ".tmp.%d" % os.getpid()
-    cmd = [
+def _compile_cmd(hipcc, extra_flags):
+    return [
         hipcc,
         f"--offload-arch={OFFLOAD_ARCH}",
         "-O3",
         "-std=c++17",
         "-fPIC",
-        "-shared",
         "-fvisibility=hidden",
         "-mcode-object-version=5",
         # keep the work-queue atomic a plain per-lane op: the optimizer's wave-reduction form
@@ -135,14 +135,57 @@ def build(force=False, verbose=False, extra_flags=(), out_path=None):
         "-mllvm",
         "-amdgpu-atomic-optimizer-strategy=None",
         "-Wall",
-        "-o",
-        tmp,
-    ] + list(extra_flags) + CSRC
+    ] + list(extra_flags)
+
+
+def build(force=False, verbose=False, extra_flags=(), out_path=None, jobs=None):
+    """Compile the HIP kernels + C-ABI into parallelwavegan_amd/lib/libpwg_hip.so (gfx950): one
+    hipcc -c per source in parallel (objects under build/<variant>/, rebuilt when a source or
+    header is newer), then one link. extra_flags/out_path build A/B measurement variants (e.g.
+    -DPWG_STORE_SC1=0) elsewhere."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    target = out_path or LIB_PATH
+    if not force and out_path is None and (os.environ.get("PWG_NO_BUILD") == "1" or not _needs_build()):
+        return LIB_PATH
+    os.makedirs(os.path.dirname(target), exist_ok=True)
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    variant = os.path.splitext(os.path.basename(target))[0]
+    objdir = os.path.join(REPO_DIR, "build", variant)
+    os.makedirs(objdir, exist_ok=True)
+    base = _compile_cmd(hipcc, extra_flags)
+    stamp = os.path.join(objdir, "flags.txt")
+    flags_txt = " ".join(base)
+    stale_flags = not os.path.exists(stamp) or open(stamp).read() != flags_txt
+    newest_header = max(os.path.getmtime(h) for h in HEADERS)
+
+    def compile_one(src):
+        obj = os.path.join(objdir, os.path.basename(src) + ".o")
+        if (not force and not stale_flags and os.path.exists(obj)
+                and os.path.getmtime(obj) >= max(os.path.getmtime(src), newest_header)):
+            return obj, ""
+        tmp = obj + ".tmp.%d" % os.getpid()
+        cmd = base + ["-c", "-o", tmp, src]
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError("hipcc failed:\n" + " ".join(cmd) + "\n" + res.stdout + res.stderr)
+        os.replace(tmp, obj)
+        return obj, res.stdout + res.stderr
+
+    n = jobs or min(len(CSRC), max(1, int(os.environ.get("MAX_JOBS", os.cpu_count() or 1))))
+    with ThreadPoolExecutor(max_workers=n) as ex:
+        results = list(ex.map(compile_one, CSRC))
+    with open(stamp, "w") as f:
+        f.write(flags_txt)
+    tmp = target + ".tmp.%d" % os.getpid()
+    cmd = [hipcc, f"--offload-arch={OFFLOAD_ARCH}", "-shared", "-fPIC", "-o", tmp] + [o for o, _ in results] + ["-ldl"]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
-        raise RuntimeError("hipcc failed:\n" + " ".join(cmd) + "\n" + res.stdout + res.stderr)
-    if verbose and (res.stdout or res.stderr):
-        print(res.stdout + res.stderr)
+        raise RuntimeError("hipcc link failed:\n" + " ".join(cmd) + "\n" + res.stdout + res.stderr)
+    if verbose:
+        for _, log in results:
+            if log:
+                print(log)
     os.replace(tmp, target)
     return target
 
@@ -183,6 +226,12 @@ def load():
             getattr(lib, name).argtypes = [vp]
             getattr(lib, name).restype = ll
         lib.pwg_run.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp]
+        lib.pwg_run_status.argtypes = [vp, vp, vp]
+        lib.pwg_get_option.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ll)]
+        lib.pwg_rccl_unique_id.argtypes = [vp]
+        lib.pwg_rccl_comm_create.argtypes = [ctypes.c_int, vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
+        lib.pwg_rccl_comm_destroy.argtypes = [vp]
+        lib.pwg_broadcast_weights.argtypes = [vp, vp, ctypes.c_int, vp, vp]
         lib.pwg_set_timing.argtypes = [vp, ctypes.c_int]
         lib.pwg_set_option.argtypes = [vp, ctypes.c_int, ctypes.c_longlong]
         lib.pwg_timing_collect.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ll)]
@@ -192,7 +241,12 @@ def load():
         return lib
 
 
+class RangeError(ArithmeticError):
+    """PWG_ERR_RANGE: a value left the fp16 pair range of the split-f16 kernels."""
+
+
 _ERRORS = {
+    PWG_ERR_RANGE: RangeError,
     PWG_ERR_INVALID: ValueError,
     PWG_ERR_ASSERT: AssertionError,
     PWG_ERR_HIP: RuntimeError,

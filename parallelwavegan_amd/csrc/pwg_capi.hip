@@ -71,9 +71,14 @@ float h2f(uint16_t h) {
   return (h & 0x8000u) ? -v : v;
 }
 
+// Values pwg_pack_weights split into fp16 pairs that left the fp16 range (|v| >= 65520 rounds
+// to inf): such an image is refused for the split-f16 kernels (PWG_ERR_RANGE).
+thread_local long long g_split_overflow = 0;
+
 // v ~= hi + lo as fp16 (hi = rne(v), lo = rne(v - hi)); returns hi | lo << 16
 uint32_t split_pair(float v) {
   const uint16_t hi = f2h(v);
+  if ((hi & 0x7c00u) == 0x7c00u) ++g_split_overflow;
   const uint16_t lo = f2h(v - h2f(hi));
   return (uint32_t)hi | ((uint32_t)lo << 16);
 }
@@ -318,12 +323,11 @@ struct PwgPlan {
   int n_utts;
   std::vector<UttDesc> utts;
   long long n_tiles, n_gap_tiles, Tpad, F_total, T_total;
-  UttDesc* d_utts = nullptr;
-  int* d_tile_utt = nullptr;
-  long long* d_gap_col0 = nullptr;
-  BlockDesc* d_blocks = nullptr;
-  // workspace offsets (bytes)
-  size_t ws_x0, ws_x1, ws_skip, ws_c1, ws_d, ws_ctr, ws_total;
+  // workspace offsets (bytes); the descriptor arrays (utts, tile_utt, gap_col0, blocks) are
+  // written by pwg_plan_desc_kernel at the start of every pwg_run
+  size_t ws_x0, ws_x1, ws_skip, ws_c1, ws_d, ws_ctr, ws_flag;
+  size_t ws_utts, ws_tile_utt, ws_gap, ws_blocks, ws_total;
+  long long max_blocks_per_utt = 0;
 };
 
 extern "C" {
@@ -469,6 +473,7 @@ long long pwg_packed_weight_count(const PwgHandle* h) { return (long long)h->pac
 int pwg_pack_weights(const PwgHandle* h, const float* ref, float* pk) {
   if (!h || !ref || !pk) return fail(PWG_ERR_INVALID, "null argument");
   std::memset(pk, 0, sizeof(float) * h->packed_total);
+  g_split_overflow = 0;
   const PwgConfig& c = h->cfg;
   const int R = h->R, G = h->G, GH = h->GH, GHPAD = h->GHPAD, MT = h->MT, S = h->S, M2T = h->M2T;
   const int A = h->A, KS = h->KS, KW = h->KW, O = h->O;
@@ -766,6 +771,10 @@ int pwg_pack_weights(const PwgHandle* h, const float* ref, float* pk) {
     }
   }
   if ((long long)(p - ref) != h->ref_total) return fail(PWG_ERR_INVALID, "internal: weight count mismatch");
+  if (g_split_overflow > 0)
+    return fail(PWG_ERR_RANGE, std::to_string(g_split_overflow) +
+                                   " weights exceed the fp16 pair range of the split-f16 layer kernels; the "
+                                   "image is complete for PWG_OPT_LAYER_KERNEL 0/1 (exact fp32) only");
   return PWG_OK;
 }
 
@@ -820,25 +829,11 @@ int pwg_plan_create(PwgHandle* h, int n_utts, const long long* frames, int layou
     delete p;
     return fail(PWG_ERR_UNSUPPORTED, "batch too large for one plan (2^31 samples); split it");
   }
-  std::vector<int> tile_utt(p->n_tiles);
-  std::vector<BlockDesc> blocks((size_t)p->n_tiles * (TILE / 32));
-  for (int u = 0; u < n_utts; ++u) {
-    const UttDesc& d = p->utts[u];
-    const long long n = (d.T + TILE - 1) / TILE;
-    for (long long t = 0; t < n; ++t) {
-      tile_utt[d.first_tile + t] = u;
-      for (int b = 0; b < TILE / 32; ++b) {
-        BlockDesc& bd = blocks[(size_t)(d.first_tile + t) * (TILE / 32) + b];
-        bd.t0 = (int)(t * TILE + 32 * b);
-        bd.col = (int)(d.seg_base + bd.t0);
-        bd.T = (int)d.T;
-        bd.frames = (int)d.frames;
-        bd.frame_base = (int)d.frame_base;
-        bd.io_off = (int)d.io_off;
-        bd.utt = u;
-        bd.pad = 0;
-      }
-    }
+  for (const UttDesc& d : p->utts)
+    p->max_blocks_per_utt = std::max(p->max_blocks_per_utt, (d.T + TILE - 1) / TILE * (TILE / 32));
+  if ((long long)gap_col0.size() != (long long)(n_utts + 1) * (h->gap / TILE)) {
+    delete p;
+    return fail(PWG_ERR_INVALID, "internal: gap tile count");
   }
   size_t o = 0;
   p->ws_x0 = o; o += align_bytes(sizeof(float) * h->RS * p->Tpad);
@@ -847,40 +842,17 @@ int pwg_plan_create(PwgHandle* h, int n_utts, const long long* frames, int layou
   p->ws_c1 = o; o += align_bytes(sizeof(float) * h->A * p->F_total);
   p->ws_d = o; o += align_bytes(sizeof(float) * h->L * h->GR * p->F_total);
   p->ws_ctr = o; o += align_bytes(sizeof(int) * h->L * SCHED_CTR_STRIDE * 8);
+  p->ws_flag = o; o += align_bytes(sizeof(int));  // split-f16 range flag (pwg_run_status)
+  p->ws_utts = o; o += align_bytes(sizeof(UttDesc) * n_utts);
+  p->ws_tile_utt = o; o += align_bytes(sizeof(int) * p->n_tiles);
+  p->ws_gap = o; o += align_bytes(sizeof(long long) * std::max<long long>(p->n_gap_tiles, 1));
+  p->ws_blocks = o; o += align_bytes(sizeof(BlockDesc) * p->n_tiles * (TILE / 32));
   p->ws_total = o;
-
-  DeviceGuard g(h->device);
-  if (!g.ok) { delete p; return fail(PWG_ERR_HIP, "hipSetDevice failed"); }
-  hipError_t e = hipMalloc(&p->d_utts, sizeof(UttDesc) * n_utts);
-  if (e == hipSuccess) e = hipMalloc(&p->d_tile_utt, sizeof(int) * p->n_tiles);
-  if (e == hipSuccess) e = hipMalloc(&p->d_gap_col0, sizeof(long long) * std::max<long long>(p->n_gap_tiles, 1));
-  if (e == hipSuccess && p->n_gap_tiles > 0)
-    e = hipMemcpy(p->d_gap_col0, gap_col0.data(), sizeof(long long) * p->n_gap_tiles, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMalloc(&p->d_blocks, sizeof(BlockDesc) * blocks.size());
-  if (e == hipSuccess)
-    e = hipMemcpy(p->d_blocks, blocks.data(), sizeof(BlockDesc) * blocks.size(), hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(p->d_utts, p->utts.data(), sizeof(UttDesc) * n_utts, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(p->d_tile_utt, tile_utt.data(), sizeof(int) * p->n_tiles, hipMemcpyHostToDevice);
-  if (e != hipSuccess) {
-    const int rc = hip_fail(e, "plan descriptor upload");
-    pwg_plan_destroy(p);
-    return rc;
-  }
   *out = p;
   return PWG_OK;
 }
 
-void pwg_plan_destroy(PwgPlan* p) {
-  if (!p) return;
-  {
-    DeviceGuard g(p->h->device);
-    if (p->d_utts) (void)hipFree(p->d_utts);
-    if (p->d_tile_utt) (void)hipFree(p->d_tile_utt);
-    if (p->d_gap_col0) (void)hipFree(p->d_gap_col0);
-    if (p->d_blocks) (void)hipFree(p->d_blocks);
-  }
-  delete p;
-}
+void pwg_plan_destroy(PwgPlan* p) { delete p; }
 
 long long pwg_plan_total_samples(const PwgPlan* p) { return p->T_total; }
 long long pwg_plan_padded_samples(const PwgPlan* p) { return p->Tpad; }
@@ -935,12 +907,28 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
     return e;
   };
 
-  hipError_t e = hipMemsetAsync(sched_ctr, 0, sizeof(int) * h->L * SCHED_CTR_STRIDE * 8, s);
+  int* range_flag = (int*)(ws + p->ws_flag);
+  // work-queue heads and the range flag (adjacent) start at zero every run
+  hipError_t e = hipMemsetAsync(sched_ctr, 0, p->ws_flag + sizeof(int) - p->ws_ctr, s);
   if (e != hipSuccess) return hip_fail(e, "work-queue reset");
+  UttDesc* d_utts = (UttDesc*)(ws + p->ws_utts);
+  int* d_tile_utt = (int*)(ws + p->ws_tile_utt);
+  long long* d_gap_col0 = (long long*)(ws + p->ws_gap);
+  BlockDesc* d_blocks = (BlockDesc*)(ws + p->ws_blocks);
+  for (int u0 = 0; u0 < p->n_utts; u0 += PLAN_CHUNK) {
+    PlanDescArgs da;
+    da.n = std::min(PLAN_CHUNK, p->n_utts - u0);
+    da.u0 = u0;
+    da.gap_tiles = (int)(h->gap / TILE);
+    for (int i = 0; i < da.n; ++i) da.utts[i] = p->utts[u0 + i];
+    da.d_utts = d_utts; da.tile_utt = d_tile_utt; da.gap_col0 = d_gap_col0; da.blocks = d_blocks;
+    e = launch_plan_desc(da, p->max_blocks_per_utt, s);
+    if (e != hipSuccess) return hip_fail(e, "plan descriptor launch");
+  }
   ConvInArgs ca;
   ca.mel = mel; ca.mean = mean; ca.scale = scale; ca.w = packed + h->off_conv_in; ca.c1 = c1;
   ca.wfrag = packed + h->off_conv_in_frag;
-  ca.utts = p->d_utts; ca.n_utts = p->n_utts; ca.F_total = p->F_total; ca.A = h->A; ca.KW = h->KW;
+  ca.utts = d_utts; ca.n_utts = p->n_utts; ca.F_total = p->F_total; ca.A = h->A; ca.KW = h->KW;
   ca.ctx = h->cfg.aux_context_window; ca.layout = p->layout; ca.use_conv_in = h->cfg.use_conv_in;
   e = timed(PWG_KERNEL_CONV_IN, [&] { return launch_conv_in(ca, s); });
   if (e != hipSuccess) return hip_fail(e, "conv_in launch");
@@ -957,7 +945,7 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
 
   FirstConvArgs fa;
   fa.noise = noise; fa.w = packed + h->off_first_w; fa.b = packed + h->off_first_b; fa.x = x0; fa.x1 = x1;
-  fa.tile_utt = p->d_tile_utt; fa.utts = p->d_utts; fa.gap_col0 = p->d_gap_col0; fa.n_work = p->n_tiles;
+  fa.tile_utt = d_tile_utt; fa.utts = d_utts; fa.gap_col0 = d_gap_col0; fa.n_work = p->n_tiles;
   fa.Tpad = p->Tpad; fa.R = h->R; fa.RS = h->RS;
   // split16 with the fused first_conv: layer 0 builds x0 itself; only the gap tiles of both
   // residual buffers are zeroed here (the work-tile branch is skipped: n_work = 0)
@@ -984,7 +972,7 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
     la.tab.Fmin = h->aux.Fmin; la.nka = h->aux.nka; la.nfwg = h->aux.nfwg;
     la.wg = L0 + h->lo_wg; la.wgp = L0 + h->lo_wgp; la.bg = L0 + h->lo_bg; la.w2 = L0 + h->lo_w2;
     la.n_blocks = p->n_tiles * (TILE / 32);
-    la.tile_utt = p->d_tile_utt; la.utts = p->d_utts; la.Tpad = p->Tpad;
+    la.tile_utt = d_tile_utt; la.utts = d_utts; la.Tpad = p->Tpad;
     la.R = h->R; la.RS = h->RS; la.S = h->S; la.SS = h->SS; la.KS = h->KS; la.dil = h->dil[l];
     la.tap_center = h->cfg.use_causal_conv ? h->KS - 1 : (h->KS - 1) / 2;
     la.first = l == 0;
@@ -1002,7 +990,7 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
       sa.tab_left = (int)(h->off_tab_left - h->off_tab_interior);
       sa.tab_right = (int)(h->off_tab_right - h->off_tab_interior);
       sa.tab_small = (int)(h->off_tab_small - h->off_tab_interior);
-      sa.blocks = p->d_blocks;
+      sa.blocks = d_blocks;
       sa.wg = reinterpret_cast<const unsigned*>(L0 + (split16 ? h->lo_split16 : h->lo_split));
       sa.hw1 = la.hw1; sa.hw2 = la.hw2; sa.hb2 = la.hb2; sa.out = out;
       if (split16) {
@@ -1018,6 +1006,7 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
       const int nwg = h->n_cu * h->wg_per_cu;
       sa.trace = nullptr;
       sa.noise = nullptr; sa.fw = sa.fb = nullptr;
+      sa.range_flag = last ? range_flag : nullptr;
       if (fuse_first && l == 0) {
         sa.noise = noise; sa.fw = packed + h->off_first_w; sa.fb = packed + h->off_first_b;
       }
@@ -1056,7 +1045,7 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
       pa2.tab_left = (int)(h->off_tab_left - h->off_tab_interior);
       pa2.tab_right = (int)(h->off_tab_right - h->off_tab_interior);
       pa2.tab_small = (int)(h->off_tab_small - h->off_tab_interior);
-      pa2.blocks = p->d_blocks;
+      pa2.blocks = d_blocks;
       pa2.wgp = la.wgp; pa2.w2 = la.w2; pa2.bg = la.bg;
       pa2.hw1 = la.hw1; pa2.hw2 = la.hw2; pa2.hb2 = la.hb2; pa2.out = out;
       pa2.H = (int)h->aux.H; pa2.J1 = h->aux.J1; pa2.TL = h->aux.TL; pa2.TR = h->aux.TR;
@@ -1115,6 +1104,22 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
   return PWG_OK;
 }
 
+int pwg_run_status(PwgPlan* p, const void* workspace, void* stream) {
+  if (!p || !workspace) return fail(PWG_ERR_INVALID, "null argument");
+  DeviceGuard g(p->h->device);
+  if (!g.ok) return fail(PWG_ERR_HIP, "hipSetDevice failed");
+  int flag = 0;
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = hipMemcpyAsync(&flag, (const char*)workspace + p->ws_flag, sizeof(int), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return hip_fail(e, "run status");
+  if (flag != 0)
+    return fail(PWG_ERR_RANGE,
+                "non-finite skip sum in the split-f16 layer kernel: a value left the fp16 pair range (or the "
+                "input is not finite); rerun with PWG_OPT_LAYER_KERNEL 0 (exact fp32)");
+  return PWG_OK;
+}
+
 int pwg_set_option(PwgHandle* h, int option, long long value) {
   if (!h) return fail(PWG_ERR_INVALID, "null handle");
   switch (option) {
@@ -1138,6 +1143,17 @@ int pwg_set_option(PwgHandle* h, int option, long long value) {
       return PWG_OK;
     default:
       return fail(PWG_ERR_INVALID, "unknown option");
+  }
+}
+
+int pwg_get_option(const PwgHandle* h, int option, long long* value) {
+  if (!h || !value) return fail(PWG_ERR_INVALID, "null argument");
+  switch (option) {
+    case PWG_OPT_LAYER_KERNEL: *value = h->layer_kernel; return PWG_OK;
+    case PWG_OPT_WAVES_PER_WG: *value = h->waves_per_wg; return PWG_OK;
+    case PWG_OPT_FUSE_FIRST_CONV: *value = h->fuse_first; return PWG_OK;
+    case PWG_OPT_WG_PER_CU: *value = h->wg_per_cu; return PWG_OK;
+    default: return fail(PWG_ERR_INVALID, "unknown option");
   }
 }
 

@@ -190,6 +190,8 @@ struct SplitArgs {
   const float* noise;         // split16 layer 0 with first_conv fused (else null): caller noise
   const float* fw;            // first_conv weight [64] and bias [64]
   const float* fb;
+  int* range_flag;            // last layer: set to 1 when a live column's final skip sum is not
+                              // finite (fp16 pair range exceeded somewhere upstream; pwg_run_status)
 };
 // dwords of one layer's split image (SplitSmem in pwg_split.hip without the head)
 constexpr int SPLIT_LAYER_DWORDS = 3 * 4 * 4 * 2 * 64 * 4 + 4 * 4 * 2 * 64 * 4 + 32 * 4 + 64;
@@ -201,6 +203,23 @@ constexpr int SCHED_CTR_STRIDE = 32;
 int set_error(int code, const char* msg);
 
 // Kernel launchers (pwg_kernels.hip).
+// Plan descriptors built on the device at the start of every pwg_run, in the caller's workspace
+// (no per-plan hipMalloc / blocking hipMemcpy / hipFree; graph-capturable): up to PLAN_CHUNK
+// utterances per launch, passed by value.
+constexpr int PLAN_CHUNK = 48;
+constexpr int GAP_TILES_MAX = 1 << 20;
+struct PlanDescArgs {
+  UttDesc utts[PLAN_CHUNK];
+  int n;          // utterances in this chunk
+  int u0;         // plan index of utts[0]
+  int gap_tiles;  // zero tiles between segments (gap / TILE)
+  UttDesc* d_utts;
+  int* tile_utt;
+  long long* gap_col0;
+  BlockDesc* blocks;
+};
+hipError_t launch_plan_desc(const PlanDescArgs& a, long long max_blocks, hipStream_t s);
+
 hipError_t launch_conv_in(const ConvInArgs& a, hipStream_t s);
 hipError_t launch_aux_proj(const AuxProjArgs& a, int layers, hipStream_t s);
 hipError_t launch_first_conv(const FirstConvArgs& a, long long n_tiles, hipStream_t s);

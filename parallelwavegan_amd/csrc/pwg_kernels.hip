@@ -1095,6 +1095,42 @@ __global__ void __launch_bounds__(PWG_PERSIST_THREADS, 1) pwg_layer_persistent_k
 }
 
 // ---------------------------------------------------------------------------------------------
+// One thread per 32-sample block of utterance blockIdx.y of the chunk: its BlockDesc, the
+// tile -> utterance map, the utterance's trailing gap tiles (chunk 0 also the leading ones) and
+// the UttDesc itself (same values pwg_plan_create computed on the host).
+__global__ void __launch_bounds__(256) pwg_plan_desc_kernel(const PlanDescArgs a) {
+  const int y = blockIdx.y;
+  const UttDesc& d = a.utts[y];
+  const long long j = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long nb = (d.T + TILE - 1) / TILE * (TILE / 32);
+  if (j < nb) {
+    BlockDesc b;
+    b.t0 = (int)(32 * j);
+    b.col = (int)(d.seg_base + b.t0);
+    b.T = (int)d.T;
+    b.frames = (int)d.frames;
+    b.frame_base = (int)d.frame_base;
+    b.io_off = (int)d.io_off;
+    b.utt = a.u0 + y;
+    b.pad = 0;
+    a.blocks[d.first_tile * (TILE / 32) + j] = b;
+    if ((j & (TILE / 32 - 1)) == 0) a.tile_utt[d.first_tile + j / (TILE / 32)] = a.u0 + y;
+  }
+  if (j < a.gap_tiles) {
+    const long long seg_end = d.seg_base + (d.T + TILE - 1) / TILE * TILE;
+    a.gap_col0[(long long)(a.u0 + y + 1) * a.gap_tiles + j] = seg_end + j * TILE;
+    if (a.u0 == 0 && y == 0) a.gap_col0[j] = j * TILE;
+  }
+  if (j == 0) a.d_utts[a.u0 + y] = d;
+}
+
+hipError_t launch_plan_desc(const PlanDescArgs& a, long long max_blocks, hipStream_t s) {
+  const long long m = max_blocks > a.gap_tiles ? max_blocks : a.gap_tiles;
+  const long long nx = m > 0 ? (m + 255) / 256 : 1;
+  hipLaunchKernelGGL(pwg_plan_desc_kernel, dim3((unsigned)nx, (unsigned)a.n), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_conv_in(const ConvInArgs& a, hipStream_t s) {
   if (a.use_conv_in && a.A <= 128) {
     const dim3 grid((unsigned)((a.F_total + 127) / 128));

@@ -315,6 +315,7 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
   BlockDesc bdn = a.blocks[blk];
   u32x4 b0[8], b1[8];
   bload(bdn.col, 0, b0);
+  bool nonfinite = false;  // LAST: a live column's final skip sum is not finite
 
   while (true) {
     const BlockDesc bd = bdn;
@@ -534,6 +535,14 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
       //      S -> O dot product across the two lane halves
       constexpr int M3 = 2, NQH = 32, NQH4 = 9;
       float hs[2][16];
+      {
+        float sum = 0.f;  // range check of the final skip sum (see pwg_split16.hip)
+#pragma unroll
+        for (int mm = 0; mm < 2; ++mm)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sum += acc2[mm][r];
+        nonfinite |= live && !__builtin_isfinite(sum);
+      }
 #pragma unroll
       for (int mm = 0; mm < 2; ++mm)
 #pragma unroll
@@ -587,6 +596,8 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
 #pragma unroll
     for (int i = 0; i < 8; ++i) b0[i] = b1[i];
   }
+  if (LAST && nonfinite && a.range_flag)
+    __hip_atomic_fetch_or(a.range_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   PWG_TR(tr_done());
 #undef PWG_TR
 }

@@ -40,6 +40,12 @@
 #ifndef PWG_SPLIT16_DIAG_NOTAP
 #define PWG_SPLIT16_DIAG_NOTAP 0
 #endif
+// Diagnostic only (wrong results): the x (bit 0) and/or skip (bit 1) streams are folded into a
+// per-XCD 2,048-column window that stays in the XCD's L2, i.e. the upper bound of what keeping those
+// streams on chip across layers (cross-layer fusion) could save with the layer's arithmetic unchanged.
+#ifndef PWG_SPLIT16_DIAG_L2
+#define PWG_SPLIT16_DIAG_L2 0
+#endif
 #ifndef PWG_SPLIT16_MG
 #define PWG_SPLIT16_MG 4  // GEMM-1 m-tiles whose A fragments are read per group
 #endif
@@ -135,6 +141,13 @@ __device__ __forceinline__ Pair16 split_pair16(float v0, float v1) {
 // 256 dwords (1 KB) apart
 __device__ __forceinline__ size_t row16(int c, int g) {
   return (size_t)(c >> 5) * 2048 + (size_t)((c >> 4) & 1) * 1024 + (size_t)g * 64 + (size_t)(c & 15) * 4;
+}
+
+// PWG_SPLIT16_DIAG_L2 column folding (identity in the product build)
+template <int BIT>
+__device__ __forceinline__ int diag_col(int col, int xcd) {
+  if constexpr ((PWG_SPLIT16_DIAG_L2 & BIT) != 0) return 512 + xcd * 2048 + (col & 2047);
+  return col;
 }
 
 // LDS image of one layer (dwords): GEMM-1 A fragments [tap 3][ks 2][m 8][hi/lo 2][lane 64][4]
@@ -239,7 +252,7 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
       const int cc = d.col + (PWG_SPLIT16_DIAG_NOTAP ? 0 : (tap - TC) * a.dil);  // NOTAP: diagnostic only
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
-        const u32x4* p = reinterpret_cast<const u32x4*>(a.x_in + row16(cc + 16 * nt + c, g));
+        const u32x4* p = reinterpret_cast<const u32x4*>(a.x_in + row16(diag_col<1>(cc + 16 * nt + c, xcd), g));
 #pragma unroll
         for (int q = 0; q < 4; ++q) b[nt * 4 + q] = p[q * 64];
       }
@@ -293,6 +306,11 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
   BlockDesc bdn = a.blocks[blk];
   u32x4 b0[8], b1[8];
   bload(bdn, 0, b0);
+  // LAST: any live column whose final skip sum is not finite. In the pair split an x, D or
+  // first_conv value beyond the fp16 range becomes (inf, -inf), which every later product turns into
+  // NaN and every skip sum downstream carries (the head's ReLU would hide it), so one check here
+  // covers every layer of the forward.
+  bool nonfinite = false;
 
   while (true) {
     const BlockDesc bd = bdn;
@@ -360,7 +378,7 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
         if (a.first) {
           acc2[ms][nt] = reinterpret_cast<const f32x4*>(a.skip0 + 16 * g)[ms];
         } else {
-          const f32x4* sp = reinterpret_cast<const f32x4*>(a.skip + row16(bd.col + 16 * nt + c, g));
+          const f32x4* sp = reinterpret_cast<const f32x4*>(a.skip + row16(diag_col<2>(bd.col + 16 * nt + c, xcd), g));
           acc2[ms][nt] = PWG16_LD_SKIP(sp + ms * 64);
         }
       }
@@ -387,7 +405,7 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
         if (a.first) {
           acc2[ms][nt] = reinterpret_cast<const f32x4*>(a.skip0 + 16 * g)[ms];
         } else {
-          const f32x4* sp = reinterpret_cast<const f32x4*>(a.skip + row16(bd.col + 16 * nt + c, g));
+          const f32x4* sp = reinterpret_cast<const f32x4*>(a.skip + row16(diag_col<2>(bd.col + 16 * nt + c, xcd), g));
           acc2[ms][nt] = PWG16_LD_SKIP(sp + ms * 64);
         }
       }
@@ -461,10 +479,10 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
       for (int nt = 0; nt < 2; ++nt) {
         const int col = bd.col + 16 * nt + c;
         const bool live = bd.t0 + 16 * nt + c < bd.T;
-        f32x4* sp = reinterpret_cast<f32x4*>(a.skip + row16(col, g));
+        f32x4* sp = reinterpret_cast<f32x4*>(a.skip + row16(diag_col<2>(col, xcd), g));
 #pragma unroll
         for (int ms = 0; ms < 4; ++ms) PWG16_ST(sp + ms * 64, acc2[ms][nt]);
-        u32x4* xp = reinterpret_cast<u32x4*>(a.x_out + row16(col, g));
+        u32x4* xp = reinterpret_cast<u32x4*>(a.x_out + row16(diag_col<1>(col, xcd), g));
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
           float v[8];
@@ -497,6 +515,15 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) acc3[m3][nt] = hb1[m3];
       u32x4 sh[2][2], sl[2][2];  // [nt][ks]
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        float sum = 0.f;  // inf/NaN in any of the 16 propagates (a finite overflow only reruns exact)
+#pragma unroll
+        for (int ms = 0; ms < 4; ++ms)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) sum += acc2[ms][nt][i];
+        nonfinite |= bd.t0 + 16 * nt + c < bd.T && !__builtin_isfinite(sum);
+      }
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
@@ -545,6 +572,8 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
 #pragma unroll
     for (int i = 0; i < 8; ++i) b0[i] = b1[i];
   }
+  if (LAST && nonfinite && a.range_flag)
+    __hip_atomic_fetch_or(a.range_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // first_conv (1x1, 1 -> 64, bias) into the split16 x layout; gap tiles zero both buffers.

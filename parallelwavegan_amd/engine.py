@@ -6,6 +6,7 @@ kernels. torch is used for device memory and the current stream only.
 """
 
 import ctypes
+import logging
 from collections import OrderedDict
 
 import numpy as np
@@ -116,6 +117,50 @@ def fold_weight_norm(state):
     return out
 
 
+# Bumped whenever any module registers a parameter (module.weight = Parameter(...),
+# register_parameter, weight-norm add/remove): invalidates every WeightTracker's parameter list.
+_PARAM_REGISTRATIONS = [0]
+
+
+def _on_parameter_registration(module, name, param):
+    _PARAM_REGISTRATIONS[0] += 1
+
+
+torch.nn.modules.module.register_module_parameter_registration_hook(_on_parameter_registration)
+
+
+class WeightTracker:
+    """Per-call "do the packed weights still match the module?" check for the drop-in modules.
+
+    The first version walked every parameter's (data_ptr, _version) per call (640 us for PWG v1's
+    221 parameters). This keeps the parameter list (re-collected only after a parameter
+    registration anywhere or an explicit ``invalidate()``, which the modules call from ``_apply``,
+    i.e. ``.to()``/``.cuda()``) and compares the list's ``_version`` counters, which every in-place
+    update bumps (load_state_dict's copy_, optimizer steps, ``add_`` under no_grad): ~22 us."""
+
+    def __init__(self):
+        self._key = None
+        self._params = None
+        self._versions = None
+
+    def invalidate(self):
+        self._key = None
+
+    def changed(self, module, extra=()):
+        """extra: tensors outside module.parameters() the packed image also holds (a PQMF
+        filter buffer); compared by identity as well as version."""
+        key = (_PARAM_REGISTRATIONS[0], id(module), tuple(id(t) for t in extra))
+        if key != self._key:
+            self._params = list(module.parameters()) + list(extra)
+            self._key = key
+            self._versions = None
+        versions = [p._version for p in self._params]
+        return versions != self._versions
+
+    def mark_packed(self):
+        self._versions = [p._version for p in self._params]
+
+
 class HostHandle:
     """A pwg handle used for host-only work (packing, shape queries); needs no GPU."""
 
@@ -154,10 +199,17 @@ class HostHandle:
         return flat
 
     def pack(self, state):
-        """Host-side packed image (np.float32, pwg_packed_weight_count)."""
+        """Host-side packed image (np.float32, pwg_packed_weight_count).
+
+        Sets ``split_range_ok``: False when a weight of the split-f16 images exceeds the fp16 range
+        (pwg_pack_weights returned PWG_ERR_RANGE); the image is then complete for the exact-fp32
+        layer kernels only."""
         flat = self.flatten_state_dict(state)
         packed = np.empty(self.packed_weight_count, np.float32)
-        _lib.check(self._lib.pwg_pack_weights(self._h, flat.ctypes.data, packed.ctypes.data))
+        rc = self._lib.pwg_pack_weights(self._h, flat.ctypes.data, packed.ctypes.data)
+        self.split_range_ok = rc != _lib.PWG_ERR_RANGE
+        if rc != _lib.PWG_ERR_RANGE:
+            _lib.check(rc)
         return packed
 
 
@@ -211,8 +263,11 @@ class Engine:
         self.packed_weight_count = lib.pwg_packed_weight_count(h)
         self.packed = None
         self._plans = OrderedDict()
-        self._workspace = None
+        self._workspaces = {}  # one per stream: concurrent runs on different streams never share one
         self.timing_enabled = False
+        self.split_range_ok = True
+        self.range_reruns = 0  # runs redone on the exact-fp32 kernel after a split-f16 range flag
+        self.layer_kernel = self.get_option("layer_kernel")
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -227,6 +282,10 @@ class Engine:
 
     def load_state_dict(self, state):
         packed = self.pack(state)
+        if not self.split_range_ok and self.layer_kernel in (2, 3):
+            logging.warning("generator weights exceed the fp16 pair range of the split-f16 layer kernel: "
+                            "using the exact-fp32 layer kernel")
+            self.set_option("layer_kernel", "persistent")
         self.set_packed(torch.from_numpy(packed).to(self.device))
         return self.packed
 
@@ -250,11 +309,23 @@ class Engine:
             self._plans.move_to_end(key)
         return p
 
-    def workspace(self, nbytes):
-        if self._workspace is None or self._workspace.numel() < nbytes:
-            self._workspace = None
-            self._workspace = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=self.device)
-        return self._workspace
+    def workspace(self, nbytes, stream=None):
+        """The cached workspace of ``stream`` (default: the current stream), grown to ``nbytes``
+        and allocated on that stream, so runs on different streams never share buffers."""
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device)
+        key = stream.cuda_stream
+        ws = self._workspaces.get(key)
+        if ws is None or ws.numel() < nbytes:
+            self._workspaces.pop(key, None)
+            with torch.cuda.stream(stream):
+                ws = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=self.device)
+            self._workspaces[key] = ws
+        return ws
+
+    def release_workspace(self):
+        """Drop the cached workspaces (the caching allocator keeps the memory for reuse)."""
+        self._workspaces = {}
 
     # ---------------------------------------------------------------- options
     LAYER_KERNELS = {"persistent": 0, "tiled": 1, "split": 2, "split16": 3}
@@ -265,7 +336,19 @@ class Engine:
                 "wg_per_cu": _lib.PWG_OPT_WG_PER_CU, "fuse_first_conv": _lib.PWG_OPT_FUSE_FIRST_CONV}
         if option == "layer_kernel" and isinstance(value, str):
             value = self.LAYER_KERNELS[value]
+        if option == "layer_kernel" and int(value) in (2, 3) and not self.split_range_ok:
+            raise _lib.RangeError("the loaded weights exceed the fp16 pair range of the split-f16 layer kernels")
         _lib.check(self._lib.pwg_set_option(self._h, opts[option], int(value)))
+        if option == "layer_kernel":
+            self.layer_kernel = int(value)
+
+    _OPTS = {"layer_kernel": _lib.PWG_OPT_LAYER_KERNEL, "waves_per_wg": _lib.PWG_OPT_WAVES_PER_WG,
+             "wg_per_cu": _lib.PWG_OPT_WG_PER_CU, "fuse_first_conv": _lib.PWG_OPT_FUSE_FIRST_CONV}
+
+    def get_option(self, option):
+        v = ctypes.c_longlong()
+        _lib.check(self._lib.pwg_get_option(self._h, self._OPTS[option], ctypes.byref(v)))
+        return int(v.value)
 
     # ---------------------------------------------------------------- timing
     def set_timing(self, enable):
@@ -279,8 +362,40 @@ class Engine:
         return {k: (ms[i], n[i]) for i, k in enumerate(_lib.KERNEL_BUCKETS)}
 
     # ---------------------------------------------------------------- run
-    def run(self, plan, mel, noise, out, mean=None, scale=None, stream=None):
-        """Enqueue one forward of ``plan`` on ``stream`` (default: torch's current stream)."""
+    def run(self, plan, mel, noise, out, mean=None, scale=None, stream=None, check=True):
+        """Enqueue one forward of ``plan`` on ``stream`` (default: torch's current stream).
+
+        check=True (the drop-in's setting) runs the split-f16 range check after the forward
+        (pwg_run_status, one stream synchronisation) and, when a value left the fp16 pair range,
+        redoes the forward on the exact-fp32 layer kernel, so the result always holds fp32
+        semantics. check=False only enqueues (the bench's timed loop; check afterwards with
+        ``run_status``)."""
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device)
+        self._enqueue(plan, mel, noise, out, mean, scale, stream)
+        if check and self.layer_kernel in (2, 3):
+            try:
+                self.run_status(plan, stream)
+            except _lib.RangeError as e:
+                logging.warning("%s; rerunning on the exact-fp32 layer kernel", e)
+                kernel = self.layer_kernel
+                self.set_option("layer_kernel", "persistent")
+                try:
+                    self._enqueue(plan, mel, noise, out, mean, scale, stream)
+                finally:
+                    self.set_option("layer_kernel", kernel)
+                self.range_reruns += 1
+        return out
+
+    def run_status(self, plan, stream=None):
+        """pwg_run_status of the last run on ``stream``'s workspace: raises _lib.RangeError when the
+        split-f16 range flag is set (synchronises the stream)."""
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device)
+        ws = self.workspace(plan.workspace_bytes, stream)
+        _lib.check(self._lib.pwg_run_status(plan._p, ws.data_ptr(), stream.cuda_stream))
+
+    def _enqueue(self, plan, mel, noise, out, mean, scale, stream):
         if self.packed is None:
             raise RuntimeError("no weights loaded")
         for name, t in (("mel", mel), ("noise", noise), ("out", out)):
@@ -301,9 +416,7 @@ class Engine:
             mean = mean.to(self.device, torch.float32).contiguous()
             scale = scale.to(self.device, torch.float32).contiguous()
             mp, sp = mean.data_ptr(), scale.data_ptr()
-        ws = self.workspace(plan.workspace_bytes)
-        if stream is None:
-            stream = torch.cuda.current_stream(self.device)
+        ws = self.workspace(plan.workspace_bytes, stream)
         _lib.check(
             self._lib.pwg_run(
                 plan._p,

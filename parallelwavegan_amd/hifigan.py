@@ -19,6 +19,7 @@ import numpy as np
 import torch
 
 from . import cnet
+from .engine import WeightTracker
 from .melgan import _slope
 
 
@@ -103,6 +104,7 @@ class HiFiGANGenerator(torch.nn.Module):
             self.apply_weight_norm()
         self.reset_parameters()
         self._engine = None
+        self._weights = WeightTracker()
         self._sig = None
 
     # ------------------------------------------------------------------ reference API
@@ -205,17 +207,21 @@ class HiFiGANGenerator(torch.nn.Module):
                                "with .to('cuda') (there is no CPU fallback)")
         return dev
 
+    def _apply(self, fn, *args, **kwargs):
+        if getattr(self, "_weights", None) is not None:
+            self._weights.invalidate()  # .to() / .cuda() replace parameter storage
+        return super()._apply(fn, *args, **kwargs)
+
     def engine(self):
         dev = self._device()
         if self._engine is None or self._engine.device != dev:
             self._engine = cnet.CnetEngine(self.program(), dev)
-            self._sig = None
-        sig = tuple((p.data_ptr(), p._version) for p in self.parameters())
-        if sig != self._sig:
+            self._weights.invalidate()
+        if self._weights.changed(self):
             with torch.no_grad():
                 state = {k: v for k, v in self.state_dict().items() if k not in ("mean", "scale")}
                 self._engine.load_state_dict(state)
-            self._sig = sig
+            self._weights.mark_packed()
         return self._engine
 
     def forward(self, c):

@@ -20,6 +20,7 @@ import numpy as np
 import torch
 
 from . import cnet
+from .engine import WeightTracker
 
 
 def _kaiser(m, beta):
@@ -286,11 +287,10 @@ class MelGANGenerator(torch.nn.Module):
                                "with .to('cuda') (there is no CPU fallback)")
         return dev
 
-    def _signature(self, with_pqmf):
-        sig = tuple((p.data_ptr(), p._version) for p in self.parameters())
-        if with_pqmf:
-            sig += (self.pqmf.synthesis_filter.data_ptr(), self.pqmf.synthesis_filter._version)
-        return sig
+    def _apply(self, fn, *args, **kwargs):
+        for ent in getattr(self, "_engines", {}).values():
+            ent[1].invalidate()  # .to() / .cuda() replace parameter storage
+        return super()._apply(fn, *args, **kwargs)
 
     def engine(self, with_pqmf=None):
         if with_pqmf is None:
@@ -299,16 +299,15 @@ class MelGANGenerator(torch.nn.Module):
         ent = self._engines.get(with_pqmf)
         if ent is None or ent[0].device != dev:
             P, extra = self.program(with_pqmf)
-            ent = [cnet.CnetEngine(P, dev), None]
+            ent = [cnet.CnetEngine(P, dev), WeightTracker()]
             self._engines[with_pqmf] = ent
-        sig = self._signature(with_pqmf)
-        if ent[1] != sig:
+        if ent[1].changed(self, (self.pqmf.synthesis_filter,) if with_pqmf else ()):
             _, extra = self.program(with_pqmf)
             with torch.no_grad():
                 state = {k: v for k, v in self.state_dict().items() if not k.startswith("pqmf.") and
                          k not in ("mean", "scale")}
                 ent[0].load_state_dict(state, extra)
-            ent[1] = sig
+            ent[1].mark_packed()
         return ent[0]
 
     # ------------------------------------------------------------------ forward paths

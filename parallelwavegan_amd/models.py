@@ -20,7 +20,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .engine import Engine
+from .engine import Engine, WeightTracker
 
 
 def _kaiming_conv1d(*args, **kwargs):
@@ -163,7 +163,7 @@ class ParallelWaveGANGenerator(torch.nn.Module):
         if use_weight_norm:
             self.apply_weight_norm()
         self._engine = None
-        self._packed_sig = None
+        self._weights = WeightTracker()
 
     # ------------------------------------------------------------------ reference API
     def remove_weight_norm(self):
@@ -219,22 +219,23 @@ class ParallelWaveGANGenerator(torch.nn.Module):
                 "module with .to('cuda') (there is no CPU fallback)")
         return dev
 
-    def _signature(self):
-        return tuple((p.data_ptr(), p._version) for p in self.parameters())
+    def _apply(self, fn, *args, **kwargs):
+        if getattr(self, "_weights", None) is not None:
+            self._weights.invalidate()  # .to() / .cuda() replace parameter storage
+        return super()._apply(fn, *args, **kwargs)
 
     def engine(self):
         """The HIP engine with this module's current weights packed (re-packed when a
-        parameter changes)."""
+        parameter changes: WeightTracker)."""
         dev = self._device()
         if self._engine is None or self._engine.device != dev:
             self._engine = Engine(self._params, dev)
-            self._packed_sig = None
-        sig = self._signature()
-        if sig != self._packed_sig:
+            self._weights.invalidate()
+        if self._weights.changed(self):
             with torch.no_grad():
                 state = {k: v for k, v in self.state_dict().items() if k not in ("mean", "scale")}
                 self._engine.load_state_dict(state)
-            self._packed_sig = sig
+            self._weights.mark_packed()
         return self._engine
 
     # ------------------------------------------------------------------ forward paths

@@ -48,6 +48,38 @@ def broadcast_packed_weights(packed, src=0, group=None):
     return packed
 
 
+def broadcast_weights_rccl(engine, packed, src=0, group=None):
+    """The same broadcast through the C-ABI's RCCL entry points (include/pwg.h
+    pwg_rccl_unique_id / pwg_rccl_comm_create / pwg_broadcast_weights), i.e. the path a
+    non-Python host uses: rank ``src`` makes the RCCL id, the 128 bytes travel over the existing
+    process group, every rank joins a one-shot RCCL communicator on its engine's device and
+    receives the image in place on the current stream. Returns ``packed``."""
+    if not dist.is_available() or not dist.is_initialized():
+        return packed
+    import ctypes
+
+    from . import _lib
+
+    lib = _lib.load()
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    buf = ctypes.create_string_buffer(_lib.PWG_RCCL_UNIQUE_ID_BYTES)
+    if rank == src:
+        _lib.check(lib.pwg_rccl_unique_id(buf))
+    obj = [bytes(buf.raw)]
+    dist.broadcast_object_list(obj, src=src, group=group)
+    buf = ctypes.create_string_buffer(obj[0], _lib.PWG_RCCL_UNIQUE_ID_BYTES)
+    dev = packed.device.index if packed.device.index is not None else torch.cuda.current_device()
+    comm = ctypes.c_void_p()
+    _lib.check(lib.pwg_rccl_comm_create(world, buf, rank, dev, ctypes.byref(comm)))
+    try:
+        stream = torch.cuda.current_stream(packed.device)
+        _lib.check(lib.pwg_broadcast_weights(engine._h, comm, src, packed.data_ptr(), stream.cuda_stream))
+        stream.synchronize()
+    finally:
+        _lib.check(lib.pwg_rccl_comm_destroy(comm))
+    return packed
+
+
 def max_over_ranks(value, device=None):
     """Max of a float over all ranks (timing reduction for bench.py)."""
     if not dist.is_available() or not dist.is_initialized():

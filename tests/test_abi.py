@@ -147,3 +147,38 @@ def test_config_translation():
     cfg = make_config(configs.generator_params("libritts_v1"))
     assert list(cfg.upsample_scales)[: cfg.num_scales] == [4, 5, 3, 5]
     assert cfg.use_conv_in == 1 and cfg.aux_context_window == 2
+
+
+def test_pack_reports_fp16_pair_range(built_lib):
+    """pwg_pack_weights returns PWG_ERR_RANGE (image still complete for the exact-fp32 kernels)
+    when a weight of the split-f16 images leaves the fp16 range; in-range weights pack clean."""
+    params = configs.generator_params("libritts_v1")
+    h = HostHandle(params)
+    sd = synthetic.make_state_dict(params, seed=0)
+    ok = h.pack(sd)
+    assert h.split_range_ok
+    sd["conv_layers.3.conv.weight"] = sd["conv_layers.3.conv.weight"].copy()
+    sd["conv_layers.3.conv.weight"][5, 7, 1] = 7e4
+    bad = h.pack(sd)
+    assert not h.split_range_ok
+    assert "fp16" in built_lib.pwg_last_error().decode()
+    assert np.isfinite(ok).all() and bad.shape == ok.shape
+
+
+def test_get_option_reports_default_layer_kernel(built_lib):
+    for name, kernel in (("libritts_v1", 3), ("yesno_debug", 0), ("reference_test", 0)):
+        h = HostHandle(configs.generator_params(name))
+        v = ctypes.c_longlong()
+        _lib.check(built_lib.pwg_get_option(h._h, _lib.PWG_OPT_LAYER_KERNEL, ctypes.byref(v)))
+        assert v.value == kernel, name
+
+
+def test_rccl_entry_points_validate_arguments(built_lib):
+    """Argument checks of the RCCL entries need no GPU (no communicator is created)."""
+    assert built_lib.pwg_rccl_unique_id(None) == _lib.PWG_ERR_INVALID
+    comm = ctypes.c_void_p()
+    assert built_lib.pwg_rccl_comm_create(2, None, 0, 0, ctypes.byref(comm)) == _lib.PWG_ERR_INVALID
+    buf = ctypes.create_string_buffer(_lib.PWG_RCCL_UNIQUE_ID_BYTES)
+    assert built_lib.pwg_rccl_comm_create(2, buf, 2, 0, ctypes.byref(comm)) == _lib.PWG_ERR_INVALID
+    assert built_lib.pwg_broadcast_weights(None, None, 0, None, None) == _lib.PWG_ERR_INVALID
+    assert built_lib.pwg_rccl_comm_destroy(None) == _lib.PWG_OK

@@ -58,14 +58,20 @@ def test_golden_vectors(name, kernel, built_lib, cuda_device):
 
 
 @pytest.mark.parametrize("kernel", ["split", "split16", "persistent", "tiled"])
-@pytest.mark.parametrize("cfg, frames", [("ljspeech_v1", 64), ("libritts_v1", 41), ("yesno_debug", 100)])
-def test_against_numpy_oracle(cfg, frames, kernel, built_lib, cuda_device):
+@pytest.mark.parametrize("cfg, frames, over", [
+    ("ljspeech_v1", 64, {}), ("libritts_v1", 41, {}), ("yesno_debug", 100, {}),
+    # the causal generators at the PWG v1 shape run on split16 by default (a16)
+    ("ljspeech_v1", 64, {"use_causal_conv": True}),
+    ("libritts_v1", 41, {"use_causal_conv": True}),
+    ("libritts_v1", 23, {"use_causal_conv": True, "aux_context_window": 0}),
+], ids=["lj", "libritts", "yesno", "lj_causal", "libritts_causal", "libritts_causal_w0"])
+def test_against_numpy_oracle(cfg, frames, over, kernel, built_lib, cuda_device):
     from oracle import pwg_numpy
     from parallelwavegan_amd import configs, synthetic
 
-    params = configs.generator_params(cfg)
+    params = configs.generator_params(cfg, **over)
     sd = synthetic.make_state_dict(params, seed=7)
-    m = _module(configs.generator_params(cfg), sd, cuda_device)
+    m = _module(configs.generator_params(cfg, **over), sd, cuda_device)
     _set_kernel(m, kernel)
     H = m.upsample_factor
     mel = synthetic.make_mel(frames, 80, seed=11)
@@ -92,6 +98,93 @@ def test_full_size_against_torch_cpu(built_lib, cuda_device):
     ref = TorchCPUGenerator(sd, params).inference(mel, noise).numpy()
     err = np.abs(y - ref).max()
     assert err < ATOL, f"max|d| = {err:.3e}"
+
+
+def test_full_length_libritts_batch_against_torch_cpu(built_lib, cuda_device):
+    """The bench's configuration on its default (split16) kernel against the CPU oracle directly,
+    not against another HIP kernel: a ragged LibriTTS v1 batch holding a full-length utterance
+    (T' = 1199, the top of RandomState(3).randint(80, 1200); 359,700 samples) plus two shorter
+    ones, each checked against oracle/pwg_torch_cpu.py (the reference's aten op sequence)."""
+    from oracle.pwg_torch_cpu import TorchCPUGenerator
+    from parallelwavegan_amd import Engine, configs, synthetic
+
+    params = configs.generator_params("libritts_v1")
+    sd = synthetic.make_state_dict(params, seed=0)
+    eng = Engine(params, cuda_device)
+    eng.load_state_dict(sd)
+    assert eng.layer_kernel == Engine.LAYER_KERNELS["split16"]
+    lengths = [1199, 80, 517]
+    mels = [synthetic.make_mel(f, 80, seed=300 + i) for i, f in enumerate(lengths)]
+    noises = [synthetic.make_noise(f * 300, seed=400 + i) for i, f in enumerate(lengths)]
+    ys = eng.infer([torch.from_numpy(m).to(cuda_device) for m in mels],
+                   [torch.from_numpy(n).to(cuda_device) for n in noises])
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    gen = TorchCPUGenerator(sd, params)
+    for f, mel, noise, y in zip(lengths, mels, noises, ys):
+        ref = gen.inference(mel, noise).numpy()
+        err = np.abs(y.cpu().numpy() - ref).max()
+        assert err < ATOL, f"T'={f}: max|d| = {err:.3e}"
+
+
+@pytest.mark.parametrize("case", ["mel_x30", "mel_x30_res_w_x2", "mel_x30_res_w_x4", "first_conv_overflow",
+                                  "weight_overflow"])
+def test_split_range_guard(case, built_lib, cuda_device):
+    """Stress and fp16 range guard of the split-f16 path (pwg_pack_weights PWG_ERR_RANGE, the
+    in-kernel non-finite flag read by pwg_run_status), against the float64 oracle. Bar: max|d| <
+    max(1e-4, 3 x the error of the reference's own fp32 op sequence, oracle/pwg_torch_cpu.py). The
+    second term matters only where the network itself is ill-conditioned in fp32:
+      mel_x30, mel_x30_res_w_x2: large activations, well conditioned: |d| < 1e-4 holds outright;
+      mel_x30_res_w_x4: every residual-block weight x4 makes the stack chaotic: the fp32 reference
+        itself lands ~0.6 from fp64 (profiles/r02_v1b/stress.jsonl), so the split kernel is held
+        to the fp32 reference's own accuracy class;
+      first_conv_overflow: first_conv.weight x1e5 puts x0 beyond 65504, the pair split makes
+        inf/-inf: the run must be flagged and redone on the exact-fp32 kernel (range_reruns == 1);
+      weight_overflow: a gate weight of 7e4 cannot be packed as fp16 pairs; packing reports it and
+        the engine uses the exact-fp32 kernel from the start."""
+    from oracle import pwg_numpy
+    from oracle.pwg_torch_cpu import TorchCPUGenerator
+    from parallelwavegan_amd import Engine, _lib, configs, synthetic
+
+    params = configs.generator_params("libritts_v1")
+    sd = synthetic.make_state_dict(params, seed=21)
+    mel = synthetic.make_mel(37, 80, seed=22)
+    noise = synthetic.make_noise(37 * 300, seed=23)
+    if case.startswith("mel_x30"):
+        mel = mel * 30
+        wx = {"mel_x30": 1, "mel_x30_res_w_x2": 2, "mel_x30_res_w_x4": 4}[case]
+        sd = {k: (v * wx if k.startswith("conv_layers.") and k.endswith(".weight") else v) for k, v in sd.items()}
+    elif case == "first_conv_overflow":
+        sd["first_conv.weight"] = sd["first_conv.weight"] * 1e5
+    else:
+        sd["conv_layers.3.conv.weight"] = sd["conv_layers.3.conv.weight"].copy()
+        sd["conv_layers.3.conv.weight"][5, 7, 1] = 7e4
+    eng = Engine(params, cuda_device)
+    eng.load_state_dict(sd)
+    if case == "weight_overflow":
+        assert not eng.split_range_ok and eng.layer_kernel == Engine.LAYER_KERNELS["persistent"]
+        with pytest.raises(_lib.RangeError):
+            eng.set_option("layer_kernel", "split16")
+    else:
+        assert eng.split_range_ok and eng.layer_kernel == Engine.LAYER_KERNELS["split16"]
+    y = eng.infer([torch.from_numpy(mel).to(cuda_device)], [torch.from_numpy(noise).to(cuda_device)])[0]
+    y = y.cpu().numpy()
+    ref = pwg_numpy.inference(mel, noise, sd, params)
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    fp32_err = np.abs(TorchCPUGenerator(sd, params).inference(mel, noise).numpy() - ref).max()
+    assert np.isfinite(ref).all() and np.isfinite(y).all()
+    err = np.abs(y - ref).max()
+    assert err < max(ATOL, 3 * fp32_err), f"{case}: max|d| = {err:.3e}, fp32 reference {fp32_err:.3e}"
+    if case in ("mel_x30", "mel_x30_res_w_x2"):
+        assert err < ATOL
+    assert eng.range_reruns == (1 if case == "first_conv_overflow" else 0)
+    if case == "first_conv_overflow":
+        # the raw C-ABI path reports the flag instead of rerunning
+        plan = eng.plan([37])
+        out = torch.empty(37 * 300, device=cuda_device)
+        eng.run(plan, torch.from_numpy(mel).to(cuda_device).reshape(-1), torch.from_numpy(noise).to(cuda_device).reshape(-1),
+                out, check=False)
+        with pytest.raises(_lib.RangeError):
+            eng.run_status(plan)
 
 
 @pytest.mark.parametrize("wscale", [1.0, 2.0])

@@ -11,7 +11,7 @@ timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smo
 cat "$OUT/smoke.log" | tail -1
 timeout -k 10 300 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
 cat "$OUT/bench.json"
-cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --cpu-seconds 0 > "$GRAFT_REPO_ROOT/$OUT/bench_prof.json" 2> "$GRAFT_REPO_ROOT/$OUT/prof.err"
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --cpu-seconds 0 --no-latency > "$GRAFT_REPO_ROOT/$OUT/bench_prof.json" 2> "$GRAFT_REPO_ROOT/$OUT/prof.err"
 
 cd "$GRAFT_REPO_ROOT"
 # PMC passes (separate rocprofv3 runs) -> HBM traffic per split-layer launch

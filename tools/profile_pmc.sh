@@ -5,7 +5,7 @@
 set -e
 OUT=${1:-gpurun_out/pmc}; shift || true
 ARGS="$@"
-[ -z "$ARGS" ] && ARGS="--utts 32 --steps 1 --warmup 1 --cpu-seconds 0"
+[ -z "$ARGS" ] && ARGS="--utts 32 --steps 1 --warmup 1 --cpu-seconds 0 --no-latency"
 export TMPDIR=/tmp
 mkdir -p "$OUT"
 i=0
