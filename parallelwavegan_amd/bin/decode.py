@@ -6,7 +6,9 @@ Same arguments for the mel-to-wave case (--dumpdir with ``*-feats.npy`` files, -
 --checkpoint, --config, --normalize-before, --verbose) and the same outputs
 (``{outdir}/{utt_id}_gen.wav``, PCM_16, and the mean per-utterance RTF in the log). Differences:
   * utterances are decoded in ragged BATCHES of up to --batch-frames mel frames per engine pass
-    (the reference runs one utterance per call); the logged RTF is per batch wall time / audio;
+    (the reference runs one utterance per call), by default sized from the free device memory;
+    the logged RTF is per batch wall time / audio;
+  * features are read lazily: lengths from the .npy headers, data per batch of the rank's shard;
   * under ``torch.distributed.run`` every rank decodes its LPT share of the utterances on its own
     GPU (sharding.decode_sharded) and writes its own wavs;
   * --scp (kaldiio), hdf5 dumps and --use-f0 are not available in this image: they raise.
@@ -22,6 +24,26 @@ import numpy as np
 import torch
 
 
+def engines_of(model):
+    """The HIP engine(s) a drop-in module holds (PWG: one; MelGAN: one per PQMF setting)."""
+    if hasattr(model, "_engines"):
+        return [e[0] for e in model._engines.values()]
+    return [model.engine()]
+
+
+def auto_batch_frames(model, device, frac=0.25, cap_gib=8.0, probe_frames=512):
+    """Mel frames per ragged engine pass that fit ``frac`` of the free device memory (at most
+    ``cap_gib``): the plan workspace of a probe batch per audio sample, plus the caller's mel input
+    (4 B x channels per frame) and noise / output (4 B per sample and channel)."""
+    eng = model.engine()
+    hop = int(getattr(model, "upsample_factor", None) or eng.hop)
+    plan = eng.plan([probe_frames])
+    per_frame = plan.workspace_bytes / probe_frames + 4 * 80 + 4 * hop * 3
+    free, _ = torch.cuda.mem_get_info(device)
+    budget = min(free * frac, cap_gib * (1 << 30))
+    return max(probe_frames, int(budget // per_frame))
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description="Decode dumped features with the MI355X generator engine.")
     ap.add_argument("--scp", default=None, type=str)
@@ -33,8 +55,11 @@ def main(argv=None):
     ap.add_argument("--normalize-before", default=False, action="store_true")
     ap.add_argument("--verbose", type=int, default=1)
     ap.add_argument("--use-f0", default=False, action="store_true")
-    ap.add_argument("--batch-frames", type=int, default=200000,
-                    help="max mel frames per engine pass (ragged batch)")
+    ap.add_argument("--batch-frames", type=int, default=None,
+                    help="max mel frames per engine pass (ragged batch); default: sized from free device "
+                         "memory (--batch-mem-frac of it, at most --batch-mem-gib)")
+    ap.add_argument("--batch-mem-frac", type=float, default=0.25)
+    ap.add_argument("--batch-mem-gib", type=float, default=8.0)
     args = ap.parse_args(argv)
 
     level = logging.DEBUG if args.verbose > 1 else (logging.INFO if args.verbose > 0 else logging.WARN)
@@ -78,10 +103,14 @@ def main(argv=None):
 
     files = find_files(args.dumpdir, "*-feats.npy")
     utt_ids = [os.path.basename(f).replace("-feats.npy", "") for f in files]
-    feats = [np.load(f, allow_pickle=False) for f in files]
-    lengths = [int(f.shape[0]) for f in feats]
+    # lengths from the .npy headers only (memory-mapped, nothing read); each rank loads the
+    # features of its own shard, one batch at a time
+    lengths = [int(np.load(f, mmap_mode="r", allow_pickle=False).shape[0]) for f in files]
     logging.info(f"The number of features to be decoded = {len(files)}.")
     sr = config["sampling_rate"]
+    if args.batch_frames is None:
+        args.batch_frames = auto_batch_frames(model, device, args.batch_mem_frac, args.batch_mem_gib)
+        logging.info(f"batch size: {args.batch_frames} mel frames per engine pass")
 
     def decode(idx):
         outs = [None] * len(idx)
@@ -92,7 +121,8 @@ def main(argv=None):
             nonlocal batch, nfr, total_rtf, n
             if not batch:
                 return
-            cs = [torch.from_numpy(np.ascontiguousarray(feats[i], np.float32)) for _, i in batch]
+            cs = [torch.from_numpy(np.ascontiguousarray(np.load(files[i], allow_pickle=False), np.float32))
+                  for _, i in batch]
             start = time.time()
             with torch.no_grad():
                 ys = model.inference_batch(cs, normalize_before=args.normalize_before)
@@ -117,6 +147,8 @@ def main(argv=None):
 
     local = sharding.decode_sharded(lengths, decode)
     logging.info(f"rank {rank}: wrote {len(local)} utterances to {config['outdir']}")
+    for eng in engines_of(model):
+        eng.release_workspace()
     if world > 1:
         import torch.distributed as dist
 

@@ -242,7 +242,7 @@ class CnetEngine:
         self.packed_weight_count = L.pwg_cnet_packed_weight_count(h)
         self.packed = None
         self._plans = OrderedDict()
-        self._workspace = None
+        self._workspaces = {}
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -273,11 +273,23 @@ class CnetEngine:
             self._plans.move_to_end(key)
         return p
 
-    def workspace(self, nbytes):
-        if self._workspace is None or self._workspace.numel() < nbytes:
-            self._workspace = None
-            self._workspace = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=self.device)
-        return self._workspace
+    def workspace(self, nbytes, stream=None):
+        """The cached workspace of ``stream`` (default: the current stream), grown to ``nbytes``
+        and allocated on that stream: runs on different streams never share buffers."""
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device)
+        key = stream.cuda_stream
+        ws = self._workspaces.get(key)
+        if ws is None or ws.numel() < nbytes:
+            self._workspaces.pop(key, None)
+            with torch.cuda.stream(stream):
+                ws = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=self.device)
+            self._workspaces[key] = ws
+        return ws
+
+    def release_workspace(self):
+        """Drop the cached workspaces (the caching allocator keeps the memory for reuse)."""
+        self._workspaces = {}
 
     @property
     def out_channels(self):
@@ -302,9 +314,9 @@ class CnetEngine:
             mean = mean.to(self.device, torch.float32).contiguous()
             scale = scale.to(self.device, torch.float32).contiguous()
             mp, sp = mean.data_ptr(), scale.data_ptr()
-        ws = self.workspace(plan.workspace_bytes)
         if stream is None:
             stream = torch.cuda.current_stream(self.device)
+        ws = self.workspace(plan.workspace_bytes, stream)
         _lib.check(self._lib.pwg_cnet_run(plan._p, self.packed.data_ptr(), mel.data_ptr(), mp, sp, out.data_ptr(),
                                           ws.data_ptr(), stream.cuda_stream))
         return out

@@ -37,6 +37,16 @@
 #else
 #define PWG16_LD_SKIP(p) (*(p))
 #endif
+// Write-through stores that drop the line from the XCD's L2 (buffer store, cache policy
+// PWG_SPLIT16_SC1_AUX = sc1): bit 0 the skip stream, bit 1 the x stream. Neither is re-read within
+// the layer, so keeping their lines in L2 only shortens the life of the x rows the dilated taps
+// re-read (rocprofv3: x reads fetch 1.65x their bytes, profiles/r02_pmc1).
+#ifndef PWG_SPLIT16_SC1
+#define PWG_SPLIT16_SC1 0
+#endif
+#ifndef PWG_SPLIT16_SC1_AUX
+#define PWG_SPLIT16_SC1_AUX 16
+#endif
 #ifndef PWG_SPLIT16_DIAG_NOTAP
 #define PWG_SPLIT16_DIAG_NOTAP 0
 #endif
@@ -45,6 +55,14 @@
 // streams on chip across layers (cross-layer fusion) could save with the layer's arithmetic unchanged.
 #ifndef PWG_SPLIT16_DIAG_L2
 #define PWG_SPLIT16_DIAG_L2 0
+#endif
+// Tap prefetch schedule. 0: tap 0 of block i+1 is loaded during block i's center-tap MFMAs, the
+// other and center taps of a block at its own start (half a GEMM-1 ahead of use). 1: all three taps
+// of block i+1 are in flight before block i's GEMM 2 (the "other" and center taps after the gate,
+// into the registers GEMM 1's B operands free), so they get GEMM 2 + the epilogue to arrive.
+// 2: as 1 with the other tap issued before the gate.
+#ifndef PWG_SPLIT16_PF
+#define PWG_SPLIT16_PF 0
 #endif
 #ifndef PWG_SPLIT16_MG
 #define PWG_SPLIT16_MG 4  // GEMM-1 m-tiles whose A fragments are read per group
@@ -141,6 +159,16 @@ __device__ __forceinline__ Pair16 split_pair16(float v0, float v1) {
 // 256 dwords (1 KB) apart
 __device__ __forceinline__ size_t row16(int c, int g) {
   return (size_t)(c >> 5) * 2048 + (size_t)((c >> 4) & 1) * 1024 + (size_t)g * 64 + (size_t)(c & 15) * 4;
+}
+
+// 16-byte store through a buffer resource based at the wave-uniform tile address `base`
+// (PWG_SPLIT16_SC1); byte offsets stay inside the 8 KB tile
+__device__ __forceinline__ void st16_policy(const void* base, unsigned byte_off, u32x4 v) {
+  const unsigned long long b = (unsigned long long)base;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b), hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
+  void* ub = (void*)(((unsigned long long)hi << 32) | lo);
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(ub, 0, 0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, byte_off, 0, PWG_SPLIT16_SC1_AUX);
 }
 
 // PWG_SPLIT16_DIAG_L2 column folding (identity in the product build)
@@ -304,8 +332,16 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
   if (nblk >= x_end) nblk = -1;
   if (blk < 0) return;
   BlockDesc bdn = a.blocks[blk];
-  u32x4 b0[8], b1[8];
+  constexpr int T1 = TC == 1 ? 2 : 1;  // the non-center tap after tap 0
+  // prefetch schedule (PWG_SPLIT16_PF; layer 0 with the fused first_conv builds its taps with VALU
+  // and keeps schedule 0: the deeper one spills there)
+  constexpr int PF = FIRST ? 0 : PWG_SPLIT16_PF;
+  u32x4 b0[8], b1[8], b2[8];  // b2: center tap (PF > 0)
   bload(bdn, 0, b0);
+  if constexpr (PF > 0) {
+    bload(bdn, T1, b1);
+    bload(bdn, TC, b2);
+  }
   // LAST: any live column whose final skip sum is not finite. In the pair split an x, D or
   // first_conv value beyond the fp16 range becomes (inf, -inf), which every later product turns into
   // NaN and every skip sum downstream carries (the head's ReLU would hide it), so one check here
@@ -384,15 +420,23 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
       }
 
 #endif
-    constexpr int T1 = TC == 1 ? 2 : 1;
-    bload(bd, T1, b1);
-    mma_tap(acc, b0, 0);
-    load_dv();
-    bload(bd, TC, b0);
-    mma_tap(acc, b1, T1);
-    bload(bdn, 0, b1);  // the next block's (bdn = bd when there is none)
-    mma_tap(acc, b0, TC);
-    if (!LAST) x_seed(b0, acc2);
+    if constexpr (PF > 0) {
+      mma_tap(acc, b0, 0);
+      load_dv();
+      mma_tap(acc, b1, T1);
+      bload(bdn, 0, b0);  // the next block's (bdn = bd when there is none)
+      mma_tap(acc, b2, TC);
+      if (!LAST) x_seed(b2, acc2);
+    } else {
+      bload(bd, T1, b1);
+      mma_tap(acc, b0, 0);
+      load_dv();
+      bload(bd, TC, b0);
+      mma_tap(acc, b1, T1);
+      bload(bdn, 0, b1);  // the next block's (bdn = bd when there is none)
+      mma_tap(acc, b0, TC);
+      if (!LAST) x_seed(b0, acc2);
+    }
 
     int ticket = 0;
     if (nblk >= 0) ticket = ticket_issue();
@@ -434,6 +478,7 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
       }
     }
 
+    if constexpr (PF == 2) bload(bdn, T1, b1);
     // ---- gate -> GEMM-2 B pairs: k-step ks element j = channel chan16(ks, g, j) = acc row
     u32x4 gh[2][2], gl[2][2];  // [nt][ks]
 #pragma unroll
@@ -449,6 +494,8 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
         split8x<0>(gv, gh[nt][ks], gl[nt][ks]);
       }
 
+    if constexpr (PF == 1) bload(bdn, T1, b1);
+    if constexpr (PF > 0) bload(bdn, TC, b2);
     // ---- GEMM 2: [skip; out] rows, 8 m-tiles (last layer: the 4 skip tiles)
     constexpr int M2 = LAST ? 4 : 8;
     const u32x4* w2l = reinterpret_cast<const u32x4*>(s_w2) + lane;
@@ -475,13 +522,21 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
       }
 
     if (!LAST) {
+      // tile bases (wave-uniform) and the lane's byte offset inside a tile, for policy stores
+      const size_t tile_dw = (size_t)(bd.col >> 5) * 2048;
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
         const int col = bd.col + 16 * nt + c;
         const bool live = bd.t0 + 16 * nt + c < bd.T;
+        const unsigned lane_b = (unsigned)(row16(col, g) - tile_dw) * 4u;
         f32x4* sp = reinterpret_cast<f32x4*>(a.skip + row16(diag_col<2>(col, xcd), g));
 #pragma unroll
-        for (int ms = 0; ms < 4; ++ms) PWG16_ST(sp + ms * 64, acc2[ms][nt]);
+        for (int ms = 0; ms < 4; ++ms) {
+          if constexpr ((PWG_SPLIT16_SC1 & 1) != 0)
+            st16_policy(a.skip + tile_dw, lane_b + ms * 1024u, __builtin_bit_cast(u32x4, acc2[ms][nt]));
+          else
+            PWG16_ST(sp + ms * 64, acc2[ms][nt]);
+        }
         u32x4* xp = reinterpret_cast<u32x4*>(a.x_out + row16(diag_col<1>(col, xcd), g));
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
@@ -497,8 +552,13 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
               vl[k] = live ? vl[k] : 0u;
             }
           }
-          PWG16_ST(xp + (ks * 2) * 64, vh);
-          PWG16_ST(xp + (ks * 2 + 1) * 64, vl);
+          if constexpr ((PWG_SPLIT16_SC1 & 2) != 0) {
+            st16_policy(a.x_out + tile_dw, lane_b + (ks * 2) * 1024u, vh);
+            st16_policy(a.x_out + tile_dw, lane_b + (ks * 2 + 1) * 1024u, vl);
+          } else {
+            PWG16_ST(xp + (ks * 2) * 64, vh);
+            PWG16_ST(xp + (ks * 2 + 1) * 64, vl);
+          }
         }
       }
     } else {
@@ -569,8 +629,10 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
     if (nblk < 0) break;
     blk = nblk;
     nblk = ticket_resolve(ticket);
+    if constexpr (PF == 0) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) b0[i] = b1[i];
+      for (int i = 0; i < 8; ++i) b0[i] = b1[i];
+    }
   }
   if (LAST && nonfinite && a.range_flag)
     __hip_atomic_fetch_or(a.range_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

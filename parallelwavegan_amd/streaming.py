@@ -22,15 +22,30 @@ import math
 import torch
 
 
+def upsample_reach_frames(scales, causal):
+    """Input frames the FIR chain reaches from one output sample (layers/upsample.py:97-103,
+    112-128): stage i filters at rate prod(s_1..s_i) with s_i taps per side (2 s_i to the left,
+    causal), i.e. 1 / prod(s_1..s_{i-1}) frames (2x causal). Summed over stages: <= 2 (<= 4)."""
+    reach, prev = 0.0, 1
+    for s in scales:
+        reach += (2.0 if causal else 1.0) / prev
+        prev *= int(s)
+    return reach
+
+
 def halo_frames(engine, causal=None):
-    """Context frames a chunk needs on each side (left only for causal generators)."""
+    """Context frames a chunk needs on each side (left only for causal generators): the WaveNet
+    stack's reach in samples (models/parallel_wavegan.py:197-211) over the hop, plus the FIR
+    chain's reach (upsample_reach_frames), plus conv_in's aux_context_window, plus one frame for
+    the sample's position inside its frame."""
     cfg = engine.config
     causal = bool(cfg.use_causal_conv) if causal is None else causal
     rf = int(engine.receptive_field_size)
     reach = rf - 1 if causal else (rf - 1) // 2
     H = int(engine.upsample_factor)
-    # + conv_in context, + the FIR chain and the engine's edge tables (< 3 frames)
-    return int(math.ceil(reach / H)) + int(cfg.aux_context_window) + 3
+    scales = [int(cfg.upsample_scales[i]) for i in range(int(cfg.num_scales))]
+    up = upsample_reach_frames(scales, causal)
+    return int(math.ceil(reach / H + up)) + int(cfg.aux_context_window) + 1
 
 
 def chunk_ranges(frames, chunk_frames, halo, causal=False):

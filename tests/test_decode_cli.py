@@ -76,8 +76,9 @@ def test_pcm16_wav_round_trip(tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("batch", ["20", None], ids=["batch20", "auto"])
 @pytest.mark.parametrize("name", ["reference_test", "mb_melgan_test", "hifigan_noadd_test"])
-def test_decode_cli_end_to_end(name, tmp_path, built_lib, cuda_device):
+def test_decode_cli_end_to_end(name, batch, tmp_path, built_lib, cuda_device):
     from parallelwavegan_amd.bin import decode
 
     ckpt, state, A = _make_ckpt(str(tmp_path), name)
@@ -88,8 +89,10 @@ def test_decode_cli_end_to_end(name, tmp_path, built_lib, cuda_device):
         np.save(dump / f"{u}-feats.npy", synthetic.make_mel(f, A, seed=50 + i))
     out = tmp_path / "wav"
     torch.manual_seed(0)
-    assert decode.main(["--dumpdir", str(dump), "--outdir", str(out), "--checkpoint", ckpt,
-                        "--batch-frames", "20", "--verbose", "0"]) == 0
+    argv = ["--dumpdir", str(dump), "--outdir", str(out), "--checkpoint", ckpt, "--verbose", "0"]
+    if batch is not None:
+        argv += ["--batch-frames", batch]  # else sized from free device memory
+    assert decode.main(argv) == 0
     m = load_model(ckpt)
     m.remove_weight_norm()
     m = m.eval().to(cuda_device)

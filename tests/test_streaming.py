@@ -64,6 +64,35 @@ def test_causal_stream_equals_whole_utterance(name, built_lib, cuda_device):
     np.testing.assert_array_equal(np.concatenate(outs, 0), full)
 
 
+def test_upsample_reach_frames():
+    assert streaming.upsample_reach_frames([4, 4, 4, 4], False) == pytest.approx(1 + 1 / 4 + 1 / 16 + 1 / 64)
+    assert streaming.upsample_reach_frames([2] * 8, True) == pytest.approx(2 * (2 - 2 ** -7))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("causal", [False, True], ids=["noncausal", "causal"])
+def test_many_small_scales_chunked_and_streamed(causal, built_lib, cuda_device):
+    """Eight x2 upsample stages (hop 256): the FIR chain reaches ~2 frames (~4 causal), more than
+    a constant allowance covered; chunking and streaming stay bit-identical."""
+    from parallelwavegan_amd import synthetic
+
+    eng = _engine("reference_test", cuda_device, use_causal_conv=causal,
+                  upsample_params={"upsample_scales": [2] * 8})
+    A, H = eng.config.aux_channels, eng.upsample_factor
+    frames = 90
+    mel = torch.from_numpy(synthetic.make_mel(frames, A, seed=7)).to(cuda_device)
+    noise = torch.from_numpy(synthetic.make_noise(frames * H, seed=8)).to(cuda_device).reshape(-1)
+    full = eng.infer([mel], [noise])[0].cpu().numpy()
+    np.testing.assert_array_equal(streaming.infer_chunked(eng, mel, noise, 11).cpu().numpy(), full)
+    if causal:
+        st = streaming.CausalStream(eng)
+        outs, f = [], 0
+        for n in (1, 3, 17, 5, 64):
+            outs.append(st.push(mel[f:f + n], noise[f * H:(f + n) * H]).cpu().numpy())
+            f += n
+        np.testing.assert_array_equal(np.concatenate(outs, 0), full)
+
+
 @pytest.mark.gpu
 def test_causal_stream_rejects_noncausal(built_lib, cuda_device):
     eng = _engine("reference_test", cuda_device)
