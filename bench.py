@@ -413,6 +413,8 @@ def main():
     ap.add_argument("--cpu-utts", type=int, default=4,
                     help="CPU baseline sample: utterances of BASELINE.md sec 4's stratified subset (16 = all of it)")
     ap.add_argument("--no-latency", action="store_true", help="skip the B=1 / B=16 latency rows")
+    ap.add_argument("--sub-plans", type=int, default=1,
+                    help="experiment: run the per-GPU utterances as this many sequential sub-batches")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "layer_traffic.json"))
     ap.add_argument("--layer-kernel", default=None, choices=["split", "split16", "persistent", "tiled"],
                     help="default: split where the shape allows, else persistent (the engine default)")
@@ -485,10 +487,28 @@ def main():
     mel = torch.from_numpy(rs.standard_normal(int(lengths.sum()) * A).astype(np.float32)).to(dev)
     noise = torch.from_numpy(rs.standard_normal(plan.total_samples).astype(np.float32)).to(dev)
     out = torch.empty(plan.total_samples * params["out_channels"], dtype=torch.float32, device=dev)
+    subs = None
+    if args.sub_plans > 1:
+        # sequential sub-batches of consecutive utterances (views into the same buffers)
+        subs, f0 = [], 0
+        for part in np.array_split(np.arange(len(lengths)), args.sub_plans):
+            fl = [int(lengths[i]) for i in part]
+            sp = eng.plan(fl)
+            n = sum(fl)
+            subs.append((sp, mel[f0 * A:(f0 + n) * A], noise[f0 * H:(f0 + n) * H],
+                         out[f0 * H * params["out_channels"]:(f0 + n) * H * params["out_channels"]]))
+            f0 += n
     torch.cuda.synchronize(dev)
 
+    def run_step():
+        if subs is None:
+            eng.run(plan, mel, noise, out, check=False)
+        else:
+            for sp, m_, n_, o_ in subs:
+                eng.run(sp, m_, n_, o_, check=False)
+
     for _ in range(args.warmup):
-        eng.run(plan, mel, noise, out, check=False)
+        run_step()
     torch.cuda.synchronize(dev)
 
     eng.set_timing(True)
@@ -498,7 +518,7 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        eng.run(plan, mel, noise, out, check=False)
+        run_step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
