@@ -16,10 +16,15 @@
  *                     + res[o, t] + (accumulate ? y_old[o, t] : 0) ) / out_div )
  *
  * pre = optional (x - mean)/scale (first op) then LeakyReLU(pre_slope) (slope 1 = identity);
- * taps outside an utterance read zeros (PWG_PAD_ZERO, Conv1d padding=) or the mirrored sample
- * (PWG_PAD_REFLECT, ReflectionPad1d); post = none | LeakyReLU | tanh.
+ * taps outside an utterance read zeros (PWG_PAD_ZERO, Conv1d padding=), the mirrored sample
+ * (PWG_PAD_REFLECT, ReflectionPad1d) or the nearest edge sample (PWG_PAD_REPLICATE,
+ * ReplicationPad1d); post = none | LeakyReLU | tanh. A causal conv (layers/causal_conv.py:12-40,
+ * CausalConv1d: pad (K-1)*dil on the left, keep the first T outputs) is pad = (K-1)*dil.
  * PWG_CNET_CONVT is ConvTranspose1d(kernel 2*stride): split into `stride` output phases, each a
- * 2-tap conv of the input (models/melgan.py:86-100, models/hifigan.py:96-107).
+ * 2-tap conv of the input (models/melgan.py:86-100, models/hifigan.py:96-107). With its source's
+ * pad_mode = PWG_PAD_REPLICATE and padding = output_padding = 0 it is CausalConvTranspose1d
+ * (layers/causal_conv.py:43-78: ReplicationPad1d((1, 0)), ConvTranspose1d, trim stride on both
+ * sides), i.e. y[q*s + r] = W[:, :, r] x[q] + W[:, :, r + s] x[max(q - 1, 0)].
  * PWG_CNET_PQMF is PQMF.synthesis (layers/pqmf.py:133-149) with host-supplied filters.
  *
  * Buffers are time-major [rows][ld] fp32 (ld = channels rounded up to 16); buffer b of a plan
@@ -40,7 +45,7 @@ extern "C" {
 #define PWG_CNET_ABI_VERSION 1
 
 enum { PWG_CNET_CONV = 0, PWG_CNET_CONVT = 1, PWG_CNET_PQMF = 2 };
-enum { PWG_PAD_ZERO = 0, PWG_PAD_REFLECT = 1 };
+enum { PWG_PAD_ZERO = 0, PWG_PAD_REFLECT = 1, PWG_PAD_REPLICATE = 2 };
 enum { PWG_ACT_NONE = 0, PWG_ACT_LRELU = 1, PWG_ACT_TANH = 2 };
 
 typedef struct PwgCnetSrc {

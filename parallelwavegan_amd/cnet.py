@@ -18,7 +18,7 @@ from . import _lib
 from .engine import fold_weight_norm
 
 CONV, CONVT, PQMF = 0, 1, 2
-PAD_ZERO, PAD_REFLECT = 0, 1
+PAD_ZERO, PAD_REFLECT, PAD_REPLICATE = 0, 1, 2
 ACT_NONE, ACT_LRELU, ACT_TANH = 0, 1, 2
 
 CNET_SYMBOLS = tuple(n for n in _lib.EXPORTED_SYMBOLS if n.startswith("pwg_cnet_"))

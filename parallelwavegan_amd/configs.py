@@ -117,7 +117,28 @@ VOCODER_PARAMS = {
                                                     nonlinear_activation_params={"negative_slope": 0.1},
                                                     use_weight_norm=True)),
 }
-VOCODER_PQMF = {"mb_melgan_v2": dict(subbands=4), "mb_melgan_test": dict(subbands=4)}
+
+def _causal(name, **over):
+    cls, p = VOCODER_PARAMS[name]
+    p = copy.deepcopy(p)
+    p.update(use_causal_conv=True, **over)
+    return cls, p
+
+
+# causal variants (models/melgan.py:73-151, models/hifigan.py:83-164, layers/causal_conv.py;
+# the reference's causality tests use odd and mixed upsample scales, test/test_hifigan.py:163-196,
+# test/test_melgan.py:267-274)
+VOCODER_PARAMS.update({
+    "melgan_causal_test": _causal("melgan_test"),
+    "mb_melgan_causal_test": _causal("mb_melgan_test", upsample_scales=[3, 2]),
+    "hifigan_causal_test": _causal("hifigan_test", upsample_scales=[5, 3], upsample_kernel_sizes=[10, 6]),
+    "hifigan_noadd_causal_test": _causal("hifigan_noadd_test"),
+    "mb_melgan_v2_causal": _causal("mb_melgan_v2"),
+    "hifigan_v1_causal": _causal("hifigan_v1"),
+    "melgan_v1_causal": _causal("melgan_v1"),
+})
+VOCODER_PQMF = {"mb_melgan_v2": dict(subbands=4), "mb_melgan_test": dict(subbands=4),
+                "mb_melgan_v2_causal": dict(subbands=4), "mb_melgan_causal_test": dict(subbands=4)}
 SAMPLING_RATE.update(melgan_v1=22050, mb_melgan_v2=22050, hifigan_v1=22050)
 
 

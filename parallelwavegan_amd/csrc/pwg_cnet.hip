@@ -105,6 +105,19 @@ __device__ __forceinline__ int reflect_row(int p, int T) {
   return p < 0 ? 0 : (p >= T ? T - 1 : p);  // masked columns / tiny T: stay in bounds
 }
 
+// Row p of a T-row utterance under the source's edge mode, clamped in bounds; false: the tap reads
+// zero (PWG_PAD_ZERO outside the utterance). REFLECT mirrors (ReflectionPad1d), REPLICATE takes
+// the edge row (ReplicationPad1d: CausalConvTranspose1d's left pad).
+__device__ __forceinline__ bool edge_row(int& p, int T, int mode) {
+  if (mode == PWG_PAD_REFLECT) {
+    p = reflect_row(p, T);
+    return true;
+  }
+  const bool inside = p >= 0 && p < T;
+  p = p < 0 ? 0 : (p >= T ? T - 1 : p);
+  return inside || mode == PWG_PAD_REPLICATE;
+}
+
 typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x8v __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
@@ -150,12 +163,7 @@ __global__ void __launch_bounds__(256) pwg_cnet_conv_kernel(const CnConvArgs a) 
 #pragma unroll
     for (int n = 0; n < NT; ++n) {
       int p = qb + 32 * n + cd.row_off;
-      bool ok = true;
-      if (s.pad_mode == PWG_PAD_REFLECT) p = reflect_row(p, sg.y);
-      else {
-        ok = p >= 0 && p < sg.y;
-        p = p < 0 ? 0 : (p >= sg.y ? sg.y - 1 : p);
-      }
+      const bool ok = edge_row(p, sg.y, s.pad_mode);
       r.v[n] = *reinterpret_cast<const f32x8v*>(s.x + (size_t)(sg.x + p) * s.ld + ch);
       r.ok[n] = ok;
     }
@@ -932,12 +940,7 @@ __global__ void __launch_bounds__(128) pwg_cnet_thin_kernel(const CnConvArgs a, 
       for (int i = threadIdx.x; i < s.span * 4; i += 128) {
         const int r = i >> 2, qd = i & 3;
         int p = blk.y + s.off_min + r;
-        bool ok = true;
-        if (s.pad_mode == PWG_PAD_REFLECT) p = reflect_row(p, sg.y);
-        else {
-          ok = p >= 0 && p < sg.y;
-          p = p < 0 ? 0 : (p >= sg.y ? sg.y - 1 : p);
-        }
+        const bool ok = edge_row(p, sg.y, s.pad_mode);
         const int ch = 16 * cb + 4 * qd;
         f32x4v v = *reinterpret_cast<const f32x4v*>(s.x + (size_t)(sg.x + p) * s.ld + ch);
         if (s.normalize) {
@@ -1234,6 +1237,10 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
         return fail(PWG_ERR_INVALID, where + "conv source and destination rates differ");
       }
       if (src.normalize && src.buf != 0) { delete n; return fail(PWG_ERR_INVALID, where + "normalize on a non-input buffer"); }
+      if (src.pad_mode < PWG_PAD_ZERO || src.pad_mode > PWG_PAD_REPLICATE) {
+        delete n;
+        return fail(PWG_ERR_INVALID, where + "bad pad_mode");
+      }
     }
     if (op.res >= 0 && (op.res >= n_bufs || rate[op.res] != rate[op.dst] || channels[op.res] < op.out_channels ||
                         op.res == n_bufs - 1)) {
@@ -1247,9 +1254,16 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
     int n_phase = 1;
     if (op.kind == PWG_CNET_CONVT) {
       const int s = op.stride;
-      if (s < 1 || rate[op.dst] != s * rate[op.src[0].buf] || s - 2 * op.padding + op.output_padding != 0) {
+      // causal (CausalConvTranspose1d): replicate-padded source, no padding, T -> stride*T after the trim
+      const bool causal = op.src[0].pad_mode == PWG_PAD_REPLICATE;
+      if (s < 1 || rate[op.dst] != s * rate[op.src[0].buf] ||
+          (causal ? op.padding != 0 || op.output_padding != 0 : s - 2 * op.padding + op.output_padding != 0)) {
         delete n;
         return fail(PWG_ERR_UNSUPPORTED, where + "ConvTranspose1d must map T -> stride*T (kernel 2*stride)");
+      }
+      if (op.src[0].pad_mode == PWG_PAD_REFLECT) {
+        delete n;
+        return fail(PWG_ERR_UNSUPPORTED, where + "reflection padding on a ConvTranspose1d");
       }
       if (!check_w(op.src[0].w_off, (long long)op.src[0].channels * op.out_channels * 2 * s)) {
         delete n;
@@ -1675,7 +1689,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         CnSrc& d = a.src[si];
         if (si < nsrc) {
           d.x = bufs[src.buf]; d.seg = seg_of(src.buf); d.ld = n->ld[src.buf];
-          d.pad_mode = op.kind == PWG_CNET_CONVT ? PWG_PAD_ZERO : src.pad_mode;
+          d.pad_mode = src.pad_mode;  // CONVT: ZERO, or REPLICATE for the causal form
           d.normalize = src.normalize && mean && scale;  // normalize_before: caller passes stats
           d.slope = src.pre_slope;
           d.taps = ph.thin_taps[si]; d.nc = ph.thin_nc[si]; d.chunk_base = ph.thin_base[si];

@@ -18,7 +18,7 @@ import logging
 import numpy as np
 import torch
 
-from . import cnet
+from . import causal, cnet
 from .engine import WeightTracker
 from .melgan import _slope
 
@@ -30,33 +30,43 @@ class HiFiGANResidualBlock(torch.nn.Module):
                  nonlinear_activation="LeakyReLU", nonlinear_activation_params={"negative_slope": 0.1},
                  use_causal_conv=False):
         super().__init__()
-        if use_causal_conv:
-            raise NotImplementedError("causal HiFiGAN is not supported by the MI355X engine")
         assert kernel_size % 2 == 1, "Kernel size must be odd number."
         self.use_additional_convs = use_additional_convs
+        self.use_causal_conv = bool(use_causal_conv)
         self.kernel_size = kernel_size
         self.dilations = tuple(dilations)
         act = getattr(torch.nn, nonlinear_activation)
+
+        def conv(d):
+            if use_causal_conv:  # layers/residual_block.py:198-241
+                return causal.CausalConv1d(channels, channels, kernel_size, dilation=d, bias=bias)
+            return torch.nn.Conv1d(channels, channels, kernel_size, 1, dilation=d, bias=bias,
+                                   padding=(kernel_size - 1) // 2 * d)
+
         self.convs1 = torch.nn.ModuleList()
         if use_additional_convs:
             self.convs2 = torch.nn.ModuleList()
         for d in dilations:
-            self.convs1 += [torch.nn.Sequential(
-                act(**nonlinear_activation_params),
-                torch.nn.Conv1d(channels, channels, kernel_size, 1, dilation=d, bias=bias,
-                                padding=(kernel_size - 1) // 2 * d))]
+            self.convs1 += [torch.nn.Sequential(act(**nonlinear_activation_params), conv(d))]
             if use_additional_convs:
-                self.convs2 += [torch.nn.Sequential(
-                    act(**nonlinear_activation_params),
-                    torch.nn.Conv1d(channels, channels, kernel_size, dilation=1, bias=bias,
-                                    padding=(kernel_size - 1) // 2))]
+                self.convs2 += [torch.nn.Sequential(act(**nonlinear_activation_params), conv(1))]
 
 
 def _conv_src(P, buf, ch, seq, key, normalize=False):
-    """Source descriptor of Sequential(act, Conv1d) (zero padding from the conv)."""
+    """Source descriptor of Sequential(act, Conv1d | CausalConv1d) (zero padding from the conv)."""
     act, conv = seq[0], seq[1]
+    if isinstance(conv, causal.CausalConv1d):
+        return causal.conv_src(P, buf, ch, conv, key + ".1", _slope(act), normalize=normalize)
     return P.src(buf, ch, conv.kernel_size[0], conv.dilation[0], conv.padding[0], cnet.PAD_ZERO, _slope(act),
                  key + ".1.weight", normalize=normalize)
+
+
+def _conv_bias(seq, key):
+    """State-dict key of the bias of Sequential(act, Conv1d | CausalConv1d) ``key``, or None."""
+    conv = seq[1]
+    if isinstance(conv, causal.CausalConv1d):
+        return key + ".1.conv.bias" if conv.conv.bias is not None else None
+    return key + ".1.bias" if conv.bias is not None else None
 
 
 class HiFiGANGenerator(torch.nn.Module):
@@ -71,33 +81,41 @@ class HiFiGANGenerator(torch.nn.Module):
         assert kernel_size % 2 == 1, "Kernel size must be odd number."
         assert len(upsample_scales) == len(upsample_kernel_sizes)
         assert len(resblock_dilations) == len(resblock_kernel_sizes)
-        if use_causal_conv:
-            raise NotImplementedError("causal HiFiGAN is not supported by the MI355X engine")
         self.num_upsamples = len(upsample_kernel_sizes)
         self.num_blocks = len(resblock_kernel_sizes)
-        self.use_causal_conv = False
+        self.use_causal_conv = bool(use_causal_conv)
         self.in_channels, self.out_channels = in_channels, out_channels
         self.upsample_factor = int(np.prod(upsample_scales))
         act = getattr(torch.nn, nonlinear_activation)
-        self.input_conv = torch.nn.Conv1d(in_channels, channels, kernel_size, bias=bias,
-                                          padding=(kernel_size - 1) // 2)
+        if not use_causal_conv:
+            self.input_conv = torch.nn.Conv1d(in_channels, channels, kernel_size, bias=bias,
+                                              padding=(kernel_size - 1) // 2)
+        else:  # models/hifigan.py:83-88
+            self.input_conv = causal.CausalConv1d(in_channels, channels, kernel_size, bias=bias)
         self.upsamples = torch.nn.ModuleList()
         self.blocks = torch.nn.ModuleList()
         for i in range(len(upsample_kernel_sizes)):
             assert upsample_kernel_sizes[i] == 2 * upsample_scales[i]
             s = upsample_scales[i]
-            self.upsamples += [torch.nn.Sequential(
-                act(**nonlinear_activation_params),
-                torch.nn.ConvTranspose1d(channels // (2 ** i), channels // (2 ** (i + 1)), upsample_kernel_sizes[i], s,
-                                         padding=s // 2 + s % 2, output_padding=s % 2, bias=bias))]
+            cin, cout = channels // (2 ** i), channels // (2 ** (i + 1))
+            if not use_causal_conv:
+                up = torch.nn.ConvTranspose1d(cin, cout, upsample_kernel_sizes[i], s, padding=s // 2 + s % 2,
+                                              output_padding=s % 2, bias=bias)
+            else:  # models/hifigan.py:110-124
+                up = causal.CausalConvTranspose1d(cin, cout, upsample_kernel_sizes[i], s, bias=bias)
+            self.upsamples += [torch.nn.Sequential(act(**nonlinear_activation_params), up)]
             for j in range(len(resblock_kernel_sizes)):
-                self.blocks += [HiFiGANResidualBlock(resblock_kernel_sizes[j], channels // (2 ** (i + 1)),
-                                                     resblock_dilations[j], bias, use_additional_convs,
-                                                     nonlinear_activation, nonlinear_activation_params)]
+                self.blocks += [HiFiGANResidualBlock(resblock_kernel_sizes[j], cout, resblock_dilations[j], bias,
+                                                     use_additional_convs, nonlinear_activation,
+                                                     nonlinear_activation_params, use_causal_conv)]
+        cout = channels // (2 ** (i + 1))
+        if not use_causal_conv:
+            oconv = torch.nn.Conv1d(cout, out_channels, kernel_size, bias=bias, padding=(kernel_size - 1) // 2)
+        else:  # models/hifigan.py:153-164
+            oconv = causal.CausalConv1d(cout, out_channels, kernel_size, bias=bias)
         self.output_conv = torch.nn.Sequential(
             torch.nn.LeakyReLU(),  # slope 0.01, as the reference (models/hifigan.py:149-152)
-            torch.nn.Conv1d(channels // (2 ** (i + 1)), out_channels, kernel_size, bias=bias,
-                            padding=(kernel_size - 1) // 2),
+            oconv,
             torch.nn.Tanh(),
         )
         if use_weight_norm:
@@ -148,21 +166,33 @@ class HiFiGANGenerator(torch.nn.Module):
     def program(self):
         P = cnet.Program(self.in_channels)
         ic = self.input_conv
-        ch = ic.out_channels
-        cur = P.buffer(ch, 1)
-        P.conv("input_conv", cur, ch,
-               [P.src(0, self.in_channels, ic.kernel_size[0], 1, ic.padding[0], cnet.PAD_ZERO, 1.0,
-                      "input_conv.weight", normalize=True)],
-               bias="input_conv.bias" if ic.bias is not None else None)
+        if isinstance(ic, causal.CausalConv1d):
+            ch = ic.conv.out_channels
+            cur = P.buffer(ch, 1)
+            P.conv("input_conv", cur, ch, [causal.conv_src(P, 0, self.in_channels, ic, "input_conv", normalize=True)],
+                   bias="input_conv.conv.bias" if ic.conv.bias is not None else None)
+        else:
+            ch = ic.out_channels
+            cur = P.buffer(ch, 1)
+            P.conv("input_conv", cur, ch,
+                   [P.src(0, self.in_channels, ic.kernel_size[0], 1, ic.padding[0], cnet.PAD_ZERO, 1.0,
+                          "input_conv.weight", normalize=True)],
+                   bias="input_conv.bias" if ic.bias is not None else None)
         rate = 1
         for i in range(self.num_upsamples):
             act, ct = self.upsamples[i][0], self.upsamples[i][1]
-            s = ct.stride[0]
-            rate *= s
             key = f"upsamples.{i}.1"
+            if isinstance(ct, causal.CausalConvTranspose1d):
+                src, s = causal.convt_src(P, cur, ch, ct, key, _slope(act))
+                ct, key, padding, output_padding = ct.deconv, key + ".deconv", 0, 0
+            else:
+                s = ct.stride[0]
+                src = P.src(cur, ch, pre_slope=_slope(act), weight=key + ".weight")
+                padding, output_padding = ct.padding[0], ct.output_padding[0]
+            rate *= s
             up = P.buffer(ct.out_channels, rate)
-            P.convt(key, up, ct.out_channels, P.src(cur, ch, pre_slope=_slope(act), weight=key + ".weight"), s,
-                    ct.padding[0], ct.output_padding[0], bias=key + ".bias" if ct.bias is not None else None)
+            P.convt(key, up, ct.out_channels, src, s, padding, output_padding,
+                    bias=key + ".bias" if ct.bias is not None else None)
             ch = ct.out_channels
             acc = P.buffer(ch, rate)
             for j in range(self.num_blocks):
@@ -177,26 +207,21 @@ class HiFiGANGenerator(torch.nn.Module):
                     fin = dict(accumulate=j > 0, out_div=float(self.num_blocks) if j == self.num_blocks - 1 else 1.0)
                     if blk.use_additional_convs:
                         t = P.buffer(ch, rate)
-                        P.conv(k1, t, ch, [_conv_src(P, x, ch, c1, k1)],
-                               bias=k1 + ".1.bias" if c1[1].bias is not None else None)
+                        P.conv(k1, t, ch, [_conv_src(P, x, ch, c1, k1)], bias=_conv_bias(c1, k1))
                         c2 = blk.convs2[d]
                         k2 = f"{bkey}.convs2.{d}"
                         dst = acc if last else P.buffer(ch, rate)
-                        P.conv(k2, dst, ch, [_conv_src(P, t, ch, c2, k2)],
-                               bias=k2 + ".1.bias" if c2[1].bias is not None else None, res=x,
+                        P.conv(k2, dst, ch, [_conv_src(P, t, ch, c2, k2)], bias=_conv_bias(c2, k2), res=x,
                                **(fin if last else {}))
                     else:
                         dst = acc if last else P.buffer(ch, rate)
-                        P.conv(k1, dst, ch, [_conv_src(P, x, ch, c1, k1)],
-                               bias=k1 + ".1.bias" if c1[1].bias is not None else None, res=x,
+                        P.conv(k1, dst, ch, [_conv_src(P, x, ch, c1, k1)], bias=_conv_bias(c1, k1), res=x,
                                **(fin if last else {}))
                     x = dst
             cur = acc
-        act, oc = self.output_conv[0], self.output_conv[1]
         out = P.buffer(self.out_channels, rate)
-        P.conv("output_conv.1", out, self.out_channels,
-               [P.src(cur, ch, oc.kernel_size[0], 1, oc.padding[0], cnet.PAD_ZERO, _slope(act), "output_conv.1.weight")],
-               bias="output_conv.1.bias" if oc.bias is not None else None, post_act=cnet.ACT_TANH)
+        P.conv("output_conv.1", out, self.out_channels, [_conv_src(P, cur, ch, self.output_conv, "output_conv")],
+               bias=_conv_bias(self.output_conv, "output_conv"), post_act=cnet.ACT_TANH)
         return P
 
     # ------------------------------------------------------------------ engine plumbing

@@ -19,7 +19,7 @@ import logging
 import numpy as np
 import torch
 
-from . import cnet
+from . import causal, cnet
 from .engine import WeightTracker
 
 
@@ -81,23 +81,31 @@ class PQMF(torch.nn.Module):
 
 class ResidualStack(torch.nn.Module):
     """Parameter holder with the reference's sub-module layout (layers/residual_stack.py:13-85):
-    stack = [act, pad, Conv1d(dilated), act, Conv1d 1x1], skip_layer = Conv1d 1x1."""
+    stack = [act, pad, Conv1d(dilated), act, Conv1d 1x1] ([act, CausalConv1d, act, Conv1d 1x1]
+    when causal), skip_layer = Conv1d 1x1."""
 
     def __init__(self, kernel_size=3, channels=32, dilation=1, bias=True, nonlinear_activation="LeakyReLU",
                  nonlinear_activation_params={"negative_slope": 0.2}, pad="ReflectionPad1d", pad_params={},
                  use_causal_conv=False):
         super().__init__()
-        if use_causal_conv:
-            raise NotImplementedError("causal MelGAN is not supported by the MI355X engine")
-        assert (kernel_size - 1) % 2 == 0, "Not support even number kernel size."
         act = getattr(torch.nn, nonlinear_activation)
-        self.stack = torch.nn.Sequential(
-            act(**nonlinear_activation_params),
-            getattr(torch.nn, pad)((kernel_size - 1) // 2 * dilation, **pad_params),
-            torch.nn.Conv1d(channels, channels, kernel_size, dilation=dilation, bias=bias),
-            act(**nonlinear_activation_params),
-            torch.nn.Conv1d(channels, channels, 1, bias=bias),
-        )
+        if not use_causal_conv:
+            assert (kernel_size - 1) % 2 == 0, "Not support even number kernel size."
+            self.stack = torch.nn.Sequential(
+                act(**nonlinear_activation_params),
+                getattr(torch.nn, pad)((kernel_size - 1) // 2 * dilation, **pad_params),
+                torch.nn.Conv1d(channels, channels, kernel_size, dilation=dilation, bias=bias),
+                act(**nonlinear_activation_params),
+                torch.nn.Conv1d(channels, channels, 1, bias=bias),
+            )
+        else:  # residual_stack.py:65-80
+            self.stack = torch.nn.Sequential(
+                act(**nonlinear_activation_params),
+                causal.CausalConv1d(channels, channels, kernel_size, dilation=dilation, bias=bias, pad=pad,
+                                    pad_params=pad_params),
+                act(**nonlinear_activation_params),
+                torch.nn.Conv1d(channels, channels, 1, bias=bias),
+            )
         self.skip_layer = torch.nn.Conv1d(channels, channels, 1, bias=bias)
 
 
@@ -140,28 +148,38 @@ class MelGANGenerator(torch.nn.Module):
         super().__init__()
         assert channels >= np.prod(upsample_scales)
         assert channels % (2 ** len(upsample_scales)) == 0
-        if use_causal_conv:
-            raise NotImplementedError("causal MelGAN is not supported by the MI355X engine")
-        assert (kernel_size - 1) % 2 == 0, "Not support even number kernel size."
+        if not use_causal_conv:
+            assert (kernel_size - 1) % 2 == 0, "Not support even number kernel size."
         act = getattr(torch.nn, nonlinear_activation)
         padm = getattr(torch.nn, pad)
-        mods = [padm((kernel_size - 1) // 2, **pad_params), torch.nn.Conv1d(in_channels, channels, kernel_size, bias=bias)]
+        if not use_causal_conv:
+            mods = [padm((kernel_size - 1) // 2, **pad_params),
+                    torch.nn.Conv1d(in_channels, channels, kernel_size, bias=bias)]
+        else:  # models/melgan.py:73-84
+            mods = [causal.CausalConv1d(in_channels, channels, kernel_size, bias=bias, pad=pad, pad_params=pad_params)]
         ch = channels
         for i, s in enumerate(upsample_scales):
             mods.append(act(**nonlinear_activation_params))
-            mods.append(torch.nn.ConvTranspose1d(ch, ch // 2, s * 2, stride=s, padding=s // 2 + s % 2,
-                                                 output_padding=s % 2, bias=bias))
+            if not use_causal_conv:
+                mods.append(torch.nn.ConvTranspose1d(ch, ch // 2, s * 2, stride=s, padding=s // 2 + s % 2,
+                                                     output_padding=s % 2, bias=bias))
+            else:
+                mods.append(causal.CausalConvTranspose1d(ch, ch // 2, s * 2, stride=s, bias=bias))
             ch //= 2
             for j in range(stacks):
                 mods.append(ResidualStack(stack_kernel_size, ch, stack_kernel_size ** j, bias, nonlinear_activation,
-                                          nonlinear_activation_params, pad, pad_params))
+                                          nonlinear_activation_params, pad, pad_params, use_causal_conv))
         mods.append(act(**nonlinear_activation_params))
-        mods.append(padm((kernel_size - 1) // 2, **pad_params))
-        mods.append(torch.nn.Conv1d(ch, out_channels, kernel_size, bias=bias))
+        if not use_causal_conv:
+            mods.append(padm((kernel_size - 1) // 2, **pad_params))
+            mods.append(torch.nn.Conv1d(ch, out_channels, kernel_size, bias=bias))
+        else:
+            mods.append(causal.CausalConv1d(ch, out_channels, kernel_size, bias=bias, pad=pad, pad_params=pad_params))
         if use_final_nonlinear_activation:
             mods.append(torch.nn.Tanh())
         self.melgan = torch.nn.Sequential(*mods)
         self.in_channels, self.out_channels = in_channels, out_channels
+        self.use_causal_conv = bool(use_causal_conv)
         self.upsample_factor = int(np.prod(upsample_scales))
         if use_weight_norm:
             self.apply_weight_norm()
@@ -235,6 +253,22 @@ class MelGANGenerator(torch.nn.Module):
                 src = P.src(cur, cur_ch, k, d, p, mode, slope, key + ".weight", normalize=first)
                 P.conv(key, dst, m.out_channels, [src], bias=_bias_key(key, m))
                 cur, cur_ch, slope, pad, first = dst, m.out_channels, 1.0, None, False
+            elif isinstance(m, causal.CausalConv1d):
+                if pad is not None:
+                    raise NotImplementedError("padding module before a CausalConv1d")
+                dst = P.buffer(m.conv.out_channels, rate)
+                P.conv(key + ".conv", dst, m.conv.out_channels,
+                       [causal.conv_src(P, cur, cur_ch, m, key, slope, normalize=first)],
+                       bias=_bias_key(key + ".conv", m.conv))
+                cur, cur_ch, slope, first = dst, m.conv.out_channels, 1.0, False
+            elif isinstance(m, causal.CausalConvTranspose1d):
+                if pad is not None:
+                    raise NotImplementedError("padding module before a CausalConvTranspose1d")
+                src, s = causal.convt_src(P, cur, cur_ch, m, key, slope, normalize=first)
+                rate *= s
+                dst = P.buffer(m.deconv.out_channels, rate)
+                P.convt(key + ".deconv", dst, m.deconv.out_channels, src, s, 0, 0, bias=_bias_key(key + ".deconv", m.deconv))
+                cur, cur_ch, slope, first = dst, m.deconv.out_channels, 1.0, False
             elif isinstance(m, torch.nn.ConvTranspose1d):
                 s = m.stride[0]
                 if m.kernel_size[0] != 2 * s or pad is not None:
@@ -247,19 +281,27 @@ class MelGANGenerator(torch.nn.Module):
             elif isinstance(m, ResidualStack):
                 if slope != 1.0 or pad is not None:
                     raise NotImplementedError("activation before a ResidualStack")
-                a0, pd, cd, a1, c1 = m.stack
-                pp, mode = _pad_of(pd)
                 h = P.buffer(cur_ch, rate)
-                P.conv(key + ".stack.2", h, cur_ch,
-                       [P.src(cur, cur_ch, cd.kernel_size[0], cd.dilation[0], pp, mode, _slope(a0),
-                              key + ".stack.2.weight", normalize=first)],
-                       bias=_bias_key(key + ".stack.2", cd))
+                if len(m.stack) == 4:  # causal: [act, CausalConv1d, act, 1x1]
+                    a0, cc, a1, c1 = m.stack
+                    i1 = 3
+                    P.conv(key + ".stack.1.conv", h, cur_ch,
+                           [causal.conv_src(P, cur, cur_ch, cc, key + ".stack.1", _slope(a0), normalize=first)],
+                           bias=_bias_key(key + ".stack.1.conv", cc.conv))
+                else:
+                    a0, pd, cd, a1, c1 = m.stack
+                    i1 = 4
+                    pp, mode = _pad_of(pd)
+                    P.conv(key + ".stack.2", h, cur_ch,
+                           [P.src(cur, cur_ch, cd.kernel_size[0], cd.dilation[0], pp, mode, _slope(a0),
+                                  key + ".stack.2.weight", normalize=first)],
+                           bias=_bias_key(key + ".stack.2", cd))
                 y = P.buffer(cur_ch, rate)
                 # stack(c) + skip_layer(c) as ONE two-source 1x1 op over [lrelu(h); c]
-                P.conv(key + ".stack.4+skip_layer", y, cur_ch,
-                       [P.src(h, cur_ch, pre_slope=_slope(a1), weight=key + ".stack.4.weight"),
+                P.conv(key + f".stack.{i1}+skip_layer", y, cur_ch,
+                       [P.src(h, cur_ch, pre_slope=_slope(a1), weight=key + f".stack.{i1}.weight"),
                         P.src(cur, cur_ch, weight=key + ".skip_layer.weight", normalize=first)],
-                       bias=_bias_key(key + ".stack.4", c1), bias2=_bias_key(key + ".skip_layer", m.skip_layer))
+                       bias=_bias_key(key + f".stack.{i1}", c1), bias2=_bias_key(key + ".skip_layer", m.skip_layer))
                 cur, first = y, False
             elif isinstance(m, torch.nn.Tanh):
                 P.ops[-1]["post_act"] = cnet.ACT_TANH

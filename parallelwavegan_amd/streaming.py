@@ -48,12 +48,21 @@ def halo_frames(engine, causal=None):
     return int(math.ceil(reach / H + up)) + int(cfg.aux_context_window) + 1
 
 
-def chunk_ranges(frames, chunk_frames, halo, causal=False):
-    """[(lo, s, e, hi)]: chunk core [s, e) computed from frames [lo, hi)."""
+def align_frames(hop, block=32):
+    """Chunk starts must be multiples of this many frames for bit-identity. Every layer kernel
+    works in 32-sample blocks counted from the utterance start and places a block's aux frames
+    (frame = t // hop) in MFMA K slots relative to the block's first frame; a chunk that starts
+    off that phase sums the same products in another order (hop 300: every 8 frames)."""
+    return block // math.gcd(int(hop), block)
+
+
+def chunk_ranges(frames, chunk_frames, halo, causal=False, align=1):
+    """[(lo, s, e, hi)]: chunk core [s, e) computed from frames [lo, hi); lo is rounded down to a
+    multiple of ``align`` (at least ``halo`` frames of left context)."""
     out = []
     for s in range(0, frames, chunk_frames):
         e = min(frames, s + chunk_frames)
-        lo = max(0, s - halo)
+        lo = max(0, (s - halo) // align * align)
         hi = e if causal else min(frames, e + halo)
         out.append((lo, s, e, hi))
     return out
@@ -69,7 +78,7 @@ def infer_chunked(engine, mel, noise, chunk_frames, halo=None, mean=None, scale=
     noise = noise.reshape(-1)
     if noise.numel() != F * H:
         raise ValueError("noise must have frames * upsample_factor samples")
-    rng = chunk_ranges(F, int(chunk_frames), halo, causal)
+    rng = chunk_ranges(F, int(chunk_frames), halo, causal, align_frames(H))
     mels = [mel[lo:hi] for lo, _, _, hi in rng]
     noises = [noise[lo * H:hi * H] for lo, _, _, hi in rng]
     outs = engine.infer(mels, noises, mean, scale)
@@ -89,6 +98,7 @@ class CausalStream:
         self.engine = engine
         self.halo = halo_frames(engine) if halo is None else int(halo)
         self.H = int(engine.upsample_factor)
+        self.align = align_frames(self.H)
         self.mean, self.scale = mean, scale
         self._mel = None
         self._noise = None
@@ -109,7 +119,10 @@ class CausalStream:
             z = torch.cat([self._noise, noise], 0)
             ctx = int(self._mel.shape[0])
         y = self.engine.infer([m.contiguous()], [z.contiguous()], self.mean, self.scale)[0]
-        keep = min(self.halo, int(m.shape[0]))
+        # keep >= halo frames so that the next pass starts on an aligned frame (align_frames)
+        total = self.frames_out + n
+        keep = min(self.halo + (total - self.halo) % self.align, int(m.shape[0])) if total > self.halo \
+            else int(m.shape[0])
         self._mel = m[-keep:].clone()
         self._noise = z[-keep * self.H:].clone()
         self.frames_out += n

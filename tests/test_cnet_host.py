@@ -17,7 +17,8 @@ def _holder(name):
     return {"MelGANGenerator": MelGANGenerator, "HiFiGANGenerator": HiFiGANGenerator}[cls](**p)
 
 
-@pytest.mark.parametrize("name", ["mb_melgan_v2", "melgan_v1", "hifigan_v1", "mb_melgan_test", "hifigan_noadd_test"])
+@pytest.mark.parametrize("name", ["mb_melgan_v2", "melgan_v1", "hifigan_v1", "mb_melgan_test", "hifigan_noadd_test",
+                                  "mb_melgan_v2_causal", "hifigan_v1_causal", "hifigan_causal_test"])
 def test_program_covers_every_weight_and_packs(name, built_lib):
     m = _holder(name)
     if isinstance(m, MelGANGenerator) and m.out_channels > 1:
@@ -82,7 +83,7 @@ def test_convt_fragment_layout(built_lib):
         np.testing.assert_array_equal(packed[base + 2048: base + 2080], b)
 
 
-@pytest.mark.parametrize("bad", ["rate", "channels", "dst", "convt_pad"])
+@pytest.mark.parametrize("bad", ["rate", "channels", "dst", "convt_pad", "causal_convt_pad", "convt_reflect"])
 def test_invalid_programs_raise(bad, built_lib):
     P = cnet.Program(16)
     if bad == "rate":
@@ -94,18 +95,43 @@ def test_invalid_programs_raise(bad, built_lib):
     elif bad == "dst":
         out = P.buffer(4, 1)
         P.conv("c", out, 8, [P.src(0, 16, weight="w")])
-    else:
+    elif bad == "convt_pad":
         out = P.buffer(8, 4)
         P.convt("c", out, 8, P.src(0, 16, weight="w"), 4, 1, 0)
+    elif bad == "causal_convt_pad":  # the causal (replicate-padded) form has no padding
+        out = P.buffer(8, 4)
+        P.convt("c", out, 8, P.src(0, 16, weight="w", pad_mode=cnet.PAD_REPLICATE), 4, 2, 0)
+    else:
+        out = P.buffer(8, 4)
+        P.convt("c", out, 8, P.src(0, 16, weight="w", pad_mode=cnet.PAD_REFLECT), 4, 2, 0)
     with pytest.raises((ValueError, NotImplementedError)):
         cnet.CnetEngine(P, None, host_only=True)
 
 
+def test_causal_lowering(built_lib):
+    """CausalConv1d -> pad (K-1)*dil with the pad module's edge mode; CausalConvTranspose1d -> a
+    CONVT op with padding 0 and a replicate-padded source (layers/causal_conv.py:12-78)."""
+    m = _holder("mb_melgan_causal_test")
+    P, _ = m.program(False)
+    first = P.ops[0]["srcs"][0]
+    assert (first["taps"], first["pad"], first["pad_mode"], first["normalize"]) == (7, 6, cnet.PAD_REFLECT, True)
+    convts = [op for op in P.ops if op["kind"] == cnet.CONVT]
+    assert convts and all(op["padding"] == 0 and op["srcs"][0]["pad_mode"] == cnet.PAD_REPLICATE for op in convts)
+    dil = [op["srcs"][0] for op in P.ops if op["srcs"][0]["dilation"] > 1]
+    assert dil and all(s["pad"] == (s["taps"] - 1) * s["dilation"] for s in dil)
+    h = _holder("hifigan_causal_test")
+    assert all(op["srcs"][0]["pad_mode"] == cnet.PAD_ZERO for op in h.program().ops if op["kind"] == cnet.CONV)
+
+
 def test_unsupported_modules_raise():
+    # a causal conv padded with a non-zero constant has no engine edge mode
+    m = MelGANGenerator(**configs.vocoder_params("melgan_causal_test", pad="ConstantPad1d",
+                                                 pad_params={"value": 1.0})[1])
     with pytest.raises(NotImplementedError):
-        MelGANGenerator(use_causal_conv=True)
+        m.program(False)
     with pytest.raises(NotImplementedError):
-        HiFiGANGenerator(use_causal_conv=True)
+        MelGANGenerator(**configs.vocoder_params("melgan_test", nonlinear_activation="ELU",
+                                                 nonlinear_activation_params={}) [1]).program(False)
 
 
 def test_cpu_module_fails_loudly(built_lib):

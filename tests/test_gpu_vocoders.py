@@ -40,7 +40,9 @@ def test_vocoder_golden_vectors(name, split, built_lib, cuda_device):
 
 
 @pytest.mark.parametrize("split", [True, False], ids=["split_f16", "fp32"])
-@pytest.mark.parametrize("cfg, frames", [("mb_melgan_v2", 40), ("hifigan_v1", 12), ("melgan_v1", 16)])
+@pytest.mark.parametrize("cfg, frames", [("mb_melgan_v2", 40), ("hifigan_v1", 12), ("melgan_v1", 16),
+                                         ("mb_melgan_v2_causal", 40), ("hifigan_v1_causal", 12),
+                                         ("melgan_v1_causal", 16)])
 def test_full_size_configs_against_oracle(cfg, frames, split, built_lib, cuda_device):
     from oracle import melgan_numpy
     from parallelwavegan_amd import configs, synthetic
@@ -71,7 +73,7 @@ def test_full_size_configs_against_oracle(cfg, frames, split, built_lib, cuda_de
     assert err < ATOL, f"{cfg}: max|d| = {err:.3e}"
 
 
-@pytest.mark.parametrize("cfg", ["mb_melgan_test", "hifigan_test"])
+@pytest.mark.parametrize("cfg", ["mb_melgan_test", "hifigan_test", "mb_melgan_causal_test", "hifigan_causal_test"])
 def test_ragged_batch_is_bitwise_equal_to_single_utterances(cfg, built_lib, cuda_device):
     from parallelwavegan_amd import configs, synthetic
     from parallelwavegan_amd.hifigan import HiFiGANGenerator
@@ -83,7 +85,7 @@ def test_ragged_batch_is_bitwise_equal_to_single_utterances(cfg, built_lib, cuda
     if cfg in configs.VOCODER_PQMF:
         m.pqmf = PQMF(**configs.VOCODER_PQMF[cfg])
     m = m.to(cuda_device)
-    lengths = [4, 37, 5, 130, 9]
+    lengths = [7, 37, 8, 130, 9] if params.get("use_causal_conv") else [4, 37, 5, 130, 9]
     mels = [synthetic.make_mel(f, 80, seed=30 + i) for i, f in enumerate(lengths)]
     with torch.no_grad():
         batch = [y.cpu().numpy() for y in m.inference_batch(mels)]
@@ -140,3 +142,36 @@ def test_fused_conv_pairs_bitwise_equal_to_unfused(steps, built_lib, cuda_device
     assert sum(1 for _, _, n in t if n == 0) == 18
     for a, b in zip(got, ref):
         np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("cfg, over", [
+    ("hifigan_v1_causal", {"upsample_scales": [5, 5, 4, 3], "upsample_kernel_sizes": [10, 10, 8, 6]}),
+    ("hifigan_v1_causal", {"upsample_scales": [4, 5, 4, 3], "upsample_kernel_sizes": [8, 10, 8, 6]}),
+    ("hifigan_v1_causal", {}),
+    ("melgan_v1_causal", {}),
+    ("melgan_v1_causal", {"upsample_scales": [4, 5, 4, 3]}),
+])
+def test_causal_generators_are_causal(cfg, over, built_lib, cuda_device):
+    """Restates test/test_hifigan.py:198-225 and test/test_melgan.py:275-301: B = 4 utterances of
+    8192 (HiFiGAN) / 4096 (MelGAN) samples through forward(); replacing the second half of the
+    frames leaves the first half of the output bit-identical, and T_out = T' * hop."""
+    from parallelwavegan_amd import configs, synthetic
+    from parallelwavegan_amd.hifigan import HiFiGANGenerator
+    from parallelwavegan_amd.melgan import MelGANGenerator
+
+    cls_name, params = configs.vocoder_params(cfg, **over)
+    m = {"MelGANGenerator": MelGANGenerator, "HiFiGANGenerator": HiFiGANGenerator}[cls_name](**params)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic.make_module_state_dict(m, seed=8).items()})
+    m = m.to(cuda_device).eval()
+    hop = int(np.prod(params["upsample_scales"]))
+    T = (8192 if cls_name == "HiFiGANGenerator" else 4096) // hop
+    g = torch.Generator().manual_seed(0)
+    c = torch.randn(4, 80, T, generator=g)
+    c2 = c.clone()
+    c2[..., T // 2:] = torch.randn(c[..., T // 2:].shape, generator=g)
+    with torch.no_grad():
+        y = m(c.to(cuda_device)).cpu().numpy()
+        y2 = m(c2.to(cuda_device)).cpu().numpy()
+    assert y.shape[2] == T * hop
+    np.testing.assert_array_equal(y[..., :T // 2 * hop], y2[..., :T // 2 * hop])
+    assert not np.array_equal(y, y2)

@@ -16,6 +16,15 @@ def test_chunk_ranges_cover_exactly():
             assert lo == max(0, s - 17) and (hi == e if causal else hi == min(1000, e + 17))
             if nxt:
                 assert nxt[1] == e
+    # aligned starts: lo a multiple of align, at least halo frames of context
+    for lo, s, e, hi in streaming.chunk_ranges(1000, 61, 15, False, align=8):
+        assert lo % 8 == 0 and (lo == 0 or s - lo >= 15) and s - lo < 15 + 8
+
+
+def test_align_frames():
+    assert streaming.align_frames(256) == 1  # LJSpeech hop: every frame starts a block
+    assert streaming.align_frames(300) == 8  # LibriTTS hop: 8 x 300 = 75 x 32
+    assert streaming.align_frames(120) == 4
 
 
 def _engine(name, cuda_device, **over):
@@ -28,7 +37,8 @@ def _engine(name, cuda_device, **over):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name, frames, chunk", [("ljspeech_v1", 300, 64), ("libritts_v1", 161, 40)])
+@pytest.mark.parametrize("name, frames, chunk", [("ljspeech_v1", 300, 64), ("libritts_v1", 161, 40),
+                                                 ("libritts_v1", 171, 37)])
 def test_chunked_equals_whole_utterance(name, frames, chunk, built_lib, cuda_device):
     from parallelwavegan_amd import synthetic
 
@@ -45,7 +55,7 @@ def test_chunked_equals_whole_utterance(name, frames, chunk, built_lib, cuda_dev
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["reference_test", "ljspeech_v1"])
+@pytest.mark.parametrize("name", ["reference_test", "ljspeech_v1", "libritts_v1"])
 def test_causal_stream_equals_whole_utterance(name, built_lib, cuda_device):
     from parallelwavegan_amd import synthetic
 
