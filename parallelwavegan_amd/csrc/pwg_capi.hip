@@ -13,6 +13,10 @@
 #include "../../include/pwg.h"
 #include "pwg_internal.h"
 
+#ifndef PWG_SMALL_SPREAD
+#define PWG_SMALL_SPREAD 1  // small plans: fewer waves per workgroup, every CU (A/B: 0)
+#endif
+
 using namespace pwg;
 
 namespace {
@@ -972,6 +976,12 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
     la.tab.Fmin = h->aux.Fmin; la.nka = h->aux.nka; la.nfwg = h->aux.nfwg;
     la.wg = L0 + h->lo_wg; la.wgp = L0 + h->lo_wgp; la.bg = L0 + h->lo_bg; la.w2 = L0 + h->lo_w2;
     la.n_blocks = p->n_tiles * (TILE / 32);
+    // Small plans (the B = 1 latency path): at most one 32-sample block per wave, spread over every
+    // CU with fewer waves per workgroup, rather than crowding the blocks into the first workgroups
+    // of each XCD at 8 waves per CU.
+    const long long nwg_all = (long long)h->n_cu * h->wg_per_cu;
+    int wpw = h->waves_per_wg;
+    if (PWG_SMALL_SPREAD && la.n_blocks < nwg_all * wpw) wpw = (int)std::max(1LL, (la.n_blocks + nwg_all - 1) / nwg_all);
     la.tile_utt = d_tile_utt; la.utts = d_utts; la.Tpad = p->Tpad;
     la.R = h->R; la.RS = h->RS; la.S = h->S; la.SS = h->SS; la.KS = h->KS; la.dil = h->dil[l];
     la.tap_center = h->cfg.use_causal_conv ? h->KS - 1 : (h->KS - 1) / 2;
@@ -1018,8 +1028,8 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
       sa.trace = d_trace_s + per_layer_s * (l % 64);
 #endif
       e = timed(PWG_KERNEL_RESIDUAL_LAYER, [&] {
-        return split16 ? launch_layer_split16(sa, last, la.tap_center, h->waves_per_wg, nwg, s)
-                       : launch_layer_split(sa, last, la.tap_center, h->waves_per_wg, nwg, s);
+        return split16 ? launch_layer_split16(sa, last, la.tap_center, wpw, nwg, s)
+                       : launch_layer_split(sa, last, la.tap_center, wpw, nwg, s);
       });
 #if PWG_TRACE
       if (e == hipSuccess && last) {
@@ -1066,7 +1076,6 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
         return fail(PWG_ERR_HIP, "trace buffer");
       pa2.trace = d_trace + per_layer * (l % 64);
       if (last) {
-        const int wpw = h->waves_per_wg;
         auto kick = [=, &e]() {
           std::vector<unsigned long long> host(per_layer * h->L);
           e = hipStreamSynchronize(s);
@@ -1083,7 +1092,7 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
           }
         };
         e = timed(PWG_KERNEL_RESIDUAL_LAYER, [&] {
-          return launch_layer_persistent(pa2, h->MT, h->M2T, last, h->waves_per_wg, nwg, s);
+          return launch_layer_persistent(pa2, h->MT, h->M2T, last, wpw, nwg, s);
         });
         if (e == hipSuccess) kick();
         if (e != hipSuccess) return hip_fail(e, "residual layer launch (trace)");
@@ -1092,7 +1101,7 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
       }
 #endif
       e = timed(PWG_KERNEL_RESIDUAL_LAYER, [&] {
-        return launch_layer_persistent(pa2, h->MT, h->M2T, last, h->waves_per_wg, nwg, s);
+        return launch_layer_persistent(pa2, h->MT, h->M2T, last, wpw, nwg, s);
       });
     } else {
       e = timed(PWG_KERNEL_RESIDUAL_LAYER,

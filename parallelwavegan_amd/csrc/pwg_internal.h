@@ -233,4 +233,20 @@ hipError_t launch_layer_split(const SplitArgs& a, bool last, int tap_center, int
 hipError_t launch_layer_persistent(const PersistArgs& a, int mt, int m2t, bool last, int waves_per_wg, int n_wg,
                                    hipStream_t s);
 
+// Copy n 16-byte vectors global -> LDS with the workgroup's nthr threads: 8 loads in flight per
+// thread before their stores (a plain load/store loop waits one L2 round trip per vector, which
+// dominated a layer launch on small plans: 16-64 dependent trips per thread).
+template <typename V>
+__device__ __forceinline__ void stage_lds(V* dst, const V* src, int n, int tid, int nthr) {
+  int i = tid;
+  for (; i + 7 * nthr < n; i += 8 * nthr) {
+    V r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = src[i + j * nthr];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dst[i + j * nthr] = r[j];
+  }
+  for (; i < n; i += nthr) dst[i] = src[i];
+}
+
 }  // namespace pwg

@@ -132,23 +132,34 @@ __global__ void __launch_bounds__(256) pwg_conv_in_mfma_kernel(const ConvInArgs 
     for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
   int i = hh / a.KW, kk = hh - i * a.KW;  // k = 2s + hh = i*KW + kk
   const float* wl = a.wfrag + lane;
-  for (int s = 0; s < nks; ++s) {
-    float x = 0.f;
-    if (i < a.A) {
-      const long long fp = f + kk;
-      if (a.layout == PWG_LAYOUT_INFERENCE) {
-        long long src = fp - a.ctx;
-        src = src < 0 ? 0 : (src >= Tf ? Tf - 1 : src);  // ReplicationPad1d
-        x = a.mel[ud.mel_off + src * a.A + i];
-        if (a.mean != nullptr) x = (x - a.mean[i]) / a.scale[i];
-      } else {
-        x = a.mel[ud.mel_off + (long long)i * Tin + fp];
+  // groups of 8 k-steps: every input and weight load of a group is issued before its MFMAs (one
+  // load at a time made a small plan a chain of ~200 dependent L2 round trips: 90 us at T' = 64)
+  for (int s0 = 0; s0 < nks; s0 += 8) {
+    float x[8], w[8][MT];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int s = s0 + j;
+      x[j] = 0.f;
+      if (s < nks && i < a.A) {
+        const long long fp = f + kk;
+        if (a.layout == PWG_LAYOUT_INFERENCE) {
+          long long src = fp - a.ctx;
+          src = src < 0 ? 0 : (src >= Tf ? Tf - 1 : src);  // ReplicationPad1d
+          x[j] = a.mel[ud.mel_off + src * a.A + i];
+          if (a.mean != nullptr) x[j] = (x[j] - a.mean[i]) / a.scale[i];
+        } else {
+          x[j] = a.mel[ud.mel_off + (long long)i * Tin + fp];
+        }
       }
+#pragma unroll
+      for (int m = 0; m < MT; ++m) w[j][m] = s < nks ? wl[(s * MT + m) * 64] : 0.f;
+      kk += 2;
+      while (kk >= a.KW) { kk -= a.KW; ++i; }
     }
 #pragma unroll
-    for (int m = 0; m < MT; ++m) acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(wl[(s * MT + m) * 64], x, acc[m], 0, 0, 0);
-    kk += 2;
-    while (kk >= a.KW) { kk -= a.KW; ++i; }
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int m = 0; m < MT; ++m) acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(w[j][m], x[j], acc[m], 0, 0, 0);
   }
   if (!valid) return;
 #pragma unroll
@@ -182,13 +193,21 @@ __global__ void __launch_bounds__(256) pwg_aux_proj_kernel(const AuxProjArgs a) 
   for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
-  for (int s = 0; s < nks; ++s) {
-    const int i = 2 * s + hh;
-    const float bv = a.c1[(size_t)(i < a.A ? i : 0) * a.F_total + fc];
-    const float b = i < a.A ? bv : 0.f;
+  for (int s0 = 0; s0 < nks; s0 += 8) {  // groups of 8 k-steps, loads first (as conv_in)
+    float b[8], wv[8][MT];
 #pragma unroll
-    for (int m = 0; m < MT; ++m)
-      acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(w[(s * MT + m) * 64], b, acc[m], 0, 0, 0);
+    for (int j = 0; j < 8; ++j) {
+      const int s = s0 + j;
+      const int i = 2 * s + hh;
+      const float bv = a.c1[(size_t)(i < a.A ? i : 0) * a.F_total + fc];
+      b[j] = i < a.A ? bv : 0.f;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) wv[j][m] = s < nks ? w[(s * MT + m) * 64] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int m = 0; m < MT; ++m) acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(wv[j][m], b[j], acc[m], 0, 0, 0);
   }
   if constexpr (GR == 128) if (a.split == 2) {
     // split16 layout: row r = 16 m16 + c16 of a frame at dword c16 * 8 + m16, so a layer-kernel
@@ -700,19 +719,11 @@ __global__ void __launch_bounds__(PWG_PERSIST_THREADS, 1) pwg_layer_persistent_k
 
   // ---- one-time: this layer's weights into LDS
   {
-    const int nthr = blockDim.x;
-    const f32x4* src = reinterpret_cast<const f32x4*>(a.wgp);
-    f32x4* dst = reinterpret_cast<f32x4*>(s_wg);
-    for (int i = threadIdx.x; i < K1 / 8 * MT * 64; i += nthr) dst[i] = src[i];
-    src = reinterpret_cast<const f32x4*>(a.w2);
-    dst = reinterpret_cast<f32x4*>(s_w2);
-    for (int i = threadIdx.x; i < SM::W2 / 4; i += nthr) dst[i] = src[i];
-    for (int i = threadIdx.x; i < GR; i += nthr) s_bg[i] = a.bg[i];
-    if (LAST) {
-      src = reinterpret_cast<const f32x4*>(a.hw1);
-      dst = reinterpret_cast<f32x4*>(s_hw1);
-      for (int i = threadIdx.x; i < SM::HW1 / 4; i += nthr) dst[i] = src[i];
-    }
+    const int nthr = blockDim.x, tid = (int)threadIdx.x;
+    stage_lds(reinterpret_cast<f32x4*>(s_wg), reinterpret_cast<const f32x4*>(a.wgp), K1 / 8 * MT * 64, tid, nthr);
+    stage_lds(reinterpret_cast<f32x4*>(s_w2), reinterpret_cast<const f32x4*>(a.w2), SM::W2 / 4, tid, nthr);
+    for (int i = tid; i < GR; i += nthr) s_bg[i] = a.bg[i];
+    if (LAST) stage_lds(reinterpret_cast<f32x4*>(s_hw1), reinterpret_cast<const f32x4*>(a.hw1), SM::HW1 / 4, tid, nthr);
     __syncthreads();
   }
 

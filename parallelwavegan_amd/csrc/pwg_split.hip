@@ -192,15 +192,12 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
   float* s_hw1 = s_bo + SplitSmem::BO;
   {
     const int nthr = blockDim.x;
-    const u32x4* src = reinterpret_cast<const u32x4*>(a.wg);
-    u32x4* dst = reinterpret_cast<u32x4*>(s_wg);
-    for (int i = threadIdx.x; i < (SplitSmem::WG + SplitSmem::W2 + SplitSmem::BG + SplitSmem::BO) / 4; i += nthr)
-      dst[i] = src[i];  // the four sections are contiguous in the packed image too
-    if (LAST) {
-      src = reinterpret_cast<const u32x4*>(a.hw1);
-      dst = reinterpret_cast<u32x4*>(s_hw1);
-      for (int i = threadIdx.x; i < SplitSmem::HW1 / 4; i += nthr) dst[i] = src[i];
-    }
+    // the four sections are contiguous in the packed image too
+    stage_lds(reinterpret_cast<u32x4*>(s_wg), reinterpret_cast<const u32x4*>(a.wg),
+              (SplitSmem::WG + SplitSmem::W2 + SplitSmem::BG + SplitSmem::BO) / 4, (int)threadIdx.x, nthr);
+    if (LAST)
+      stage_lds(reinterpret_cast<u32x4*>(s_hw1), reinterpret_cast<const u32x4*>(a.hw1), SplitSmem::HW1 / 4,
+                (int)threadIdx.x, nthr);
     __syncthreads();
   }
 

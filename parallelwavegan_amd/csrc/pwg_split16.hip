@@ -208,15 +208,13 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
   float* s_fwb = reinterpret_cast<float*>(smem16 + Split16Smem::dwords(LAST));  // FIRST: w[64] | b[64]
   {
     const int nthr = blockDim.x;
-    const u32x4* src = reinterpret_cast<const u32x4*>(a.wg);
-    u32x4* dst = reinterpret_cast<u32x4*>(s_wg);
-    for (int i = threadIdx.x; i < SPLIT_LAYER_DWORDS / 4; i += nthr) dst[i] = src[i];
-    if (LAST) {
-      src = reinterpret_cast<const u32x4*>(a.hw1);
-      dst = reinterpret_cast<u32x4*>(s_hw1);
-      for (int i = threadIdx.x; i < Split16Smem::HW1 / 4; i += nthr) dst[i] = src[i];
-    }
-    if (FIRST && threadIdx.x < 128) s_fwb[threadIdx.x] = threadIdx.x < 64 ? a.fw[threadIdx.x] : a.fb[threadIdx.x - 64];
+    stage_lds(reinterpret_cast<u32x4*>(s_wg), reinterpret_cast<const u32x4*>(a.wg), SPLIT_LAYER_DWORDS / 4,
+              (int)threadIdx.x, nthr);
+    if (LAST)
+      stage_lds(reinterpret_cast<u32x4*>(s_hw1), reinterpret_cast<const u32x4*>(a.hw1), Split16Smem::HW1 / 4,
+                (int)threadIdx.x, nthr);
+    if (FIRST)
+      for (int i = threadIdx.x; i < 128; i += nthr) s_fwb[i] = i < 64 ? a.fw[i] : a.fb[i - 64];
     __syncthreads();
   }
 
