@@ -32,7 +32,7 @@ import torch.distributed as dist
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-from parallelwavegan_amd import Engine, _lib, configs, synthetic  # noqa: E402
+from parallelwavegan_amd import Engine, GraphedRun, _lib, configs, synthetic  # noqa: E402
 from parallelwavegan_amd.sharding import (  # noqa: E402
     broadcast_packed_weights, broadcast_weights_rccl, lpt_partition, max_over_ranks, shard_loads)
 
@@ -114,6 +114,77 @@ def dist_setup(n_gpus):
     if n_gpus != 1:
         print(f"[bench] --gpus {n_gpus} without torch.distributed.run: running 1 process", file=sys.stderr)
     return 0, 1, torch.device("cuda", 0)
+
+
+def measure_layer_traffic(args):
+    """HBM bytes per middle residual-layer launch of THIS workload, measured in this run: two
+    rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE: separate passes on gfx950) over a child
+    process that runs one warmup and one timed forward of the same plan. FETCH_SIZE is doubled
+    (MI355X_MICROARCH.md: gfx950 reports half the bytes of wide coalesced reads), KB -> bytes.
+    Runs before this process touches the GPU (the child is a separate process, never an exec).
+    Returns (bytes or None, source note)."""
+    import glob
+    import shutil
+    import tempfile
+
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None, "rocprofv3 not found"
+    kernel = f"pwg_layer_{args.layer_kernel or 'split16'}_kernel<false"
+    per = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        with tempfile.TemporaryDirectory(prefix="pwg_pmc_", dir="/tmp") as d:
+            cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "pmc", "--", sys.executable,
+                   os.path.abspath(__file__), "--pmc-child", "--config", args.config, "--utts", str(args.utts)]
+            if args.layer_kernel:
+                cmd += ["--layer-kernel", args.layer_kernel]
+            env = dict(os.environ, TMPDIR="/tmp")
+            for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+                env.pop(k, None)
+            try:
+                r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=240)
+            except subprocess.TimeoutExpired:
+                return None, f"rocprofv3 --pmc {ctr} pass timed out"
+            if r.returncode != 0:
+                return None, f"rocprofv3 --pmc {ctr} pass failed (rc {r.returncode})"
+            vals = {}
+            for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+                import csv
+
+                for row in csv.DictReader(open(path)):
+                    name = row.get("Kernel_Name", "")
+                    # middle layers: not the last (<true...>) and not layer 0 with the fused first_conv
+                    if kernel in name and ", true>" not in name and row.get("Counter_Name") == ctr:
+                        disp = row.get("Dispatch_Id")
+                        vals[disp] = vals.get(disp, 0.0) + float(row.get("Counter_Value") or 0)
+            if not vals:
+                return None, f"rocprofv3 --pmc {ctr}: no {kernel}...> dispatches found"
+            per[ctr] = (sum(vals.values()) / len(vals), len(vals))
+    fetch = per["FETCH_SIZE"][0] * 1024 * 2
+    write = per["WRITE_SIZE"][0] * 1024
+    note = (f"measured in this run: rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) and WRITE_SIZE passes over "
+            f"one forward of this workload in a child process, mean of {per['FETCH_SIZE'][1]} middle-layer launches; "
+            f"read {fetch / 1e9:.3f} GB + write {write / 1e9:.3f} GB")
+    return fetch + write, note
+
+
+def pmc_child(args):
+    """--pmc-child: one warmup + one forward of the bench plan, nothing printed (profiled by
+    measure_layer_traffic)."""
+    dev = torch.device("cuda", 0)
+    params = configs.generator_params(args.config)
+    eng = Engine(params, dev)
+    eng.set_option("layer_kernel", args.layer_kernel or "split16")
+    eng.load_state_dict(synthetic.make_state_dict(params, seed=0))
+    lengths = synthetic.libritts_lengths(args.utts, seed=3)
+    plan = eng.plan(lengths.tolist())
+    rs = np.random.RandomState(100)
+    mel = torch.from_numpy(rs.standard_normal(int(lengths.sum()) * params["aux_channels"]).astype(np.float32)).to(dev)
+    noise = torch.from_numpy(rs.standard_normal(plan.total_samples).astype(np.float32)).to(dev)
+    out = torch.empty(plan.total_samples * params["out_channels"], dtype=torch.float32, device=dev)
+    for _ in range(2):
+        eng.run(plan, mel, noise, out, check=False)
+    torch.cuda.synchronize(dev)
 
 
 def host_cpus():
@@ -382,6 +453,15 @@ def latency_rows(dev, reps=20):
                 dev_ms = sorted(timed(call) for _ in range(reps))
                 host_ms = sorted(timed(call_host) for _ in range(max(3, reps // 4)))
                 eng = m.engine()
+                graph_ms = None
+                if B == 1:
+                    # the same call pattern replayed from a HIP graph (pwg_graph_create): inputs
+                    # copied into the graph's buffers, one submission, range check included
+                    g = GraphedRun(eng, eng.plan([F]))
+                    for _ in range(3):
+                        g(mels[0], noises[0])
+                    graph_ms = sorted(timed(lambda: g(mels[0], noises[0])) for _ in range(reps))
+                    del g
                 eng.set_timing(True)
                 eng.collect_timing()
                 call()
@@ -393,6 +473,7 @@ def latency_rows(dev, reps=20):
                              "first_call_ms": round(first, 3), "median_ms": round(med, 3),
                              "min_ms": round(dev_ms[0], 3), "host_to_host_median_ms": round(host_ms[len(host_ms) // 2], 3),
                              "kernel_ms": round(kern, 3), "overhead_ms": round(med - kern, 3),
+                             "graph_replay_median_ms": graph_ms and round(graph_ms[len(graph_ms) // 2], 3),
                              "samples_per_s": round(F * H * B / (med * 1e-3), 1)})
     return {"model": "ljspeech_v1 ParallelWaveGANGenerator.inference / inference_batch (drop-in)",
             "rows": rows}
@@ -415,7 +496,11 @@ def main():
     ap.add_argument("--no-latency", action="store_true", help="skip the B=1 / B=16 latency rows")
     ap.add_argument("--sub-plans", type=int, default=1,
                     help="experiment: run the per-GPU utterances as this many sequential sub-batches")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "layer_traffic.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "layer_traffic.json"),
+                    help="fallback for roofline.traffic when the in-run PMC passes are off or fail")
+    ap.add_argument("--pmc", choices=["auto", "off"], default="auto",
+                    help="auto: measure roofline.traffic with two rocprofv3 --pmc passes before the run (N=1)")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--layer-kernel", default=None, choices=["split", "split16", "persistent", "tiled"],
                     help="default: split where the shape allows, else persistent (the engine default)")
     ap.add_argument("--waves-per-wg", type=int, default=None)
@@ -430,6 +515,14 @@ def main():
     if args.cpu_seconds == 0:
         args.cpu_utts = 0
 
+    if args.pmc_child:
+        return pmc_child(args)
+    # measured HBM traffic of the dominant kernel, before this process touches the GPU
+    live_traffic = (None, "off")
+    if (args.pmc == "auto" and int(os.environ.get("WORLD_SIZE", "1")) == 1 and args.config not in VOCODERS
+            and not args.strong and args.sub_plans == 1 and args.layer_kernel in (None, "split16")
+            and not args.no_fuse_first and not args.waves_per_wg and not args.wg_per_cu):
+        live_traffic = measure_layer_traffic(args)
     rank, world, dev = dist_setup(args.gpus)
     _lib.build()
     if args.config in VOCODERS:
@@ -562,7 +655,9 @@ def main():
     achieved_tflops = flops_launch / layer_avg_s / 1e12
     traffic = mfma_insts = None
     traffic_source = None
-    if os.path.exists(args.traffic_json):
+    if live_traffic[0] is not None:
+        traffic, traffic_source = live_traffic
+    elif os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
             if (tj.get("config") == args.config and tj.get("utts") == args.utts and not args.strong
@@ -571,7 +666,7 @@ def main():
                 mfma_insts = tj.get("mfma_insts_per_launch")
                 traffic_source = (f"{os.path.relpath(args.traffic_json, REPO)} (rocprofv3 --pmc FETCH_SIZE x2 + "
                                   f"WRITE_SIZE of this workload, {tj.get('source', 'committed profile')}; "
-                                  f"not measured in this run)")
+                                  f"not measured in this run: {live_traffic[1]})")
         except (OSError, ValueError):
             traffic = None
     L = params["layers"]

@@ -166,6 +166,22 @@ PWG_API int pwg_run(PwgPlan* p, const float* packed, const float* mel, const flo
  * what the Python drop-in does. The exact-fp32 kernels never set the flag. */
 PWG_API int pwg_run_status(PwgPlan* p, const void* workspace, void* stream);
 
+/* HIP graph of one pwg_run with fixed buffers (no reference counterpart: the replay path for
+ * repeated shapes, e.g. fixed-size streaming chunks or a serving loop over one batch shape).
+ * pwg_graph_create captures pwg_run(p, packed, mel, noise, mean, scale, out, workspace) on
+ * `stream` (a created stream, not the legacy null stream; timing must be off) into an executable
+ * graph (after one eager, synchronised pwg_run on the same buffers, so that first-launch work
+ * stays outside the capture). pwg_graph_launch replays the whole forward (workspace reset, plan descriptors, conv_in,
+ * aux projection, L layer launches) as one submission on any stream; the caller refills mel /
+ * noise in place between launches and may call pwg_run_status on the same workspace after it.
+ * The graph reads the plan's descriptors and options as they were at capture time. */
+typedef struct PwgGraph PwgGraph;
+PWG_API int pwg_graph_create(PwgPlan* p, const float* packed, const float* mel, const float* noise,
+                             const float* mean, const float* scale, float* out, void* workspace, void* stream,
+                             PwgGraph** out_graph);
+PWG_API int pwg_graph_launch(PwgGraph* g, void* stream);
+PWG_API void pwg_graph_destroy(PwgGraph* g);
+
 /* Engine options (pwg_set_option). Defaults are the tuned values; the others exist for A/B
  * measurement (bench.py --layer-kernel ...). */
 enum {

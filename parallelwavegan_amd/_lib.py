@@ -65,6 +65,9 @@ EXPORTED_SYMBOLS = (
     "pwg_plan_workspace_bytes",
     "pwg_run",
     "pwg_run_status",
+    "pwg_graph_create",
+    "pwg_graph_launch",
+    "pwg_graph_destroy",
     "pwg_set_option",
     "pwg_get_option",
     "pwg_set_timing",
@@ -227,6 +230,10 @@ def load():
             getattr(lib, name).restype = ll
         lib.pwg_run.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp]
         lib.pwg_run_status.argtypes = [vp, vp, vp]
+        lib.pwg_graph_create.argtypes = [vp] * 9 + [ctypes.POINTER(vp)]
+        lib.pwg_graph_launch.argtypes = [vp, vp]
+        lib.pwg_graph_destroy.argtypes = [vp]
+        lib.pwg_graph_destroy.restype = None
         lib.pwg_get_option.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ll)]
         lib.pwg_rccl_unique_id.argtypes = [vp]
         lib.pwg_rccl_comm_create.argtypes = [ctypes.c_int, vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]

@@ -912,9 +912,7 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
   };
 
   int* range_flag = (int*)(ws + p->ws_flag);
-  // work-queue heads and the range flag (adjacent) start at zero every run
-  hipError_t e = hipMemsetAsync(sched_ctr, 0, p->ws_flag + sizeof(int) - p->ws_ctr, s);
-  if (e != hipSuccess) return hip_fail(e, "work-queue reset");
+  hipError_t e = hipSuccess;
   UttDesc* d_utts = (UttDesc*)(ws + p->ws_utts);
   int* d_tile_utt = (int*)(ws + p->ws_tile_utt);
   long long* d_gap_col0 = (long long*)(ws + p->ws_gap);
@@ -926,6 +924,9 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
     da.gap_tiles = (int)(h->gap / TILE);
     for (int i = 0; i < da.n; ++i) da.utts[i] = p->utts[u0 + i];
     da.d_utts = d_utts; da.tile_utt = d_tile_utt; da.gap_col0 = d_gap_col0; da.blocks = d_blocks;
+    // work-queue heads and the range flag (adjacent) start at zero every run
+    da.zero = u0 == 0 ? sched_ctr : nullptr;
+    da.n_zero = (int)((p->ws_flag + sizeof(int) - p->ws_ctr) / sizeof(int));
     e = launch_plan_desc(da, p->max_blocks_per_utt, s);
     if (e != hipSuccess) return hip_fail(e, "plan descriptor launch");
   }
@@ -1127,6 +1128,74 @@ int pwg_run_status(PwgPlan* p, const void* workspace, void* stream) {
                 "non-finite skip sum in the split-f16 layer kernel: a value left the fp16 pair range (or the "
                 "input is not finite); rerun with PWG_OPT_LAYER_KERNEL 0 (exact fp32)");
   return PWG_OK;
+}
+
+struct PwgGraph {
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  int device = 0;
+};
+
+int pwg_graph_create(PwgPlan* p, const float* packed, const float* mel, const float* noise, const float* mean,
+                     const float* scale, float* out, void* workspace, void* stream, PwgGraph** out_graph) {
+  if (!p || !out_graph) return fail(PWG_ERR_INVALID, "null argument");
+  *out_graph = nullptr;
+  if (stream == nullptr) return fail(PWG_ERR_INVALID, "graph capture needs a created stream, not the null stream");
+  PwgHandle* h = p->h;
+  if (h->timing) return fail(PWG_ERR_INVALID, "disable timing (pwg_set_timing) before capturing a graph");
+  DeviceGuard g(h->device);
+  if (!g.ok) return fail(PWG_ERR_HIP, "hipSetDevice failed");
+  if (h->n_cu == 0) {  // pwg_run queries it on first use; not inside the capture
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || n < 1)
+      return fail(PWG_ERR_HIP, "cannot query the CU count");
+    h->n_cu = n;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  // one eager run first, so that the kernels' first-launch work (code-object load, LDS size
+  // attribute) happens outside the capture
+  int rc0 = pwg_run(p, packed, mel, noise, mean, scale, out, workspace, stream);
+  if (rc0 != PWG_OK) return rc0;
+  hipError_t e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return hip_fail(e, "graph warm-up run");
+  e = hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed);
+  if (e != hipSuccess) return hip_fail(e, "hipStreamBeginCapture");
+  const int rc = pwg_run(p, packed, mel, noise, mean, scale, out, workspace, stream);
+  hipGraph_t graph = nullptr;
+  e = hipStreamEndCapture(s, &graph);
+  if (rc != PWG_OK) {
+    if (graph) (void)hipGraphDestroy(graph);
+    return rc;  // pwg_run's message stands
+  }
+  if (e != hipSuccess || !graph) return hip_fail(e != hipSuccess ? e : hipErrorUnknown, "hipStreamEndCapture");
+  hipGraphExec_t exec = nullptr;
+  e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+  if (e != hipSuccess) {
+    (void)hipGraphDestroy(graph);
+    return hip_fail(e, "hipGraphInstantiate");
+  }
+  PwgGraph* gr = new PwgGraph();
+  gr->graph = graph;
+  gr->exec = exec;
+  gr->device = h->device;
+  *out_graph = gr;
+  return PWG_OK;
+}
+
+int pwg_graph_launch(PwgGraph* gr, void* stream) {
+  if (!gr) return fail(PWG_ERR_INVALID, "null graph");
+  DeviceGuard g(gr->device);
+  if (!g.ok) return fail(PWG_ERR_HIP, "hipSetDevice failed");
+  const hipError_t e = hipGraphLaunch(gr->exec, (hipStream_t)stream);
+  return e == hipSuccess ? PWG_OK : hip_fail(e, "hipGraphLaunch");
+}
+
+void pwg_graph_destroy(PwgGraph* gr) {
+  if (!gr) return;
+  DeviceGuard g(gr->device);
+  if (gr->exec) (void)hipGraphExecDestroy(gr->exec);
+  if (gr->graph) (void)hipGraphDestroy(gr->graph);
+  delete gr;
 }
 
 int pwg_set_option(PwgHandle* h, int option, long long value) {

@@ -217,6 +217,8 @@ struct PlanDescArgs {
   int* tile_utt;
   long long* gap_col0;
   BlockDesc* blocks;
+  int* zero;      // first chunk only: the run's work-queue heads + range flag, zeroed here
+  int n_zero;
 };
 hipError_t launch_plan_desc(const PlanDescArgs& a, long long max_blocks, hipStream_t s);
 

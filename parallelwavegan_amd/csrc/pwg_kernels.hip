@@ -1133,6 +1133,10 @@ __global__ void __launch_bounds__(256) pwg_plan_desc_kernel(const PlanDescArgs a
     if (a.u0 == 0 && y == 0) a.gap_col0[j] = j * TILE;
   }
   if (j == 0) a.d_utts[a.u0 + y] = d;
+  // the run's work-queue heads and range flag start at zero (a kernel, not hipMemsetAsync: a
+  // memset captured into a HIP graph did not reset them on every replay)
+  if (a.zero != nullptr && blockIdx.x == 0 && y == 0)
+    for (int i = threadIdx.x; i < a.n_zero; i += 256) a.zero[i] = 0;
 }
 
 hipError_t launch_plan_desc(const PlanDescArgs& a, long long max_blocks, hipStream_t s) {

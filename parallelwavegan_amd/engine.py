@@ -452,3 +452,77 @@ class Engine:
             res.append(out[off * O:(off + T) * O].view(T, O))
             off += T
         return res
+
+
+class GraphedRun:
+    """One forward of ``plan`` captured as a HIP graph (pwg_graph_create) over static buffers
+    owned by this object: refill ``mel`` / ``noise`` (or pass them to ``__call__``), replay the
+    whole forward as one submission, read ``out`` (overwritten by the next replay). For repeated
+    shapes (fixed-size streaming chunks, a serving loop over one batch shape); ``Engine.run`` is
+    the general path. The graph keeps the weights, options and plan of capture time: reloading
+    weights into the engine (a new packed image) invalidates it, and __call__ then raises."""
+
+    def __init__(self, engine, plan, mean=None, scale=None):
+        if plan.layout != _lib.PWG_LAYOUT_INFERENCE:
+            raise ValueError("graphs are captured for the inference layout")
+        if engine.packed is None:
+            raise RuntimeError("no weights loaded")
+        if engine.timing_enabled:
+            raise RuntimeError("disable engine timing before capturing a graph")
+        dev = engine.device
+        self.engine, self.plan = engine, plan
+        A, O = engine.config.aux_channels, engine.config.out_channels
+        self.mel = torch.zeros(sum(plan.frames) * A, dtype=torch.float32, device=dev)
+        self.noise = torch.zeros(plan.total_samples, dtype=torch.float32, device=dev)
+        self.out = torch.empty(plan.total_samples * O, dtype=torch.float32, device=dev)
+        self.mean = self.scale = None
+        if mean is not None:
+            self.mean = mean.to(dev, torch.float32).contiguous().clone()
+            self.scale = scale.to(dev, torch.float32).contiguous().clone()
+        self.ws = torch.empty(max(int(plan.workspace_bytes), 256), dtype=torch.uint8, device=dev)
+        self._packed = engine.packed
+        self._kernel = engine.layer_kernel
+        stream = torch.cuda.Stream(dev)  # capture needs a created stream
+        torch.cuda.synchronize(dev)
+        g = ctypes.c_void_p()
+        _lib.check(engine._lib.pwg_graph_create(
+            plan._p, self._packed.data_ptr(), self.mel.data_ptr(), self.noise.data_ptr(),
+            self.mean.data_ptr() if self.mean is not None else None,
+            self.scale.data_ptr() if self.scale is not None else None,
+            self.out.data_ptr(), self.ws.data_ptr(), stream.cuda_stream, ctypes.byref(g)))
+        self._g = g
+        self._lib = engine._lib
+
+    def __del__(self):
+        g = getattr(self, "_g", None)
+        if g is not None and g.value:
+            self._lib.pwg_graph_destroy(g)
+            self._g = None
+
+    def __call__(self, mel=None, noise=None, check=True):
+        """Replay on torch's current stream; returns ``out`` (flat, total_samples * out_channels).
+        check=True: split-f16 range check (one synchronisation); a flagged replay is redone by
+        ``Engine.run`` on the exact-fp32 kernel, as the drop-in does."""
+        eng = self.engine
+        if eng.packed is not self._packed:
+            raise RuntimeError("the engine's weights changed after capture: capture a new GraphedRun")
+        if mel is not None:
+            self.mel.copy_(mel.reshape(-1))
+        if noise is not None:
+            self.noise.copy_(noise.reshape(-1))
+        stream = torch.cuda.current_stream(eng.device)
+        _lib.check(self._lib.pwg_graph_launch(self._g, stream.cuda_stream))
+        if check and self._kernel in (2, 3):
+            try:
+                _lib.check(self._lib.pwg_run_status(self.plan._p, self.ws.data_ptr(), stream.cuda_stream))
+            except _lib.RangeError as e:
+                logging.warning("%s; rerunning on the exact-fp32 layer kernel", e)
+                kernel = eng.layer_kernel
+                eng.set_option("layer_kernel", "persistent")
+                try:
+                    eng._enqueue(self.plan, self.mel, self.noise, self.out, self.mean, self.scale, stream)
+                finally:
+                    eng.set_option("layer_kernel", kernel)
+                eng.range_reruns += 1
+        return self.out
+

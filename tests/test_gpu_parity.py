@@ -404,3 +404,28 @@ def test_maximum_size_utterance(built_lib, cuda_device):
     torch.cuda.empty_cache()
     with pytest.raises((ValueError, RuntimeError, NotImplementedError)):
         eng.plan([(1 << 31) // 300 + 1])
+
+
+def test_graph_replay_equals_run(built_lib, cuda_device):
+    """pwg_graph_create / pwg_graph_launch (engine.GraphedRun): the captured forward of a ragged
+    LibriTTS plan replayed with two different inputs is bit-identical to Engine.run on each, and
+    stale weights are refused."""
+    from parallelwavegan_amd import Engine, GraphedRun, configs, synthetic
+
+    params = configs.generator_params("libritts_v1")
+    eng = Engine(params, cuda_device)
+    eng.load_state_dict(synthetic.make_state_dict(params, seed=5))
+    frames = [37, 5, 120]
+    plan = eng.plan(frames)
+    g = GraphedRun(eng, plan)
+    for seed in (1, 2):
+        rs = np.random.RandomState(seed)
+        mel = torch.from_numpy(rs.standard_normal(sum(frames) * 80).astype(np.float32)).to(cuda_device)
+        noise = torch.from_numpy(rs.standard_normal(plan.total_samples).astype(np.float32)).to(cuda_device)
+        ref = torch.empty(plan.total_samples, dtype=torch.float32, device=cuda_device)
+        eng.run(plan, mel, noise, ref)
+        got = g(mel, noise).clone()
+        assert torch.equal(got, ref)
+    eng.load_state_dict(synthetic.make_state_dict(params, seed=6))
+    with pytest.raises(RuntimeError):
+        g(mel, noise)
