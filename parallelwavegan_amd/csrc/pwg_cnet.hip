@@ -28,6 +28,7 @@
 #include <cmath>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/pwg_cnet.h"
@@ -398,6 +399,251 @@ __global__ void __launch_bounds__(256) pwg_cnet_conv_kernel(const CnConvArgs a) 
   }
 }
 
+// Fused MelGAN ResidualStack (split-f16 mode; layers/residual_stack.py:75-85 stack(c) + skip_layer(c)):
+// op A  h = conv_k(pre_A(x)) + b1             (dilated, zero / reflection / replication edges)
+// op B  y = post(W2 pre_B(h) + W3 x + b2 + b3 [+ res] [+ y_old]) / div   (the two-source 1x1)
+// as ONE launch in which h never leaves the chip. Workgroup = 4 waves x 32 columns (one 128-column
+// block of one utterance), every output row (MT m-tiles of 32 cover all C channels):
+//   * stage 1: op A's chunks exactly as pwg_cnet_conv_kernel runs them (A fragments staged in LDS,
+//     double-buffered; B rows from HBM one chunk ahead, pre-activated and pair-split);
+//   * h + b1, op B's pre-activation and the fp16 pair split go to a wave-private LDS tile
+//     [32 columns][C + 8 halves] (hi and lo images);
+//   * stage 2: op B's chunks in its own order (h chunks read from LDS, x chunks from HBM / L2 again,
+//     raw), then op B's epilogue.
+// Chunk order, pair split, fp32 accumulation and epilogue order are the two unfused ops' exactly:
+// the result is bit-identical to running op A then op B in split mode. HBM traffic per stack: x read
+// once (+ its L2-hot center re-read) and y written, instead of x, h written, h and x read, y written.
+struct CnStackArgs {
+  CnSrc x1;               // op A's source (its taps come from the chunk list)
+  CnSrc x2;               // op B's second source: the same buffer, op B's pre-activation
+  const ChunkDesc* ch1;
+  int n1;
+  const float* w1;        // split-f16 fragments [chunk][MT][hi/lo][lane][4 dwords]
+  const float* b1;
+  float slope_h;          // op B's pre-activation of h
+  int ldh;                // h channels (C rounded up to 16)
+  const ChunkDesc* ch2;   // op B: src 0 chunks (h) then src 1 chunks (x)
+  int n2;
+  const float* w2;
+  const float* b2;        // both biases of op B, summed host-side
+  const float* res;
+  const int* seg_res;
+  int ld_res;
+  float* y;
+  const int* seg_y;
+  int ld_y;
+  int M;                  // op B's output channels
+  int accumulate;
+  float out_div;
+  int post_act;
+  float post_slope;
+  const int2* blocks;     // (utt, q0)
+  const int* ncols;
+  const float* mean;
+  const float* scale;
+};
+
+template <int MT>
+__global__ void __launch_bounds__(256) pwg_cnet_stack_kernel(const CnStackArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char st_smem[];
+  float* s_a = reinterpret_cast<float*>(st_smem);                      // [2][MT * 512] A staging
+  const int hrow = a.ldh + 8;                                          // halves per h column (+16 B pad)
+  _Float16* s_h = reinterpret_cast<_Float16*>(st_smem + 2 * MT * 512 * sizeof(float));
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int hh = lane >> 5;
+  const int cl = lane & 31;
+  const int2 blk = a.blocks[blockIdx.x];
+  const int u = blk.x;
+  const int qb = blk.y + wave * 32 + cl;
+  const int nq = a.ncols[u];
+  _Float16* h_hi = s_h + (size_t)(wave * 32 + cl) * 2 * hrow;          // this lane's column: [hi][lo]
+  _Float16* h_lo = h_hi + hrow;
+
+  // B row of chunk cd from source s (column qb + row_off), raw: loaded one chunk ahead
+  auto braw = [&](const CnSrc& s, const ChunkDesc& cd, f32x8v& v, bool& ok) {
+    const int2 sg = *reinterpret_cast<const int2*>(s.seg + 2 * u);
+    int p = qb + cd.row_off;
+    ok = edge_row(p, sg.y, s.pad_mode);
+    v = *reinterpret_cast<const f32x8v*>(s.x + (size_t)(sg.x + p) * s.ld + cd.c0 + 8 * hh);
+  };
+  auto bprep = [&](const CnSrc& s, const ChunkDesc& cd, f32x8v x, bool ok, u32x4v& bh, u32x4v& bl) {
+    const int ch = cd.c0 + 8 * hh;
+    if (s.normalize) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) x[i] = (x[i] - a.mean[ch + i]) / a.scale[ch + i];
+    }
+    if (s.slope != 1.f) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) x[i] = x[i] > 0.f ? x[i] : x[i] * s.slope;
+    }
+    if (!ok) x = f32x8v{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    cn_split8(x, bh, bl);
+  };
+  auto aload = [&](const float* w, int c, f32x4v (&r)[(MT + 1) / 2]) {
+    const f32x4v* gp = reinterpret_cast<const f32x4v*>(w + (size_t)c * MT * 512);
+#pragma unroll
+    for (int i = 0; i < (MT + 1) / 2; ++i) {
+      const int idx = threadIdx.x + 256 * i;
+      r[i] = idx < MT * 128 ? gp[idx] : f32x4v{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto astore = [&](int buf, const f32x4v (&r)[(MT + 1) / 2]) {
+    f32x4v* d = reinterpret_cast<f32x4v*>(s_a + buf * MT * 512);
+#pragma unroll
+    for (int i = 0; i < (MT + 1) / 2; ++i) {
+      const int idx = threadIdx.x + 256 * i;
+      if (idx < MT * 128) d[idx] = r[i];
+    }
+  };
+  f32x16 acc[MT];
+  auto compute = [&](int buf, const u32x4v bh, const u32x4v bl) {
+    const u32x4v* sa = reinterpret_cast<const u32x4v*>(s_a + buf * MT * 512) + lane;
+    u32x4v ah[MT], al[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      ah[m] = sa[(m * 2) * 64];
+      al[m] = sa[(m * 2 + 1) * 64];
+    }
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, ah[m]), __builtin_bit_cast(f16x8v, bh),
+                                                      acc[m], 0, 0, 0);
+      acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, ah[m]), __builtin_bit_cast(f16x8v, bl),
+                                                      acc[m], 0, 0, 0);
+      acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, al[m]), __builtin_bit_cast(f16x8v, bh),
+                                                      acc[m], 0, 0, 0);
+    }
+  };
+  // one GEMM over n chunks: A fragments double-buffered through LDS (one barrier per chunk), the
+  // B operand of chunk c from src (global, one chunk ahead) or, for stage-2 chunks of source 0,
+  // from the wave's h tile
+  auto gemm = [&](const ChunkDesc* chunks, int n, const float* w, auto stage2_c) {
+    constexpr bool stage2 = decltype(stage2_c)::value;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
+    auto src_of = [&](const ChunkDesc&) -> const CnSrc& { return stage2 ? a.x2 : a.x1; };
+    auto from_h = [&](const ChunkDesc& cd) { return stage2 && cd.src == 0; };
+    auto hread = [&](const ChunkDesc& cd, u32x4v& bh, u32x4v& bl) {
+      bh = *reinterpret_cast<const u32x4v*>(h_hi + cd.c0 + 8 * hh);
+      bl = *reinterpret_cast<const u32x4v*>(h_lo + cd.c0 + 8 * hh);
+    };
+    f32x4v ar[(MT + 1) / 2];
+    aload(w, 0, ar);
+    astore(0, ar);
+    ChunkDesc cd = chunks[0];
+    u32x4v bh, bl;
+    f32x8v xr;
+    bool ok;
+    if (from_h(cd)) {
+      hread(cd, bh, bl);
+    } else {
+      braw(src_of(cd), cd, xr, ok);
+      bprep(src_of(cd), cd, xr, ok, bh, bl);
+    }
+    __syncthreads();
+    for (int c = 0; c < n; ++c) {
+      const bool more = c + 1 < n;
+      ChunkDesc cn = cd;
+      if (more) {
+        cn = chunks[c + 1];
+        aload(w, c + 1, ar);
+        if (!from_h(cn)) braw(src_of(cn), cn, xr, ok);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      compute(c & 1, bh, bl);
+      __builtin_amdgcn_sched_barrier(0);
+      if (more) astore((c + 1) & 1, ar);
+      __syncthreads();
+      if (more) {
+        if (from_h(cn)) hread(cn, bh, bl);
+        else bprep(src_of(cn), cn, xr, ok, bh, bl);
+      }
+      cd = cn;
+    }
+  };
+
+  // ---- stage 1: h = op A
+  gemm(a.ch1, a.n1, a.w1, std::false_type{});
+  // h + b1, op B's pre-activation, pair split -> this lane's LDS column (rows >= ldh: padding)
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int j4 = 0; j4 < 4; ++j4) {
+      const int row = 32 * m + 8 * j4 + 4 * hh;
+      if (row >= a.ldh) continue;
+      const f32x4v b = *reinterpret_cast<const f32x4v*>(a.b1 + row);
+      _Float16 hv[4], lv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float v = acc[m][4 * j4 + i] + b[i];
+        v = v > 0.f ? v : v * a.slope_h;
+        hv[i] = (_Float16)v;
+        lv[i] = (_Float16)(v - (float)hv[i]);
+      }
+      *reinterpret_cast<f16x4v*>(h_hi + row) = f16x4v{hv[0], hv[1], hv[2], hv[3]};
+      *reinterpret_cast<f16x4v*>(h_lo + row) = f16x4v{lv[0], lv[1], lv[2], lv[3]};
+    }
+  // (the h tile is wave-private: the barrier inside stage 2's prologue orders these writes)
+
+  // ---- stage 2: y = op B over [pre_B(h); x]
+  gemm(a.ch2, a.n2, a.w2, std::true_type{});
+  if (qb >= nq) return;
+  const int2 sd = *reinterpret_cast<const int2*>(a.seg_y + 2 * u);
+  const int2 sr = a.res ? *reinterpret_cast<const int2*>(a.seg_res + 2 * u) : make_int2(0, 0);
+  float* yrow = a.y + (size_t)(sd.x + qb) * a.ld_y;
+  const float* rrow = a.res ? a.res + (size_t)(sr.x + qb) * a.ld_res : nullptr;
+  const bool quad = (a.ld_y & 3) == 0;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int j4 = 0; j4 < 4; ++j4) {
+      const int row = 32 * m + 8 * j4 + 4 * hh;
+      if (row >= a.M) {
+        if (quad && row < a.ld_y) *reinterpret_cast<f32x4v*>(yrow + row) = f32x4v{0.f, 0.f, 0.f, 0.f};
+        continue;
+      }
+      const f32x4v b = *reinterpret_cast<const f32x4v*>(a.b2 + row);
+      f32x4v v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = acc[m][4 * j4 + i] + b[i];
+      if (quad) {
+        if (rrow) v += *reinterpret_cast<const f32x4v*>(rrow + row);
+        if (a.accumulate) v = *reinterpret_cast<const f32x4v*>(yrow + row) + v;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (row + i >= a.M) continue;
+          if (rrow) v[i] += rrow[row + i];
+          if (a.accumulate) v[i] = yrow[row + i] + v[i];
+        }
+      }
+      if (a.out_div != 1.f) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = v[i] / a.out_div;
+      }
+      if (a.post_act == PWG_ACT_LRELU) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = v[i] > 0.f ? v[i] : v[i] * a.post_slope;
+      } else if (a.post_act == PWG_ACT_TANH) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = tanhf(v[i]);
+      }
+      if (quad) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (row + i >= a.M) v[i] = 0.f;
+        *reinterpret_cast<f32x4v*>(yrow + row) = v;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (row + i < a.M) yrow[row + i] = v[i];
+      }
+    }
+}
+
 // Fused conv pair (split-f16 mode): y = post((conv2(pre2(conv1(pre1(x)) + b1)) + b2 + res [+ y_old]) / div)
 // with conv2's intermediate never leaving the chip. This is HiFiGAN's ResBlock step
 // (layers/residual_block.py:231-237: xt = c1(lrelu(x)); xt = c2(lrelu(xt)); x = xt + x) and any other
@@ -414,6 +660,9 @@ __global__ void __launch_bounds__(256) pwg_cnet_conv_kernel(const CnConvArgs a) 
 //     chunk ahead, stage-2 B rows from LDS.
 // The arithmetic (chunk order, pair split, fp32 accumulate, epilogue order) is the unfused ops'
 // exactly, so the fused result is bit-identical to running op A then op B in split mode.
+#ifndef PWG_STACK_MAX_MT
+#define PWG_STACK_MAX_MT 3  // ResidualStack fusion up to 3 m-tiles (96 channels); 7 = every shape (A/B)
+#endif
 constexpr int PR_HALO = 16;
 constexpr int PR_MAX_XS = 128 + 2 * 64;        // x tile columns (stage-1 tap reach +-64 - PR_HALO)
 constexpr int PR_XQ = PR_MAX_XS * 8 / 256;     // 16-byte x quads per thread
@@ -1069,6 +1318,8 @@ struct OpPhase {          // one launch
   int pair_xmin = 0, pair_xs = 0, pair_lds = 0;  // its x tile offset / width and dynamic LDS bytes
   bool pair_resident = true;  // weights resident (pwg_cnet_pair_kernel) or streamed (_stream_kernel)
   int pair_step = 128;        // columns per kernel step (streamed 128-channel pairs: 64)
+  int stack_b = -1;           // phase index of the two-source 1x1 fused with this conv (pwg_cnet_stack_kernel)
+  int stack_lds = 0;          // its dynamic LDS bytes
 };
 
 }  // namespace
@@ -1389,6 +1640,38 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
       n->phases[i].pair_step = step;
     }
   }
+  // Fusable ResidualStacks (pwg_cnet_stack_kernel): op A = single-source conv X -> H with no
+  // residual / accumulate / division / post activation; the next op B = 1x1 over [H; X] (taps 1,
+  // no padding); nobody else reads H; both ops have the same rows (<= 7 m-tiles: the fused kernel
+// covers all of them) and the h tile fits LDS.
+  for (size_t i = 0; i + 1 < n->phases.size(); ++i) {
+    OpPhase& pa = n->phases[i];
+    const OpPhase& pb = n->phases[i + 1];
+    if (pa.pair_b >= 0 || pb.op != pa.op + 1) continue;
+    const PwgCnetOp& A = n->ops[pa.op];
+    const PwgCnetOp& B = n->ops[pb.op];
+    if (A.kind != PWG_CNET_CONV || B.kind != PWG_CNET_CONV || pa.thin || pb.thin || pa.NT != 1 || pb.NT != 1) continue;
+    if (A.src[1].buf >= 0 || A.res >= 0 || A.accumulate || A.out_div != 1.f || A.post_act != PWG_ACT_NONE) continue;
+    const PwgCnetSrc& b0 = B.src[0];
+    const PwgCnetSrc& b1 = B.src[1];
+    if (b0.buf != A.dst || b1.buf != A.src[0].buf || b0.taps != 1 || b1.taps != 1 || b0.pad != 0 || b1.pad != 0) continue;
+    if (b0.channels != A.out_channels || b1.channels != A.src[0].channels || b0.normalize) continue;
+    // the fused kernel covers every row in one workgroup: measured faster than the two ops up to
+    // 96 channels (MB-MelGAN v2: 48 ch 0.49 -> 0.31 ms, 96 ch 0.535 -> 0.50 ms per stack) and
+    // slower at 192 (0.43 -> 0.61 ms: one 126 KB-LDS workgroup per CU), profiles/r02_stack
+    if (pa.mt_total != pb.mt_total || pa.mt_total > PWG_STACK_MAX_MT) continue;
+    if (B.dst != n_bufs - 1 && n->ld[B.dst] % 4 != 0) continue;
+    bool ok = true;
+    for (int k = 0; k < n_ops && ok; ++k) {
+      if (k == pb.op || k == pa.op) continue;
+      const PwgCnetOp& o2 = n->ops[k];
+      ok = o2.src[0].buf != A.dst && o2.src[1].buf != A.dst && o2.res != A.dst && o2.dst != A.dst;
+    }
+    const long long lds = 2LL * pa.mt_total * 512 * 4 + 128LL * 2 * (n->ld[A.dst] + 8) * 2;
+    if (!ok || lds > PR_MAX_LDS) continue;
+    pa.stack_b = (int)i + 1;
+    pa.stack_lds = (int)lds;
+  }
   *out = n;  // device tables are uploaded by the first plan: packing needs no GPU
   return PWG_OK;
 }
@@ -1630,7 +1913,8 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
   for (size_t pi = 0; pi < n->phases.size(); ++pi) {
     const OpPhase& ph = n->phases[pi];
     const PwgCnetOp& op = n->ops[ph.op];
-    if (fuse && pi > 0 && n->phases[pi - 1].pair_b == (int)pi) continue;  // ran inside the pair
+    if (fuse && pi > 0 && (n->phases[pi - 1].pair_b == (int)pi || n->phases[pi - 1].stack_b == (int)pi))
+      continue;  // ran inside the fused pair / stack
     hipEvent_t ea = nullptr, eb = nullptr;
     if (n->timing) {
       for (hipEvent_t* ev : {&ea, &eb}) {
@@ -1674,6 +1958,52 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
           hipLaunchKernelGGL((pwg_cnet_pair_stream_kernel<2, 4, PR_SG>), pgrid, dim3(256), (size_t)ph.pair_lds, s, a);
         else
           hipLaunchKernelGGL((pwg_cnet_pair_stream_kernel<4, 2, 2>), pgrid, dim3(256), (size_t)ph.pair_lds, s, a);
+      }
+    } else if (fuse && ph.stack_b >= 0) {
+      if (p->n_blocks[pi] > 0) {
+        const OpPhase& pb = n->phases[ph.stack_b];
+        const PwgCnetOp& opb = n->ops[pb.op];
+        CnStackArgs a;
+        auto src_args = [&](const PwgCnetSrc& src, CnSrc& d) {
+          d = CnSrc{};
+          d.x = bufs[src.buf]; d.seg = seg_of(src.buf); d.ld = n->ld[src.buf];
+          d.pad_mode = src.pad_mode;
+          d.normalize = src.normalize && mean && scale;
+          d.slope = src.pre_slope;
+        };
+        src_args(op.src[0], a.x1);
+        src_args(opb.src[1], a.x2);
+        a.ch1 = ph.d_chunks; a.n1 = (int)ph.chunks.size(); a.w1 = packed + ph.frag16_off; a.b1 = packed + ph.bias_off;
+        a.slope_h = opb.src[0].pre_slope; a.ldh = n->ld[op.dst];
+        a.ch2 = pb.d_chunks; a.n2 = (int)pb.chunks.size(); a.w2 = packed + pb.frag16_off; a.b2 = packed + pb.bias_off;
+        a.res = opb.res >= 0 ? bufs[opb.res] : nullptr; a.seg_res = opb.res >= 0 ? seg_of(opb.res) : nullptr;
+        a.ld_res = opb.res >= 0 ? n->ld[opb.res] : 0;
+        a.y = bufs[opb.dst]; a.seg_y = seg_of(opb.dst); a.ld_y = n->ld[opb.dst]; a.M = opb.out_channels;
+        a.accumulate = opb.accumulate; a.out_div = opb.out_div; a.post_act = opb.post_act; a.post_slope = opb.post_slope;
+        a.blocks = p->d_blocks[pi]; a.ncols = p->d_ncols[pi];
+        a.mean = mean; a.scale = scale;
+        const void* kf = nullptr;
+        switch (ph.mt_total) {
+          case 1: kf = reinterpret_cast<const void*>(pwg_cnet_stack_kernel<1>); break;
+          case 2: kf = reinterpret_cast<const void*>(pwg_cnet_stack_kernel<2>); break;
+          case 3: kf = reinterpret_cast<const void*>(pwg_cnet_stack_kernel<3>); break;
+          case 4: kf = reinterpret_cast<const void*>(pwg_cnet_stack_kernel<4>); break;
+          case 5: kf = reinterpret_cast<const void*>(pwg_cnet_stack_kernel<5>); break;
+          case 6: kf = reinterpret_cast<const void*>(pwg_cnet_stack_kernel<6>); break;
+          default: kf = reinterpret_cast<const void*>(pwg_cnet_stack_kernel<7>); break;
+        }
+        const hipError_t ea2 = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, ph.stack_lds);
+        if (ea2 != hipSuccess) return hipf(ea2, "stack kernel LDS attribute");
+        const dim3 sgrid((unsigned)p->n_blocks[pi]);
+        switch (ph.mt_total) {
+          case 1: hipLaunchKernelGGL(pwg_cnet_stack_kernel<1>, sgrid, dim3(256), (size_t)ph.stack_lds, s, a); break;
+          case 2: hipLaunchKernelGGL(pwg_cnet_stack_kernel<2>, sgrid, dim3(256), (size_t)ph.stack_lds, s, a); break;
+          case 3: hipLaunchKernelGGL(pwg_cnet_stack_kernel<3>, sgrid, dim3(256), (size_t)ph.stack_lds, s, a); break;
+          case 4: hipLaunchKernelGGL(pwg_cnet_stack_kernel<4>, sgrid, dim3(256), (size_t)ph.stack_lds, s, a); break;
+          case 5: hipLaunchKernelGGL(pwg_cnet_stack_kernel<5>, sgrid, dim3(256), (size_t)ph.stack_lds, s, a); break;
+          case 6: hipLaunchKernelGGL(pwg_cnet_stack_kernel<6>, sgrid, dim3(256), (size_t)ph.stack_lds, s, a); break;
+          default: hipLaunchKernelGGL(pwg_cnet_stack_kernel<7>, sgrid, dim3(256), (size_t)ph.stack_lds, s, a); break;
+        }
       }
     } else if (op.kind == PWG_CNET_PQMF) {
       CnPqmfArgs a;

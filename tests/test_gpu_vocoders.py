@@ -175,3 +175,38 @@ def test_causal_generators_are_causal(cfg, over, built_lib, cuda_device):
     assert y.shape[2] == T * hop
     np.testing.assert_array_equal(y[..., :T // 2 * hop], y2[..., :T // 2 * hop])
     assert not np.array_equal(y, y2)
+
+
+@pytest.mark.parametrize("cfg", ["mb_melgan_v2", "mb_melgan_v2_causal", "melgan_v1", "mb_melgan_test"])
+def test_fused_residual_stacks_bitwise_equal_to_unfused(cfg, built_lib, cuda_device):
+    """pwg_cnet_stack_kernel (MelGAN ResidualStack: dilated conv + the two-source 1x1 in one
+    launch, h in LDS) against the two unfused split-f16 ops: same chunk order, pair split and
+    epilogue order, so bit-identical; every ResidualStack runs fused."""
+    from parallelwavegan_amd import configs, synthetic
+    from parallelwavegan_amd.melgan import PQMF, MelGANGenerator
+
+    _, params = configs.vocoder_params(cfg)
+    m = MelGANGenerator(**params)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic.make_module_state_dict(m, seed=4).items()})
+    if cfg in configs.VOCODER_PQMF:
+        m.pqmf = PQMF(**configs.VOCODER_PQMF[cfg])
+    m = m.to(cuda_device)
+    eng = m.engine()
+    mels = [synthetic.make_mel(f, 80, seed=70 + i) for i, f in enumerate([9, 40, 7, 23])]
+    with torch.no_grad():
+        eng.set_fuse_pairs(False)
+        ref = [y.cpu().numpy() for y in m.inference_batch(mels)]
+        eng.set_fuse_pairs(True)
+        eng.set_timing(True)
+        got = [y.cpu().numpy() for y in m.inference_batch(mels)]
+        t = eng.collect_timing()
+        eng.set_timing(False)
+    # stacks of <= 96 channels run fused (PWG_STACK_MAX_MT)
+    ch, stacks = params["channels"], 0
+    for _ in params["upsample_scales"]:
+        ch //= 2
+        stacks += params["stacks"] if ch <= 96 else 0
+    assert stacks > 0
+    assert sum(1 for name, _, n in t if n == 0 and "skip_layer" in name) == stacks
+    for a, b in zip(got, ref):
+        np.testing.assert_array_equal(a, b)
