@@ -51,6 +51,9 @@ constexpr int CN_G = PWG_CNET_G;   // 16-channel chunks staged per barrier
 #ifndef PWG_CNET_NT2_MT
 #define PWG_CNET_NT2_MT 0  // > 0: split-mode conv ops with MT >= this use 2 column tiles per wave (A/B)
 #endif
+#ifndef PWG_CNET_NW8_MT
+#define PWG_CNET_NW8_MT 4  // conv ops with MT >= this run 8-wave workgroups (256 columns); 0: 4 waves (A/B)
+#endif
 #ifndef PWG_CNET_DEPTH2
 #define PWG_CNET_DEPTH2 0  // 1: loads two chunk groups ahead (A/B variant)
 #endif
@@ -134,8 +137,10 @@ __device__ __forceinline__ void cn_split8(const f32x8v& v, u32x4v& hi, u32x4v& l
   }
 }
 
-template <int MT, int NT, int G, bool SPLIT = false>
-__global__ void __launch_bounds__(256) pwg_cnet_conv_kernel(const CnConvArgs a) {
+template <int MT, int NT, int G, bool SPLIT = false, int NW = 4>
+__global__ void __launch_bounds__(64 * NW) pwg_cnet_conv_kernel(const CnConvArgs a) {
+  constexpr int NTH = 64 * NW;                      // threads: NW waves x 32 * NT columns each
+  constexpr int AQ = (MT * 128 + NTH - 1) / NTH;    // A-fragment 16-B vectors per thread and chunk
   __shared__ __attribute__((aligned(16))) float s_a[2][G * MT * 512];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -189,24 +194,24 @@ __global__ void __launch_bounds__(256) pwg_cnet_conv_kernel(const CnConvArgs a) 
   };
   // (G chunks are staged per barrier; the host pads the chunk list to a multiple of G with
   // zero-weight chunks)
-  auto aload = [&](int cg, f32x4v (&r)[G][(MT + 1) / 2]) {
+  auto aload = [&](int cg, f32x4v (&r)[G][AQ]) {
 #pragma unroll
     for (int g2 = 0; g2 < G; ++g2) {
       const f32x4v* gp = reinterpret_cast<const f32x4v*>(a.wfrag + ((size_t)(cg * G + g2) * a.mt_total + m0) * 512);
 #pragma unroll
-      for (int i = 0; i < (MT + 1) / 2; ++i) {
-        const int idx = threadIdx.x + 256 * i;
+      for (int i = 0; i < AQ; ++i) {
+        const int idx = threadIdx.x + NTH * i;
         r[g2][i] = idx < MT * 128 ? gp[idx] : f32x4v{0.f, 0.f, 0.f, 0.f};
       }
     }
   };
-  auto astore = [&](int buf, const f32x4v (&r)[G][(MT + 1) / 2]) {
+  auto astore = [&](int buf, const f32x4v (&r)[G][AQ]) {
 #pragma unroll
     for (int g2 = 0; g2 < G; ++g2) {
       f32x4v* d = reinterpret_cast<f32x4v*>(s_a[buf] + g2 * MT * 512);
 #pragma unroll
-      for (int i = 0; i < (MT + 1) / 2; ++i) {
-        const int idx = threadIdx.x + 256 * i;
+      for (int i = 0; i < AQ; ++i) {
+        const int idx = threadIdx.x + NTH * i;
         if (idx < MT * 128) d[idx] = r[g2][i];
       }
     }
@@ -271,7 +276,7 @@ __global__ void __launch_bounds__(256) pwg_cnet_conv_kernel(const CnConvArgs a) 
   // Loads run TWO chunk groups ahead (register ring of 2): chunk c+2's A fragments and raw B rows
   // are issued before chunk c's MFMAs; chunk c+1's (issued one step earlier) are staged / prepared
   // after them.
-  f32x4v ar0[G][(MT + 1) / 2], ar1[G][(MT + 1) / 2];
+  f32x4v ar0[G][AQ], ar1[G][AQ];
   BRaw br0[G], br1[G];
   aload(0, ar0);
   astore(0, ar0);
@@ -286,7 +291,7 @@ __global__ void __launch_bounds__(256) pwg_cnet_conv_kernel(const CnConvArgs a) 
     for (int g2 = 0; g2 < G; ++g2) braw(G + g2, br1[g2]);
   }
   __syncthreads();
-  auto step = [&](int cg, f32x4v (&rl)[G][(MT + 1) / 2], BRaw (&bl2)[G], f32x4v (&rs)[G][(MT + 1) / 2],
+  auto step = [&](int cg, f32x4v (&rl)[G][AQ], BRaw (&bl2)[G], f32x4v (&rs)[G][AQ],
                   BRaw (&bs)[G]) {
     if (cg + 2 < n_groups) {
       aload(cg + 2, rl);
@@ -309,7 +314,7 @@ __global__ void __launch_bounds__(256) pwg_cnet_conv_kernel(const CnConvArgs a) 
     if (cg + 1 < n_groups) step(cg + 1, ar1, br1, ar0, br0);
   }
 #else
-  f32x4v ar[G][(MT + 1) / 2];
+  f32x4v ar[G][AQ];
   aload(0, ar);
   astore(0, ar);
   BRaw bnext[G];
@@ -1309,7 +1314,8 @@ struct OpPhase {          // one launch
   ChunkDesc* d_chunks = nullptr;
   int ostride, ophase;
   int k_a, off_a;         // CONVT
-  int NT;                 // column tiles per wave (workgroup = 4 waves x NT x 32 columns)
+  int NT;                 // column tiles per wave (workgroup = NW waves x NT x 32 columns)
+  int NW = 4;             // waves per workgroup of pwg_cnet_conv_kernel
   int n_real_chunks = 0;  // chunks before padding to a multiple of CN_G (the rest pack as zeros)
   bool thin = false;      // M <= 8: VALU kernel with an LDS-staged input tile
   int thin_taps[2] = {0, 0}, thin_nc[2] = {0, 0}, thin_base[2] = {0, 0}, thin_off_min[2] = {0, 0},
@@ -1536,6 +1542,8 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
       OpPhase ph;
       ph.op = oi; ph.phase = r; ph.MT = MT; ph.mt_total = mt_total;
       ph.NT = 1;  // NT 2/4 for thin row tiles measured SLOWER (fewer workgroups in flight)
+      // 8 waves (256 columns) share each staged A chunk of the wide ops (A/B: PWG_CNET_NW8_MT)
+      if (PWG_CNET_NW8_MT > 0 && MT >= PWG_CNET_NW8_MT && op.kind == PWG_CNET_CONV) ph.NW = 8;
       if (PWG_CNET_NT2_MT > 0 && MT >= PWG_CNET_NT2_MT && op.kind == PWG_CNET_CONV) ph.NT = 2;  // A/B
       ph.ostride = op.kind == PWG_CNET_CONVT ? op.stride : 1;
       ph.ophase = r;
@@ -1650,7 +1658,9 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
     if (pa.pair_b >= 0 || pb.op != pa.op + 1) continue;
     const PwgCnetOp& A = n->ops[pa.op];
     const PwgCnetOp& B = n->ops[pb.op];
-    if (A.kind != PWG_CNET_CONV || B.kind != PWG_CNET_CONV || pa.thin || pb.thin || pa.NT != 1 || pb.NT != 1) continue;
+    if (A.kind != PWG_CNET_CONV || B.kind != PWG_CNET_CONV || pa.thin || pb.thin || pa.NT != 1 || pb.NT != 1 ||
+        pa.NW != 4)
+      continue;
     if (A.src[1].buf >= 0 || A.res >= 0 || A.accumulate || A.out_div != 1.f || A.post_act != PWG_ACT_NONE) continue;
     const PwgCnetSrc& b0 = B.src[0];
     const PwgCnetSrc& b1 = B.src[1];
@@ -1843,7 +1853,7 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
         const long long T = frames[u] * n->rate[op.dst];
         const int nq = (int)((T - ph.ophase + ph.ostride - 1) / ph.ostride);
         ncols[u] = nq;
-        const int cols = ph.thin ? CN_COLS : CN_COLS * ph.NT;
+        const int cols = ph.thin ? CN_COLS : 32 * ph.NW * ph.NT;
         for (int q0 = 0; q0 < nq; q0 += cols) blocks.push_back(make_int2(u, q0));
       }
     }
@@ -2051,6 +2061,8 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
           case 3: hipLaunchKernelGGL((pwg_cnet_conv_kernel<3, 1, CN_G, true>), grid, block, 0, s, a); break;
           default:
             if (ph.NT == 2) hipLaunchKernelGGL((pwg_cnet_conv_kernel<4, 2, CN_G, true>), grid, block, 0, s, a);
+            else if (ph.NW == 8)
+              hipLaunchKernelGGL((pwg_cnet_conv_kernel<4, 1, CN_G, true, 8>), grid, dim3(512), 0, s, a);
             else hipLaunchKernelGGL((pwg_cnet_conv_kernel<4, 1, CN_G, true>), grid, block, 0, s, a);
             break;
         }
@@ -2061,6 +2073,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
           case 3: hipLaunchKernelGGL((pwg_cnet_conv_kernel<3, 1, CN_G>), grid, block, 0, s, a); break;
           default:
             if (ph.NT == 2) hipLaunchKernelGGL((pwg_cnet_conv_kernel<4, 2, CN_G>), grid, block, 0, s, a);
+            else if (ph.NW == 8) hipLaunchKernelGGL((pwg_cnet_conv_kernel<4, 1, CN_G, false, 8>), grid, dim3(512), 0, s, a);
             else hipLaunchKernelGGL((pwg_cnet_conv_kernel<4, 1, CN_G>), grid, block, 0, s, a);
             break;
         }
