@@ -287,6 +287,43 @@ def program_bytes_per_frame(P):
     return b
 
 
+def vocoder_latency_rows(m, dev, reps=10):
+    """the drop-in's inference() (B = 1, the reference decode loop) and
+    inference_batch (B = 16 equal-length) at T' in {64, 512, 2048}: median wall ms per call with
+    device-resident mels (synchronised), and the kernels' own ms."""
+    rows = []
+    eng = m.engine()
+    hop = eng.hop
+
+    def timed(fn):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) * 1e3
+
+    with torch.no_grad():
+        for F in (64, 512, 2048):
+            for B in (1, 16):
+                mels = [torch.from_numpy(synthetic.make_mel(F, 80, seed=30 + b)).to(dev) for b in range(B)]
+                call = (lambda: m.inference(mels[0])) if B == 1 else (lambda: m.inference_batch(mels))
+                first = timed(call)
+                for _ in range(2):
+                    call()
+                ms = sorted(timed(call) for _ in range(reps))
+                eng.set_timing(True)
+                eng.collect_timing()
+                call()
+                torch.cuda.synchronize(dev)
+                eng.set_timing(False)
+                kern = sum(t for _, t, _ in eng.collect_timing())
+                med = ms[len(ms) // 2]
+                rows.append({"frames": F, "batch": B, "samples_per_call": F * hop * B, "first_call_ms": round(first, 3),
+                             "median_ms": round(med, 3), "kernel_ms": round(kern, 3),
+                             "samples_per_s": round(F * hop * B / (med * 1e-3), 1)})
+    return {"model": f"{type(m).__name__}.inference / inference_batch (drop-in)", "rows": rows}
+
+
 def bench_vocoder(args, rank, world, dev):
     """MelGAN-family generator inference (BASELINE configs[2] multi_band_melgan.v2 and [3]
     hifigan.v1) on the conv-network executor: same ragged-batch workload shape
@@ -369,6 +406,9 @@ def bench_vocoder(args, rank, world, dev):
         cpu = dict({"value": round(done / tt, 1), "unit": "audio samples/s", "cores": threads, "kind": "port",
                     "sample": f"{args.config}: {used} utterances ({done} samples, first of the bench batch), B=1, "
                               f"torch-CPU restatement of the reference op sequence, {threads} threads"}, **info)
+    lat = None
+    if not args.no_latency and world == 1:
+        lat = vocoder_latency_rows(m, dev)
     res = {
         "metric": f"audio samples/sec/GPU ({fs / 1000:g} kHz {args.config}, 80-band mel)",
         "value": round(value, 1),
@@ -404,6 +444,7 @@ def bench_vocoder(args, rank, world, dev):
                       "executed_f16_flop_per_sample": round(3 * fl_frame / hop, 1),
                       "algorithmic_bytes_per_sample": round(by_frame / hop, 1)}),
         "cpu_baseline": cpu,
+        "latency": lat,
     }
     print(json.dumps(res), flush=True)
     if world > 1:

@@ -105,9 +105,16 @@ PWG_API int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, 
  * as one kernel with t kept in LDS; bit-identical to the unfused ops. Applies to 32-channel
  * (weights resident in LDS) and 64-channel (weights streamed) zero-padded pairs (HiFiGAN v1's
  * last two stages).
+ * The same option fuses MelGAN ResidualStacks (dilated conv + the two-source 1x1, up to 96
+ * channels; bit-identical too).
  * PWG_CNET_OPT_PAIR_STEPS (default 16): 128-column tiles per fused-pair workgroup, for plans
- * created afterwards. */
-enum { PWG_CNET_OPT_SPLIT_F16 = 0, PWG_CNET_OPT_FUSE_PAIRS = 1, PWG_CNET_OPT_PAIR_STEPS = 2 };
+ * created afterwards.
+ * PWG_CNET_OPT_XTILE (default 1, split-f16 mode): single-source dilated convs (K = 3/5/7/11, 32, 64
+ * or >= 128 rows per tile) run channel-block-major with the input tile staged once per 16-channel
+ * block (fp32 summation order differs from the tap-major kernel: parity to the oracle, not bit
+ * identity). Conv pairs of such convs then run as two of these launches instead of fused (measured
+ * faster on HiFiGAN v1); 0 restores the tap-major kernel and the fused pairs. */
+enum { PWG_CNET_OPT_SPLIT_F16 = 0, PWG_CNET_OPT_FUSE_PAIRS = 1, PWG_CNET_OPT_PAIR_STEPS = 2, PWG_CNET_OPT_XTILE = 3 };
 PWG_API int pwg_cnet_set_option(PwgCnet* n, int option, long long value);
 PWG_API int pwg_cnet_set_timing(PwgCnet* n, int enable);
 /* Adds per-op milliseconds and launch counts (arrays of n_ops) and clears the records. */

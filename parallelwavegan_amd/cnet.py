@@ -350,6 +350,12 @@ class CnetEngine:
         split-f16 mode only; bit-identical to the unfused ops)."""
         _lib.check(self._lib.pwg_cnet_set_option(self._h, 1, int(bool(enable))))
 
+    def set_xtile(self, enable):
+        """pwg_cnet_set_option(PWG_CNET_OPT_XTILE): dilated convs channel-block-major with the
+        input tile staged once per 16-channel block (default on); off: the tap-major kernel and
+        the fused conv pairs."""
+        _lib.check(self._lib.pwg_cnet_set_option(self._h, 3, int(bool(enable))))
+
     def set_pair_steps(self, steps):
         """pwg_cnet_set_option(PWG_CNET_OPT_PAIR_STEPS): 128-column tiles per fused-pair
         workgroup, for plans created afterwards (cached plans are dropped)."""

@@ -54,6 +54,21 @@ constexpr int CN_G = PWG_CNET_G;   // 16-channel chunks staged per barrier
 #ifndef PWG_CNET_NW8_MT
 #define PWG_CNET_NW8_MT 4  // conv ops with MT >= this run 8-wave workgroups (256 columns); 0: 4 waves (A/B)
 #endif
+#ifndef PWG_CNET_XTILE
+#define PWG_CNET_XTILE 1  // 0: wide dilated convs on the tap-major pwg_cnet_conv_kernel (A/B)
+#endif
+#ifndef PWG_CNET_XTILE_MINMT
+#define PWG_CNET_XTILE_MINMT 1  // smallest row tile (m-tiles of 32) that uses the x-tile kernel
+#endif
+#ifndef PWG_PAIR_OFF
+#define PWG_PAIR_OFF 0  // 1: no conv-pair fusion (A/B)
+#endif
+#ifndef PWG_CNET_XTILE_CB
+#define PWG_CNET_XTILE_CB 1  // most 16-channel blocks the x-tile kernel stages per barrier pair (2/4 measured 1 % slower on HiFiGAN v1, r02_xt5)
+#endif
+#ifndef PWG_CNET_XTILE_LDS
+#define PWG_CNET_XTILE_LDS (150 * 1024)
+#endif
 #ifndef PWG_CNET_DEPTH2
 #define PWG_CNET_DEPTH2 0  // 1: loads two chunk groups ahead (A/B variant)
 #endif
@@ -401,6 +416,240 @@ __global__ void __launch_bounds__(64 * NW) pwg_cnet_conv_kernel(const CnConvArgs
             if (row + i < a.M) yrow[row + i] = v[i];
         }
       }
+  }
+}
+
+// Wide dilated convs (split-f16, >= 128 output rows per tile, K taps > 1): channel-block-major
+// variant of pwg_cnet_conv_kernel with the input tile staged ONCE per 16-channel block.
+// pwg_cnet_conv_kernel walks chunks tap-major and loads every tap's B rows from L2 again (k loads
+// of each input column) while staging one 16-channel A chunk per barrier; on HiFiGAN's 128/256-
+// channel convs that is ~30-40 B per CU-cycle of L2 -> CU traffic, the kernel's limit. Here a
+// workgroup (8 waves x 32 columns = 256 output columns, MT m-tiles of rows) stages, per 16-channel
+// block cb:
+//   * the A fragments of ALL K taps of cb (K x MT x 2 KB), and
+//   * the block's input rows [q0 - pad, q0 + 256 - pad + (K-1) dil) x 16 channels, pre-activated
+//     (normalize, LeakyReLU, edge mode) and pair-split once, [row][hi 16 | lo 16 halves | pad],
+// then every wave runs K x MT x 3 MFMAs with A and B from LDS; the next block's loads are in
+// flight meanwhile (registers), two barriers per block. Same products and pair splits as the
+// tap-major kernel, summed channel-block-major (fp32 rounding order differs; parity vs the oracle).
+struct CnXtileArgs {
+  int K, dil, off_min;    // taps, dilation, first tap's row offset (-pad)
+  int cs;                 // 16-channel blocks of the source
+  int span;               // input rows per block: 256 + (K-1) dil
+};
+__host__ __device__ constexpr bool xtile_supported(int k) { return k == 3 || k == 5 || k == 7 || k == 11; }
+constexpr int XT_COLS = 256;
+constexpr int XT_ROWB = 80;  // bytes per staged input row: 16 hi + 16 lo halves + 16 B pad
+
+template <int MT, int K, int CB>
+__global__ void __launch_bounds__(512) pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
+  constexpr int NTH = 512;
+  constexpr int AV = CB * K * MT * 128;                // A vectors (16 B) per group of CB channel blocks
+  constexpr int AQ = (AV + NTH - 1) / NTH;
+  extern __shared__ __attribute__((aligned(16))) unsigned char xt_smem[];
+  f32x4v* s_a = reinterpret_cast<f32x4v*>(xt_smem);                          // [CB][K][MT][2][64] x 16 B
+  unsigned char* s_x = xt_smem + (size_t)CB * K * MT * 2048;                  // [CB][span][XT_ROWB]
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int hh = lane >> 5;
+  const int cl = lane & 31;
+  const int2 blk = a.blocks[blockIdx.x];
+  const int u = blk.x;
+  const int q0 = blk.y;
+  const int qb = q0 + wave * 32 + cl;
+  const int nq = a.ncols[u];
+  const int m0 = blockIdx.y * MT;
+  const CnSrc& sx = a.src[0];
+  const int2 sg = *reinterpret_cast<const int2*>(sx.seg + 2 * u);
+  const int xv = CB * xt.span * 4;                     // input quads (4 channels) per group
+  constexpr int XQ_MAX = (CB * (XT_COLS + 192) * 4 + NTH - 1) / NTH;
+
+  f32x4v ar[AQ];
+  f32x4v xr[XQ_MAX];
+  bool xok[XQ_MAX];
+  // group g = channel blocks [CB g, CB g + CB): global -> registers
+  auto load = [&](int grp) {
+#pragma unroll
+    for (int i = 0; i < AQ; ++i) {
+      const int idx = threadIdx.x + NTH * i;  // [c][tap][m][128 vectors]
+      const int c = idx / (K * MT * 128), rem1 = idx - c * (K * MT * 128);
+      const int tap = rem1 / (MT * 128), rem = rem1 - tap * (MT * 128);
+      ar[i] = idx < AV ? reinterpret_cast<const f32x4v*>(
+                             a.wfrag + ((size_t)(tap * xt.cs + CB * grp + c) * a.mt_total + m0) * 512)[rem]
+                       : f32x4v{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int i = 0; i < XQ_MAX; ++i) {
+      const int idx = threadIdx.x + NTH * i;  // [c][row][quad]
+      const bool in = idx < xv;
+      const int c = in ? idx / (xt.span * 4) : 0;
+      const int r = in ? (idx >> 2) - c * xt.span : 0, qd = idx & 3;
+      int p = q0 + xt.off_min + r;
+      xok[i] = edge_row(p, sg.y, sx.pad_mode) && in;
+      xr[i] = in ? *reinterpret_cast<const f32x4v*>(sx.x + (size_t)(sg.x + p) * sx.ld + 16 * (CB * grp + c) + 4 * qd)
+                 : f32x4v{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  // registers -> LDS (x pre-activated and pair-split on the way)
+  auto store = [&](int grp) {
+#pragma unroll
+    for (int i = 0; i < AQ; ++i) {
+      const int idx = threadIdx.x + NTH * i;
+      if (idx < AV) s_a[idx] = ar[i];
+    }
+#pragma unroll
+    for (int i = 0; i < XQ_MAX; ++i) {
+      const int idx = threadIdx.x + NTH * i;
+      if (idx >= xv) continue;
+      const int c = idx / (xt.span * 4);
+      const int r = (idx >> 2) - c * xt.span, qd = idx & 3;
+      f32x4v v = xr[i];
+      const int ch = 16 * (CB * grp + c) + 4 * qd;
+      if (sx.normalize) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (v[e] - a.mean[ch + e]) / a.scale[ch + e];
+      }
+      if (sx.slope != 1.f) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * sx.slope;
+      }
+      if (!xok[i]) v = f32x4v{0.f, 0.f, 0.f, 0.f};
+      _Float16 hv[4], lv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        hv[e] = (_Float16)v[e];
+        lv[e] = (_Float16)(v[e] - (float)hv[e]);
+      }
+      unsigned char* row = s_x + ((size_t)c * xt.span + r) * XT_ROWB;
+      *reinterpret_cast<f16x4v*>(row + 8 * qd) = f16x4v{hv[0], hv[1], hv[2], hv[3]};
+      *reinterpret_cast<f16x4v*>(row + 32 + 8 * qd) = f16x4v{lv[0], lv[1], lv[2], lv[3]};
+    }
+  };
+
+  f32x16 acc[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
+
+  const int ngrp = xt.cs / CB;
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int grp = 0; grp < ngrp; ++grp) {
+    const bool more = grp + 1 < ngrp;
+    if (more) load(grp + 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int c = 0; c < CB; ++c)
+#pragma unroll
+      for (int tap = 0; tap < K; ++tap) {
+        const unsigned char* row = s_x + ((size_t)c * xt.span + wave * 32 + cl + tap * xt.dil) * XT_ROWB;
+        const u32x4v bh = *reinterpret_cast<const u32x4v*>(row + 16 * hh);
+        const u32x4v bl = *reinterpret_cast<const u32x4v*>(row + 32 + 16 * hh);
+        const u32x4v* sa = reinterpret_cast<const u32x4v*>(s_a) + (size_t)(c * K + tap) * MT * 128 + lane;
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          const u32x4v ah = sa[(m * 2) * 64], al = sa[(m * 2 + 1) * 64];
+          acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, ah), __builtin_bit_cast(f16x8v, bh),
+                                                          acc[m], 0, 0, 0);
+          acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, ah), __builtin_bit_cast(f16x8v, bl),
+                                                          acc[m], 0, 0, 0);
+          acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, al), __builtin_bit_cast(f16x8v, bh),
+                                                          acc[m], 0, 0, 0);
+        }
+      }
+    __builtin_amdgcn_sched_barrier(0);
+    if (!more) break;
+    __syncthreads();
+    store(grp + 1);
+    __syncthreads();
+  }
+
+  // epilogue (pwg_cnet_conv_kernel's)
+  if (qb >= nq) return;
+  const int2 sd = *reinterpret_cast<const int2*>(a.seg_dst + 2 * u);
+  const int2 sr = a.res ? *reinterpret_cast<const int2*>(a.seg_res + 2 * u) : make_int2(0, 0);
+  const bool quad = (a.ld_dst & 3) == 0;
+  float* yrow = a.y + (size_t)(sd.x + qb) * a.ld_dst;
+  const float* rrow = a.res ? a.res + (size_t)(sr.x + qb) * a.ld_res : nullptr;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int j4 = 0; j4 < 4; ++j4) {
+      const int row = 32 * (m0 + m) + 8 * j4 + 4 * hh;
+      if (row >= a.M) {
+        if (quad && row < a.ld_dst) *reinterpret_cast<f32x4v*>(yrow + row) = f32x4v{0.f, 0.f, 0.f, 0.f};
+        continue;
+      }
+      const f32x4v b = *reinterpret_cast<const f32x4v*>(a.bias + row);
+      f32x4v v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = acc[m][4 * j4 + i] + b[i];
+      if (quad) {
+        if (rrow) v += *reinterpret_cast<const f32x4v*>(rrow + row);
+        if (a.accumulate) v = *reinterpret_cast<const f32x4v*>(yrow + row) + v;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (row + i >= a.M) continue;
+          if (rrow) v[i] += rrow[row + i];
+          if (a.accumulate) v[i] = yrow[row + i] + v[i];
+        }
+      }
+      if (a.out_div != 1.f) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = v[i] / a.out_div;
+      }
+      if (a.post_act == PWG_ACT_LRELU) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = v[i] > 0.f ? v[i] : v[i] * a.post_slope;
+      } else if (a.post_act == PWG_ACT_TANH) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = tanhf(v[i]);
+      }
+      if (quad) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (row + i >= a.M) v[i] = 0.f;
+        *reinterpret_cast<f32x4v*>(yrow + row) = v;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (row + i < a.M) yrow[row + i] = v[i];
+      }
+    }
+}
+
+template <int MT, int K, int CB>
+hipError_t xtile_launch_k(dim3 grid, int lds, hipStream_t s, const CnConvArgs& a, const CnXtileArgs& xt) {
+  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(pwg_cnet_xtile_kernel<MT, K, CB>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((pwg_cnet_xtile_kernel<MT, K, CB>), grid, dim3(512), (size_t)lds, s, a, xt);
+  return hipGetLastError();
+}
+template <int MT, int CB>
+hipError_t xtile_launch_mt(int k, dim3 grid, int lds, hipStream_t s, const CnConvArgs& a, const CnXtileArgs& xt) {
+  switch (k) {
+    case 3: return xtile_launch_k<MT, 3, CB>(grid, lds, s, a, xt);
+    case 5: return xtile_launch_k<MT, 5, CB>(grid, lds, s, a, xt);
+    case 7: return xtile_launch_k<MT, 7, CB>(grid, lds, s, a, xt);
+    case 11: return xtile_launch_k<MT, 11, CB>(grid, lds, s, a, xt);
+    default: return hipErrorInvalidValue;
+  }
+}
+hipError_t xtile_launch(int mt, int k, int cb, dim3 grid, int lds, hipStream_t s, const CnConvArgs& a,
+                        const CnXtileArgs& xt) {
+  if (cb == 4 && mt == 1) return xtile_launch_mt<1, 4>(k, grid, lds, s, a, xt);
+  if (cb == 2 && mt == 2) return xtile_launch_mt<2, 2>(k, grid, lds, s, a, xt);
+  if (cb == 2 && mt == 4) return xtile_launch_mt<4, 2>(k, grid, lds, s, a, xt);
+  if (cb != 1) return hipErrorInvalidValue;
+  switch (mt) {
+    case 1: return xtile_launch_mt<1, 1>(k, grid, lds, s, a, xt);
+    case 2: return xtile_launch_mt<2, 1>(k, grid, lds, s, a, xt);
+    case 4: return xtile_launch_mt<4, 1>(k, grid, lds, s, a, xt);
+    default: return hipErrorInvalidValue;
   }
 }
 
@@ -1316,6 +1565,9 @@ struct OpPhase {          // one launch
   int k_a, off_a;         // CONVT
   int NT;                 // column tiles per wave (workgroup = NW waves x NT x 32 columns)
   int NW = 4;             // waves per workgroup of pwg_cnet_conv_kernel
+  bool xtile = false;     // split mode runs pwg_cnet_xtile_kernel (channel-block-major, staged input tile)
+  int xt_lds = 0;
+  int xt_cb = 1;          // its 16-channel blocks per staging step
   int n_real_chunks = 0;  // chunks before padding to a multiple of CN_G (the rest pack as zeros)
   bool thin = false;      // M <= 8: VALU kernel with an LDS-staged input tile
   int thin_taps[2] = {0, 0}, thin_nc[2] = {0, 0}, thin_base[2] = {0, 0}, thin_off_min[2] = {0, 0},
@@ -1338,6 +1590,7 @@ struct PwgCnet {
   int split_f16 = 1;  // PWG_CNET_OPT_SPLIT_F16
   int fuse_pairs = 1; // PWG_CNET_OPT_FUSE_PAIRS (split-f16 mode only)
   int pair_steps = 16; // PWG_CNET_OPT_PAIR_STEPS: 128-column tiles per fused-pair strip (plan time)
+  int xtile = 1;       // PWG_CNET_OPT_XTILE
   bool pair_attr_set = false;
   std::vector<PwgCnetOp> ops;
   std::vector<int> channels, rate, ld;
@@ -1544,6 +1797,27 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
       ph.NT = 1;  // NT 2/4 for thin row tiles measured SLOWER (fewer workgroups in flight)
       // 8 waves (256 columns) share each staged A chunk of the wide ops (A/B: PWG_CNET_NW8_MT)
       if (PWG_CNET_NW8_MT > 0 && MT >= PWG_CNET_NW8_MT && op.kind == PWG_CNET_CONV) ph.NW = 8;
+      // wide dilated single-source convs: the staged-input-tile kernel (split mode)
+      if (PWG_CNET_XTILE && op.kind == PWG_CNET_CONV && nsrc == 1 && MT >= PWG_CNET_XTILE_MINMT &&
+          (MT == 1 || MT == 2 || MT == 4) && mt_total % MT == 0 &&
+          xtile_supported(op.src[0].taps) && (op.src[0].taps - 1) * op.src[0].dilation <= 191 &&
+          op.src[0].channels % 16 == 0) {
+        ph.xtile = true;
+        ph.NW = 8;  // 256-column blocks
+        // channel blocks staged per barrier pair: the most of {4 (MT 1), 2 (MT 2, 4)} that divides the
+        // source's blocks and fits LDS next to the A fragments
+        const int cs = op.src[0].channels / 16;
+        const int span = XT_COLS + (op.src[0].taps - 1) * op.src[0].dilation;
+        auto lds_of = [&](int cb) { return cb * (op.src[0].taps * MT * 2048 + span * XT_ROWB); };
+        ph.xt_cb = 1;
+        for (int cb : {4, 2})
+          if (((cb == 4 && MT == 1) || (cb == 2 && MT >= 2)) && cs % cb == 0 && lds_of(cb) <= PWG_CNET_XTILE_LDS &&
+              cb * span * 4 <= cb * (XT_COLS + 192) * 4 && PWG_CNET_XTILE_CB >= cb) {
+            ph.xt_cb = cb;
+            break;
+          }
+        ph.xt_lds = lds_of(ph.xt_cb);
+      }
       if (PWG_CNET_NT2_MT > 0 && MT >= PWG_CNET_NT2_MT && op.kind == PWG_CNET_CONV) ph.NT = 2;  // A/B
       ph.ostride = op.kind == PWG_CNET_CONVT ? op.stride : 1;
       ph.ophase = r;
@@ -1606,7 +1880,7 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
     const PwgCnetOp& A = n->ops[pa.op];
     const PwgCnetOp& B = n->ops[pb.op];
     const int C = A.out_channels;
-    if (A.kind != PWG_CNET_CONV || B.kind != PWG_CNET_CONV || pa.thin || pb.thin) continue;
+    if (PWG_PAIR_OFF || A.kind != PWG_CNET_CONV || B.kind != PWG_CNET_CONV || pa.thin || pb.thin) continue;
     if (A.src[1].buf >= 0 || B.src[1].buf >= 0 || B.src[0].buf != A.dst) continue;
     if (A.res >= 0 || A.accumulate || A.out_div != 1.f || A.post_act != PWG_ACT_NONE) continue;
     if (A.src[0].pad_mode != PWG_PAD_ZERO || A.src[0].normalize || B.src[0].pad_mode != PWG_PAD_ZERO) continue;
@@ -1659,7 +1933,7 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
     const PwgCnetOp& A = n->ops[pa.op];
     const PwgCnetOp& B = n->ops[pb.op];
     if (A.kind != PWG_CNET_CONV || B.kind != PWG_CNET_CONV || pa.thin || pb.thin || pa.NT != 1 || pb.NT != 1 ||
-        pa.NW != 4)
+        (pa.NW != 4 && !pa.xtile))
       continue;
     if (A.src[1].buf >= 0 || A.res >= 0 || A.accumulate || A.out_div != 1.f || A.post_act != PWG_ACT_NONE) continue;
     const PwgCnetSrc& b0 = B.src[0];
@@ -1681,6 +1955,8 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
     if (!ok || lds > PR_MAX_LDS) continue;
     pa.stack_b = (int)i + 1;
     pa.stack_lds = (int)lds;
+    pa.xtile = false;  // the fused stack replaces op A's launch (128-column blocks)
+    pa.NW = 4;
   }
   *out = n;  // device tables are uploaded by the first plan: packing needs no GPU
   return PWG_OK;
@@ -1920,10 +2196,14 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
   for (int b = 1; b < nb - 1; ++b) bufs[b] = (float*)((char*)workspace + p->buf_off[b]);
   auto seg_of = [&](int b) -> const int* { return p->d_seg + (size_t)b * p->n_utts * 2; };
   const bool fuse = n->fuse_pairs && n->split_f16;
+  const bool xt = n->xtile && n->split_f16;
+  // a conv pair runs fused unless its convs run on the x-tile kernel (measured faster unfused)
+  auto pair_fused = [&](const OpPhase& q) { return fuse && q.pair_b >= 0 && !(xt && q.xtile); };
   for (size_t pi = 0; pi < n->phases.size(); ++pi) {
     const OpPhase& ph = n->phases[pi];
     const PwgCnetOp& op = n->ops[ph.op];
-    if (fuse && pi > 0 && (n->phases[pi - 1].pair_b == (int)pi || n->phases[pi - 1].stack_b == (int)pi))
+    if (pi > 0 && ((pair_fused(n->phases[pi - 1]) && n->phases[pi - 1].pair_b == (int)pi) ||
+                   (fuse && n->phases[pi - 1].stack_b == (int)pi)))
       continue;  // ran inside the fused pair / stack
     hipEvent_t ea = nullptr, eb = nullptr;
     if (n->timing) {
@@ -1933,7 +2213,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
       }
       (void)hipEventRecord(ea, s);
     }
-    if (fuse && ph.pair_b >= 0) {
+    if (pair_fused(ph)) {
       if (p->n_strips[pi] > 0) {
         const OpPhase& pb = n->phases[ph.pair_b];
         const PwgCnetOp& opb = n->ops[pb.op];
@@ -2054,10 +2334,22 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         else if (op.out_channels <= 4) hipLaunchKernelGGL(pwg_cnet_thin_kernel<4>, tgrid, tblock, 0, s, a, nsrc);
         else hipLaunchKernelGGL(pwg_cnet_thin_kernel<8>, tgrid, tblock, 0, s, a, nsrc);
       } else
-      if (split) {
+      if (xt && ph.xtile) {
+        CnXtileArgs xt;
+        xt.K = op.src[0].taps; xt.dil = op.src[0].dilation; xt.off_min = -op.src[0].pad;
+        xt.cs = op.src[0].channels / 16; xt.span = XT_COLS + (xt.K - 1) * xt.dil;
+        const hipError_t ea2 = xtile_launch(ph.MT, xt.K, ph.xt_cb, grid, ph.xt_lds, s, a, xt);
+        if (ea2 != hipSuccess) return hipf(ea2, "xtile kernel launch");
+      } else if (split) {
         switch (ph.MT) {
-          case 1: hipLaunchKernelGGL((pwg_cnet_conv_kernel<1, 1, CN_G, true>), grid, block, 0, s, a); break;
-          case 2: hipLaunchKernelGGL((pwg_cnet_conv_kernel<2, 1, CN_G, true>), grid, block, 0, s, a); break;
+          case 1:
+            if (ph.NW == 8) hipLaunchKernelGGL((pwg_cnet_conv_kernel<1, 1, CN_G, true, 8>), grid, dim3(512), 0, s, a);
+            else hipLaunchKernelGGL((pwg_cnet_conv_kernel<1, 1, CN_G, true>), grid, block, 0, s, a);
+            break;
+          case 2:
+            if (ph.NW == 8) hipLaunchKernelGGL((pwg_cnet_conv_kernel<2, 1, CN_G, true, 8>), grid, dim3(512), 0, s, a);
+            else hipLaunchKernelGGL((pwg_cnet_conv_kernel<2, 1, CN_G, true>), grid, block, 0, s, a);
+            break;
           case 3: hipLaunchKernelGGL((pwg_cnet_conv_kernel<3, 1, CN_G, true>), grid, block, 0, s, a); break;
           default:
             if (ph.NT == 2) hipLaunchKernelGGL((pwg_cnet_conv_kernel<4, 2, CN_G, true>), grid, block, 0, s, a);
@@ -2067,9 +2359,16 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
             break;
         }
       } else {
+        // (x-tile phases use 256-column blocks: their exact-fp32 form runs 8-wave workgroups)
         switch (ph.MT) {
-          case 1: hipLaunchKernelGGL((pwg_cnet_conv_kernel<1, 1, CN_G>), grid, block, 0, s, a); break;
-          case 2: hipLaunchKernelGGL((pwg_cnet_conv_kernel<2, 1, CN_G>), grid, block, 0, s, a); break;
+          case 1:
+            if (ph.NW == 8) hipLaunchKernelGGL((pwg_cnet_conv_kernel<1, 1, CN_G, false, 8>), grid, dim3(512), 0, s, a);
+            else hipLaunchKernelGGL((pwg_cnet_conv_kernel<1, 1, CN_G>), grid, block, 0, s, a);
+            break;
+          case 2:
+            if (ph.NW == 8) hipLaunchKernelGGL((pwg_cnet_conv_kernel<2, 1, CN_G, false, 8>), grid, dim3(512), 0, s, a);
+            else hipLaunchKernelGGL((pwg_cnet_conv_kernel<2, 1, CN_G>), grid, block, 0, s, a);
+            break;
           case 3: hipLaunchKernelGGL((pwg_cnet_conv_kernel<3, 1, CN_G>), grid, block, 0, s, a); break;
           default:
             if (ph.NT == 2) hipLaunchKernelGGL((pwg_cnet_conv_kernel<4, 2, CN_G>), grid, block, 0, s, a);
@@ -2096,9 +2395,11 @@ int pwg_cnet_set_option(PwgCnet* n, int option, long long value) {
     n->pair_steps = (int)value;
     return PWG_OK;
   }
-  if (option != PWG_CNET_OPT_SPLIT_F16 && option != PWG_CNET_OPT_FUSE_PAIRS) return fail(PWG_ERR_INVALID, "unknown option");
+  if (option != PWG_CNET_OPT_SPLIT_F16 && option != PWG_CNET_OPT_FUSE_PAIRS && option != PWG_CNET_OPT_XTILE)
+    return fail(PWG_ERR_INVALID, "unknown option");
   if (value != 0 && value != 1) return fail(PWG_ERR_INVALID, "option value must be 0 or 1");
-  (option == PWG_CNET_OPT_SPLIT_F16 ? n->split_f16 : n->fuse_pairs) = (int)value;
+  (option == PWG_CNET_OPT_SPLIT_F16 ? n->split_f16 : option == PWG_CNET_OPT_FUSE_PAIRS ? n->fuse_pairs : n->xtile) =
+      (int)value;
   return PWG_OK;
 }
 

@@ -128,6 +128,7 @@ def test_fused_conv_pairs_bitwise_equal_to_unfused(steps, built_lib, cuda_device
     m = m.to(cuda_device)
     eng = m.engine()
     eng.set_pair_steps(steps)
+    eng.set_xtile(False)  # pairs of x-tile convs run unfused (PWG_CNET_OPT_XTILE)
     mels = [synthetic.make_mel(f, 80, seed=60 + i) for i, f in enumerate([3, 1, 14, 5])]
     with torch.no_grad():
         eng.set_fuse_pairs(False)
@@ -192,6 +193,7 @@ def test_fused_residual_stacks_bitwise_equal_to_unfused(cfg, built_lib, cuda_dev
         m.pqmf = PQMF(**configs.VOCODER_PQMF[cfg])
     m = m.to(cuda_device)
     eng = m.engine()
+    eng.set_xtile(False)  # the unfused reference run on the tap-major kernel, like the stack kernel
     mels = [synthetic.make_mel(f, 80, seed=70 + i) for i, f in enumerate([9, 40, 7, 23])]
     with torch.no_grad():
         eng.set_fuse_pairs(False)
@@ -210,3 +212,27 @@ def test_fused_residual_stacks_bitwise_equal_to_unfused(cfg, built_lib, cuda_dev
     assert sum(1 for name, _, n in t if n == 0 and "skip_layer" in name) == stacks
     for a, b in zip(got, ref):
         np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("cfg", ["hifigan_v1", "melgan_v1", "hifigan_v1_causal"])
+def test_xtile_kernel_matches_tap_major(cfg, built_lib, cuda_device):
+    """PWG_CNET_OPT_XTILE: the channel-block-major kernel with staged input tiles sums the same
+    split-f16 products as the tap-major kernel in another order: outputs agree to fp32 rounding
+    (|d| < 1e-5) on ragged batches, edges included; both are pinned to the oracle by the goldens."""
+    from parallelwavegan_amd import configs, synthetic
+    from parallelwavegan_amd.hifigan import HiFiGANGenerator
+    from parallelwavegan_amd.melgan import MelGANGenerator
+
+    cls_name, params = configs.vocoder_params(cfg)
+    m = {"MelGANGenerator": MelGANGenerator, "HiFiGANGenerator": HiFiGANGenerator}[cls_name](**params)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic.make_module_state_dict(m, seed=6).items()})
+    m = m.to(cuda_device)
+    eng = m.engine()
+    mels = [synthetic.make_mel(f, 80, seed=80 + i) for i, f in enumerate([4, 11, 5])]  # reflect pad 3 < T
+    with torch.no_grad():
+        eng.set_xtile(False)
+        ref = [y.cpu().numpy() for y in m.inference_batch(mels)]
+        eng.set_xtile(True)
+        got = [y.cpu().numpy() for y in m.inference_batch(mels)]
+    for a, b in zip(got, ref):
+        assert np.abs(a - b).max() < 1e-5
