@@ -142,7 +142,7 @@ def measure_layer_traffic(args):
             for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
                 env.pop(k, None)
             try:
-                r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=240)
+                r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=150)
             except subprocess.TimeoutExpired:
                 return None, f"rocprofv3 --pmc {ctr} pass timed out"
             if r.returncode != 0:
@@ -597,8 +597,14 @@ def main():
     broadcast = "none (one process)"
     if world > 1:
         if os.environ.get("PWG_BENCH_BACKEND", "nccl") == "nccl":
-            broadcast_weights_rccl(eng, packed, src=0)
-            broadcast = "pwg_broadcast_weights (C-ABI, RCCL over xGMI)"
+            try:
+                broadcast_weights_rccl(eng, packed, src=0)
+                broadcast = "pwg_broadcast_weights (C-ABI, RCCL over xGMI)"
+            except (RuntimeError, OSError, NotImplementedError) as e:  # keep the scaling run alive
+                print(f"[bench] C-ABI RCCL broadcast failed ({e}); using torch.distributed.broadcast",
+                      file=sys.stderr)
+                broadcast_packed_weights(packed, src=0)
+                broadcast = "torch.distributed.broadcast over RCCL (C-ABI broadcast failed)"
         else:
             broadcast_packed_weights(packed, src=0)
             broadcast = "torch.distributed.broadcast (gloo rehearsal)"
@@ -789,7 +795,10 @@ def main():
         "metric": "audio samples/sec/GPU (24 kHz PWG, 80-band mel) + RTF at 1/2/4/8 MI355X",
         "value": round(value, 1),
         "unit": "audio samples/s (whole job, all GPUs)",
-        "n_gpus": world,
+        # ranks sharing a device (the gloo rehearsal on a 1-GPU box) count the devices, not ranks
+        "n_gpus": world if os.environ.get("PWG_BENCH_BACKEND", "nccl") == "nccl"
+                  else min(world, max(torch.cuda.device_count(), 1)),
+        "ranks": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
