@@ -69,6 +69,9 @@ constexpr int CN_G = PWG_CNET_G;   // 16-channel chunks staged per barrier
 #ifndef PWG_CNET_XTILE_LDS
 #define PWG_CNET_XTILE_LDS (150 * 1024)
 #endif
+#ifndef PWG_CNET_CONVT_ONE_LAUNCH
+#define PWG_CNET_CONVT_ONE_LAUNCH 1  // 0: one launch per ConvTranspose phase (A/B)
+#endif
 #ifndef PWG_CNET_DEPTH2
 #define PWG_CNET_DEPTH2 0  // 1: loads two chunk groups ahead (A/B variant)
 #endif
@@ -116,6 +119,11 @@ struct CnConvArgs {
   int ostride, ophase;
   const float* mean;
   const float* scale;
+  // ConvTranspose1d in ONE launch: blockIdx.z = output phase r (phase 0 = the fields above);
+  // phases share the block list (every phase has T / stride columns per utterance)
+  const ChunkDesc* z_chunks[8];
+  const float* z_wfrag[8];
+  const float* z_bias[8];
 };
 
 __device__ __forceinline__ int reflect_row(int p, int T) {
@@ -166,6 +174,12 @@ __global__ void __launch_bounds__(64 * NW) pwg_cnet_conv_kernel(const CnConvArgs
   const int qb = blk.y + wave * 32 * NT + cl;  // this lane's column in n-tile 0 (phase index space)
   const int nq = a.ncols[u];
   const int m0 = blockIdx.y * MT;              // first m-tile of this workgroup
+  // ConvTranspose phase of this workgroup (all phases in one launch; 0 for plain convs)
+  const int zp = blockIdx.z;
+  const ChunkDesc* const chunks_ = zp == 0 ? a.chunks : a.z_chunks[zp];
+  const float* const wfrag_ = zp == 0 ? a.wfrag : a.z_wfrag[zp];
+  const float* const bias_ = zp == 0 ? a.bias : a.z_bias[zp];
+  const int ophase_ = a.ophase + zp;
 
   // B operands of chunk c for the NT column tiles: 8 channels of one input row each. The load
   // (braw) and the pre-activation (bprep) are split so the raw loads of chunk c+1 stay in flight
@@ -176,7 +190,7 @@ __global__ void __launch_bounds__(64 * NW) pwg_cnet_conv_kernel(const CnConvArgs
     int c;
   };
   auto braw = [&](int c, BRaw& r) {
-    const ChunkDesc cd = a.chunks[c];
+    const ChunkDesc cd = chunks_[c];
     const CnSrc& s = a.src[cd.src];
     const int2 sg = *reinterpret_cast<const int2*>(s.seg + 2 * u);
     const int ch = cd.c0 + 8 * hh;
@@ -190,7 +204,7 @@ __global__ void __launch_bounds__(64 * NW) pwg_cnet_conv_kernel(const CnConvArgs
     }
   };
   auto bprep = [&](const BRaw& r, f32x8v (&v)[NT]) {
-    const ChunkDesc cd = a.chunks[r.c];
+    const ChunkDesc cd = chunks_[r.c];
     const CnSrc& s = a.src[cd.src];
     const int ch = cd.c0 + 8 * hh;
 #pragma unroll
@@ -212,7 +226,7 @@ __global__ void __launch_bounds__(64 * NW) pwg_cnet_conv_kernel(const CnConvArgs
   auto aload = [&](int cg, f32x4v (&r)[G][AQ]) {
 #pragma unroll
     for (int g2 = 0; g2 < G; ++g2) {
-      const f32x4v* gp = reinterpret_cast<const f32x4v*>(a.wfrag + ((size_t)(cg * G + g2) * a.mt_total + m0) * 512);
+      const f32x4v* gp = reinterpret_cast<const f32x4v*>(wfrag_ + ((size_t)(cg * G + g2) * a.mt_total + m0) * 512);
 #pragma unroll
       for (int i = 0; i < AQ; ++i) {
         const int idx = threadIdx.x + NTH * i;
@@ -366,7 +380,7 @@ __global__ void __launch_bounds__(64 * NW) pwg_cnet_conv_kernel(const CnConvArgs
   for (int n = 0; n < NT; ++n) {
     const int q = qb + 32 * n;
     if (q >= nq) continue;
-    const int t = q * a.ostride + a.ophase;
+    const int t = q * a.ostride + ophase_;
     float* yrow = a.y + (size_t)(sd.x + t) * a.ld_dst;
     const float* rrow = a.res ? a.res + (size_t)(sr.x + t) * a.ld_res : nullptr;
 #pragma unroll
@@ -379,7 +393,7 @@ __global__ void __launch_bounds__(64 * NW) pwg_cnet_conv_kernel(const CnConvArgs
           if (quad && row < a.ld_dst) *reinterpret_cast<f32x4v*>(yrow + row) = f32x4v{0.f, 0.f, 0.f, 0.f};
           continue;
         }
-        const f32x4v b = *reinterpret_cast<const f32x4v*>(a.bias + row);
+        const f32x4v b = *reinterpret_cast<const f32x4v*>(bias_ + row);
         f32x4v v;
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = acc[m][n][4 * j4 + i] + b[i];
@@ -1568,6 +1582,7 @@ struct OpPhase {          // one launch
   bool xtile = false;     // split mode runs pwg_cnet_xtile_kernel (channel-block-major, staged input tile)
   int xt_lds = 0;
   int xt_cb = 1;          // its 16-channel blocks per staging step
+  int z_phases = 1;       // CONVT phase 0: phases launched together (gridDim.z); others: 0 (merged)
   int n_real_chunks = 0;  // chunks before padding to a multiple of CN_G (the rest pack as zeros)
   bool thin = false;      // M <= 8: VALU kernel with an LDS-staged input tile
   int thin_taps[2] = {0, 0}, thin_nc[2] = {0, 0}, thin_base[2] = {0, 0}, thin_off_min[2] = {0, 0},
@@ -1870,6 +1885,23 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
     }
   }
   n->packed_count = off;
+  // ConvTranspose phases run as ONE launch (gridDim.z = stride) on the tap-major kernel: a launch
+  // per phase left most of the chip idle (MB-MelGAN's x8 upsample: 8 launches of ~380 workgroups)
+  for (size_t i = 0; i < n->phases.size(); ++i) {
+    OpPhase& ph = n->phases[i];
+    const PwgCnetOp& op = n->ops[ph.op];
+    if (op.kind != PWG_CNET_CONVT || ph.phase != 0 || !PWG_CNET_CONVT_ONE_LAUNCH) continue;
+    const int s2 = op.stride;
+    bool ok = s2 <= 8 && i + s2 <= n->phases.size() && !ph.thin && !ph.xtile;
+    for (int r = 1; ok && r < s2; ++r) {
+      const OpPhase& q = n->phases[i + r];
+      ok = q.op == ph.op && q.phase == r && q.MT == ph.MT && q.NT == ph.NT && q.NW == ph.NW && !q.thin &&
+           q.chunks.size() == ph.chunks.size() && q.mt_total == ph.mt_total;
+    }
+    if (!ok) continue;
+    ph.z_phases = s2;
+    for (int r = 1; r < s2; ++r) n->phases[i + r].z_phases = 0;
+  }
   // Fusable pairs (pwg_cnet_pair_kernel): op A = single-source zero-padded conv C_in -> C writing t
   // with no residual / accumulate / division / post activation; the next op B = single-source
   // zero-padded conv C -> C reading t, taps within +-PR_HALO; nobody else reads t.
@@ -2205,6 +2237,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
     if (pi > 0 && ((pair_fused(n->phases[pi - 1]) && n->phases[pi - 1].pair_b == (int)pi) ||
                    (fuse && n->phases[pi - 1].stack_b == (int)pi)))
       continue;  // ran inside the fused pair / stack
+    if (ph.z_phases == 0) continue;  // ran in its ConvTranspose's one launch
     hipEvent_t ea = nullptr, eb = nullptr;
     if (n->timing) {
       for (hipEvent_t* ev : {&ea, &eb}) {
@@ -2327,7 +2360,13 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
       a.accumulate = op.accumulate; a.out_div = op.out_div; a.post_act = op.post_act; a.post_slope = op.post_slope;
       a.blocks = p->d_blocks[pi]; a.ncols = p->d_ncols[pi]; a.ostride = ph.ostride; a.ophase = ph.ophase;
       a.mean = mean; a.scale = scale;
-      const dim3 grid((unsigned)p->n_blocks[pi], (unsigned)(ph.mt_total / ph.MT)), block(256);
+      for (int r = 0; r < 8; ++r) {
+        const OpPhase& q = n->phases[pi + (r < ph.z_phases ? r : 0)];
+        a.z_chunks[r] = q.d_chunks;
+        a.z_wfrag[r] = packed + (split ? q.frag16_off : q.frag_off);
+        a.z_bias[r] = packed + q.bias_off;
+      }
+      const dim3 grid((unsigned)p->n_blocks[pi], (unsigned)(ph.mt_total / ph.MT), (unsigned)ph.z_phases), block(256);
       if (ph.thin) {
         const dim3 tgrid((unsigned)p->n_blocks[pi]), tblock(CN_COLS);
         if (op.out_channels <= 1) hipLaunchKernelGGL(pwg_cnet_thin_kernel<1>, tgrid, tblock, 0, s, a, nsrc);
