@@ -72,6 +72,12 @@ constexpr int CN_G = PWG_CNET_G;   // 16-channel chunks staged per barrier
 #ifndef PWG_CNET_CONVT_ONE_LAUNCH
 #define PWG_CNET_CONVT_ONE_LAUNCH 1  // 0: one launch per ConvTranspose phase (A/B)
 #endif
+#ifndef PWG_CNET_XPAIR
+#define PWG_CNET_XPAIR 1  // 0: x-tile conv pairs as two launches (A/B)
+#endif
+#ifndef PWG_CNET_XPAIR_MAXK
+#define PWG_CNET_XPAIR_MAXK 11  // largest kernel size fused into an x-tile pair
+#endif
 #ifndef PWG_CNET_DEPTH2
 #define PWG_CNET_DEPTH2 0  // 1: loads two chunk groups ahead (A/B variant)
 #endif
@@ -665,6 +671,300 @@ hipError_t xtile_launch(int mt, int k, int cb, dim3 grid, int lds, hipStream_t s
     case 4: return xtile_launch_mt<4, 1>(k, grid, lds, s, a, xt);
     default: return hipErrorInvalidValue;
   }
+}
+
+// Fused conv pair on the x-tile scheme (split-f16; HiFiGAN ResBlock step x = c2(lrelu(c1(lrelu(x)))) + x,
+// layers/residual_block.py:231-237, 32 or 64 channels): one workgroup = 8 waves, 224 output columns.
+//   stage 1: h over the 256 columns [q0 - 16, q0 + 240) (wave w: 32 of them), channel-block-major
+//            exactly as pwg_cnet_xtile_kernel runs conv 1 (A fragments of all taps of a 16-channel
+//            block + the block's pre-activated, pair-split input rows staged once per block);
+//   h + b1, conv 2's LeakyReLU, zero outside the utterance (conv 2's zero padding), pair split ->
+//            an LDS tile [256 rows][hi C | lo C | 16 B];
+//   stage 2: waves 0..6 compute the 7 output tiles from the h tile (conv 2's taps reach within
+//            +-16 columns), channel-block-major as the x-tile kernel runs conv 2; conv 2's
+//            epilogue (+ b2 + residual [+ y_old] [/ div]).
+// Same arithmetic and order as two pwg_cnet_xtile_kernel launches: bit-identical to them. h never
+// leaves the chip: per pair x is read once (+ the L2-hot residual rows), y written once.
+struct CnXpairArgs {
+  int K1, dil1, off1;     // conv 1 taps, dilation, first tap's row offset (-pad)
+  int K2, off2;           // conv 2 taps (dilation 1), first tap's offset
+  int cs;                 // 16-channel blocks (C / 16)
+  int span1;              // conv-1 input rows per block: 256 + (K1-1) dil1
+  float slope_h;          // conv 2's pre-activation
+  const float* w2;        // conv 2 split fragments [tap * cs + cb][MT][hi/lo][lane][4 dwords]
+  const float* b2;
+};
+constexpr int XP_OUT = 224;   // output columns per workgroup (7 tiles; h covers 8)
+
+template <int MT, int K1, int K2>
+__global__ void __launch_bounds__(512) pwg_cnet_xpair_kernel(const CnConvArgs a, const CnXpairArgs xp) {
+  constexpr int NTH = 512;
+  constexpr int C = 32 * MT;
+  constexpr int HROWB = 4 * C + 16;                     // h tile row: hi C halves | lo C halves | pad
+  constexpr int AV1 = K1 * MT * 128, AQ1 = (AV1 + NTH - 1) / NTH;
+  constexpr int AV2 = K2 * MT * 128, AQ2 = (AV2 + NTH - 1) / NTH;
+  constexpr int AQ = AQ1 > AQ2 ? AQ1 : AQ2;
+  constexpr int XQ_MAX = ((XT_COLS + 192) * 4 + NTH - 1) / NTH;
+  extern __shared__ __attribute__((aligned(16))) unsigned char xp_smem[];
+  f32x4v* s_a = reinterpret_cast<f32x4v*>(xp_smem);                                   // A of one block
+  unsigned char* s_x = xp_smem + (size_t)(K1 > K2 ? K1 : K2) * MT * 2048;              // [span1][80 B]
+  unsigned char* s_h = s_x + (size_t)(XT_COLS + 192) * XT_ROWB;                        // [256][HROWB]
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int hh = lane >> 5;
+  const int cl = lane & 31;
+  const int2 blk = a.blocks[blockIdx.x];
+  const int u = blk.x;
+  const int q0 = blk.y;                 // first output column
+  const int h0 = q0 - 16;               // first h column
+  const int nq = a.ncols[u];
+  const CnSrc& sx = a.src[0];
+  const int2 sg = *reinterpret_cast<const int2*>(sx.seg + 2 * u);
+  const int xv = xp.span1 * 4;
+
+  f32x4v ar[AQ];
+  f32x4v xr[XQ_MAX];
+  bool xok[XQ_MAX];
+  auto aload = [&](const float* w, int K, int cb) {
+    const int av = K * MT * 128;
+#pragma unroll
+    for (int i = 0; i < AQ; ++i) {
+      const int idx = threadIdx.x + NTH * i;  // [tap][m][128 vectors]
+      const int tap = idx / (MT * 128), rem = idx - tap * (MT * 128);
+      ar[i] = idx < av ? reinterpret_cast<const f32x4v*>(w + ((size_t)(tap * xp.cs + cb) * MT) * 512)[rem]
+                       : f32x4v{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto astore = [&](int K) {
+    const int av = K * MT * 128;
+#pragma unroll
+    for (int i = 0; i < AQ; ++i) {
+      const int idx = threadIdx.x + NTH * i;
+      if (idx < av) s_a[idx] = ar[i];
+    }
+  };
+  auto xload = [&](int cb) {
+#pragma unroll
+    for (int i = 0; i < XQ_MAX; ++i) {
+      const int idx = threadIdx.x + NTH * i;
+      const bool in = idx < xv;
+      const int r = in ? idx >> 2 : 0, qd = idx & 3;
+      int p = h0 + xp.off1 + r;
+      xok[i] = edge_row(p, sg.y, sx.pad_mode) && in;
+      xr[i] = in ? *reinterpret_cast<const f32x4v*>(sx.x + (size_t)(sg.x + p) * sx.ld + 16 * cb + 4 * qd)
+                 : f32x4v{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto xstore = [&](int cb) {
+#pragma unroll
+    for (int i = 0; i < XQ_MAX; ++i) {
+      const int idx = threadIdx.x + NTH * i;
+      if (idx >= xv) continue;
+      const int r = idx >> 2, qd = idx & 3;
+      f32x4v v = xr[i];
+      const int ch = 16 * cb + 4 * qd;
+      if (sx.normalize) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (v[e] - a.mean[ch + e]) / a.scale[ch + e];
+      }
+      if (sx.slope != 1.f) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * sx.slope;
+      }
+      if (!xok[i]) v = f32x4v{0.f, 0.f, 0.f, 0.f};
+      _Float16 hv[4], lv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        hv[e] = (_Float16)v[e];
+        lv[e] = (_Float16)(v[e] - (float)hv[e]);
+      }
+      unsigned char* row = s_x + (size_t)r * XT_ROWB;
+      *reinterpret_cast<f16x4v*>(row + 8 * qd) = f16x4v{hv[0], hv[1], hv[2], hv[3]};
+      *reinterpret_cast<f16x4v*>(row + 32 + 8 * qd) = f16x4v{lv[0], lv[1], lv[2], lv[3]};
+    }
+  };
+  f32x16 acc[MT];
+  auto mma3 = [&](int m, const u32x4v ah, const u32x4v al, const u32x4v bh, const u32x4v bl) {
+    acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, ah), __builtin_bit_cast(f16x8v, bh),
+                                                    acc[m], 0, 0, 0);
+    acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, ah), __builtin_bit_cast(f16x8v, bl),
+                                                    acc[m], 0, 0, 0);
+    acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, al), __builtin_bit_cast(f16x8v, bh),
+                                                    acc[m], 0, 0, 0);
+  };
+
+  // ---- stage 1: h (conv 1) for h columns h0 + 32 wave + cl
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
+  aload(a.wfrag, K1, 0);
+  xload(0);
+  astore(K1);
+  xstore(0);
+  __syncthreads();
+  for (int cb = 0; cb < xp.cs; ++cb) {
+    const bool more = cb + 1 < xp.cs;
+    if (more) {
+      aload(a.wfrag, K1, cb + 1);
+      xload(cb + 1);
+    } else {
+      aload(xp.w2, K2, 0);  // stage 2's first block, in flight during the last stage-1 block
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int tap = 0; tap < K1; ++tap) {
+      const unsigned char* row = s_x + (size_t)(wave * 32 + cl + tap * xp.dil1) * XT_ROWB;
+      const u32x4v bh = *reinterpret_cast<const u32x4v*>(row + 16 * hh);
+      const u32x4v bl = *reinterpret_cast<const u32x4v*>(row + 32 + 16 * hh);
+      const u32x4v* sa = reinterpret_cast<const u32x4v*>(s_a) + (size_t)tap * MT * 128 + lane;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) mma3(m, sa[(m * 2) * 64], sa[(m * 2 + 1) * 64], bh, bl);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+    if (more) {
+      astore(K1);
+      xstore(cb + 1);
+      __syncthreads();
+    }
+  }
+  // h + b1, conv 2's LeakyReLU, zero outside the utterance, pair split -> h tile row (wave 32 + cl)
+  {
+    const int hcol = h0 + wave * 32 + cl;
+    const bool inside = hcol >= 0 && hcol < nq;
+    unsigned char* hrow = s_h + (size_t)(wave * 32 + cl) * HROWB;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int j4 = 0; j4 < 4; ++j4) {
+        const int row = 32 * m + 8 * j4 + 4 * hh;
+        const f32x4v b = *reinterpret_cast<const f32x4v*>(a.bias + row);
+        _Float16 hv[4], lv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float v = acc[m][4 * j4 + i] + b[i];
+          v = v > 0.f ? v : v * xp.slope_h;
+          v = inside ? v : 0.f;
+          hv[i] = (_Float16)v;
+          lv[i] = (_Float16)(v - (float)hv[i]);
+        }
+        *reinterpret_cast<f16x4v*>(hrow + 2 * row) = f16x4v{hv[0], hv[1], hv[2], hv[3]};
+        *reinterpret_cast<f16x4v*>(hrow + 2 * C + 2 * row) = f16x4v{lv[0], lv[1], lv[2], lv[3]};
+      }
+  }
+  astore(K2);
+  __syncthreads();
+
+  // ---- stage 2: output tile wave (columns q0 + 32 wave + cl), waves 0..6
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
+  for (int cb = 0; cb < xp.cs; ++cb) {
+    const bool more = cb + 1 < xp.cs;
+    if (more) aload(xp.w2, K2, cb + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (wave < XP_OUT / 32) {
+#pragma unroll
+      for (int tap = 0; tap < K2; ++tap) {
+        // output column q0 + 32 wave + cl reads h column + off2 + tap = h row 16 + 32 wave + cl + off2 + tap
+        const unsigned char* hrow = s_h + (size_t)(16 + wave * 32 + cl + xp.off2 + tap) * HROWB;
+        const u32x4v bh = *reinterpret_cast<const u32x4v*>(hrow + 2 * (16 * cb + 8 * hh));
+        const u32x4v bl = *reinterpret_cast<const u32x4v*>(hrow + 2 * C + 2 * (16 * cb + 8 * hh));
+        const u32x4v* sa = reinterpret_cast<const u32x4v*>(s_a) + (size_t)tap * MT * 128 + lane;
+#pragma unroll
+        for (int m = 0; m < MT; ++m) mma3(m, sa[(m * 2) * 64], sa[(m * 2 + 1) * 64], bh, bl);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (!more) break;
+    __syncthreads();
+    astore(K2);
+    __syncthreads();
+  }
+
+  // ---- conv 2's epilogue (pwg_cnet_conv_kernel's)
+  const int qb = q0 + wave * 32 + cl;
+  if (wave >= XP_OUT / 32 || qb >= nq || qb >= q0 + XP_OUT) return;
+  const int2 sd = *reinterpret_cast<const int2*>(a.seg_dst + 2 * u);
+  const int2 sr = a.res ? *reinterpret_cast<const int2*>(a.seg_res + 2 * u) : make_int2(0, 0);
+  const bool quad = (a.ld_dst & 3) == 0;
+  float* yrow = a.y + (size_t)(sd.x + qb) * a.ld_dst;
+  const float* rrow = a.res ? a.res + (size_t)(sr.x + qb) * a.ld_res : nullptr;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int j4 = 0; j4 < 4; ++j4) {
+      const int row = 32 * m + 8 * j4 + 4 * hh;
+      if (row >= a.M) {
+        if (quad && row < a.ld_dst) *reinterpret_cast<f32x4v*>(yrow + row) = f32x4v{0.f, 0.f, 0.f, 0.f};
+        continue;
+      }
+      const f32x4v b = *reinterpret_cast<const f32x4v*>(xp.b2 + row);
+      f32x4v v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = acc[m][4 * j4 + i] + b[i];
+      if (quad) {
+        if (rrow) v += *reinterpret_cast<const f32x4v*>(rrow + row);
+        if (a.accumulate) v = *reinterpret_cast<const f32x4v*>(yrow + row) + v;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (row + i >= a.M) continue;
+          if (rrow) v[i] += rrow[row + i];
+          if (a.accumulate) v[i] = yrow[row + i] + v[i];
+        }
+      }
+      if (a.out_div != 1.f) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = v[i] / a.out_div;
+      }
+      if (a.post_act == PWG_ACT_LRELU) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = v[i] > 0.f ? v[i] : v[i] * a.post_slope;
+      } else if (a.post_act == PWG_ACT_TANH) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = tanhf(v[i]);
+      }
+      if (quad) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (row + i >= a.M) v[i] = 0.f;
+        *reinterpret_cast<f32x4v*>(yrow + row) = v;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (row + i < a.M) yrow[row + i] = v[i];
+      }
+    }
+}
+
+template <int MT, int K1, int K2>
+hipError_t xpair_launch_k(dim3 grid, int lds, hipStream_t s, const CnConvArgs& a, const CnXpairArgs& xp) {
+  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(pwg_cnet_xpair_kernel<MT, K1, K2>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((pwg_cnet_xpair_kernel<MT, K1, K2>), grid, dim3(512), (size_t)lds, s, a, xp);
+  return hipGetLastError();
+}
+template <int MT>
+hipError_t xpair_launch_mt(int k, dim3 grid, int lds, hipStream_t s, const CnConvArgs& a, const CnXpairArgs& xp) {
+  switch (k) {  // HiFiGAN ResBlocks: conv 1 and conv 2 share the kernel size
+    case 3: return xpair_launch_k<MT, 3, 3>(grid, lds, s, a, xp);
+    case 5: return xpair_launch_k<MT, 5, 5>(grid, lds, s, a, xp);
+    case 7: return xpair_launch_k<MT, 7, 7>(grid, lds, s, a, xp);
+    case 11: return xpair_launch_k<MT, 11, 11>(grid, lds, s, a, xp);
+    default: return hipErrorInvalidValue;
+  }
+}
+hipError_t xpair_launch(int mt, int k, dim3 grid, int lds, hipStream_t s, const CnConvArgs& a, const CnXpairArgs& xp) {
+  if (mt == 1) return xpair_launch_mt<1>(k, grid, lds, s, a, xp);
+  if (mt == 2) return xpair_launch_mt<2>(k, grid, lds, s, a, xp);
+  return hipErrorInvalidValue;
+}
+__host__ __device__ constexpr int xpair_lds(int mt, int k, int span1) {
+  return (k * mt * 2048) + (XT_COLS + 192) * XT_ROWB + 256 * (4 * 32 * mt + 16) + 0 * span1;
 }
 
 // Fused MelGAN ResidualStack (split-f16 mode; layers/residual_stack.py:75-85 stack(c) + skip_layer(c)):
@@ -1583,6 +1883,8 @@ struct OpPhase {          // one launch
   int xt_lds = 0;
   int xt_cb = 1;          // its 16-channel blocks per staging step
   int z_phases = 1;       // CONVT phase 0: phases launched together (gridDim.z); others: 0 (merged)
+  int xpair_b = -1;       // x-tile conv pair: phase index of conv 2 (pwg_cnet_xpair_kernel)
+  int xpair_lds = 0;
   int n_real_chunks = 0;  // chunks before padding to a multiple of CN_G (the rest pack as zeros)
   bool thin = false;      // M <= 8: VALU kernel with an LDS-staged input tile
   int thin_taps[2] = {0, 0}, thin_nc[2] = {0, 0}, thin_base[2] = {0, 0}, thin_off_min[2] = {0, 0},
@@ -1631,6 +1933,8 @@ struct PwgCnetPlan {
   std::vector<int*> d_ncols;                 // per phase
   std::vector<int2*> d_strips;               // per phase: fused-pair strips (utt, q0), or null
   std::vector<int> n_strips;
+  std::vector<int2*> d_xblocks;              // per phase: x-tile pair blocks (utt, q0 step XP_OUT), or null
+  std::vector<int> n_xblocks;
   int pair_steps = 16;
 };
 
@@ -1990,6 +2294,37 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
     pa.xtile = false;  // the fused stack replaces op A's launch (128-column blocks)
     pa.NW = 4;
   }
+  // x-tile conv pairs (pwg_cnet_xpair_kernel): both convs on the x-tile kernel, 32 or 64 channels
+  // in one row tile, conv 1 single-source zero-padded with no epilogue extras, conv 2 the only
+  // reader of its output, same kernel size, dilation 1 and taps within +-16 columns.
+  for (size_t i = 0; i + 1 < n->phases.size(); ++i) {
+    OpPhase& pa = n->phases[i];
+    const OpPhase& pb = n->phases[i + 1];
+    if (pb.op != pa.op + 1 || !pa.xtile || !pb.xtile || pa.stack_b >= 0) continue;
+    const PwgCnetOp& A = n->ops[pa.op];
+    const PwgCnetOp& B = n->ops[pb.op];
+    const int C = A.out_channels;
+    if ((C != 32 && C != 64) || pa.MT != C / 32 || pa.mt_total != pa.MT || pb.MT != pa.MT || pb.mt_total != pb.MT) continue;
+    if (A.src[1].buf >= 0 || B.src[1].buf >= 0 || B.src[0].buf != A.dst || A.src[0].channels != C ||
+        B.src[0].channels != C || B.out_channels != C || n->ld[A.dst] != C || n->ld[A.src[0].buf] != C)
+      continue;
+    if (A.res >= 0 || A.accumulate || A.out_div != 1.f || A.post_act != PWG_ACT_NONE) continue;
+    if (A.src[0].pad_mode != PWG_PAD_ZERO || B.src[0].pad_mode != PWG_PAD_ZERO || A.src[0].normalize) continue;
+    const int K = A.src[0].taps;
+    if (B.src[0].taps != K || B.src[0].dilation != 1 || -B.src[0].pad < -16 || -B.src[0].pad + K - 1 > 16) continue;
+    if ((K - 1) * A.src[0].dilation > 192 || K > PWG_CNET_XPAIR_MAXK) continue;
+    if (B.dst != n_bufs - 1 && n->ld[B.dst] % 4 != 0) continue;
+    bool ok = true;
+    for (int k = 0; k < n_ops && ok; ++k) {
+      if (k == pb.op || k == pa.op) continue;
+      const PwgCnetOp& o2 = n->ops[k];
+      ok = o2.src[0].buf != A.dst && o2.src[1].buf != A.dst && o2.res != A.dst && o2.dst != A.dst;
+    }
+    const int lds = xpair_lds(pa.MT, K, 0);
+    if (!ok || lds > PR_MAX_LDS || !PWG_CNET_XPAIR) continue;
+    pa.xpair_b = (int)i + 1;
+    pa.xpair_lds = lds;
+  }
   *out = n;  // device tables are uploaded by the first plan: packing needs no GPU
   return PWG_OK;
 }
@@ -2187,6 +2522,17 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
     }
     p->d_strips.push_back(dstr);
     p->n_strips.push_back((int)strips.size());
+    std::vector<int2> xblocks;
+    if (ph.xpair_b >= 0)
+      for (int u = 0; u < n_utts; ++u)
+        for (int q0 = 0; q0 < ncols[u]; q0 += XP_OUT) xblocks.push_back(make_int2(u, q0));
+    int2* dxb = nullptr;
+    if (e == hipSuccess && !xblocks.empty()) {
+      e = hipMalloc(&dxb, sizeof(int2) * xblocks.size());
+      if (e == hipSuccess) e = hipMemcpy(dxb, xblocks.data(), sizeof(int2) * xblocks.size(), hipMemcpyHostToDevice);
+    }
+    p->d_xblocks.push_back(dxb);
+    p->n_xblocks.push_back((int)xblocks.size());
   }
   if (e != hipSuccess) {
     const int rc = hipf(e, "cnet plan upload");
@@ -2204,6 +2550,7 @@ void pwg_cnet_plan_destroy(PwgCnetPlan* p) {
   for (auto* x : p->d_blocks) if (x) (void)hipFree(x);
   for (auto* x : p->d_ncols) if (x) (void)hipFree(x);
   for (auto* x : p->d_strips) if (x) (void)hipFree(x);
+  for (auto* x : p->d_xblocks) if (x) (void)hipFree(x);
   delete p;
 }
 
@@ -2238,6 +2585,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
                    (fuse && n->phases[pi - 1].stack_b == (int)pi)))
       continue;  // ran inside the fused pair / stack
     if (ph.z_phases == 0) continue;  // ran in its ConvTranspose's one launch
+    if (xt && fuse && pi > 0 && n->phases[pi - 1].xpair_b == (int)pi) continue;  // ran in the x-tile pair
     hipEvent_t ea = nullptr, eb = nullptr;
     if (n->timing) {
       for (hipEvent_t* ev : {&ea, &eb}) {
@@ -2373,7 +2721,25 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         else if (op.out_channels <= 4) hipLaunchKernelGGL(pwg_cnet_thin_kernel<4>, tgrid, tblock, 0, s, a, nsrc);
         else hipLaunchKernelGGL(pwg_cnet_thin_kernel<8>, tgrid, tblock, 0, s, a, nsrc);
       } else
-      if (xt && ph.xtile) {
+      if (xt && fuse && ph.xpair_b >= 0) {
+        const OpPhase& pb = n->phases[ph.xpair_b];
+        const PwgCnetOp& opb = n->ops[pb.op];
+        CnXpairArgs xp;
+        xp.K1 = op.src[0].taps; xp.dil1 = op.src[0].dilation; xp.off1 = -op.src[0].pad;
+        xp.K2 = opb.src[0].taps; xp.off2 = -opb.src[0].pad; xp.cs = op.out_channels / 16;
+        xp.span1 = XT_COLS + (xp.K1 - 1) * xp.dil1; xp.slope_h = opb.src[0].pre_slope;
+        xp.w2 = packed + pb.frag16_off; xp.b2 = packed + pb.bias_off;
+        // conv 2's epilogue fields in a
+        a.res = opb.res >= 0 ? bufs[opb.res] : nullptr; a.seg_res = opb.res >= 0 ? seg_of(opb.res) : nullptr;
+        a.ld_res = opb.res >= 0 ? n->ld[opb.res] : 0;
+        a.y = bufs[opb.dst]; a.seg_dst = seg_of(opb.dst); a.ld_dst = n->ld[opb.dst]; a.M = opb.out_channels;
+        a.accumulate = opb.accumulate; a.out_div = opb.out_div; a.post_act = opb.post_act; a.post_slope = opb.post_slope;
+        a.blocks = p->d_xblocks[pi];
+        if (p->n_xblocks[pi] > 0) {
+          const hipError_t ea2 = xpair_launch(ph.MT, xp.K1, dim3((unsigned)p->n_xblocks[pi]), ph.xpair_lds, s, a, xp);
+          if (ea2 != hipSuccess) return hipf(ea2, "xpair kernel launch");
+        }
+      } else if (xt && ph.xtile) {
         CnXtileArgs xt;
         xt.K = op.src[0].taps; xt.dil = op.src[0].dilation; xt.off_min = -op.src[0].pad;
         xt.cs = op.src[0].channels / 16; xt.span = XT_COLS + (xt.K - 1) * xt.dil;

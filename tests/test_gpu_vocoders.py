@@ -113,6 +113,34 @@ def test_vocoder_timing_and_weight_update(built_lib, cuda_device):
     assert np.abs(y2 - y1).max() > 1e-3
 
 
+@pytest.mark.parametrize("causal", [False, True], ids=["noncausal", "causal"])
+def test_xtile_pairs_bitwise_equal_to_unfused(causal, built_lib, cuda_device):
+    """pwg_cnet_xpair_kernel (HiFiGAN ResBlock conv pairs of 32/64 channels on the x-tile scheme,
+    h in LDS, 224-column workgroups) against the same two convs as two x-tile launches: same
+    chunk order, pair split and epilogue order, so bit-identical; ragged utterances exercise
+    utterance edges inside a workgroup (conv 2's zero padding of h)."""
+    from parallelwavegan_amd import configs, synthetic
+    from parallelwavegan_amd.hifigan import HiFiGANGenerator
+
+    _, params = configs.vocoder_params("hifigan_v1_causal" if causal else "hifigan_v1")
+    m = HiFiGANGenerator(**params)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic.make_module_state_dict(m, seed=4).items()})
+    m = m.to(cuda_device)
+    eng = m.engine()
+    mels = [synthetic.make_mel(f, 80, seed=90 + i) for i, f in enumerate([3, 1, 14, 5])]
+    with torch.no_grad():
+        eng.set_fuse_pairs(False)
+        ref = [y.cpu().numpy() for y in m.inference_batch(mels)]
+        eng.set_fuse_pairs(True)
+        eng.set_timing(True)
+        got = [y.cpu().numpy() for y in m.inference_batch(mels)]
+        t = eng.collect_timing()
+        eng.set_timing(False)
+    assert sum(1 for _, _, n in t if n == 0) == 18  # the 64- and 32-channel stages' 3 x 3 pairs
+    for a, b in zip(got, ref):
+        np.testing.assert_array_equal(a, b)
+
+
 @pytest.mark.parametrize("steps", [1, 3, 8])
 def test_fused_conv_pairs_bitwise_equal_to_unfused(steps, built_lib, cuda_device):
     """pwg_cnet_pair_kernel (ResBlock conv pairs with the intermediate in LDS) against the two
