@@ -668,6 +668,7 @@ hipError_t xtile_launch(int mt, int k, int cb, dim3 grid, int lds, hipStream_t s
   switch (mt) {
     case 1: return xtile_launch_mt<1, 1>(k, grid, lds, s, a, xt);
     case 2: return xtile_launch_mt<2, 1>(k, grid, lds, s, a, xt);
+    case 3: return xtile_launch_mt<3, 1>(k, grid, lds, s, a, xt);
     case 4: return xtile_launch_mt<4, 1>(k, grid, lds, s, a, xt);
     default: return hipErrorInvalidValue;
   }
@@ -2118,7 +2119,7 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
       if (PWG_CNET_NW8_MT > 0 && MT >= PWG_CNET_NW8_MT && op.kind == PWG_CNET_CONV) ph.NW = 8;
       // wide dilated single-source convs: the staged-input-tile kernel (split mode)
       if (PWG_CNET_XTILE && op.kind == PWG_CNET_CONV && nsrc == 1 && MT >= PWG_CNET_XTILE_MINMT &&
-          (MT == 1 || MT == 2 || MT == 4) && mt_total % MT == 0 &&
+          (MT == 1 || MT == 2 || MT == 3 || MT == 4) && mt_total % MT == 0 &&
           xtile_supported(op.src[0].taps) && (op.src[0].taps - 1) * op.src[0].dilation <= 191 &&
           op.src[0].channels % 16 == 0) {
         ph.xtile = true;
@@ -2755,7 +2756,10 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
             if (ph.NW == 8) hipLaunchKernelGGL((pwg_cnet_conv_kernel<2, 1, CN_G, true, 8>), grid, dim3(512), 0, s, a);
             else hipLaunchKernelGGL((pwg_cnet_conv_kernel<2, 1, CN_G, true>), grid, block, 0, s, a);
             break;
-          case 3: hipLaunchKernelGGL((pwg_cnet_conv_kernel<3, 1, CN_G, true>), grid, block, 0, s, a); break;
+          case 3:
+            if (ph.NW == 8) hipLaunchKernelGGL((pwg_cnet_conv_kernel<3, 1, CN_G, true, 8>), grid, dim3(512), 0, s, a);
+            else hipLaunchKernelGGL((pwg_cnet_conv_kernel<3, 1, CN_G, true>), grid, block, 0, s, a);
+            break;
           default:
             if (ph.NT == 2) hipLaunchKernelGGL((pwg_cnet_conv_kernel<4, 2, CN_G, true>), grid, block, 0, s, a);
             else if (ph.NW == 8)
@@ -2774,7 +2778,10 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
             if (ph.NW == 8) hipLaunchKernelGGL((pwg_cnet_conv_kernel<2, 1, CN_G, false, 8>), grid, dim3(512), 0, s, a);
             else hipLaunchKernelGGL((pwg_cnet_conv_kernel<2, 1, CN_G>), grid, block, 0, s, a);
             break;
-          case 3: hipLaunchKernelGGL((pwg_cnet_conv_kernel<3, 1, CN_G>), grid, block, 0, s, a); break;
+          case 3:
+            if (ph.NW == 8) hipLaunchKernelGGL((pwg_cnet_conv_kernel<3, 1, CN_G, false, 8>), grid, dim3(512), 0, s, a);
+            else hipLaunchKernelGGL((pwg_cnet_conv_kernel<3, 1, CN_G>), grid, block, 0, s, a);
+            break;
           default:
             if (ph.NT == 2) hipLaunchKernelGGL((pwg_cnet_conv_kernel<4, 2, CN_G>), grid, block, 0, s, a);
             else if (ph.NW == 8) hipLaunchKernelGGL((pwg_cnet_conv_kernel<4, 1, CN_G, false, 8>), grid, dim3(512), 0, s, a);
