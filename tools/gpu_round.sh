@@ -16,6 +16,10 @@ timeout -k 10 400 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
 cat "$OUT/bench.json"
 timeout -k 10 300 python bench.py --strong --steps 2 --warmup 1 --cpu-seconds 0 --no-latency > "$OUT/strong.json" 2> "$OUT/strong.err"
 cat "$OUT/strong.json"
+for c in hifigan_v1 mb_melgan_v2 melgan_v1; do
+  timeout -k 10 300 python bench.py --config $c > "$OUT/$c.json" 2> "$OUT/$c.err"
+  python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], d['roofline']['frac'])" "$OUT/$c.json" $c
+done
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --cpu-seconds 0 --no-latency > "$GRAFT_REPO_ROOT/$OUT/bench_prof.json" 2> "$GRAFT_REPO_ROOT/$OUT/prof.err"
 cd "$GRAFT_REPO_ROOT"
 python - <<'PY' "$OUT"
