@@ -66,6 +66,9 @@ constexpr int CN_G = PWG_CNET_G;   // 16-channel chunks staged per barrier
 #ifndef PWG_CNET_XTILE_CB
 #define PWG_CNET_XTILE_CB 1  // most 16-channel blocks the x-tile kernel stages per barrier pair (2/4 measured 1 % slower on HiFiGAN v1, r02_xt5)
 #endif
+#ifndef PWG_CNET_XTILE_CB_MAXK
+#define PWG_CNET_XTILE_CB_MAXK 11  // grouping only for kernel sizes up to this (A/B)
+#endif
 #ifndef PWG_CNET_XTILE_LDS
 #define PWG_CNET_XTILE_LDS (150 * 1024)
 #endif
@@ -2132,7 +2135,8 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
         ph.xt_cb = 1;
         for (int cb : {4, 2})
           if (((cb == 4 && MT == 1) || (cb == 2 && MT >= 2)) && cs % cb == 0 && lds_of(cb) <= PWG_CNET_XTILE_LDS &&
-              cb * span * 4 <= cb * (XT_COLS + 192) * 4 && PWG_CNET_XTILE_CB >= cb) {
+              cb * span * 4 <= cb * (XT_COLS + 192) * 4 && PWG_CNET_XTILE_CB >= cb &&
+              op.src[0].taps <= PWG_CNET_XTILE_CB_MAXK) {
             ph.xt_cb = cb;
             break;
           }
