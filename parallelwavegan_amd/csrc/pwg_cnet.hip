@@ -81,6 +81,12 @@ constexpr int CN_G = PWG_CNET_G;   // 16-channel chunks staged per barrier
 #ifndef PWG_CNET_XPAIR_MAXK
 #define PWG_CNET_XPAIR_MAXK 11  // largest kernel size fused into an x-tile pair
 #endif
+#ifndef PWG_CNET_XSTACK
+#define PWG_CNET_XSTACK 1  // 1: ResidualStacks on the x-tile scheme when x-tile is on (A/B)
+#endif
+#ifndef PWG_CNET_XSTACK_OCC2
+#define PWG_CNET_XSTACK_OCC2 1  // 1: size the x-tile stack's LDS for two workgroups per CU when it can (A/B)
+#endif
 #ifndef PWG_CNET_DEPTH2
 #define PWG_CNET_DEPTH2 0  // 1: loads two chunk groups ahead (A/B variant)
 #endif
@@ -1216,6 +1222,312 @@ __global__ void __launch_bounds__(256) pwg_cnet_stack_kernel(const CnStackArgs a
     }
 }
 
+// ResidualStack on the x-tile scheme (split-f16; default with x-tile + fuse-pairs): 8 waves x 32
+// columns = 256 columns per workgroup. Stage 1 is the dilated conv exactly as pwg_cnet_xtile_kernel
+// runs it (per 16-channel block: A fragments of all taps + the block's pre-activated, pair-split
+// input rows staged once); h + b1, the 1x1's LeakyReLU and the pair split go to an LDS tile
+// [256][4 ldh + 16 B] that reuses the input-row space; stage 2 is the two-source 1x1 in op B's
+// chunk order (h chunks from the tile, x chunks from L2, raw) with its A fragments staged g2
+// chunks at a time where stage 1's were. LDS = max(A) + max(input rows, h tile): <= 80 KB (two
+// workgroups per CU) up to 64 channels. Bit-identical to the x-tile conv + the tap-major 1x1.
+constexpr int XS_G2MAX = 12;  // stage-2 chunks per staged group, at most
+struct CnXstackArgs {
+  int K1, dil1, off1, cs1, span1;  // stage 1: taps, dilation, first offset, input blocks, rows
+  int g2;                          // stage-2 chunks staged per group
+  int x_off;                       // LDS byte offset of the input rows / h tile region
+};
+
+template <int MT, int K1>
+__global__ void __launch_bounds__(512) pwg_cnet_xstack_kernel(const CnStackArgs a, const CnXstackArgs xs) {
+  constexpr int NTH = 512;
+  constexpr int AV1 = K1 * MT * 128, AQ1 = (AV1 + NTH - 1) / NTH;
+  constexpr int XQ_MAX = ((XT_COLS + 192) * 4 + NTH - 1) / NTH;
+  constexpr int AQ2 = (XS_G2MAX * MT * 128 + NTH - 1) / NTH;
+  extern __shared__ __attribute__((aligned(16))) unsigned char xs_smem[];
+  f32x4v* s_a = reinterpret_cast<f32x4v*>(xs_smem);
+  unsigned char* s_x = xs_smem + xs.x_off;
+  unsigned char* s_h = s_x;  // after stage 1
+  const int hrowb = 4 * a.ldh + 16;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int hh = lane >> 5;
+  const int cl = lane & 31;
+  const int2 blk = a.blocks[blockIdx.x];
+  const int u = blk.x;
+  const int q0 = blk.y;
+  const int qb = q0 + wave * 32 + cl;
+  const int nq = a.ncols[u];
+  const CnSrc& sx = a.x1;
+  const int2 sg = *reinterpret_cast<const int2*>(sx.seg + 2 * u);
+  const int xv = xs.span1 * 4;
+
+  f32x4v ar[AQ1 > AQ2 ? AQ1 : AQ2];
+  f32x4v xr[XQ_MAX];
+  bool xok[XQ_MAX];
+  f32x16 acc[MT];
+  auto mma3 = [&](int m, const u32x4v ah, const u32x4v al, const u32x4v bh, const u32x4v bl) {
+    acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, ah), __builtin_bit_cast(f16x8v, bh),
+                                                    acc[m], 0, 0, 0);
+    acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, ah), __builtin_bit_cast(f16x8v, bl),
+                                                    acc[m], 0, 0, 0);
+    acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, al), __builtin_bit_cast(f16x8v, bh),
+                                                    acc[m], 0, 0, 0);
+  };
+  // stage 1 block cb: A fragments of all taps + input rows, global -> registers -> LDS
+  auto load1 = [&](int cb) {
+#pragma unroll
+    for (int i = 0; i < AQ1; ++i) {
+      const int idx = threadIdx.x + NTH * i;
+      const int tap = idx / (MT * 128), rem = idx - tap * (MT * 128);
+      ar[i] = idx < AV1 ? reinterpret_cast<const f32x4v*>(a.w1 + ((size_t)(tap * xs.cs1 + cb) * MT) * 512)[rem]
+                        : f32x4v{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int i = 0; i < XQ_MAX; ++i) {
+      const int idx = threadIdx.x + NTH * i;
+      const bool in = idx < xv;
+      const int r = in ? idx >> 2 : 0, qd = idx & 3;
+      int p = q0 + xs.off1 + r;
+      xok[i] = edge_row(p, sg.y, sx.pad_mode) && in;
+      xr[i] = in ? *reinterpret_cast<const f32x4v*>(sx.x + (size_t)(sg.x + p) * sx.ld + 16 * cb + 4 * qd)
+                 : f32x4v{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto store1 = [&](int cb) {
+#pragma unroll
+    for (int i = 0; i < AQ1; ++i) {
+      const int idx = threadIdx.x + NTH * i;
+      if (idx < AV1) s_a[idx] = ar[i];
+    }
+#pragma unroll
+    for (int i = 0; i < XQ_MAX; ++i) {
+      const int idx = threadIdx.x + NTH * i;
+      if (idx >= xv) continue;
+      const int r = idx >> 2, qd = idx & 3;
+      f32x4v v = xr[i];
+      const int ch = 16 * cb + 4 * qd;
+      if (sx.normalize) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (v[e] - a.mean[ch + e]) / a.scale[ch + e];
+      }
+      if (sx.slope != 1.f) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * sx.slope;
+      }
+      if (!xok[i]) v = f32x4v{0.f, 0.f, 0.f, 0.f};
+      _Float16 hv[4], lv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        hv[e] = (_Float16)v[e];
+        lv[e] = (_Float16)(v[e] - (float)hv[e]);
+      }
+      unsigned char* row = s_x + (size_t)r * XT_ROWB;
+      *reinterpret_cast<f16x4v*>(row + 8 * qd) = f16x4v{hv[0], hv[1], hv[2], hv[3]};
+      *reinterpret_cast<f16x4v*>(row + 32 + 8 * qd) = f16x4v{lv[0], lv[1], lv[2], lv[3]};
+    }
+  };
+  // stage 2 group g: op B's chunk fragments [g2 chunks][MT][2][64] x 16 B
+  auto load2 = [&](int grp) {
+    const int av = xs.g2 * MT * 128;
+#pragma unroll
+    for (int i = 0; i < AQ2; ++i) {
+      const int idx = threadIdx.x + NTH * i;
+      ar[i] = idx < av ? reinterpret_cast<const f32x4v*>(a.w2 + (size_t)grp * xs.g2 * MT * 512)[idx]
+                       : f32x4v{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto store2 = [&]() {
+    const int av = xs.g2 * MT * 128;
+#pragma unroll
+    for (int i = 0; i < AQ2; ++i) {
+      const int idx = threadIdx.x + NTH * i;
+      if (idx < av) s_a[idx] = ar[i];
+    }
+  };
+
+  // ---- stage 1: h for columns qb
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
+  load1(0);
+  store1(0);
+  __syncthreads();
+  for (int cb = 0; cb < xs.cs1; ++cb) {
+    const bool more = cb + 1 < xs.cs1;
+    if (more) load1(cb + 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int tap = 0; tap < K1; ++tap) {
+      const unsigned char* row = s_x + (size_t)(wave * 32 + cl + tap * xs.dil1) * XT_ROWB;
+      const u32x4v bh = *reinterpret_cast<const u32x4v*>(row + 16 * hh);
+      const u32x4v bl = *reinterpret_cast<const u32x4v*>(row + 32 + 16 * hh);
+      const u32x4v* sa = reinterpret_cast<const u32x4v*>(s_a) + (size_t)tap * MT * 128 + lane;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) mma3(m, sa[(m * 2) * 64], sa[(m * 2 + 1) * 64], bh, bl);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+    if (more) {
+      store1(cb + 1);
+      __syncthreads();
+    }
+  }
+  // ---- stage 2: op B's chunks over [pre_B(h); x]
+  const unsigned char* hrow = s_h + (size_t)(wave * 32 + cl) * hrowb;
+  const CnSrc& s2 = a.x2;
+  const int2 sg2 = *reinterpret_cast<const int2*>(s2.seg + 2 * u);
+  const int ngrp = a.n2 / xs.g2;
+  // x chunks' B rows (raw, from L2) one chunk ahead
+  f32x8v xr2;
+  bool ok2 = true;
+  auto braw2 = [&](const ChunkDesc& d) {
+    if (d.src == 0) return;
+    int p = qb + d.row_off;
+    ok2 = edge_row(p, sg2.y, s2.pad_mode);
+    xr2 = *reinterpret_cast<const f32x8v*>(s2.x + (size_t)(sg2.x + p) * s2.ld + d.c0 + 8 * hh);
+  };
+  ChunkDesc cd = a.ch2[0];
+  braw2(cd);
+  load2(0);
+  __syncthreads();  // stage 1's last block is done with the staging space
+  store2();
+  // h + b1, the 1x1's LeakyReLU, pair split -> h tile row (wave 32 + cl); rows >= ldh: padding
+  {
+    unsigned char* hw = s_h + (size_t)(wave * 32 + cl) * hrowb;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int j4 = 0; j4 < 4; ++j4) {
+        const int row = 32 * m + 8 * j4 + 4 * hh;
+        if (row >= a.ldh) continue;
+        const f32x4v b = *reinterpret_cast<const f32x4v*>(a.b1 + row);
+        _Float16 hv[4], lv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float v = acc[m][4 * j4 + i] + b[i];
+          v = v > 0.f ? v : v * a.slope_h;
+          hv[i] = (_Float16)v;
+          lv[i] = (_Float16)(v - (float)hv[i]);
+        }
+        *reinterpret_cast<f16x4v*>(hw + 2 * row) = f16x4v{hv[0], hv[1], hv[2], hv[3]};
+        *reinterpret_cast<f16x4v*>(hw + 2 * a.ldh + 2 * row) = f16x4v{lv[0], lv[1], lv[2], lv[3]};
+      }
+  }
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
+  __syncthreads();
+  for (int grp = 0; grp < ngrp; ++grp) {
+    const bool more = grp + 1 < ngrp;
+    if (more) load2(grp + 1);
+    for (int c = 0; c < xs.g2; ++c) {
+      const int ci = grp * xs.g2 + c;
+      u32x4v bh, bl;
+      if (cd.src == 0) {
+        bh = *reinterpret_cast<const u32x4v*>(hrow + 2 * (cd.c0 + 8 * hh));
+        bl = *reinterpret_cast<const u32x4v*>(hrow + 2 * a.ldh + 2 * (cd.c0 + 8 * hh));
+      } else {
+        f32x8v x = xr2;
+        const int ch = cd.c0 + 8 * hh;
+        if (s2.normalize) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) x[i] = (x[i] - a.mean[ch + i]) / a.scale[ch + i];
+        }
+        if (s2.slope != 1.f) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) x[i] = x[i] > 0.f ? x[i] : x[i] * s2.slope;
+        }
+        if (!ok2) x = f32x8v{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        cn_split8(x, bh, bl);
+      }
+      const ChunkDesc cn = ci + 1 < a.n2 ? a.ch2[ci + 1] : cd;
+      if (ci + 1 < a.n2) braw2(cn);
+      const u32x4v* sa = reinterpret_cast<const u32x4v*>(s_a) + (size_t)c * MT * 128 + lane;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) mma3(m, sa[(m * 2) * 64], sa[(m * 2 + 1) * 64], bh, bl);
+      cd = cn;
+    }
+    if (!more) break;
+    __syncthreads();
+    store2();
+    __syncthreads();
+  }
+
+  // ---- op B's epilogue
+  if (qb >= nq) return;
+  const int2 sd = *reinterpret_cast<const int2*>(a.seg_y + 2 * u);
+  const int2 sr = a.res ? *reinterpret_cast<const int2*>(a.seg_res + 2 * u) : make_int2(0, 0);
+  float* yrow = a.y + (size_t)(sd.x + qb) * a.ld_y;
+  const float* rrow = a.res ? a.res + (size_t)(sr.x + qb) * a.ld_res : nullptr;
+  const bool quad = (a.ld_y & 3) == 0;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int j4 = 0; j4 < 4; ++j4) {
+      const int row = 32 * m + 8 * j4 + 4 * hh;
+      if (row >= a.M) {
+        if (quad && row < a.ld_y) *reinterpret_cast<f32x4v*>(yrow + row) = f32x4v{0.f, 0.f, 0.f, 0.f};
+        continue;
+      }
+      const f32x4v b = *reinterpret_cast<const f32x4v*>(a.b2 + row);
+      f32x4v v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = acc[m][4 * j4 + i] + b[i];
+      if (quad) {
+        if (rrow) v += *reinterpret_cast<const f32x4v*>(rrow + row);
+        if (a.accumulate) v = *reinterpret_cast<const f32x4v*>(yrow + row) + v;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (row + i >= a.M) continue;
+          if (rrow) v[i] += rrow[row + i];
+          if (a.accumulate) v[i] = yrow[row + i] + v[i];
+        }
+      }
+      if (a.out_div != 1.f) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = v[i] / a.out_div;
+      }
+      if (a.post_act == PWG_ACT_LRELU) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = v[i] > 0.f ? v[i] : v[i] * a.post_slope;
+      } else if (a.post_act == PWG_ACT_TANH) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = tanhf(v[i]);
+      }
+      if (quad) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (row + i >= a.M) v[i] = 0.f;
+        *reinterpret_cast<f32x4v*>(yrow + row) = v;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (row + i < a.M) yrow[row + i] = v[i];
+      }
+    }
+}
+
+template <int MT, int K1>
+hipError_t xstack_launch_k(dim3 grid, int lds, hipStream_t s, const CnStackArgs& a, const CnXstackArgs& xs) {
+  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(pwg_cnet_xstack_kernel<MT, K1>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((pwg_cnet_xstack_kernel<MT, K1>), grid, dim3(512), (size_t)lds, s, a, xs);
+  return hipGetLastError();
+}
+hipError_t xstack_launch(int mt, int k, dim3 grid, int lds, hipStream_t s, const CnStackArgs& a, const CnXstackArgs& xs) {
+  if (k != 3) return hipErrorInvalidValue;  // MelGAN ResidualStack kernel size
+  switch (mt) {
+    case 1: return xstack_launch_k<1, 3>(grid, lds, s, a, xs);
+    case 2: return xstack_launch_k<2, 3>(grid, lds, s, a, xs);
+    case 3: return xstack_launch_k<3, 3>(grid, lds, s, a, xs);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 // Fused conv pair (split-f16 mode): y = post((conv2(pre2(conv1(pre1(x)) + b1)) + b2 + res [+ y_old]) / div)
 // with conv2's intermediate never leaving the chip. This is HiFiGAN's ResBlock step
 // (layers/residual_block.py:231-237: xt = c1(lrelu(x)); xt = c2(lrelu(xt)); x = xt + x) and any other
@@ -1899,6 +2211,9 @@ struct OpPhase {          // one launch
   int pair_step = 128;        // columns per kernel step (streamed 128-channel pairs: 64)
   int stack_b = -1;           // phase index of the two-source 1x1 fused with this conv (pwg_cnet_stack_kernel)
   int stack_lds = 0;          // its dynamic LDS bytes
+  int xstack_lds = 0;         // > 0: with x-tile on, the stack runs pwg_cnet_xstack_kernel (256-column blocks)
+  int xstack_g2 = 0;          // its stage-2 chunks per staged group
+  int xstack_xoff = 0;        // its input-row / h-tile region offset
 };
 
 }  // namespace
@@ -2296,8 +2611,28 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
     if (!ok || lds > PR_MAX_LDS) continue;
     pa.stack_b = (int)i + 1;
     pa.stack_lds = (int)lds;
-    pa.xtile = false;  // the fused stack replaces op A's launch (128-column blocks)
-    pa.NW = 4;
+    pa.NW = 4;  // the tap-major stack kernel's 128-column blocks (d_blocks)
+    // x-tile on: the stack on the x-tile scheme (k = 3, all rows in one tile, h tile + staging in LDS);
+    // op A unfused runs the x-tile kernel over the same 256-column blocks (d_xblocks)
+    if (pa.xtile && PWG_CNET_XSTACK && A.src[0].taps == 3 && pa.MT == pa.mt_total) {
+      // LDS = A region (stage 1: all taps of one block; stage 2: g2 chunks) + max(input rows, h
+      // tile); g2 = the largest divisor of op B's chunks that keeps the smallest layout's
+      // occupancy (two workgroups per CU when it fits 80 KB)
+      const int span = XT_COLS + 2 * A.src[0].dilation;
+      const int region = std::max(span * XT_ROWB, 256 * (4 * n->ld[A.dst] + 16));
+      const int a1 = 3 * pa.MT * 2048;
+      const int n2 = (int)pb.chunks.size();
+      const int budget = PWG_CNET_XSTACK_OCC2 && a1 + region <= PR_MAX_LDS / 2 ? PR_MAX_LDS / 2 : PR_MAX_LDS;
+      int g2 = 0;
+      for (int g = 1; g <= std::min(n2, XS_G2MAX); ++g)
+        if (n2 % g == 0 && std::max(a1, g * pa.MT * 2048) + region <= budget) g2 = g;
+      if (g2 > 0) {
+        pa.xstack_g2 = g2;
+        pa.xstack_xoff = std::max(a1, g2 * pa.MT * 2048);
+        pa.xstack_lds = pa.xstack_xoff + region;
+      }
+    }
+    if (pa.xstack_lds == 0) pa.xtile = false;
   }
   // x-tile conv pairs (pwg_cnet_xpair_kernel): both convs on the x-tile kernel, 32 or 64 channels
   // in one row tile, conv 1 single-source zero-padded with no epilogue extras, conv 2 the only
@@ -2528,9 +2863,11 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
     p->d_strips.push_back(dstr);
     p->n_strips.push_back((int)strips.size());
     std::vector<int2> xblocks;
-    if (ph.xpair_b >= 0)
+    if (ph.xpair_b >= 0 || (ph.stack_b >= 0 && ph.xtile)) {
+      const int step = ph.xpair_b >= 0 ? XP_OUT : XT_COLS;
       for (int u = 0; u < n_utts; ++u)
-        for (int q0 = 0; q0 < ncols[u]; q0 += XP_OUT) xblocks.push_back(make_int2(u, q0));
+        for (int q0 = 0; q0 < ncols[u]; q0 += step) xblocks.push_back(make_int2(u, q0));
+    }
     int2* dxb = nullptr;
     if (e == hipSuccess && !xblocks.empty()) {
       e = hipMalloc(&dxb, sizeof(int2) * xblocks.size());
@@ -2637,6 +2974,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
       }
     } else if (fuse && ph.stack_b >= 0) {
       if (p->n_blocks[pi] > 0) {
+        const bool xs_on = xt && ph.xtile;
         const OpPhase& pb = n->phases[ph.stack_b];
         const PwgCnetOp& opb = n->ops[pb.op];
         CnStackArgs a;
@@ -2656,8 +2994,17 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         a.ld_res = opb.res >= 0 ? n->ld[opb.res] : 0;
         a.y = bufs[opb.dst]; a.seg_y = seg_of(opb.dst); a.ld_y = n->ld[opb.dst]; a.M = opb.out_channels;
         a.accumulate = opb.accumulate; a.out_div = opb.out_div; a.post_act = opb.post_act; a.post_slope = opb.post_slope;
-        a.blocks = p->d_blocks[pi]; a.ncols = p->d_ncols[pi];
+        a.blocks = xs_on ? p->d_xblocks[pi] : p->d_blocks[pi]; a.ncols = p->d_ncols[pi];
         a.mean = mean; a.scale = scale;
+        if (xs_on) {
+          CnXstackArgs xs;
+          xs.K1 = op.src[0].taps; xs.dil1 = op.src[0].dilation; xs.off1 = -op.src[0].pad;
+          xs.cs1 = op.src[0].channels / 16; xs.span1 = XT_COLS + (xs.K1 - 1) * xs.dil1; xs.g2 = ph.xstack_g2;
+          xs.x_off = ph.xstack_xoff;
+          const hipError_t ea2 =
+              xstack_launch(ph.MT, xs.K1, dim3((unsigned)p->n_xblocks[pi]), ph.xstack_lds, s, a, xs);
+          if (ea2 != hipSuccess) return hipf(ea2, "xstack kernel launch");
+        } else {
         const void* kf = nullptr;
         switch (ph.mt_total) {
           case 1: kf = reinterpret_cast<const void*>(pwg_cnet_stack_kernel<1>); break;
@@ -2679,6 +3026,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
           case 5: hipLaunchKernelGGL(pwg_cnet_stack_kernel<5>, sgrid, dim3(256), (size_t)ph.stack_lds, s, a); break;
           case 6: hipLaunchKernelGGL(pwg_cnet_stack_kernel<6>, sgrid, dim3(256), (size_t)ph.stack_lds, s, a); break;
           default: hipLaunchKernelGGL(pwg_cnet_stack_kernel<7>, sgrid, dim3(256), (size_t)ph.stack_lds, s, a); break;
+        }
         }
       }
     } else if (op.kind == PWG_CNET_PQMF) {
@@ -2748,7 +3096,12 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         CnXtileArgs xt;
         xt.K = op.src[0].taps; xt.dil = op.src[0].dilation; xt.off_min = -op.src[0].pad;
         xt.cs = op.src[0].channels / 16; xt.span = XT_COLS + (xt.K - 1) * xt.dil;
-        const hipError_t ea2 = xtile_launch(ph.MT, xt.K, ph.xt_cb, grid, ph.xt_lds, s, a, xt);
+        dim3 xgrid = grid;
+        if (ph.stack_b >= 0) {  // stack op A: 128-column d_blocks belong to the tap-major stack kernel
+          a.blocks = p->d_xblocks[pi];
+          xgrid.x = (unsigned)p->n_xblocks[pi];
+        }
+        const hipError_t ea2 = xtile_launch(ph.MT, xt.K, ph.xt_cb, xgrid, ph.xt_lds, s, a, xt);
         if (ea2 != hipSuccess) return hipf(ea2, "xtile kernel launch");
       } else if (split) {
         switch (ph.MT) {

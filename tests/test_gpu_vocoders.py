@@ -206,10 +206,12 @@ def test_causal_generators_are_causal(cfg, over, built_lib, cuda_device):
     assert not np.array_equal(y, y2)
 
 
+@pytest.mark.parametrize("xtile", [False, True])
 @pytest.mark.parametrize("cfg", ["mb_melgan_v2", "mb_melgan_v2_causal", "melgan_v1", "mb_melgan_test"])
-def test_fused_residual_stacks_bitwise_equal_to_unfused(cfg, built_lib, cuda_device):
+def test_fused_residual_stacks_bitwise_equal_to_unfused(cfg, xtile, built_lib, cuda_device):
     """pwg_cnet_stack_kernel (MelGAN ResidualStack: dilated conv + the two-source 1x1 in one
-    launch, h in LDS) against the two unfused split-f16 ops: same chunk order, pair split and
+    launch, h in LDS; x-tile off) and pwg_cnet_xstack_kernel (the same on the x-tile scheme; x-tile
+    on) against the two unfused split-f16 ops of the same mode: same chunk order, pair split and
     epilogue order, so bit-identical; every ResidualStack runs fused."""
     from parallelwavegan_amd import configs, synthetic
     from parallelwavegan_amd.melgan import PQMF, MelGANGenerator
@@ -221,8 +223,8 @@ def test_fused_residual_stacks_bitwise_equal_to_unfused(cfg, built_lib, cuda_dev
         m.pqmf = PQMF(**configs.VOCODER_PQMF[cfg])
     m = m.to(cuda_device)
     eng = m.engine()
-    eng.set_xtile(False)  # the unfused reference run on the tap-major kernel, like the stack kernel
-    mels = [synthetic.make_mel(f, 80, seed=70 + i) for i, f in enumerate([9, 40, 7, 23])]
+    eng.set_xtile(xtile)  # off: conv A unfused on the tap-major kernel; on: on the x-tile kernel
+    mels = [synthetic.make_mel(f, 80, seed=70 + i) for i, f in enumerate([9, 40, 7, 23, 300])]
     with torch.no_grad():
         eng.set_fuse_pairs(False)
         ref = [y.cpu().numpy() for y in m.inference_batch(mels)]
