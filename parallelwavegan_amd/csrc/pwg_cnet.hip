@@ -84,6 +84,9 @@ constexpr int CN_G = PWG_CNET_G;   // 16-channel chunks staged per barrier
 #ifndef PWG_CNET_XSTACK
 #define PWG_CNET_XSTACK 1  // 1: ResidualStacks on the x-tile scheme when x-tile is on (A/B)
 #endif
+#ifndef PWG_CNET_XPAIR_OVERLAP
+#define PWG_CNET_XPAIR_OVERLAP 1  // 1: the x-tile pair's h tile reuses the input-row space (A/B)
+#endif
 #ifndef PWG_CNET_XSTACK_OCC2
 #define PWG_CNET_XSTACK_OCC2 1  // 1: size the x-tile stack's LDS for two workgroups per CU when it can (A/B)
 #endif
@@ -718,7 +721,8 @@ __global__ void __launch_bounds__(512) pwg_cnet_xpair_kernel(const CnConvArgs a,
   extern __shared__ __attribute__((aligned(16))) unsigned char xp_smem[];
   f32x4v* s_a = reinterpret_cast<f32x4v*>(xp_smem);                                   // A of one block
   unsigned char* s_x = xp_smem + (size_t)(K1 > K2 ? K1 : K2) * MT * 2048;              // [span1][80 B]
-  unsigned char* s_h = s_x + (size_t)(XT_COLS + 192) * XT_ROWB;                        // [256][HROWB]
+  // [256][HROWB]: after stage 1 (PWG_CNET_XPAIR_OVERLAP: over the input rows, dead by then)
+  unsigned char* s_h = PWG_CNET_XPAIR_OVERLAP ? s_x : s_x + (size_t)(XT_COLS + 192) * XT_ROWB;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int hh = lane >> 5;
@@ -974,7 +978,9 @@ hipError_t xpair_launch(int mt, int k, dim3 grid, int lds, hipStream_t s, const 
   return hipErrorInvalidValue;
 }
 __host__ __device__ constexpr int xpair_lds(int mt, int k, int span1) {
-  return (k * mt * 2048) + (XT_COLS + 192) * XT_ROWB + 256 * (4 * 32 * mt + 16) + 0 * span1;
+  return PWG_CNET_XPAIR_OVERLAP
+             ? k * mt * 2048 + (span1 * XT_ROWB > 256 * (4 * 32 * mt + 16) ? span1 * XT_ROWB : 256 * (4 * 32 * mt + 16))
+             : (k * mt * 2048) + (XT_COLS + 192) * XT_ROWB + 256 * (4 * 32 * mt + 16);
 }
 
 // Fused MelGAN ResidualStack (split-f16 mode; layers/residual_stack.py:75-85 stack(c) + skip_layer(c)):
@@ -2660,7 +2666,7 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
       const PwgCnetOp& o2 = n->ops[k];
       ok = o2.src[0].buf != A.dst && o2.src[1].buf != A.dst && o2.res != A.dst && o2.dst != A.dst;
     }
-    const int lds = xpair_lds(pa.MT, K, 0);
+    const int lds = xpair_lds(pa.MT, K, XT_COLS + (K - 1) * A.src[0].dilation);
     if (!ok || lds > PR_MAX_LDS || !PWG_CNET_XPAIR) continue;
     pa.xpair_b = (int)i + 1;
     pa.xpair_lds = lds;
