@@ -87,6 +87,16 @@ constexpr int CN_G = PWG_CNET_G;   // 16-channel chunks staged per barrier
 #ifndef PWG_CNET_XPAIR_OVERLAP
 #define PWG_CNET_XPAIR_OVERLAP 1  // 1: the x-tile pair's h tile reuses the input-row space (A/B)
 #endif
+#ifndef PWG_CNET_XTILE_CONVT
+#define PWG_CNET_XTILE_CONVT 2  // ConvTranspose phases of <= this many m-tiles on the x-tile kernel: faster
+                                // up to 64 output channels, slower at 128-256 (stride 8; profiles/r02_ct)
+#endif
+#ifndef PWG_CNET_XTILE_CONVT_CB
+#define PWG_CNET_XTILE_CONVT_CB 1  // their channel blocks per staging step, at most (A/B)
+#endif
+#ifndef PWG_CNET_XT_WPE
+#define PWG_CNET_XT_WPE 0  // waves per SIMD asked of the small x-tile kernels (0: compiler's choice; A/B)
+#endif
 #ifndef PWG_CNET_XSTACK_OCC2
 #define PWG_CNET_XSTACK_OCC2 1  // 1: size the x-tile stack's LDS for two workgroups per CU when it can (A/B)
 #endif
@@ -464,17 +474,26 @@ __global__ void __launch_bounds__(64 * NW) pwg_cnet_conv_kernel(const CnConvArgs
 // then every wave runs K x MT x 3 MFMAs with A and B from LDS; the next block's loads are in
 // flight meanwhile (registers), two barriers per block. Same products and pair splits as the
 // tap-major kernel, summed channel-block-major (fp32 rounding order differs; parity vs the oracle).
+// ConvTranspose1d phases run here too (K = 2 taps at rows q + off_a - 1, q + off_a, dilation 1;
+// rev: tap t uses the phase's weight chunk K-1-t; blockIdx.z = phase as in pwg_cnet_conv_kernel).
 struct CnXtileArgs {
   int K, dil, off_min;    // taps, dilation, first tap's row offset (-pad)
   int cs;                 // 16-channel blocks of the source
   int span;               // input rows per block: 256 + (K-1) dil
+  int rev;                // 1: tap t multiplies weight chunk K-1-t (ConvTranspose phases)
+  int z_off[8];           // ConvTranspose: off_min of phase blockIdx.z (z_off[0] = off_min)
 };
 __host__ __device__ constexpr bool xtile_supported(int k) { return k == 3 || k == 5 || k == 7 || k == 11; }
 constexpr int XT_COLS = 256;
 constexpr int XT_ROWB = 80;  // bytes per staged input row: 16 hi + 16 lo halves + 16 B pad
 
+// small shapes (MT 1, K <= 3, one block per step: ConvTranspose phases, 32-channel convs):
+// occupancy is set by VGPRs, PWG_CNET_XT_WPE waves per SIMD requested (0: compiler's choice)
 template <int MT, int K, int CB>
-__global__ void __launch_bounds__(512) pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
+constexpr int xt_wpe() { return (PWG_CNET_XT_WPE > 0 && MT == 1 && K <= 3 && CB == 1) ? PWG_CNET_XT_WPE : 1; }
+template <int MT, int K, int CB>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(xt_wpe<MT, K, CB>())))
+pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
   constexpr int NTH = 512;
   constexpr int AV = CB * K * MT * 128;                // A vectors (16 B) per group of CB channel blocks
   constexpr int AQ = (AV + NTH - 1) / NTH;
@@ -491,6 +510,11 @@ __global__ void __launch_bounds__(512) pwg_cnet_xtile_kernel(const CnConvArgs a,
   const int qb = q0 + wave * 32 + cl;
   const int nq = a.ncols[u];
   const int m0 = blockIdx.y * MT;
+  const int zp = blockIdx.z;  // ConvTranspose phase (0 for convs)
+  const float* const wfrag_ = zp == 0 ? a.wfrag : a.z_wfrag[zp];
+  const float* const bias_ = zp == 0 ? a.bias : a.z_bias[zp];
+  const int ophase_ = a.ophase + zp;
+  const int off_min = xt.z_off[zp];
   const CnSrc& sx = a.src[0];
   const int2 sg = *reinterpret_cast<const int2*>(sx.seg + 2 * u);
   const int xv = CB * xt.span * 4;                     // input quads (4 channels) per group
@@ -506,8 +530,9 @@ __global__ void __launch_bounds__(512) pwg_cnet_xtile_kernel(const CnConvArgs a,
       const int idx = threadIdx.x + NTH * i;  // [c][tap][m][128 vectors]
       const int c = idx / (K * MT * 128), rem1 = idx - c * (K * MT * 128);
       const int tap = rem1 / (MT * 128), rem = rem1 - tap * (MT * 128);
+      const int wt = xt.rev ? K - 1 - tap : tap;
       ar[i] = idx < AV ? reinterpret_cast<const f32x4v*>(
-                             a.wfrag + ((size_t)(tap * xt.cs + CB * grp + c) * a.mt_total + m0) * 512)[rem]
+                             wfrag_ + ((size_t)(wt * xt.cs + CB * grp + c) * a.mt_total + m0) * 512)[rem]
                        : f32x4v{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
@@ -516,7 +541,7 @@ __global__ void __launch_bounds__(512) pwg_cnet_xtile_kernel(const CnConvArgs a,
       const bool in = idx < xv;
       const int c = in ? idx / (xt.span * 4) : 0;
       const int r = in ? (idx >> 2) - c * xt.span : 0, qd = idx & 3;
-      int p = q0 + xt.off_min + r;
+      int p = q0 + off_min + r;
       xok[i] = edge_row(p, sg.y, sx.pad_mode) && in;
       xr[i] = in ? *reinterpret_cast<const f32x4v*>(sx.x + (size_t)(sg.x + p) * sx.ld + 16 * (CB * grp + c) + 4 * qd)
                  : f32x4v{0.f, 0.f, 0.f, 0.f};
@@ -603,8 +628,9 @@ __global__ void __launch_bounds__(512) pwg_cnet_xtile_kernel(const CnConvArgs a,
   const int2 sd = *reinterpret_cast<const int2*>(a.seg_dst + 2 * u);
   const int2 sr = a.res ? *reinterpret_cast<const int2*>(a.seg_res + 2 * u) : make_int2(0, 0);
   const bool quad = (a.ld_dst & 3) == 0;
-  float* yrow = a.y + (size_t)(sd.x + qb) * a.ld_dst;
-  const float* rrow = a.res ? a.res + (size_t)(sr.x + qb) * a.ld_res : nullptr;
+  const int t = qb * a.ostride + ophase_;
+  float* yrow = a.y + (size_t)(sd.x + t) * a.ld_dst;
+  const float* rrow = a.res ? a.res + (size_t)(sr.x + t) * a.ld_res : nullptr;
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -614,7 +640,7 @@ __global__ void __launch_bounds__(512) pwg_cnet_xtile_kernel(const CnConvArgs a,
         if (quad && row < a.ld_dst) *reinterpret_cast<f32x4v*>(yrow + row) = f32x4v{0.f, 0.f, 0.f, 0.f};
         continue;
       }
-      const f32x4v b = *reinterpret_cast<const f32x4v*>(a.bias + row);
+      const f32x4v b = *reinterpret_cast<const f32x4v*>(bias_ + row);
       f32x4v v;
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] = acc[m][4 * j4 + i] + b[i];
@@ -664,6 +690,7 @@ hipError_t xtile_launch_k(dim3 grid, int lds, hipStream_t s, const CnConvArgs& a
 template <int MT, int CB>
 hipError_t xtile_launch_mt(int k, dim3 grid, int lds, hipStream_t s, const CnConvArgs& a, const CnXtileArgs& xt) {
   switch (k) {
+    case 2: return xtile_launch_k<MT, 2, CB>(grid, lds, s, a, xt);
     case 3: return xtile_launch_k<MT, 3, CB>(grid, lds, s, a, xt);
     case 5: return xtile_launch_k<MT, 5, CB>(grid, lds, s, a, xt);
     case 7: return xtile_launch_k<MT, 7, CB>(grid, lds, s, a, xt);
@@ -2442,22 +2469,24 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
       // 8 waves (256 columns) share each staged A chunk of the wide ops (A/B: PWG_CNET_NW8_MT)
       if (PWG_CNET_NW8_MT > 0 && MT >= PWG_CNET_NW8_MT && op.kind == PWG_CNET_CONV) ph.NW = 8;
       // wide dilated single-source convs: the staged-input-tile kernel (split mode)
-      if (PWG_CNET_XTILE && op.kind == PWG_CNET_CONV && nsrc == 1 && MT >= PWG_CNET_XTILE_MINMT &&
-          (MT == 1 || MT == 2 || MT == 3 || MT == 4) && mt_total % MT == 0 &&
-          xtile_supported(op.src[0].taps) && (op.src[0].taps - 1) * op.src[0].dilation <= 191 &&
-          op.src[0].channels % 16 == 0) {
+      // (ConvTranspose phases: 2 taps of dilation 1, PWG_CNET_XTILE_CONVT)
+      const bool convt = op.kind == PWG_CNET_CONVT;
+      const int xk = convt ? 2 : op.src[0].taps, xd = convt ? 1 : op.src[0].dilation;
+      if (PWG_CNET_XTILE && (op.kind == PWG_CNET_CONV || (convt && mt_total <= PWG_CNET_XTILE_CONVT)) && nsrc == 1 &&
+          MT >= PWG_CNET_XTILE_MINMT && (MT == 1 || MT == 2 || MT == 3 || MT == 4) && mt_total % MT == 0 &&
+          (convt || xtile_supported(xk)) && (xk - 1) * xd <= 191 && op.src[0].channels % 16 == 0) {
         ph.xtile = true;
         ph.NW = 8;  // 256-column blocks
         // channel blocks staged per barrier pair: the most of {4 (MT 1), 2 (MT 2, 4)} that divides the
         // source's blocks and fits LDS next to the A fragments
         const int cs = op.src[0].channels / 16;
-        const int span = XT_COLS + (op.src[0].taps - 1) * op.src[0].dilation;
-        auto lds_of = [&](int cb) { return cb * (op.src[0].taps * MT * 2048 + span * XT_ROWB); };
+        const int span = XT_COLS + (xk - 1) * xd;
+        auto lds_of = [&](int cb) { return cb * (xk * MT * 2048 + span * XT_ROWB); };
         ph.xt_cb = 1;
         for (int cb : {4, 2})
           if (((cb == 4 && MT == 1) || (cb == 2 && MT >= 2)) && cs % cb == 0 && lds_of(cb) <= PWG_CNET_XTILE_LDS &&
               cb * span * 4 <= cb * (XT_COLS + 192) * 4 && PWG_CNET_XTILE_CB >= cb &&
-              op.src[0].taps <= PWG_CNET_XTILE_CB_MAXK) {
+              xk <= PWG_CNET_XTILE_CB_MAXK && (!convt || cb <= PWG_CNET_XTILE_CONVT_CB)) {
             ph.xt_cb = cb;
             break;
           }
@@ -3100,8 +3129,13 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         }
       } else if (xt && ph.xtile) {
         CnXtileArgs xt;
-        xt.K = op.src[0].taps; xt.dil = op.src[0].dilation; xt.off_min = -op.src[0].pad;
+        const bool convt = op.kind == PWG_CNET_CONVT;
+        xt.K = convt ? 2 : op.src[0].taps; xt.dil = convt ? 1 : op.src[0].dilation;
+        xt.off_min = convt ? ph.off_a - 1 : -op.src[0].pad;
         xt.cs = op.src[0].channels / 16; xt.span = XT_COLS + (xt.K - 1) * xt.dil;
+        xt.rev = convt ? 1 : 0;
+        for (int r = 0; r < 8; ++r)
+          xt.z_off[r] = convt && r < ph.z_phases ? n->phases[pi + r].off_a - 1 : xt.off_min;
         dim3 xgrid = grid;
         if (ph.stack_b >= 0) {  // stack op A: 128-column d_blocks belong to the tap-major stack kernel
           a.blocks = p->d_xblocks[pi];
