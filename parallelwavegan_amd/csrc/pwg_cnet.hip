@@ -2086,10 +2086,13 @@ __global__ void __launch_bounds__(256) pwg_cnet_pair_stream_kernel(const CnPairA
 // chunk it loads its 16 input channels (pre-activation and edge mode as in the MFMA kernel) and
 // FMAs them with the M x 16 weights, which are wave-uniform scalar loads from the same packed
 // fragments (chunk c, m-tile 0: output o / channel c0+8h+i sit at lane o+32h, k-step i).
+// The staged tile is dynamic LDS sized by the phase's span (a fixed 640-row array held 40 KB per
+// 2-wave workgroup: 4 workgroups per CU).
 constexpr int THIN_MAX_SPAN = 128 + 512;
+constexpr int THIN_ROW = 16;
 template <int M>
 __global__ void __launch_bounds__(128) pwg_cnet_thin_kernel(const CnConvArgs a, int nsrc) {
-  __shared__ __attribute__((aligned(16))) float s_x[THIN_MAX_SPAN * 16];
+  extern __shared__ __attribute__((aligned(16))) float s_x[];  // [span][THIN_ROW]
   const int2 blk = a.blocks[blockIdx.x];
   const int u = blk.x;
   const int q = blk.y + threadIdx.x;
@@ -2117,13 +2120,13 @@ __global__ void __launch_bounds__(128) pwg_cnet_thin_kernel(const CnConvArgs a, 
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * s.slope;
         }
-        *reinterpret_cast<f32x4v*>(s_x + 16 * r + 4 * qd) = ok ? v : f32x4v{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<f32x4v*>(s_x + THIN_ROW * r + 4 * qd) = ok ? v : f32x4v{0.f, 0.f, 0.f, 0.f};
       }
       __syncthreads();
       for (int k = 0; k < s.taps; ++k) {
         const int c = s.chunk_base + k * s.nc + cb;
         const int r = threadIdx.x + a.chunks[c].row_off - s.off_min;
-        const float* xr = s_x + 16 * r;
+        const float* xr = s_x + THIN_ROW * r;
         const float* wf = a.wfrag + (size_t)c * a.mt_total * 512;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -3105,9 +3108,10 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
       const dim3 grid((unsigned)p->n_blocks[pi], (unsigned)(ph.mt_total / ph.MT), (unsigned)ph.z_phases), block(256);
       if (ph.thin) {
         const dim3 tgrid((unsigned)p->n_blocks[pi]), tblock(CN_COLS);
-        if (op.out_channels <= 1) hipLaunchKernelGGL(pwg_cnet_thin_kernel<1>, tgrid, tblock, 0, s, a, nsrc);
-        else if (op.out_channels <= 4) hipLaunchKernelGGL(pwg_cnet_thin_kernel<4>, tgrid, tblock, 0, s, a, nsrc);
-        else hipLaunchKernelGGL(pwg_cnet_thin_kernel<8>, tgrid, tblock, 0, s, a, nsrc);
+        const size_t tl = (size_t)std::max(ph.thin_span[0], ph.thin_span[1]) * THIN_ROW * sizeof(float);
+        if (op.out_channels <= 1) hipLaunchKernelGGL(pwg_cnet_thin_kernel<1>, tgrid, tblock, tl, s, a, nsrc);
+        else if (op.out_channels <= 4) hipLaunchKernelGGL(pwg_cnet_thin_kernel<4>, tgrid, tblock, tl, s, a, nsrc);
+        else hipLaunchKernelGGL(pwg_cnet_thin_kernel<8>, tgrid, tblock, tl, s, a, nsrc);
       } else
       if (xt && fuse && ph.xpair_b >= 0) {
         const OpPhase& pb = n->phases[ph.xpair_b];
