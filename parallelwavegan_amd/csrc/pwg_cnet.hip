@@ -97,6 +97,9 @@ constexpr int CN_G = PWG_CNET_G;   // 16-channel chunks staged per barrier
 #ifndef PWG_CNET_XT_WPE
 #define PWG_CNET_XT_WPE 0  // waves per SIMD asked of the small x-tile kernels (0: compiler's choice; A/B)
 #endif
+#ifndef PWG_CNET_XT_MT2_MAXK
+#define PWG_CNET_XT_MT2_MAXK 7  // >= 256-row convs with <= this many taps: 2 m-tiles per workgroup (0: off; A/B)
+#endif
 #ifndef PWG_CNET_XSTACK_OCC2
 #define PWG_CNET_XSTACK_OCC2 1  // 1: size the x-tile stack's LDS for two workgroups per CU when it can (A/B)
 #endif
@@ -2433,7 +2436,13 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
     }
     if (op.out_div == 0.f) { delete n; return fail(PWG_ERR_INVALID, where + "out_div must be non-zero"); }
     const int mt_total0 = (op.out_channels + 31) / 32;
-    const int MT = pick_mt(mt_total0);
+    int MT = pick_mt(mt_total0);
+    // >= 256-row single-source convs with <= 7 taps run 2 m-tiles per x-tile workgroup (half the A
+    // staging, more workgroups in flight): HiFiGAN v1's 256-channel k = 3 / 7 convs -10 / -12 %;
+    // slower at k = 11 and at 128 rows (profiles/r02_mt2)
+    if (op.kind == PWG_CNET_CONV && op.src[1].buf < 0 && MT == 4 && mt_total0 >= 8 &&
+        op.src[0].taps <= PWG_CNET_XT_MT2_MAXK)
+      MT = 2;
     const int mt_total = (mt_total0 + MT - 1) / MT * MT;
     int n_phase = 1;
     if (op.kind == PWG_CNET_CONVT) {
