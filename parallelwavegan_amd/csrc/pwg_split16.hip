@@ -64,6 +64,9 @@
 #ifndef PWG_SPLIT16_PF
 #define PWG_SPLIT16_PF 0
 #endif
+#ifndef PWG_SPLIT16_DIAG_LDS
+#define PWG_SPLIT16_DIAG_LDS 0  // diagnostic (wrong results, needs PF > 0): taps share A fragments
+#endif
 #ifndef PWG_SPLIT16_MG
 #define PWG_SPLIT16_MG 4  // GEMM-1 m-tiles whose A fragments are read per group
 #endif
@@ -310,6 +313,42 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
       }
     }
   };
+#if PWG_SPLIT16_DIAG_LDS
+  // Diagnostic only (wrong results): the three taps share tap 0's A fragments, so GEMM 1 reads a
+  // third of its LDS bytes (the MFMA count is unchanged): the energy upper bound of register-blocking
+  // more columns per wave.
+  auto mma_3tap_diag = [&](f32x4 (&acc)[8][2], const u32x4 (&t0)[8], const u32x4 (&t1)[8], const u32x4 (&t2)[8]) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int mh = 0; mh < 8 / MG; ++mh) {
+        u32x4 ah[MG], al[MG];
+#pragma unroll
+        for (int mm = 0; mm < MG; ++mm) {
+          const int m = MG * mh + mm;
+          ah[mm] = wgl[((ks * 8 + m) * 2) * 64];
+          al[mm] = wgl[((ks * 8 + m) * 2 + 1) * 64];
+        }
+#pragma unroll
+        for (int mm = 0; mm < MG; ++mm)
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) {
+            f32x4& ac = acc[MG * mh + mm][nt];
+            ac = mma16(ah[mm], t0[nt * 4 + ks * 2], ac);
+            ac = mma16(ah[mm], t0[nt * 4 + ks * 2 + 1], ac);
+            ac = mma16(al[mm], t0[nt * 4 + ks * 2], ac);
+            ac = mma16(ah[mm], t1[nt * 4 + ks * 2], ac);
+            ac = mma16(ah[mm], t1[nt * 4 + ks * 2 + 1], ac);
+            ac = mma16(al[mm], t1[nt * 4 + ks * 2], ac);
+            ac = mma16(ah[mm], t2[nt * 4 + ks * 2], ac);
+            ac = mma16(ah[mm], t2[nt * 4 + ks * 2 + 1], ac);
+            ac = mma16(al[mm], t2[nt * 4 + ks * 2], ac);
+          }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+#endif
   // GEMM-2 out-row seeds sqrt(.5)(x + b_out) from the center tap's pieces: acc2[4 + 2ks + (j>>2)][nt][j&3]
   const f32x4* bo_l = reinterpret_cast<const f32x4*>(s_bo + 16 * g);
   auto x_seed = [&](const u32x4 (&b)[8], f32x4 (&acc2)[8][2]) {
@@ -419,12 +458,22 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
 
 #endif
     if constexpr (PF > 0) {
+#if PWG_SPLIT16_DIAG_LDS
+      load_dv();
+      mma_3tap_diag(acc, b0, b1, b2);
+      bload(bdn, 0, b0);
+      if (!LAST) x_seed(b2, acc2);
+      if (false) {
+#endif
       mma_tap(acc, b0, 0);
       load_dv();
       mma_tap(acc, b1, T1);
       bload(bdn, 0, b0);  // the next block's (bdn = bd when there is none)
       mma_tap(acc, b2, TC);
       if (!LAST) x_seed(b2, acc2);
+#if PWG_SPLIT16_DIAG_LDS
+      }
+#endif
     } else {
       bload(bd, T1, b1);
       mma_tap(acc, b0, 0);
