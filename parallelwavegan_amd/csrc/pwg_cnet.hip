@@ -84,6 +84,9 @@ constexpr int CN_G = PWG_CNET_G;   // 16-channel chunks staged per barrier
 #ifndef PWG_CNET_XSTACK
 #define PWG_CNET_XSTACK 1  // 1: ResidualStacks on the x-tile scheme when x-tile is on (A/B)
 #endif
+#ifndef PWG_CNET_XPAIR_C128
+#define PWG_CNET_XPAIR_C128 1  // 1: 128-channel k = 3 pairs on the x-tile pair kernel too (159.7 KB of LDS; A/B)
+#endif
 #ifndef PWG_CNET_XPAIR_OVERLAP
 #define PWG_CNET_XPAIR_OVERLAP 1  // 1: the x-tile pair's h tile reuses the input-row space (A/B)
 #endif
@@ -717,7 +720,7 @@ hipError_t xtile_launch(int mt, int k, int cb, dim3 grid, int lds, hipStream_t s
 }
 
 // Fused conv pair on the x-tile scheme (split-f16; HiFiGAN ResBlock step x = c2(lrelu(c1(lrelu(x)))) + x,
-// layers/residual_block.py:231-237, 32 or 64 channels): one workgroup = 8 waves, 224 output columns.
+// layers/residual_block.py:231-237, 32 or 64 channels, 128 at k = 3): one workgroup = 8 waves, 224 output columns.
 //   stage 1: h over the 256 columns [q0 - 16, q0 + 240) (wave w: 32 of them), channel-block-major
 //            exactly as pwg_cnet_xtile_kernel runs conv 1 (A fragments of all taps of a 16-channel
 //            block + the block's pre-activated, pair-split input rows staged once per block);
@@ -1005,6 +1008,10 @@ hipError_t xpair_launch_mt(int k, dim3 grid, int lds, hipStream_t s, const CnCon
 hipError_t xpair_launch(int mt, int k, dim3 grid, int lds, hipStream_t s, const CnConvArgs& a, const CnXpairArgs& xp) {
   if (mt == 1) return xpair_launch_mt<1>(k, grid, lds, s, a, xp);
   if (mt == 2) return xpair_launch_mt<2>(k, grid, lds, s, a, xp);
+#if PWG_CNET_XPAIR_C128
+  // 128 channels: only k = 3 fits (A of one block 24 KB + the h tile 256 x 528 B = 159.7 KB)
+  if (mt == 4 && k == 3) return xpair_launch_k<4, 3, 3>(grid, lds, s, a, xp);
+#endif
   return hipErrorInvalidValue;
 }
 __host__ __device__ constexpr int xpair_lds(int mt, int k, int span1) {
@@ -2682,7 +2689,7 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
     if (pa.xstack_lds == 0) pa.xtile = false;
   }
   // x-tile conv pairs (pwg_cnet_xpair_kernel): both convs on the x-tile kernel, 32 or 64 channels
-  // in one row tile, conv 1 single-source zero-padded with no epilogue extras, conv 2 the only
+  // (128 at k = 3) in one row tile, conv 1 single-source zero-padded with no epilogue extras, conv 2 the only
   // reader of its output, same kernel size, dilation 1 and taps within +-16 columns.
   for (size_t i = 0; i + 1 < n->phases.size(); ++i) {
     OpPhase& pa = n->phases[i];
@@ -2691,7 +2698,8 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
     const PwgCnetOp& A = n->ops[pa.op];
     const PwgCnetOp& B = n->ops[pb.op];
     const int C = A.out_channels;
-    if ((C != 32 && C != 64) || pa.MT != C / 32 || pa.mt_total != pa.MT || pb.MT != pa.MT || pb.mt_total != pb.MT) continue;
+    const bool c128 = PWG_CNET_XPAIR_C128 && C == 128 && A.src[0].taps == 3;
+    if ((C != 32 && C != 64 && !c128) || pa.MT != C / 32 || pa.mt_total != pa.MT || pb.MT != pa.MT || pb.mt_total != pb.MT) continue;
     if (A.src[1].buf >= 0 || B.src[1].buf >= 0 || B.src[0].buf != A.dst || A.src[0].channels != C ||
         B.src[0].channels != C || B.out_channels != C || n->ld[A.dst] != C || n->ld[A.src[0].buf] != C)
       continue;
