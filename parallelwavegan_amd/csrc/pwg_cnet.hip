@@ -100,6 +100,11 @@ constexpr int CN_G = PWG_CNET_G;   // 16-channel chunks staged per barrier
 #ifndef PWG_CNET_XT_WPE
 #define PWG_CNET_XT_WPE 0  // waves per SIMD asked of the small x-tile kernels (0: compiler's choice; A/B)
 #endif
+#ifndef PWG_CNET_XT_NC2
+#define PWG_CNET_XT_NC2 0  // unfused x-tile convs with 512 columns per workgroup: 0 never, 1 where the
+                           // workgroups per CU do not drop, 2 wherever it fits LDS (A/B: bit-identical,
+                           // not faster: HiFiGAN v1 58.6 ms off, 61.8 ms with 1 or 2, profiles/r02_nc)
+#endif
 #ifndef PWG_CNET_XT_MT2_MAXK
 #define PWG_CNET_XT_MT2_MAXK 7  // >= 256-row convs with <= this many taps: 2 m-tiles per workgroup (0: off; A/B)
 #endif
@@ -497,7 +502,11 @@ constexpr int XT_ROWB = 80;  // bytes per staged input row: 16 hi + 16 lo halves
 // occupancy is set by VGPRs, PWG_CNET_XT_WPE waves per SIMD requested (0: compiler's choice)
 template <int MT, int K, int CB>
 constexpr int xt_wpe() { return (PWG_CNET_XT_WPE > 0 && MT == 1 && K <= 3 && CB == 1) ? PWG_CNET_XT_WPE : 1; }
-template <int MT, int K, int CB>
+// NC column tiles of 256 per workgroup (wave w: columns 256 nc + 32 w + [0, 32)): the staged A
+// fragments of a channel block serve NC x 256 columns, so NC = 2 halves the L2 -> LDS weight bytes
+// per column (PWG_CNET_XT_NC2). Every accumulator sums the same products in the same order as
+// with NC = 1: bit-identical.
+template <int MT, int K, int CB, int NC = 1>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(xt_wpe<MT, K, CB>())))
 pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
   constexpr int NTH = 512;
@@ -513,10 +522,11 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
   const int2 blk = a.blocks[blockIdx.x];
   const int u = blk.x;
   const int q0 = blk.y;
-  const int qb = q0 + wave * 32 + cl;
   const int nq = a.ncols[u];
   const int m0 = blockIdx.y * MT;
   const int zp = blockIdx.z;  // ConvTranspose phase (0 for convs)
+  // column tiles holding live columns (uniform over the workgroup)
+  const int nc_live = NC == 1 ? 1 : (nq - q0 > XT_COLS ? NC : 1);
   const float* const wfrag_ = zp == 0 ? a.wfrag : a.z_wfrag[zp];
   const float* const bias_ = zp == 0 ? a.bias : a.z_bias[zp];
   const int ophase_ = a.ophase + zp;
@@ -524,7 +534,7 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
   const CnSrc& sx = a.src[0];
   const int2 sg = *reinterpret_cast<const int2*>(sx.seg + 2 * u);
   const int xv = CB * xt.span * 4;                     // input quads (4 channels) per group
-  constexpr int XQ_MAX = (CB * (XT_COLS + 192) * 4 + NTH - 1) / NTH;
+  constexpr int XQ_MAX = (CB * (NC * XT_COLS + 192) * 4 + NTH - 1) / NTH;
 
   f32x4v ar[AQ];
   f32x4v xr[XQ_MAX];
@@ -589,11 +599,13 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
     }
   };
 
-  f32x16 acc[MT];
+  f32x16 acc[NC][MT];
 #pragma unroll
-  for (int m = 0; m < MT; ++m)
+  for (int nc = 0; nc < NC; ++nc)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[nc][m][r] = 0.f;
 
   const int ngrp = xt.cs / CB;
   load(0);
@@ -607,19 +619,29 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
     for (int c = 0; c < CB; ++c)
 #pragma unroll
       for (int tap = 0; tap < K; ++tap) {
-        const unsigned char* row = s_x + ((size_t)c * xt.span + wave * 32 + cl + tap * xt.dil) * XT_ROWB;
-        const u32x4v bh = *reinterpret_cast<const u32x4v*>(row + 16 * hh);
-        const u32x4v bl = *reinterpret_cast<const u32x4v*>(row + 32 + 16 * hh);
         const u32x4v* sa = reinterpret_cast<const u32x4v*>(s_a) + (size_t)(c * K + tap) * MT * 128 + lane;
+        u32x4v bh[NC], bl[NC];
+#pragma unroll
+        for (int nc = 0; nc < NC; ++nc) {
+          const unsigned char* row =
+              s_x + ((size_t)c * xt.span + nc * XT_COLS + wave * 32 + cl + tap * xt.dil) * XT_ROWB;
+          bh[nc] = *reinterpret_cast<const u32x4v*>(row + 16 * hh);
+          bl[nc] = *reinterpret_cast<const u32x4v*>(row + 32 + 16 * hh);
+        }
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
           const u32x4v ah = sa[(m * 2) * 64], al = sa[(m * 2 + 1) * 64];
-          acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, ah), __builtin_bit_cast(f16x8v, bh),
-                                                          acc[m], 0, 0, 0);
-          acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, ah), __builtin_bit_cast(f16x8v, bl),
-                                                          acc[m], 0, 0, 0);
-          acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, al), __builtin_bit_cast(f16x8v, bh),
-                                                          acc[m], 0, 0, 0);
+#pragma unroll
+          for (int nc = 0; nc < NC; ++nc) {
+            if (nc > 0 && nc >= nc_live) continue;
+            f32x16& ac = acc[nc][m];
+            ac = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, ah), __builtin_bit_cast(f16x8v, bh[nc]),
+                                                        ac, 0, 0, 0);
+            ac = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, ah), __builtin_bit_cast(f16x8v, bl[nc]),
+                                                        ac, 0, 0, 0);
+            ac = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, al), __builtin_bit_cast(f16x8v, bh[nc]),
+                                                        ac, 0, 0, 0);
+          }
         }
       }
     __builtin_amdgcn_sched_barrier(0);
@@ -630,10 +652,13 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
   }
 
   // epilogue (pwg_cnet_conv_kernel's)
-  if (qb >= nq) return;
   const int2 sd = *reinterpret_cast<const int2*>(a.seg_dst + 2 * u);
   const int2 sr = a.res ? *reinterpret_cast<const int2*>(a.seg_res + 2 * u) : make_int2(0, 0);
   const bool quad = (a.ld_dst & 3) == 0;
+#pragma unroll
+  for (int nc = 0; nc < NC; ++nc) {
+  const int qb = q0 + nc * XT_COLS + wave * 32 + cl;
+  if (qb >= nq) break;
   const int t = qb * a.ostride + ophase_;
   float* yrow = a.y + (size_t)(sd.x + t) * a.ld_dst;
   const float* rrow = a.res ? a.res + (size_t)(sr.x + t) * a.ld_res : nullptr;
@@ -649,7 +674,7 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
       const f32x4v b = *reinterpret_cast<const f32x4v*>(bias_ + row);
       f32x4v v;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = acc[m][4 * j4 + i] + b[i];
+      for (int i = 0; i < 4; ++i) v[i] = acc[nc][m][4 * j4 + i] + b[i];
       if (quad) {
         if (rrow) v += *reinterpret_cast<const f32x4v*>(rrow + row);
         if (a.accumulate) v = *reinterpret_cast<const f32x4v*>(yrow + row) + v;
@@ -683,15 +708,26 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
           if (row + i < a.M) yrow[row + i] = v[i];
       }
     }
+  }
 }
 
-template <int MT, int K, int CB>
+template <int MT, int K, int CB, int NC = 1>
 hipError_t xtile_launch_k(dim3 grid, int lds, hipStream_t s, const CnConvArgs& a, const CnXtileArgs& xt) {
-  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(pwg_cnet_xtile_kernel<MT, K, CB>),
+  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(pwg_cnet_xtile_kernel<MT, K, CB, NC>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((pwg_cnet_xtile_kernel<MT, K, CB>), grid, dim3(512), (size_t)lds, s, a, xt);
+  hipLaunchKernelGGL((pwg_cnet_xtile_kernel<MT, K, CB, NC>), grid, dim3(512), (size_t)lds, s, a, xt);
   return hipGetLastError();
+}
+template <int MT>
+hipError_t xtile_launch_nc2(int k, dim3 grid, int lds, hipStream_t s, const CnConvArgs& a, const CnXtileArgs& xt) {
+  switch (k) {
+    case 3: return xtile_launch_k<MT, 3, 1, 2>(grid, lds, s, a, xt);
+    case 5: return xtile_launch_k<MT, 5, 1, 2>(grid, lds, s, a, xt);
+    case 7: return xtile_launch_k<MT, 7, 1, 2>(grid, lds, s, a, xt);
+    case 11: return xtile_launch_k<MT, 11, 1, 2>(grid, lds, s, a, xt);
+    default: return hipErrorInvalidValue;
+  }
 }
 template <int MT, int CB>
 hipError_t xtile_launch_mt(int k, dim3 grid, int lds, hipStream_t s, const CnConvArgs& a, const CnXtileArgs& xt) {
@@ -704,8 +740,22 @@ hipError_t xtile_launch_mt(int k, dim3 grid, int lds, hipStream_t s, const CnCon
     default: return hipErrorInvalidValue;
   }
 }
-hipError_t xtile_launch(int mt, int k, int cb, dim3 grid, int lds, hipStream_t s, const CnConvArgs& a,
+hipError_t xtile_launch(int mt, int k, int cb, int nc, dim3 grid, int lds, hipStream_t s, const CnConvArgs& a,
                         const CnXtileArgs& xt) {
+  if (nc == 2) {
+    if constexpr (PWG_CNET_XT_NC2 != 0) {  // instantiated only in A/B builds
+      if (cb != 1) return hipErrorInvalidValue;
+      switch (mt) {
+        case 1: return xtile_launch_nc2<1>(k, grid, lds, s, a, xt);
+        case 2: return xtile_launch_nc2<2>(k, grid, lds, s, a, xt);
+        case 3: return xtile_launch_nc2<3>(k, grid, lds, s, a, xt);
+        case 4: return xtile_launch_nc2<4>(k, grid, lds, s, a, xt);
+        default: return hipErrorInvalidValue;
+      }
+    }
+    return hipErrorInvalidValue;
+  }
+  if (nc != 1) return hipErrorInvalidValue;
   if (cb == 4 && mt == 1) return xtile_launch_mt<1, 4>(k, grid, lds, s, a, xt);
   if (cb == 2 && mt == 2) return xtile_launch_mt<2, 2>(k, grid, lds, s, a, xt);
   if (cb == 2 && mt == 4) return xtile_launch_mt<4, 2>(k, grid, lds, s, a, xt);
@@ -2244,6 +2294,7 @@ struct OpPhase {          // one launch
   bool xtile = false;     // split mode runs pwg_cnet_xtile_kernel (channel-block-major, staged input tile)
   int xt_lds = 0;
   int xt_cb = 1;          // its 16-channel blocks per staging step
+  int xt_nc = 1;          // its 256-column tiles per workgroup (2: 512-column blocks in d_xblocks)
   int z_phases = 1;       // CONVT phase 0: phases launched together (gridDim.z); others: 0 (merged)
   int xpair_b = -1;       // x-tile conv pair: phase index of conv 2 (pwg_cnet_xpair_kernel)
   int xpair_lds = 0;
@@ -2720,6 +2771,21 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
     pa.xpair_b = (int)i + 1;
     pa.xpair_lds = lds;
   }
+  // unfused x-tile convs: 512 columns per workgroup where the weights' L2 -> LDS staging is the
+  // larger share (the A fragments of a channel block then serve twice the columns)
+  for (size_t i = 0; i < n->phases.size(); ++i) {
+    OpPhase& ph = n->phases[i];
+    const PwgCnetOp& op = n->ops[ph.op];
+    if (!PWG_CNET_XT_NC2 || !ph.xtile || op.kind != PWG_CNET_CONV || ph.xt_cb != 1 || ph.stack_b >= 0 ||
+        ph.xpair_b >= 0 || (i > 0 && n->phases[i - 1].xpair_b == (int)i) || !xtile_supported(op.src[0].taps))
+      continue;
+    const int ext = (op.src[0].taps - 1) * op.src[0].dilation;
+    const int lds2 = op.src[0].taps * ph.MT * 2048 + (2 * XT_COLS + ext) * XT_ROWB;
+    if (lds2 > PWG_CNET_XTILE_LDS) continue;
+    if (PWG_CNET_XT_NC2 == 1 && 2 * ph.xt_lds <= 160 * 1024) continue;  // two workgroups per CU today
+    ph.xt_nc = 2;
+    ph.xt_lds = lds2;
+  }
   *out = n;  // device tables are uploaded by the first plan: packing needs no GPU
   return PWG_OK;
 }
@@ -2918,8 +2984,8 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
     p->d_strips.push_back(dstr);
     p->n_strips.push_back((int)strips.size());
     std::vector<int2> xblocks;
-    if (ph.xpair_b >= 0 || (ph.stack_b >= 0 && ph.xtile)) {
-      const int step = ph.xpair_b >= 0 ? XP_OUT : XT_COLS;
+    if (ph.xpair_b >= 0 || (ph.stack_b >= 0 && ph.xtile) || ph.xt_nc == 2) {
+      const int step = ph.xpair_b >= 0 ? XP_OUT : ph.xt_nc * XT_COLS;
       for (int u = 0; u < n_utts; ++u)
         for (int q0 = 0; q0 < ncols[u]; q0 += step) xblocks.push_back(make_int2(u, q0));
     }
@@ -3153,16 +3219,17 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         const bool convt = op.kind == PWG_CNET_CONVT;
         xt.K = convt ? 2 : op.src[0].taps; xt.dil = convt ? 1 : op.src[0].dilation;
         xt.off_min = convt ? ph.off_a - 1 : -op.src[0].pad;
-        xt.cs = op.src[0].channels / 16; xt.span = XT_COLS + (xt.K - 1) * xt.dil;
+        xt.cs = op.src[0].channels / 16; xt.span = ph.xt_nc * XT_COLS + (xt.K - 1) * xt.dil;
         xt.rev = convt ? 1 : 0;
         for (int r = 0; r < 8; ++r)
           xt.z_off[r] = convt && r < ph.z_phases ? n->phases[pi + r].off_a - 1 : xt.off_min;
         dim3 xgrid = grid;
-        if (ph.stack_b >= 0) {  // stack op A: 128-column d_blocks belong to the tap-major stack kernel
+        // stack op A: 128-column d_blocks belong to the tap-major stack kernel; xt_nc 2: 512-column blocks
+        if (ph.stack_b >= 0 || ph.xt_nc == 2) {
           a.blocks = p->d_xblocks[pi];
           xgrid.x = (unsigned)p->n_xblocks[pi];
         }
-        const hipError_t ea2 = xtile_launch(ph.MT, xt.K, ph.xt_cb, xgrid, ph.xt_lds, s, a, xt);
+        const hipError_t ea2 = xtile_launch(ph.MT, xt.K, ph.xt_cb, ph.xt_nc, xgrid, ph.xt_lds, s, a, xt);
         if (ea2 != hipSuccess) return hipf(ea2, "xtile kernel launch");
       } else if (split) {
         switch (ph.MT) {

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--nofuse", action="store_true")
     ap.add_argument("--pair-steps", type=int, default=None)
+    ap.add_argument("--dump", default=None, help="save the first forward's output (.npy) for a bitwise A/B")
     a = ap.parse_args()
     cls, p = configs.vocoder_params(a.config)
     m = {"MelGANGenerator": MelGANGenerator, "HiFiGANGenerator": HiFiGANGenerator}[cls](**p)
@@ -37,10 +38,13 @@ def main():
     lengths = synthetic.libritts_lengths(a.utts, seed=3)
     frames = int(lengths.sum())
     plan = eng.plan(lengths.tolist())
+    torch.manual_seed(0)
     mel = torch.randn(frames * 80, device=dev)
     out = torch.empty(plan.out_rows * eng.out_channels, device=dev)
     eng.run(plan, mel, out)
     torch.cuda.synchronize()
+    if a.dump:
+        np.save(a.dump, out.cpu().numpy())
     eng.set_timing(True)
     eng.collect_timing()
     for _ in range(a.steps):
