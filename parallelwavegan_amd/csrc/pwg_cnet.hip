@@ -657,57 +657,57 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
   const bool quad = (a.ld_dst & 3) == 0;
 #pragma unroll
   for (int nc = 0; nc < NC; ++nc) {
-  const int qb = q0 + nc * XT_COLS + wave * 32 + cl;
-  if (qb >= nq) break;
-  const int t = qb * a.ostride + ophase_;
-  float* yrow = a.y + (size_t)(sd.x + t) * a.ld_dst;
-  const float* rrow = a.res ? a.res + (size_t)(sr.x + t) * a.ld_res : nullptr;
+    const int qb = q0 + nc * XT_COLS + wave * 32 + cl;
+    if (qb >= nq) break;
+    const int t = qb * a.ostride + ophase_;
+    float* yrow = a.y + (size_t)(sd.x + t) * a.ld_dst;
+    const float* rrow = a.res ? a.res + (size_t)(sr.x + t) * a.ld_res : nullptr;
 #pragma unroll
-  for (int m = 0; m < MT; ++m)
+    for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int j4 = 0; j4 < 4; ++j4) {
-      const int row = 32 * (m0 + m) + 8 * j4 + 4 * hh;
-      if (row >= a.M) {
-        if (quad && row < a.ld_dst) *reinterpret_cast<f32x4v*>(yrow + row) = f32x4v{0.f, 0.f, 0.f, 0.f};
-        continue;
-      }
-      const f32x4v b = *reinterpret_cast<const f32x4v*>(bias_ + row);
-      f32x4v v;
+      for (int j4 = 0; j4 < 4; ++j4) {
+        const int row = 32 * (m0 + m) + 8 * j4 + 4 * hh;
+        if (row >= a.M) {
+          if (quad && row < a.ld_dst) *reinterpret_cast<f32x4v*>(yrow + row) = f32x4v{0.f, 0.f, 0.f, 0.f};
+          continue;
+        }
+        const f32x4v b = *reinterpret_cast<const f32x4v*>(bias_ + row);
+        f32x4v v;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = acc[nc][m][4 * j4 + i] + b[i];
-      if (quad) {
-        if (rrow) v += *reinterpret_cast<const f32x4v*>(rrow + row);
-        if (a.accumulate) v = *reinterpret_cast<const f32x4v*>(yrow + row) + v;
-      } else {
+        for (int i = 0; i < 4; ++i) v[i] = acc[nc][m][4 * j4 + i] + b[i];
+        if (quad) {
+          if (rrow) v += *reinterpret_cast<const f32x4v*>(rrow + row);
+          if (a.accumulate) v = *reinterpret_cast<const f32x4v*>(yrow + row) + v;
+        } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          if (row + i >= a.M) continue;
-          if (rrow) v[i] += rrow[row + i];
-          if (a.accumulate) v[i] = yrow[row + i] + v[i];
+          for (int i = 0; i < 4; ++i) {
+            if (row + i >= a.M) continue;
+            if (rrow) v[i] += rrow[row + i];
+            if (a.accumulate) v[i] = yrow[row + i] + v[i];
+          }
+        }
+        if (a.out_div != 1.f) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = v[i] / a.out_div;
+        }
+        if (a.post_act == PWG_ACT_LRELU) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = v[i] > 0.f ? v[i] : v[i] * a.post_slope;
+        } else if (a.post_act == PWG_ACT_TANH) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = tanhf(v[i]);
+        }
+        if (quad) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (row + i >= a.M) v[i] = 0.f;
+          *reinterpret_cast<f32x4v*>(yrow + row) = v;
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (row + i < a.M) yrow[row + i] = v[i];
         }
       }
-      if (a.out_div != 1.f) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = v[i] / a.out_div;
-      }
-      if (a.post_act == PWG_ACT_LRELU) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = v[i] > 0.f ? v[i] : v[i] * a.post_slope;
-      } else if (a.post_act == PWG_ACT_TANH) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = tanhf(v[i]);
-      }
-      if (quad) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (row + i >= a.M) v[i] = 0.f;
-        *reinterpret_cast<f32x4v*>(yrow + row) = v;
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (row + i < a.M) yrow[row + i] = v[i];
-      }
-    }
   }
 }
 
