@@ -105,6 +105,10 @@ constexpr int CN_G = PWG_CNET_G;   // 16-channel chunks staged per barrier
                            // workgroups per CU do not drop, 2 wherever it fits LDS (A/B: bit-identical,
                            // not faster: HiFiGAN v1 58.6 ms off, 61.8 ms with 1 or 2, profiles/r02_nc)
 #endif
+#ifndef PWG_CNET_XT_SYNC
+#define PWG_CNET_XT_SYNC 1  // unfused x-tile convs that would run one workgroup per CU (register prefetch
+                            // over 128 VGPRs) but fit two in LDS: synchronous staging, 128 VGPRs (A/B)
+#endif
 #ifndef PWG_CNET_XT_MT2_MAXK
 #define PWG_CNET_XT_MT2_MAXK 7  // >= 256-row convs with <= this many taps: 2 m-tiles per workgroup (0: off; A/B)
 #endif
@@ -500,14 +504,19 @@ constexpr int XT_ROWB = 80;  // bytes per staged input row: 16 hi + 16 lo halves
 
 // small shapes (MT 1, K <= 3, one block per step: ConvTranspose phases, 32-channel convs):
 // occupancy is set by VGPRs, PWG_CNET_XT_WPE waves per SIMD requested (0: compiler's choice)
-template <int MT, int K, int CB>
-constexpr int xt_wpe() { return (PWG_CNET_XT_WPE > 0 && MT == 1 && K <= 3 && CB == 1) ? PWG_CNET_XT_WPE : 1; }
+// SY (synchronous staging): no register prefetch of the next channel block; the kernel is held to
+// 128 VGPRs (4 waves per SIMD) so two workgroups share a CU and one's staging overlaps the other's
+// MFMAs (PWG_CNET_XT_SYNC). Same arithmetic and order: bit-identical.
+template <int MT, int K, int CB, bool SY = false>
+constexpr int xt_wpe() {
+  return SY ? 4 : (PWG_CNET_XT_WPE > 0 && MT == 1 && K <= 3 && CB == 1) ? PWG_CNET_XT_WPE : 1;
+}
 // NC column tiles of 256 per workgroup (wave w: columns 256 nc + 32 w + [0, 32)): the staged A
 // fragments of a channel block serve NC x 256 columns, so NC = 2 halves the L2 -> LDS weight bytes
 // per column (PWG_CNET_XT_NC2). Every accumulator sums the same products in the same order as
 // with NC = 1: bit-identical.
-template <int MT, int K, int CB, int NC = 1>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(xt_wpe<MT, K, CB>())))
+template <int MT, int K, int CB, int NC = 1, bool SY = false>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(xt_wpe<MT, K, CB, SY>())))
 pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
   constexpr int NTH = 512;
   constexpr int AV = CB * K * MT * 128;                // A vectors (16 B) per group of CB channel blocks
@@ -599,6 +608,48 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
     }
   };
 
+  // SY: each vector goes global -> LDS on its own (the compiler batches them within 128 VGPRs)
+  auto stage_sync = [&](int grp) {
+#pragma unroll
+    for (int i = 0; i < AQ; ++i) {
+      const int idx = threadIdx.x + NTH * i;
+      if (idx >= AV) continue;
+      const int c = idx / (K * MT * 128), rem1 = idx - c * (K * MT * 128);
+      const int tap = rem1 / (MT * 128), rem = rem1 - tap * (MT * 128);
+      const int wt = xt.rev ? K - 1 - tap : tap;
+      s_a[idx] = reinterpret_cast<const f32x4v*>(wfrag_ + ((size_t)(wt * xt.cs + CB * grp + c) * a.mt_total + m0) * 512)[rem];
+    }
+#pragma unroll
+    for (int i = 0; i < XQ_MAX; ++i) {
+      const int idx = threadIdx.x + NTH * i;
+      if (idx >= xv) continue;
+      const int c = idx / (xt.span * 4);
+      const int r = (idx >> 2) - c * xt.span, qd = idx & 3;
+      int p = q0 + off_min + r;
+      const bool ok = edge_row(p, sg.y, sx.pad_mode);
+      f32x4v v = *reinterpret_cast<const f32x4v*>(sx.x + (size_t)(sg.x + p) * sx.ld + 16 * (CB * grp + c) + 4 * qd);
+      const int ch = 16 * (CB * grp + c) + 4 * qd;
+      if (sx.normalize) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (v[e] - a.mean[ch + e]) / a.scale[ch + e];
+      }
+      if (sx.slope != 1.f) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * sx.slope;
+      }
+      if (!ok) v = f32x4v{0.f, 0.f, 0.f, 0.f};
+      _Float16 hv[4], lv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        hv[e] = (_Float16)v[e];
+        lv[e] = (_Float16)(v[e] - (float)hv[e]);
+      }
+      unsigned char* row = s_x + ((size_t)c * xt.span + r) * XT_ROWB;
+      *reinterpret_cast<f16x4v*>(row + 8 * qd) = f16x4v{hv[0], hv[1], hv[2], hv[3]};
+      *reinterpret_cast<f16x4v*>(row + 32 + 8 * qd) = f16x4v{lv[0], lv[1], lv[2], lv[3]};
+    }
+  };
+
   f32x16 acc[NC][MT];
 #pragma unroll
   for (int nc = 0; nc < NC; ++nc)
@@ -608,12 +659,16 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
       for (int r = 0; r < 16; ++r) acc[nc][m][r] = 0.f;
 
   const int ngrp = xt.cs / CB;
-  load(0);
-  store(0);
+  if constexpr (SY) {
+    stage_sync(0);
+  } else {
+    load(0);
+    store(0);
+  }
   __syncthreads();
   for (int grp = 0; grp < ngrp; ++grp) {
     const bool more = grp + 1 < ngrp;
-    if (more) load(grp + 1);
+    if (!SY && more) load(grp + 1);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int c = 0; c < CB; ++c)
@@ -647,7 +702,11 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
     __builtin_amdgcn_sched_barrier(0);
     if (!more) break;
     __syncthreads();
-    store(grp + 1);
+    if constexpr (SY) {
+      stage_sync(grp + 1);
+    } else {
+      store(grp + 1);
+    }
     __syncthreads();
   }
 
@@ -711,13 +770,23 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
   }
 }
 
-template <int MT, int K, int CB, int NC = 1>
+template <int MT, int K, int CB, int NC = 1, bool SY = false>
 hipError_t xtile_launch_k(dim3 grid, int lds, hipStream_t s, const CnConvArgs& a, const CnXtileArgs& xt) {
-  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(pwg_cnet_xtile_kernel<MT, K, CB, NC>),
+  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(pwg_cnet_xtile_kernel<MT, K, CB, NC, SY>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((pwg_cnet_xtile_kernel<MT, K, CB, NC>), grid, dim3(512), (size_t)lds, s, a, xt);
+  hipLaunchKernelGGL((pwg_cnet_xtile_kernel<MT, K, CB, NC, SY>), grid, dim3(512), (size_t)lds, s, a, xt);
   return hipGetLastError();
+}
+template <int MT>
+hipError_t xtile_launch_sync(int k, dim3 grid, int lds, hipStream_t s, const CnConvArgs& a, const CnXtileArgs& xt) {
+  switch (k) {
+    case 3: return xtile_launch_k<MT, 3, 1, 1, true>(grid, lds, s, a, xt);
+    case 5: return xtile_launch_k<MT, 5, 1, 1, true>(grid, lds, s, a, xt);
+    case 7: return xtile_launch_k<MT, 7, 1, 1, true>(grid, lds, s, a, xt);
+    case 11: return xtile_launch_k<MT, 11, 1, 1, true>(grid, lds, s, a, xt);
+    default: return hipErrorInvalidValue;
+  }
 }
 template <int MT>
 hipError_t xtile_launch_nc2(int k, dim3 grid, int lds, hipStream_t s, const CnConvArgs& a, const CnXtileArgs& xt) {
@@ -740,8 +809,20 @@ hipError_t xtile_launch_mt(int k, dim3 grid, int lds, hipStream_t s, const CnCon
     default: return hipErrorInvalidValue;
   }
 }
-hipError_t xtile_launch(int mt, int k, int cb, int nc, dim3 grid, int lds, hipStream_t s, const CnConvArgs& a,
-                        const CnXtileArgs& xt) {
+hipError_t xtile_launch(int mt, int k, int cb, int nc, bool sync, dim3 grid, int lds, hipStream_t s,
+                        const CnConvArgs& a, const CnXtileArgs& xt) {
+  if (sync) {
+    if constexpr (PWG_CNET_XT_SYNC != 0) {  // instantiated only when the option is built in
+      if (cb != 1 || nc != 1) return hipErrorInvalidValue;
+      switch (mt) {
+        case 2: return xtile_launch_sync<2>(k, grid, lds, s, a, xt);
+        case 3: return xtile_launch_sync<3>(k, grid, lds, s, a, xt);
+        case 4: return xtile_launch_sync<4>(k, grid, lds, s, a, xt);
+        default: return hipErrorInvalidValue;
+      }
+    }
+    return hipErrorInvalidValue;
+  }
   if (nc == 2) {
     if constexpr (PWG_CNET_XT_NC2 != 0) {  // instantiated only in A/B builds
       if (cb != 1) return hipErrorInvalidValue;
@@ -2295,6 +2376,7 @@ struct OpPhase {          // one launch
   int xt_lds = 0;
   int xt_cb = 1;          // its 16-channel blocks per staging step
   int xt_nc = 1;          // its 256-column tiles per workgroup (2: 512-column blocks in d_xblocks)
+  bool xt_sync = false;   // synchronous staging at 128 VGPRs (two workgroups per CU)
   int z_phases = 1;       // CONVT phase 0: phases launched together (gridDim.z); others: 0 (merged)
   int xpair_b = -1;       // x-tile conv pair: phase index of conv 2 (pwg_cnet_xpair_kernel)
   int xpair_lds = 0;
@@ -2786,6 +2868,18 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
     ph.xt_nc = 2;
     ph.xt_lds = lds2;
   }
+  // unfused x-tile convs whose prefetching kernel needs > 128 VGPRs (MT >= 3, or MT 2 at k = 11:
+  // one workgroup per CU) but whose LDS fits two workgroups per CU: synchronous staging
+  for (size_t i = 0; i < n->phases.size(); ++i) {
+    OpPhase& ph = n->phases[i];
+    const PwgCnetOp& op = n->ops[ph.op];
+    if (!PWG_CNET_XT_SYNC || !ph.xtile || op.kind != PWG_CNET_CONV || ph.xt_cb != 1 || ph.xt_nc != 1 ||
+        ph.stack_b >= 0 || ph.xpair_b >= 0 || (i > 0 && n->phases[i - 1].xpair_b == (int)i) ||
+        !xtile_supported(op.src[0].taps))
+      continue;
+    if (!(ph.MT >= 3 || (ph.MT == 2 && op.src[0].taps >= 11)) || 2 * ph.xt_lds > 160 * 1024) continue;
+    ph.xt_sync = true;
+  }
   *out = n;  // device tables are uploaded by the first plan: packing needs no GPU
   return PWG_OK;
 }
@@ -3229,7 +3323,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
           a.blocks = p->d_xblocks[pi];
           xgrid.x = (unsigned)p->n_xblocks[pi];
         }
-        const hipError_t ea2 = xtile_launch(ph.MT, xt.K, ph.xt_cb, ph.xt_nc, xgrid, ph.xt_lds, s, a, xt);
+        const hipError_t ea2 = xtile_launch(ph.MT, xt.K, ph.xt_cb, ph.xt_nc, ph.xt_sync, xgrid, ph.xt_lds, s, a, xt);
         if (ea2 != hipSuccess) return hipf(ea2, "xtile kernel launch");
       } else if (split) {
         switch (ph.MT) {
