@@ -109,6 +109,10 @@ constexpr int CN_G = PWG_CNET_G;   // 16-channel chunks staged per barrier
 #define PWG_CNET_XT_SYNC 1  // unfused x-tile convs that would run one workgroup per CU (register prefetch
                             // over 128 VGPRs) but fit two in LDS: synchronous staging, 128 VGPRs (A/B)
 #endif
+#ifndef PWG_CNET_XT_TSPLIT
+#define PWG_CNET_XT_TSPLIT 1  // synchronous staging of k = 11, 4-m-tile convs in two tap steps (6 + 5 taps):
+                              // A region 48 KB, two workgroups per CU (A/B)
+#endif
 #ifndef PWG_CNET_XT_MT2_MAXK
 #define PWG_CNET_XT_MT2_MAXK 7  // >= 256-row convs with <= this many taps: 2 m-tiles per workgroup (0: off; A/B)
 #endif
@@ -515,15 +519,18 @@ constexpr int xt_wpe() {
 // fragments of a channel block serve NC x 256 columns, so NC = 2 halves the L2 -> LDS weight bytes
 // per column (PWG_CNET_XT_NC2). Every accumulator sums the same products in the same order as
 // with NC = 1: bit-identical.
-template <int MT, int K, int CB, int NC = 1, bool SY = false>
+// KS (SY only): taps whose A fragments are staged per step; KS < K stages a channel block's taps in
+// ceil(K / KS) steps (same MFMA order) so the A region fits two workgroups per CU (k = 11, MT 4).
+template <int MT, int K, int CB, int NC = 1, bool SY = false, int KS = K>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(xt_wpe<MT, K, CB, SY>())))
 pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
+  static_assert(KS == K || SY, "tap-split staging is a synchronous-staging variant");
   constexpr int NTH = 512;
   constexpr int AV = CB * K * MT * 128;                // A vectors (16 B) per group of CB channel blocks
   constexpr int AQ = (AV + NTH - 1) / NTH;
   extern __shared__ __attribute__((aligned(16))) unsigned char xt_smem[];
   f32x4v* s_a = reinterpret_cast<f32x4v*>(xt_smem);                          // [CB][K][MT][2][64] x 16 B
-  unsigned char* s_x = xt_smem + (size_t)CB * K * MT * 2048;                  // [CB][span][XT_ROWB]
+  unsigned char* s_x = xt_smem + (size_t)CB * KS * MT * 2048;                 // [CB][span][XT_ROWB]
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int hh = lane >> 5;
@@ -609,16 +616,19 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
   };
 
   // SY: each vector goes global -> LDS on its own (the compiler batches them within 128 VGPRs)
-  auto stage_sync = [&](int grp) {
+  constexpr int AVS = CB * KS * MT * 128, AQS = (AVS + NTH - 1) / NTH;
+  auto stage_sync = [&](int grp, int th) {  // A fragments of taps [th KS, th KS + KS); x rows at th 0
 #pragma unroll
-    for (int i = 0; i < AQ; ++i) {
+    for (int i = 0; i < AQS; ++i) {
       const int idx = threadIdx.x + NTH * i;
-      if (idx >= AV) continue;
-      const int c = idx / (K * MT * 128), rem1 = idx - c * (K * MT * 128);
-      const int tap = rem1 / (MT * 128), rem = rem1 - tap * (MT * 128);
+      if (idx >= AVS) continue;
+      const int c = idx / (KS * MT * 128), rem1 = idx - c * (KS * MT * 128);
+      const int tap = th * KS + rem1 / (MT * 128), rem = rem1 - (rem1 / (MT * 128)) * (MT * 128);
+      if (tap >= K) continue;
       const int wt = xt.rev ? K - 1 - tap : tap;
       s_a[idx] = reinterpret_cast<const f32x4v*>(wfrag_ + ((size_t)(wt * xt.cs + CB * grp + c) * a.mt_total + m0) * 512)[rem];
     }
+    if (th != 0) return;
 #pragma unroll
     for (int i = 0; i < XQ_MAX; ++i) {
       const int idx = threadIdx.x + NTH * i;
@@ -659,22 +669,14 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
       for (int r = 0; r < 16; ++r) acc[nc][m][r] = 0.f;
 
   const int ngrp = xt.cs / CB;
-  if constexpr (SY) {
-    stage_sync(0);
-  } else {
-    load(0);
-    store(0);
-  }
-  __syncthreads();
-  for (int grp = 0; grp < ngrp; ++grp) {
-    const bool more = grp + 1 < ngrp;
-    if (!SY && more) load(grp + 1);
-    __builtin_amdgcn_sched_barrier(0);
+  // taps [T0, T1) of the staged channel blocks (A fragments of tap t at slot t - T0)
+  auto mma_taps = [&](auto t0c, auto t1c) {
+    constexpr int T0 = decltype(t0c)::value, T1 = decltype(t1c)::value;
 #pragma unroll
     for (int c = 0; c < CB; ++c)
 #pragma unroll
-      for (int tap = 0; tap < K; ++tap) {
-        const u32x4v* sa = reinterpret_cast<const u32x4v*>(s_a) + (size_t)(c * K + tap) * MT * 128 + lane;
+      for (int tap = T0; tap < T1; ++tap) {
+        const u32x4v* sa = reinterpret_cast<const u32x4v*>(s_a) + (size_t)(c * KS + tap - T0) * MT * 128 + lane;
         u32x4v bh[NC], bl[NC];
 #pragma unroll
         for (int nc = 0; nc < NC; ++nc) {
@@ -699,15 +701,40 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
           }
         }
       }
-    __builtin_amdgcn_sched_barrier(0);
-    if (!more) break;
+  };
+  if constexpr (SY) {
+    constexpr int NH = (K + KS - 1) / KS;
+    stage_sync(0, 0);
     __syncthreads();
-    if constexpr (SY) {
-      stage_sync(grp + 1);
-    } else {
-      store(grp + 1);
+    for (int grp = 0; grp < ngrp; ++grp) {
+      const bool more = grp + 1 < ngrp;
+      mma_taps(std::integral_constant<int, 0>{}, std::integral_constant<int, KS < K ? KS : K>{});
+      if constexpr (NH > 1) {
+        __syncthreads();
+        stage_sync(grp, 1);
+        __syncthreads();
+        mma_taps(std::integral_constant<int, KS>{}, std::integral_constant<int, K>{});
+      }
+      if (!more) break;
+      __syncthreads();
+      stage_sync(grp + 1, 0);
+      __syncthreads();
     }
+  } else {
+    load(0);
+    store(0);
     __syncthreads();
+    for (int grp = 0; grp < ngrp; ++grp) {
+      const bool more = grp + 1 < ngrp;
+      if (more) load(grp + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      mma_taps(std::integral_constant<int, 0>{}, std::integral_constant<int, K>{});
+      __builtin_amdgcn_sched_barrier(0);
+      if (!more) break;
+      __syncthreads();
+      store(grp + 1);
+      __syncthreads();
+    }
   }
 
   // epilogue (pwg_cnet_conv_kernel's)
@@ -770,16 +797,22 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
   }
 }
 
-template <int MT, int K, int CB, int NC = 1, bool SY = false>
+template <int MT, int K, int CB, int NC = 1, bool SY = false, int KS = K>
 hipError_t xtile_launch_k(dim3 grid, int lds, hipStream_t s, const CnConvArgs& a, const CnXtileArgs& xt) {
-  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(pwg_cnet_xtile_kernel<MT, K, CB, NC, SY>),
+  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(pwg_cnet_xtile_kernel<MT, K, CB, NC, SY, KS>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((pwg_cnet_xtile_kernel<MT, K, CB, NC, SY>), grid, dim3(512), (size_t)lds, s, a, xt);
+  hipLaunchKernelGGL((pwg_cnet_xtile_kernel<MT, K, CB, NC, SY, KS>), grid, dim3(512), (size_t)lds, s, a, xt);
   return hipGetLastError();
 }
 template <int MT>
-hipError_t xtile_launch_sync(int k, dim3 grid, int lds, hipStream_t s, const CnConvArgs& a, const CnXtileArgs& xt) {
+hipError_t xtile_launch_sync(int k, int ks, dim3 grid, int lds, hipStream_t s, const CnConvArgs& a,
+                             const CnXtileArgs& xt) {
+  if (ks != k) {  // tap-split staging: k = 11 in steps of 6 taps
+    if constexpr (PWG_CNET_XT_TSPLIT != 0 && MT == 4)
+      if (k == 11 && ks == 6) return xtile_launch_k<MT, 11, 1, 1, true, 6>(grid, lds, s, a, xt);
+    return hipErrorInvalidValue;
+  }
   switch (k) {
     case 3: return xtile_launch_k<MT, 3, 1, 1, true>(grid, lds, s, a, xt);
     case 5: return xtile_launch_k<MT, 5, 1, 1, true>(grid, lds, s, a, xt);
@@ -809,15 +842,15 @@ hipError_t xtile_launch_mt(int k, dim3 grid, int lds, hipStream_t s, const CnCon
     default: return hipErrorInvalidValue;
   }
 }
-hipError_t xtile_launch(int mt, int k, int cb, int nc, bool sync, dim3 grid, int lds, hipStream_t s,
+hipError_t xtile_launch(int mt, int k, int cb, int nc, bool sync, int ks, dim3 grid, int lds, hipStream_t s,
                         const CnConvArgs& a, const CnXtileArgs& xt) {
   if (sync) {
     if constexpr (PWG_CNET_XT_SYNC != 0) {  // instantiated only when the option is built in
       if (cb != 1 || nc != 1) return hipErrorInvalidValue;
       switch (mt) {
-        case 2: return xtile_launch_sync<2>(k, grid, lds, s, a, xt);
-        case 3: return xtile_launch_sync<3>(k, grid, lds, s, a, xt);
-        case 4: return xtile_launch_sync<4>(k, grid, lds, s, a, xt);
+        case 2: return xtile_launch_sync<2>(k, ks, grid, lds, s, a, xt);
+        case 3: return xtile_launch_sync<3>(k, ks, grid, lds, s, a, xt);
+        case 4: return xtile_launch_sync<4>(k, ks, grid, lds, s, a, xt);
         default: return hipErrorInvalidValue;
       }
     }
@@ -2377,6 +2410,7 @@ struct OpPhase {          // one launch
   int xt_cb = 1;          // its 16-channel blocks per staging step
   int xt_nc = 1;          // its 256-column tiles per workgroup (2: 512-column blocks in d_xblocks)
   bool xt_sync = false;   // synchronous staging at 128 VGPRs (two workgroups per CU)
+  int xt_ks = 0;          // with xt_sync: taps staged per step (the kernel size unless split)
   int z_phases = 1;       // CONVT phase 0: phases launched together (gridDim.z); others: 0 (merged)
   int xpair_b = -1;       // x-tile conv pair: phase index of conv 2 (pwg_cnet_xpair_kernel)
   int xpair_lds = 0;
@@ -2877,8 +2911,17 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
         ph.stack_b >= 0 || ph.xpair_b >= 0 || (i > 0 && n->phases[i - 1].xpair_b == (int)i) ||
         !xtile_supported(op.src[0].taps))
       continue;
-    if (!(ph.MT >= 3 || (ph.MT == 2 && op.src[0].taps >= 11)) || 2 * ph.xt_lds > 160 * 1024) continue;
-    ph.xt_sync = true;
+    if (!(ph.MT >= 3 || (ph.MT == 2 && op.src[0].taps >= 11))) continue;
+    const int K = op.src[0].taps;
+    const int span = XT_COLS + (K - 1) * op.src[0].dilation;
+    if (2 * ph.xt_lds <= 160 * 1024) {
+      ph.xt_sync = true;
+      ph.xt_ks = K;
+    } else if (PWG_CNET_XT_TSPLIT && ph.MT == 4 && K == 11 && 2 * (6 * 4 * 2048 + span * XT_ROWB) <= 160 * 1024) {
+      ph.xt_sync = true;
+      ph.xt_ks = 6;
+      ph.xt_lds = 6 * 4 * 2048 + span * XT_ROWB;
+    }
   }
   *out = n;  // device tables are uploaded by the first plan: packing needs no GPU
   return PWG_OK;
@@ -3323,7 +3366,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
           a.blocks = p->d_xblocks[pi];
           xgrid.x = (unsigned)p->n_xblocks[pi];
         }
-        const hipError_t ea2 = xtile_launch(ph.MT, xt.K, ph.xt_cb, ph.xt_nc, ph.xt_sync, xgrid, ph.xt_lds, s, a, xt);
+        const hipError_t ea2 = xtile_launch(ph.MT, xt.K, ph.xt_cb, ph.xt_nc, ph.xt_sync, ph.xt_ks, xgrid, ph.xt_lds, s, a, xt);
         if (ea2 != hipSuccess) return hipf(ea2, "xtile kernel launch");
       } else if (split) {
         switch (ph.MT) {
