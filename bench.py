@@ -95,6 +95,41 @@ def model_flops_per_sample(params):
     return L * layer_flops_per_sample(params) + 2 * (conv_in + fir + head)
 
 
+def launch_command(n, argv, port):
+    """The torch.distributed.run command that starts N ranks of this script with the same
+    arguments (the form the driver itself uses for N > 1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` started as ONE process (no WORLD_SIZE in the environment): start the N
+    ranks as a child torch.distributed.run and return its exit code. The reference's multi-GPU
+    entry does the same from one command (parallel_wavegan/distributed/launch.py:117-171).
+
+    Called before this process makes any GPU call; the child is a subprocess, never an exec.
+    On the nccl backend (one process per GPU) fewer than N visible devices is an error, so a
+    scaling run can never record fewer GPUs than its label; PWG_BENCH_BACKEND=gloo rehearses N
+    ranks sharing the devices there are. Rank 0's JSON line reaches our stdout directly (the
+    child inherits it; the other ranks print nothing there)."""
+    import socket
+
+    backend = os.environ.get("PWG_BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()  # does not initialise the GPU on this image
+    if backend == "nccl" and ndev < n:
+        print(f"[bench] --gpus {n}: only {ndev} GPU(s) visible; one process per GPU needs {n}", file=sys.stderr)
+        return 2
+    if backend != "nccl" and ndev < 1:
+        print("[bench] no GPU visible", file=sys.stderr)
+        return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run(launch_command(n, argv, port), env=env)
+    return r.returncode
+
+
 def dist_setup(n_gpus):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
@@ -110,10 +145,23 @@ def dist_setup(n_gpus):
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+        if world != n_gpus:
+            print(f"[bench] WORLD_SIZE={world} but --gpus {n_gpus}: reporting {world} ranks", file=sys.stderr)
         return dist.get_rank(), world, dev
     if n_gpus != 1:
-        print(f"[bench] --gpus {n_gpus} without torch.distributed.run: running 1 process", file=sys.stderr)
+        raise RuntimeError(f"--gpus {n_gpus} reached single-process setup (launch_ranks should have run)")
     return 0, 1, torch.device("cuda", 0)
+
+
+def per_rank_seconds(local_s, world, dev):
+    """Every rank's timed-region wall seconds (all_gather; host tensor on gloo)."""
+    if world == 1:
+        return [local_s]
+    gloo = dist.get_backend() == "gloo"
+    t = torch.tensor([local_s], dtype=torch.float64, device="cpu" if gloo else dev)
+    ts = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(ts, t)
+    return [float(x.item()) for x in ts]
 
 
 def measure_layer_traffic(args):
@@ -358,13 +406,13 @@ def bench_vocoder(args, rank, world, dev):
     mel = torch.from_numpy(rs.standard_normal(int(lengths.sum()) * 80).astype(np.float32)).to(dev)
     out = torch.empty(plan.out_rows * eng.out_channels, dtype=torch.float32, device=dev)
     for _ in range(args.warmup):
-        eng.run(plan, mel, out)
+        eng.run(plan, mel, out, check=False)
     torch.cuda.synchronize(dev)
     # untimed pass with per-op timing on: its events return to the executor's pool, so the timed
     # steps record pooled events instead of creating ~2 per op on the host between launches
     eng.set_timing(True)
     for _ in range(args.steps):
-        eng.run(plan, mel, out)
+        eng.run(plan, mel, out, check=False)
     torch.cuda.synchronize(dev)
     eng.collect_timing()
     if world > 1:
@@ -372,13 +420,17 @@ def bench_vocoder(args, rank, world, dev):
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        eng.run(plan, mel, out)
+        eng.run(plan, mel, out, check=False)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
-    elapsed = max_over_ranks(time.perf_counter() - t0, dev)
+    local_elapsed = time.perf_counter() - t0
+    elapsed = max_over_ranks(local_elapsed, dev)
+    rank_seconds = per_rank_seconds(local_elapsed, world, dev)
     eng.set_timing(False)
     timing = eng.collect_timing()
+    if eng.split_f16:
+        eng.run_status(plan)  # split-f16 range flag of the last timed run (raises when set)
     if not torch.isfinite(out).all():
         raise RuntimeError("non-finite generator output")
     samples = int(lengths.sum()) * hop
@@ -418,7 +470,10 @@ def bench_vocoder(args, rank, world, dev):
         "metric": f"audio samples/sec/GPU ({fs / 1000:g} kHz {args.config}, 80-band mel)",
         "value": round(value, 1),
         "unit": "audio samples/s (whole job, all GPUs)",
-        "n_gpus": world,
+        "n_gpus": world if os.environ.get("PWG_BENCH_BACKEND", "nccl") == "nccl"
+                  else min(world, max(torch.cuda.device_count(), 1)),
+        "ranks": world,
+        "rank_seconds": [round(x, 4) for x in rank_seconds],
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -433,6 +488,7 @@ def bench_vocoder(args, rank, world, dev):
                    "parallelism": f"utterance-sharded x{world}",
                    "fused_conv_pairs": sum(1 for _, _, n in timing if n == 0)},
         "x_realtime_per_gpu": round(value / world / fs, 1),
+        "range_check": "ok (pwg_cnet_run_status after the timed steps)" if eng.split_f16 else "n/a (exact fp32)",
         "kernel_ms_per_step": round(kern_ms, 3),
         "top_ops_ms_per_step": {n: round(ms / args.steps, 3) for n, ms, _ in top},
         "roofline": ({"kernel": "all conv ops (fp32 MFMA implicit GEMM), whole program", "bound": "mfma",
@@ -563,6 +619,10 @@ def main():
 
     if args.pmc_child:
         return pmc_child(args)
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     # measured HBM traffic of the dominant kernel, before this process touches the GPU
     live_traffic = (None, "off")
     if (args.pmc == "auto" and int(os.environ.get("WORLD_SIZE", "1")) == 1 and args.config not in VOCODERS
@@ -776,17 +836,8 @@ def main():
             "executed_frac": mfma_insts and round(mfma_insts * 4096 / layer_avg_s / 1e12 / FP32_PEAK_TFLOPS, 4),
             "hbm_GBs": traffic and round(traffic / layer_avg_s / 1e9, 1),
         }
-    busy = {"local_s": local_elapsed}
-    if args.strong:
-        # per-rank compute time next to the max: load imbalance of the LPT partition
-        gloo = dist.is_initialized() and dist.get_backend() == "gloo"
-        t = torch.tensor([local_elapsed], dtype=torch.float64, device="cpu" if gloo else dev)
-        if world > 1:
-            ts = [torch.zeros_like(t) for _ in range(world)]
-            dist.all_gather(ts, t)
-            busy["per_rank_s"] = [float(x.item()) for x in ts]
-        else:
-            busy["per_rank_s"] = [local_elapsed]
+    # per-rank wall time of the timed steps next to the max (load imbalance of the partition)
+    rank_seconds = per_rank_seconds(local_elapsed, world, dev)
 
     if rank != 0:
         dist.destroy_process_group()
@@ -841,8 +892,9 @@ def main():
         "cpu_baseline": cpu,
         "latency": lat,
     }
+    res["rank_seconds"] = [round(x, 4) for x in rank_seconds]
     if args.strong:
-        per = busy["per_rank_s"]
+        per = rank_seconds
         res["strong"] = {"shard_frames": loads, "frame_imbalance": round(max(loads) / (sum(loads) / world), 4),
                          "rank_seconds": [round(x, 4) for x in per],
                          "time_imbalance": round(max(per) / (sum(per) / world), 4)}

@@ -98,6 +98,14 @@ PWG_API long long pwg_cnet_plan_workspace_bytes(const PwgCnetPlan* p);
  * mean/scale: device or NULL (ops with normalize=1 need them). */
 PWG_API int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const float* mean,
                  const float* scale, float* out, void* workspace, void* stream);
+/* Split-f16 range status of the last pwg_cnet_run on this workspace (synchronises `stream`):
+ * PWG_ERR_RANGE when the program output holds a non-finite value, i.e. some activation left the
+ * fp16 pair range upstream (it became (inf, -inf), every later product NaN) or the input was not
+ * finite. The caller reruns with PWG_CNET_OPT_SPLIT_F16 = 0 to get the reference's fp32 semantics
+ * (parallelwavegan_amd.cnet.CnetEngine.run(check=True) does). Exact-fp32 runs always return PWG_OK.
+ * pwg_cnet_pack_weights likewise returns PWG_ERR_RANGE when a weight cannot be carried as an fp16
+ * pair; the packed image is still complete for the exact-fp32 mode. */
+PWG_API int pwg_cnet_run_status(PwgCnetPlan* p, const void* workspace, void* stream);
 /* Options. PWG_CNET_OPT_SPLIT_F16 (default 1): fp32 operands as fp16 hi+lo pairs on the f16
  * MFMA (three products, fp32 accumulate; error class of fp32); 0: fp32 MFMA.
  * PWG_CNET_OPT_FUSE_PAIRS (default 1, split-f16 mode): run "conv A -> t -> conv B" pairs whose

@@ -9,6 +9,7 @@ runs in libpwg_hip.so, and a missing library or a CPU device raises.
 """
 
 import ctypes
+import logging
 from collections import OrderedDict
 
 import numpy as np
@@ -83,6 +84,7 @@ def lib():
         L.pwg_cnet_plan_workspace_bytes.argtypes = [vp]
         L.pwg_cnet_plan_workspace_bytes.restype = ll
         L.pwg_cnet_run.argtypes = [vp] * 8
+        L.pwg_cnet_run_status.argtypes = [vp, vp, vp]
         L.pwg_cnet_set_timing.argtypes = [vp, ctypes.c_int]
         L.pwg_cnet_set_option.argtypes = [vp, ctypes.c_int, ctypes.c_longlong]
         L.pwg_cnet_timing_collect.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ll)]
@@ -243,6 +245,9 @@ class CnetEngine:
         self.packed = None
         self._plans = OrderedDict()
         self._workspaces = {}
+        self.split_f16 = True       # PWG_CNET_OPT_SPLIT_F16 (the library default)
+        self.split_range_ok = True  # the loaded weights fit the fp16 pair range
+        self.range_reruns = 0       # runs redone in exact fp32 after a split-f16 range flag
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -252,13 +257,23 @@ class CnetEngine:
             self._h = None
 
     def pack(self, state, extra=None):
+        """Host-side packed image. Sets ``split_range_ok``: False when a weight cannot be carried
+        as an fp16 pair (pwg_cnet_pack_weights returned PWG_ERR_RANGE); the image is then complete
+        for the exact-fp32 mode only."""
         flat = self.program.flatten(state, extra)
         packed = np.empty(self.packed_weight_count, np.float32)
-        _lib.check(self._lib.pwg_cnet_pack_weights(self._h, flat.ctypes.data, packed.ctypes.data))
+        rc = self._lib.pwg_cnet_pack_weights(self._h, flat.ctypes.data, packed.ctypes.data)
+        self.split_range_ok = rc != _lib.PWG_ERR_RANGE
+        if rc != _lib.PWG_ERR_RANGE:
+            _lib.check(rc)
         return packed
 
     def load_state_dict(self, state, extra=None):
-        self.packed = torch.from_numpy(self.pack(state, extra)).to(self.device)
+        packed = self.pack(state, extra)
+        if not self.split_range_ok and self.split_f16:
+            logging.warning("vocoder weights exceed the fp16 pair range of the split-f16 mode: using exact fp32")
+            self._set_split(False)
+        self.packed = torch.from_numpy(packed).to(self.device)
         return self.packed
 
     def plan(self, frames):
@@ -299,7 +314,38 @@ class CnetEngine:
     def hop(self):
         return self.program.rate[-1]
 
-    def run(self, plan, mel, out, mean=None, scale=None, stream=None):
+    def run(self, plan, mel, out, mean=None, scale=None, stream=None, check=True):
+        """Enqueue one forward of ``plan`` on ``stream`` (default: torch's current stream).
+
+        check=True (the drop-ins' setting) reads the split-f16 range status after the forward
+        (pwg_cnet_run_status: one stream synchronisation) and, when the output came out non-finite,
+        redoes the forward in exact fp32, so the result always holds the reference's fp32
+        semantics. check=False only enqueues (the bench's timed loop; ``run_status`` afterwards)."""
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device)
+        self._enqueue(plan, mel, out, mean, scale, stream)
+        if check and self.split_f16:
+            try:
+                self.run_status(plan, stream)
+            except _lib.RangeError as e:
+                logging.warning("%s; rerunning in exact fp32", e)
+                self._set_split(False)
+                try:
+                    self._enqueue(plan, mel, out, mean, scale, stream)
+                finally:
+                    self._set_split(True)
+                self.range_reruns += 1
+        return out
+
+    def run_status(self, plan, stream=None):
+        """pwg_cnet_run_status of the last run on ``stream``'s workspace: raises _lib.RangeError
+        when the split-f16 range flag is set (synchronises the stream)."""
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device)
+        ws = self.workspace(plan.workspace_bytes, stream)
+        _lib.check(self._lib.pwg_cnet_run_status(plan._p, ws.data_ptr(), stream.cuda_stream))
+
+    def _enqueue(self, plan, mel, out, mean, scale, stream):
         if self.packed is None:
             raise RuntimeError("no weights loaded")
         for name, t in (("mel", mel), ("out", out)):
@@ -314,8 +360,6 @@ class CnetEngine:
             mean = mean.to(self.device, torch.float32).contiguous()
             scale = scale.to(self.device, torch.float32).contiguous()
             mp, sp = mean.data_ptr(), scale.data_ptr()
-        if stream is None:
-            stream = torch.cuda.current_stream(self.device)
         ws = self.workspace(plan.workspace_bytes, stream)
         _lib.check(self._lib.pwg_cnet_run(plan._p, self.packed.data_ptr(), mel.data_ptr(), mp, sp, out.data_ptr(),
                                           ws.data_ptr(), stream.cuda_stream))
@@ -339,10 +383,16 @@ class CnetEngine:
     def set_timing(self, enable):
         _lib.check(self._lib.pwg_cnet_set_timing(self._h, int(enable)))
 
+    def _set_split(self, enable):
+        _lib.check(self._lib.pwg_cnet_set_option(self._h, 0, int(bool(enable))))
+
     def set_split_f16(self, enable):
         """pwg_cnet_set_option(PWG_CNET_OPT_SPLIT_F16): fp16-pair operands on the f16 MFMA
-        (default) or exact fp32 MFMA."""
-        _lib.check(self._lib.pwg_cnet_set_option(self._h, 0, int(bool(enable))))
+        (default) or exact fp32 MFMA. Refused (RangeError) for weights beyond the pair range."""
+        if enable and not self.split_range_ok:
+            raise _lib.RangeError("the loaded weights exceed the fp16 pair range of the split-f16 mode")
+        self._set_split(enable)
+        self.split_f16 = bool(enable)
 
     def set_fuse_pairs(self, enable):
         """pwg_cnet_set_option(PWG_CNET_OPT_FUSE_PAIRS): run conv pairs whose intermediate has no

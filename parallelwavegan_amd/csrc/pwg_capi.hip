@@ -945,6 +945,7 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
   pa.split = split16 ? 2 : split ? 1 : 0;
   pa.split_scale_a = (float)SPLIT_GATE_SCALE_TANH;
   pa.split_scale_b = (float)SPLIT_GATE_SCALE_SIGM;
+  pa.range_flag = split ? range_flag : nullptr;
   e = timed(PWG_KERNEL_UPSAMPLE, [&] { return launch_aux_proj(pa, h->L, s); });
   if (e != hipSuccess) return hip_fail(e, "aux projection launch");
 
@@ -1125,7 +1126,8 @@ int pwg_run_status(PwgPlan* p, const void* workspace, void* stream) {
   if (e != hipSuccess) return hip_fail(e, "run status");
   if (flag != 0)
     return fail(PWG_ERR_RANGE,
-                "non-finite skip sum in the split-f16 layer kernel: a value left the fp16 pair range (or the "
+                "split-f16 range flag: a value left the fp16 pair range (an aux projection row, the "
+                "scaled final skip sum, or upstream x / first_conv values making a skip sum non-finite; or the "
                 "input is not finite); rerun with PWG_OPT_LAYER_KERNEL 0 (exact fp32)");
   return PWG_OK;
 }

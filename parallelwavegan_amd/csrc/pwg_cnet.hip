@@ -171,6 +171,8 @@ struct CnConvArgs {
   const ChunkDesc* z_chunks[8];
   const float* z_wfrag[8];
   const float* z_bias[8];
+  int* range_flag;        // thin kernel writing the program output (split-f16 mode): set to 1 on a
+                          // non-finite output value (pwg_cnet_run_status), else null
 };
 
 __device__ __forceinline__ int reflect_row(int p, int T) {
@@ -2329,6 +2331,7 @@ __global__ void __launch_bounds__(128) pwg_cnet_thin_kernel(const CnConvArgs a, 
     const int2 sr = *reinterpret_cast<const int2*>(a.seg_res + 2 * u);
     rrow = a.res + (size_t)(sr.x + t) * a.ld_res;
   }
+  bool bad = false;
 #pragma unroll
   for (int o = 0; o < M; ++o) {
     if (o >= a.M) break;
@@ -2338,9 +2341,13 @@ __global__ void __launch_bounds__(128) pwg_cnet_thin_kernel(const CnConvArgs a, 
     if (a.out_div != 1.f) v = v / a.out_div;
     if (a.post_act == PWG_ACT_LRELU) v = v > 0.f ? v : v * a.post_slope;
     else if (a.post_act == PWG_ACT_TANH) v = tanhf(v);
+    bad |= !__builtin_isfinite(v);
     yrow[o] = v;
   }
   for (int o = a.M; o < a.ld_dst; ++o) yrow[o] = 0.f;  // padding channels stay zero
+  // program output in split-f16 mode: a value beyond the fp16 pair range anywhere upstream became
+  // (inf, -inf), every later product NaN, and nothing on the way (LeakyReLU, tanh, sums) clears it
+  if (a.range_flag) flag_range(a.range_flag, bad, (int)(threadIdx.x & 63));
 }
 
 // PQMF synthesis (layers/pqmf.py:133-149): y[t] = sum_m sum_k h[m][k] * S * x[(t+k-P)/S][m] over
@@ -2355,6 +2362,7 @@ struct CnPqmfArgs {
   int ld_dst;
   const int2* blocks; // (utt, first output sample) per 256-sample block
   int S, NT;
+  int* range_flag;    // as CnConvArgs::range_flag
 };
 
 // One workgroup = 256 consecutive output samples of one utterance. The subband rows it needs
@@ -2389,6 +2397,16 @@ __global__ void __launch_bounds__(256) pwg_cnet_pqmf_kernel(const CnPqmfArgs a) 
     for (int m = 0; m < S; ++m) acc = fmaf(s_h[m * NT + k], s_x[rr * S + m], acc);
   }
   a.y[(size_t)(sd.x + t) * a.ld_dst] = acc;
+  if (a.range_flag) flag_range(a.range_flag, !__builtin_isfinite(acc), (int)(threadIdx.x & 63));
+}
+
+// Non-finite check of the program output when its last op is not a thin or PQMF launch (split-f16
+// range flag, pwg_cnet_run_status): rows x ld floats, grid-stride.
+__global__ void __launch_bounds__(256) pwg_cnet_finite_kernel(const float* y, long long n, int* flag) {
+  bool bad = false;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+    bad |= !__builtin_isfinite(y[i]);
+  flag_range(flag, bad, (int)(threadIdx.x & 63));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2459,6 +2477,7 @@ struct PwgCnetPlan {
   std::vector<long long> rows;               // per buffer
   std::vector<size_t> buf_off;               // workspace offsets (SIZE_MAX: external)
   size_t ws_bytes = 0;
+  size_t ws_flag = 0;                        // split-f16 range flag (one int) in the workspace
   int* d_seg = nullptr;                      // [n_bufs][n_utts][2]
   std::vector<int2*> d_blocks;               // per phase
   std::vector<int> n_blocks;
@@ -2942,6 +2961,7 @@ long long pwg_cnet_packed_weight_count(const PwgCnet* n) { return n ? n->packed_
 int pwg_cnet_pack_weights(const PwgCnet* n, const float* ref, float* packed) {
   if (!n || !ref || !packed) return fail(PWG_ERR_INVALID, "null argument");
   std::memset(packed, 0, sizeof(float) * n->packed_count);
+  long long overflow = 0;  // split-f16 weights whose pair would be (inf, -inf)
   for (const OpPhase& ph : n->phases) {
     const PwgCnetOp& op = n->ops[ph.op];
     if (op.kind == PWG_CNET_PQMF) {
@@ -2975,6 +2995,7 @@ int pwg_cnet_pack_weights(const PwgCnet* n, const float* ref, float* packed) {
               const int o = 32 * m + (l & 31);
               const int ch = cd.c0 + 8 * (l >> 5) + 2 * d + e2;
               const float w = ref_weight(op, ph, ref, cd.src, o, ch, tap);
+              overflow += !ph.thin && !(std::fabs(w) < 65520.f);  // the thin kernel reads fp32
               const uint16_t h = cn_f2h(w);
               const uint16_t lo = cn_f2h(w - cn_h2f(h));
               hv |= (uint32_t)h << (16 * e2);
@@ -2991,6 +3012,10 @@ int pwg_cnet_pack_weights(const PwgCnet* n, const float* ref, float* packed) {
       packed[ph.bias_off + o] = b;
     }
   }
+  if (overflow)
+    return fail(PWG_ERR_RANGE, std::to_string(overflow) +
+                                   " weight(s) beyond the fp16 pair range (|w| >= 65520 or not finite): the image "
+                                   "is complete for the exact-fp32 mode only (PWG_CNET_OPT_SPLIT_F16 0)");
   return PWG_OK;
 }
 
@@ -3062,7 +3087,8 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
     p->buf_off[b] = slots[pick].off;
     slots[pick].free_after = std::max(last_use[b], first_def[b]);
   }
-  p->ws_bytes = std::max<size_t>(o, 256);
+  p->ws_flag = o;  // after the buffer slots (256-byte aligned)
+  p->ws_bytes = o + 256;
   Guard g(n->device);
   if (!g.ok) { delete p; return fail(PWG_ERR_HIP, "hipSetDevice failed"); }
   hipError_t e = hipSuccess;
@@ -3176,6 +3202,13 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
   auto seg_of = [&](int b) -> const int* { return p->d_seg + (size_t)b * p->n_utts * 2; };
   const bool fuse = n->fuse_pairs && n->split_f16;
   const bool xt = n->xtile && n->split_f16;
+  // split-f16 range flag: zeroed per run, set by the launch that writes the program output
+  int* rflag = n->split_f16 ? (int*)((char*)workspace + p->ws_flag) : nullptr;
+  bool out_checked = false;
+  if (rflag) {
+    const hipError_t ez = hipMemsetAsync(rflag, 0, sizeof(int), s);
+    if (ez != hipSuccess) return hipf(ez, "range flag reset");
+  }
   // a conv pair runs fused unless its convs run on the x-tile kernel (measured faster unfused)
   auto pair_fused = [&](const OpPhase& q) { return fuse && q.pair_b >= 0 && !(xt && q.xtile); };
   for (size_t pi = 0; pi < n->phases.size(); ++pi) {
@@ -3292,9 +3325,12 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
       a.x = bufs[op.src[0].buf]; a.seg_src = seg_of(op.src[0].buf); a.ld_src = n->ld[op.src[0].buf];
       a.h = packed + ph.frag_off; a.y = bufs[op.dst]; a.seg_dst = seg_of(op.dst); a.ld_dst = n->ld[op.dst];
       a.blocks = p->d_blocks[pi]; a.S = op.stride; a.NT = op.padding;
+      a.range_flag = op.dst == nb - 1 ? rflag : nullptr;
+      out_checked |= op.dst == nb - 1;
       hipLaunchKernelGGL(pwg_cnet_pqmf_kernel, dim3((unsigned)p->n_blocks[pi]), dim3(256), 0, s, a);
     } else if (p->n_blocks[pi] > 0) {
       CnConvArgs a;
+      a.range_flag = nullptr;
       const int nsrc = (op.src[1].buf >= 0 && op.kind == PWG_CNET_CONV) ? 2 : 1;
       for (int si = 0; si < 2; ++si) {
         const PwgCnetSrc& src = op.src[si];
@@ -3329,6 +3365,8 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
       if (ph.thin) {
         const dim3 tgrid((unsigned)p->n_blocks[pi]), tblock(CN_COLS);
         const size_t tl = (size_t)std::max(ph.thin_span[0], ph.thin_span[1]) * THIN_ROW * sizeof(float);
+        a.range_flag = op.dst == nb - 1 ? rflag : nullptr;
+        out_checked |= op.dst == nb - 1;
         if (op.out_channels <= 1) hipLaunchKernelGGL(pwg_cnet_thin_kernel<1>, tgrid, tblock, tl, s, a, nsrc);
         else if (op.out_channels <= 4) hipLaunchKernelGGL(pwg_cnet_thin_kernel<4>, tgrid, tblock, tl, s, a, nsrc);
         else hipLaunchKernelGGL(pwg_cnet_thin_kernel<8>, tgrid, tblock, tl, s, a, nsrc);
@@ -3419,6 +3457,29 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
       n->records.push_back({ph.op, ea, eb});
     }
   }
+  if (rflag && !out_checked && p->rows[nb - 1] > 0) {
+    const long long cnt = p->rows[nb - 1] * n->ld[nb - 1];
+    const long long nblk = std::min<long long>((cnt + 255) / 256, 4096);
+    hipLaunchKernelGGL(pwg_cnet_finite_kernel, dim3((unsigned)nblk), dim3(256), 0, s, (const float*)out, cnt, rflag);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return hipf(e, "output range check launch");
+  }
+  return PWG_OK;
+}
+
+int pwg_cnet_run_status(PwgCnetPlan* p, const void* workspace, void* stream) {
+  if (!p || !workspace) return fail(PWG_ERR_INVALID, "null argument");
+  Guard g(p->n->device);
+  if (!g.ok) return fail(PWG_ERR_HIP, "hipSetDevice failed");
+  int flag = 0;
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = hipMemcpyAsync(&flag, (const char*)workspace + p->ws_flag, sizeof(int), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return hipf(e, "cnet run status");
+  if (flag != 0)
+    return fail(PWG_ERR_RANGE,
+                "non-finite program output in split-f16 mode: a value left the fp16 pair range upstream (or the "
+                "input is not finite); rerun with PWG_CNET_OPT_SPLIT_F16 0 (exact fp32)");
   return PWG_OK;
 }
 

@@ -71,6 +71,8 @@ struct AuxProjArgs {
                          // rows [0, GR/2) scaled by split_scale_a, the rest by split_scale_b;
                          // 2: the same in the split16 row order (row 16m + c at c * 8 + m)
   float split_scale_a, split_scale_b;
+  int* range_flag;       // split modes: set to 1 when a scaled D value leaves the fp16 pair range
+                         // (|v| >= 65520 or not finite; pwg_run_status)
 };
 // Pre-scaling of the split kernel's gate rows (pwg_split.hip gate()): tanh rows by -2 log2(e),
 // sigmoid rows by -log2(e).
@@ -249,6 +251,14 @@ __device__ __forceinline__ void stage_lds(V* dst, const V* src, int n, int tid, 
     for (int j = 0; j < 8; ++j) dst[i + j * nthr] = r[j];
   }
   for (; i < n; i += nthr) dst[i] = src[i];
+}
+
+// Split-f16 range flag: one vector atomic per wave (from its lowest flagging lane) when any active
+// lane saw a value the fp16 pair split cannot carry. Lanes that already exited simply do not vote.
+__device__ __forceinline__ void flag_range(int* flag, bool bad, int lane) {
+  const unsigned long long m = __ballot(bad ? 1 : 0);
+  if (bad && flag != nullptr && lane == __builtin_ctzll(m))
+    __hip_atomic_fetch_or(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace pwg

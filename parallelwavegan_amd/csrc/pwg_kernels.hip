@@ -215,6 +215,7 @@ __global__ void __launch_bounds__(256) pwg_aux_proj_kernel(const AuxProjArgs a) 
     // stride 129 dwords: conflict-free column writes), then stored as whole 512-byte frame rows.
     __shared__ unsigned s_d[4][32][129];
     typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+    bool bad = false;  // a value the pair split cannot carry (it would become inf / -inf)
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -224,10 +225,12 @@ __global__ void __launch_bounds__(256) pwg_aux_proj_kernel(const AuxProjArgs a) 
         for (int i = 0; i < 4; ++i) {
           const int r = 32 * m + 8 * j4 + 4 * hh + i;
           const float x = acc[m][4 * j4 + i] * sc;
+          bad |= !(__builtin_fabsf(x) < 65520.f);
           const _Float16 hi = (_Float16)x;
           s_d[wave][cl][(r & 15) * 8 + (r >> 4)] = __builtin_bit_cast(unsigned, f16x2{hi, (_Float16)(x - (float)hi)});
         }
       }
+    flag_range(a.range_flag, bad && f < a.F_total, lane);
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes done (wave-private rows)
     __builtin_amdgcn_wave_barrier();
     const long long f0 = (long long)blockIdx.x * 128 + wave * 32;
@@ -256,12 +259,16 @@ __global__ void __launch_bounds__(256) pwg_aux_proj_kernel(const AuxProjArgs a) 
         typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
         u32x4 u;
         const float sc = 32 * m + 8 * j4 < GR / 2 ? a.split_scale_a : a.split_scale_b;
+        bool bad = false;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float x = v[i] * sc;
+          bad |= !(__builtin_fabsf(x) < 65520.f);
           const _Float16 hi = (_Float16)x;
           u[i] = __builtin_bit_cast(unsigned, f16x2{hi, (_Float16)(x - (float)hi)});
         }
+        if (bad && a.range_flag)  // rare; lanes of exited waves never reach here (f < F_total)
+          __hip_atomic_fetch_or(a.range_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *reinterpret_cast<u32x4*>(d + 32 * m + 8 * j4 + 4 * hh) = u;
       } else {
         *reinterpret_cast<f32x4*>(d + 32 * m + 8 * j4 + 4 * hh) = v;

@@ -624,7 +624,7 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
       u32x4 sh[2][2], sl[2][2];  // [nt][ks]
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
-        float sum = 0.f;  // inf/NaN in any of the 16 propagates (a finite overflow only reruns exact)
+        float sum = 0.f;  // inf/NaN in any of the 16 propagates (ReLU's fmaxf below would hide NaN)
 #pragma unroll
         for (int ms = 0; ms < 4; ++ms)
 #pragma unroll
@@ -636,8 +636,14 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
           float hv[8];
+          float hmax = 0.f;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) hv[j] = fmaxf(acc2[2 * ks + (j >> 2)][nt][j & 3] * a.skip_scale, 0.f);
+          for (int j = 0; j < 8; ++j) {
+            hv[j] = fmaxf(acc2[2 * ks + (j >> 2)][nt][j & 3] * a.skip_scale, 0.f);
+            hmax = fmaxf(hmax, hv[j]);
+          }
+          // a finite skip sum whose scaled value the pair split cannot carry (hi = inf, lo = -inf)
+          nonfinite |= bd.t0 + 16 * nt + c < bd.T && hmax >= 65520.f;
           split8x<0>(hv, sh[nt][ks], sl[nt][ks]);
         }
 #pragma unroll

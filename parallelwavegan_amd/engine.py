@@ -132,33 +132,42 @@ torch.nn.modules.module.register_module_parameter_registration_hook(_on_paramete
 class WeightTracker:
     """Per-call "do the packed weights still match the module?" check for the drop-in modules.
 
-    The first version walked every parameter's (data_ptr, _version) per call (640 us for PWG v1's
-    221 parameters). This keeps the parameter list (re-collected only after a parameter
-    registration anywhere or an explicit ``invalidate()``, which the modules call from ``_apply``,
-    i.e. ``.to()``/``.cuda()``) and compares the list's ``_version`` counters, which every in-place
-    update bumps (load_state_dict's copy_, optimizer steps, ``add_`` under no_grad): ~22 us."""
+    The first version re-walked ``module.parameters()`` per call (640 us for PWG v1's 221
+    parameters). This keeps the parameter list (re-collected only after a parameter registration
+    anywhere or an explicit ``invalidate()``, which the modules call from ``_apply``, i.e.
+    ``.to()``/``.cuda()``) and compares each listed tensor's ``(data_ptr, _version)``:
+    - ``_version`` catches in-place updates through the parameter itself (load_state_dict's
+      ``copy_``, optimizer steps, ``add_`` under no_grad);
+    - ``data_ptr`` catches storage replacement, ``p.data = t``, which keeps ``_version``.
+    Not detectable without reading the values: an in-place write through the ``.data`` alias
+    (``p.data.copy_(t)``, ``p.data.mul_(s)``): ``.data`` is a new tensor with its own version
+    counter over the same storage. After such a write call ``invalidate_weights()`` on the module
+    (or re-load the state dict). ~25 us per check."""
 
     def __init__(self):
         self._key = None
         self._params = None
-        self._versions = None
+        self._sig = None
 
     def invalidate(self):
         self._key = None
+        self._sig = None
+
+    def _signature(self):
+        return [(p.data_ptr(), p._version) for p in self._params]
 
     def changed(self, module, extra=()):
         """extra: tensors outside module.parameters() the packed image also holds (a PQMF
-        filter buffer); compared by identity as well as version."""
+        filter buffer); compared by identity as well as storage and version."""
         key = (_PARAM_REGISTRATIONS[0], id(module), tuple(id(t) for t in extra))
         if key != self._key:
             self._params = list(module.parameters()) + list(extra)
             self._key = key
-            self._versions = None
-        versions = [p._version for p in self._params]
-        return versions != self._versions
+            self._sig = None
+        return self._signature() != self._sig
 
     def mark_packed(self):
-        self._versions = [p._version for p in self._params]
+        self._sig = self._signature()
 
 
 class HostHandle:

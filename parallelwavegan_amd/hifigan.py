@@ -237,6 +237,11 @@ class HiFiGANGenerator(torch.nn.Module):
             self._weights.invalidate()  # .to() / .cuda() replace parameter storage
         return super()._apply(fn, *args, **kwargs)
 
+    def invalidate_weights(self):
+        """Force a re-pack on the next call (after writes through ``p.data`` aliases, which the
+        WeightTracker cannot see)."""
+        self._weights.invalidate()
+
     def engine(self):
         dev = self._device()
         if self._engine is None or self._engine.device != dev:

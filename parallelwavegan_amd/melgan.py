@@ -334,6 +334,12 @@ class MelGANGenerator(torch.nn.Module):
             ent[1].invalidate()  # .to() / .cuda() replace parameter storage
         return super()._apply(fn, *args, **kwargs)
 
+    def invalidate_weights(self):
+        """Force a re-pack on the next call (after writes through ``p.data`` aliases, which the
+        WeightTracker cannot see)."""
+        for ent in self._engines.values():
+            ent[1].invalidate()
+
     def engine(self, with_pqmf=None):
         if with_pqmf is None:
             with_pqmf = self.pqmf is not None

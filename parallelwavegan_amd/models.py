@@ -224,6 +224,11 @@ class ParallelWaveGANGenerator(torch.nn.Module):
             self._weights.invalidate()  # .to() / .cuda() replace parameter storage
         return super()._apply(fn, *args, **kwargs)
 
+    def invalidate_weights(self):
+        """Force a re-pack on the next call (after writes through ``p.data`` aliases, which the
+        WeightTracker cannot see)."""
+        self._weights.invalidate()
+
     def engine(self):
         """The HIP engine with this module's current weights packed (re-packed when a
         parameter changes: WeightTracker)."""

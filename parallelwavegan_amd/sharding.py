@@ -53,7 +53,13 @@ def broadcast_weights_rccl(engine, packed, src=0, group=None):
     pwg_rccl_unique_id / pwg_rccl_comm_create / pwg_broadcast_weights), i.e. the path a
     non-Python host uses: rank ``src`` makes the RCCL id, the 128 bytes travel over the existing
     process group, every rank joins a one-shot RCCL communicator on its engine's device and
-    receives the image in place on the current stream. Returns ``packed``."""
+    receives the image in place on the current stream. Returns ``packed``.
+
+    Failure is collective: every phase ends with an agreement (MIN over the process group of a
+    per-rank success flag), so either every rank returns or every rank raises RcclBroadcastError
+    and the caller can fall back on all ranks together. Phase 1, before any rank enters RCCL, has
+    every rank load librccl and make an id (the src rank's is the one used), so a rank that
+    cannot reach RCCL never leaves the others waiting in the communicator's collective init."""
     if not dist.is_available() or not dist.is_initialized():
         return packed
     import ctypes
@@ -62,29 +68,59 @@ def broadcast_weights_rccl(engine, packed, src=0, group=None):
 
     lib = _lib.load()
     rank, world = dist.get_rank(group), dist.get_world_size(group)
+
+    def agree(ok, what):
+        if not all_ranks_ok(ok, group, packed.device):
+            raise RcclBroadcastError(f"RCCL weight broadcast: {what} failed on at least one rank")
+
     buf = ctypes.create_string_buffer(_lib.PWG_RCCL_UNIQUE_ID_BYTES)
-    if rank == src:
-        _lib.check(lib.pwg_rccl_unique_id(buf))
-    obj = [bytes(buf.raw)]
+    ok = lib.pwg_rccl_unique_id(buf) == _lib.PWG_OK
+    agree(ok, "librccl / ncclGetUniqueId")
+    obj = [bytes(buf.raw) if rank == src else None]
     dist.broadcast_object_list(obj, src=src, group=group)
     buf = ctypes.create_string_buffer(obj[0], _lib.PWG_RCCL_UNIQUE_ID_BYTES)
     dev = packed.device.index if packed.device.index is not None else torch.cuda.current_device()
     comm = ctypes.c_void_p()
-    _lib.check(lib.pwg_rccl_comm_create(world, buf, rank, dev, ctypes.byref(comm)))
+    ok = lib.pwg_rccl_comm_create(world, buf, rank, dev, ctypes.byref(comm)) == _lib.PWG_OK
     try:
+        agree(ok, "ncclCommInitRank")
         stream = torch.cuda.current_stream(packed.device)
-        _lib.check(lib.pwg_broadcast_weights(engine._h, comm, src, packed.data_ptr(), stream.cuda_stream))
-        stream.synchronize()
+        ok = lib.pwg_broadcast_weights(engine._h, comm, src, packed.data_ptr(), stream.cuda_stream) == _lib.PWG_OK
+        if ok:
+            stream.synchronize()
+        agree(ok, "pwg_broadcast_weights")
     finally:
-        _lib.check(lib.pwg_rccl_comm_destroy(comm))
+        if comm.value:
+            lib.pwg_rccl_comm_destroy(comm)
     return packed
+
+
+class RcclBroadcastError(RuntimeError):
+    """The C-ABI RCCL weight broadcast failed on at least one rank (raised on every rank)."""
+
+
+def all_ranks_ok(ok, group=None, device=None):
+    """Collective AND of a per-rank boolean (all_reduce MIN); host tensor on gloo."""
+    if not dist.is_available() or not dist.is_initialized():
+        return bool(ok)
+    on_host = dist.get_backend(group) == "gloo" or device is None or torch.device(device).type != "cuda"
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device="cpu" if on_host else device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(t.item())
+
+
+def _reduce_device(device):
+    """Where a small reduction tensor lives: the host on gloo, else the rank's device."""
+    if device is None or dist.get_backend() == "gloo":
+        return "cpu"
+    return device
 
 
 def max_over_ranks(value, device=None):
     """Max of a float over all ranks (timing reduction for bench.py)."""
     if not dist.is_available() or not dist.is_initialized():
         return float(value)
-    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=_reduce_device(device))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -92,7 +128,7 @@ def max_over_ranks(value, device=None):
 def sum_over_ranks(value, device=None):
     if not dist.is_available() or not dist.is_initialized():
         return float(value)
-    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=_reduce_device(device))
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
 

@@ -127,7 +127,7 @@ def test_full_length_libritts_batch_against_torch_cpu(built_lib, cuda_device):
 
 
 @pytest.mark.parametrize("case", ["mel_x30", "mel_x30_res_w_x2", "mel_x30_res_w_x4", "first_conv_overflow",
-                                  "weight_overflow"])
+                                  "skip_overflow", "aux_overflow", "weight_overflow"])
 def test_split_range_guard(case, built_lib, cuda_device):
     """Stress and fp16 range guard of the split-f16 path (pwg_pack_weights PWG_ERR_RANGE, the
     in-kernel non-finite flag read by pwg_run_status), against the float64 oracle. Bar: max|d| <
@@ -139,6 +139,12 @@ def test_split_range_guard(case, built_lib, cuda_device):
         to the fp32 reference's own accuracy class;
       first_conv_overflow: first_conv.weight x1e5 puts x0 beyond 65504, the pair split makes
         inf/-inf: the run must be flagged and redone on the exact-fp32 kernel (range_reruns == 1);
+      skip_overflow: every conv1x1_skip weight and bias x3e4 and last_conv_layers.1.weight / 3e4 (the
+        same function): the final skip sum stays finite but relu(skip * sqrt(1/L)) reaches ~8e4,
+        beyond what the head's pair split carries; the last layer flags it (range_reruns == 1);
+      aux_overflow: conv_layers.5.conv1x1_aux.weight x1e5: that layer's frame-rate aux projection D
+        leaves the pair range (the gate saturates in the reference, a finite result); the aux
+        projection kernel flags it (range_reruns == 1);
       weight_overflow: a gate weight of 7e4 cannot be packed as fp16 pairs; packing reports it and
         the engine uses the exact-fp32 kernel from the start."""
     from oracle import pwg_numpy
@@ -155,6 +161,12 @@ def test_split_range_guard(case, built_lib, cuda_device):
         sd = {k: (v * wx if k.startswith("conv_layers.") and k.endswith(".weight") else v) for k, v in sd.items()}
     elif case == "first_conv_overflow":
         sd["first_conv.weight"] = sd["first_conv.weight"] * 1e5
+    elif case == "skip_overflow":
+        k = 3e4
+        sd = {key: (v * k if ".conv1x1_skip." in key else v) for key, v in sd.items()}
+        sd["last_conv_layers.1.weight"] = sd["last_conv_layers.1.weight"] / k
+    elif case == "aux_overflow":
+        sd["conv_layers.5.conv1x1_aux.weight"] = sd["conv_layers.5.conv1x1_aux.weight"] * 1e5
     else:
         sd["conv_layers.3.conv.weight"] = sd["conv_layers.3.conv.weight"].copy()
         sd["conv_layers.3.conv.weight"][5, 7, 1] = 7e4
@@ -174,10 +186,11 @@ def test_split_range_guard(case, built_lib, cuda_device):
     assert np.isfinite(ref).all() and np.isfinite(y).all()
     err = np.abs(y - ref).max()
     assert err < max(ATOL, 3 * fp32_err), f"{case}: max|d| = {err:.3e}, fp32 reference {fp32_err:.3e}"
-    if case in ("mel_x30", "mel_x30_res_w_x2"):
+    flagged = case in ("first_conv_overflow", "skip_overflow", "aux_overflow")
+    if case in ("mel_x30", "mel_x30_res_w_x2", "skip_overflow", "aux_overflow"):
         assert err < ATOL
-    assert eng.range_reruns == (1 if case == "first_conv_overflow" else 0)
-    if case == "first_conv_overflow":
+    assert eng.range_reruns == (1 if flagged else 0)
+    if flagged:
         # the raw C-ABI path reports the flag instead of rerunning
         plan = eng.plan([37])
         out = torch.empty(37 * 300, device=cuda_device)

@@ -84,3 +84,25 @@ def test_rccl_broadcast_capi(built_lib, cuda_device):
     y = eng.infer([mel], [noise])[0]
     eng.set_packed(ref)
     assert torch.equal(y, eng.infer([mel], [noise])[0])
+
+
+def test_bench_self_launches_ranks(built_lib, cuda_device):
+    """`bench.py --gpus 2` as ONE command starts its two ranks itself (a torch.distributed.run
+    child); on this 1-GPU box they share cuda:0 over gloo. The line reports 2 ranks, 1 device and
+    both ranks' seconds."""
+    import json
+
+    env = dict(os.environ, PWG_NO_BUILD="1", PWG_BENCH_BACKEND="gloo", OMP_NUM_THREADS="4")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "1",
+           "--utts", "8", "--no-latency", "--cpu-seconds", "0", "--pmc", "off"]
+    res = subprocess.run(cmd, env=env, cwd=REPO, capture_output=True, text=True, timeout=110)
+    assert res.returncode == 0, res.stdout[-3000:] + res.stderr[-3000:]
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, res.stdout
+    line = json.loads(lines[0])
+    assert line["ranks"] == 2 and line["n_gpus"] == 1
+    assert len(line["rank_seconds"]) == 2 and all(t > 0 for t in line["rank_seconds"])
+    assert line["config"]["global_batch"] == 16
+    assert line["value"] > 0

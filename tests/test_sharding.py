@@ -80,6 +80,9 @@ def _worker(rank, world, port, result_dir):
         gathered = sharding.gather_outputs(local, len(lengths))
         tmax = sharding.max_over_ranks(float(rank + 1))
         tsum = sharding.sum_over_ranks(float(rank + 1))
+        # collective agreement of the RCCL broadcast's phases: one failing rank fails all
+        assert sharding.all_ranks_ok(True)
+        assert not sharding.all_ranks_ok(rank != 1)
         if rank == 0:
             ref = decode(range(len(lengths)))
             for a, b in zip(gathered, ref):
