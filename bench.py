@@ -164,13 +164,11 @@ def per_rank_seconds(local_s, world, dev):
     return [float(x.item()) for x in ts]
 
 
-def measure_layer_traffic(args):
-    """HBM bytes per middle residual-layer launch of THIS workload, measured in this run: two
-    rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE: separate passes on gfx950) over a child
-    process that runs one warmup and one timed forward of the same plan. FETCH_SIZE is doubled
-    (MI355X_MICROARCH.md: gfx950 reports half the bytes of wide coalesced reads), KB -> bytes.
-    Runs before this process touches the GPU (the child is a separate process, never an exec).
-    Returns (bytes or None, source note)."""
+def _pmc_passes(args):
+    """Two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE: separate passes on gfx950) over a child
+    process (`bench.py --pmc-child`, never an exec) that runs two forwards of this workload.
+    Returns ({counter: {dispatch_id: (kernel_name, value)}}, None) or (None, failure note)."""
+    import csv
     import glob
     import shutil
     import tempfile
@@ -178,7 +176,6 @@ def measure_layer_traffic(args):
     prof = shutil.which("rocprofv3")
     if prof is None:
         return None, "rocprofv3 not found"
-    kernel = f"pwg_layer_{args.layer_kernel or 'split16'}_kernel<false"
     per = {}
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         with tempfile.TemporaryDirectory(prefix="pwg_pmc_", dir="/tmp") as d:
@@ -197,29 +194,80 @@ def measure_layer_traffic(args):
                 return None, f"rocprofv3 --pmc {ctr} pass failed (rc {r.returncode})"
             vals = {}
             for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-                import csv
-
                 for row in csv.DictReader(open(path)):
-                    name = row.get("Kernel_Name", "")
-                    # middle layers: not the last (<true...>) and not layer 0 with the fused first_conv
-                    if kernel in name and ", true>" not in name and row.get("Counter_Name") == ctr:
-                        disp = row.get("Dispatch_Id")
-                        vals[disp] = vals.get(disp, 0.0) + float(row.get("Counter_Value") or 0)
+                    if row.get("Counter_Name") != ctr:
+                        continue
+                    disp = int(row.get("Dispatch_Id") or 0)
+                    name, v = vals.get(disp, (row.get("Kernel_Name", ""), 0.0))
+                    vals[disp] = (name, v + float(row.get("Counter_Value") or 0))
             if not vals:
-                return None, f"rocprofv3 --pmc {ctr}: no {kernel}...> dispatches found"
-            per[ctr] = (sum(vals.values()) / len(vals), len(vals))
-    fetch = per["FETCH_SIZE"][0] * 1024 * 2
-    write = per["WRITE_SIZE"][0] * 1024
+                return None, f"rocprofv3 --pmc {ctr}: no dispatches recorded"
+            per[ctr] = vals
+    return per, None
+
+
+def measure_layer_traffic(args):
+    """HBM bytes per middle residual-layer launch of THIS workload, measured in this run (two
+    --pmc passes over a child running the same plan, _pmc_passes). FETCH_SIZE is doubled
+    (MI355X_MICROARCH.md: gfx950 reports half the bytes of wide coalesced reads), KB -> bytes.
+    Runs before this process touches the GPU. Returns (bytes or None, source note)."""
+    per, err = _pmc_passes(args)
+    if per is None:
+        return None, err
+    kernel = f"pwg_layer_{args.layer_kernel or 'split16'}_kernel<false"
+    mean = {}
+    for ctr, vals in per.items():
+        # middle layers: not the last (<true...>) and not layer 0 with the fused first_conv
+        v = [x for name, x in vals.values() if kernel in name and ", true>" not in name]
+        if not v:
+            return None, f"rocprofv3 --pmc {ctr}: no {kernel}...> dispatches found"
+        mean[ctr] = (sum(v) / len(v), len(v))
+    fetch = mean["FETCH_SIZE"][0] * 1024 * 2
+    write = mean["WRITE_SIZE"][0] * 1024
     note = (f"measured in this run: rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) and WRITE_SIZE passes over "
-            f"one forward of this workload in a child process, mean of {per['FETCH_SIZE'][1]} middle-layer launches; "
+            f"two forwards of this workload in a child process, mean of {mean['FETCH_SIZE'][1]} middle-layer launches; "
             f"read {fetch / 1e9:.3f} GB + write {write / 1e9:.3f} GB")
     return fetch + write, note
 
 
+def measure_program_traffic(args):
+    """Vocoder configs: HBM bytes of ONE whole forward (every launch of the conv program), measured
+    as measure_layer_traffic does, from the second of the child's two forwards (the later half of
+    its dispatches). Returns (bytes or None, source note, {kernel: bytes} of the top kernels)."""
+    per, err = _pmc_passes(args)
+    if per is None:
+        return None, err, None
+    tot, by_kernel = {}, {}
+    for ctr, vals in per.items():
+        ids = sorted(vals)
+        second = ids[len(ids) // 2:]
+        scale = 2048.0 if ctr == "FETCH_SIZE" else 1024.0
+        tot[ctr] = sum(vals[i][1] for i in second) * scale
+        for i in second:
+            name = vals[i][0].split("(")[0].replace("void ", "").replace("pwg::", "")
+            by_kernel[name] = by_kernel.get(name, 0.0) + vals[i][1] * scale
+    note = (f"measured in this run: rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) and WRITE_SIZE passes over "
+            f"two forwards in a child process, the second forward's {len(per['FETCH_SIZE']) // 2} dispatches; read "
+            f"{tot['FETCH_SIZE'] / 1e9:.3f} GB + write {tot['WRITE_SIZE'] / 1e9:.3f} GB per forward")
+    top = dict(sorted(((k, round(v / 1e9, 4)) for k, v in by_kernel.items()), key=lambda kv: -kv[1])[:6])
+    return tot["FETCH_SIZE"] + tot["WRITE_SIZE"], note, top
+
+
 def pmc_child(args):
-    """--pmc-child: one warmup + one forward of the bench plan, nothing printed (profiled by
-    measure_layer_traffic)."""
+    """--pmc-child: two forwards of the bench plan (PWG or vocoder), nothing printed (profiled by
+    _pmc_passes)."""
     dev = torch.device("cuda", 0)
+    if args.config in VOCODERS:
+        m, eng, _, _, _ = vocoder_setup(args, dev)
+        lengths = synthetic.libritts_lengths(args.utts, seed=3)
+        plan = eng.plan(lengths.tolist())
+        rs = np.random.RandomState(100)
+        mel = torch.from_numpy(rs.standard_normal(int(lengths.sum()) * 80).astype(np.float32)).to(dev)
+        out = torch.empty(plan.out_rows * eng.out_channels, dtype=torch.float32, device=dev)
+        for _ in range(2):
+            eng.run(plan, mel, out, check=False)
+        torch.cuda.synchronize(dev)
+        return
     params = configs.generator_params(args.config)
     eng = Engine(params, dev)
     eng.set_option("layer_kernel", args.layer_kernel or "split16")
@@ -372,12 +420,9 @@ def vocoder_latency_rows(m, dev, reps=10):
     return {"model": f"{type(m).__name__}.inference / inference_batch (drop-in)", "rows": rows}
 
 
-def bench_vocoder(args, rank, world, dev):
-    """MelGAN-family generator inference (BASELINE configs[2] multi_band_melgan.v2 and [3]
-    hifigan.v1, SURVEY.md sec 8(f)) on the conv-network executor: same ragged-batch workload shape
-    as the PWG bench, weak scaling, utterance sharding, RCCL weight broadcast."""
-    from oracle.melgan_torch_cpu import TorchCPUVocoder  # cpu_baseline leg only
-    from parallelwavegan_amd.engine import fold_weight_norm
+def vocoder_setup(args, dev):
+    """The drop-in module of a vocoder config with seeded weights on `dev` and its engine set up
+    as the bench runs it. Returns (module, engine, class name, params, (state dict, PQMF taps))."""
     from parallelwavegan_amd.hifigan import HiFiGANGenerator
     from parallelwavegan_amd.melgan import PQMF, MelGANGenerator
 
@@ -395,6 +440,17 @@ def bench_vocoder(args, rank, world, dev):
     eng.set_fuse_pairs(not args.cnet_nofuse)
     if args.pair_steps:
         eng.set_pair_steps(args.pair_steps)
+    return m, eng, cls_name, params, (sd, syn)
+
+
+def bench_vocoder(args, rank, world, dev, live_traffic=(None, "off", None)):
+    """MelGAN-family generator inference (BASELINE configs[2] multi_band_melgan.v2 and [3]
+    hifigan.v1, SURVEY.md sec 8(f)) on the conv-network executor: same ragged-batch workload shape
+    as the PWG bench, weak scaling, utterance sharding, RCCL weight broadcast."""
+    from oracle.melgan_torch_cpu import TorchCPUVocoder  # cpu_baseline leg only
+    from parallelwavegan_amd.engine import fold_weight_norm
+
+    m, eng, cls_name, params, (sd, syn) = vocoder_setup(args, dev)
     if world > 1:
         broadcast_packed_weights(eng.packed, src=0)
     P = eng.program
@@ -441,6 +497,7 @@ def bench_vocoder(args, rank, world, dev):
     fl_frame = program_flops_per_frame(P)
     by_frame = program_bytes_per_frame(P)
     kern_ms = sum(ms for _, ms, _ in timing) / args.steps
+    voc_bytes = live_traffic[0] and int(live_traffic[0])  # HBM bytes of one forward (rocprofv3 --pmc)
     frames = int(lengths.sum())
     achieved = fl_frame * frames / (kern_ms * 1e-3) / 1e12
     top = sorted(timing, key=lambda r: -r[1])[:5]
@@ -493,13 +550,19 @@ def bench_vocoder(args, rank, world, dev):
         "top_ops_ms_per_step": {n: round(ms / args.steps, 3) for n, ms, _ in top},
         "roofline": ({"kernel": "all conv ops (fp32 MFMA implicit GEMM), whole program", "bound": "mfma",
                       "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                      "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                      "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": voc_bytes,
+                      "traffic_source": live_traffic[1], "traffic_top_kernels_GB": live_traffic[2],
+                      "hbm_GBs_measured": voc_bytes and round(voc_bytes / (kern_ms * 1e-3) / 1e9, 1),
+                      "hbm_frac_measured": voc_bytes and round(voc_bytes / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                       "flop_per_sample": round(fl_frame / hop, 1),
                       "algorithmic_bytes_per_sample": round(by_frame / hop, 1)} if args.cnet_fp32 else
                      # split-f16: every reference product runs as three f16 MFMA products
                      {"kernel": "all conv ops (split-f16 MFMA implicit GEMM), whole program", "bound": "mfma",
                       "achieved": round(3 * achieved, 3), "peak": F16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                      "frac": round(3 * achieved / F16_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                      "frac": round(3 * achieved / F16_MFMA_PEAK_TFLOPS, 4), "traffic": voc_bytes,
+                      "traffic_source": live_traffic[1], "traffic_top_kernels_GB": live_traffic[2],
+                      "hbm_GBs_measured": voc_bytes and round(voc_bytes / (kern_ms * 1e-3) / 1e9, 1),
+                      "hbm_frac_measured": voc_bytes and round(voc_bytes / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                       "reference_tflops": round(achieved, 3),
                       "flop_per_sample": round(fl_frame / hop, 1),
                       "executed_f16_flop_per_sample": round(3 * fl_frame / hop, 1),
@@ -625,14 +688,18 @@ def main():
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     # measured HBM traffic of the dominant kernel, before this process touches the GPU
     live_traffic = (None, "off")
-    if (args.pmc == "auto" and int(os.environ.get("WORLD_SIZE", "1")) == 1 and args.config not in VOCODERS
+    single = args.pmc == "auto" and int(os.environ.get("WORLD_SIZE", "1")) == 1
+    if (single and args.config not in VOCODERS
             and not args.strong and args.sub_plans == 1 and args.layer_kernel in (None, "split16")
             and not args.no_fuse_first and not args.waves_per_wg and not args.wg_per_cu):
         live_traffic = measure_layer_traffic(args)
+    voc_traffic = (None, "off", None)
+    if single and args.config in VOCODERS:
+        voc_traffic = measure_program_traffic(args)
     rank, world, dev = dist_setup(args.gpus)
     _lib.build()
     if args.config in VOCODERS:
-        return bench_vocoder(args, rank, world, dev)
+        return bench_vocoder(args, rank, world, dev, voc_traffic)
     params = configs.generator_params(args.config)
     fs = configs.SAMPLING_RATE[args.config]
     eng = Engine(params, dev)

@@ -163,7 +163,10 @@ PWG_API int pwg_run(PwgPlan* p, const float* packed, const float* mel, const flo
  * if any live column's final skip sum was not finite, i.e. some x / D / first_conv value
  * exceeded the fp16 range (|v| >= 65520) or the input itself was not finite. The output of
  * such a run is not valid; rerun it with PWG_OPT_LAYER_KERNEL 0 (exact fp32), which is
- * what the Python drop-in does. The exact-fp32 kernels never set the flag. */
+ * what the Python drop-in does. The exact-fp32 kernels never set the flag. The split16 aux
+ * projection also flags a D value beyond the pair range, and the last layer a scaled skip sum
+ * the head cannot split. PWG_ERR_HIP: a layer-pipelined run (PWG_OPT_PIPELINE) whose bounded
+ * dependency wait gave up; its output is invalid. */
 PWG_API int pwg_run_status(PwgPlan* p, const void* workspace, void* stream);
 
 /* HIP graph of one pwg_run with fixed buffers (no reference counterpart: the replay path for
@@ -193,9 +196,16 @@ enum {
                                     kernel 3) */
   PWG_OPT_WAVES_PER_WG = 1,   /* persistent kernel: waves per workgroup (1..8, default 8) */
   PWG_OPT_WG_PER_CU = 2,      /* persistent kernel: workgroups per CU in the grid (default 1) */
-  PWG_OPT_FUSE_FIRST_CONV = 3 /* split16 layer kernel: first_conv evaluated inside layer 0 from the
+  PWG_OPT_FUSE_FIRST_CONV = 3, /* split16 layer kernel: first_conv evaluated inside layer 0 from the
                                     noise, x0 never stored (default 1; bit-identical to 0) */
+  PWG_OPT_PIPELINE = 4         /* split16: plans with at most this many padded samples run all
+                                    residual layers in ONE layer-pipelined launch (each CU keeps one
+                                    layer's weights; blocks flow layer to layer through per-block
+                                    progress words), bit-identical to the per-layer launches; the
+                                    B = 1 decode path of bin/decode.py. 0 = never. Applies to plans
+                                    created afterwards (default PWG_PIPE_MAX_DEFAULT). */
 };
+#define PWG_PIPE_MAX_DEFAULT 0LL /* off: measured slower than the per-layer launches */
 PWG_API int pwg_set_option(PwgHandle* h, int option, long long value);
 /* Current value of an option (the layer kernel the handle picked for its shape, ...). */
 PWG_API int pwg_get_option(const PwgHandle* h, int option, long long* value);

@@ -97,6 +97,7 @@ PWG_OPT_LAYER_KERNEL = 0
 PWG_OPT_WAVES_PER_WG = 1
 PWG_OPT_WG_PER_CU = 2
 PWG_OPT_FUSE_FIRST_CONV = 3
+PWG_OPT_PIPELINE = 4
 
 
 class PwgConfig(ctypes.Structure):

@@ -31,17 +31,25 @@ def engines_of(model):
     return [model.engine()]
 
 
-def auto_batch_frames(model, device, frac=0.25, cap_gib=8.0, probe_frames=512):
-    """Mel frames per ragged engine pass that fit ``frac`` of the free device memory (at most
-    ``cap_gib``): the plan workspace of a probe batch per audio sample, plus the caller's mel input
-    (4 B x channels per frame) and noise / output (4 B per sample and channel)."""
+def batch_cost_model(model, device, frac=0.25, cap_gib=8.0, probe_frames=512, probe_utts=8):
+    """Bytes of one engine pass as a function of (mel frames, utterances) and the budget they must
+    fit: ``frac`` of the free device memory, at most ``cap_gib``. Per frame: the plan workspace of
+    a one-utterance probe, plus the caller's mel input (4 B x input channels) and noise / output
+    (4 B per audio sample and output channel, the noise for PWG only). Per utterance: what a probe
+    of ``probe_utts`` equal utterances of the same total length adds over the one-utterance probe
+    (segment gaps and tile padding). Channel counts and samples per frame come from the model."""
     eng = model.engine()
-    hop = int(getattr(model, "upsample_factor", None) or eng.hop)
-    plan = eng.plan([probe_frames])
-    per_frame = plan.workspace_bytes / probe_frames + 4 * 80 + 4 * hop * 3
+    if hasattr(model, "aux_channels"):  # ParallelWaveGANGenerator: mel in, noise in, audio out
+        in_ch, hop, out_ch, noise = model.aux_channels, model.upsample_factor, model.out_channels, 1
+    else:  # MelGAN family: the program's input channels, output rate (PQMF included) and channels
+        in_ch, hop, out_ch, noise = eng.program.channels[0], eng.hop, eng.out_channels, 0
+    one = eng.plan([probe_frames]).workspace_bytes
+    many = eng.plan([probe_frames // probe_utts] * probe_utts).workspace_bytes
+    per_frame = one / probe_frames + 4 * in_ch + 4 * hop * (out_ch + noise)
+    per_utt = max(0.0, (many - one) / (probe_utts - 1))
     free, _ = torch.cuda.mem_get_info(device)
     budget = min(free * frac, cap_gib * (1 << 30))
-    return max(probe_frames, int(budget // per_frame))
+    return per_frame, per_utt, budget
 
 
 def main(argv=None):
@@ -109,8 +117,15 @@ def main(argv=None):
     logging.info(f"The number of features to be decoded = {len(files)}.")
     sr = config["sampling_rate"]
     if args.batch_frames is None:
-        args.batch_frames = auto_batch_frames(model, device, args.batch_mem_frac, args.batch_mem_gib)
-        logging.info(f"batch size: {args.batch_frames} mel frames per engine pass")
+        per_frame, per_utt, budget = batch_cost_model(model, device, args.batch_mem_frac, args.batch_mem_gib)
+        logging.info(f"batch budget: {budget / 2**30:.2f} GiB, {per_frame:.0f} B per mel frame + {per_utt:.0f} B "
+                     f"per utterance")
+
+        def fits(nfr, nutt):
+            return nfr * per_frame + nutt * per_utt <= budget
+    else:
+        def fits(nfr, nutt):
+            return nfr <= args.batch_frames
 
     def decode(idx):
         outs = [None] * len(idx)
@@ -137,7 +152,7 @@ def main(argv=None):
             batch, nfr = [], 0
 
         for slot, i in enumerate(idx):
-            if batch and nfr + lengths[i] > args.batch_frames:
+            if batch and not fits(nfr + lengths[i], len(batch) + 1):
                 flush()
             batch.append((slot, i))
             nfr += lengths[i]

@@ -273,6 +273,7 @@ class CnetEngine:
         if not self.split_range_ok and self.split_f16:
             logging.warning("vocoder weights exceed the fp16 pair range of the split-f16 mode: using exact fp32")
             self._set_split(False)
+            self.split_f16 = False
         self.packed = torch.from_numpy(packed).to(self.device)
         return self.packed
 

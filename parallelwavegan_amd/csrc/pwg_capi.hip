@@ -314,6 +314,7 @@ struct PwgHandle {
   // options
   int layer_kernel = 0, waves_per_wg = 8, wg_per_cu = 1;
   int fuse_first = 1;  // PWG_OPT_FUSE_FIRST_CONV
+  long long pipe_max = PWG_PIPE_MAX_DEFAULT;  // PWG_OPT_PIPELINE: largest padded plan on the layer pipeline
   int n_cu = 0;
   // timing
   bool timing = false;
@@ -331,6 +332,9 @@ struct PwgPlan {
   // written by pwg_plan_desc_kernel at the start of every pwg_run
   size_t ws_x0, ws_x1, ws_skip, ws_c1, ws_d, ws_ctr, ws_flag;
   size_t ws_utts, ws_tile_utt, ws_gap, ws_blocks, ws_total;
+  // layer pipeline (split16, plans whose residual plane fits 2 GB): third plane + progress words
+  bool pipe_ok = false;
+  size_t ws_x2 = 0, ws_prog = 0;
   long long max_blocks_per_utt = 0;
 };
 
@@ -851,6 +855,22 @@ int pwg_plan_create(PwgHandle* h, int n_utts, const long long* frames, int layou
   p->ws_tile_utt = o; o += align_bytes(sizeof(int) * p->n_tiles);
   p->ws_gap = o; o += align_bytes(sizeof(long long) * std::max<long long>(p->n_gap_tiles, 1));
   p->ws_blocks = o; o += align_bytes(sizeof(BlockDesc) * p->n_tiles * (TILE / 32));
+  // the layer pipeline addresses a plane with 32-bit buffer offsets (< 2 GB) and polls the blocks
+  // its dependencies span with one wave (<= 64); its extra plane is only allocated when it can run
+  const int tc = h->cfg.use_causal_conv ? h->KS - 1 : (h->KS - 1) / 2;
+  auto reach = [](long long taps, int d) { return (int)((taps * d + 31) / 32); };
+  bool lanes_ok = h->KS == 3;
+  for (int l = 0; l < h->L && lanes_ok; ++l) {
+    const int rl1 = reach(tc, h->dil[l]), rr1 = reach(h->KS - 1 - tc, h->dil[l]);
+    const int rl2 = l >= 2 ? reach(tc, h->dil[l - 2]) : 0, rr2 = l >= 2 ? reach(h->KS - 1 - tc, h->dil[l - 2]) : 0;
+    lanes_ok = std::max(rl1, rr2) + std::max(rr1, rl2) + 1 <= 64;
+  }
+  p->pipe_ok = h->split_ok && h->L >= 2 && h->L <= PIPE_MAX_LAYERS && lanes_ok &&
+               (long long)h->RS * 4 * (p->Tpad + h->gap) < (1LL << 31) && p->Tpad <= h->pipe_max;
+  if (p->pipe_ok) {
+    p->ws_x2 = o; o += align_bytes(sizeof(float) * h->RS * p->Tpad);
+    p->ws_prog = o; o += align_bytes(sizeof(int) * p->n_tiles * (TILE / 32));
+  }
   p->ws_total = o;
   *out = p;
   return PWG_OK;
@@ -913,6 +933,10 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
 
   int* range_flag = (int*)(ws + p->ws_flag);
   hipError_t e = hipSuccess;
+  // all residual layers in ONE layer-pipelined launch (split16, small plans); the
+  // grid needs one workgroup per CU for every layer and a multiple of 8 workgroups
+  const int pipe_wg = h->n_cu / 8 * 8;
+  const bool use_pipe = p->pipe_ok && h->layer_kernel == 3 && p->Tpad <= h->pipe_max && pipe_wg >= h->L;
   UttDesc* d_utts = (UttDesc*)(ws + p->ws_utts);
   int* d_tile_utt = (int*)(ws + p->ws_tile_utt);
   long long* d_gap_col0 = (long long*)(ws + p->ws_gap);
@@ -927,6 +951,7 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
     // work-queue heads and the range flag (adjacent) start at zero every run
     da.zero = u0 == 0 ? sched_ctr : nullptr;
     da.n_zero = (int)((p->ws_flag + sizeof(int) - p->ws_ctr) / sizeof(int));
+    da.prog = use_pipe ? (int*)(ws + p->ws_prog) : nullptr;
     e = launch_plan_desc(da, p->max_blocks_per_utt, s);
     if (e != hipSuccess) return hip_fail(e, "plan descriptor launch");
   }
@@ -953,6 +978,7 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
   fa.noise = noise; fa.w = packed + h->off_first_w; fa.b = packed + h->off_first_b; fa.x = x0; fa.x1 = x1;
   fa.tile_utt = d_tile_utt; fa.utts = d_utts; fa.gap_col0 = d_gap_col0; fa.n_work = p->n_tiles;
   fa.Tpad = p->Tpad; fa.R = h->R; fa.RS = h->RS;
+  fa.x2 = use_pipe ? (float*)(ws + p->ws_x2) : nullptr;
   // split16 with the fused first_conv: layer 0 builds x0 itself; only the gap tiles of both
   // residual buffers are zeroed here (the work-tile branch is skipped: n_work = 0)
   const bool fuse_first = split16 && h->fuse_first && h->L > 1;
@@ -965,6 +991,45 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
   });
   if (e != hipSuccess) return hip_fail(e, "first_conv launch");
 
+  if (use_pipe) {
+    PipeArgs pp;
+    SplitArgs& sa = pp.base;
+    sa.x_in = nullptr; sa.x_out = nullptr;
+    sa.skip = skip; sa.skip0 = packed + h->off_skip0_16;
+    sa.d = nullptr;
+    sa.tab = packed + h->off_tab_interior;
+    sa.tab_left = (int)(h->off_tab_left - h->off_tab_interior);
+    sa.tab_right = (int)(h->off_tab_right - h->off_tab_interior);
+    sa.tab_small = (int)(h->off_tab_small - h->off_tab_interior);
+    sa.blocks = d_blocks;
+    sa.wg = nullptr;
+    sa.hw1 = packed + h->off_head16_w1; sa.hw2 = packed + h->off_head16_w2; sa.hb2 = packed + h->off_head_b2;
+    sa.out = out;
+    sa.H = (int)h->aux.H; sa.J1 = h->aux.J1; sa.TL = h->aux.TL; sa.TR = h->aux.TR; sa.Fmin = h->aux.Fmin;
+    sa.n_blocks = (int)(p->n_tiles * (TILE / 32)); sa.dil = 1; sa.first = 0; sa.O = h->O;
+    if (p->layout == PWG_LAYOUT_INFERENCE) { sa.out_stride_t = h->O; sa.out_stride_o = 1; }
+    else { sa.out_stride_t = 1; sa.out_stride_o = (int)p->utts[0].T; }
+    sa.skip_scale = (float)std::sqrt(1.0 / h->L);
+    sa.ctr = nullptr; sa.trace = nullptr; sa.compute_waves = 8;
+    sa.noise = fuse_first ? noise : nullptr;
+    sa.fw = packed + h->off_first_w; sa.fb = packed + h->off_first_b;
+    sa.range_flag = range_flag;
+    pp.wg0 = reinterpret_cast<const unsigned*>(packed + h->off_layers + h->lo_split16);
+    pp.wg_stride = (long long)h->layer_stride;
+    pp.d0 = reinterpret_cast<const unsigned*>(dproj);
+    pp.d_stride = p->F_total * h->GR;
+    pp.x[0] = reinterpret_cast<unsigned*>(x0);
+    pp.x[1] = reinterpret_cast<unsigned*>(x1);
+    pp.x[2] = reinterpret_cast<unsigned*>(ws + p->ws_x2);
+    pp.prog = (int*)(ws + p->ws_prog);
+    pp.ctr = sched_ctr;
+    pp.L = h->L;
+    for (int l = 0; l < PIPE_MAX_LAYERS; ++l) pp.dil[l] = l < h->L ? h->dil[l] : 1;
+    const int tc = h->cfg.use_causal_conv ? h->KS - 1 : (h->KS - 1) / 2;
+    e = timed(PWG_KERNEL_RESIDUAL_LAYER, [&] { return launch_pipe_split16(pp, tc, pipe_wg, s); });
+    if (e != hipSuccess) return hip_fail(e, "layer-pipelined forward launch");
+    return PWG_OK;
+  }
   float* xin = x0;
   float* xout = x1;
   for (int l = 0; l < h->L; ++l) {
@@ -1022,34 +1087,39 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
       if (fuse_first && l == 0) {
         sa.noise = noise; sa.fw = packed + h->off_first_w; sa.fb = packed + h->off_first_b;
       }
-#if PWG_TRACE
+      // split16: all of a launch's waves stage the image, wpw of them take blocks. Mid-size plans
+      // (8-32 blocks per CU) run 4 computing waves, one per SIMD: with two per SIMD and two or three
+      // blocks each, the SIMD's issue arbitration lets one wave finish a block-time before its
+      // partner and the launch waits for the later one (LJ T' = 512: 1.58 -> 1.47 ms per forward)
+      const int launch_w = split16 ? std::min(8, h->waves_per_wg) : wpw;
+      if (split16 && la.n_blocks > 8LL * h->n_cu && la.n_blocks <= 32LL * h->n_cu) wpw = std::min(wpw, 4);
+      sa.compute_waves = std::min(wpw, launch_w);
+      // diagnostic per-wave timeline (PWG_TRACE_FILE set; split16): every layer's records, dumped
+      // after the last layer of the run (tools/trace_layer.py)
       static unsigned long long* d_trace_s = nullptr;
-      const size_t per_layer_s = (size_t)nwg * 8 * 8;
-      if (!d_trace_s && hipMalloc((void**)&d_trace_s, per_layer_s * 64 * sizeof(unsigned long long)) != hipSuccess)
-        return fail(PWG_ERR_HIP, "trace buffer");
-      sa.trace = d_trace_s + per_layer_s * (l % 64);
-#endif
+      const char* trace_fn = split16 ? getenv("PWG_TRACE_FILE") : nullptr;
+      const size_t per_layer_s = (size_t)nwg * launch_w * 8;
+      if (trace_fn) {
+        if (!d_trace_s && hipMalloc((void**)&d_trace_s, (size_t)nwg * 8 * 8 * 64 * sizeof(unsigned long long)) != hipSuccess)
+          return fail(PWG_ERR_HIP, "trace buffer");
+        sa.trace = d_trace_s + per_layer_s * (l % 64);
+      }
       e = timed(PWG_KERNEL_RESIDUAL_LAYER, [&] {
-        return split16 ? launch_layer_split16(sa, last, la.tap_center, wpw, nwg, s)
+        return split16 ? launch_layer_split16(sa, last, la.tap_center, launch_w, nwg, s)
                        : launch_layer_split(sa, last, la.tap_center, wpw, nwg, s);
       });
-#if PWG_TRACE
-      if (e == hipSuccess && last) {
-        std::vector<unsigned long long> host(per_layer_s * h->L);
+      if (e == hipSuccess && last && trace_fn) {
+        std::vector<unsigned long long> host(per_layer_s * std::min(h->L, 64));
         e = hipStreamSynchronize(s);
         if (e == hipSuccess) e = hipMemcpy(host.data(), d_trace_s, host.size() * 8, hipMemcpyDeviceToHost);
-        const char* fn = getenv("PWG_TRACE_FILE");
-        if (e == hipSuccess && fn) {
-          FILE* f = fopen(fn, "wb");
-          if (f) {
-            const long long hdr[4] = {h->L, nwg, h->waves_per_wg, 8};
-            fwrite(hdr, sizeof(hdr), 1, f);
-            fwrite(host.data(), 8, host.size(), f);
-            fclose(f);
-          }
+        FILE* f = e == hipSuccess ? fopen(trace_fn, "wb") : nullptr;
+        if (f) {
+          const long long hdr[4] = {std::min(h->L, 64), nwg, launch_w, 8};
+          fwrite(hdr, sizeof(hdr), 1, f);
+          fwrite(host.data(), 8, host.size(), f);
+          fclose(f);
         }
       }
-#endif
     } else if (h->layer_kernel == 0 && h->aux.nka <= 4) {
       PersistArgs pa2;
       pa2.x_in = xin; pa2.x_out = xout; pa2.skip = skip; pa2.d = la.d;
@@ -1124,6 +1194,9 @@ int pwg_run_status(PwgPlan* p, const void* workspace, void* stream) {
   hipError_t e = hipMemcpyAsync(&flag, (const char*)workspace + p->ws_flag, sizeof(int), hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return hip_fail(e, "run status");
+  if (flag & 2)
+    return fail(PWG_ERR_HIP, "layer-pipelined forward: a dependency wait timed out (the output is invalid); "
+                              "rerun with PWG_OPT_PIPELINE 0 and report this");
   if (flag != 0)
     return fail(PWG_ERR_RANGE,
                 "split-f16 range flag: a value left the fp16 pair range (an aux projection row, the "
@@ -1221,6 +1294,11 @@ int pwg_set_option(PwgHandle* h, int option, long long value) {
       if (value < 1 || value > 64) return fail(PWG_ERR_INVALID, "workgroups per CU must be in [1, 64]");
       h->wg_per_cu = (int)value;
       return PWG_OK;
+    case PWG_OPT_PIPELINE:
+      if (value < 0) return fail(PWG_ERR_INVALID, "pipeline plan limit must be >= 0");
+      h->pipe_max = value;
+      return PWG_OK;
+
     default:
       return fail(PWG_ERR_INVALID, "unknown option");
   }
@@ -1233,6 +1311,8 @@ int pwg_get_option(const PwgHandle* h, int option, long long* value) {
     case PWG_OPT_WAVES_PER_WG: *value = h->waves_per_wg; return PWG_OK;
     case PWG_OPT_FUSE_FIRST_CONV: *value = h->fuse_first; return PWG_OK;
     case PWG_OPT_WG_PER_CU: *value = h->wg_per_cu; return PWG_OK;
+    case PWG_OPT_PIPELINE: *value = h->pipe_max; return PWG_OK;
+
     default: return fail(PWG_ERR_INVALID, "unknown option");
   }
 }

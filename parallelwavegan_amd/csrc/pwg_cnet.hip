@@ -44,84 +44,17 @@ typedef float f32x8v __attribute__((ext_vector_type(8)));
 constexpr int CN_COLS = 128;       // output columns per workgroup (4 waves x 32)
 constexpr int CN_CHUNK = 16;       // input channels per K chunk
 constexpr int CN_MAX_CHUNKS = 4096;
-#ifndef PWG_CNET_G
-#define PWG_CNET_G 1  // 2 (two chunks per barrier) measured 9 % slower on HiFiGAN v1
-#endif
-constexpr int CN_G = PWG_CNET_G;   // 16-channel chunks staged per barrier
-#ifndef PWG_CNET_NT2_MT
-#define PWG_CNET_NT2_MT 0  // > 0: split-mode conv ops with MT >= this use 2 column tiles per wave (A/B)
-#endif
-#ifndef PWG_CNET_NW8_MT
-#define PWG_CNET_NW8_MT 4  // conv ops with MT >= this run 8-wave workgroups (256 columns); 0: 4 waves (A/B)
-#endif
-#ifndef PWG_CNET_XTILE
-#define PWG_CNET_XTILE 1  // 0: wide dilated convs on the tap-major pwg_cnet_conv_kernel (A/B)
-#endif
-#ifndef PWG_CNET_XTILE_MINMT
-#define PWG_CNET_XTILE_MINMT 1  // smallest row tile (m-tiles of 32) that uses the x-tile kernel
-#endif
-#ifndef PWG_PAIR_OFF
-#define PWG_PAIR_OFF 0  // 1: no conv-pair fusion (A/B)
-#endif
-#ifndef PWG_CNET_XTILE_CB
-#define PWG_CNET_XTILE_CB 1  // most 16-channel blocks the x-tile kernel stages per barrier pair (2/4 measured 1 % slower on HiFiGAN v1, r02_xt5)
-#endif
-#ifndef PWG_CNET_XTILE_CB_MAXK
-#define PWG_CNET_XTILE_CB_MAXK 11  // grouping only for kernel sizes up to this (A/B)
-#endif
-#ifndef PWG_CNET_XTILE_LDS
-#define PWG_CNET_XTILE_LDS (150 * 1024)
-#endif
-#ifndef PWG_CNET_CONVT_ONE_LAUNCH
-#define PWG_CNET_CONVT_ONE_LAUNCH 1  // 0: one launch per ConvTranspose phase (A/B)
-#endif
-#ifndef PWG_CNET_XPAIR
-#define PWG_CNET_XPAIR 1  // 0: x-tile conv pairs as two launches (A/B)
-#endif
-#ifndef PWG_CNET_XPAIR_MAXK
-#define PWG_CNET_XPAIR_MAXK 11  // largest kernel size fused into an x-tile pair
-#endif
-#ifndef PWG_CNET_XSTACK
-#define PWG_CNET_XSTACK 1  // 1: ResidualStacks on the x-tile scheme when x-tile is on (A/B)
-#endif
-#ifndef PWG_CNET_XPAIR_C128
-#define PWG_CNET_XPAIR_C128 1  // 1: 128-channel k = 3 pairs on the x-tile pair kernel too (159.7 KB of LDS; A/B)
-#endif
-#ifndef PWG_CNET_XPAIR_OVERLAP
-#define PWG_CNET_XPAIR_OVERLAP 1  // 1: the x-tile pair's h tile reuses the input-row space (A/B)
-#endif
-#ifndef PWG_CNET_XTILE_CONVT
-#define PWG_CNET_XTILE_CONVT 2  // ConvTranspose phases of <= this many m-tiles on the x-tile kernel: faster
-                                // up to 64 output channels, slower at 128-256 (stride 8; profiles/r02_ct)
-#endif
-#ifndef PWG_CNET_XTILE_CONVT_CB
-#define PWG_CNET_XTILE_CONVT_CB 1  // their channel blocks per staging step, at most (A/B)
-#endif
-#ifndef PWG_CNET_XT_WPE
-#define PWG_CNET_XT_WPE 0  // waves per SIMD asked of the small x-tile kernels (0: compiler's choice; A/B)
-#endif
-#ifndef PWG_CNET_XT_NC2
-#define PWG_CNET_XT_NC2 0  // unfused x-tile convs with 512 columns per workgroup: 0 never, 1 where the
-                           // workgroups per CU do not drop, 2 wherever it fits LDS (A/B: bit-identical,
-                           // not faster: HiFiGAN v1 58.6 ms off, 61.8 ms with 1 or 2, profiles/r02_nc)
-#endif
-#ifndef PWG_CNET_XT_SYNC
-#define PWG_CNET_XT_SYNC 1  // unfused x-tile convs that would run one workgroup per CU (register prefetch
-                            // over 128 VGPRs) but fit two in LDS: synchronous staging, 128 VGPRs (A/B)
-#endif
-#ifndef PWG_CNET_XT_TSPLIT
-#define PWG_CNET_XT_TSPLIT 1  // synchronous staging of k = 11, 4-m-tile convs in two tap steps (6 + 5 taps):
-                              // A region 48 KB, two workgroups per CU (A/B)
-#endif
-#ifndef PWG_CNET_XT_MT2_MAXK
-#define PWG_CNET_XT_MT2_MAXK 7  // >= 256-row convs with <= this many taps: 2 m-tiles per workgroup (0: off; A/B)
-#endif
-#ifndef PWG_CNET_XSTACK_OCC2
-#define PWG_CNET_XSTACK_OCC2 1  // 1: size the x-tile stack's LDS for two workgroups per CU when it can (A/B)
-#endif
-#ifndef PWG_CNET_DEPTH2
-#define PWG_CNET_DEPTH2 0  // 1: loads two chunk groups ahead (A/B variant)
-#endif
+// Tuned choices (round 2, same-box A/B; the rejected alternatives are in git history before
+// round 3: two chunks per barrier, two column tiles per wave, 512-column x-tile workgroups, 2/4
+// channel blocks per staging step, two-deep load rings, explicit waves-per-SIMD requests).
+constexpr int CN_G = 1;                    // 16-channel chunks staged per barrier (2: 9 % slower)
+constexpr int CNET_NW8_MT = 4;             // conv ops with MT >= this run 8-wave workgroups (256 columns)
+constexpr int CNET_XTILE_LDS = 150 * 1024; // LDS budget of one x-tile workgroup
+constexpr int CNET_XPAIR_MAXK = 11;        // largest kernel size fused into an x-tile pair
+constexpr int CNET_XTILE_CONVT = 2;        // ConvTranspose phases of <= this many m-tiles on the x-tile
+                                           // kernel: faster up to 64 output channels, slower at 128-256
+                                           // (stride 8; profiles/r02_ct)
+constexpr int CNET_XT_MT2_MAXK = 7;        // >= 256-row convs with <= this many taps: 2 m-tiles per workgroup
 
 struct ChunkDesc {   // one K chunk of an op (uniform per launch)
   int src;           // 0 / 1
@@ -350,48 +283,6 @@ __global__ void __launch_bounds__(64 * NW) pwg_cnet_conv_kernel(const CnConvArgs
 
   const int n_groups = a.n_chunks / G;
   f32x8v bcur[G][NT];
-#if PWG_CNET_DEPTH2
-  // Loads run TWO chunk groups ahead (register ring of 2): chunk c+2's A fragments and raw B rows
-  // are issued before chunk c's MFMAs; chunk c+1's (issued one step earlier) are staged / prepared
-  // after them.
-  f32x4v ar0[G][AQ], ar1[G][AQ];
-  BRaw br0[G], br1[G];
-  aload(0, ar0);
-  astore(0, ar0);
-#pragma unroll
-  for (int g2 = 0; g2 < G; ++g2) {
-    braw(g2, br0[g2]);
-    bprep(br0[g2], bcur[g2]);
-  }
-  if (n_groups > 1) {
-    aload(1, ar1);
-#pragma unroll
-    for (int g2 = 0; g2 < G; ++g2) braw(G + g2, br1[g2]);
-  }
-  __syncthreads();
-  auto step = [&](int cg, f32x4v (&rl)[G][AQ], BRaw (&bl2)[G], f32x4v (&rs)[G][AQ],
-                  BRaw (&bs)[G]) {
-    if (cg + 2 < n_groups) {
-      aload(cg + 2, rl);
-#pragma unroll
-      for (int g2 = 0; g2 < G; ++g2) braw((cg + 2) * G + g2, bl2[g2]);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    compute(cg & 1, bcur);
-    __builtin_amdgcn_sched_barrier(0);
-    const bool more = cg + 1 < n_groups;
-    if (more) astore((cg + 1) & 1, rs);
-    __syncthreads();
-    if (more) {
-#pragma unroll
-      for (int g2 = 0; g2 < G; ++g2) bprep(bs[g2], bcur[g2]);
-    }
-  };
-  for (int cg = 0; cg < n_groups; cg += 2) {
-    step(cg, ar0, br0, ar1, br1);
-    if (cg + 1 < n_groups) step(cg + 1, ar1, br1, ar0, br0);
-  }
-#else
   f32x4v ar[G][AQ];
   aload(0, ar);
   astore(0, ar);
@@ -419,7 +310,6 @@ __global__ void __launch_bounds__(64 * NW) pwg_cnet_conv_kernel(const CnConvArgs
       for (int g2 = 0; g2 < G; ++g2) bprep(bnext[g2], bcur[g2]);
     }
   }
-#endif
 
   // epilogue
   const int2 sd = *reinterpret_cast<const int2*>(a.seg_dst + 2 * u);
@@ -508,19 +398,15 @@ __host__ __device__ constexpr bool xtile_supported(int k) { return k == 3 || k =
 constexpr int XT_COLS = 256;
 constexpr int XT_ROWB = 80;  // bytes per staged input row: 16 hi + 16 lo halves + 16 B pad
 
-// small shapes (MT 1, K <= 3, one block per step: ConvTranspose phases, 32-channel convs):
-// occupancy is set by VGPRs, PWG_CNET_XT_WPE waves per SIMD requested (0: compiler's choice)
 // SY (synchronous staging): no register prefetch of the next channel block; the kernel is held to
 // 128 VGPRs (4 waves per SIMD) so two workgroups share a CU and one's staging overlaps the other's
-// MFMAs (PWG_CNET_XT_SYNC). Same arithmetic and order: bit-identical.
+// MFMAs. Same arithmetic and order: bit-identical.
 template <int MT, int K, int CB, bool SY = false>
 constexpr int xt_wpe() {
-  return SY ? 4 : (PWG_CNET_XT_WPE > 0 && MT == 1 && K <= 3 && CB == 1) ? PWG_CNET_XT_WPE : 1;
+  return SY ? 4 : 1;
 }
-// NC column tiles of 256 per workgroup (wave w: columns 256 nc + 32 w + [0, 32)): the staged A
-// fragments of a channel block serve NC x 256 columns, so NC = 2 halves the L2 -> LDS weight bytes
-// per column (PWG_CNET_XT_NC2). Every accumulator sums the same products in the same order as
-// with NC = 1: bit-identical.
+// NC column tiles of 256 per workgroup (wave w: columns 256 nc + 32 w + [0, 32)); the engine runs
+// NC = 1 (NC = 2 measured no faster, profiles/r02_nc).
 // KS (SY only): taps whose A fragments are staged per step; KS < K stages a channel block's taps in
 // ceil(K / KS) steps (same MFMA order) so the A region fits two workgroups per CU (k = 11, MT 4).
 template <int MT, int K, int CB, int NC = 1, bool SY = false, int KS = K>
@@ -811,7 +697,7 @@ template <int MT>
 hipError_t xtile_launch_sync(int k, int ks, dim3 grid, int lds, hipStream_t s, const CnConvArgs& a,
                              const CnXtileArgs& xt) {
   if (ks != k) {  // tap-split staging: k = 11 in steps of 6 taps
-    if constexpr (PWG_CNET_XT_TSPLIT != 0 && MT == 4)
+    if constexpr (MT == 4)
       if (k == 11 && ks == 6) return xtile_launch_k<MT, 11, 1, 1, true, 6>(grid, lds, s, a, xt);
     return hipErrorInvalidValue;
   }
@@ -820,16 +706,6 @@ hipError_t xtile_launch_sync(int k, int ks, dim3 grid, int lds, hipStream_t s, c
     case 5: return xtile_launch_k<MT, 5, 1, 1, true>(grid, lds, s, a, xt);
     case 7: return xtile_launch_k<MT, 7, 1, 1, true>(grid, lds, s, a, xt);
     case 11: return xtile_launch_k<MT, 11, 1, 1, true>(grid, lds, s, a, xt);
-    default: return hipErrorInvalidValue;
-  }
-}
-template <int MT>
-hipError_t xtile_launch_nc2(int k, dim3 grid, int lds, hipStream_t s, const CnConvArgs& a, const CnXtileArgs& xt) {
-  switch (k) {
-    case 3: return xtile_launch_k<MT, 3, 1, 2>(grid, lds, s, a, xt);
-    case 5: return xtile_launch_k<MT, 5, 1, 2>(grid, lds, s, a, xt);
-    case 7: return xtile_launch_k<MT, 7, 1, 2>(grid, lds, s, a, xt);
-    case 11: return xtile_launch_k<MT, 11, 1, 2>(grid, lds, s, a, xt);
     default: return hipErrorInvalidValue;
   }
 }
@@ -844,38 +720,16 @@ hipError_t xtile_launch_mt(int k, dim3 grid, int lds, hipStream_t s, const CnCon
     default: return hipErrorInvalidValue;
   }
 }
-hipError_t xtile_launch(int mt, int k, int cb, int nc, bool sync, int ks, dim3 grid, int lds, hipStream_t s,
-                        const CnConvArgs& a, const CnXtileArgs& xt) {
+hipError_t xtile_launch(int mt, int k, bool sync, int ks, dim3 grid, int lds, hipStream_t s, const CnConvArgs& a,
+                        const CnXtileArgs& xt) {
   if (sync) {
-    if constexpr (PWG_CNET_XT_SYNC != 0) {  // instantiated only when the option is built in
-      if (cb != 1 || nc != 1) return hipErrorInvalidValue;
-      switch (mt) {
-        case 2: return xtile_launch_sync<2>(k, ks, grid, lds, s, a, xt);
-        case 3: return xtile_launch_sync<3>(k, ks, grid, lds, s, a, xt);
-        case 4: return xtile_launch_sync<4>(k, ks, grid, lds, s, a, xt);
-        default: return hipErrorInvalidValue;
-      }
+    switch (mt) {
+      case 2: return xtile_launch_sync<2>(k, ks, grid, lds, s, a, xt);
+      case 3: return xtile_launch_sync<3>(k, ks, grid, lds, s, a, xt);
+      case 4: return xtile_launch_sync<4>(k, ks, grid, lds, s, a, xt);
+      default: return hipErrorInvalidValue;
     }
-    return hipErrorInvalidValue;
   }
-  if (nc == 2) {
-    if constexpr (PWG_CNET_XT_NC2 != 0) {  // instantiated only in A/B builds
-      if (cb != 1) return hipErrorInvalidValue;
-      switch (mt) {
-        case 1: return xtile_launch_nc2<1>(k, grid, lds, s, a, xt);
-        case 2: return xtile_launch_nc2<2>(k, grid, lds, s, a, xt);
-        case 3: return xtile_launch_nc2<3>(k, grid, lds, s, a, xt);
-        case 4: return xtile_launch_nc2<4>(k, grid, lds, s, a, xt);
-        default: return hipErrorInvalidValue;
-      }
-    }
-    return hipErrorInvalidValue;
-  }
-  if (nc != 1) return hipErrorInvalidValue;
-  if (cb == 4 && mt == 1) return xtile_launch_mt<1, 4>(k, grid, lds, s, a, xt);
-  if (cb == 2 && mt == 2) return xtile_launch_mt<2, 2>(k, grid, lds, s, a, xt);
-  if (cb == 2 && mt == 4) return xtile_launch_mt<4, 2>(k, grid, lds, s, a, xt);
-  if (cb != 1) return hipErrorInvalidValue;
   switch (mt) {
     case 1: return xtile_launch_mt<1, 1>(k, grid, lds, s, a, xt);
     case 2: return xtile_launch_mt<2, 1>(k, grid, lds, s, a, xt);
@@ -920,8 +774,8 @@ __global__ void __launch_bounds__(512) pwg_cnet_xpair_kernel(const CnConvArgs a,
   extern __shared__ __attribute__((aligned(16))) unsigned char xp_smem[];
   f32x4v* s_a = reinterpret_cast<f32x4v*>(xp_smem);                                   // A of one block
   unsigned char* s_x = xp_smem + (size_t)(K1 > K2 ? K1 : K2) * MT * 2048;              // [span1][80 B]
-  // [256][HROWB]: after stage 1 (PWG_CNET_XPAIR_OVERLAP: over the input rows, dead by then)
-  unsigned char* s_h = PWG_CNET_XPAIR_OVERLAP ? s_x : s_x + (size_t)(XT_COLS + 192) * XT_ROWB;
+  // [256][HROWB]: after stage 1, over the input rows (dead by then)
+  unsigned char* s_h = s_x;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int hh = lane >> 5;
@@ -1174,16 +1028,12 @@ hipError_t xpair_launch_mt(int k, dim3 grid, int lds, hipStream_t s, const CnCon
 hipError_t xpair_launch(int mt, int k, dim3 grid, int lds, hipStream_t s, const CnConvArgs& a, const CnXpairArgs& xp) {
   if (mt == 1) return xpair_launch_mt<1>(k, grid, lds, s, a, xp);
   if (mt == 2) return xpair_launch_mt<2>(k, grid, lds, s, a, xp);
-#if PWG_CNET_XPAIR_C128
   // 128 channels: only k = 3 fits (A of one block 24 KB + the h tile 256 x 528 B = 159.7 KB)
   if (mt == 4 && k == 3) return xpair_launch_k<4, 3, 3>(grid, lds, s, a, xp);
-#endif
   return hipErrorInvalidValue;
 }
 __host__ __device__ constexpr int xpair_lds(int mt, int k, int span1) {
-  return PWG_CNET_XPAIR_OVERLAP
-             ? k * mt * 2048 + (span1 * XT_ROWB > 256 * (4 * 32 * mt + 16) ? span1 * XT_ROWB : 256 * (4 * 32 * mt + 16))
-             : (k * mt * 2048) + (XT_COLS + 192) * XT_ROWB + 256 * (4 * 32 * mt + 16);
+  return k * mt * 2048 + (span1 * XT_ROWB > 256 * (4 * 32 * mt + 16) ? span1 * XT_ROWB : 256 * (4 * 32 * mt + 16));
 }
 
 // Fused MelGAN ResidualStack (split-f16 mode; layers/residual_stack.py:75-85 stack(c) + skip_layer(c)):
@@ -1753,22 +1603,12 @@ hipError_t xstack_launch(int mt, int k, dim3 grid, int lds, hipStream_t s, const
 //     chunk ahead, stage-2 B rows from LDS.
 // The arithmetic (chunk order, pair split, fp32 accumulate, epilogue order) is the unfused ops'
 // exactly, so the fused result is bit-identical to running op A then op B in split mode.
-#ifndef PWG_STACK_MAX_MT
-#define PWG_STACK_MAX_MT 3  // ResidualStack fusion up to 3 m-tiles (96 channels); 7 = every shape (A/B)
-#endif
+constexpr int CNET_STACK_MAX_MT = 3;  // ResidualStack fusion up to 3 m-tiles (96 channels; 192: slower)
 constexpr int PR_HALO = 16;
 constexpr int PR_MAX_XS = 128 + 2 * 64;        // x tile columns (stage-1 tap reach +-64 - PR_HALO)
 constexpr int PR_XQ = PR_MAX_XS * 8 / 256;     // 16-byte x quads per thread
 constexpr int PR_MAX_LDS = 160 * 1024;
-#ifndef PWG_PAIR_STREAM_C
-#define PWG_PAIR_STREAM_C 64  // channels of the streamed-weight pair kernel (0: off)
-#endif
-#ifndef PWG_PAIR_STREAM128
-#define PWG_PAIR_STREAM128 0  // 1: 128-channel pairs on the streamed kernel, 64-column steps (A/B: slower)
-#endif
-#ifndef PWG_PAIR_RESIDENT32
-#define PWG_PAIR_RESIDENT32 1  // 0: 32-channel pairs use the streamed kernel too (A/B)
-#endif
+constexpr int CNET_PAIR_STREAM_C = 64;  // channels of the streamed-weight pair kernel (x-tile off)
 struct CnPairArgs {
   const float* x;
   const int* seg_x;
@@ -2425,8 +2265,6 @@ struct OpPhase {          // one launch
   int NW = 4;             // waves per workgroup of pwg_cnet_conv_kernel
   bool xtile = false;     // split mode runs pwg_cnet_xtile_kernel (channel-block-major, staged input tile)
   int xt_lds = 0;
-  int xt_cb = 1;          // its 16-channel blocks per staging step
-  int xt_nc = 1;          // its 256-column tiles per workgroup (2: 512-column blocks in d_xblocks)
   bool xt_sync = false;   // synchronous staging at 128 VGPRs (two workgroups per CU)
   int xt_ks = 0;          // with xt_sync: taps staged per step (the kernel size unless split)
   int z_phases = 1;       // CONVT phase 0: phases launched together (gridDim.z); others: 0 (merged)
@@ -2634,7 +2472,7 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
     // staging, more workgroups in flight): HiFiGAN v1's 256-channel k = 3 / 7 convs -10 / -12 %;
     // slower at k = 11 and at 128 rows (profiles/r02_mt2)
     if (op.kind == PWG_CNET_CONV && op.src[1].buf < 0 && MT == 4 && mt_total0 >= 8 &&
-        op.src[0].taps <= PWG_CNET_XT_MT2_MAXK)
+        op.src[0].taps <= CNET_XT_MT2_MAXK)
       MT = 2;
     const int mt_total = (mt_total0 + MT - 1) / MT * MT;
     int n_phase = 1;
@@ -2670,34 +2508,21 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
     for (int r = 0; r < n_phase; ++r) {
       OpPhase ph;
       ph.op = oi; ph.phase = r; ph.MT = MT; ph.mt_total = mt_total;
-      ph.NT = 1;  // NT 2/4 for thin row tiles measured SLOWER (fewer workgroups in flight)
-      // 8 waves (256 columns) share each staged A chunk of the wide ops (A/B: PWG_CNET_NW8_MT)
-      if (PWG_CNET_NW8_MT > 0 && MT >= PWG_CNET_NW8_MT && op.kind == PWG_CNET_CONV) ph.NW = 8;
+      // 8 waves (256 columns) share each staged A chunk of the wide ops
+      if (MT >= CNET_NW8_MT && op.kind == PWG_CNET_CONV) ph.NW = 8;
       // wide dilated single-source convs: the staged-input-tile kernel (split mode)
-      // (ConvTranspose phases: 2 taps of dilation 1, PWG_CNET_XTILE_CONVT)
+      // (ConvTranspose phases: 2 taps of dilation 1, CNET_XTILE_CONVT)
       const bool convt = op.kind == PWG_CNET_CONVT;
       const int xk = convt ? 2 : op.src[0].taps, xd = convt ? 1 : op.src[0].dilation;
-      if (PWG_CNET_XTILE && (op.kind == PWG_CNET_CONV || (convt && mt_total <= PWG_CNET_XTILE_CONVT)) && nsrc == 1 &&
-          MT >= PWG_CNET_XTILE_MINMT && (MT == 1 || MT == 2 || MT == 3 || MT == 4) && mt_total % MT == 0 &&
+      if ((op.kind == PWG_CNET_CONV || (convt && mt_total <= CNET_XTILE_CONVT)) && nsrc == 1 &&
+          (MT == 1 || MT == 2 || MT == 3 || MT == 4) && mt_total % MT == 0 &&
           (convt || xtile_supported(xk)) && (xk - 1) * xd <= 191 && op.src[0].channels % 16 == 0) {
         ph.xtile = true;
         ph.NW = 8;  // 256-column blocks
-        // channel blocks staged per barrier pair: the most of {4 (MT 1), 2 (MT 2, 4)} that divides the
-        // source's blocks and fits LDS next to the A fragments
-        const int cs = op.src[0].channels / 16;
+        // one 16-channel block per staging step (2 or 4 measured 1 % slower, r02_xt5)
         const int span = XT_COLS + (xk - 1) * xd;
-        auto lds_of = [&](int cb) { return cb * (xk * MT * 2048 + span * XT_ROWB); };
-        ph.xt_cb = 1;
-        for (int cb : {4, 2})
-          if (((cb == 4 && MT == 1) || (cb == 2 && MT >= 2)) && cs % cb == 0 && lds_of(cb) <= PWG_CNET_XTILE_LDS &&
-              cb * span * 4 <= cb * (XT_COLS + 192) * 4 && PWG_CNET_XTILE_CB >= cb &&
-              xk <= PWG_CNET_XTILE_CB_MAXK && (!convt || cb <= PWG_CNET_XTILE_CONVT_CB)) {
-            ph.xt_cb = cb;
-            break;
-          }
-        ph.xt_lds = lds_of(ph.xt_cb);
+        ph.xt_lds = xk * MT * 2048 + span * XT_ROWB;
       }
-      if (PWG_CNET_NT2_MT > 0 && MT >= PWG_CNET_NT2_MT && op.kind == PWG_CNET_CONV) ph.NT = 2;  // A/B
       ph.ostride = op.kind == PWG_CNET_CONVT ? op.stride : 1;
       ph.ophase = r;
       if (op.kind == PWG_CNET_CONVT) {
@@ -2754,7 +2579,7 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
   for (size_t i = 0; i < n->phases.size(); ++i) {
     OpPhase& ph = n->phases[i];
     const PwgCnetOp& op = n->ops[ph.op];
-    if (op.kind != PWG_CNET_CONVT || ph.phase != 0 || !PWG_CNET_CONVT_ONE_LAUNCH) continue;
+    if (op.kind != PWG_CNET_CONVT || ph.phase != 0) continue;
     const int s2 = op.stride;
     bool ok = s2 <= 8 && i + s2 <= n->phases.size() && !ph.thin && !ph.xtile;
     for (int r = 1; ok && r < s2; ++r) {
@@ -2776,16 +2601,16 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
     const PwgCnetOp& A = n->ops[pa.op];
     const PwgCnetOp& B = n->ops[pb.op];
     const int C = A.out_channels;
-    if (PWG_PAIR_OFF || A.kind != PWG_CNET_CONV || B.kind != PWG_CNET_CONV || pa.thin || pb.thin) continue;
+    if (A.kind != PWG_CNET_CONV || B.kind != PWG_CNET_CONV || pa.thin || pb.thin) continue;
     if (A.src[1].buf >= 0 || B.src[1].buf >= 0 || B.src[0].buf != A.dst) continue;
     if (A.res >= 0 || A.accumulate || A.out_div != 1.f || A.post_act != PWG_ACT_NONE) continue;
     if (A.src[0].pad_mode != PWG_PAD_ZERO || A.src[0].normalize || B.src[0].pad_mode != PWG_PAD_ZERO) continue;
     // 32 channels: both convs' weights resident in LDS; 64: weights streamed in PR_SG-chunk groups
-    if ((C != 32 && C != PWG_PAIR_STREAM_C && !(C == 128 && PWG_PAIR_STREAM128)) || A.src[0].channels != C ||
+    if ((C != 32 && C != CNET_PAIR_STREAM_C) || A.src[0].channels != C ||
         n->ld[A.src[0].buf] != C || B.out_channels != C || B.src[0].channels != C || n->ld[A.dst] != C)
       continue;
     const int MT = C / 32, cs = C / 16;
-    const bool resident = C == 32 && PWG_PAIR_RESIDENT32;
+    const bool resident = C == 32;
     const int step = C == 128 ? 64 : 128, sg = C == 128 ? 2 : PR_SG;  // streamed kernel geometry
     if (pa.mt_total != MT || pb.mt_total != MT || pa.MT != MT || pb.MT != MT) continue;
     bool ok = true;
@@ -2839,7 +2664,7 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
     // the fused kernel covers every row in one workgroup: measured faster than the two ops up to
     // 96 channels (MB-MelGAN v2: 48 ch 0.49 -> 0.31 ms, 96 ch 0.535 -> 0.50 ms per stack) and
     // slower at 192 (0.43 -> 0.61 ms: one 126 KB-LDS workgroup per CU), profiles/r02_stack
-    if (pa.mt_total != pb.mt_total || pa.mt_total > PWG_STACK_MAX_MT) continue;
+    if (pa.mt_total != pb.mt_total || pa.mt_total > CNET_STACK_MAX_MT) continue;
     if (B.dst != n_bufs - 1 && n->ld[B.dst] % 4 != 0) continue;
     bool ok = true;
     for (int k = 0; k < n_ops && ok; ++k) {
@@ -2854,7 +2679,7 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
     pa.NW = 4;  // the tap-major stack kernel's 128-column blocks (d_blocks)
     // x-tile on: the stack on the x-tile scheme (k = 3, all rows in one tile, h tile + staging in LDS);
     // op A unfused runs the x-tile kernel over the same 256-column blocks (d_xblocks)
-    if (pa.xtile && PWG_CNET_XSTACK && A.src[0].taps == 3 && pa.MT == pa.mt_total) {
+    if (pa.xtile && A.src[0].taps == 3 && pa.MT == pa.mt_total) {
       // LDS = A region (stage 1: all taps of one block; stage 2: g2 chunks) + max(input rows, h
       // tile); g2 = the largest divisor of op B's chunks that keeps the smallest layout's
       // occupancy (two workgroups per CU when it fits 80 KB)
@@ -2862,7 +2687,7 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
       const int region = std::max(span * XT_ROWB, 256 * (4 * n->ld[A.dst] + 16));
       const int a1 = 3 * pa.MT * 2048;
       const int n2 = (int)pb.chunks.size();
-      const int budget = PWG_CNET_XSTACK_OCC2 && a1 + region <= PR_MAX_LDS / 2 ? PR_MAX_LDS / 2 : PR_MAX_LDS;
+      const int budget = a1 + region <= PR_MAX_LDS / 2 ? PR_MAX_LDS / 2 : PR_MAX_LDS;
       int g2 = 0;
       for (int g = 1; g <= std::min(n2, XS_G2MAX); ++g)
         if (n2 % g == 0 && std::max(a1, g * pa.MT * 2048) + region <= budget) g2 = g;
@@ -2884,7 +2709,7 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
     const PwgCnetOp& A = n->ops[pa.op];
     const PwgCnetOp& B = n->ops[pb.op];
     const int C = A.out_channels;
-    const bool c128 = PWG_CNET_XPAIR_C128 && C == 128 && A.src[0].taps == 3;
+    const bool c128 = C == 128 && A.src[0].taps == 3;
     if ((C != 32 && C != 64 && !c128) || pa.MT != C / 32 || pa.mt_total != pa.MT || pb.MT != pa.MT || pb.mt_total != pb.MT) continue;
     if (A.src[1].buf >= 0 || B.src[1].buf >= 0 || B.src[0].buf != A.dst || A.src[0].channels != C ||
         B.src[0].channels != C || B.out_channels != C || n->ld[A.dst] != C || n->ld[A.src[0].buf] != C)
@@ -2893,7 +2718,7 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
     if (A.src[0].pad_mode != PWG_PAD_ZERO || B.src[0].pad_mode != PWG_PAD_ZERO || A.src[0].normalize) continue;
     const int K = A.src[0].taps;
     if (B.src[0].taps != K || B.src[0].dilation != 1 || -B.src[0].pad < -16 || -B.src[0].pad + K - 1 > 16) continue;
-    if ((K - 1) * A.src[0].dilation > 192 || K > PWG_CNET_XPAIR_MAXK) continue;
+    if ((K - 1) * A.src[0].dilation > 192 || K > CNET_XPAIR_MAXK) continue;
     if (B.dst != n_bufs - 1 && n->ld[B.dst] % 4 != 0) continue;
     bool ok = true;
     for (int k = 0; k < n_ops && ok; ++k) {
@@ -2902,31 +2727,16 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
       ok = o2.src[0].buf != A.dst && o2.src[1].buf != A.dst && o2.res != A.dst && o2.dst != A.dst;
     }
     const int lds = xpair_lds(pa.MT, K, XT_COLS + (K - 1) * A.src[0].dilation);
-    if (!ok || lds > PR_MAX_LDS || !PWG_CNET_XPAIR) continue;
+    if (!ok || lds > PR_MAX_LDS) continue;
     pa.xpair_b = (int)i + 1;
     pa.xpair_lds = lds;
-  }
-  // unfused x-tile convs: 512 columns per workgroup where the weights' L2 -> LDS staging is the
-  // larger share (the A fragments of a channel block then serve twice the columns)
-  for (size_t i = 0; i < n->phases.size(); ++i) {
-    OpPhase& ph = n->phases[i];
-    const PwgCnetOp& op = n->ops[ph.op];
-    if (!PWG_CNET_XT_NC2 || !ph.xtile || op.kind != PWG_CNET_CONV || ph.xt_cb != 1 || ph.stack_b >= 0 ||
-        ph.xpair_b >= 0 || (i > 0 && n->phases[i - 1].xpair_b == (int)i) || !xtile_supported(op.src[0].taps))
-      continue;
-    const int ext = (op.src[0].taps - 1) * op.src[0].dilation;
-    const int lds2 = op.src[0].taps * ph.MT * 2048 + (2 * XT_COLS + ext) * XT_ROWB;
-    if (lds2 > PWG_CNET_XTILE_LDS) continue;
-    if (PWG_CNET_XT_NC2 == 1 && 2 * ph.xt_lds <= 160 * 1024) continue;  // two workgroups per CU today
-    ph.xt_nc = 2;
-    ph.xt_lds = lds2;
   }
   // unfused x-tile convs whose prefetching kernel needs > 128 VGPRs (MT >= 3, or MT 2 at k = 11:
   // one workgroup per CU) but whose LDS fits two workgroups per CU: synchronous staging
   for (size_t i = 0; i < n->phases.size(); ++i) {
     OpPhase& ph = n->phases[i];
     const PwgCnetOp& op = n->ops[ph.op];
-    if (!PWG_CNET_XT_SYNC || !ph.xtile || op.kind != PWG_CNET_CONV || ph.xt_cb != 1 || ph.xt_nc != 1 ||
+    if (!ph.xtile || op.kind != PWG_CNET_CONV ||
         ph.stack_b >= 0 || ph.xpair_b >= 0 || (i > 0 && n->phases[i - 1].xpair_b == (int)i) ||
         !xtile_supported(op.src[0].taps))
       continue;
@@ -2936,7 +2746,7 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
     if (2 * ph.xt_lds <= 160 * 1024) {
       ph.xt_sync = true;
       ph.xt_ks = K;
-    } else if (PWG_CNET_XT_TSPLIT && ph.MT == 4 && K == 11 && 2 * (6 * 4 * 2048 + span * XT_ROWB) <= 160 * 1024) {
+    } else if (ph.MT == 4 && K == 11 && 2 * (6 * 4 * 2048 + span * XT_ROWB) <= 160 * 1024) {
       ph.xt_sync = true;
       ph.xt_ks = 6;
       ph.xt_lds = 6 * 4 * 2048 + span * XT_ROWB;
@@ -3147,8 +2957,8 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
     p->d_strips.push_back(dstr);
     p->n_strips.push_back((int)strips.size());
     std::vector<int2> xblocks;
-    if (ph.xpair_b >= 0 || (ph.stack_b >= 0 && ph.xtile) || ph.xt_nc == 2) {
-      const int step = ph.xpair_b >= 0 ? XP_OUT : ph.xt_nc * XT_COLS;
+    if (ph.xpair_b >= 0 || (ph.stack_b >= 0 && ph.xtile)) {
+      const int step = ph.xpair_b >= 0 ? XP_OUT : XT_COLS;
       for (int u = 0; u < n_utts; ++u)
         for (int q0 = 0; q0 < ncols[u]; q0 += step) xblocks.push_back(make_int2(u, q0));
     }
@@ -3202,11 +3012,13 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
   auto seg_of = [&](int b) -> const int* { return p->d_seg + (size_t)b * p->n_utts * 2; };
   const bool fuse = n->fuse_pairs && n->split_f16;
   const bool xt = n->xtile && n->split_f16;
-  // split-f16 range flag: zeroed per run, set by the launch that writes the program output
-  int* rflag = n->split_f16 ? (int*)((char*)workspace + p->ws_flag) : nullptr;
+  // split-f16 range flag: zeroed every run (exact-fp32 runs leave it clear), set by the launch that
+  // writes the program output
+  int* const flag_word = (int*)((char*)workspace + p->ws_flag);
+  int* rflag = n->split_f16 ? flag_word : nullptr;
   bool out_checked = false;
-  if (rflag) {
-    const hipError_t ez = hipMemsetAsync(rflag, 0, sizeof(int), s);
+  {
+    const hipError_t ez = hipMemsetAsync(flag_word, 0, sizeof(int), s);
     if (ez != hipSuccess) return hipf(ez, "range flag reset");
   }
   // a conv pair runs fused unless its convs run on the x-tile kernel (measured faster unfused)
@@ -3394,17 +3206,17 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         const bool convt = op.kind == PWG_CNET_CONVT;
         xt.K = convt ? 2 : op.src[0].taps; xt.dil = convt ? 1 : op.src[0].dilation;
         xt.off_min = convt ? ph.off_a - 1 : -op.src[0].pad;
-        xt.cs = op.src[0].channels / 16; xt.span = ph.xt_nc * XT_COLS + (xt.K - 1) * xt.dil;
+        xt.cs = op.src[0].channels / 16; xt.span = XT_COLS + (xt.K - 1) * xt.dil;
         xt.rev = convt ? 1 : 0;
         for (int r = 0; r < 8; ++r)
           xt.z_off[r] = convt && r < ph.z_phases ? n->phases[pi + r].off_a - 1 : xt.off_min;
         dim3 xgrid = grid;
-        // stack op A: 128-column d_blocks belong to the tap-major stack kernel; xt_nc 2: 512-column blocks
-        if (ph.stack_b >= 0 || ph.xt_nc == 2) {
+        // stack op A: 128-column d_blocks belong to the tap-major stack kernel
+        if (ph.stack_b >= 0) {
           a.blocks = p->d_xblocks[pi];
           xgrid.x = (unsigned)p->n_xblocks[pi];
         }
-        const hipError_t ea2 = xtile_launch(ph.MT, xt.K, ph.xt_cb, ph.xt_nc, ph.xt_sync, ph.xt_ks, xgrid, ph.xt_lds, s, a, xt);
+        const hipError_t ea2 = xtile_launch(ph.MT, xt.K, ph.xt_sync, ph.xt_ks, xgrid, ph.xt_lds, s, a, xt);
         if (ea2 != hipSuccess) return hipf(ea2, "xtile kernel launch");
       } else if (split) {
         switch (ph.MT) {
@@ -3421,8 +3233,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
             else hipLaunchKernelGGL((pwg_cnet_conv_kernel<3, 1, CN_G, true>), grid, block, 0, s, a);
             break;
           default:
-            if (ph.NT == 2) hipLaunchKernelGGL((pwg_cnet_conv_kernel<4, 2, CN_G, true>), grid, block, 0, s, a);
-            else if (ph.NW == 8)
+            if (ph.NW == 8)
               hipLaunchKernelGGL((pwg_cnet_conv_kernel<4, 1, CN_G, true, 8>), grid, dim3(512), 0, s, a);
             else hipLaunchKernelGGL((pwg_cnet_conv_kernel<4, 1, CN_G, true>), grid, block, 0, s, a);
             break;
@@ -3443,8 +3254,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
             else hipLaunchKernelGGL((pwg_cnet_conv_kernel<3, 1, CN_G>), grid, block, 0, s, a);
             break;
           default:
-            if (ph.NT == 2) hipLaunchKernelGGL((pwg_cnet_conv_kernel<4, 2, CN_G>), grid, block, 0, s, a);
-            else if (ph.NW == 8) hipLaunchKernelGGL((pwg_cnet_conv_kernel<4, 1, CN_G, false, 8>), grid, dim3(512), 0, s, a);
+            if (ph.NW == 8) hipLaunchKernelGGL((pwg_cnet_conv_kernel<4, 1, CN_G, false, 8>), grid, dim3(512), 0, s, a);
             else hipLaunchKernelGGL((pwg_cnet_conv_kernel<4, 1, CN_G>), grid, block, 0, s, a);
             break;
         }

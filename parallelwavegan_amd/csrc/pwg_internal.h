@@ -87,6 +87,7 @@ struct FirstConvArgs {
   const float* b;        // [R]
   float* x;              // [Tpad][RS] time-major
   float* x1;             // the other residual buffer
+  float* x2;             // split16 layer pipeline: the third residual plane (gap tiles zeroed), or null
   const int* tile_utt;
   const UttDesc* utts;
   const long long* gap_col0;
@@ -188,15 +189,34 @@ struct SplitArgs {
   int out_stride_t, out_stride_o;
   float skip_scale;
   int* ctr;
-  unsigned long long* trace;  // PWG_TRACE builds only (tools/trace_layer.py)
+  unsigned long long* trace;  // per-wave timestamps when PWG_TRACE_FILE is set (tools/trace_layer.py), else null
   const float* noise;         // split16 layer 0 with first_conv fused (else null): caller noise
   const float* fw;            // first_conv weight [64] and bias [64]
   const float* fb;
   int* range_flag;            // last layer: set to 1 when a live column's final skip sum is not
                               // finite (fp16 pair range exceeded somewhere upstream; pwg_run_status)
+  int compute_waves;          // split16: waves per workgroup that take blocks (the rest only stage)
 };
 // dwords of one layer's split image (SplitSmem in pwg_split.hip without the head)
 constexpr int SPLIT_LAYER_DWORDS = 3 * 4 * 4 * 2 * 64 * 4 + 4 * 4 * 2 * 64 * 4 + 32 * 4 + 64;
+
+// Layer-pipelined split16 forward (pwg_split16.hip pwg_pipe_split16_kernel): all L layers in one
+// launch, each workgroup serving one layer with its weights resident, blocks handed from layer to
+// layer through per-block progress words. `base` holds the fields every layer shares (the layer's
+// weights, D rows, planes and dilation are derived per workgroup).
+constexpr int PIPE_MAX_LAYERS = 64;
+struct PipeArgs {
+  SplitArgs base;            // noise non-null: layer 0 builds x0 from the noise (fused first_conv)
+  const unsigned* wg0;       // layer 0's split16 LDS image; layer l's at wg0 + l * wg_stride (dwords)
+  long long wg_stride;
+  const unsigned* d0;        // layer 0's D rows; layer l's at d0 + l * d_stride (dwords)
+  long long d_stride;
+  unsigned* x[3];            // residual planes: layer l reads x[l % 3], writes x[(l + 1) % 3]
+  int* prog;                 // [n_blocks] layers finished per block (zeroed per run)
+  int* ctr;                  // layer l's block queue head at ctr[l * SCHED_CTR_STRIDE * 8] (zeroed per run)
+  int L;
+  int dil[PIPE_MAX_LAYERS];
+};
 
 // Persistent-kernel work queues: one head per XCD, each on its own 128-byte line.
 constexpr int SCHED_CTR_STRIDE = 32;
@@ -221,6 +241,7 @@ struct PlanDescArgs {
   BlockDesc* blocks;
   int* zero;      // first chunk only: the run's work-queue heads + range flag, zeroed here
   int n_zero;
+  int* prog;      // layer pipeline: per-block progress words, zeroed with the block descriptors (or null)
 };
 hipError_t launch_plan_desc(const PlanDescArgs& a, long long max_blocks, hipStream_t s);
 
@@ -234,6 +255,7 @@ hipError_t launch_layer_split16(const SplitArgs& a, bool last, int tap_center, i
                                 hipStream_t s);
 hipError_t launch_layer_split(const SplitArgs& a, bool last, int tap_center, int waves_per_wg, int n_wg,
                               hipStream_t s);
+hipError_t launch_pipe_split16(const PipeArgs& p, int tap_center, int n_wg, hipStream_t s);
 hipError_t launch_layer_persistent(const PersistArgs& a, int mt, int m2t, bool last, int waves_per_wg, int n_wg,
                                    hipStream_t s);
 

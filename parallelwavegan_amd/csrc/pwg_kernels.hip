@@ -110,12 +110,19 @@ __global__ void __launch_bounds__(256) pwg_conv_in_kernel(const ConvInArgs a) {
 // the (replication-padded, normalized) input channel i at frame f + kk. M = A rows (MT m-tiles),
 // N = 32 frames per wave, K = A*KW in k-steps of 2 (lane half h takes k = 2s + h). The B operand
 // is one input value per lane and k-step (L1-resident: the mel tile is 5 frames wide).
+// conv_in with K split over the workgroup's 4 waves (the B = 1 latency path's first kernel): grid
+// (ceil(F_total / 32), MT), wave w sums k-steps [w Q, (w + 1) Q) of m-tile blockIdx.y for 32 frames
+// (lane layout above), loads double-buffered in groups of 8, the four
+// partial tiles summed through LDS in wave order. One wave per (32 frames, all of K, all m-tiles)
+// made a 64-frame utterance ONE chain of 200 k-steps x 3 MFMAs behind 25 load waits: 94 us.
 template <int MT>
-__global__ void __launch_bounds__(256) pwg_conv_in_mfma_kernel(const ConvInArgs a) {
+__global__ void __launch_bounds__(256) pwg_conv_in_ksplit_kernel(const ConvInArgs a) {
+  __shared__ float s_red[4][16][64];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int hh = lane >> 5, cl = lane & 31;
-  const long long g0 = (long long)blockIdx.x * 128 + wave * 32 + cl;
+  const int m = blockIdx.y;
+  const long long g0 = (long long)blockIdx.x * 32 + cl;
   const bool valid = g0 < a.F_total;
   const long long g = valid ? g0 : a.F_total - 1;
   const int u = find_utt_by_frame(a.utts, a.n_utts, g);
@@ -125,22 +132,17 @@ __global__ void __launch_bounds__(256) pwg_conv_in_mfma_kernel(const ConvInArgs 
   const long long Tin = Tf + 2 * a.ctx;
   const int K = a.A * a.KW;
   const int nks = (K + 1) / 2;
-  f32x16 acc[MT];
-#pragma unroll
-  for (int m = 0; m < MT; ++m)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
-  int i = hh / a.KW, kk = hh - i * a.KW;  // k = 2s + hh = i*KW + kk
+  const int Q = (nks + 3) / 4;
+  const int s_begin = wave * Q, s_end = min(nks, s_begin + Q);
   const float* wl = a.wfrag + lane;
-  // groups of 8 k-steps: every input and weight load of a group is issued before its MFMAs (one
-  // load at a time made a small plan a chain of ~200 dependent L2 round trips: 90 us at T' = 64)
-  for (int s0 = 0; s0 < nks; s0 += 8) {
-    float x[8], w[8][MT];
+  auto load = [&](int s0, float (&x)[8], float (&w)[8]) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int s = s0 + j;
+      const int k = 2 * s + hh;
+      const int i = k / a.KW, kk = k - i * a.KW;
       x[j] = 0.f;
-      if (s < nks && i < a.A) {
+      if (s < s_end && i < a.A) {
         const long long fp = f + kk;
         if (a.layout == PWG_LAYOUT_INFERENCE) {
           long long src = fp - a.ctx;
@@ -151,24 +153,34 @@ __global__ void __launch_bounds__(256) pwg_conv_in_mfma_kernel(const ConvInArgs 
           x[j] = a.mel[ud.mel_off + (long long)i * Tin + fp];
         }
       }
-#pragma unroll
-      for (int m = 0; m < MT; ++m) w[j][m] = s < nks ? wl[(s * MT + m) * 64] : 0.f;
-      kk += 2;
-      while (kk >= a.KW) { kk -= a.KW; ++i; }
+      w[j] = s < s_end ? wl[(s * MT + m) * 64] : 0.f;
     }
+  };
+  f32x16 acc;
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  float xa[8], wa[8], xb[8], wb[8];
+  load(s_begin, xa, wa);
+  for (int s0 = s_begin; s0 < s_end; s0 += 16) {
+    load(s0 + 8, xb, wb);  // in flight during group s0's MFMAs
 #pragma unroll
-      for (int m = 0; m < MT; ++m) acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(w[j][m], x[j], acc[m], 0, 0, 0);
+    for (int j = 0; j < 8; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[j], xa[j], acc, 0, 0, 0);
+    load(s0 + 16, xa, wa);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wb[j], xb[j], acc, 0, 0, 0);
   }
-  if (!valid) return;
 #pragma unroll
-  for (int m = 0; m < MT; ++m)
+  for (int r = 0; r < 16; ++r) s_red[wave][r][lane] = acc[r];
+  __syncthreads();
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int o = 32 * m + (r & 3) + 8 * (r >> 2) + 4 * hh;
-      if (o < a.A) a.c1[(size_t)o * a.F_total + g] = acc[m][r];
-    }
+  for (int j = 0; j < 4; ++j) {
+    const int v = threadIdx.x + 256 * j;
+    const int r = v >> 6, l = v & 63;
+    const float sum = ((s_red[0][r][l] + s_red[1][r][l]) + s_red[2][r][l]) + s_red[3][r][l];
+    const long long gg = (long long)blockIdx.x * 32 + (l & 31);
+    const int o = 32 * m + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
+    if (gg < a.F_total && o < a.A) a.c1[(size_t)o * a.F_total + gg] = sum;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1132,6 +1144,7 @@ __global__ void __launch_bounds__(256) pwg_plan_desc_kernel(const PlanDescArgs a
     b.utt = a.u0 + y;
     b.pad = 0;
     a.blocks[d.first_tile * (TILE / 32) + j] = b;
+    if (a.prog != nullptr) a.prog[d.first_tile * (TILE / 32) + j] = 0;
     if ((j & (TILE / 32 - 1)) == 0) a.tile_utt[d.first_tile + j / (TILE / 32)] = a.u0 + y;
   }
   if (j < a.gap_tiles) {
@@ -1155,12 +1168,13 @@ hipError_t launch_plan_desc(const PlanDescArgs& a, long long max_blocks, hipStre
 
 hipError_t launch_conv_in(const ConvInArgs& a, hipStream_t s) {
   if (a.use_conv_in && a.A <= 128) {
-    const dim3 grid((unsigned)((a.F_total + 127) / 128));
-    switch ((a.A + 31) / 32) {
-      case 1: hipLaunchKernelGGL(pwg_conv_in_mfma_kernel<1>, grid, dim3(256), 0, s, a); break;
-      case 2: hipLaunchKernelGGL(pwg_conv_in_mfma_kernel<2>, grid, dim3(256), 0, s, a); break;
-      case 3: hipLaunchKernelGGL(pwg_conv_in_mfma_kernel<3>, grid, dim3(256), 0, s, a); break;
-      default: hipLaunchKernelGGL(pwg_conv_in_mfma_kernel<4>, grid, dim3(256), 0, s, a); break;
+    const int mt = (a.A + 31) / 32;
+    const dim3 grid((unsigned)((a.F_total + 31) / 32), (unsigned)mt);
+    switch (mt) {
+      case 1: hipLaunchKernelGGL(pwg_conv_in_ksplit_kernel<1>, grid, dim3(256), 0, s, a); break;
+      case 2: hipLaunchKernelGGL(pwg_conv_in_ksplit_kernel<2>, grid, dim3(256), 0, s, a); break;
+      case 3: hipLaunchKernelGGL(pwg_conv_in_ksplit_kernel<3>, grid, dim3(256), 0, s, a); break;
+      default: hipLaunchKernelGGL(pwg_conv_in_ksplit_kernel<4>, grid, dim3(256), 0, s, a); break;
     }
     return hipGetLastError();
   }

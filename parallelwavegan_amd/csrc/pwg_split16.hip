@@ -20,57 +20,6 @@
 // Reference: layers/residual_block.py:102-140, models/parallel_wavegan.py:131-138,160-171.
 #include "pwg_internal.h"
 
-#ifndef PWG_SPLIT16_EARLY_SKIP
-#define PWG_SPLIT16_EARLY_SKIP 0
-#endif
-// streams touched once per layer: non-temporal (PWG_SPLIT16_NT bit 0: stores, bit 1: skip loads)
-#ifndef PWG_SPLIT16_NT
-#define PWG_SPLIT16_NT 3
-#endif
-#if PWG_SPLIT16_NT & 1
-#define PWG16_ST(p, v) __builtin_nontemporal_store((v), (p))
-#else
-#define PWG16_ST(p, v) (*(p) = (v))
-#endif
-#if PWG_SPLIT16_NT & 2
-#define PWG16_LD_SKIP(p) __builtin_nontemporal_load(p)
-#else
-#define PWG16_LD_SKIP(p) (*(p))
-#endif
-// Write-through stores that drop the line from the XCD's L2 (buffer store, cache policy
-// PWG_SPLIT16_SC1_AUX = sc1): bit 0 the skip stream, bit 1 the x stream. Neither is re-read within
-// the layer, so keeping their lines in L2 only shortens the life of the x rows the dilated taps
-// re-read (rocprofv3: x reads fetch 1.65x their bytes, profiles/r02_pmc1).
-#ifndef PWG_SPLIT16_SC1
-#define PWG_SPLIT16_SC1 0
-#endif
-#ifndef PWG_SPLIT16_SC1_AUX
-#define PWG_SPLIT16_SC1_AUX 16
-#endif
-#ifndef PWG_SPLIT16_DIAG_NOTAP
-#define PWG_SPLIT16_DIAG_NOTAP 0
-#endif
-// Diagnostic only (wrong results): the x (bit 0) and/or skip (bit 1) streams are folded into a
-// per-XCD 2,048-column window that stays in the XCD's L2, i.e. the upper bound of what keeping those
-// streams on chip across layers (cross-layer fusion) could save with the layer's arithmetic unchanged.
-#ifndef PWG_SPLIT16_DIAG_L2
-#define PWG_SPLIT16_DIAG_L2 0
-#endif
-// Tap prefetch schedule. 0: tap 0 of block i+1 is loaded during block i's center-tap MFMAs, the
-// other and center taps of a block at its own start (half a GEMM-1 ahead of use). 1: all three taps
-// of block i+1 are in flight before block i's GEMM 2 (the "other" and center taps after the gate,
-// into the registers GEMM 1's B operands free), so they get GEMM 2 + the epilogue to arrive.
-// 2: as 1 with the other tap issued before the gate.
-#ifndef PWG_SPLIT16_PF
-#define PWG_SPLIT16_PF 0
-#endif
-#ifndef PWG_SPLIT16_DIAG_LDS
-#define PWG_SPLIT16_DIAG_LDS 0  // diagnostic (wrong results, needs PF > 0): taps share A fragments
-#endif
-#ifndef PWG_SPLIT16_MG
-#define PWG_SPLIT16_MG 4  // GEMM-1 m-tiles whose A fragments are read per group
-#endif
-
 namespace pwg {
 
 namespace {
@@ -164,26 +113,29 @@ __device__ __forceinline__ size_t row16(int c, int g) {
   return (size_t)(c >> 5) * 2048 + (size_t)((c >> 4) & 1) * 1024 + (size_t)g * 64 + (size_t)(c & 15) * 4;
 }
 
-// 16-byte store through a buffer resource based at the wave-uniform tile address `base`
-// (PWG_SPLIT16_SC1); byte offsets stay inside the 8 KB tile
-__device__ __forceinline__ void st16_policy(const void* base, unsigned byte_off, u32x4 v) {
+// byte offset of piece q of column c for lane group g (row16 in bytes)
+__device__ __forceinline__ unsigned row16_bytes(int c, int g) { return (unsigned)row16(c, g) * 4u; }
+
+// buffer resource over a wave-uniform base (num_records 2 GB: the pipelined path's planes are smaller)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc16(const void* base) {
   const unsigned long long b = (unsigned long long)base;
   const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b), hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
-  void* ub = (void*)(((unsigned long long)hi << 32) | lo);
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(ub, 0, 0x7fffffff, 0x00020000);
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, byte_off, 0, PWG_SPLIT16_SC1_AUX);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), 0, 0x7fffffff, 0x00020000);
 }
-
-// PWG_SPLIT16_DIAG_L2 column folding (identity in the product build)
-template <int BIT>
-__device__ __forceinline__ int diag_col(int col, int xcd) {
-  if constexpr ((PWG_SPLIT16_DIAG_L2 & BIT) != 0) return 512 + xcd * 2048 + (col & 2047);
-  return col;
+// sc1 (write-through / L1-bypassing) 16-byte accesses: the pipelined kernel's hand-off bytes
+// (cdna_hip_programming.md Guideline 16: every store and every load of a handed-off byte is sc1)
+constexpr int AUX_SC1 = 16;
+__device__ __forceinline__ u32x4 ld16_sc1(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX_SC1));
+}
+__device__ __forceinline__ void st16_sc1(__amdgpu_buffer_rsrc_t r, unsigned off, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, AUX_SC1);
 }
 
 // LDS image of one layer (dwords): GEMM-1 A fragments [tap 3][ks 2][m 8][hi/lo 2][lane 64][4]
 // | GEMM-2 [ks 2][m 8][hi/lo 2][lane 64][4] | gate bias pairs [m 8][c 16] | sqrt(.5) b_out [g 4][16]
-// | last layer: head W1 [ms 4][m3 4][lane 64][4] fp32 + b1 [g 4][16].
+// | last layer: head W1 [ms 4][m3 4][lane 64][4] fp32 + b1 [g 4][16]; layer 0 with the fused
+// first_conv: w[64] | b[64] after that.
 struct Split16Smem {
   static constexpr int WG = 3 * 2 * 8 * 2 * 64 * 4;
   static constexpr int W2 = 2 * 8 * 2 * 64 * 4;
@@ -195,38 +147,449 @@ struct Split16Smem {
 static_assert(Split16Smem::WG + Split16Smem::W2 + Split16Smem::BG + Split16Smem::BO == SPLIT_LAYER_DWORDS,
               "split16 layer image size");
 
-// FIRST (layer 0 with PWG_OPT_FUSE_FIRST_CONV): first_conv (models/parallel_wavegan.py:81,161,
-// x0 = w z + b, zero outside the utterance) is evaluated on the fly from the 4-byte noise while
-// the tap pieces are built, with the same fmaf and pair split as pwg_first_conv_split16_kernel
-// (bit-identical), so x0 is never written to or read from HBM. w, b sit in LDS after the image.
-template <bool LAST, int TC, bool FIRST>
-__global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitArgs a) {
-  constexpr int MG = PWG_SPLIT16_MG;
-  extern __shared__ __attribute__((aligned(16))) unsigned smem16[];
-  unsigned* s_wg = smem16;
-  unsigned* s_w2 = s_wg + Split16Smem::WG;
-  unsigned* s_bg = s_w2 + Split16Smem::W2;
-  float* s_bo = reinterpret_cast<float*>(s_bg + Split16Smem::BG);
-  float* s_hw1 = s_bo + Split16Smem::BO;
-  float* s_fwb = reinterpret_cast<float*>(smem16 + Split16Smem::dwords(LAST));  // FIRST: w[64] | b[64]
-  {
-    const int nthr = blockDim.x;
-    stage_lds(reinterpret_cast<u32x4*>(s_wg), reinterpret_cast<const u32x4*>(a.wg), SPLIT_LAYER_DWORDS / 4,
-              (int)threadIdx.x, nthr);
-    if (LAST)
-      stage_lds(reinterpret_cast<u32x4*>(s_hw1), reinterpret_cast<const u32x4*>(a.hw1), Split16Smem::HW1 / 4,
-                (int)threadIdx.x, nthr);
-    if (FIRST)
-      for (int i = threadIdx.x; i < 128; i += nthr) s_fwb[i] = i < 64 ? a.fw[i] : a.fb[i - 64];
-    __syncthreads();
+// Stage one layer's image (and the head / first_conv constants of its role) into LDS; every
+// thread of the workgroup calls it, a __syncthreads() follows.
+template <bool LAST, bool FIRST>
+__device__ __forceinline__ void s16_stage(const SplitArgs& a, unsigned* smem16) {
+  const int nthr = blockDim.x;
+  stage_lds(reinterpret_cast<u32x4*>(smem16), reinterpret_cast<const u32x4*>(a.wg), SPLIT_LAYER_DWORDS / 4,
+            (int)threadIdx.x, nthr);
+  if (LAST)
+    stage_lds(reinterpret_cast<u32x4*>(smem16 + SPLIT_LAYER_DWORDS), reinterpret_cast<const u32x4*>(a.hw1),
+              Split16Smem::HW1 / 4, (int)threadIdx.x, nthr);
+  if (FIRST) {
+    float* s_fwb = reinterpret_cast<float*>(smem16 + Split16Smem::dwords(LAST));
+    for (int i = threadIdx.x; i < 128; i += nthr) s_fwb[i] = i < 64 ? a.fw[i] : a.fb[i - 64];
   }
+}
 
+// A lane's tap row pieces of one block for both n-tiles: b[nt*4 + ks*2 + hl]. FIRST (layer 0 with
+// PWG_OPT_FUSE_FIRST_CONV): first_conv (models/parallel_wavegan.py:81,161, x0 = w z + b, zero
+// outside the utterance) is evaluated from the 4-byte noise with the same fmaf and pair split as
+// pwg_first_conv_split16_kernel (bit-identical), so x0 never touches HBM. PIPE: sc1 loads.
+template <int TC, bool FIRST, bool PIPE>
+__device__ __forceinline__ void s16_bload(const SplitArgs& a, const float* s_fwb, const BlockDesc& d, int tap,
+                                          u32x4 (&b)[8], int g, int c) {
+  if constexpr (FIRST) {
+    const f32x4* fw4 = reinterpret_cast<const f32x4*>(s_fwb) + g;
+    const f32x4* fb4 = reinterpret_cast<const f32x4*>(s_fwb + 64) + g;
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const int t = d.t0 + 16 * nt + c + (tap - TC) * a.dil;
+      const bool inside = t >= 0 && t < d.T;
+      const float z = a.noise[d.io_off + (t < 0 ? 0 : (t >= d.T ? d.T - 1 : t))];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        float v[8];
+#pragma unroll
+        for (int jh = 0; jh < 2; ++jh) {
+          const f32x4 w = fw4[4 * (2 * ks + jh)], bb = fb4[4 * (2 * ks + jh)];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[4 * jh + i] = inside ? fmaf(w[i], z, bb[i]) : 0.f;
+        }
+        split8x<0>(v, b[nt * 4 + ks * 2], b[nt * 4 + ks * 2 + 1]);
+      }
+    }
+  } else if constexpr (PIPE) {
+    const __amdgpu_buffer_rsrc_t r = rsrc16(a.x_in);
+    const int cc = d.col + (tap - TC) * a.dil;
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const unsigned off = row16_bytes(cc + 16 * nt + c, g);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) b[nt * 4 + q] = ld16_sc1(r, off + q * 1024u);
+    }
+  } else {
+    const int cc = d.col + (tap - TC) * a.dil;
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const u32x4* p = reinterpret_cast<const u32x4*>(a.x_in + row16(cc + 16 * nt + c, g));
+#pragma unroll
+      for (int q = 0; q < 4; ++q) b[nt * 4 + q] = p[q * 64];
+    }
+  }
+}
+
+// D rows of a block's aux window: lane group g covers window frames fw0 + 2g, fw0 + 2g + 1 of the
+// frame-rate aux projection, in the split16 layout [c 16][m 8] (pwg_aux_proj_kernel, split == 2).
+__device__ __forceinline__ void s16_load_dv(const SplitArgs& a, const BlockDesc& bd, unsigned (&dv)[2][8], int g,
+                                            int c) {
+  const int fw0 = bd.t0 / a.H - a.J1;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int f = fw0 + 2 * g + j;
+    const int fc = f < 0 ? 0 : (f >= bd.frames ? bd.frames - 1 : f);  // weight 0 there
+    const u32x4* drow = reinterpret_cast<const u32x4*>(a.d + (size_t)(bd.frame_base + fc) * 128 + 8 * c);
+    const u32x4 d0 = drow[0], d1 = drow[1];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      dv[j][m] = d0[m];
+      dv[j][m + 4] = d1[m];
+    }
+  }
+}
+
+// The old skip sum of a block as GEMM-2 seeds sk[ms][nt] (skip rows 16 ms + 4 g + i of column
+// bd.col + 16 nt + c). Layer 0: the sum of all layers' skip biases.
+template <bool PIPE>
+__device__ __forceinline__ void s16_load_skip(const SplitArgs& a, const BlockDesc& bd, f32x4 (&sk)[4][2], int g,
+                                              int c) {
+  [[maybe_unused]] __amdgpu_buffer_rsrc_t rs;
+  if constexpr (PIPE) rs = rsrc16(a.skip);
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int ms = 0; ms < 4; ++ms) {
+      if (a.first) {
+        sk[ms][nt] = reinterpret_cast<const f32x4*>(a.skip0 + 16 * g)[ms];
+      } else if constexpr (PIPE) {
+        sk[ms][nt] = __builtin_bit_cast(f32x4, ld16_sc1(rs, row16_bytes(bd.col + 16 * nt + c, g) + ms * 1024u));
+      } else {
+        const f32x4* sp = reinterpret_cast<const f32x4*>(a.skip + row16(bd.col + 16 * nt + c, g));
+        sk[ms][nt] = __builtin_nontemporal_load(sp + ms * 64);
+      }
+    }
+}
+
+// One 32-sample block of one WaveNet residual block (layers/residual_block.py:102-140) with the
+// skip accumulation (models/parallel_wavegan.py:163-165) and, on the LAST layer, the output head.
+// On entry b0 holds tap 0 of `bd`; the other taps, the D rows and the skip seeds load inside the
+// block one step ahead of use; with has_next, tap 0 of the next block `bdn` loads into b1 during
+// the center tap's MFMAs (the per-layer kernel's cross-block prefetch). `mid` runs once after
+// GEMM 1 (the caller issues its next work-queue claim there). PIPE: sc1 skip loads and sc1
+// stores of x and skip (hand-off bytes of the pipelined kernel).
+template <bool LAST, int TC, bool FIRST, bool PIPE, typename Mid>
+__device__ __forceinline__ void s16_block(const SplitArgs& a, const unsigned* smem16, const BlockDesc& bd,
+                                          const BlockDesc& bdn, bool has_next, u32x4 (&b0)[8], u32x4 (&b1)[8],
+                                          bool& nonfinite, Mid&& mid) {
+  const unsigned* s_wg = smem16;
+  const unsigned* s_w2 = s_wg + Split16Smem::WG;
+  const unsigned* s_bg = s_w2 + Split16Smem::W2;
+  const float* s_bo = reinterpret_cast<const float*>(s_bg + Split16Smem::BG);
+  const float* s_hw1 = s_bo + Split16Smem::BO;
+  const float* s_fwb = reinterpret_cast<const float*>(smem16 + Split16Smem::dwords(LAST));
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4;
   const int c = lane & 15;
-  const int nw = blockDim.x >> 6;
+  constexpr int T1 = TC == 1 ? 2 : 1;  // the non-center tap after tap 0
+  const bool full = bd.t0 + 32 <= bd.T;
+
+  // aux operands: K slots [Dh0 Dh1 Dl0 Dl1 Dh0 Dh1 bh bl] x [wh0 wh1 wh0 wh1 wl0 wl1 1 1] (bias in
+  // group 0 only); bw = the composite upsampler weights of the lane's two window frames
+  unsigned dv[2][8];  // [frame][m], loaded during GEMM 1
+  float bw[2][2];  // [nt][frame]
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int t = bd.t0 + 16 * nt + c;
+    const bool live = t < bd.T;
+    const int tc = live ? t : bd.T - 1;
+    int roff;
+    if (bd.frames < a.Fmin) roff = a.tab_small + (a.H * bd.frames * (bd.frames - 1) / 2 + tc) * AUX_J4;
+    else if (tc < a.TL) roff = a.tab_left + tc * AUX_J4;
+    else if (tc >= bd.T - a.TR) roff = a.tab_right + (bd.T - 1 - tc) * AUX_J4;
+    else roff = (tc % a.H) * AUX_J4;
+    const int shift = t / a.H - bd.t0 / a.H;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int idx = 2 * g + j - shift;
+      const bool ok = live && idx >= 0 && idx < AUX_J4;
+      const float w = a.tab[roff + (idx < 0 ? 0 : (idx >= AUX_J4 ? AUX_J4 - 1 : idx))];
+      bw[nt][j] = ok ? w : 0.f;
+    }
+  }
+  const u32x4* wgl = reinterpret_cast<const u32x4*>(s_wg) + lane;
+  auto mma_tap = [&](f32x4 (&acc)[8][2], const u32x4 (&b)[8], int tap) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int mh = 0; mh < 2; ++mh) {  // 4 m-tiles per group: their A fragments read ahead
+        u32x4 ah[4], al[4];
+#pragma unroll
+        for (int mm = 0; mm < 4; ++mm) {
+          const int m = 4 * mh + mm;
+          ah[mm] = wgl[(((tap * 2 + ks) * 8 + m) * 2) * 64];
+          al[mm] = wgl[(((tap * 2 + ks) * 8 + m) * 2 + 1) * 64];
+        }
+#pragma unroll
+        for (int mm = 0; mm < 4; ++mm)
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) {
+            f32x4& ac = acc[4 * mh + mm][nt];
+            ac = mma16(ah[mm], b[nt * 4 + ks * 2], ac);
+            ac = mma16(ah[mm], b[nt * 4 + ks * 2 + 1], ac);
+            ac = mma16(al[mm], b[nt * 4 + ks * 2], ac);
+          }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+
+  // ---- GEMM 1: taps 0, other, center (the center row becomes the GEMM-2 seeds at the end)
+  f32x4 acc[8][2];
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) acc[m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 acc2[8][2];
+  s16_bload<TC, FIRST, PIPE>(a, s_fwb, bd, T1, b1, g, c);
+  mma_tap(acc, b0, 0);
+  s16_load_dv(a, bd, dv, g, c);
+  s16_bload<TC, FIRST, PIPE>(a, s_fwb, bd, TC, b0, g, c);
+  mma_tap(acc, b1, T1);
+  if (has_next) s16_bload<TC, FIRST, PIPE>(a, s_fwb, bdn, 0, b1, g, c);  // the next block's
+  mma_tap(acc, b0, TC);
+  if (!LAST) {
+    // GEMM-2 out-row seeds sqrt(.5)(x + b_out) from the center tap: acc2[4 + 2ks + (j>>2)][nt][j&3]
+    const f32x4* bo_l = reinterpret_cast<const f32x4*>(s_bo + 16 * g);
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        float o[8];
+        seed8x(b0[nt * 4 + ks * 2], b0[nt * 4 + ks * 2 + 1], bo_l[2 * ks], bo_l[2 * ks + 1], 0.70710677f, o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc2[4 + 2 * ks + (j >> 2)][nt][j & 3] = o[j];
+      }
+  }
+  mid();
+
+  {
+    // skip seeds: old skip sum, in flight during the aux term and the gate
+    f32x4 sk[4][2];
+    s16_load_skip<PIPE>(a, bd, sk, g, c);
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int ms = 0; ms < 4; ++ms) acc2[ms][nt] = sk[ms][nt];
+  }
+
+  // ---- aux term + gate bias: one MFMA per (m, nt)
+  {
+    const Pair16 bias_one = split_pair16(g == 0 ? 1.f : 0.f, g == 0 ? 1.f : 0.f);
+    u32x4 bB[2];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const Pair16 w = split_pair16(bw[nt][0], bw[nt][1]);
+      bB[nt] = u32x4{w.hi, w.hi, w.lo, bias_one.hi};  // [wh0 wh1 | wh0 wh1 | wl0 wl1 | 1 1]
+    }
+    const unsigned* bgl = s_bg + c;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const unsigned bgp = g == 0 ? bgl[16 * m] : 0u;  // (bias hi | bias lo << 16)
+      const unsigned dh = __builtin_amdgcn_perm(dv[1][m], dv[0][m], 0x05040100u);
+      const unsigned dl = __builtin_amdgcn_perm(dv[1][m], dv[0][m], 0x07060302u);
+      const u32x4 aA = {dh, dl, dh, bgp};  // [Dh0 Dh1 | Dl0 Dl1 | Dh0 Dh1 | bh bl]
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) acc[m][nt] = mma16(aA, bB[nt], acc[m][nt]);
+    }
+  }
+
+  // ---- gate -> GEMM-2 B pairs: k-step ks element j = channel chan16(ks, g, j) = acc row
+  u32x4 gh[2][2], gl[2][2];  // [nt][ks]
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      float gv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int m = 2 * ks + (j >> 2), i = j & 3;
+        gv[j] = gate16(acc[m][nt][i], acc[m + 4][nt][i]);
+      }
+      split8x<0>(gv, gh[nt][ks], gl[nt][ks]);
+    }
+
+  // ---- GEMM 2: [skip; out] rows, 8 m-tiles (last layer: the 4 skip tiles)
+  constexpr int M2 = LAST ? 4 : 8;
+  const u32x4* w2l = reinterpret_cast<const u32x4*>(s_w2) + lane;
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int mh = 0; mh < M2 / 4; ++mh) {
+      u32x4 ah[4], al[4];
+#pragma unroll
+      for (int mm = 0; mm < 4; ++mm) {
+        ah[mm] = w2l[((ks * 8 + 4 * mh + mm) * 2) * 64];
+        al[mm] = w2l[((ks * 8 + 4 * mh + mm) * 2 + 1) * 64];
+      }
+#pragma unroll
+      for (int mm = 0; mm < 4; ++mm)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          f32x4& ac = acc2[4 * mh + mm][nt];
+          ac = mma16(ah[mm], gh[nt][ks], ac);
+          ac = mma16(ah[mm], gl[nt][ks], ac);
+          ac = mma16(al[mm], gh[nt][ks], ac);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+
+  if (!LAST) {
+    [[maybe_unused]] __amdgpu_buffer_rsrc_t rsk, rx;
+    if constexpr (PIPE) {
+      rsk = rsrc16(a.skip);
+      rx = rsrc16(a.x_out);
+    }
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const int col = bd.col + 16 * nt + c;
+      const bool live = bd.t0 + 16 * nt + c < bd.T;
+#pragma unroll
+      for (int ms = 0; ms < 4; ++ms) {
+        if constexpr (PIPE)
+          st16_sc1(rsk, row16_bytes(col, g) + ms * 1024u, __builtin_bit_cast(u32x4, acc2[ms][nt]));
+        else
+          __builtin_nontemporal_store(acc2[ms][nt], reinterpret_cast<f32x4*>(a.skip + row16(col, g)) + ms * 64);
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = acc2[4 + 2 * ks + (j >> 2)][nt][j & 3];
+        u32x4 vh, vl;
+        split8x<11>(v, vh, vl);  // inputs straight from the GEMM-2 MFMAs
+        if (!full) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            vh[k] = live ? vh[k] : 0u;
+            vl[k] = live ? vl[k] : 0u;
+          }
+        }
+        if constexpr (PIPE) {
+          st16_sc1(rx, row16_bytes(col, g) + (ks * 2) * 1024u, vh);
+          st16_sc1(rx, row16_bytes(col, g) + (ks * 2 + 1) * 1024u, vl);
+        } else {
+          u32x4* xp = reinterpret_cast<u32x4*>(a.x_out + row16(col, g));
+          __builtin_nontemporal_store(vh, xp + (ks * 2) * 64);
+          __builtin_nontemporal_store(vl, xp + (ks * 2 + 1) * 64);
+        }
+      }
+    }
+  } else {
+    // ---- fused output head (models/parallel_wavegan.py:131-138,166-171), split-f16 on
+    //      v_mfma_f32_16x16x32_f16 like the layer: h1 = W1h . relu(skip * sqrt(1/L)) + b1h with
+    //      k-step ks element j = skip row chan16(ks, g, j) = acc2[2ks + (j >> 2)][nt][j & 3]
+    //      (the W1h image is packed in that k order); then y = W2h . relu(h1) + b2h across the 4
+    //      lane groups. (The fp32 v_mfma_f32_16x16x4f32 head took 128 MFMAs of twice the cycles.)
+    const u32x4* hw1 = reinterpret_cast<const u32x4*>(s_hw1) + lane;
+    const f32x4* hb1 = reinterpret_cast<const f32x4*>(s_hw1 + 4 * 4 * 64 * 4 + 16 * g);
+    f32x4 acc3[4][2];
+#pragma unroll
+    for (int m3 = 0; m3 < 4; ++m3)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) acc3[m3][nt] = hb1[m3];
+    u32x4 sh[2][2], sl[2][2];  // [nt][ks]
+    // range check: an x, D or first_conv value beyond the fp16 pair range became (inf, -inf) and
+    // every later product NaN, which every skip sum downstream carries (the ReLU's fmaxf below
+    // would hide it), so the final skip sums cover every layer; and the scaled skip itself must
+    // fit the head's pair split
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      float sum = 0.f;
+#pragma unroll
+      for (int ms = 0; ms < 4; ++ms)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sum += acc2[ms][nt][i];
+      nonfinite |= bd.t0 + 16 * nt + c < bd.T && !__builtin_isfinite(sum);
+    }
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        float hv[8];
+        float hmax = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          hv[j] = fmaxf(acc2[2 * ks + (j >> 2)][nt][j & 3] * a.skip_scale, 0.f);
+          hmax = fmaxf(hmax, hv[j]);
+        }
+        nonfinite |= bd.t0 + 16 * nt + c < bd.T && hmax >= 65520.f;
+        split8x<0>(hv, sh[nt][ks], sl[nt][ks]);
+      }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int m3 = 0; m3 < 4; ++m3) {
+        const u32x4 ah = hw1[((ks * 4 + m3) * 2) * 64], al = hw1[((ks * 4 + m3) * 2 + 1) * 64];
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          acc3[m3][nt] = mma16(ah, sh[nt][ks], acc3[m3][nt]);
+          acc3[m3][nt] = mma16(ah, sl[nt][ks], acc3[m3][nt]);
+          acc3[m3][nt] = mma16(al, sh[nt][ks], acc3[m3][nt]);
+        }
+      }
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const int t = bd.t0 + 16 * nt + c;
+      const bool live = t < bd.T;
+      float* out = a.out + (size_t)bd.io_off * a.O + (size_t)t * a.out_stride_t;
+      for (int oc = 0; oc < a.O; ++oc) {
+        const f32x4* w = reinterpret_cast<const f32x4*>(a.hw2 + ((size_t)oc * 4 + g) * 16);
+        float part = 0.f;
+#pragma unroll
+        for (int m3 = 0; m3 < 4; ++m3) {
+          const f32x4 wq = w[m3];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) part = fmaf(wq[i], fmaxf(acc3[m3][nt][i], 0.f), part);
+        }
+        part += __shfl_xor(part, 16);
+        part += __shfl_xor(part, 32);
+        if (g == 0 && live) out[(size_t)oc * a.out_stride_o] = part + a.hb2[oc];
+      }
+    }
+  }
+}
+
+// One launch = one residual layer over the whole padded time axis (the default path).
+// XCD-local work queues with stealing: workgroup i runs on XCD i mod 8, XCD x owns
+// the x-th eighth of the blocks; rounds 0 and 1 are static, then a wave claims its next-but-one
+// block from its XCD's queue head one block ahead of use; a wave whose XCD range is drained steals
+// from the next XCDs'.
+// Small plans launch fewer computing waves per workgroup (a.compute_waves, spreading the blocks
+// over every CU) but still all the workgroup's waves stage the layer image (8 loads in flight per
+// thread over every thread).
+// a.trace (diagnostic, PWG_TRACE_FILE): per wave [start, staged, first block done, end, blocks,
+// shader clock at start, at end, XCC id], real time at 100 MHz.
+template <bool LAST, int TC, bool FIRST>
+__global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned smem16[];
+  const bool tr = a.trace != nullptr;
+  unsigned long long t_start = 0, c_start = 0, t_staged = 0, t_first = 0;
+  if (tr) {
+    t_start = __builtin_amdgcn_s_memrealtime();
+    c_start = __builtin_amdgcn_s_memtime();
+  }
+  const int lane = threadIdx.x & 63;
+  const int nw = a.compute_waves;
   const int xcd = blockIdx.x & 7;
   const int wave = threadIdx.x >> 6;
+  // the wave's first block (a static round) is known before the image is staged: its descriptor
+  // and tap-0 rows load while the workgroup stages (layer 0 with the fused first_conv builds tap 0
+  // from the first_conv weights in LDS, after the barrier)
+  const int blk0 = wave < nw ? (int)((long long)a.n_blocks * xcd / 8) + (blockIdx.x >> 3) * nw + wave : -1;
+  const bool has0 = blk0 >= 0 && blk0 < (int)((long long)a.n_blocks * (xcd + 1) / 8);
+  BlockDesc bdn;
+  u32x4 b0[8], b1[8];
+  if (has0) {
+    bdn = a.blocks[blk0];
+    if constexpr (!FIRST) s16_bload<TC, false, false>(a, nullptr, bdn, 0, b0, lane >> 4, lane & 15);
+  }
+  s16_stage<LAST, FIRST>(a, smem16);
+  __syncthreads();
+  int n_done = 0;
+  auto trace_out = [&]() {
+    if (tr && lane == 0) {
+      unsigned long long* r = a.trace + ((size_t)blockIdx.x * (blockDim.x >> 6) + wave) * 8;
+      const unsigned long long t_end = __builtin_amdgcn_s_memrealtime(), c_end = __builtin_amdgcn_s_memtime();
+      r[0] = t_start; r[1] = t_staged; r[2] = t_first; r[3] = t_end; r[4] = (unsigned long long)n_done;
+      r[5] = c_start; r[6] = c_end; r[7] = (unsigned long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));
+    }
+  };
+  if (tr) t_staged = __builtin_amdgcn_s_memrealtime();
+  if (wave >= nw) {
+    trace_out();
+    return;
+  }
   auto xcd_waves = [&](int y) { return (((int)gridDim.x - y + 7) >> 3) * nw; };
   auto xcd_first = [&](int y) { return (int)((long long)a.n_blocks * y / 8); };
   const int x_first = xcd_first(xcd), x_end = xcd_first(xcd + 1), x_waves = xcd_waves(xcd);
@@ -254,453 +617,139 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
     return -1;
   };
 
-  // a lane's tap row pieces for both n-tiles: b[nt*4 + ks*2 + hl]
-  auto bload = [&](const BlockDesc& d, int tap, u32x4 (&b)[8]) {
-    if constexpr (FIRST) {
-      // piece (ks, hl) = channels chan16(ks, g, 0..7) of x0 = w z + b at sample t
-      const f32x4* fw4 = reinterpret_cast<const f32x4*>(s_fwb) + g;
-      const f32x4* fb4 = reinterpret_cast<const f32x4*>(s_fwb + 64) + g;
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const int t = d.t0 + 16 * nt + c + (tap - TC) * a.dil;
-        const bool inside = t >= 0 && t < d.T;
-        const float z = a.noise[d.io_off + (t < 0 ? 0 : (t >= d.T ? d.T - 1 : t))];
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          float v[8];
-#pragma unroll
-          for (int jh = 0; jh < 2; ++jh) {
-            const f32x4 w = fw4[4 * (2 * ks + jh)], bb = fb4[4 * (2 * ks + jh)];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) v[4 * jh + i] = inside ? fmaf(w[i], z, bb[i]) : 0.f;
-          }
-          split8x<0>(v, b[nt * 4 + ks * 2], b[nt * 4 + ks * 2 + 1]);
-        }
-      }
-    } else {
-      const int cc = d.col + (PWG_SPLIT16_DIAG_NOTAP ? 0 : (tap - TC) * a.dil);  // NOTAP: diagnostic only
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const u32x4* p = reinterpret_cast<const u32x4*>(a.x_in + row16(diag_col<1>(cc + 16 * nt + c, xcd), g));
-#pragma unroll
-        for (int q = 0; q < 4; ++q) b[nt * 4 + q] = p[q * 64];
-      }
-    }
-  };
-  const u32x4* wgl = reinterpret_cast<const u32x4*>(s_wg) + lane;
-  auto mma_tap = [&](f32x4 (&acc)[8][2], const u32x4 (&b)[8], int tap) {
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-      for (int mh = 0; mh < 8 / MG; ++mh) {  // MG m-tiles per group: their fragments read ahead
-        u32x4 ah[MG], al[MG];
-#pragma unroll
-        for (int mm = 0; mm < MG; ++mm) {
-          const int m = MG * mh + mm;
-          ah[mm] = wgl[(((tap * 2 + ks) * 8 + m) * 2) * 64];
-          al[mm] = wgl[(((tap * 2 + ks) * 8 + m) * 2 + 1) * 64];
-        }
-#pragma unroll
-        for (int mm = 0; mm < MG; ++mm)
-#pragma unroll
-          for (int nt = 0; nt < 2; ++nt) {
-            f32x4& ac = acc[MG * mh + mm][nt];
-            ac = mma16(ah[mm], b[nt * 4 + ks * 2], ac);
-            ac = mma16(ah[mm], b[nt * 4 + ks * 2 + 1], ac);
-            ac = mma16(al[mm], b[nt * 4 + ks * 2], ac);
-          }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-  };
-#if PWG_SPLIT16_DIAG_LDS
-  // Diagnostic only (wrong results): the three taps share tap 0's A fragments, so GEMM 1 reads a
-  // third of its LDS bytes (the MFMA count is unchanged): the energy upper bound of register-blocking
-  // more columns per wave.
-  auto mma_3tap_diag = [&](f32x4 (&acc)[8][2], const u32x4 (&t0)[8], const u32x4 (&t1)[8], const u32x4 (&t2)[8]) {
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-#pragma unroll
-      for (int mh = 0; mh < 8 / MG; ++mh) {
-        u32x4 ah[MG], al[MG];
-#pragma unroll
-        for (int mm = 0; mm < MG; ++mm) {
-          const int m = MG * mh + mm;
-          ah[mm] = wgl[((ks * 8 + m) * 2) * 64];
-          al[mm] = wgl[((ks * 8 + m) * 2 + 1) * 64];
-        }
-#pragma unroll
-        for (int mm = 0; mm < MG; ++mm)
-#pragma unroll
-          for (int nt = 0; nt < 2; ++nt) {
-            f32x4& ac = acc[MG * mh + mm][nt];
-            ac = mma16(ah[mm], t0[nt * 4 + ks * 2], ac);
-            ac = mma16(ah[mm], t0[nt * 4 + ks * 2 + 1], ac);
-            ac = mma16(al[mm], t0[nt * 4 + ks * 2], ac);
-            ac = mma16(ah[mm], t1[nt * 4 + ks * 2], ac);
-            ac = mma16(ah[mm], t1[nt * 4 + ks * 2 + 1], ac);
-            ac = mma16(al[mm], t1[nt * 4 + ks * 2], ac);
-            ac = mma16(ah[mm], t2[nt * 4 + ks * 2], ac);
-            ac = mma16(ah[mm], t2[nt * 4 + ks * 2 + 1], ac);
-            ac = mma16(al[mm], t2[nt * 4 + ks * 2], ac);
-          }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-  };
-#endif
-  // GEMM-2 out-row seeds sqrt(.5)(x + b_out) from the center tap's pieces: acc2[4 + 2ks + (j>>2)][nt][j&3]
-  const f32x4* bo_l = reinterpret_cast<const f32x4*>(s_bo + 16 * g);
-  auto x_seed = [&](const u32x4 (&b)[8], f32x4 (&acc2)[8][2]) {
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        float o[8];
-        seed8x(b[nt * 4 + ks * 2], b[nt * 4 + ks * 2 + 1], bo_l[2 * ks], bo_l[2 * ks + 1], 0.70710677f, o);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc2[4 + 2 * ks + (j >> 2)][nt][j & 3] = o[j];
-      }
-  };
-
   int blk = x_first + (blockIdx.x >> 3) * nw + wave;
   int nblk = blk + x_waves;
   if (blk >= x_end) blk = -1;
   if (nblk >= x_end) nblk = -1;
-  if (blk < 0) return;
-  BlockDesc bdn = a.blocks[blk];
-  constexpr int T1 = TC == 1 ? 2 : 1;  // the non-center tap after tap 0
-  // prefetch schedule (PWG_SPLIT16_PF; layer 0 with the fused first_conv builds its taps with VALU
-  // and keeps schedule 0: the deeper one spills there)
-  constexpr int PF = FIRST ? 0 : PWG_SPLIT16_PF;
-  u32x4 b0[8], b1[8], b2[8];  // b2: center tap (PF > 0)
-  bload(bdn, 0, b0);
-  if constexpr (PF > 0) {
-    bload(bdn, T1, b1);
-    bload(bdn, TC, b2);
+  if (blk < 0) {
+    trace_out();
+    return;
   }
-  // LAST: any live column whose final skip sum is not finite. In the pair split an x, D or
-  // first_conv value beyond the fp16 range becomes (inf, -inf), which every later product turns into
-  // NaN and every skip sum downstream carries (the head's ReLU would hide it), so one check here
-  // covers every layer of the forward.
-  bool nonfinite = false;
-
+  const float* s_fwb = reinterpret_cast<const float*>(smem16 + Split16Smem::dwords(LAST));
+  if constexpr (FIRST) s16_bload<TC, true, false>(a, s_fwb, bdn, 0, b0, lane >> 4, lane & 15);
+  bool nonfinite = false;  // LAST: range flag (pwg_run_status)
   while (true) {
     const BlockDesc bd = bdn;
-    bdn = a.blocks[nblk >= 0 ? nblk : blk];
-    const bool full = bd.t0 + 32 <= bd.T;
-
-    // aux operands: lane group g covers window frames fw0 + 2g, fw0 + 2g + 1; K slots
-    // [Dh0 Dh1 Dl0 Dl1 Dh0 Dh1 bh bl] x [wh0 wh1 wh0 wh1 wl0 wl1 1 1] (bias in group 0 only)
-    const int fw0 = bd.t0 / a.H - a.J1;
-    unsigned dv[2][8];  // [frame][m]
-    auto load_dv = [&]() {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int f = fw0 + 2 * g + j;
-        const int fc = f < 0 ? 0 : (f >= bd.frames ? bd.frames - 1 : f);  // weight 0 there
-        // D row (frame) in the split16 layout [c 16][m 8] (pwg_aux_proj_kernel, split == 2)
-        const u32x4* drow = reinterpret_cast<const u32x4*>(a.d + (size_t)(bd.frame_base + fc) * 128 + 8 * c);
-#if PWG_SPLIT16_DIAG_NOD  // diagnostic: no D loads (wrong results)
-#pragma unroll
-        for (int m = 0; m < 8; ++m) dv[j][m] = (unsigned)(fc + m);
-#else
-        const u32x4 d0 = drow[0], d1 = drow[1];
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          dv[j][m] = d0[m];
-          dv[j][m + 4] = d1[m];
-        }
-#endif
-      }
-    };
-    float bw[2][2];  // [nt][frame]
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-      const int t = bd.t0 + 16 * nt + c;
-      const bool live = t < bd.T;
-      const int tc = live ? t : bd.T - 1;
-      int roff;
-      if (bd.frames < a.Fmin) roff = a.tab_small + (a.H * bd.frames * (bd.frames - 1) / 2 + tc) * AUX_J4;
-      else if (tc < a.TL) roff = a.tab_left + tc * AUX_J4;
-      else if (tc >= bd.T - a.TR) roff = a.tab_right + (bd.T - 1 - tc) * AUX_J4;
-      else roff = (tc % a.H) * AUX_J4;
-      const int shift = t / a.H - bd.t0 / a.H;
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int idx = 2 * g + j - shift;
-        const bool ok = live && idx >= 0 && idx < AUX_J4;
-        const float w = a.tab[roff + (idx < 0 ? 0 : (idx >= AUX_J4 ? AUX_J4 - 1 : idx))];
-        bw[nt][j] = ok ? w : 0.f;
-      }
-    }
-
-    // ---- GEMM 1: taps 0, other, center (the center row becomes the GEMM-2 seeds at the end)
-    f32x4 acc[8][2];
-#pragma unroll
-    for (int m = 0; m < 8; ++m)
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) acc[m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    f32x4 acc2[8][2];
-#if PWG_SPLIT16_EARLY_SKIP
-    // skip seeds first: the old skip sum streams from HBM, its latency hides behind GEMM 1
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-      for (int ms = 0; ms < 4; ++ms) {
-        if (a.first) {
-          acc2[ms][nt] = reinterpret_cast<const f32x4*>(a.skip0 + 16 * g)[ms];
-        } else {
-          const f32x4* sp = reinterpret_cast<const f32x4*>(a.skip + row16(diag_col<2>(bd.col + 16 * nt + c, xcd), g));
-          acc2[ms][nt] = PWG16_LD_SKIP(sp + ms * 64);
-        }
-      }
-
-#endif
-    if constexpr (PF > 0) {
-#if PWG_SPLIT16_DIAG_LDS
-      load_dv();
-      mma_3tap_diag(acc, b0, b1, b2);
-      bload(bdn, 0, b0);
-      if (!LAST) x_seed(b2, acc2);
-      if (false) {
-#endif
-      mma_tap(acc, b0, 0);
-      load_dv();
-      mma_tap(acc, b1, T1);
-      bload(bdn, 0, b0);  // the next block's (bdn = bd when there is none)
-      mma_tap(acc, b2, TC);
-      if (!LAST) x_seed(b2, acc2);
-#if PWG_SPLIT16_DIAG_LDS
-      }
-#endif
-    } else {
-      bload(bd, T1, b1);
-      mma_tap(acc, b0, 0);
-      load_dv();
-      bload(bd, TC, b0);
-      mma_tap(acc, b1, T1);
-      bload(bdn, 0, b1);  // the next block's (bdn = bd when there is none)
-      mma_tap(acc, b0, TC);
-      if (!LAST) x_seed(b0, acc2);
-    }
-
+    bdn = a.blocks[nblk >= 0 ? nblk : blk];  // prefetch target (bd itself when there is none)
     int ticket = 0;
-    if (nblk >= 0) ticket = ticket_issue();
-#if !PWG_SPLIT16_EARLY_SKIP
-    // skip seeds: old skip sum (layer 0: the sum of all layers' skip biases, [g][16] layout)
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-      for (int ms = 0; ms < 4; ++ms) {
-        if (a.first) {
-          acc2[ms][nt] = reinterpret_cast<const f32x4*>(a.skip0 + 16 * g)[ms];
-        } else {
-          const f32x4* sp = reinterpret_cast<const f32x4*>(a.skip + row16(diag_col<2>(bd.col + 16 * nt + c, xcd), g));
-          acc2[ms][nt] = PWG16_LD_SKIP(sp + ms * 64);
-        }
-      }
-
-#endif
-    // ---- aux term + gate bias: one MFMA per (m, nt)
-    {
-      const Pair16 bias_one = split_pair16(g == 0 ? 1.f : 0.f, g == 0 ? 1.f : 0.f);
-      u32x4 bB[2];
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const Pair16 w = split_pair16(bw[nt][0], bw[nt][1]);
-        // [wh0 wh1 | wh0 wh1 | wl0 wl1 | 1 1]
-        bB[nt] = u32x4{w.hi, w.hi, w.lo, bias_one.hi};
-      }
-      const unsigned* bgl = s_bg + c;
-#pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        const unsigned bgp = g == 0 ? bgl[16 * m] : 0u;  // (bias hi | bias lo << 16)
-        const unsigned dh = __builtin_amdgcn_perm(dv[1][m], dv[0][m], 0x05040100u);
-        const unsigned dl = __builtin_amdgcn_perm(dv[1][m], dv[0][m], 0x07060302u);
-        // [Dh0 Dh1 | Dl0 Dl1 | Dh0 Dh1 | bh bl]
-        const u32x4 aA = {dh, dl, dh, bgp};
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt) acc[m][nt] = mma16(aA, bB[nt], acc[m][nt]);
-      }
-    }
-
-    if constexpr (PF == 2) bload(bdn, T1, b1);
-    // ---- gate -> GEMM-2 B pairs: k-step ks element j = channel chan16(ks, g, j) = acc row
-    u32x4 gh[2][2], gl[2][2];  // [nt][ks]
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        float gv[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int m = 2 * ks + (j >> 2), i = j & 3;
-          gv[j] = gate16(acc[m][nt][i], acc[m + 4][nt][i]);
-        }
-        split8x<0>(gv, gh[nt][ks], gl[nt][ks]);
-      }
-
-    if constexpr (PF == 1) bload(bdn, T1, b1);
-    if constexpr (PF > 0) bload(bdn, TC, b2);
-    // ---- GEMM 2: [skip; out] rows, 8 m-tiles (last layer: the 4 skip tiles)
-    constexpr int M2 = LAST ? 4 : 8;
-    const u32x4* w2l = reinterpret_cast<const u32x4*>(s_w2) + lane;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int mh = 0; mh < M2 / 4; ++mh) {
-        u32x4 ah[4], al[4];
-#pragma unroll
-        for (int mm = 0; mm < 4; ++mm) {
-          ah[mm] = w2l[((ks * 8 + 4 * mh + mm) * 2) * 64];
-          al[mm] = w2l[((ks * 8 + 4 * mh + mm) * 2 + 1) * 64];
-        }
-#pragma unroll
-        for (int mm = 0; mm < 4; ++mm)
-#pragma unroll
-          for (int nt = 0; nt < 2; ++nt) {
-            f32x4& ac = acc2[4 * mh + mm][nt];
-            ac = mma16(ah[mm], gh[nt][ks], ac);
-            ac = mma16(ah[mm], gl[nt][ks], ac);
-            ac = mma16(al[mm], gh[nt][ks], ac);
-          }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-
-    if (!LAST) {
-      // tile bases (wave-uniform) and the lane's byte offset inside a tile, for policy stores
-      const size_t tile_dw = (size_t)(bd.col >> 5) * 2048;
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const int col = bd.col + 16 * nt + c;
-        const bool live = bd.t0 + 16 * nt + c < bd.T;
-        const unsigned lane_b = (unsigned)(row16(col, g) - tile_dw) * 4u;
-        f32x4* sp = reinterpret_cast<f32x4*>(a.skip + row16(diag_col<2>(col, xcd), g));
-#pragma unroll
-        for (int ms = 0; ms < 4; ++ms) {
-          if constexpr ((PWG_SPLIT16_SC1 & 1) != 0)
-            st16_policy(a.skip + tile_dw, lane_b + ms * 1024u, __builtin_bit_cast(u32x4, acc2[ms][nt]));
-          else
-            PWG16_ST(sp + ms * 64, acc2[ms][nt]);
-        }
-        u32x4* xp = reinterpret_cast<u32x4*>(a.x_out + row16(diag_col<1>(col, xcd), g));
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          float v[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = acc2[4 + 2 * ks + (j >> 2)][nt][j & 3];
-          u32x4 vh, vl;
-          split8x<11>(v, vh, vl);  // inputs straight from the GEMM-2 MFMAs
-          if (!full) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              vh[k] = live ? vh[k] : 0u;
-              vl[k] = live ? vl[k] : 0u;
-            }
-          }
-          if constexpr ((PWG_SPLIT16_SC1 & 2) != 0) {
-            st16_policy(a.x_out + tile_dw, lane_b + (ks * 2) * 1024u, vh);
-            st16_policy(a.x_out + tile_dw, lane_b + (ks * 2 + 1) * 1024u, vl);
-          } else {
-            PWG16_ST(xp + (ks * 2) * 64, vh);
-            PWG16_ST(xp + (ks * 2 + 1) * 64, vl);
-          }
-        }
-      }
-    } else {
-      // ---- fused output head (models/parallel_wavegan.py:131-138,166-171), split-f16 on
-      //      v_mfma_f32_16x16x32_f16 like the layer: h1 = W1h . relu(skip * sqrt(1/L)) + b1h with
-      //      k-step ks element j = skip row chan16(ks, g, j) = acc2[2ks + (j >> 2)][nt][j & 3]
-      //      (the W1h image is packed in that k order); then y = W2h . relu(h1) + b2h across the 4
-      //      lane groups. (The fp32 v_mfma_f32_16x16x4f32 head took 128 MFMAs of twice the cycles.)
-      const u32x4* hw1 = reinterpret_cast<const u32x4*>(s_hw1) + lane;
-      const f32x4* hb1 = reinterpret_cast<const f32x4*>(s_hw1 + 4 * 4 * 64 * 4 + 16 * g);
-      f32x4 acc3[4][2];
-#pragma unroll
-      for (int m3 = 0; m3 < 4; ++m3)
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt) acc3[m3][nt] = hb1[m3];
-      u32x4 sh[2][2], sl[2][2];  // [nt][ks]
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        float sum = 0.f;  // inf/NaN in any of the 16 propagates (ReLU's fmaxf below would hide NaN)
-#pragma unroll
-        for (int ms = 0; ms < 4; ++ms)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) sum += acc2[ms][nt][i];
-        nonfinite |= bd.t0 + 16 * nt + c < bd.T && !__builtin_isfinite(sum);
-      }
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          float hv[8];
-          float hmax = 0.f;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            hv[j] = fmaxf(acc2[2 * ks + (j >> 2)][nt][j & 3] * a.skip_scale, 0.f);
-            hmax = fmaxf(hmax, hv[j]);
-          }
-          // a finite skip sum whose scaled value the pair split cannot carry (hi = inf, lo = -inf)
-          nonfinite |= bd.t0 + 16 * nt + c < bd.T && hmax >= 65520.f;
-          split8x<0>(hv, sh[nt][ks], sl[nt][ks]);
-        }
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int m3 = 0; m3 < 4; ++m3) {
-          const u32x4 ah = hw1[((ks * 4 + m3) * 2) * 64], al = hw1[((ks * 4 + m3) * 2 + 1) * 64];
-#pragma unroll
-          for (int nt = 0; nt < 2; ++nt) {
-            acc3[m3][nt] = mma16(ah, sh[nt][ks], acc3[m3][nt]);
-            acc3[m3][nt] = mma16(ah, sl[nt][ks], acc3[m3][nt]);
-            acc3[m3][nt] = mma16(al, sh[nt][ks], acc3[m3][nt]);
-          }
-        }
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const int t = bd.t0 + 16 * nt + c;
-        const bool live = t < bd.T;
-        float* out = a.out + (size_t)bd.io_off * a.O + (size_t)t * a.out_stride_t;
-        for (int oc = 0; oc < a.O; ++oc) {
-          const f32x4* w = reinterpret_cast<const f32x4*>(a.hw2 + ((size_t)oc * 4 + g) * 16);
-          float part = 0.f;
-#pragma unroll
-          for (int m3 = 0; m3 < 4; ++m3) {
-            const f32x4 wq = w[m3];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) part = fmaf(wq[i], fmaxf(acc3[m3][nt][i], 0.f), part);
-          }
-          part += __shfl_xor(part, 16);
-          part += __shfl_xor(part, 32);
-          if (g == 0 && live) out[(size_t)oc * a.out_stride_o] = part + a.hb2[oc];
-        }
-      }
-    }
-
+    s16_block<LAST, TC, FIRST, false>(a, smem16, bd, bdn, true, b0, b1, nonfinite, [&]() {
+      if (nblk >= 0) ticket = ticket_issue();
+    });
+    if (tr && n_done++ == 0) t_first = __builtin_amdgcn_s_memrealtime();
     if (nblk < 0) break;
     blk = nblk;
     nblk = ticket_resolve(ticket);
-    if constexpr (PF == 0) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) b0[i] = b1[i];
+    b0[0] = b1[0]; b0[1] = b1[1]; b0[2] = b1[2]; b0[3] = b1[3];
+    b0[4] = b1[4]; b0[5] = b1[5]; b0[6] = b1[6]; b0[7] = b1[7];
+  }
+  if (LAST && nonfinite && a.range_flag)
+    __hip_atomic_fetch_or(a.range_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  trace_out();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Layer-pipelined forward (all L residual layers in ONE launch): workgroup w (one per CU) keeps
+// layer l(w)'s weights resident in LDS for the whole forward and its waves take that layer's
+// blocks in order from a per-layer queue; a block of layer l starts once layer l - 1 has finished
+// the blocks its dilated taps read (RAW on x) and layer l - 2 the blocks whose columns this write
+// overwrites (x lives in 3 rotating planes: layer l reads plane l % 3, writes (l + 1) % 3; skip is
+// updated in place). prog[b] = layers finished on block b. Hand-off bytes (x, skip) are stored and
+// loaded sc1, each storing wave drains its stores (s_waitcnt vmcnt(0)) before it publishes
+// prog[b] with an sc1 atomic store; consumers poll prog relaxed (Guideline 16, R1 with sc1 loads).
+// Every spin is bounded: a wait that gives up sets bit 1 of the range word (pwg_run_status
+// reports it) and the grid still drains. Requires every workgroup resident: grid <= CUs, one
+// 512-thread workgroup per CU (the LDS image holds that).
+constexpr int PIPE_SPIN_LIMIT = 1 << 20;
+
+template <bool LAST, int TC, bool FIRST>
+__device__ __forceinline__ void pipe_layer(const PipeArgs& p, int l, unsigned* smem16) {
+  SplitArgs a = p.base;
+  a.wg = p.wg0 + (size_t)l * p.wg_stride;
+  a.d = p.d0 + (size_t)l * p.d_stride;
+  a.x_in = p.x[l % 3];
+  a.x_out = p.x[(l + 1) % 3];
+  a.dil = p.dil[l];
+  a.first = l == 0;
+  if (!FIRST) a.noise = nullptr;
+  s16_stage<LAST, FIRST>(a, smem16);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  int* const queue = p.ctr + l * SCHED_CTR_STRIDE * 8;
+  // waits, in blocks around b: layer l - 1 done on [b - rl1, b + rr1] (what this layer's taps read:
+  // TC * dil to the left, (2 - TC) * dil to the right), layer l - 2 done on [b - rr2, b + rl2] (the
+  // blocks whose taps read the columns of b in the plane this layer overwrites)
+  const int rl1 = (TC * a.dil + 31) / 32, rr1 = ((2 - TC) * a.dil + 31) / 32;
+  const int rl2 = l >= 2 ? (TC * p.dil[l - 2] + 31) / 32 : 0, rr2 = l >= 2 ? ((2 - TC) * p.dil[l - 2] + 31) / 32 : 0;
+  const int left = rl1 > rr2 ? rl1 : rr2, right = rr1 > rl2 ? rr1 : rl2;  // left + right < 64 (plan check)
+  auto ticket = [&]() -> int {
+    int v = 0;
+    if (lane == 0) v = __hip_atomic_fetch_add(queue, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __builtin_amdgcn_readfirstlane(v);
+  };
+  auto wait_deps = [&](int b) {
+    if (l == 0) return;
+    const int i = lane - left, bb = b + i;
+    const bool need = lane <= left + right && bb >= 0 && bb < a.n_blocks;
+    const int thr = (i >= -rl1 && i <= rr1) ? l : l - 1;
+    for (int spins = 0;; ++spins) {
+      const int v = need ? __hip_atomic_load(p.prog + (need ? bb : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                         : 0x7fffffff;
+      if (__all(v >= thr)) break;
+      if (spins >= PIPE_SPIN_LIMIT) {
+        if (lane == 0) __hip_atomic_fetch_or(p.base.range_flag, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the sc1 loads below the poll
+  };
+
+  bool nonfinite = false;
+  const float* s_fwb = reinterpret_cast<const float*>(smem16 + Split16Smem::dwords(LAST));
+  int blk = ticket();
+  u32x4 b0[8], b1[8];
+  while (blk < a.n_blocks) {
+    const BlockDesc bd = a.blocks[blk];
+    wait_deps(blk);
+    s16_bload<TC, FIRST, true>(a, s_fwb, bd, 0, b0, lane >> 4, lane & 15);
+    int next = 0;
+    s16_block<LAST, TC, FIRST, true>(a, smem16, bd, bd, false, b0, b1, nonfinite, [&]() { next = ticket(); });
+    if (!LAST) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores have landed
+      if (lane == 0) __hip_atomic_store(p.prog + blk, l + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    blk = next;
   }
   if (LAST && nonfinite && a.range_flag)
     __hip_atomic_fetch_or(a.range_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// first_conv (1x1, 1 -> 64, bias) into the split16 x layout; gap tiles zero both buffers.
+template <int TC>
+__global__ void __launch_bounds__(512, 1) pwg_pipe_split16_kernel(const PipeArgs p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned smem16[];
+  // layers laid out over the XCDs in order (workgroup i runs on XCD i mod 8 in practice: consecutive
+  // layers then share an L2; placement is a speed heuristic only, correctness does not depend on it)
+  const int nwg = gridDim.x;
+  const int lin = (blockIdx.x & 7) * (nwg >> 3) + (blockIdx.x >> 3);
+  const int l = (int)((long long)lin * p.L / nwg);
+  if (l == p.L - 1) pipe_layer<true, TC, false>(p, l, smem16);
+  else if (l == 0 && p.base.noise != nullptr) pipe_layer<false, TC, true>(p, l, smem16);
+  else pipe_layer<false, TC, false>(p, l, smem16);
+}
+
+// first_conv (1x1, 1 -> 64, bias) into the split16 x layout; gap tiles zero every residual plane.
 __global__ void __launch_bounds__(256) pwg_first_conv_split16_kernel(const FirstConvArgs a) {
   const long long tile = blockIdx.x;
   unsigned* x = reinterpret_cast<unsigned*>(a.x);
   unsigned* x1 = reinterpret_cast<unsigned*>(a.x1);
+  unsigned* x2 = reinterpret_cast<unsigned*>(a.x2);
   if (tile >= a.n_work) {
     const long long col0 = a.gap_col0[tile - a.n_work];
     for (int idx = threadIdx.x; idx < 64 * TILE; idx += 256) {
       x[(size_t)col0 * 64 + idx] = 0u;
       x1[(size_t)col0 * 64 + idx] = 0u;
+      if (x2 != nullptr) x2[(size_t)col0 * 64 + idx] = 0u;
     }
     return;
   }
@@ -740,6 +789,7 @@ hipError_t launch_first_conv_split16(const FirstConvArgs& a, long long n_tiles, 
 hipError_t launch_layer_split16(const SplitArgs& a, bool last, int tap_center, int waves_per_wg, int n_wg,
                                 hipStream_t s) {
   if (waves_per_wg > 8) waves_per_wg = 8;
+  if (a.compute_waves < 1 || a.compute_waves > waves_per_wg) return hipErrorInvalidValue;
   const dim3 grid((unsigned)n_wg), block((unsigned)(64 * waves_per_wg));
 #define PWG_SPLIT16_LAUNCH(LAST_, TC_, FIRST_)                                                          \
   {                                                                                                     \
@@ -762,6 +812,19 @@ hipError_t launch_layer_split16(const SplitArgs& a, bool last, int tap_center, i
   }
 #undef PWG_SPLIT16_LAUNCH
   return hipErrorInvalidValue;
+}
+
+hipError_t launch_pipe_split16(const PipeArgs& p, int tap_center, int n_wg, hipStream_t s) {
+  const size_t lds = sizeof(unsigned) * (Split16Smem::dwords(true) > Split16Smem::dwords(false) + 128
+                                             ? Split16Smem::dwords(true) : Split16Smem::dwords(false) + 128);
+  if (n_wg < p.L || n_wg % 8 != 0) return hipErrorInvalidValue;
+  auto kfn = tap_center == 1 ? &pwg_pipe_split16_kernel<1> : tap_center == 2 ? &pwg_pipe_split16_kernel<2> : nullptr;
+  if (kfn == nullptr) return hipErrorInvalidValue;
+  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(kfn, dim3((unsigned)n_wg), dim3(512), lds, s, p);
+  return hipGetLastError();
 }
 
 }  // namespace pwg

