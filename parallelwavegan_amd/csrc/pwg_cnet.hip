@@ -2251,17 +2251,16 @@ __global__ void __launch_bounds__(256) pwg_cnet_finite_kernel(const float* y, lo
 
 // ---------------------------------------------------------------------------------------------
 struct OpPhase {          // one launch
-  int op;
-  int phase;              // CONVT phase r, else 0
-  int MT, mt_total;
-  long long frag_off;     // floats into the packed image
+  int op = 0;
+  int phase = 0;          // CONVT phase r, else 0
+  int MT = 0, mt_total = 0;
+  long long frag_off = 0; // floats into the packed image
   long long frag16_off = -1;  // split-f16 A fragments (same size), MFMA phases only
-  long long bias_off;
+  long long bias_off = -1;
   std::vector<ChunkDesc> chunks;
   ChunkDesc* d_chunks = nullptr;
-  int ostride, ophase;
-  int k_a, off_a;         // CONVT
-  int NT;                 // column tiles per wave (workgroup = NW waves x NT x 32 columns)
+  int ostride = 1, ophase = 0;
+  int k_a = 0, off_a = 0; // CONVT
   int NW = 4;             // waves per workgroup of pwg_cnet_conv_kernel
   bool xtile = false;     // split mode runs pwg_cnet_xtile_kernel (channel-block-major, staged input tile)
   int xt_lds = 0;
@@ -2434,7 +2433,7 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
         return fail(PWG_ERR_INVALID, where + "bad PQMF op");
       }
       OpPhase ph;
-      ph.op = oi; ph.phase = 0; ph.MT = 0; ph.mt_total = 0; ph.frag_off = off; ph.bias_off = -1; ph.NT = 1;
+      ph.op = oi; ph.phase = 0; ph.MT = 0; ph.mt_total = 0; ph.frag_off = off; ph.bias_off = -1;
       ph.ostride = 1; ph.ophase = 0;
       off += (long long)op.stride * op.padding;
       n->phases.push_back(ph);
@@ -2584,7 +2583,7 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
     bool ok = s2 <= 8 && i + s2 <= n->phases.size() && !ph.thin && !ph.xtile;
     for (int r = 1; ok && r < s2; ++r) {
       const OpPhase& q = n->phases[i + r];
-      ok = q.op == ph.op && q.phase == r && q.MT == ph.MT && q.NT == ph.NT && q.NW == ph.NW && !q.thin &&
+      ok = q.op == ph.op && q.phase == r && q.MT == ph.MT && q.NW == ph.NW && !q.thin &&
            q.chunks.size() == ph.chunks.size() && q.mt_total == ph.mt_total;
     }
     if (!ok) continue;
@@ -2653,7 +2652,7 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
     if (pa.pair_b >= 0 || pb.op != pa.op + 1) continue;
     const PwgCnetOp& A = n->ops[pa.op];
     const PwgCnetOp& B = n->ops[pb.op];
-    if (A.kind != PWG_CNET_CONV || B.kind != PWG_CNET_CONV || pa.thin || pb.thin || pa.NT != 1 || pb.NT != 1 ||
+    if (A.kind != PWG_CNET_CONV || B.kind != PWG_CNET_CONV || pa.thin || pb.thin ||
         (pa.NW != 4 && !pa.xtile))
       continue;
     if (A.src[1].buf >= 0 || A.res >= 0 || A.accumulate || A.out_div != 1.f || A.post_act != PWG_ACT_NONE) continue;
@@ -2930,7 +2929,7 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
         const long long T = frames[u] * n->rate[op.dst];
         const int nq = (int)((T - ph.ophase + ph.ostride - 1) / ph.ostride);
         ncols[u] = nq;
-        const int cols = ph.thin ? CN_COLS : 32 * ph.NW * ph.NT;
+        const int cols = ph.thin ? CN_COLS : 32 * ph.NW;
         for (int q0 = 0; q0 < nq; q0 += cols) blocks.push_back(make_int2(u, q0));
       }
     }

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-2 verification pass (GPU box): full GPU suite, smoke, default bench (latency rows + CPU
+# Round verification pass (GPU box): full GPU suite, smoke, default bench (latency rows + CPU
 # baseline), strong-scaling bench of the 512-utterance list, rocprofv3 kernel stats.
 # Usage: bash tools/gpu_round.sh OUTDIR [skip-tests]
 set -e
