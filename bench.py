@@ -237,10 +237,12 @@ def measure_program_traffic(args):
     per, err = _pmc_passes(args)
     if per is None:
         return None, err, None
-    tot, by_kernel = {}, {}
+    tot, by_kernel, n_fwd = {}, {}, 0
     for ctr, vals in per.items():
-        ids = sorted(vals)
+        # the conv program's own launches only (module setup runs torch / copy kernels before them)
+        ids = sorted(i for i in vals if "pwg_cnet_" in vals[i][0])
         second = ids[len(ids) // 2:]
+        n_fwd = len(second)
         scale = 2048.0 if ctr == "FETCH_SIZE" else 1024.0
         tot[ctr] = sum(vals[i][1] for i in second) * scale
         for i in second:
@@ -248,7 +250,7 @@ def measure_program_traffic(args):
             name = name.split("(")[0].replace("void ", "")
             by_kernel[name] = by_kernel.get(name, 0.0) + vals[i][1] * scale
     note = (f"measured in this run: rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) and WRITE_SIZE passes over "
-            f"two forwards in a child process, the second forward's {len(per['FETCH_SIZE']) // 2} dispatches; read "
+            f"two forwards in a child process, the second forward's {n_fwd} conv-program launches; read "
             f"{tot['FETCH_SIZE'] / 1e9:.3f} GB + write {tot['WRITE_SIZE'] / 1e9:.3f} GB per forward")
     top = dict(sorted(((k, round(v / 1e9, 4)) for k, v in by_kernel.items()), key=lambda kv: -kv[1])[:6])
     return tot["FETCH_SIZE"] + tot["WRITE_SIZE"], note, top
