@@ -121,8 +121,16 @@ PWG_API int pwg_cnet_run_status(PwgCnetPlan* p, const void* workspace, void* str
  * or >= 128 rows per tile) run channel-block-major with the input tile staged once per 16-channel
  * block (fp32 summation order differs from the tap-major kernel: parity to the oracle, not bit
  * identity). Conv pairs of such convs then run as two of these launches instead of fused (measured
- * faster on HiFiGAN v1); 0 restores the tap-major kernel and the fused pairs. */
-enum { PWG_CNET_OPT_SPLIT_F16 = 0, PWG_CNET_OPT_FUSE_PAIRS = 1, PWG_CNET_OPT_PAIR_STEPS = 2, PWG_CNET_OPT_XTILE = 3 };
+ * faster on HiFiGAN v1); 0 restores the tap-major kernel and the fused pairs.
+ * PWG_CNET_OPT_XT_DMA (flags, default 9 = 1 | 8): x-tile kernels that stage their weight
+ * fragments by global_load_lds into two LDS buffers, the next tap group's copy running under the
+ * current one's MFMAs. 1: the convs where that measured faster (>= 96-row workgroups at k >= 7,
+ * k = 3 up to 192 channels); 2: every eligible conv; 4: the fewest tap groups (one workgroup per
+ * CU) instead of groups sized for two; these are bit-identical to the register-staged x-tile
+ * kernels. 8: the wide (> 64 output channels) ConvTranspose phases on this kernel instead of the
+ * tap-major one (channel-block-major summation: parity to the oracle, not bit identity). */
+enum { PWG_CNET_OPT_SPLIT_F16 = 0, PWG_CNET_OPT_FUSE_PAIRS = 1, PWG_CNET_OPT_PAIR_STEPS = 2, PWG_CNET_OPT_XTILE = 3,
+       PWG_CNET_OPT_XT_DMA = 4 };
 PWG_API int pwg_cnet_set_option(PwgCnet* n, int option, long long value);
 PWG_API int pwg_cnet_set_timing(PwgCnet* n, int enable);
 /* Adds per-op milliseconds and launch counts (arrays of n_ops) and clears the records. */

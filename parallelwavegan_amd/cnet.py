@@ -297,9 +297,12 @@ class CnetEngine:
         key = stream.cuda_stream
         ws = self._workspaces.get(key)
         if ws is None or ws.numel() < nbytes:
+            # grow geometrically (x1.5): a run of growing batch shapes reallocates O(log) times
+            grow = int(ws.numel() * 1.5) if ws is not None else 0
             self._workspaces.pop(key, None)
+            ws = None
             with torch.cuda.stream(stream):
-                ws = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=self.device)
+                ws = torch.empty(max(int(nbytes), grow, 256), dtype=torch.uint8, device=self.device)
             self._workspaces[key] = ws
         return ws
 
@@ -406,6 +409,15 @@ class CnetEngine:
         input tile staged once per 16-channel block (default on); off: the tap-major kernel and
         the fused conv pairs."""
         _lib.check(self._lib.pwg_cnet_set_option(self._h, 3, int(bool(enable))))
+
+    XT_DMA_RULE, XT_DMA_ALL, XT_DMA_FEWEST, XT_DMA_CONVT = 1, 2, 4, 8  # include/pwg_cnet.h flags
+
+    def set_xt_dma(self, mode):
+        """pwg_cnet_set_option(PWG_CNET_OPT_XT_DMA) flags: x-tile convs stage their weight fragments
+        by DMA (global_load_lds) into two LDS buffers, overlapped with the MFMAs (bit-identical to
+        the register-staged kernels): 1 the shapes where that measured faster, 2 every eligible conv,
+        4 the fewest tap groups; 8 the wide ConvTranspose phases on that kernel. Default 9."""
+        _lib.check(self._lib.pwg_cnet_set_option(self._h, 4, int(mode)))
 
     def set_pair_steps(self, steps):
         """pwg_cnet_set_option(PWG_CNET_OPT_PAIR_STEPS): 128-column tiles per fused-pair

@@ -54,6 +54,8 @@ constexpr int CNET_XPAIR_MAXK = 11;        // largest kernel size fused into an 
 constexpr int CNET_XTILE_CONVT = 2;        // ConvTranspose phases of <= this many m-tiles on the x-tile
                                            // kernel: faster up to 64 output channels, slower at 128-256
                                            // (stride 8; profiles/r02_ct)
+// PWG_CNET_OPT_XT_DMA flags (include/pwg_cnet.h)
+constexpr int CNET_DMA_RULE = 1, CNET_DMA_ALL = 2, CNET_DMA_FEWEST = 4, CNET_DMA_CONVT = 8;
 constexpr int CNET_XT_MT2_MAXK = 7;        // >= 256-row convs with <= this many taps: 2 m-tiles per workgroup
 
 struct ChunkDesc {   // one K chunk of an op (uniform per launch)
@@ -401,24 +403,33 @@ constexpr int XT_ROWB = 80;  // bytes per staged input row: 16 hi + 16 lo halves
 // SY (synchronous staging): no register prefetch of the next channel block; the kernel is held to
 // 128 VGPRs (4 waves per SIMD) so two workgroups share a CU and one's staging overlaps the other's
 // MFMAs. Same arithmetic and order: bit-identical.
-template <int MT, int K, int CB, bool SY = false>
+template <int MT, int K, int CB, bool SY = false, bool DB = false>
 constexpr int xt_wpe() {
-  return SY ? 4 : 1;
+  return SY || DB ? 4 : 1;  // DB: also held to 128 VGPRs, two workgroups per CU when LDS allows
 }
 // NC column tiles of 256 per workgroup (wave w: columns 256 nc + 32 w + [0, 32)); the engine runs
 // NC = 1 (NC = 2 measured no faster, profiles/r02_nc).
 // KS (SY only): taps whose A fragments are staged per step; KS < K stages a channel block's taps in
 // ceil(K / KS) steps (same MFMA order) so the A region fits two workgroups per CU (k = 11, MT 4).
-template <int MT, int K, int CB, int NC = 1, bool SY = false, int KS = K>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(xt_wpe<MT, K, CB, SY>())))
+// DB (double-buffered DMA staging): the A fragments of the next tap group go global -> LDS by
+// global_load_lds (no registers) into the second of two A buffers while the waves run the MFMAs of
+// the current one; the next channel block's input rows are loaded to registers over the last tap
+// group's MFMAs and converted into the (single) row buffer after it. KS < K: two tap groups per
+// channel block, [0, KS) always in buffer 0 and [KS, K) in buffer 1; KS == K: the buffers alternate
+// per block. Same products in the same order as the other variants: bit-identical.
+template <int MT, int K, int CB, int NC = 1, bool SY = false, int KS = K, bool DB = false>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(xt_wpe<MT, K, CB, SY, DB>())))
 pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
-  static_assert(KS == K || SY, "tap-split staging is a synchronous-staging variant");
+  static_assert(KS == K || SY || DB, "tap-split staging is a synchronous-staging or DMA variant");
+  static_assert(!DB || (CB == 1 && NC == 1 && !SY), "DMA staging: one block, one column tile");
   constexpr int NTH = 512;
   constexpr int AV = CB * K * MT * 128;                // A vectors (16 B) per group of CB channel blocks
-  constexpr int AQ = (AV + NTH - 1) / NTH;
+  constexpr int AQ = DB ? 1 : (AV + NTH - 1) / NTH;
+  constexpr int A_BYTES = CB * KS * MT * 2048;
   extern __shared__ __attribute__((aligned(16))) unsigned char xt_smem[];
   f32x4v* s_a = reinterpret_cast<f32x4v*>(xt_smem);                          // [CB][K][MT][2][64] x 16 B
-  unsigned char* s_x = xt_smem + (size_t)CB * KS * MT * 2048;                 // [CB][span][XT_ROWB]
+  f32x4v* s_a1 = reinterpret_cast<f32x4v*>(xt_smem + (DB ? A_BYTES : 0));   // DB: second A buffer
+  unsigned char* s_x = xt_smem + (size_t)(DB ? 2 : 1) * A_BYTES;              // [CB][span][XT_ROWB]
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int hh = lane >> 5;
@@ -444,7 +455,7 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
   f32x4v xr[XQ_MAX];
   bool xok[XQ_MAX];
   // group g = channel blocks [CB g, CB g + CB): global -> registers
-  auto load = [&](int grp) {
+  auto aload = [&](int grp) {
 #pragma unroll
     for (int i = 0; i < AQ; ++i) {
       const int idx = threadIdx.x + NTH * i;  // [c][tap][m][128 vectors]
@@ -455,6 +466,8 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
                              wfrag_ + ((size_t)(wt * xt.cs + CB * grp + c) * a.mt_total + m0) * 512)[rem]
                        : f32x4v{0.f, 0.f, 0.f, 0.f};
     }
+  };
+  auto xload = [&](int grp) {
 #pragma unroll
     for (int i = 0; i < XQ_MAX; ++i) {
       const int idx = threadIdx.x + NTH * i;  // [c][row][quad]
@@ -467,13 +480,19 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
                  : f32x4v{0.f, 0.f, 0.f, 0.f};
     }
   };
+  auto load = [&](int grp) {
+    aload(grp);
+    xload(grp);
+  };
   // registers -> LDS (x pre-activated and pair-split on the way)
-  auto store = [&](int grp) {
+  auto astore = [&]() {
 #pragma unroll
     for (int i = 0; i < AQ; ++i) {
       const int idx = threadIdx.x + NTH * i;
       if (idx < AV) s_a[idx] = ar[i];
     }
+  };
+  auto xstore = [&](int grp) {
 #pragma unroll
     for (int i = 0; i < XQ_MAX; ++i) {
       const int idx = threadIdx.x + NTH * i;
@@ -500,6 +519,22 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
       unsigned char* row = s_x + ((size_t)c * xt.span + r) * XT_ROWB;
       *reinterpret_cast<f16x4v*>(row + 8 * qd) = f16x4v{hv[0], hv[1], hv[2], hv[3]};
       *reinterpret_cast<f16x4v*>(row + 32 + 8 * qd) = f16x4v{lv[0], lv[1], lv[2], lv[3]};
+    }
+  };
+  auto store = [&](int grp) {
+    astore();
+    xstore(grp);
+  };
+  // DB: A fragments of taps [t0, t0 + nt) of channel block grp, global -> LDS buffer dst by DMA
+  // (1 KB per wave-instruction: 64 lanes x 16 B of one (tap, m, hi|lo) fragment, lane-linear)
+  auto dma = [&](int grp, int t0, int nt, f32x4v* dst) {
+    typedef __attribute__((address_space(1))) void* gptr_t;
+    typedef __attribute__((address_space(3))) void* lptr_t;
+    for (int i = wave; i < nt * MT * 2; i += NTH / 64) {
+      const int tl = i / (MT * 2), j = i - tl * (MT * 2);
+      const int tap = t0 + tl, wt = xt.rev ? K - 1 - tap : tap;
+      const float* src = wfrag_ + ((size_t)(wt * xt.cs + grp) * a.mt_total + m0) * 512 + j * 256 + lane * 4;
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + (size_t)i * 64), 16, 0, 0);
     }
   };
 
@@ -558,13 +593,13 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
 
   const int ngrp = xt.cs / CB;
   // taps [T0, T1) of the staged channel blocks (A fragments of tap t at slot t - T0)
-  auto mma_taps = [&](auto t0c, auto t1c) {
+  auto mma_taps = [&](auto t0c, auto t1c, const f32x4v* abase) {
     constexpr int T0 = decltype(t0c)::value, T1 = decltype(t1c)::value;
 #pragma unroll
     for (int c = 0; c < CB; ++c)
 #pragma unroll
       for (int tap = T0; tap < T1; ++tap) {
-        const u32x4v* sa = reinterpret_cast<const u32x4v*>(s_a) + (size_t)(c * KS + tap - T0) * MT * 128 + lane;
+        const u32x4v* sa = reinterpret_cast<const u32x4v*>(abase) + (size_t)(c * KS + tap - T0) * MT * 128 + lane;
         u32x4v bh[NC], bl[NC];
 #pragma unroll
         for (int nc = 0; nc < NC; ++nc) {
@@ -590,18 +625,60 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
         }
       }
   };
-  if constexpr (SY) {
+  if constexpr (DB) {
+    // tap groups h = 0 .. NH-1 of KS taps ([h KS, min(K, h KS + KS))); global group g = grp NH + h
+    // computes from buffer g & 1 while the DMA of group g + 1 fills the other buffer
+    constexpr int NH = (K + KS - 1) / KS;
+    dma(0, 0, KS, s_a);
+    xload(0);
+    xstore(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int grp = 0; grp < ngrp; ++grp) {
+      const bool more = grp + 1 < ngrp;
+      auto stage = [&](auto hc) {
+        constexpr int h = decltype(hc)::value;
+        constexpr int T0 = h * KS, T1 = (h + 1) * KS < K ? (h + 1) * KS : K;
+        const int g = grp * NH + h;
+        f32x4v* const cur = (g & 1) ? s_a1 : s_a;
+        f32x4v* const nxt = (g & 1) ? s_a : s_a1;  // read last by group g - 1, before the barrier
+        if constexpr (h + 1 < NH) {
+          constexpr int T2 = (h + 2) * KS < K ? (h + 2) * KS : K;
+          dma(grp, T1, T2 - T1, nxt);
+        } else if (more) {
+          dma(grp + 1, 0, KS, nxt);
+          if constexpr (MT < 4) xload(grp + 1);  // MT 4: after the MFMAs (128 VGPRs hold no prefetch)
+        }
+        mma_taps(std::integral_constant<int, T0>{}, std::integral_constant<int, T1>{}, cur);
+        if constexpr (h + 1 < NH) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __syncthreads();
+        } else if (more) {
+          __syncthreads();  // every wave is done with this block's input rows
+          if constexpr (MT >= 4) xload(grp + 1);
+          xstore(grp + 1);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __syncthreads();
+        }
+      };
+      stage(std::integral_constant<int, 0>{});
+      if constexpr (NH > 1) stage(std::integral_constant<int, (NH > 1 ? 1 : 0)>{});
+      if constexpr (NH > 2) stage(std::integral_constant<int, (NH > 2 ? 2 : 0)>{});
+      if constexpr (NH > 3) stage(std::integral_constant<int, (NH > 3 ? 3 : 0)>{});
+      static_assert(NH <= 4, "at most four tap groups");
+    }
+  } else if constexpr (SY) {
     constexpr int NH = (K + KS - 1) / KS;
     stage_sync(0, 0);
     __syncthreads();
     for (int grp = 0; grp < ngrp; ++grp) {
       const bool more = grp + 1 < ngrp;
-      mma_taps(std::integral_constant<int, 0>{}, std::integral_constant<int, KS < K ? KS : K>{});
+      mma_taps(std::integral_constant<int, 0>{}, std::integral_constant<int, KS < K ? KS : K>{}, s_a);
       if constexpr (NH > 1) {
         __syncthreads();
         stage_sync(grp, 1);
         __syncthreads();
-        mma_taps(std::integral_constant<int, KS>{}, std::integral_constant<int, K>{});
+        mma_taps(std::integral_constant<int, KS>{}, std::integral_constant<int, K>{}, s_a);
       }
       if (!more) break;
       __syncthreads();
@@ -616,7 +693,7 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
       const bool more = grp + 1 < ngrp;
       if (more) load(grp + 1);
       __builtin_amdgcn_sched_barrier(0);
-      mma_taps(std::integral_constant<int, 0>{}, std::integral_constant<int, K>{});
+      mma_taps(std::integral_constant<int, 0>{}, std::integral_constant<int, K>{}, s_a);
       __builtin_amdgcn_sched_barrier(0);
       if (!more) break;
       __syncthreads();
@@ -685,12 +762,12 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
   }
 }
 
-template <int MT, int K, int CB, int NC = 1, bool SY = false, int KS = K>
+template <int MT, int K, int CB, int NC = 1, bool SY = false, int KS = K, bool DB = false>
 hipError_t xtile_launch_k(dim3 grid, int lds, hipStream_t s, const CnConvArgs& a, const CnXtileArgs& xt) {
-  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(pwg_cnet_xtile_kernel<MT, K, CB, NC, SY, KS>),
+  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(pwg_cnet_xtile_kernel<MT, K, CB, NC, SY, KS, DB>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((pwg_cnet_xtile_kernel<MT, K, CB, NC, SY, KS>), grid, dim3(512), (size_t)lds, s, a, xt);
+  hipLaunchKernelGGL((pwg_cnet_xtile_kernel<MT, K, CB, NC, SY, KS, DB>), grid, dim3(512), (size_t)lds, s, a, xt);
   return hipGetLastError();
 }
 template <int MT>
@@ -720,8 +797,62 @@ hipError_t xtile_launch_mt(int k, dim3 grid, int lds, hipStream_t s, const CnCon
     default: return hipErrorInvalidValue;
   }
 }
+// DMA-staged launches: KS = K, or tap groups of ceil(K / NH) for NH = 2..4 at >= 64 rows
+template <int MT, int K, int KS>
+hipError_t xtile_launch_db_ks(dim3 grid, int lds, hipStream_t s, const CnConvArgs& a, const CnXtileArgs& xt) {
+  return xtile_launch_k<MT, K, 1, 1, false, KS, true>(grid, lds, s, a, xt);
+}
+template <int MT>
+hipError_t xtile_launch_db(int k, int ks, dim3 grid, int lds, hipStream_t s, const CnConvArgs& a,
+                           const CnXtileArgs& xt) {
+  if (ks == k) {
+    switch (k) {
+      case 2:  // ConvTranspose phases (3 or 4 m-tiles)
+        if constexpr (MT >= 3) return xtile_launch_db_ks<MT, 2, 2>(grid, lds, s, a, xt);
+        return hipErrorInvalidValue;
+      case 3: return xtile_launch_db_ks<MT, 3, 3>(grid, lds, s, a, xt);
+      case 5: return xtile_launch_db_ks<MT, 5, 5>(grid, lds, s, a, xt);
+      case 7: return xtile_launch_db_ks<MT, 7, 7>(grid, lds, s, a, xt);
+      case 11: return xtile_launch_db_ks<MT, 11, 11>(grid, lds, s, a, xt);
+      default: return hipErrorInvalidValue;
+    }
+  }
+  if constexpr (MT >= 2) {
+    if (k == 3 && ks == 2) return xtile_launch_db_ks<MT, 3, 2>(grid, lds, s, a, xt);
+    if (k == 5 && ks == 3) return xtile_launch_db_ks<MT, 5, 3>(grid, lds, s, a, xt);
+    if (k == 7 && ks == 4) return xtile_launch_db_ks<MT, 7, 4>(grid, lds, s, a, xt);
+    if (k == 7 && ks == 3) return xtile_launch_db_ks<MT, 7, 3>(grid, lds, s, a, xt);
+    if (k == 11 && ks == 6) return xtile_launch_db_ks<MT, 11, 6>(grid, lds, s, a, xt);
+    if (k == 11 && ks == 4) return xtile_launch_db_ks<MT, 11, 4>(grid, lds, s, a, xt);
+    if (k == 11 && ks == 3) return xtile_launch_db_ks<MT, 11, 3>(grid, lds, s, a, xt);
+  }
+  return hipErrorInvalidValue;
+}
+// the tap-group sizes xtile_launch_db instantiates for kernel size k (ks == k first)
+inline int db_ks_options(int k, int mt, int* out) {
+  int n = 0;
+  out[n++] = k;
+  if (mt < 2) return n;
+  switch (k) {
+    case 3: out[n++] = 2; break;
+    case 5: out[n++] = 3; break;
+    case 7: out[n++] = 4; out[n++] = 3; break;
+    case 11: out[n++] = 6; out[n++] = 4; out[n++] = 3; break;
+    default: break;
+  }
+  return n;
+}
 hipError_t xtile_launch(int mt, int k, bool sync, int ks, dim3 grid, int lds, hipStream_t s, const CnConvArgs& a,
-                        const CnXtileArgs& xt) {
+                        const CnXtileArgs& xt, bool db = false) {
+  if (db) {
+    switch (mt) {
+      case 1: return xtile_launch_db<1>(k, ks, grid, lds, s, a, xt);
+      case 2: return xtile_launch_db<2>(k, ks, grid, lds, s, a, xt);
+      case 3: return xtile_launch_db<3>(k, ks, grid, lds, s, a, xt);
+      case 4: return xtile_launch_db<4>(k, ks, grid, lds, s, a, xt);
+      default: return hipErrorInvalidValue;
+    }
+  }
   if (sync) {
     switch (mt) {
       case 2: return xtile_launch_sync<2>(k, ks, grid, lds, s, a, xt);
@@ -1833,7 +1964,6 @@ __global__ void __launch_bounds__(256) pwg_cnet_pair_kernel(const CnPairArgs a) 
       if (live) {
 #pragma unroll
         for (int j4 = 0; j4 < 4; ++j4) {
-          const int row = 8 * j4 + 4 * hh;
           const f32x4v b = rb2[j4];
           f32x4v v;
 #pragma unroll
@@ -2266,6 +2396,12 @@ struct OpPhase {          // one launch
   int xt_lds = 0;
   bool xt_sync = false;   // synchronous staging at 128 VGPRs (two workgroups per CU)
   int xt_ks = 0;          // with xt_sync: taps staged per step (the kernel size unless split)
+  bool xt_db = false;     // PWG_CNET_OPT_XT_DMA applies: double-buffered DMA staging of the A fragments
+  bool xt_db_pick = false; // ... and the measured rule picks it (option value 1)
+  bool xt_convt_db = false;  // wide ConvTranspose phase (> 2 m-tiles): tap-major kernel, or the DMA
+                             // x-tile kernel over 256-column blocks (d_xblocks) when PWG_CNET_OPT_XT_DMA
+  int xt_db_ks[2] = {0, 0}, xt_db_lds[2] = {0, 0};  // taps per tap group and LDS bytes: [0] the fewest
+                                                     // groups within 80 KB (two workgroups per CU), [1] within 160 KB
   int z_phases = 1;       // CONVT phase 0: phases launched together (gridDim.z); others: 0 (merged)
   int xpair_b = -1;       // x-tile conv pair: phase index of conv 2 (pwg_cnet_xpair_kernel)
   int xpair_lds = 0;
@@ -2295,6 +2431,7 @@ struct PwgCnet {
   int fuse_pairs = 1; // PWG_CNET_OPT_FUSE_PAIRS (split-f16 mode only)
   int pair_steps = 16; // PWG_CNET_OPT_PAIR_STEPS: 128-column tiles per fused-pair strip (plan time)
   int xtile = 1;       // PWG_CNET_OPT_XTILE
+  int xt_dma = 9;      // PWG_CNET_OPT_XT_DMA flags (CNET_DMA_RULE | CNET_DMA_CONVT)
   bool pair_attr_set = false;
   std::vector<PwgCnetOp> ops;
   std::vector<int> channels, rate, ld;
@@ -2521,6 +2658,11 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
         // one 16-channel block per staging step (2 or 4 measured 1 % slower, r02_xt5)
         const int span = XT_COLS + (xk - 1) * xd;
         ph.xt_lds = xk * MT * 2048 + span * XT_ROWB;
+      } else if (convt && nsrc == 1 && (MT == 3 || MT == 4) && mt_total % MT == 0 && op.src[0].channels % 16 == 0) {
+        ph.xt_convt_db = true;  // 2 taps: both tap groups' A (2 x MT x 4 KB) + 257 input rows, <= 53 KB
+        ph.xt_db = ph.xt_db_pick = true;
+        ph.xt_db_ks[0] = ph.xt_db_ks[1] = 2;
+        ph.xt_db_lds[0] = ph.xt_db_lds[1] = 2 * 2 * MT * 2048 + (XT_COLS + 1) * XT_ROWB;
       }
       ph.ostride = op.kind == PWG_CNET_CONVT ? op.stride : 1;
       ph.ophase = r;
@@ -2739,9 +2881,33 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
         ph.stack_b >= 0 || ph.xpair_b >= 0 || (i > 0 && n->phases[i - 1].xpair_b == (int)i) ||
         !xtile_supported(op.src[0].taps))
       continue;
-    if (!(ph.MT >= 3 || (ph.MT == 2 && op.src[0].taps >= 11))) continue;
     const int K = op.src[0].taps;
     const int span = XT_COLS + (K - 1) * op.src[0].dilation;
+    // DMA-staged variant: two A buffers of one tap group each + the input rows; the fewest tap
+    // groups that fit two workgroups per CU (80 KB), else one workgroup per CU
+    {
+      int opts[4];
+      const int nopt = db_ks_options(K, ph.MT, opts);
+      for (int pass = 1; pass >= 0; --pass)
+        for (int oi2 = 0; oi2 < nopt; ++oi2) {
+          const int lds = 2 * opts[oi2] * ph.MT * 2048 + span * XT_ROWB;
+          if (lds > (pass == 0 ? 80 * 1024 : 160 * 1024)) continue;
+          ph.xt_db = true;
+          ph.xt_db_ks[pass] = opts[oi2];
+          ph.xt_db_lds[pass] = lds;
+          break;
+        }
+      if (ph.xt_db && ph.xt_db_ks[0] == 0) {  // nothing fits 80 KB: the 160 KB choice for both
+        ph.xt_db_ks[0] = ph.xt_db_ks[1];
+        ph.xt_db_lds[0] = ph.xt_db_lds[1];
+      }
+      // measured (r03_dma, same box, bit-identical): DMA staging wins at >= 96 rows per workgroup
+      // for k >= 7 (HiFiGAN's 128/256-ch k = 7/11: -3..9 %) and for k = 3 up to 192 channels
+      // (MB-MelGAN 192-ch -13..19 %, MelGAN 128-ch -3..13 %); it loses at 256-ch k = 3 (+4..8 %)
+      // and at 64-row workgroups
+      ph.xt_db_pick = ph.xt_db && ph.MT >= 3 && (K >= 7 || ph.mt_total <= 6);
+    }
+    if (!(ph.MT >= 3 || (ph.MT == 2 && op.src[0].taps >= 11))) continue;
     if (2 * ph.xt_lds <= 160 * 1024) {
       ph.xt_sync = true;
       ph.xt_ks = K;
@@ -2956,7 +3122,7 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
     p->d_strips.push_back(dstr);
     p->n_strips.push_back((int)strips.size());
     std::vector<int2> xblocks;
-    if (ph.xpair_b >= 0 || (ph.stack_b >= 0 && ph.xtile)) {
+    if (ph.xpair_b >= 0 || (ph.stack_b >= 0 && ph.xtile) || ph.xt_convt_db) {
       const int step = ph.xpair_b >= 0 ? XP_OUT : XT_COLS;
       for (int u = 0; u < n_utts; ++u)
         for (int q0 = 0; q0 < ncols[u]; q0 += step) xblocks.push_back(make_int2(u, q0));
@@ -3200,7 +3366,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
           const hipError_t ea2 = xpair_launch(ph.MT, xp.K1, dim3((unsigned)p->n_xblocks[pi]), ph.xpair_lds, s, a, xp);
           if (ea2 != hipSuccess) return hipf(ea2, "xpair kernel launch");
         }
-      } else if (xt && ph.xtile) {
+      } else if (xt && (ph.xtile || (ph.xt_convt_db && (n->xt_dma & CNET_DMA_CONVT)))) {
         CnXtileArgs xt;
         const bool convt = op.kind == PWG_CNET_CONVT;
         xt.K = convt ? 2 : op.src[0].taps; xt.dil = convt ? 1 : op.src[0].dilation;
@@ -3210,12 +3376,16 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         for (int r = 0; r < 8; ++r)
           xt.z_off[r] = convt && r < ph.z_phases ? n->phases[pi + r].off_a - 1 : xt.off_min;
         dim3 xgrid = grid;
-        // stack op A: 128-column d_blocks belong to the tap-major stack kernel
-        if (ph.stack_b >= 0) {
+        // stack op A / wide ConvTranspose: 128-column d_blocks belong to the tap-major kernels
+        if (ph.stack_b >= 0 || ph.xt_convt_db) {
           a.blocks = p->d_xblocks[pi];
           xgrid.x = (unsigned)p->n_xblocks[pi];
         }
-        const hipError_t ea2 = xtile_launch(ph.MT, xt.K, ph.xt_sync, ph.xt_ks, xgrid, ph.xt_lds, s, a, xt);
+        const bool db = ph.xt_convt_db ||
+                        (ph.xt_db && ((n->xt_dma & CNET_DMA_ALL) || ((n->xt_dma & CNET_DMA_RULE) && ph.xt_db_pick)));
+        const int dv = (n->xt_dma & CNET_DMA_FEWEST) ? 1 : 0;
+        const hipError_t ea2 = db ? xtile_launch(ph.MT, xt.K, false, ph.xt_db_ks[dv], xgrid, ph.xt_db_lds[dv], s, a, xt, true)
+                                  : xtile_launch(ph.MT, xt.K, ph.xt_sync, ph.xt_ks, xgrid, ph.xt_lds, s, a, xt);
         if (ea2 != hipSuccess) return hipf(ea2, "xtile kernel launch");
       } else if (split) {
         switch (ph.MT) {
@@ -3299,11 +3469,15 @@ int pwg_cnet_set_option(PwgCnet* n, int option, long long value) {
     n->pair_steps = (int)value;
     return PWG_OK;
   }
-  if (option != PWG_CNET_OPT_SPLIT_F16 && option != PWG_CNET_OPT_FUSE_PAIRS && option != PWG_CNET_OPT_XTILE)
-    return fail(PWG_ERR_INVALID, "unknown option");
-  if (value != 0 && value != 1) return fail(PWG_ERR_INVALID, "option value must be 0 or 1");
-  (option == PWG_CNET_OPT_SPLIT_F16 ? n->split_f16 : option == PWG_CNET_OPT_FUSE_PAIRS ? n->fuse_pairs : n->xtile) =
-      (int)value;
+  int* slot = option == PWG_CNET_OPT_SPLIT_F16   ? &n->split_f16
+              : option == PWG_CNET_OPT_FUSE_PAIRS ? &n->fuse_pairs
+              : option == PWG_CNET_OPT_XTILE      ? &n->xtile
+              : option == PWG_CNET_OPT_XT_DMA     ? &n->xt_dma
+                                                  : nullptr;
+  if (!slot) return fail(PWG_ERR_INVALID, "unknown option");
+  if (value != 0 && value != 1 && !(option == PWG_CNET_OPT_XT_DMA && value >= 0 && value <= 15))
+    return fail(PWG_ERR_INVALID, "option value must be 0 or 1 (PWG_CNET_OPT_XT_DMA: flags 0 - 15)");
+  *slot = (int)value;
   return PWG_OK;
 }
 

@@ -326,9 +326,12 @@ class Engine:
         key = stream.cuda_stream
         ws = self._workspaces.get(key)
         if ws is None or ws.numel() < nbytes:
+            # grow geometrically (x1.5): a run of growing batch shapes reallocates O(log) times
+            grow = int(ws.numel() * 1.5) if ws is not None else 0
             self._workspaces.pop(key, None)
+            ws = None
             with torch.cuda.stream(stream):
-                ws = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=self.device)
+                ws = torch.empty(max(int(nbytes), grow, 256), dtype=torch.uint8, device=self.device)
             self._workspaces[key] = ws
         return ws
 

@@ -266,3 +266,41 @@ def test_xtile_kernel_matches_tap_major(cfg, built_lib, cuda_device):
         got = [y.cpu().numpy() for y in m.inference_batch(mels)]
     for a, b in zip(got, ref):
         assert np.abs(a - b).max() < 1e-5
+
+
+@pytest.mark.parametrize("cfg", ["hifigan_v1", "mb_melgan_v2", "melgan_v1", "hifigan_v1_causal"])
+def test_xtile_dma_staging_bitwise_equal(cfg, built_lib, cuda_device):
+    """PWG_CNET_OPT_XT_DMA: x-tile convs with their weight fragments DMA-staged (global_load_lds,
+    two LDS buffers, tap groups sized for one or two workgroups per CU) run the same MFMAs in the
+    same order as the register-staged kernels: bit-identical, on the measured rule's shapes and on
+    every eligible conv, on ragged batches whose utterances are shorter than, equal to and longer
+    than one 256-column tile. The wide ConvTranspose phases on the DMA kernel (flag 8, in every arm
+    here) sum channel-block-major where the tap-major kernel sums tap-major: the two agree to fp32
+    rounding (|d| < 1e-5)."""
+    from parallelwavegan_amd import configs, synthetic
+    from parallelwavegan_amd.cnet import CnetEngine
+    from parallelwavegan_amd.hifigan import HiFiGANGenerator
+    from parallelwavegan_amd.melgan import PQMF, MelGANGenerator
+
+    cls_name, params = configs.vocoder_params(cfg)
+    m = {"MelGANGenerator": MelGANGenerator, "HiFiGANGenerator": HiFiGANGenerator}[cls_name](**params)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic.make_module_state_dict(m, seed=7).items()})
+    if cfg in configs.VOCODER_PQMF:
+        m.pqmf = PQMF(**configs.VOCODER_PQMF[cfg])
+    m = m.to(cuda_device)
+    eng = m.engine()
+    mels = [synthetic.make_mel(f, 80, seed=120 + i) for i, f in enumerate([4, 5, 37, 9, 130])]
+    C = CnetEngine
+    outs = {}
+    with torch.no_grad():
+        for mode in (C.XT_DMA_CONVT, C.XT_DMA_CONVT | C.XT_DMA_RULE, C.XT_DMA_CONVT | C.XT_DMA_ALL,
+                     C.XT_DMA_CONVT | C.XT_DMA_ALL | C.XT_DMA_FEWEST, 0):
+            eng.set_xt_dma(mode)
+            outs[mode] = [y.cpu().numpy() for y in m.inference_batch(mels)]
+        eng.set_xt_dma(C.XT_DMA_CONVT | C.XT_DMA_RULE)
+    ref = outs[C.XT_DMA_CONVT]
+    for mode in (9, 10, 14):
+        for a, b in zip(outs[mode], ref):
+            np.testing.assert_array_equal(a, b)
+    for a, b in zip(outs[0], ref):
+        assert np.abs(a - b).max() < 1e-5

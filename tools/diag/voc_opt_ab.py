@@ -1,6 +1,6 @@
 """Per-op time of a vocoder program under two option settings (diagnostic, GPU box): same plan,
 same input, interleaved repetitions; prints the per-op ms of both and the step totals, and checks
-the outputs bitwise. Usage: python tools/diag/voc_opt_ab.py CONFIG OPTION [reps] [on-value]
+the outputs bitwise. Usage: python tools/diag/voc_opt_ab.py CONFIG OPTION [reps] [on-value] [off-value]
 (OPTION = a CnetEngine setter name, e.g. set_xt_dma)"""
 import os
 import sys
@@ -16,6 +16,7 @@ from parallelwavegan_amd.melgan import PQMF, MelGANGenerator  # noqa: E402
 cfg, opt = sys.argv[1], sys.argv[2]
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
 val_on = int(sys.argv[4]) if len(sys.argv) > 4 else 1  # the setter's "on" value
+val_off = int(sys.argv[5]) if len(sys.argv) > 5 else 0  # ... and its "off" value
 cls, p = configs.vocoder_params(cfg)
 m = {"MelGANGenerator": MelGANGenerator, "HiFiGANGenerator": HiFiGANGenerator}[cls](**p)
 m.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic.make_module_state_dict(m, seed=0).items()})
@@ -32,7 +33,7 @@ tot = {0: [], 1: []}
 per = {0: None, 1: None}
 for r in range(reps + 1):
     for v in (0, 1):
-        getattr(eng, opt)(val_on if v else 0)
+        getattr(eng, opt)(val_on if v else val_off)
         out = torch.empty(plan.out_rows * eng.out_channels, device=dev)
         eng.set_timing(True)
         eng.collect_timing()
@@ -49,7 +50,8 @@ for r in range(reps + 1):
         else:
             for row, (_, ms, _) in zip(per[v], t):
                 row[1] = min(row[1], ms)
-print(cfg, opt, "bitwise equal:", bool(np.array_equal(outs[0], outs[1])))
+print(cfg, opt, val_off, "->", val_on, "bitwise equal:", bool(np.array_equal(outs[0], outs[1])),
+      "max|d|", float(np.abs(outs[0] - outs[1]).max()))
 print(f"step ms  off {min(tot[0]):.3f}  on {min(tot[1]):.3f}")
 for (name, a, n), (_, b, _) in zip(per[0], per[1]):
     if a > 0.05 or b > 0.05:
