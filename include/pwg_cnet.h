@@ -128,9 +128,12 @@ PWG_API int pwg_cnet_run_status(PwgCnetPlan* p, const void* workspace, void* str
  * k = 3 up to 192 channels); 2: every eligible conv; 4: the fewest tap groups (one workgroup per
  * CU) instead of groups sized for two; these are bit-identical to the register-staged x-tile
  * kernels. 8: the wide (> 64 output channels) ConvTranspose phases on this kernel instead of the
- * tap-major one (channel-block-major summation: parity to the oracle, not bit identity). */
+ * tap-major one (channel-block-major summation: parity to the oracle, not bit identity).
+ * PWG_CNET_OPT_XCD_ORDER (default 1): launches with several m-groups or ConvTranspose phases per
+ * column block deal a block's siblings to one XCD in consecutive rounds, so they share its L2
+ * instead of each fetching the block's input rows from HBM (0: grid order; same results). */
 enum { PWG_CNET_OPT_SPLIT_F16 = 0, PWG_CNET_OPT_FUSE_PAIRS = 1, PWG_CNET_OPT_PAIR_STEPS = 2, PWG_CNET_OPT_XTILE = 3,
-       PWG_CNET_OPT_XT_DMA = 4 };
+       PWG_CNET_OPT_XT_DMA = 4, PWG_CNET_OPT_XCD_ORDER = 5 };
 PWG_API int pwg_cnet_set_option(PwgCnet* n, int option, long long value);
 PWG_API int pwg_cnet_set_timing(PwgCnet* n, int enable);
 /* Adds per-op milliseconds and launch counts (arrays of n_ops) and clears the records. */

@@ -419,6 +419,11 @@ class CnetEngine:
         4 the fewest tap groups; 8 the wide ConvTranspose phases on that kernel. Default 9."""
         _lib.check(self._lib.pwg_cnet_set_option(self._h, 4, int(mode)))
 
+    def set_xcd_order(self, enable):
+        """pwg_cnet_set_option(PWG_CNET_OPT_XCD_ORDER): the m-groups / ConvTranspose phases of one
+        column block run on one XCD back to back, sharing its L2 (default on; same results)."""
+        _lib.check(self._lib.pwg_cnet_set_option(self._h, 5, int(bool(enable))))
+
     def set_pair_steps(self, steps):
         """pwg_cnet_set_option(PWG_CNET_OPT_PAIR_STEPS): 128-column tiles per fused-pair
         workgroup, for plans created afterwards (cached plans are dropped)."""

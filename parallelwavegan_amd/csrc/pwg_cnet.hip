@@ -108,7 +108,36 @@ struct CnConvArgs {
   const float* z_bias[8];
   int* range_flag;        // thin kernel writing the program output (split-f16 mode): set to 1 on a
                           // non-finite output value (pwg_cnet_run_status), else null
+  int xcd_order;          // 1: XCD-aware tile order (xcd_tile), PWG_CNET_OPT_XCD_ORDER
 };
+
+// Workgroup -> (column block, m-group, ConvTranspose phase). Workgroup ids are dispatched x-fastest
+// and dealt round-robin over the 8 XCDs, each with its own L2: in grid order the m-groups and phases
+// of one column block (which stage the same input rows) land on different XCDs, nx dispatches apart,
+// and each re-fetches those rows from HBM. The XCD-aware order deals the ny x nz siblings of a
+// column block to ONE XCD in consecutive rounds (ids L, L + 8, ...), where the later ones find the
+// rows in L2. A bijection over the grid (the last partial group of 8 column blocks keeps a plain
+// order); the tiles, and so the results, are the same.
+struct TileId { int x, y, z; };
+__device__ __forceinline__ TileId xcd_tile(int enable) {
+  const int nx = gridDim.x, ns = gridDim.y * gridDim.z;
+  if (!enable || ns == 1) return {(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
+  const long long L = blockIdx.x + (long long)nx * (blockIdx.y + (long long)gridDim.y * blockIdx.z);
+  const long long G = 8LL * ns, full = nx / 8;
+  const long long g = L / G;
+  int x, sib;
+  if (g < full) {
+    const int r = (int)(L - g * G);
+    x = (int)(g * 8) + (r & 7);
+    sib = r >> 3;
+  } else {
+    const int tail = nx - (int)(full * 8);
+    const int r = (int)(L - full * G);
+    x = (int)(full * 8) + r % tail;
+    sib = r / tail;
+  }
+  return {x, sib % (int)gridDim.y, sib / (int)gridDim.y};
+}
 
 __device__ __forceinline__ int reflect_row(int p, int T) {
   p = p < 0 ? -p : p;
@@ -153,13 +182,14 @@ __global__ void __launch_bounds__(64 * NW) pwg_cnet_conv_kernel(const CnConvArgs
   const int wave = threadIdx.x >> 6;
   const int hh = lane >> 5;
   const int cl = lane & 31;
-  const int2 blk = a.blocks[blockIdx.x];
+  const TileId tid = xcd_tile(a.xcd_order);
+  const int2 blk = a.blocks[tid.x];
   const int u = blk.x;
   const int qb = blk.y + wave * 32 * NT + cl;  // this lane's column in n-tile 0 (phase index space)
   const int nq = a.ncols[u];
-  const int m0 = blockIdx.y * MT;              // first m-tile of this workgroup
+  const int m0 = tid.y * MT;                   // first m-tile of this workgroup
   // ConvTranspose phase of this workgroup (all phases in one launch; 0 for plain convs)
-  const int zp = blockIdx.z;
+  const int zp = tid.z;
   const ChunkDesc* const chunks_ = zp == 0 ? a.chunks : a.z_chunks[zp];
   const float* const wfrag_ = zp == 0 ? a.wfrag : a.z_wfrag[zp];
   const float* const bias_ = zp == 0 ? a.bias : a.z_bias[zp];
@@ -434,12 +464,13 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
   const int wave = threadIdx.x >> 6;
   const int hh = lane >> 5;
   const int cl = lane & 31;
-  const int2 blk = a.blocks[blockIdx.x];
+  const TileId tid = xcd_tile(a.xcd_order);
+  const int2 blk = a.blocks[tid.x];
   const int u = blk.x;
   const int q0 = blk.y;
   const int nq = a.ncols[u];
-  const int m0 = blockIdx.y * MT;
-  const int zp = blockIdx.z;  // ConvTranspose phase (0 for convs)
+  const int m0 = tid.y * MT;
+  const int zp = tid.z;  // ConvTranspose phase (0 for convs)
   // column tiles holding live columns (uniform over the workgroup)
   const int nc_live = NC == 1 ? 1 : (nq - q0 > XT_COLS ? NC : 1);
   const float* const wfrag_ = zp == 0 ? a.wfrag : a.z_wfrag[zp];
@@ -2432,6 +2463,7 @@ struct PwgCnet {
   int pair_steps = 16; // PWG_CNET_OPT_PAIR_STEPS: 128-column tiles per fused-pair strip (plan time)
   int xtile = 1;       // PWG_CNET_OPT_XTILE
   int xt_dma = 9;      // PWG_CNET_OPT_XT_DMA flags (CNET_DMA_RULE | CNET_DMA_CONVT)
+  int xcd_order = 1;   // PWG_CNET_OPT_XCD_ORDER
   bool pair_attr_set = false;
   std::vector<PwgCnetOp> ops;
   std::vector<int> channels, rate, ld;
@@ -3308,6 +3340,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
     } else if (p->n_blocks[pi] > 0) {
       CnConvArgs a;
       a.range_flag = nullptr;
+      a.xcd_order = n->xcd_order;
       const int nsrc = (op.src[1].buf >= 0 && op.kind == PWG_CNET_CONV) ? 2 : 1;
       for (int si = 0; si < 2; ++si) {
         const PwgCnetSrc& src = op.src[si];
@@ -3473,6 +3506,7 @@ int pwg_cnet_set_option(PwgCnet* n, int option, long long value) {
               : option == PWG_CNET_OPT_FUSE_PAIRS ? &n->fuse_pairs
               : option == PWG_CNET_OPT_XTILE      ? &n->xtile
               : option == PWG_CNET_OPT_XT_DMA     ? &n->xt_dma
+              : option == PWG_CNET_OPT_XCD_ORDER  ? &n->xcd_order
                                                   : nullptr;
   if (!slot) return fail(PWG_ERR_INVALID, "unknown option");
   if (value != 0 && value != 1 && !(option == PWG_CNET_OPT_XT_DMA && value >= 0 && value <= 15))

@@ -304,3 +304,32 @@ def test_xtile_dma_staging_bitwise_equal(cfg, built_lib, cuda_device):
             np.testing.assert_array_equal(a, b)
     for a, b in zip(outs[0], ref):
         assert np.abs(a - b).max() < 1e-5
+
+
+@pytest.mark.parametrize("cfg", ["hifigan_v1", "melgan_v1", "mb_melgan_v2"])
+def test_xcd_tile_order_bitwise_equal(cfg, built_lib, cuda_device):
+    """PWG_CNET_OPT_XCD_ORDER only permutes which workgroup computes which (column block, m-group,
+    ConvTranspose phase) tile: bit-identical output, with and without the DMA x-tile kernels, on
+    a ragged batch whose block counts are not multiples of 8 (the bijection's tail)."""
+    from parallelwavegan_amd import configs, synthetic
+    from parallelwavegan_amd.hifigan import HiFiGANGenerator
+    from parallelwavegan_amd.melgan import PQMF, MelGANGenerator
+
+    cls_name, params = configs.vocoder_params(cfg)
+    m = {"MelGANGenerator": MelGANGenerator, "HiFiGANGenerator": HiFiGANGenerator}[cls_name](**params)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic.make_module_state_dict(m, seed=8).items()})
+    if cfg in configs.VOCODER_PQMF:
+        m.pqmf = PQMF(**configs.VOCODER_PQMF[cfg])
+    m = m.to(cuda_device)
+    eng = m.engine()
+    mels = [synthetic.make_mel(f, 80, seed=140 + i) for i, f in enumerate([7, 61, 4, 23, 150])]
+    with torch.no_grad():
+        for dma in (0, 9):
+            eng.set_xt_dma(dma)
+            outs = []
+            for order in (0, 1):
+                eng.set_xcd_order(order)
+                outs.append([y.cpu().numpy() for y in m.inference_batch(mels)])
+            for a, b in zip(*outs):
+                np.testing.assert_array_equal(a, b)
+        eng.set_xt_dma(9)
