@@ -2266,7 +2266,10 @@ __global__ void __launch_bounds__(256) pwg_cnet_pair_stream_kernel(const CnPairA
 // The staged tile is dynamic LDS sized by the phase's span (a fixed 640-row array held 40 KB per
 // 2-wave workgroup: 4 workgroups per CU).
 constexpr int THIN_MAX_SPAN = 128 + 512;
-constexpr int THIN_ROW = 16;
+// staged row stride in floats: 16 channels + 4 of pad. At 16 (64 B) the per-lane row reads
+// (ds_read_b128, lane i at 64 i + 16 j bytes) hit the same banks every 4 lanes (69 % of LDS cycles
+// were bank conflicts, r02_voc_pmc); 80-B rows put 16 lanes on 16 disjoint 4-bank groups
+constexpr int THIN_ROW = 20;
 template <int M>
 __global__ void __launch_bounds__(128) pwg_cnet_thin_kernel(const CnConvArgs a, int nsrc) {
   extern __shared__ __attribute__((aligned(16))) float s_x[];  // [span][THIN_ROW]
