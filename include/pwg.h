@@ -198,14 +198,20 @@ enum {
   PWG_OPT_WG_PER_CU = 2,      /* persistent kernel: workgroups per CU in the grid (default 1) */
   PWG_OPT_FUSE_FIRST_CONV = 3, /* split16 layer kernel: first_conv evaluated inside layer 0 from the
                                     noise, x0 never stored (default 1; bit-identical to 0) */
-  PWG_OPT_PIPELINE = 4         /* split16: plans with at most this many padded samples run all
+  PWG_OPT_PIPELINE = 4,        /* split16: plans with at most this many padded samples run all
                                     residual layers in ONE layer-pipelined launch (each CU keeps one
                                     layer's weights; blocks flow layer to layer through per-block
                                     progress words), bit-identical to the per-layer launches; the
                                     B = 1 decode path of bin/decode.py. 0 = never. Applies to plans
                                     created afterwards (default PWG_PIPE_MAX_DEFAULT). */
+  PWG_OPT_HALF_BLOCKS = 5      /* split16: launches of at most this many 32-sample blocks (every layer
+                                    but the last) take half blocks (16 columns) as work units: twice
+                                    the waves, half of a block's dependent MFMA chain per wave; the
+                                    B = 1 latency path. Bit-identical. 0 = never; default 4 x the
+                                    CU count (one unit per wave at 8 waves per CU: LJ T' = 64
+                                    0.42 -> 0.35 ms per forward; slower from ~4 blocks per CU on). */
 };
-#define PWG_PIPE_MAX_DEFAULT 0LL /* off: measured slower than the per-layer launches (DESIGN.md 3.6) */
+#define PWG_PIPE_MAX_DEFAULT 0LL /* off: measured slower than the per-layer launches (DESIGN.md 9) */
 PWG_API int pwg_set_option(PwgHandle* h, int option, long long value);
 /* Current value of an option (the layer kernel the handle picked for its shape, ...). */
 PWG_API int pwg_get_option(const PwgHandle* h, int option, long long* value);

@@ -98,6 +98,7 @@ PWG_OPT_WAVES_PER_WG = 1
 PWG_OPT_WG_PER_CU = 2
 PWG_OPT_FUSE_FIRST_CONV = 3
 PWG_OPT_PIPELINE = 4
+PWG_OPT_HALF_BLOCKS = 5
 
 
 class PwgConfig(ctypes.Structure):

@@ -315,6 +315,7 @@ struct PwgHandle {
   int layer_kernel = 0, waves_per_wg = 8, wg_per_cu = 1;
   int fuse_first = 1;  // PWG_OPT_FUSE_FIRST_CONV
   long long pipe_max = PWG_PIPE_MAX_DEFAULT;  // PWG_OPT_PIPELINE: largest padded plan on the layer pipeline
+  long long half_max = -1;  // PWG_OPT_HALF_BLOCKS: most blocks of a half-block launch (-1: 4 x n_cu)
   int n_cu = 0;
   // timing
   bool timing = false;
@@ -1047,8 +1048,12 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
     // CU with fewer waves per workgroup, rather than crowding the blocks into the first workgroups
     // of each XCD at 8 waves per CU.
     const long long nwg_all = (long long)h->n_cu * h->wg_per_cu;
+    // small plans on split16: half-block work units (PWG_OPT_HALF_BLOCKS), every layer but the last
+    const long long half_max = h->half_max >= 0 ? h->half_max : 4LL * h->n_cu;
+    const bool half = h->layer_kernel == 3 && l != h->L - 1 && la.n_blocks <= half_max;
+    const long long units = half ? 2 * la.n_blocks : la.n_blocks;
     int wpw = h->waves_per_wg;
-    if (PWG_SMALL_SPREAD && la.n_blocks < nwg_all * wpw) wpw = (int)std::max(1LL, (la.n_blocks + nwg_all - 1) / nwg_all);
+    if (PWG_SMALL_SPREAD && units < nwg_all * wpw) wpw = (int)std::max(1LL, (units + nwg_all - 1) / nwg_all);
     la.tile_utt = d_tile_utt; la.utts = d_utts; la.Tpad = p->Tpad;
     la.R = h->R; la.RS = h->RS; la.S = h->S; la.SS = h->SS; la.KS = h->KS; la.dil = h->dil[l];
     la.tap_center = h->cfg.use_causal_conv ? h->KS - 1 : (h->KS - 1) / 2;
@@ -1092,7 +1097,7 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
       // blocks each, the SIMD's issue arbitration lets one wave finish a block-time before its
       // partner and the launch waits for the later one (LJ T' = 512: 1.58 -> 1.47 ms per forward)
       const int launch_w = split16 ? std::min(8, h->waves_per_wg) : wpw;
-      if (split16 && la.n_blocks > 8LL * h->n_cu && la.n_blocks <= 32LL * h->n_cu) wpw = std::min(wpw, 4);
+      if (split16 && units > 8LL * h->n_cu && units <= 32LL * h->n_cu) wpw = std::min(wpw, 4);
       sa.compute_waves = std::min(wpw, launch_w);
       // diagnostic per-wave timeline (PWG_TRACE_FILE set; split16): every layer's records, dumped
       // after the last layer of the run (tools/trace_layer.py)
@@ -1105,7 +1110,7 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
         sa.trace = d_trace_s + per_layer_s * (l % 64);
       }
       e = timed(PWG_KERNEL_RESIDUAL_LAYER, [&] {
-        return split16 ? launch_layer_split16(sa, last, la.tap_center, launch_w, nwg, s)
+        return split16 ? launch_layer_split16(sa, last, la.tap_center, launch_w, nwg, s, half)
                        : launch_layer_split(sa, last, la.tap_center, wpw, nwg, s);
       });
       if (e == hipSuccess && last && trace_fn) {
@@ -1298,6 +1303,10 @@ int pwg_set_option(PwgHandle* h, int option, long long value) {
       if (value < 0) return fail(PWG_ERR_INVALID, "pipeline plan limit must be >= 0");
       h->pipe_max = value;
       return PWG_OK;
+    case PWG_OPT_HALF_BLOCKS:
+      if (value < 0) return fail(PWG_ERR_INVALID, "half-block limit must be >= 0");
+      h->half_max = value;
+      return PWG_OK;
 
     default:
       return fail(PWG_ERR_INVALID, "unknown option");
@@ -1312,6 +1321,7 @@ int pwg_get_option(const PwgHandle* h, int option, long long* value) {
     case PWG_OPT_FUSE_FIRST_CONV: *value = h->fuse_first; return PWG_OK;
     case PWG_OPT_WG_PER_CU: *value = h->wg_per_cu; return PWG_OK;
     case PWG_OPT_PIPELINE: *value = h->pipe_max; return PWG_OK;
+    case PWG_OPT_HALF_BLOCKS: *value = h->half_max >= 0 ? h->half_max : 4LL * h->n_cu; return PWG_OK;
 
     default: return fail(PWG_ERR_INVALID, "unknown option");
   }

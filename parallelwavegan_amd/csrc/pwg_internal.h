@@ -252,7 +252,7 @@ hipError_t launch_layer(const LayerArgs& a, int mt, int m2t, bool last, long lon
 hipError_t launch_first_conv_split(const FirstConvArgs& a, long long n_tiles, hipStream_t s);
 hipError_t launch_first_conv_split16(const FirstConvArgs& a, long long n_tiles, hipStream_t s);
 hipError_t launch_layer_split16(const SplitArgs& a, bool last, int tap_center, int waves_per_wg, int n_wg,
-                                hipStream_t s);
+                                hipStream_t s, bool half = false);
 hipError_t launch_layer_split(const SplitArgs& a, bool last, int tap_center, int waves_per_wg, int n_wg,
                               hipStream_t s);
 hipError_t launch_pipe_split16(const PipeArgs& p, int tap_center, int n_wg, hipStream_t s);

@@ -163,19 +163,20 @@ __device__ __forceinline__ void s16_stage(const SplitArgs& a, unsigned* smem16) 
   }
 }
 
-// A lane's tap row pieces of one block for both n-tiles: b[nt*4 + ks*2 + hl]. FIRST (layer 0 with
+// A lane's tap row pieces of one block for its NTN n-tiles from column h16 on (NTN = 2: both, h16 =
+// 0; NTN = 1: one half block): b[nt*4 + ks*2 + hl]. FIRST (layer 0 with
 // PWG_OPT_FUSE_FIRST_CONV): first_conv (models/parallel_wavegan.py:81,161, x0 = w z + b, zero
 // outside the utterance) is evaluated from the 4-byte noise with the same fmaf and pair split as
 // pwg_first_conv_split16_kernel (bit-identical), so x0 never touches HBM. PIPE: sc1 loads.
-template <int TC, bool FIRST, bool PIPE>
+template <int TC, bool FIRST, bool PIPE, int NTN = 2>
 __device__ __forceinline__ void s16_bload(const SplitArgs& a, const float* s_fwb, const BlockDesc& d, int tap,
-                                          u32x4 (&b)[8], int g, int c) {
+                                          u32x4 (&b)[8], int g, int c, int h16 = 0) {
   if constexpr (FIRST) {
     const f32x4* fw4 = reinterpret_cast<const f32x4*>(s_fwb) + g;
     const f32x4* fb4 = reinterpret_cast<const f32x4*>(s_fwb + 64) + g;
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-      const int t = d.t0 + 16 * nt + c + (tap - TC) * a.dil;
+    for (int nt = 0; nt < NTN; ++nt) {
+      const int t = d.t0 + h16 + 16 * nt + c + (tap - TC) * a.dil;
       const bool inside = t >= 0 && t < d.T;
       const float z = a.noise[d.io_off + (t < 0 ? 0 : (t >= d.T ? d.T - 1 : t))];
 #pragma unroll
@@ -192,17 +193,17 @@ __device__ __forceinline__ void s16_bload(const SplitArgs& a, const float* s_fwb
     }
   } else if constexpr (PIPE) {
     const __amdgpu_buffer_rsrc_t r = rsrc16(a.x_in);
-    const int cc = d.col + (tap - TC) * a.dil;
+    const int cc = d.col + h16 + (tap - TC) * a.dil;
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
+    for (int nt = 0; nt < NTN; ++nt) {
       const unsigned off = row16_bytes(cc + 16 * nt + c, g);
 #pragma unroll
       for (int q = 0; q < 4; ++q) b[nt * 4 + q] = ld16_sc1(r, off + q * 1024u);
     }
   } else {
-    const int cc = d.col + (tap - TC) * a.dil;
+    const int cc = d.col + h16 + (tap - TC) * a.dil;
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
+    for (int nt = 0; nt < NTN; ++nt) {
       const u32x4* p = reinterpret_cast<const u32x4*>(a.x_in + row16(cc + 16 * nt + c, g));
 #pragma unroll
       for (int q = 0; q < 4; ++q) b[nt * 4 + q] = p[q * 64];
@@ -231,21 +232,21 @@ __device__ __forceinline__ void s16_load_dv(const SplitArgs& a, const BlockDesc&
 
 // The old skip sum of a block as GEMM-2 seeds sk[ms][nt] (skip rows 16 ms + 4 g + i of column
 // bd.col + 16 nt + c). Layer 0: the sum of all layers' skip biases.
-template <bool PIPE>
+template <bool PIPE, int NTN = 2>
 __device__ __forceinline__ void s16_load_skip(const SplitArgs& a, const BlockDesc& bd, f32x4 (&sk)[4][2], int g,
-                                              int c) {
+                                              int c, int h16 = 0) {
   [[maybe_unused]] __amdgpu_buffer_rsrc_t rs;
   if constexpr (PIPE) rs = rsrc16(a.skip);
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt)
+  for (int nt = 0; nt < NTN; ++nt)
 #pragma unroll
     for (int ms = 0; ms < 4; ++ms) {
       if (a.first) {
         sk[ms][nt] = reinterpret_cast<const f32x4*>(a.skip0 + 16 * g)[ms];
       } else if constexpr (PIPE) {
-        sk[ms][nt] = __builtin_bit_cast(f32x4, ld16_sc1(rs, row16_bytes(bd.col + 16 * nt + c, g) + ms * 1024u));
+        sk[ms][nt] = __builtin_bit_cast(f32x4, ld16_sc1(rs, row16_bytes(bd.col + h16 + 16 * nt + c, g) + ms * 1024u));
       } else {
-        const f32x4* sp = reinterpret_cast<const f32x4*>(a.skip + row16(bd.col + 16 * nt + c, g));
+        const f32x4* sp = reinterpret_cast<const f32x4*>(a.skip + row16(bd.col + h16 + 16 * nt + c, g));
         sk[ms][nt] = __builtin_nontemporal_load(sp + ms * 64);
       }
     }
@@ -258,10 +259,15 @@ __device__ __forceinline__ void s16_load_skip(const SplitArgs& a, const BlockDes
 // the center tap's MFMAs (the per-layer kernel's cross-block prefetch). `mid` runs once after
 // GEMM 1 (the caller issues its next work-queue claim there). PIPE: sc1 skip loads and sc1
 // stores of x and skip (hand-off bytes of the pipelined kernel).
-template <bool LAST, int TC, bool FIRST, bool PIPE, typename Mid>
+// NTN = 1 (half blocks, the small-plan latency path): only n-tile h16 / 16 of `bd` (columns
+// bd.col + h16 + [0, 16)); the next unit's half is h16n. Every column's accumulators sum the same
+// products in the same order as with NTN = 2, and the aux K slots stay anchored at the 32-sample
+// block's first frame: bit-identical per column.
+template <bool LAST, int TC, bool FIRST, bool PIPE, int NTN = 2, typename Mid>
 __device__ __forceinline__ void s16_block(const SplitArgs& a, const unsigned* smem16, const BlockDesc& bd,
                                           const BlockDesc& bdn, bool has_next, u32x4 (&b0)[8], u32x4 (&b1)[8],
-                                          bool& nonfinite, Mid&& mid) {
+                                          bool& nonfinite, Mid&& mid, int h16 = 0, int h16n = 0) {
+  static_assert(NTN == 2 || (!LAST && !PIPE), "half blocks: middle layers of the per-layer kernel");
   const unsigned* s_wg = smem16;
   const unsigned* s_w2 = s_wg + Split16Smem::WG;
   const unsigned* s_bg = s_w2 + Split16Smem::W2;
@@ -272,15 +278,15 @@ __device__ __forceinline__ void s16_block(const SplitArgs& a, const unsigned* sm
   const int g = lane >> 4;
   const int c = lane & 15;
   constexpr int T1 = TC == 1 ? 2 : 1;  // the non-center tap after tap 0
-  const bool full = bd.t0 + 32 <= bd.T;
+  const bool full = bd.t0 + h16 + 16 * NTN <= bd.T;
 
   // aux operands: K slots [Dh0 Dh1 Dl0 Dl1 Dh0 Dh1 bh bl] x [wh0 wh1 wh0 wh1 wl0 wl1 1 1] (bias in
   // group 0 only); bw = the composite upsampler weights of the lane's two window frames
   unsigned dv[2][8];  // [frame][m], loaded during GEMM 1
   float bw[2][2];  // [nt][frame]
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
-    const int t = bd.t0 + 16 * nt + c;
+  for (int nt = 0; nt < NTN; ++nt) {
+    const int t = bd.t0 + h16 + 16 * nt + c;
     const bool live = t < bd.T;
     const int tc = live ? t : bd.T - 1;
     int roff;
@@ -313,7 +319,7 @@ __device__ __forceinline__ void s16_block(const SplitArgs& a, const unsigned* sm
 #pragma unroll
         for (int mm = 0; mm < 4; ++mm)
 #pragma unroll
-          for (int nt = 0; nt < 2; ++nt) {
+          for (int nt = 0; nt < NTN; ++nt) {
             f32x4& ac = acc[4 * mh + mm][nt];
             ac = mma16(ah[mm], b[nt * 4 + ks * 2], ac);
             ac = mma16(ah[mm], b[nt * 4 + ks * 2 + 1], ac);
@@ -329,20 +335,20 @@ __device__ __forceinline__ void s16_block(const SplitArgs& a, const unsigned* sm
 #pragma unroll
   for (int m = 0; m < 8; ++m)
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) acc[m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int nt = 0; nt < NTN; ++nt) acc[m][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 acc2[8][2];
-  s16_bload<TC, FIRST, PIPE>(a, s_fwb, bd, T1, b1, g, c);
+  s16_bload<TC, FIRST, PIPE, NTN>(a, s_fwb, bd, T1, b1, g, c, h16);
   mma_tap(acc, b0, 0);
   s16_load_dv(a, bd, dv, g, c);
-  s16_bload<TC, FIRST, PIPE>(a, s_fwb, bd, TC, b0, g, c);
+  s16_bload<TC, FIRST, PIPE, NTN>(a, s_fwb, bd, TC, b0, g, c, h16);
   mma_tap(acc, b1, T1);
-  if (has_next) s16_bload<TC, FIRST, PIPE>(a, s_fwb, bdn, 0, b1, g, c);  // the next block's
+  if (has_next) s16_bload<TC, FIRST, PIPE, NTN>(a, s_fwb, bdn, 0, b1, g, c, h16n);  // the next block's
   mma_tap(acc, b0, TC);
   if (!LAST) {
     // GEMM-2 out-row seeds sqrt(.5)(x + b_out) from the center tap: acc2[4 + 2ks + (j>>2)][nt][j&3]
     const f32x4* bo_l = reinterpret_cast<const f32x4*>(s_bo + 16 * g);
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
+    for (int nt = 0; nt < NTN; ++nt)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         float o[8];
@@ -356,9 +362,9 @@ __device__ __forceinline__ void s16_block(const SplitArgs& a, const unsigned* sm
   {
     // skip seeds: old skip sum, in flight during the aux term and the gate
     f32x4 sk[4][2];
-    s16_load_skip<PIPE>(a, bd, sk, g, c);
+    s16_load_skip<PIPE, NTN>(a, bd, sk, g, c, h16);
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
+    for (int nt = 0; nt < NTN; ++nt)
 #pragma unroll
       for (int ms = 0; ms < 4; ++ms) acc2[ms][nt] = sk[ms][nt];
   }
@@ -368,7 +374,7 @@ __device__ __forceinline__ void s16_block(const SplitArgs& a, const unsigned* sm
     const Pair16 bias_one = split_pair16(g == 0 ? 1.f : 0.f, g == 0 ? 1.f : 0.f);
     u32x4 bB[2];
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
+    for (int nt = 0; nt < NTN; ++nt) {
       const Pair16 w = split_pair16(bw[nt][0], bw[nt][1]);
       bB[nt] = u32x4{w.hi, w.hi, w.lo, bias_one.hi};  // [wh0 wh1 | wh0 wh1 | wl0 wl1 | 1 1]
     }
@@ -380,14 +386,14 @@ __device__ __forceinline__ void s16_block(const SplitArgs& a, const unsigned* sm
       const unsigned dl = __builtin_amdgcn_perm(dv[1][m], dv[0][m], 0x07060302u);
       const u32x4 aA = {dh, dl, dh, bgp};  // [Dh0 Dh1 | Dl0 Dl1 | Dh0 Dh1 | bh bl]
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) acc[m][nt] = mma16(aA, bB[nt], acc[m][nt]);
+      for (int nt = 0; nt < NTN; ++nt) acc[m][nt] = mma16(aA, bB[nt], acc[m][nt]);
     }
   }
 
   // ---- gate -> GEMM-2 B pairs: k-step ks element j = channel chan16(ks, g, j) = acc row
   u32x4 gh[2][2], gl[2][2];  // [nt][ks]
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt)
+  for (int nt = 0; nt < NTN; ++nt)
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       float gv[8];
@@ -415,7 +421,7 @@ __device__ __forceinline__ void s16_block(const SplitArgs& a, const unsigned* sm
 #pragma unroll
       for (int mm = 0; mm < 4; ++mm)
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {
+        for (int nt = 0; nt < NTN; ++nt) {
           f32x4& ac = acc2[4 * mh + mm][nt];
           ac = mma16(ah[mm], gh[nt][ks], ac);
           ac = mma16(ah[mm], gl[nt][ks], ac);
@@ -431,9 +437,9 @@ __device__ __forceinline__ void s16_block(const SplitArgs& a, const unsigned* sm
       rx = rsrc16(a.x_out);
     }
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-      const int col = bd.col + 16 * nt + c;
-      const bool live = bd.t0 + 16 * nt + c < bd.T;
+    for (int nt = 0; nt < NTN; ++nt) {
+      const int col = bd.col + h16 + 16 * nt + c;
+      const bool live = bd.t0 + h16 + 16 * nt + c < bd.T;
 #pragma unroll
       for (int ms = 0; ms < 4; ++ms) {
         if constexpr (PIPE)
@@ -550,8 +556,13 @@ __device__ __forceinline__ void s16_block(const SplitArgs& a, const unsigned* sm
 // thread over every thread).
 // a.trace (diagnostic, PWG_TRACE_FILE): per wave [start, staged, first block done, end, blocks,
 // shader clock at start, at end, XCC id], real time at 100 MHz.
-template <bool LAST, int TC, bool FIRST>
+// NTN = 1 (small plans, the B = 1 latency path): the work unit is half a block (one 16-column
+// n-tile; unit u = block u / 2, columns 16 (u % 2) + [0, 16)), so twice the waves share a layer and
+// each wave's dependent chain runs half the MFMAs; bit-identical to whole blocks.
+template <bool LAST, int TC, bool FIRST, int NTN = 2>
 __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitArgs a) {
+  constexpr int UB = NTN == 1 ? 1 : 0;  // log2(units per block)
+  const int n_units = a.n_blocks << UB;
   extern __shared__ __attribute__((aligned(16))) unsigned smem16[];
   const bool tr = a.trace != nullptr;
   unsigned long long t_start = 0, c_start = 0, t_staged = 0, t_first = 0;
@@ -566,13 +577,15 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
   // the wave's first block (a static round) is known before the image is staged: its descriptor
   // and tap-0 rows load while the workgroup stages (layer 0 with the fused first_conv builds tap 0
   // from the first_conv weights in LDS, after the barrier)
-  const int blk0 = wave < nw ? (int)((long long)a.n_blocks * xcd / 8) + (blockIdx.x >> 3) * nw + wave : -1;
-  const bool has0 = blk0 >= 0 && blk0 < (int)((long long)a.n_blocks * (xcd + 1) / 8);
+  const int blk0 = wave < nw ? (int)((long long)n_units * xcd / 8) + (blockIdx.x >> 3) * nw + wave : -1;
+  const bool has0 = blk0 >= 0 && blk0 < (int)((long long)n_units * (xcd + 1) / 8);
   BlockDesc bdn;
+  int h16n = 0;
   u32x4 b0[8], b1[8];
   if (has0) {
-    bdn = a.blocks[blk0];
-    if constexpr (!FIRST) s16_bload<TC, false, false>(a, nullptr, bdn, 0, b0, lane >> 4, lane & 15);
+    bdn = a.blocks[blk0 >> UB];
+    h16n = NTN == 1 ? 16 * (blk0 & 1) : 0;
+    if constexpr (!FIRST) s16_bload<TC, false, false, NTN>(a, nullptr, bdn, 0, b0, lane >> 4, lane & 15, h16n);
   }
   s16_stage<LAST, FIRST>(a, smem16);
   __syncthreads();
@@ -591,7 +604,7 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
     return;
   }
   auto xcd_waves = [&](int y) { return (((int)gridDim.x - y + 7) >> 3) * nw; };
-  auto xcd_first = [&](int y) { return (int)((long long)a.n_blocks * y / 8); };
+  auto xcd_first = [&](int y) { return (int)((long long)n_units * y / 8); };
   const int x_first = xcd_first(xcd), x_end = xcd_first(xcd + 1), x_waves = xcd_waves(xcd);
   int victim = 0;
   auto ticket_issue = [&]() -> int {
@@ -626,15 +639,18 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
     return;
   }
   const float* s_fwb = reinterpret_cast<const float*>(smem16 + Split16Smem::dwords(LAST));
-  if constexpr (FIRST) s16_bload<TC, true, false>(a, s_fwb, bdn, 0, b0, lane >> 4, lane & 15);
+  if constexpr (FIRST) s16_bload<TC, true, false, NTN>(a, s_fwb, bdn, 0, b0, lane >> 4, lane & 15, h16n);
   bool nonfinite = false;  // LAST: range flag (pwg_run_status)
   while (true) {
     const BlockDesc bd = bdn;
-    bdn = a.blocks[nblk >= 0 ? nblk : blk];  // prefetch target (bd itself when there is none)
+    const int h16 = h16n;
+    const int pf = nblk >= 0 ? nblk : blk;  // prefetch target (this unit itself when there is none)
+    bdn = a.blocks[pf >> UB];
+    h16n = NTN == 1 ? 16 * (pf & 1) : 0;
     int ticket = 0;
-    s16_block<LAST, TC, FIRST, false>(a, smem16, bd, bdn, true, b0, b1, nonfinite, [&]() {
+    s16_block<LAST, TC, FIRST, false, NTN>(a, smem16, bd, bdn, true, b0, b1, nonfinite, [&]() {
       if (nblk >= 0) ticket = ticket_issue();
-    });
+    }, h16, h16n);
     if (tr && n_done++ == 0) t_first = __builtin_amdgcn_s_memrealtime();
     if (nblk < 0) break;
     blk = nblk;
@@ -787,14 +803,15 @@ hipError_t launch_first_conv_split16(const FirstConvArgs& a, long long n_tiles, 
 }
 
 hipError_t launch_layer_split16(const SplitArgs& a, bool last, int tap_center, int waves_per_wg, int n_wg,
-                                hipStream_t s) {
+                                hipStream_t s, bool half) {
   if (waves_per_wg > 8) waves_per_wg = 8;
   if (a.compute_waves < 1 || a.compute_waves > waves_per_wg) return hipErrorInvalidValue;
+  if (half && last) return hipErrorInvalidValue;  // the head needs both n-tiles of a block
   const dim3 grid((unsigned)n_wg), block((unsigned)(64 * waves_per_wg));
-#define PWG_SPLIT16_LAUNCH(LAST_, TC_, FIRST_)                                                          \
+#define PWG_SPLIT16_LAUNCH(LAST_, TC_, FIRST_, NTN_)                                                    \
   {                                                                                                     \
     const size_t lds = sizeof(unsigned) * (Split16Smem::dwords(LAST_) + (FIRST_ ? 128 : 0));            \
-    auto kfn = &pwg_layer_split16_kernel<LAST_, TC_, FIRST_>;                                           \
+    auto kfn = &pwg_layer_split16_kernel<LAST_, TC_, FIRST_, NTN_>;                                     \
     hipError_t e_ = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),                             \
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);           \
     if (e_ != hipSuccess) return e_;                                                                    \
@@ -804,11 +821,17 @@ hipError_t launch_layer_split16(const SplitArgs& a, bool last, int tap_center, i
   const bool first = a.noise != nullptr;  // fused first_conv (never together with last: L > 1)
   if (first && last) return hipErrorInvalidValue;
   if (tap_center == 1) {
-    if (first) PWG_SPLIT16_LAUNCH(false, 1, true)
-    if (last) PWG_SPLIT16_LAUNCH(true, 1, false) else PWG_SPLIT16_LAUNCH(false, 1, false)
+    if (half) {
+      if (first) PWG_SPLIT16_LAUNCH(false, 1, true, 1) else PWG_SPLIT16_LAUNCH(false, 1, false, 1)
+    }
+    if (first) PWG_SPLIT16_LAUNCH(false, 1, true, 2)
+    if (last) PWG_SPLIT16_LAUNCH(true, 1, false, 2) else PWG_SPLIT16_LAUNCH(false, 1, false, 2)
   } else if (tap_center == 2) {
-    if (first) PWG_SPLIT16_LAUNCH(false, 2, true)
-    if (last) PWG_SPLIT16_LAUNCH(true, 2, false) else PWG_SPLIT16_LAUNCH(false, 2, false)
+    if (half) {
+      if (first) PWG_SPLIT16_LAUNCH(false, 2, true, 1) else PWG_SPLIT16_LAUNCH(false, 2, false, 1)
+    }
+    if (first) PWG_SPLIT16_LAUNCH(false, 2, true, 2)
+    if (last) PWG_SPLIT16_LAUNCH(true, 2, false, 2) else PWG_SPLIT16_LAUNCH(false, 2, false, 2)
   }
 #undef PWG_SPLIT16_LAUNCH
   return hipErrorInvalidValue;

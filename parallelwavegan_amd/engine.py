@@ -344,7 +344,7 @@ class Engine:
 
     def set_option(self, option, value):
         """pwg_set_option: option in {"layer_kernel", "waves_per_wg", "wg_per_cu", "fuse_first_conv",
-        "pipeline"}. "pipeline" (largest padded plan on the layer-pipelined launch, 0 = never)
+        "pipeline", "half_blocks"}. "pipeline" (largest padded plan on the layer-pipelined launch, 0 = never)
         applies to plans created afterwards: the cached plans are dropped."""
         opts = self._OPTS
         if option == "layer_kernel" and isinstance(value, str):
@@ -359,7 +359,7 @@ class Engine:
 
     _OPTS = {"layer_kernel": _lib.PWG_OPT_LAYER_KERNEL, "waves_per_wg": _lib.PWG_OPT_WAVES_PER_WG,
              "wg_per_cu": _lib.PWG_OPT_WG_PER_CU, "fuse_first_conv": _lib.PWG_OPT_FUSE_FIRST_CONV,
-             "pipeline": _lib.PWG_OPT_PIPELINE}
+             "pipeline": _lib.PWG_OPT_PIPELINE, "half_blocks": _lib.PWG_OPT_HALF_BLOCKS}
 
     def get_option(self, option):
         v = ctypes.c_longlong()

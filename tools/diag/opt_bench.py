@@ -18,6 +18,8 @@ plans = [("ljspeech_v1", [64]), ("ljspeech_v1", [512]), ("ljspeech_v1", [1024]),
          ("libritts_v1", synthetic.libritts_lengths(32, seed=3).tolist())]
 if os.environ.get("PLANS") == "small":
     plans = plans[:4]
+elif os.environ.get("PLANS") == "lat":
+    plans = [("ljspeech_v1", [f]) for f in (64, 96, 128, 192, 256, 384, 512)]
 for cfg, lengths in plans:
     params = configs.generator_params(cfg)
     row = {"config": cfg, "frames": lengths if len(lengths) <= 2 else f"{len(lengths)} utts, {sum(lengths)} frames"}
