@@ -58,9 +58,12 @@ enum {
   PWG_ERR_ASSERT = 2,      /* AssertionError */
   PWG_ERR_HIP = 3,         /* RuntimeError (HIP runtime failure) */
   PWG_ERR_UNSUPPORTED = 4, /* NotImplementedError */
-  PWG_ERR_RANGE = 5        /* a value left the fp16 pair range of the split-f16 kernels (no reference
+  PWG_ERR_RANGE = 5,       /* a value left the fp16 pair range of the split-f16 kernels (no reference
                               counterpart: the reference computes in fp32; the drop-in reruns on the
                               exact-fp32 kernel, see pwg_run_status) */
+  PWG_ERR_RERUN = 6        /* pwg_run_status: the grid-synchronised forward (PWG_OPT_SYNC) found the GPU
+                              shared and wrote no output; rerun with PWG_OPT_SYNC 0 (the Python
+                              engine does) */
 };
 
 /* Input layouts accepted by pwg_plan_create / pwg_run. */
@@ -204,12 +207,22 @@ enum {
                                     progress words), bit-identical to the per-layer launches; the
                                     B = 1 decode path of bin/decode.py. 0 = never. Applies to plans
                                     created afterwards (default PWG_PIPE_MAX_DEFAULT). */
-  PWG_OPT_HALF_BLOCKS = 5      /* split16: launches of at most this many 32-sample blocks (every layer
+  PWG_OPT_HALF_BLOCKS = 5,     /* split16: launches of at most this many 32-sample blocks (every layer
                                     but the last) take half blocks (16 columns) as work units: twice
                                     the waves, half of a block's dependent MFMA chain per wave; the
                                     B = 1 latency path. Bit-identical. 0 = never; default 4 x the
                                     CU count (one unit per wave at 8 waves per CU: LJ T' = 64
                                     0.42 -> 0.35 ms per forward; slower from ~4 blocks per CU on). */
+  PWG_OPT_SYNC = 6             /* split16: plans of at most this many 32-sample blocks run all residual
+                                    layers in ONE launch, one workgroup per CU, a grid barrier in place
+                                    of each launch boundary (the next layer's weights stage while the
+                                    barrier completes); same work units and kernel body as the
+                                    per-layer launches, bit-identical. 0 = never; default 64 x the
+                                    CU count (LJ B = 1, T' = 64 / 512 / 2048: 0.35 -> 0.33, 1.49 ->
+                                    1.19, 4.04 -> 3.93 ms per forward; slower than the per-layer
+                                    launches' work queues at 256 blocks per CU). A launch that
+                                    finds the GPU shared writes nothing and pwg_run_status returns
+                                    PWG_ERR_RERUN. */
 };
 #define PWG_PIPE_MAX_DEFAULT 0LL /* off: measured slower than the per-layer launches */
 PWG_API int pwg_set_option(PwgHandle* h, int option, long long value);

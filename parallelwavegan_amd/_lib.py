@@ -39,6 +39,7 @@ PWG_ERR_ASSERT = 2
 PWG_ERR_HIP = 3
 PWG_ERR_UNSUPPORTED = 4
 PWG_ERR_RANGE = 5
+PWG_ERR_RERUN = 6
 PWG_RCCL_UNIQUE_ID_BYTES = 128
 
 PWG_LAYOUT_INFERENCE = 0
@@ -99,6 +100,7 @@ PWG_OPT_WG_PER_CU = 2
 PWG_OPT_FUSE_FIRST_CONV = 3
 PWG_OPT_PIPELINE = 4
 PWG_OPT_HALF_BLOCKS = 5
+PWG_OPT_SYNC = 6
 
 
 class PwgConfig(ctypes.Structure):
@@ -255,8 +257,13 @@ class RangeError(ArithmeticError):
     """PWG_ERR_RANGE: a value left the fp16 pair range of the split-f16 kernels."""
 
 
+class RerunError(RuntimeError):
+    """PWG_ERR_RERUN: the grid-synchronised forward found the GPU shared and wrote no output."""
+
+
 _ERRORS = {
     PWG_ERR_RANGE: RangeError,
+    PWG_ERR_RERUN: RerunError,
     PWG_ERR_INVALID: ValueError,
     PWG_ERR_ASSERT: AssertionError,
     PWG_ERR_HIP: RuntimeError,

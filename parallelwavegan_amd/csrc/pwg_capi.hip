@@ -315,6 +315,7 @@ struct PwgHandle {
   int layer_kernel = 0, waves_per_wg = 8, wg_per_cu = 1;
   int fuse_first = 1;  // PWG_OPT_FUSE_FIRST_CONV
   long long pipe_max = PWG_PIPE_MAX_DEFAULT;  // PWG_OPT_PIPELINE: largest padded plan on the layer pipeline
+  long long sync_max = -1;  // PWG_OPT_SYNC: most 32-sample blocks on the grid-synchronised forward (-1: 64 x n_cu)
   long long half_max = -1;  // PWG_OPT_HALF_BLOCKS: most blocks of a half-block launch (-1: 4 x n_cu)
   int n_cu = 0;
   // timing
@@ -1031,9 +1032,77 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
     if (e != hipSuccess) return hip_fail(e, "layer-pipelined forward launch");
     return PWG_OK;
   }
+  // the residual layers but the last in ONE grid-synchronised launch (split16, PWG_OPT_SYNC: the
+  // B = 1 decode path)
+  const long long n_blocks_all = p->n_tiles * (TILE / 32);
+  const long long half_max_all = h->half_max >= 0 ? h->half_max : 4LL * h->n_cu;
+  const bool use_sync = split16 && h->split_ok && h->L >= 2 && h->L <= PIPE_MAX_LAYERS && h->KS == 3 &&
+                        n_blocks_all <= (h->sync_max >= 0 ? h->sync_max : 64LL * h->n_cu) &&
+                        (long long)h->RS * 4 * (p->Tpad + h->gap) < (1LL << 31);
+  // the layers it covers: 0 .. L - 2 (from 1 on whole-block plans with the fused first_conv)
+  SyncArgs sy;
+  int sync_begin = h->L, sync_end = h->L;
+  if (use_sync) {
+    SplitArgs& sa = sy.base;
+    sa.x_in = nullptr; sa.x_out = nullptr;
+    sa.skip = skip; sa.skip0 = packed + h->off_skip0_16;
+    sa.d = nullptr;
+    sa.tab = packed + h->off_tab_interior;
+    sa.tab_left = (int)(h->off_tab_left - h->off_tab_interior);
+    sa.tab_right = (int)(h->off_tab_right - h->off_tab_interior);
+    sa.tab_small = (int)(h->off_tab_small - h->off_tab_interior);
+    sa.blocks = d_blocks;
+    sa.wg = nullptr;
+    sa.hw1 = packed + h->off_head16_w1; sa.hw2 = packed + h->off_head16_w2; sa.hb2 = packed + h->off_head_b2;
+    sa.out = out;
+    sa.H = (int)h->aux.H; sa.J1 = h->aux.J1; sa.TL = h->aux.TL; sa.TR = h->aux.TR; sa.Fmin = h->aux.Fmin;
+    sa.n_blocks = (int)n_blocks_all; sa.dil = 1; sa.first = 0; sa.O = h->O;
+    if (p->layout == PWG_LAYOUT_INFERENCE) { sa.out_stride_t = h->O; sa.out_stride_o = 1; }
+    else { sa.out_stride_t = 1; sa.out_stride_o = (int)p->utts[0].T; }
+    sa.skip_scale = (float)std::sqrt(1.0 / h->L);
+    sa.ctr = nullptr; sa.trace = nullptr; sa.compute_waves = 8;
+    sa.noise = fuse_first ? noise : nullptr;
+    sa.fw = packed + h->off_first_w; sa.fb = packed + h->off_first_b;
+    sa.range_flag = range_flag;
+    sy.wg0 = reinterpret_cast<const unsigned*>(packed + h->off_layers + h->lo_split16);
+    sy.wg_stride = (long long)h->layer_stride;
+    sy.d0 = reinterpret_cast<const unsigned*>(dproj);
+    sy.d_stride = p->F_total * h->GR;
+    sy.x[0] = reinterpret_cast<unsigned*>(x0);
+    sy.x[1] = reinterpret_cast<unsigned*>(x1);
+    sy.half = n_blocks_all <= half_max_all;
+    sync_begin = (!sy.half && fuse_first) ? 1 : 0;
+    sync_end = h->L - 1;
+    sy.l0 = sync_begin;
+    // its counters: the work-queue heads of the first layer it covers (no per-layer launch uses
+    // them; zeroed by the plan-descriptor kernel every run)
+    sy.ctr = sched_ctr + (size_t)sync_begin * SCHED_CTR_STRIDE * 8;
+    sy.L = sync_end - sync_begin;
+    for (int l = 0; l < PIPE_MAX_LAYERS; ++l) sy.dil[l] = l < h->L ? h->dil[l] : 1;
+    // the per-layer launch's work-unit rules (below), at one workgroup per CU
+    const long long nwg = h->n_cu;
+    auto waves = [&](long long units) {
+      int w = std::min(8, h->waves_per_wg);
+      if (PWG_SMALL_SPREAD && units < nwg * w) w = (int)std::max(1LL, (units + nwg - 1) / nwg);
+      if (units > 8LL * h->n_cu && units <= 32LL * h->n_cu) w = std::min(w, 4);
+      return w;
+    };
+    sy.waves_mid = waves(sy.half ? 2 * n_blocks_all : n_blocks_all);
+  }
+  // the per-layer launches; the grid-synchronised launch takes the place of layers
+  // [sync_begin, sync_end)
   float* xin = x0;
   float* xout = x1;
   for (int l = 0; l < h->L; ++l) {
+    if (l == sync_begin && sync_begin < sync_end) {
+      const int tc = h->cfg.use_causal_conv ? h->KS - 1 : (h->KS - 1) / 2;
+      e = timed(PWG_KERNEL_RESIDUAL_LAYER, [&] { return launch_sync_split16(sy, tc, h->n_cu, s); });
+      if (e != hipSuccess) return hip_fail(e, "grid-synchronised forward launch");
+    }
+    if (l >= sync_begin && l < sync_end) {
+      std::swap(xin, xout);
+      continue;
+    }
     const float* L0 = packed + h->off_layers + h->layer_stride * l;
     LayerArgs la;
     la.x_in = xin; la.x_out = xout; la.skip = skip;
@@ -1199,9 +1268,13 @@ int pwg_run_status(PwgPlan* p, const void* workspace, void* stream) {
   hipError_t e = hipMemcpyAsync(&flag, (const char*)workspace + p->ws_flag, sizeof(int), hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return hip_fail(e, "run status");
+  if (flag & 4)
+    return fail(PWG_ERR_RERUN, "grid-synchronised forward: not every workgroup could start (the GPU is shared "
+                               "with other work), so it did nothing; rerun with PWG_OPT_SYNC 0");
   if (flag & 2)
-    return fail(PWG_ERR_HIP, "layer-pipelined forward: a dependency wait timed out (the output is invalid); "
-                              "rerun with PWG_OPT_PIPELINE 0 and report this");
+    return fail(PWG_ERR_HIP, "layer-pipelined or grid-synchronised forward: a dependency or barrier wait timed "
+                              "out (the output is invalid); rerun with PWG_OPT_PIPELINE 0 and PWG_OPT_SYNC 0 "
+                              "and report this");
   if (flag != 0)
     return fail(PWG_ERR_RANGE,
                 "split-f16 range flag: a value left the fp16 pair range (an aux projection row, the "
@@ -1307,6 +1380,10 @@ int pwg_set_option(PwgHandle* h, int option, long long value) {
       if (value < 0) return fail(PWG_ERR_INVALID, "half-block limit must be >= 0");
       h->half_max = value;
       return PWG_OK;
+    case PWG_OPT_SYNC:
+      if (value < 0) return fail(PWG_ERR_INVALID, "grid-synchronised plan limit must be >= 0");
+      h->sync_max = value;
+      return PWG_OK;
 
     default:
       return fail(PWG_ERR_INVALID, "unknown option");
@@ -1322,6 +1399,7 @@ int pwg_get_option(const PwgHandle* h, int option, long long* value) {
     case PWG_OPT_WG_PER_CU: *value = h->wg_per_cu; return PWG_OK;
     case PWG_OPT_PIPELINE: *value = h->pipe_max; return PWG_OK;
     case PWG_OPT_HALF_BLOCKS: *value = h->half_max >= 0 ? h->half_max : 4LL * h->n_cu; return PWG_OK;
+    case PWG_OPT_SYNC: *value = h->sync_max >= 0 ? h->sync_max : 64LL * h->n_cu; return PWG_OK;
 
     default: return fail(PWG_ERR_INVALID, "unknown option");
   }

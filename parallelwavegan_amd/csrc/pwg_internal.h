@@ -218,6 +218,23 @@ struct PipeArgs {
   int dil[PIPE_MAX_LAYERS];
 };
 
+// Grid-synchronised forward (pwg_sync_split16_kernel): all layers in one launch, a grid barrier
+// between layers; x ping-pongs between two planes (layer l reads x[l & 1]).
+struct SyncArgs {
+  SplitArgs base;            // noise non-null: layer 0 builds x0 from the noise (fused first_conv)
+  const unsigned* wg0;       // layer l's split16 LDS image at wg0 + l * wg_stride (dwords)
+  long long wg_stride;
+  const unsigned* d0;        // layer l's D rows at d0 + l * d_stride (dwords)
+  long long d_stride;
+  unsigned* x[2];
+  int* ctr;                  // barrier counter, arrival counter, residency decision, each on a
+                             // line of its own (SCHED_CTR_STRIDE ints apart; zeroed per run)
+  int l0, L;                 // the launch runs layers l0 .. l0 + L - 1
+  int half;                  // half-block work units
+  int waves_mid;             // computing waves per workgroup
+  int dil[PIPE_MAX_LAYERS];
+};
+
 // Persistent-kernel work queues: one head per XCD, each on its own 128-byte line.
 constexpr int SCHED_CTR_STRIDE = 32;
 
@@ -256,6 +273,7 @@ hipError_t launch_layer_split16(const SplitArgs& a, bool last, int tap_center, i
 hipError_t launch_layer_split(const SplitArgs& a, bool last, int tap_center, int waves_per_wg, int n_wg,
                               hipStream_t s);
 hipError_t launch_pipe_split16(const PipeArgs& p, int tap_center, int n_wg, hipStream_t s);
+hipError_t launch_sync_split16(const SyncArgs& p, int tap_center, int n_wg, hipStream_t s);
 hipError_t launch_layer_persistent(const PersistArgs& a, int mt, int m2t, bool last, int waves_per_wg, int n_wg,
                                    hipStream_t s);
 

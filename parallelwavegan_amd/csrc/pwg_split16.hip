@@ -267,7 +267,7 @@ template <bool LAST, int TC, bool FIRST, bool PIPE, int NTN = 2, typename Mid>
 __device__ __forceinline__ void s16_block(const SplitArgs& a, const unsigned* smem16, const BlockDesc& bd,
                                           const BlockDesc& bdn, bool has_next, u32x4 (&b0)[8], u32x4 (&b1)[8],
                                           bool& nonfinite, Mid&& mid, int h16 = 0, int h16n = 0) {
-  static_assert(NTN == 2 || (!LAST && !PIPE), "half blocks: middle layers of the per-layer kernel");
+  static_assert(NTN == 2 || !LAST, "half blocks: middle layers");
   const unsigned* s_wg = smem16;
   const unsigned* s_w2 = s_wg + Split16Smem::WG;
   const unsigned* s_bg = s_w2 + Split16Smem::W2;
@@ -754,6 +754,146 @@ __global__ void __launch_bounds__(512, 1) pwg_pipe_split16_kernel(const PipeArgs
   else pipe_layer<false, TC, false>(p, l, smem16);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Grid-synchronised forward (residual layers l0 .. l0 + L - 1 in ONE launch, one workgroup per CU;
+// the B = 1 decode path; the last layer, with the output head, runs as its own per-layer launch,
+// and so does layer 0 with the fused first_conv on whole-block plans). Each layer runs the
+// per-layer launch's work units (its static rounds: XCD x takes the x-th eighth of the units, wave
+// w of workgroup b every x_waves-th unit from (b >> 3) nw + w) through the same block body, so the
+// forward is bit-identical; a grid barrier replaces each launch boundary, and a workgroup stages
+// the next layer's LDS image while the barrier completes (the per-layer path pays ~2.2 us of launch
+// gap plus ~1.9 us of staging per layer after the previous layer's tail).
+// Residency: the static split needs every workgroup on the GPU at once, which a second stream or
+// process holding CUs can prevent. So every workgroup first counts itself in, and the first one to
+// see either the full count or its bounded wait expire decides for all (one CAS): "run" (every
+// workgroup had started, so all are resident) or "abort" (every workgroup exits at once, no x or skip
+// written; pwg_run_status returns PWG_ERR_RERUN and the engine reruns on the per-layer launches).
+// Measured: claiming units dynamically instead (one queue per layer, deadlock-free without the
+// check) cost 0.35 -> 0.89 ms at LJ T' = 64: the claims serialise on the queue head.
+// Hand-off (cdna_hip_programming.md Guideline 16; MI355X_MICROARCH.md hand-off table, row 1): every
+// store and every load of x and skip is sc1 (the PIPE forms of s16_block), every storing wave
+// drains (s_waitcnt vmcnt(0)) before a workgroup barrier, then one lane adds to the barrier counter
+// (agent-scope atomic); one lane polls it with sc1 loads and a workgroup barrier follows. Bounded
+// spins: a wait that gives up sets bit 1 of the range word (pwg_run_status reports it).
+template <int TC, bool FIRST, int NTN>
+__device__ __forceinline__ void sync_layer(const SplitArgs& a, const unsigned* smem16) {
+  constexpr int UB = NTN == 1 ? 1 : 0;
+  const int n_units = a.n_blocks << UB;
+  const int nw = a.compute_waves;
+  const int wave = threadIdx.x >> 6;
+  if (wave >= nw) return;
+  const int lane = threadIdx.x & 63;
+  const int xcd = blockIdx.x & 7;
+  const int x_first = (int)((long long)n_units * xcd / 8), x_end = (int)((long long)n_units * (xcd + 1) / 8);
+  const int x_waves = (((int)gridDim.x - xcd + 7) >> 3) * nw;
+  int u = x_first + (blockIdx.x >> 3) * nw + wave;
+  if (u >= x_end) return;
+  const float* s_fwb = reinterpret_cast<const float*>(smem16 + Split16Smem::dwords(false));
+  bool nonfinite = false;  // (middle layers never set it)
+  BlockDesc bd = a.blocks[u >> UB];
+  int h16 = NTN == 1 ? 16 * (u & 1) : 0;
+  u32x4 b0[8], b1[8];
+  s16_bload<TC, FIRST, true, NTN>(a, s_fwb, bd, 0, b0, lane >> 4, lane & 15, h16);
+  while (true) {
+    const int un = u + x_waves;
+    const bool has_next = un < x_end;
+    const BlockDesc bdn = a.blocks[(has_next ? un : u) >> UB];
+    const int h16n = NTN == 1 ? 16 * ((has_next ? un : u) & 1) : 0;
+    s16_block<false, TC, FIRST, true, NTN>(a, smem16, bd, bdn, has_next, b0, b1, nonfinite, []() {}, h16, h16n);
+    if (!has_next) break;
+    u = un;
+    bd = bdn;
+    h16 = h16n;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) b0[q] = b1[q];
+  }
+}
+
+constexpr int SYNC_RESIDENCY_SPINS = 512;  // bounded wait for every workgroup to start (~0.5 ms)
+
+template <int TC, int NTN>
+__global__ void __launch_bounds__(512, 1) pwg_sync_split16_kernel(const SyncArgs p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned smem16[];
+  __shared__ int s_decision;
+  const int nwg = gridDim.x;
+  int* const bar = p.ctr;
+  int* const arrive = p.ctr + SCHED_CTR_STRIDE;
+  int* const decision = p.ctr + 2 * SCHED_CTR_STRIDE;
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  auto layer_args = [&](int l) {
+    SplitArgs a = p.base;
+    a.wg = p.wg0 + (size_t)l * p.wg_stride;
+    a.d = p.d0 + (size_t)l * p.d_stride;
+    a.x_in = p.x[l & 1];
+    a.x_out = p.x[(l + 1) & 1];
+    a.dil = p.dil[l];
+    a.first = l == 0;
+    a.compute_waves = p.waves_mid;
+    if (l != 0) a.noise = nullptr;
+    return a;
+  };
+  // layer 0 with the fused first_conv: half-block launches only (whole-block launches start at
+  // layer 1; the register budget holds one block body per kernel there)
+  const bool fused = NTN == 1 && p.base.noise != nullptr;
+  auto stage = [&](int l) {
+    const SplitArgs a = layer_args(l);
+    if (l == 0 && fused) s16_stage<false, true>(a, smem16);
+    else s16_stage<false, false>(a, smem16);
+  };
+  const int l_end = p.l0 + p.L;
+  stage(p.l0);
+  if (threadIdx.x == 0) {
+    int d = 0;
+    for (int spins = 0;; ++spins) {
+      d = __hip_atomic_load(decision, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (d != 0) break;
+      int want = 0;
+      if (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nwg)
+        __hip_atomic_compare_exchange_strong(decision, &want, 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+      else if (spins >= SYNC_RESIDENCY_SPINS)
+        __hip_atomic_compare_exchange_strong(decision, &want, 2, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+      else
+        __builtin_amdgcn_s_sleep(1);
+    }
+    s_decision = d;
+  }
+  __syncthreads();
+  if (s_decision != 1) {
+    if (threadIdx.x == 0) __hip_atomic_fetch_or(p.base.range_flag, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  bool timed_out = false;
+  for (int l = p.l0; l < l_end; ++l) {
+    const SplitArgs a = layer_args(l);
+    if constexpr (NTN == 1) {
+      if (l == 0 && fused) sync_layer<TC, true, NTN>(a, smem16);
+      else sync_layer<TC, false, NTN>(a, smem16);
+    } else {
+      sync_layer<TC, false, NTN>(a, smem16);
+    }
+    if (l == l_end - 1) break;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores have landed
+    __syncthreads();                                   // ... and every wave's; LDS image free
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    stage(l + 1);
+    if (threadIdx.x == 0) {
+      const int target = (l - p.l0 + 1) * nwg;
+      for (int spins = 0;; ++spins) {
+        if (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+        if (spins >= PIPE_SPIN_LIMIT) {
+          timed_out = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __syncthreads();
+  }
+  if (timed_out) __hip_atomic_fetch_or(p.base.range_flag, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // first_conv (1x1, 1 -> 64, bias) into the split16 x layout; gap tiles zero every residual plane.
 __global__ void __launch_bounds__(256) pwg_first_conv_split16_kernel(const FirstConvArgs a) {
   const long long tile = blockIdx.x;
@@ -835,6 +975,20 @@ hipError_t launch_layer_split16(const SplitArgs& a, bool last, int tap_center, i
   }
 #undef PWG_SPLIT16_LAUNCH
   return hipErrorInvalidValue;
+}
+
+hipError_t launch_sync_split16(const SyncArgs& p, int tap_center, int n_wg, hipStream_t s) {
+  const size_t lds = sizeof(unsigned) * (Split16Smem::dwords(false) + 128);
+  if (p.L < 1 || p.L > PIPE_MAX_LAYERS || p.waves_mid < 1 || p.waves_mid > 8) return hipErrorInvalidValue;
+  auto kfn = tap_center == 1 ? (p.half ? &pwg_sync_split16_kernel<1, 1> : &pwg_sync_split16_kernel<1, 2>)
+             : tap_center == 2 ? (p.half ? &pwg_sync_split16_kernel<2, 1> : &pwg_sync_split16_kernel<2, 2>)
+                               : nullptr;
+  if (kfn == nullptr) return hipErrorInvalidValue;
+  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(kfn, dim3((unsigned)n_wg), dim3(512), lds, s, p);
+  return hipGetLastError();
 }
 
 hipError_t launch_pipe_split16(const PipeArgs& p, int tap_center, int n_wg, hipStream_t s) {

@@ -276,6 +276,7 @@ class Engine:
         self.timing_enabled = False
         self.split_range_ok = True
         self.range_reruns = 0  # runs redone on the exact-fp32 kernel after a split-f16 range flag
+        self.sync_reruns = 0  # grid-synchronised runs redone per-layer (the GPU was shared)
         self.layer_kernel = self.get_option("layer_kernel")
 
     def __del__(self):
@@ -344,7 +345,7 @@ class Engine:
 
     def set_option(self, option, value):
         """pwg_set_option: option in {"layer_kernel", "waves_per_wg", "wg_per_cu", "fuse_first_conv",
-        "pipeline", "half_blocks"}. "pipeline" (largest padded plan on the layer-pipelined launch, 0 = never)
+        "pipeline", "half_blocks", "sync"}. "pipeline" (largest padded plan on the layer-pipelined launch, 0 = never)
         applies to plans created afterwards: the cached plans are dropped."""
         opts = self._OPTS
         if option == "layer_kernel" and isinstance(value, str):
@@ -359,7 +360,8 @@ class Engine:
 
     _OPTS = {"layer_kernel": _lib.PWG_OPT_LAYER_KERNEL, "waves_per_wg": _lib.PWG_OPT_WAVES_PER_WG,
              "wg_per_cu": _lib.PWG_OPT_WG_PER_CU, "fuse_first_conv": _lib.PWG_OPT_FUSE_FIRST_CONV,
-             "pipeline": _lib.PWG_OPT_PIPELINE, "half_blocks": _lib.PWG_OPT_HALF_BLOCKS}
+             "pipeline": _lib.PWG_OPT_PIPELINE, "half_blocks": _lib.PWG_OPT_HALF_BLOCKS,
+             "sync": _lib.PWG_OPT_SYNC}
 
     def get_option(self, option):
         v = ctypes.c_longlong()
@@ -389,19 +391,40 @@ class Engine:
         if stream is None:
             stream = torch.cuda.current_stream(self.device)
         self._enqueue(plan, mel, noise, out, mean, scale, stream)
-        if check and self.layer_kernel in (2, 3):
+        if check:
+            self._range_check(plan, mel, noise, out, mean, scale, stream)
+        return out
+
+    def _range_check(self, plan, mel, noise, out, mean, scale, stream):
+        """Split-f16 range check of the run just enqueued on ``stream``; a flagged run is redone
+        on the exact-fp32 layer kernel. A grid-synchronised run that found the GPU shared
+        (PWG_ERR_RERUN: it wrote nothing) is redone on the per-layer launches first."""
+        if self.layer_kernel not in (2, 3):
+            return
+        try:
             try:
                 self.run_status(plan, stream)
-            except _lib.RangeError as e:
-                logging.warning("%s; rerunning on the exact-fp32 layer kernel", e)
-                kernel = self.layer_kernel
-                self.set_option("layer_kernel", "persistent")
-                try:
-                    self._enqueue(plan, mel, noise, out, mean, scale, stream)
-                finally:
-                    self.set_option("layer_kernel", kernel)
-                self.range_reruns += 1
-        return out
+            except _lib.RerunError:
+                self._enqueue_per_layer(plan, mel, noise, out, mean, scale, stream)
+                self.sync_reruns += 1
+                self.run_status(plan, stream)
+        except _lib.RangeError as e:
+            logging.warning("%s; rerunning on the exact-fp32 layer kernel", e)
+            kernel = self.layer_kernel
+            self.set_option("layer_kernel", "persistent")
+            try:
+                self._enqueue(plan, mel, noise, out, mean, scale, stream)
+            finally:
+                self.set_option("layer_kernel", kernel)
+            self.range_reruns += 1
+
+    def _enqueue_per_layer(self, plan, mel, noise, out, mean, scale, stream):
+        sync = self.get_option("sync")
+        self.set_option("sync", 0)
+        try:
+            self._enqueue(plan, mel, noise, out, mean, scale, stream)
+        finally:
+            self.set_option("sync", sync)
 
     def run_status(self, plan, stream=None):
         """pwg_run_status of the last run on ``stream``'s workspace: raises _lib.RangeError when the
@@ -448,11 +471,14 @@ class Engine:
         )
         return out
 
-    def infer(self, mels, noises, mean=None, scale=None):
+    def infer(self, mels, noises, mean=None, scale=None, refresh=None):
         """Ragged batch of inference() calls in ONE engine pass.
 
         mels: list of (T'_u, aux) float32 device tensors; noises: list of (T_u,) or (T_u, 1).
         Returns a list of (T_u, out_channels) tensors (views of one output buffer).
+        refresh: optional callable run after the forward is enqueued and before the range check;
+        it returns True when it re-packed the weights (the drop-in module's weight check, run while
+        the GPU works), and the forward is then enqueued again on the new image.
         """
         frames = [int(m.shape[0]) for m in mels]
         plan = self.plan(frames, _lib.PWG_LAYOUT_INFERENCE)
@@ -460,7 +486,14 @@ class Engine:
         noise = torch.cat([n.reshape(-1) for n in noises]) if len(noises) > 1 else noises[0].reshape(-1).contiguous()
         O = self.config.out_channels
         out = torch.empty(plan.total_samples * O, dtype=torch.float32, device=self.device)
-        self.run(plan, mel, noise, out, mean, scale)
+        if refresh is None:
+            self.run(plan, mel, noise, out, mean, scale)
+        else:
+            stream = torch.cuda.current_stream(self.device)
+            self._enqueue(plan, mel, noise, out, mean, scale, stream)
+            if refresh():  # the weights changed under the enqueued forward: redo it on the new image
+                self._enqueue(plan, mel, noise, out, mean, scale, stream)
+            self._range_check(plan, mel, noise, out, mean, scale, stream)
         res, off = [], 0
         H = self.upsample_factor
         for f in frames:
@@ -530,7 +563,13 @@ class GraphedRun:
         _lib.check(self._lib.pwg_graph_launch(self._g, stream.cuda_stream))
         if check and self._kernel in (2, 3):
             try:
-                _lib.check(self._lib.pwg_run_status(self.plan._p, self.ws.data_ptr(), stream.cuda_stream))
+                try:
+                    _lib.check(self._lib.pwg_run_status(self.plan._p, self.ws.data_ptr(), stream.cuda_stream))
+                except _lib.RerunError:
+                    # (the rerun uses the engine's workspace for this stream, so its status is there)
+                    eng._enqueue_per_layer(self.plan, self.mel, self.noise, self.out, self.mean, self.scale, stream)
+                    eng.sync_reruns += 1
+                    eng.run_status(self.plan, stream)
             except _lib.RangeError as e:
                 logging.warning("%s; rerunning on the exact-fp32 layer kernel", e)
                 kernel = eng.layer_kernel

@@ -286,6 +286,24 @@ class ParallelWaveGANGenerator(torch.nn.Module):
         c = c.to(dev, torch.float32)
         return self.inference_batch([c], [x], normalize_before)[0]
 
+    def _engine_deferred(self):
+        """(engine, refresh): the engine with the weights packed at the last check, and a callable
+        that runs the weight check (WeightTracker, ~25-50 us of host time for PWG v1) and re-packs
+        when a parameter changed, returning True then. The drop-in calls refresh() after the
+        forward is enqueued, so the check overlaps the GPU; a re-pack redoes the forward. Before
+        the first pack (or on a new device) the engine is built and checked up front."""
+        dev = self._device()
+        if self._engine is None or self._engine.device != dev or self._engine.packed is None:
+            return self.engine(), None
+
+        def refresh():
+            if not self._weights.changed(self):
+                return False
+            self.engine()
+            return True
+
+        return self._engine, refresh
+
     def inference_batch(self, cs, xs=None, normalize_before=False):
         """Ragged multi-utterance inference in ONE engine pass (no reference counterpart; the
         reference decodes one utterance per call, bin/decode.py:236-268).
@@ -293,7 +311,7 @@ class ParallelWaveGANGenerator(torch.nn.Module):
         cs: list of (T'_u, aux); xs: list of (T_u, 1) or None (CPU randn per utterance).
         Returns a list of (T_u, out_channels) device tensors.
         """
-        eng = self.engine()
+        eng, refresh = self._engine_deferred()
         dev = eng.device
         cs = [torch.as_tensor(c, dtype=torch.float32).to(dev).contiguous() for c in cs]
         for c in cs:
@@ -307,4 +325,4 @@ class ParallelWaveGANGenerator(torch.nn.Module):
         mean = scale = None
         if normalize_before:
             mean, scale = self.mean, self.scale  # AttributeError without register_stats, as the reference
-        return eng.infer(cs, xs, mean, scale)
+        return eng.infer(cs, xs, mean, scale, refresh=refresh)

@@ -333,6 +333,26 @@ def test_module_repacks_after_weight_update(built_lib, cuda_device):
     np.testing.assert_allclose(y2 - y1, 1.0, atol=1e-5)
 
 
+def test_module_repacks_after_storage_swap(built_lib, cuda_device):
+    """The drop-in checks its weights while the forward runs (models._engine_deferred): a call
+    after ``p.data = t`` launches on the old image, sees the swap, re-packs and redoes the
+    forward, so its output is the new weights' output; the next call launches on the new image."""
+    from parallelwavegan_amd import ParallelWaveGANGenerator, configs, synthetic
+
+    m = ParallelWaveGANGenerator(**configs.generator_params("reference_test")).eval().to(cuda_device)
+    mel = synthetic.make_mel(8, 10, seed=3)
+    x = synthetic.make_noise(8 * 16, seed=4)
+    y1 = m.inference(mel, x).cpu().numpy()
+    packed1 = m.engine().packed
+    b = m.last_conv_layers[3].bias
+    b.data = b.data + 2.0
+    y2 = m.inference(mel, x).cpu().numpy()
+    np.testing.assert_allclose(y2 - y1, 2.0, atol=1e-5)
+    assert m.engine().packed is not packed1
+    y3 = m.inference(mel, x).cpu().numpy()
+    np.testing.assert_array_equal(y2, y3)
+
+
 def test_engine_timing_buckets(built_lib, cuda_device):
     from parallelwavegan_amd import Engine, configs, synthetic
 

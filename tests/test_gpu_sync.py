@@ -1,0 +1,183 @@
+"""Grid-synchronised forward (PWG_OPT_SYNC; csrc/pwg_split16.hip pwg_sync_split16_kernel): residual
+layers 0 .. L - 2 of a small plan in ONE launch, one workgroup per CU, a grid barrier between
+layers (x and skip handed over with sc1 stores and loads), the last layer as its own launch (and
+layer 0 too on whole-block plans with the fused first_conv). Every
+layer runs the per-layer kernel's work units through the same block body, so the forward must be
+BIT-IDENTICAL to the per-layer launches: ragged batches, utterances shorter than a block, causal
+configs, first_conv fused or not, the batched forward() layout, graph replay and the drop-in's
+B = 1 call (bin/decode.py:236-268). GPU only; every forward goes through include/pwg.h."""
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _engines(params, dev, seed=0):
+    from parallelwavegan_amd import Engine, synthetic
+
+    sd = synthetic.make_state_dict(params, seed=seed)
+    engs = []
+    for sync in (0, 1 << 30):
+        e = Engine(params, dev)
+        e.load_state_dict(sd)
+        e.set_option("sync", sync)
+        assert e.get_option("sync") == sync
+        engs.append(e)
+    return engs
+
+
+def _inputs(lengths, hop, dev, seed=5):
+    rs = np.random.RandomState(seed)
+    mels = [torch.from_numpy(rs.standard_normal((f, 80)).astype(np.float32)).to(dev) for f in lengths]
+    noises = [torch.from_numpy(rs.standard_normal((f * hop, 1)).astype(np.float32)).to(dev) for f in lengths]
+    return mels, noises
+
+
+@pytest.mark.parametrize("cfg, lengths, over, fuse", [
+    ("ljspeech_v1", [64], {}, 1),
+    ("ljspeech_v1", [64], {}, 0),
+    ("ljspeech_v1", [128], {}, 1),
+    ("ljspeech_v1", [7, 30, 1, 2], {}, 1),
+    ("libritts_v1", [43, 17, 1, 20], {}, 1),
+    ("libritts_v1", [3, 1, 40], {"use_causal_conv": True}, 1),
+    ("ljspeech_v1", [7, 90, 2], {"use_causal_conv": True}, 0),
+    # whole-block plans (more blocks than PWG_OPT_HALF_BLOCKS allows): layer 0 runs per-layer when
+    # first_conv is fused
+    ("ljspeech_v1", [300], {}, 1),
+    ("ljspeech_v1", [300], {}, 0),
+    ("libritts_v1", [143, 17, 250], {"use_causal_conv": True}, 1),
+])
+def test_sync_bitwise_equal_to_per_layer(cfg, lengths, over, fuse, built_lib, cuda_device):
+    from parallelwavegan_amd import configs
+
+    params = configs.generator_params(cfg, **over)
+    per_layer, sync = _engines(params, cuda_device)
+    for e in (per_layer, sync):
+        e.set_option("fuse_first_conv", fuse)
+    hop = per_layer.upsample_factor
+    mels, noises = _inputs(lengths, hop, cuda_device)
+    ref = [y.cpu().numpy() for y in per_layer.infer(mels, noises)]
+    got = [y.cpu().numpy() for y in sync.infer(mels, noises)]
+    for a, b in zip(got, ref):
+        assert np.isfinite(a).all()
+        np.testing.assert_array_equal(a, b)
+
+
+def test_sync_launch_count_forward_layout_and_graph(built_lib, cuda_device):
+    """Two residual launches (the synchronised one and the last layer), the batched forward(z, c)
+    layout (models/parallel_wavegan.py:144-173), and graph replay: all bit-identical."""
+    from parallelwavegan_amd import GraphedRun, _lib, configs
+
+    params = configs.generator_params("ljspeech_v1")
+    per_layer, sync = _engines(params, cuda_device, seed=2)
+    mels, noises = _inputs([33], 256, cuda_device, seed=7)
+    sync.set_timing(True)
+    sync.collect_timing()
+    y = sync.infer(mels, noises)[0]
+    t = sync.collect_timing()
+    sync.set_timing(False)
+    assert t["residual_layer"][1] == 2
+    assert torch.equal(y, per_layer.infer(mels, noises)[0])
+
+    B, F, w = 2, 9, params["aux_context_window"]
+    rs = np.random.RandomState(3)
+    c = torch.from_numpy(rs.standard_normal((B, 80, F + 2 * w)).astype(np.float32)).to(cuda_device)
+    z = torch.from_numpy(rs.standard_normal((B, 1, F * 256)).astype(np.float32)).to(cuda_device)
+    outs = []
+    for e in (per_layer, sync):
+        plan = e.plan([F] * B, _lib.PWG_LAYOUT_FORWARD)
+        out = torch.empty(B, 1, F * 256, device=cuda_device)
+        e.run(plan, c, z, out)
+        outs.append(out.cpu().numpy())
+    np.testing.assert_array_equal(outs[1], outs[0])
+
+    g = GraphedRun(sync, sync.plan([64]))
+    for seed in (1, 2):
+        mels, noises = _inputs([64], 256, cuda_device, seed=seed)
+        y = g(mels[0], noises[0]).clone()
+        assert torch.equal(y, per_layer.infer(mels, noises)[0].reshape(-1))
+    del g
+
+
+def test_sync_many_runs_stay_identical(built_lib, cuda_device):
+    """The barrier counter is reset by every run (plan-descriptor kernel): 20 back-to-back runs on
+    one stream, no synchronisation between them, all bit-identical and none flagged."""
+    from parallelwavegan_amd import configs
+
+    params = configs.generator_params("ljspeech_v1")
+    per_layer, sync = _engines(params, cuda_device, seed=4)
+    mels, noises = _inputs([64, 5], 256, cuda_device, seed=9)
+    ref = per_layer.infer(mels, noises)[0].clone()
+    plan = sync.plan([64, 5])
+    mel = torch.cat([m.reshape(-1) for m in mels])
+    noise = torch.cat([n.reshape(-1) for n in noises])
+    outs = [torch.empty(plan.total_samples, device=cuda_device) for _ in range(20)]
+    for o in outs:
+        sync.run(plan, mel, noise, o, check=False)
+    sync.run_status(plan)
+    for o in outs:
+        assert torch.equal(o[: ref.numel()], ref.reshape(-1))
+
+
+def test_sync_concurrent_streams_complete(built_lib, cuda_device):
+    """Two synchronised forwards in flight at once on two streams (each wants every CU): each either
+    runs with all its workgroups resident or finds the GPU shared, decides "abort" for all its
+    workgroups at once and writes nothing, which pwg_run_status reports as PWG_ERR_RERUN and the
+    engine's check redoes on the per-layer launches. No wait may time out, and every output is
+    bit-identical to the per-layer forward."""
+    from parallelwavegan_amd import configs
+
+    params = configs.generator_params("ljspeech_v1")
+    per_layer, sync = _engines(params, cuda_device, seed=6)
+    lengths = [200]  # whole-block plan: 1,600 blocks, 6 per CU
+    mels, noises = _inputs(lengths, 256, cuda_device, seed=11)
+    ref = per_layer.infer(mels, noises)[0].reshape(-1).clone()
+    plan = sync.plan(lengths)
+    mel = mels[0].reshape(-1).contiguous()
+    noise = noises[0].reshape(-1).contiguous()
+    streams = [torch.cuda.Stream(cuda_device) for _ in range(2)]
+    torch.cuda.synchronize(cuda_device)
+    for _ in range(8):
+        outs = [torch.empty(plan.total_samples, device=cuda_device) for _ in streams]
+        for st, o in zip(streams, outs):
+            with torch.cuda.stream(st):
+                sync.run(plan, mel, noise, o, stream=st, check=False)
+        for st, o in zip(streams, outs):
+            with torch.cuda.stream(st):
+                sync._range_check(plan, mel, noise, o, None, None, st)
+        torch.cuda.synchronize(cuda_device)
+        for o in outs:
+            assert torch.equal(o, ref)
+    print("sync reruns", sync.sync_reruns)
+
+
+def test_sync_abort_reruns_per_layer(built_lib, cuda_device):
+    """The "abort" path itself: a stream kept busy by a long per-layer forward while the
+    synchronised one is queued on another stream; whatever the decision, the checked result is
+    the per-layer forward's, bit for bit."""
+    from parallelwavegan_amd import configs
+
+    params = configs.generator_params("ljspeech_v1")
+    per_layer, sync = _engines(params, cuda_device, seed=8)
+    mels, noises = _inputs([64], 256, cuda_device, seed=12)
+    ref = per_layer.infer(mels, noises)[0].reshape(-1).clone()
+    big = [512] * 8
+    bm, bn = _inputs(big, 256, cuda_device, seed=13)
+    bplan = per_layer.plan(big)
+    bmel = torch.cat([m.reshape(-1) for m in bm])
+    bnoise = torch.cat([n.reshape(-1) for n in bn])
+    bout = torch.empty(bplan.total_samples, device=cuda_device)
+    plan = sync.plan([64])
+    s1, s2 = torch.cuda.Stream(cuda_device), torch.cuda.Stream(cuda_device)
+    torch.cuda.synchronize(cuda_device)
+    for _ in range(4):
+        with torch.cuda.stream(s1):
+            per_layer.run(bplan, bmel, bnoise, bout, stream=s1, check=False)
+        o = torch.empty(plan.total_samples, device=cuda_device)
+        with torch.cuda.stream(s2):
+            sync.run(plan, mels[0].reshape(-1), noises[0].reshape(-1), o, stream=s2)
+        torch.cuda.synchronize(cuda_device)
+        assert torch.equal(o, ref)
+    print("sync reruns", sync.sync_reruns)

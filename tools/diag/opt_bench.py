@@ -20,6 +20,9 @@ if os.environ.get("PLANS") == "small":
     plans = plans[:4]
 elif os.environ.get("PLANS") == "lat":
     plans = [("ljspeech_v1", [f]) for f in (64, 96, 128, 192, 256, 384, 512)]
+elif os.environ.get("PLANS") == "latx":
+    plans = [("ljspeech_v1", [f]) for f in (64, 128, 256, 512, 768, 1024, 1536, 2048)]
+    plans += [("ljspeech_v1", [64] * 4), ("ljspeech_v1", [512] * 4), ("libritts_v1", [300, 120, 40])]
 for cfg, lengths in plans:
     params = configs.generator_params(cfg)
     row = {"config": cfg, "frames": lengths if len(lengths) <= 2 else f"{len(lengths)} utts, {sum(lengths)} frames"}
