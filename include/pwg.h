@@ -213,7 +213,7 @@ enum {
                                     B = 1 latency path. Bit-identical. 0 = never; default 4 x the
                                     CU count (one unit per wave at 8 waves per CU: LJ T' = 64
                                     0.42 -> 0.35 ms per forward; slower from ~4 blocks per CU on). */
-  PWG_OPT_SYNC = 6             /* split16: plans of at most this many 32-sample blocks run all residual
+  PWG_OPT_SYNC = 6,            /* split16: plans of at most this many 32-sample blocks run all residual
                                     layers in ONE launch, one workgroup per CU, a grid barrier in place
                                     of each launch boundary (the next layer's weights stage while the
                                     barrier completes); same work units and kernel body as the
@@ -223,6 +223,9 @@ enum {
                                     launches' work queues at 256 blocks per CU). A launch that
                                     finds the GPU shared writes nothing and pwg_run_status returns
                                     PWG_ERR_RERUN. */
+  PWG_OPT_SYNC_ABORT = 7       /* test hook: 1 makes every grid-synchronised launch take its "GPU shared"
+                                    exit (no output, PWG_ERR_RERUN from pwg_run_status), so the
+                                    caller's rerun path can be tested; default 0 */
 };
 #define PWG_PIPE_MAX_DEFAULT 0LL /* off: measured slower than the per-layer launches */
 PWG_API int pwg_set_option(PwgHandle* h, int option, long long value);

@@ -101,6 +101,7 @@ PWG_OPT_FUSE_FIRST_CONV = 3
 PWG_OPT_PIPELINE = 4
 PWG_OPT_HALF_BLOCKS = 5
 PWG_OPT_SYNC = 6
+PWG_OPT_SYNC_ABORT = 7
 
 
 class PwgConfig(ctypes.Structure):

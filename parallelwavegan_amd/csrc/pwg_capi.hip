@@ -315,6 +315,7 @@ struct PwgHandle {
   int layer_kernel = 0, waves_per_wg = 8, wg_per_cu = 1;
   int fuse_first = 1;  // PWG_OPT_FUSE_FIRST_CONV
   long long pipe_max = PWG_PIPE_MAX_DEFAULT;  // PWG_OPT_PIPELINE: largest padded plan on the layer pipeline
+  int sync_abort = 0;       // PWG_OPT_SYNC_ABORT (test hook)
   long long sync_max = -1;  // PWG_OPT_SYNC: most 32-sample blocks on the grid-synchronised forward (-1: 64 x n_cu)
   long long half_max = -1;  // PWG_OPT_HALF_BLOCKS: most blocks of a half-block launch (-1: 4 x n_cu)
   int n_cu = 0;
@@ -939,6 +940,9 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
   // grid needs one workgroup per CU for every layer and a multiple of 8 workgroups
   const int pipe_wg = h->n_cu / 8 * 8;
   const bool use_pipe = p->pipe_ok && h->layer_kernel == 3 && p->Tpad <= h->pipe_max && pipe_wg >= h->L;
+  const bool split = h->layer_kernel == 2 || h->layer_kernel == 3;
+  const bool split16 = h->layer_kernel == 3;
+  const bool fuse_first = split16 && h->fuse_first && h->L > 1;
   UttDesc* d_utts = (UttDesc*)(ws + p->ws_utts);
   int* d_tile_utt = (int*)(ws + p->ws_tile_utt);
   long long* d_gap_col0 = (long long*)(ws + p->ws_gap);
@@ -954,6 +958,10 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
     da.zero = u0 == 0 ? sched_ctr : nullptr;
     da.n_zero = (int)((p->ws_flag + sizeof(int) - p->ws_ctr) / sizeof(int));
     da.prog = use_pipe ? (int*)(ws + p->ws_prog) : nullptr;
+    // split16 with the fused first_conv: the gap tiles are zeroed here, not by a first_conv launch
+    da.zx[0] = fuse_first ? reinterpret_cast<unsigned*>(x0) : nullptr;
+    da.zx[1] = fuse_first ? reinterpret_cast<unsigned*>(x1) : nullptr;
+    da.zx[2] = fuse_first && use_pipe ? reinterpret_cast<unsigned*>(ws + p->ws_x2) : nullptr;
     e = launch_plan_desc(da, p->max_blocks_per_utt, s);
     if (e != hipSuccess) return hip_fail(e, "plan descriptor launch");
   }
@@ -966,8 +974,6 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
   if (e != hipSuccess) return hip_fail(e, "conv_in launch");
 
   AuxProjArgs pa;
-  const bool split = h->layer_kernel == 2 || h->layer_kernel == 3;
-  const bool split16 = h->layer_kernel == 3;
   pa.c1 = c1; pa.waux = packed + h->off_waux; pa.d = dproj; pa.F_total = p->F_total; pa.A = h->A; pa.GR = h->GR;
   pa.split = split16 ? 2 : split ? 1 : 0;
   pa.split_scale_a = (float)SPLIT_GATE_SCALE_TANH;
@@ -983,10 +989,9 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
   fa.x2 = use_pipe ? (float*)(ws + p->ws_x2) : nullptr;
   // split16 with the fused first_conv: layer 0 builds x0 itself; only the gap tiles of both
   // residual buffers are zeroed here (the work-tile branch is skipped: n_work = 0)
-  const bool fuse_first = split16 && h->fuse_first && h->L > 1;
   if (fuse_first) fa.n_work = 0;
   e = timed(PWG_KERNEL_FIRST_CONV, [&] {
-    if (fuse_first) return p->n_gap_tiles > 0 ? launch_first_conv_split16(fa, p->n_gap_tiles, s) : hipSuccess;
+    if (fuse_first) return hipSuccess;  // gap tiles zeroed by the plan-descriptor kernel
     return split16 ? launch_first_conv_split16(fa, p->n_tiles + p->n_gap_tiles, s)
            : split ? launch_first_conv_split(fa, p->n_tiles + p->n_gap_tiles, s)
                    : launch_first_conv(fa, p->n_tiles + p->n_gap_tiles, s);
@@ -1071,6 +1076,7 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
     sy.x[0] = reinterpret_cast<unsigned*>(x0);
     sy.x[1] = reinterpret_cast<unsigned*>(x1);
     sy.half = n_blocks_all <= half_max_all;
+    sy.force_abort = h->sync_abort;
     sync_begin = (!sy.half && fuse_first) ? 1 : 0;
     sync_end = h->L - 1;
     sy.l0 = sync_begin;
@@ -1384,6 +1390,10 @@ int pwg_set_option(PwgHandle* h, int option, long long value) {
       if (value < 0) return fail(PWG_ERR_INVALID, "grid-synchronised plan limit must be >= 0");
       h->sync_max = value;
       return PWG_OK;
+    case PWG_OPT_SYNC_ABORT:
+      if (value != 0 && value != 1) return fail(PWG_ERR_INVALID, "sync_abort must be 0 or 1");
+      h->sync_abort = (int)value;
+      return PWG_OK;
 
     default:
       return fail(PWG_ERR_INVALID, "unknown option");
@@ -1400,6 +1410,7 @@ int pwg_get_option(const PwgHandle* h, int option, long long* value) {
     case PWG_OPT_PIPELINE: *value = h->pipe_max; return PWG_OK;
     case PWG_OPT_HALF_BLOCKS: *value = h->half_max >= 0 ? h->half_max : 4LL * h->n_cu; return PWG_OK;
     case PWG_OPT_SYNC: *value = h->sync_max >= 0 ? h->sync_max : 64LL * h->n_cu; return PWG_OK;
+    case PWG_OPT_SYNC_ABORT: *value = h->sync_abort; return PWG_OK;
 
     default: return fail(PWG_ERR_INVALID, "unknown option");
   }

@@ -231,6 +231,7 @@ struct SyncArgs {
                              // line of its own (SCHED_CTR_STRIDE ints apart; zeroed per run)
   int l0, L;                 // the launch runs layers l0 .. l0 + L - 1
   int half;                  // half-block work units
+  int force_abort;           // test hook (PWG_OPT_SYNC_ABORT): take the "GPU shared" exit
   int waves_mid;             // computing waves per workgroup
   int dil[PIPE_MAX_LAYERS];
 };
@@ -259,6 +260,8 @@ struct PlanDescArgs {
   int* zero;      // first chunk only: the run's work-queue heads + range flag, zeroed here
   int n_zero;
   int* prog;      // layer pipeline: per-block progress words, zeroed with the block descriptors (or null)
+  unsigned* zx[3];  // split16 with the fused first_conv: residual planes whose gap tiles are zeroed
+                    // here (null: not here; x[2] null without the layer pipeline's third plane)
 };
 hipError_t launch_plan_desc(const PlanDescArgs& a, long long max_blocks, hipStream_t s);
 

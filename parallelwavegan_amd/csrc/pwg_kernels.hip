@@ -110,14 +110,17 @@ __global__ void __launch_bounds__(256) pwg_conv_in_kernel(const ConvInArgs a) {
 // the (replication-padded, normalized) input channel i at frame f + kk. M = A rows (MT m-tiles),
 // N = 32 frames per wave, K = A*KW in k-steps of 2 (lane half h takes k = 2s + h). The B operand
 // is one input value per lane and k-step (L1-resident: the mel tile is 5 frames wide).
-// conv_in with K split over the workgroup's 4 waves (the B = 1 latency path's first kernel): grid
-// (ceil(F_total / 32), MT), wave w sums k-steps [w Q, (w + 1) Q) of m-tile blockIdx.y for 32 frames
-// (lane layout above), loads double-buffered in groups of 8, the four
+// conv_in with K split over the workgroup's CONV_IN_WAVES waves (the B = 1 latency path's first
+// kernel): grid (ceil(F_total / 32), MT), wave w sums k-steps [w Q, (w + 1) Q) of m-tile
+// blockIdx.y for 32 frames (lane layout above), loads double-buffered in groups of 8, the
 // partial tiles summed through LDS in wave order. One wave per (32 frames, all of K, all m-tiles)
-// made a 64-frame utterance ONE chain of 200 k-steps x 3 MFMAs behind 25 load waits: 94 us.
+// made a 64-frame utterance ONE chain of 200 k-steps x 3 MFMAs behind 25 load waits: 94 us; 4
+// waves 23 us; 16 waves (13 k-steps, two load groups each) measured below that.
+constexpr int CONV_IN_WAVES = 16;
 template <int MT>
-__global__ void __launch_bounds__(256) pwg_conv_in_ksplit_kernel(const ConvInArgs a) {
-  __shared__ float s_red[4][16][64];
+__global__ void __launch_bounds__(64 * CONV_IN_WAVES) pwg_conv_in_ksplit_kernel(const ConvInArgs a) {
+  constexpr int NW = CONV_IN_WAVES;
+  __shared__ float s_red[NW][16][64];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int hh = lane >> 5, cl = lane & 31;
@@ -132,7 +135,7 @@ __global__ void __launch_bounds__(256) pwg_conv_in_ksplit_kernel(const ConvInArg
   const long long Tin = Tf + 2 * a.ctx;
   const int K = a.A * a.KW;
   const int nks = (K + 1) / 2;
-  const int Q = (nks + 3) / 4;
+  const int Q = (nks + NW - 1) / NW;
   const int s_begin = wave * Q, s_end = min(nks, s_begin + Q);
   const float* wl = a.wfrag + lane;
   auto load = [&](int s0, float (&x)[8], float (&w)[8]) {
@@ -172,11 +175,11 @@ __global__ void __launch_bounds__(256) pwg_conv_in_ksplit_kernel(const ConvInArg
 #pragma unroll
   for (int r = 0; r < 16; ++r) s_red[wave][r][lane] = acc[r];
   __syncthreads();
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int v = threadIdx.x + 256 * j;
+  for (int v = threadIdx.x; v < 16 * 64; v += 64 * NW) {
     const int r = v >> 6, l = v & 63;
-    const float sum = ((s_red[0][r][l] + s_red[1][r][l]) + s_red[2][r][l]) + s_red[3][r][l];
+    float sum = s_red[0][r][l];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) sum += s_red[w][r][l];
     const long long gg = (long long)blockIdx.x * 32 + (l & 31);
     const int o = 32 * m + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
     if (gg < a.F_total && o < a.A) a.c1[(size_t)o * a.F_total + gg] = sum;
@@ -205,6 +208,8 @@ __global__ void __launch_bounds__(256) pwg_aux_proj_kernel(const AuxProjArgs a) 
   for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
+  // (issuing all 40 k-steps' loads at once measured slower, 14 -> 25 us at LJ T' = 64: past the
+  // wave's 63 outstanding vector loads the waits serialise anyway)
   for (int s0 = 0; s0 < nks; s0 += 8) {  // groups of 8 k-steps, loads first (as conv_in)
     float b[8], wv[8][MT];
 #pragma unroll
@@ -1157,6 +1162,23 @@ __global__ void __launch_bounds__(256) pwg_plan_desc_kernel(const PlanDescArgs a
   // memset captured into a HIP graph did not reset them on every replay)
   if (a.zero != nullptr && blockIdx.x == 0 && y == 0)
     for (int i = threadIdx.x; i < a.n_zero; i += 256) a.zero[i] = 0;
+  // gap tiles of the residual planes (the layers read them as the zero padding of the dilated
+  // taps): the gap after this utterance, and chunk 0's leading gap (saves the B = 1 path a launch)
+  if (a.zx[0] != nullptr && blockIdx.x == 0) {
+    const long long seg_end = d.seg_base + (d.T + TILE - 1) / TILE * TILE;
+    const int lead = a.u0 == 0 && y == 0 ? a.gap_tiles : 0;
+    const int n4 = 64 * TILE / 4;  // 16-byte stores per tile per plane
+    typedef unsigned u32x4z __attribute__((ext_vector_type(4)));
+    for (int t = 0; t < a.gap_tiles + lead; ++t) {
+      const long long col0 = t < a.gap_tiles ? seg_end + (long long)t * TILE : (long long)(t - a.gap_tiles) * TILE;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) {
+        if (a.zx[pl] == nullptr) continue;
+        u32x4z* z = reinterpret_cast<u32x4z*>(a.zx[pl] + (size_t)col0 * 64);
+        for (int i = threadIdx.x; i < n4; i += 256) z[i] = u32x4z{0u, 0u, 0u, 0u};
+      }
+    }
+  }
 }
 
 hipError_t launch_plan_desc(const PlanDescArgs& a, long long max_blocks, hipStream_t s) {
@@ -1171,10 +1193,10 @@ hipError_t launch_conv_in(const ConvInArgs& a, hipStream_t s) {
     const int mt = (a.A + 31) / 32;
     const dim3 grid((unsigned)((a.F_total + 31) / 32), (unsigned)mt);
     switch (mt) {
-      case 1: hipLaunchKernelGGL(pwg_conv_in_ksplit_kernel<1>, grid, dim3(256), 0, s, a); break;
-      case 2: hipLaunchKernelGGL(pwg_conv_in_ksplit_kernel<2>, grid, dim3(256), 0, s, a); break;
-      case 3: hipLaunchKernelGGL(pwg_conv_in_ksplit_kernel<3>, grid, dim3(256), 0, s, a); break;
-      default: hipLaunchKernelGGL(pwg_conv_in_ksplit_kernel<4>, grid, dim3(256), 0, s, a); break;
+      case 1: hipLaunchKernelGGL(pwg_conv_in_ksplit_kernel<1>, grid, dim3(64 * CONV_IN_WAVES), 0, s, a); break;
+      case 2: hipLaunchKernelGGL(pwg_conv_in_ksplit_kernel<2>, grid, dim3(64 * CONV_IN_WAVES), 0, s, a); break;
+      case 3: hipLaunchKernelGGL(pwg_conv_in_ksplit_kernel<3>, grid, dim3(64 * CONV_IN_WAVES), 0, s, a); break;
+      default: hipLaunchKernelGGL(pwg_conv_in_ksplit_kernel<4>, grid, dim3(64 * CONV_IN_WAVES), 0, s, a); break;
     }
     return hipGetLastError();
   }

@@ -860,7 +860,7 @@ __global__ void __launch_bounds__(512, 1) pwg_sync_split16_kernel(const SyncArgs
     s_decision = d;
   }
   __syncthreads();
-  if (s_decision != 1) {
+  if (s_decision != 1 || p.force_abort) {
     if (threadIdx.x == 0) __hip_atomic_fetch_or(p.base.range_flag, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }

@@ -361,7 +361,7 @@ class Engine:
     _OPTS = {"layer_kernel": _lib.PWG_OPT_LAYER_KERNEL, "waves_per_wg": _lib.PWG_OPT_WAVES_PER_WG,
              "wg_per_cu": _lib.PWG_OPT_WG_PER_CU, "fuse_first_conv": _lib.PWG_OPT_FUSE_FIRST_CONV,
              "pipeline": _lib.PWG_OPT_PIPELINE, "half_blocks": _lib.PWG_OPT_HALF_BLOCKS,
-             "sync": _lib.PWG_OPT_SYNC}
+             "sync": _lib.PWG_OPT_SYNC, "sync_abort": _lib.PWG_OPT_SYNC_ABORT}
 
     def get_option(self, option):
         v = ctypes.c_longlong()

@@ -181,3 +181,36 @@ def test_sync_abort_reruns_per_layer(built_lib, cuda_device):
         torch.cuda.synchronize(cuda_device)
         assert torch.equal(o, ref)
     print("sync reruns", sync.sync_reruns)
+
+
+def test_sync_abort_path_writes_nothing_and_reruns(built_lib, cuda_device):
+    """PWG_OPT_SYNC_ABORT forces the residency exit: the launch writes no x or skip,
+    pwg_run_status returns PWG_ERR_RERUN, and Engine.run(check=True) / the drop-in redo the forward
+    on the per-layer launches: bit-identical output, one rerun counted per call."""
+    from parallelwavegan_amd import ParallelWaveGANGenerator, _lib, configs, synthetic
+
+    params = configs.generator_params("ljspeech_v1")
+    per_layer, sync = _engines(params, cuda_device, seed=9)
+    sync.set_option("sync_abort", 1)
+    mels, noises = _inputs([64, 3], 256, cuda_device, seed=14)
+    ref = [y.clone() for y in per_layer.infer(mels, noises)]
+    plan = sync.plan([64, 3])
+    mel = torch.cat([m.reshape(-1) for m in mels])
+    noise = torch.cat([n.reshape(-1) for n in noises])
+    out = torch.full((plan.total_samples,), float("nan"), device=cuda_device)
+    sync.run(plan, mel, noise, out, check=False)
+    with pytest.raises(_lib.RerunError):
+        sync.run_status(plan)
+    sync.run(plan, mel, noise, out)  # check=True: reruns per-layer
+    assert sync.sync_reruns == 1
+    assert torch.equal(out, torch.cat([y.reshape(-1) for y in ref]))
+
+    m = ParallelWaveGANGenerator(**params)
+    m.remove_weight_norm()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic.make_state_dict(params, seed=9).items()})
+    m = m.eval().to(cuda_device)
+    m.engine().set_option("sync_abort", 1)
+    with torch.no_grad():
+        y = m.inference(mels[0], noises[0])
+    assert m.engine().sync_reruns == 1
+    assert torch.equal(y.reshape(-1), ref[0].reshape(-1))
