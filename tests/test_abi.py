@@ -173,6 +173,24 @@ def test_get_option_reports_default_layer_kernel(built_lib):
         assert v.value == kernel, name
 
 
+def test_sync_options_round_trip_and_validate(built_lib):
+    """PWG_OPT_SYNC (grid-synchronised plan limit, >= 0) and PWG_OPT_SYNC_ABORT (test hook, 0/1):
+    set / get round trip and argument checks, host-only; the error codes map to the Python
+    exceptions (PWG_ERR_RERUN -> RerunError)."""
+    h = HostHandle(configs.generator_params("ljspeech_v1"))
+    v = ctypes.c_longlong()
+    for opt, good, bad in ((_lib.PWG_OPT_SYNC, (0, 4096, 1 << 40), (-1,)),
+                           (_lib.PWG_OPT_SYNC_ABORT, (0, 1), (2, -1))):
+        for val in good:
+            _lib.check(built_lib.pwg_set_option(h._h, opt, val))
+            _lib.check(built_lib.pwg_get_option(h._h, opt, ctypes.byref(v)))
+            assert v.value == val
+        for val in bad:
+            assert built_lib.pwg_set_option(h._h, opt, val) == _lib.PWG_ERR_INVALID
+    assert _lib._ERRORS[_lib.PWG_ERR_RERUN] is _lib.RerunError
+    assert issubclass(_lib.RerunError, RuntimeError)
+
+
 def test_rccl_entry_points_validate_arguments(built_lib):
     """Argument checks of the RCCL entries need no GPU (no communicator is created)."""
     assert built_lib.pwg_rccl_unique_id(None) == _lib.PWG_ERR_INVALID
