@@ -1085,12 +1085,14 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
     sy.ctr = sched_ctr + (size_t)sync_begin * SCHED_CTR_STRIDE * 8;
     sy.L = sync_end - sync_begin;
     for (int l = 0; l < PIPE_MAX_LAYERS; ++l) sy.dil[l] = l < h->L ? h->dil[l] : 1;
-    // the per-layer launch's work-unit rules (below), at one workgroup per CU
+    // the per-layer launch's work-unit rules (below), at one workgroup per CU, without its 4-wave
+    // cap for 8-32 units per CU (that cap answers the work queues' issue-arbitration imbalance;
+    // with the static split 8 waves measured faster: LJ T' = 768 1.65 -> 1.57 ms, T' = 1024
+    // 2.15 -> 1.92 ms, `profiles/r03_sync/cap8_*.jsonl`)
     const long long nwg = h->n_cu;
     auto waves = [&](long long units) {
       int w = std::min(8, h->waves_per_wg);
       if (PWG_SMALL_SPREAD && units < nwg * w) w = (int)std::max(1LL, (units + nwg - 1) / nwg);
-      if (units > 8LL * h->n_cu && units <= 32LL * h->n_cu) w = std::min(w, 4);
       return w;
     };
     sy.waves_mid = waves(sy.half ? 2 * n_blocks_all : n_blocks_all);
