@@ -340,7 +340,7 @@ def cpu_baseline(params, sd, config, n_utts, reps=1):
     H = int(np.prod(params["upsample_params"]["upsample_scales"]))
     gen.inference(synthetic.make_mel(40, A, seed=99), synthetic.make_noise(40 * H, seed=98))  # warm-up
     idx, lengths = cpu_subset(n_pick=n_utts)
-    done, t_total = 0, 0.0
+    done, t_total, rates = 0, 0.0, []
     for i, f in zip(idx, lengths):
         mel = synthetic.make_mel(int(f), A, seed=1000 + i)
         noise = synthetic.make_noise(int(f) * H, seed=2000 + i)
@@ -352,14 +352,18 @@ def cpu_baseline(params, sd, config, n_utts, reps=1):
             best = dt if best is None else min(best, dt)
         t_total += best
         done += int(f) * H
+        rates.append(int(f) * H / best)
     protocol = ("BASELINE.md sec 4 protocol (16-utterance subset, best of 3)" if n_utts >= 16 and reps >= 3 else
-                f"{len(idx)} of BASELINE.md sec 4's 16 subset utterances, best of {reps} (the full protocol, "
-                f"--cpu-utts 16 --cpu-reps 3, takes ~5 min of CPU; this line keeps to a bounded sample)")
+                f"BASELINE.md sec 4's 16-utterance subset, best of {reps}" if n_utts >= 16 else
+                f"{len(idx)} of BASELINE.md sec 4's 16 subset utterances, best of {reps}")
     desc = (f"{config}: {len(idx)} utterances of the 512-utterance RandomState(3) list at evenly spaced length "
             f"ranks (T' = {', '.join(str(int(f)) for f in lengths)}; {done} samples), B=1 each, torch-CPU aten "
             f"restatement of the reference op sequence, {threads} threads; {protocol}")
+    rates.sort()
+    spread = {"min": round(rates[0], 1), "median": round(rates[len(rates) // 2], 1), "max": round(rates[-1], 1),
+              "unit": "audio samples/s per utterance"}
     return dict({"value": round(done / t_total, 1), "unit": "audio samples/s", "cores": threads, "kind": "port",
-                 "sample": desc, "seconds": round(t_total, 2)}, **info)
+                 "sample": desc, "seconds": round(t_total, 2), "per_utterance_spread": spread}, **info)
 
 
 VOCODERS = ["mb_melgan_v2", "hifigan_v1", "melgan_v1"]
@@ -456,10 +460,12 @@ def vocoder_setup(args, dev):
     return m, eng, cls_name, params, (sd, syn)
 
 
-def bench_vocoder(args, rank, world, dev, live_traffic=(None, "off", None)):
+def bench_vocoder(args, rank, world, dev, live_traffic=(None, "off", None), embedded=False):
     """MelGAN-family generator inference (BASELINE configs[2] multi_band_melgan.v2 and [3]
     hifigan.v1) on the conv-network executor: same ragged-batch workload shape
-    as the PWG bench, weak scaling, utterance sharding, RCCL weight broadcast."""
+    as the PWG bench, weak scaling, utterance sharding, RCCL weight broadcast.
+    embedded: called from the default PWG line (N = 1): return the result object instead of
+    printing it (the line's "vocoders" object)."""
     from oracle.melgan_torch_cpu import TorchCPUVocoder  # cpu_baseline leg only
     from parallelwavegan_amd.engine import fold_weight_norm
 
@@ -495,7 +501,7 @@ def bench_vocoder(args, rank, world, dev, live_traffic=(None, "off", None)):
         dist.barrier()
     local_elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(local_elapsed, dev)
-    rank_seconds = per_rank_seconds(local_elapsed, world, dev)
+    rank_seconds = per_rank_seconds(local_elapsed, world, dev) if not embedded else [local_elapsed]
     eng.set_timing(False)
     timing = eng.collect_timing()
     if eng.split_f16:
@@ -505,8 +511,9 @@ def bench_vocoder(args, rank, world, dev, live_traffic=(None, "off", None)):
     samples = int(lengths.sum()) * hop
     value = samples * world * args.steps / elapsed
     if rank != 0:
-        dist.destroy_process_group()
-        return
+        if not embedded:
+            dist.destroy_process_group()
+        return None
     fl_frame = program_flops_per_frame(P)
     by_frame = program_bytes_per_frame(P)
     kern_ms = sum(ms for _, ms, _ in timing) / args.steps
@@ -583,9 +590,63 @@ def bench_vocoder(args, rank, world, dev, live_traffic=(None, "off", None)):
         "cpu_baseline": cpu,
         "latency": lat,
     }
+    if embedded:
+        for k in ("n_gpus", "ranks", "rank_seconds", "higher_is_better", "scaling", "vs_baseline", "data", "warmup"):
+            res.pop(k, None)
+        res["config"].pop("parallelism", None)
+        return res
     print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+# Vocoder configs carried in the default PWG line (BASELINE.json configs[2] and [3]).
+EMBED_VOCODERS = ["mb_melgan_v2", "hifigan_v1"]
+
+
+def with_config(args, config):
+    """A copy of the parsed arguments with another --config (the embedded vocoder runs)."""
+    a = argparse.Namespace(**vars(args))
+    a.config = config
+    a.layer_kernel = None
+    return a
+
+
+def exact_fp32_leg(eng, plan, mel, noise, out, params, steps):
+    """The precision-matched number: the same PWG bench batch on the
+    exact-fp32 layer kernel (pwg_layer_persistent_kernel, v_mfma_f32_32x32x2_f32, no fp16 pairs),
+    one warm-up and `steps` timed forwards, per-launch HIP events. The roofline is the fp32 MFMA
+    peak in the reference formulation's FLOPs."""
+    dev = eng.device
+    kernel = eng.layer_kernel
+    eng.set_option("layer_kernel", "persistent")
+    try:
+        eng.run(plan, mel, noise, out, check=False)
+        torch.cuda.synchronize(dev)
+        eng.set_timing(True)
+        eng.collect_timing()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            eng.run(plan, mel, noise, out, check=False)
+        torch.cuda.synchronize(dev)
+        wall = time.perf_counter() - t0
+        eng.set_timing(False)
+        timing = eng.collect_timing()
+    finally:
+        eng.set_option("layer_kernel", kernel)
+    if not torch.isfinite(out).all():
+        raise RuntimeError("non-finite exact-fp32 output")
+    layer_ms, layer_n = timing["residual_layer"]
+    avg_s = layer_ms / 1e3 / max(layer_n, 1)
+    flop_launch = layer_flops_per_sample(params) * plan.total_samples
+    tf = flop_launch / avg_s / 1e12
+    return {"kernel": "pwg_layer_persistent_kernel (exact fp32, v_mfma_f32_32x32x2_f32)", "dtype": "f32",
+            "value": round(plan.total_samples * steps / wall, 1), "unit": "audio samples/s",
+            "steps": steps, "ms_per_step": round(wall / steps * 1e3, 3),
+            "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(tf / FP32_PEAK_TFLOPS, 4), "avg_launch_ms": round(avg_s * 1e3, 4),
+                         "launches_timed": layer_n, "reference_flop_per_launch": int(flop_launch),
+                         "note": "reference-formulation FLOPs (the aux 1x1 runs at frame rate, so fewer are executed)"}}
 
 
 def latency_rows(dev, reps=20):
@@ -669,10 +730,15 @@ def main():
                     help="SURVEY.md sec 8(d)(5): the fixed 512-utterance RandomState(3) list, LPT-sharded over "
                          "the ranks (strong scaling); one step = the whole list")
     ap.add_argument("--cpu-seconds", type=float, default=None, help="0 = skip the CPU baseline (other values: legacy)")
-    ap.add_argument("--cpu-utts", type=int, default=4,
+    ap.add_argument("--cpu-utts", type=int, default=16,
                     help="CPU baseline sample: utterances of BASELINE.md sec 4's stratified subset (16 = all of it)")
     ap.add_argument("--cpu-reps", type=int, default=1, help="CPU baseline: timings per utterance, best kept (3 = BASELINE.md)")
     ap.add_argument("--no-latency", action="store_true", help="skip the B=1 / B=16 latency rows")
+    ap.add_argument("--no-vocoders", action="store_true",
+                    help="PWG line: skip the embedded MB-MelGAN v2 / HiFiGAN v1 runs (configs[2], [3])")
+    ap.add_argument("--no-exact", action="store_true", help="PWG line: skip the exact-fp32 leg")
+    ap.add_argument("--voc-cpu-seconds", type=float, default=6.0,
+                    help="embedded vocoder runs: CPU-baseline budget per vocoder (0 = skip)")
     ap.add_argument("--sub-plans", type=int, default=1,
                     help="experiment: run the per-GPU utterances as this many sequential sub-batches")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "layer_traffic.json"),
@@ -710,6 +776,13 @@ def main():
     voc_traffic = (None, "off", None)
     if single and args.config in VOCODERS:
         voc_traffic = measure_program_traffic(args)
+    embed = (int(os.environ.get("WORLD_SIZE", "1")) == 1 and args.config not in VOCODERS and not args.strong
+             and not args.no_vocoders and args.sub_plans == 1)
+    embed_traffic = {}
+    if embed:
+        for vc in EMBED_VOCODERS:
+            embed_traffic[vc] = (measure_program_traffic(with_config(args, vc)) if args.pmc == "auto"
+                                 else (None, "off", None))
     rank, world, dev = dist_setup(args.gpus)
     _lib.build()
     if args.config in VOCODERS:
@@ -822,6 +895,10 @@ def main():
         eng.run_status(plan)
     if not torch.isfinite(out).all():
         raise RuntimeError("non-finite generator output")
+    exact = None
+    if (world == 1 and not args.no_exact and not args.strong and subs is None
+            and args.layer_kernel in ("split", "split16")):
+        exact = exact_fp32_leg(eng, plan, mel, noise, out, params, max(2, min(args.steps, 5)))
 
     # PCIe-inclusive rate (never `value`): host mel + noise in pinned memory -> H2D -> forward ->
     # D2H of the audio, like inference() called on host arrays (models/parallel_wavegan.py:244-263)
@@ -974,6 +1051,14 @@ def main():
         "latency": lat,
     }
     res["rank_seconds"] = [round(x, 4) for x in rank_seconds]
+    res["exact_fp32"] = exact
+    if embed:
+        vocs = {}
+        for vc in EMBED_VOCODERS:
+            va = with_config(args, vc)
+            va.cpu_seconds = args.voc_cpu_seconds
+            vocs[vc] = bench_vocoder(va, 0, 1, dev, embed_traffic[vc], embedded=True)
+        res["vocoders"] = vocs
     if args.strong:
         per = rank_seconds
         res["strong"] = {"shard_frames": loads, "frame_imbalance": round(max(loads) / (sum(loads) / world), 4),

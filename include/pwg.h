@@ -61,9 +61,10 @@ enum {
   PWG_ERR_RANGE = 5,       /* a value left the fp16 pair range of the split-f16 kernels (no reference
                               counterpart: the reference computes in fp32; the drop-in reruns on the
                               exact-fp32 kernel, see pwg_run_status) */
-  PWG_ERR_RERUN = 6        /* pwg_run_status: the grid-synchronised forward (PWG_OPT_SYNC) found the GPU
-                              shared and wrote no output; rerun with PWG_OPT_SYNC 0 (the Python
-                              engine does) */
+  PWG_ERR_RERUN = 6        /* pwg_run_status: a grid-synchronised (PWG_OPT_SYNC) or layer-pipelined
+                              forward did not complete (the GPU was shared, or a bounded wait gave
+                              up); its output is invalid (NaN); rerun with PWG_OPT_SYNC 0 and
+                              PWG_OPT_PIPELINE 0 (the Python engine does) */
 };
 
 /* Input layouts accepted by pwg_plan_create / pwg_run. */
@@ -161,15 +162,25 @@ PWG_API long long pwg_plan_workspace_bytes(const PwgPlan* p);
 PWG_API int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* noise,
             const float* mean, const float* scale, float* out, void* workspace, void* stream);
 
-/* Range check of the last pwg_run on `workspace` (split-f16 layer kernels, which carry
- * fp32 operands as fp16 hi+lo pairs): synchronises `stream` and returns PWG_ERR_RANGE
- * if any live column's final skip sum was not finite, i.e. some x / D / first_conv value
- * exceeded the fp16 range (|v| >= 65520) or the input itself was not finite. The output of
- * such a run is not valid; rerun it with PWG_OPT_LAYER_KERNEL 0 (exact fp32), which is
- * what the Python drop-in does. The exact-fp32 kernels never set the flag. The split16 aux
- * projection also flags a D value beyond the pair range, and the last layer a scaled skip sum
- * the head cannot split. PWG_ERR_HIP: a layer-pipelined run (PWG_OPT_PIPELINE) whose bounded
- * dependency wait gave up; its output is invalid. */
+/* Status of the last pwg_run on `workspace`, and of every run of this handle since the previous
+ * pwg_run_status call on it (a sticky per-handle word that this call reads and clears):
+ * synchronises `stream`, then returns
+ *   PWG_ERR_RERUN  a grid-synchronised forward (PWG_OPT_SYNC) found the GPU shared and computed
+ *                  nothing (status bit 4), or one of its grid-barrier waits gave up (bit 8), or a
+ *                  layer-pipelined forward's dependency wait gave up (bit 2). The output of such a
+ *                  run is not valid (after a bit-4 or bit-8 run the last layer writes NaN audio);
+ *                  rerun it with PWG_OPT_SYNC 0 (and PWG_OPT_PIPELINE 0), which rebuilds every
+ *                  intermediate from the mel and the noise. The Python drop-in does this itself.
+ *   PWG_ERR_RANGE  (split-f16 layer kernels, which carry fp32 operands as fp16 hi+lo pairs; bit 1)
+ *                  a live column's final skip sum was not finite, i.e. some x / D / first_conv value
+ *                  exceeded the fp16 range (|v| >= 65520), or the input itself was not finite; the
+ *                  split16 aux projection also flags a D value beyond the pair range, and the last
+ *                  layer a scaled skip sum the head cannot split. Rerun with PWG_OPT_LAYER_KERNEL 0
+ *                  (exact fp32), as the drop-in does. The exact-fp32 kernels never set it.
+ * While PWG_OPT_SYNC is on (the default for small plans) a caller that enqueues runs without
+ * checking each one must still call this before trusting any of their outputs: the sticky word
+ * makes one call per batch of runs enough to learn that SOME run needs redoing (it does not say
+ * which; redo them all, or check after every run as the drop-in does). */
 PWG_API int pwg_run_status(PwgPlan* p, const void* workspace, void* stream);
 
 /* HIP graph of one pwg_run with fixed buffers (no reference counterpart: the replay path for
@@ -223,9 +234,13 @@ enum {
                                     launches' work queues at 256 blocks per CU). A launch that
                                     finds the GPU shared writes nothing and pwg_run_status returns
                                     PWG_ERR_RERUN. */
-  PWG_OPT_SYNC_ABORT = 7       /* test hook: 1 makes every grid-synchronised launch take its "GPU shared"
+  PWG_OPT_SYNC_ABORT = 7,      /* test hook: 1 makes every grid-synchronised launch take its "GPU shared"
                                     exit (no output, PWG_ERR_RERUN from pwg_run_status), so the
                                     caller's rerun path can be tested; default 0 */
+  PWG_OPT_SYNC_TIMEOUT = 8     /* test hook: 1 makes every grid-barrier wait of a grid-synchronised
+                                    launch give up at once (its workgroups run ahead on partial
+                                    planes, status bit 8, NaN audio, PWG_ERR_RERUN from
+                                    pwg_run_status); default 0 */
 };
 #define PWG_PIPE_MAX_DEFAULT 0LL /* off: measured slower than the per-layer launches */
 PWG_API int pwg_set_option(PwgHandle* h, int option, long long value);

@@ -82,7 +82,9 @@ typedef struct PwgCnet PwgCnet;
 typedef struct PwgCnetPlan PwgCnetPlan;
 
 PWG_API int pwg_cnet_abi_version(void);
-/* n_bufs buffers with `channels[b]` channels and `rate[b]` rows per input frame. */
+/* n_bufs buffers with `channels[b]` channels and `rate[b]` rows per input frame. device -1 creates a
+ * host-only handle: packing, and plans that are built and checked (pwg_cnet_plan_rows /
+ * _workspace_bytes answer) but never uploaded; pwg_cnet_run refuses them. */
 PWG_API int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* channels, const int* rate,
                     long long ref_weight_count, int device, PwgCnet** out);
 PWG_API void pwg_cnet_destroy(PwgCnet* n);

@@ -102,6 +102,7 @@ PWG_OPT_PIPELINE = 4
 PWG_OPT_HALF_BLOCKS = 5
 PWG_OPT_SYNC = 6
 PWG_OPT_SYNC_ABORT = 7
+PWG_OPT_SYNC_TIMEOUT = 8
 
 
 class PwgConfig(ctypes.Structure):
@@ -147,7 +148,7 @@ def _compile_cmd(hipcc, extra_flags):
     ] + list(extra_flags)
 
 
-def build(force=False, verbose=False, extra_flags=(), out_path=None, jobs=None):
+def build(force=False, verbose=False, extra_flags=(), out_path=None, jobs=None, link_flags=()):
     """Compile the HIP kernels + C-ABI into parallelwavegan_amd/lib/libpwg_hip.so (gfx950): one
     hipcc -c per source in parallel (objects under build/<variant>/, rebuilt when a source or
     header is newer), then one link. extra_flags/out_path build A/B measurement variants (e.g.
@@ -187,7 +188,8 @@ def build(force=False, verbose=False, extra_flags=(), out_path=None, jobs=None):
     with open(stamp, "w") as f:
         f.write(flags_txt)
     tmp = target + ".tmp.%d" % os.getpid()
-    cmd = [hipcc, f"--offload-arch={OFFLOAD_ARCH}", "-shared", "-fPIC", "-o", tmp] + [o for o, _ in results] + ["-ldl"]
+    cmd = ([hipcc, f"--offload-arch={OFFLOAD_ARCH}", "-shared", "-fPIC", "-o", tmp] + [o for o, _ in results]
+           + list(link_flags) + ["-ldl"])
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError("hipcc link failed:\n" + " ".join(cmd) + "\n" + res.stdout + res.stderr)
@@ -197,6 +199,66 @@ def build(force=False, verbose=False, extra_flags=(), out_path=None, jobs=None):
                 print(log)
     os.replace(tmp, target)
     return target
+
+
+# Host-side sanitizer build: the C-ABI's host code (config checks, weight
+# packing, PWG and conv-network plan builders) under AddressSanitizer + UndefinedBehaviorSanitizer,
+# with every uninitialised automatic variable filled with a 0xAA pattern (a field that is never
+# assigned then holds a large, deterministic garbage value instead of whatever the stack held,
+# which is how an uninitialised OpPhase field once produced a garbage block list and a GPU fault).
+# Device code is built unoptimised (-O0: 1 min instead of 3; it never runs) and unsanitised (each
+# -fsanitize= only after -Xarch_host): this library is for the host-only tests in this container
+# (tests/test_host_sanitized.py), never for a GPU run.
+SANITIZE_FLAGS = ["-O1", "-g", "-Xarch_device", "-O0"] + [f for x in ("-fsanitize=address", "-fsanitize=undefined", "-fno-omit-frame-pointer",
+                                               "-ftrivial-auto-var-init=pattern") for f in ("-Xarch_host", x)]
+SANITIZE_LINK = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined", "-shared-libsan"]
+SANITIZED_LIB_PATH = os.path.join(REPO_DIR, "build", "sanitized", "libpwg_hip_asan.so")
+
+
+SANITIZED_SOURCES = ("pwg_capi.hip", "pwg_cnet.hip")  # the host plan builders; the others are launchers
+
+
+def build_host_sanitized(force=False):
+    """Build SANITIZED_LIB_PATH: pwg_capi.hip and pwg_cnet.hip (config checks, packing, plan
+    builders) compiled with SANITIZE_FLAGS, linked with the product build's objects of the other
+    sources (kernels and their launchers; build() first). Returns the library path."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    build()
+    objdir = os.path.dirname(SANITIZED_LIB_PATH)
+    os.makedirs(objdir, exist_ok=True)
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    base = _compile_cmd(hipcc, SANITIZE_FLAGS)
+    newest = max(os.path.getmtime(f) for f in CSRC + HEADERS)
+    if not force and os.path.exists(SANITIZED_LIB_PATH) and os.path.getmtime(SANITIZED_LIB_PATH) >= newest:
+        return SANITIZED_LIB_PATH
+
+    def compile_one(src):
+        obj = os.path.join(objdir, os.path.basename(src) + ".o")
+        res = subprocess.run(base + ["-c", "-o", obj, src], capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError("hipcc (sanitized) failed:\n" + res.stdout + res.stderr)
+        return obj
+
+    srcs = [c for c in CSRC if os.path.basename(c) in SANITIZED_SOURCES]
+    with ThreadPoolExecutor(max_workers=len(srcs)) as ex:
+        objs = list(ex.map(compile_one, srcs))
+    product = os.path.join(REPO_DIR, "build", os.path.splitext(os.path.basename(LIB_PATH))[0])
+    objs += [os.path.join(product, os.path.basename(c) + ".o") for c in CSRC if os.path.basename(c) not in SANITIZED_SOURCES]
+    cmd = ([hipcc, f"--offload-arch={OFFLOAD_ARCH}", "-shared", "-fPIC", "-o", SANITIZED_LIB_PATH] + objs
+           + SANITIZE_LINK + ["-ldl"])
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError("hipcc link (sanitized) failed:\n" + res.stdout + res.stderr)
+    return SANITIZED_LIB_PATH
+
+
+def sanitizer_runtime():
+    """The ASan runtime to LD_PRELOAD into an uninstrumented python (None if absent)."""
+    import glob
+
+    hits = sorted(glob.glob("/opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so"))
+    return hits[-1] if hits else None
 
 
 _lib = None
@@ -259,7 +321,9 @@ class RangeError(ArithmeticError):
 
 
 class RerunError(RuntimeError):
-    """PWG_ERR_RERUN: the grid-synchronised forward found the GPU shared and wrote no output."""
+    """PWG_ERR_RERUN: a grid-synchronised or layer-pipelined forward did not complete (the GPU was
+    shared, or a bounded wait gave up); its output is invalid and the run must be redone on the
+    per-layer launches."""
 
 
 _ERRORS = {

@@ -235,7 +235,7 @@ class CnetEngine:
         ch = (ctypes.c_int * nb)(*program.channels)
         rt = (ctypes.c_int * nb)(*program.rate)
         _, n_ref = program.offsets()
-        idx = 0
+        idx = -1  # host-only handle: packing and checked plans, nothing on a GPU (include/pwg_cnet.h)
         if not host_only:
             idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
         h = ctypes.c_void_p()

@@ -316,9 +316,18 @@ struct PwgHandle {
   int fuse_first = 1;  // PWG_OPT_FUSE_FIRST_CONV
   long long pipe_max = PWG_PIPE_MAX_DEFAULT;  // PWG_OPT_PIPELINE: largest padded plan on the layer pipeline
   int sync_abort = 0;       // PWG_OPT_SYNC_ABORT (test hook)
+  int sync_timeout = 0;     // PWG_OPT_SYNC_TIMEOUT (test hook)
   long long sync_max = -1;  // PWG_OPT_SYNC: most 32-sample blocks on the grid-synchronised forward (-1: 64 x n_cu)
   long long half_max = -1;  // PWG_OPT_HALF_BLOCKS: most blocks of a half-block launch (-1: 4 x n_cu)
   int n_cu = 0;
+  // sticky run status (device, one int on its own 256-B allocation, zeroed once): every status bit a
+  // run sets is also ORed here, pwg_run_status reports and clears it (allocated by the first pwg_run)
+  int* d_status = nullptr;
+  // diagnostic per-wave timeline of the split16 layer launches (PWG_TRACE_FILE, read once at
+  // pwg_create; tools/trace_layer.py): this handle's device buffer, grown to the largest run
+  std::string trace_fn;
+  unsigned long long* d_trace = nullptr;
+  size_t trace_words = 0;
   // timing
   bool timing = false;
   std::vector<TimingRecord> records;
@@ -369,6 +378,7 @@ int pwg_create(const PwgConfig* cfg, int device, PwgHandle** out) {
     if (c.upsample_scales[i] < 1) return fail(PWG_ERR_INVALID, "upsample scales must be >= 1");
 
   PwgHandle* h = new PwgHandle();
+  if (const char* tf = getenv("PWG_TRACE_FILE")) h->trace_fn = tf;
   h->cfg = c;
   h->device = device;
   h->R = c.residual_channels;
@@ -462,6 +472,8 @@ void pwg_destroy(PwgHandle* h) {
     DeviceGuard g(h->device);
     for (auto& r : h->records) { (void)hipEventDestroy(r.start); (void)hipEventDestroy(r.stop); }
     for (auto e : h->event_pool) (void)hipEventDestroy(e);
+    if (h->d_status) (void)hipFree(h->d_status);
+    if (h->d_trace) (void)hipFree(h->d_trace);
   }
   delete h;
 }
@@ -912,6 +924,10 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
       return fail(PWG_ERR_HIP, "cannot query the CU count");
     h->n_cu = n;
   }
+  if (h->d_status == nullptr) {  // once per handle (pwg_graph_create runs eagerly before capturing)
+    if (hipMalloc((void**)&h->d_status, 256) != hipSuccess) return fail(PWG_ERR_HIP, "status word allocation");
+    if (hipMemset(h->d_status, 0, 256) != hipSuccess) return fail(PWG_ERR_HIP, "status word reset");
+  }
   hipStream_t s = (hipStream_t)stream;
   char* ws = (char*)workspace;
   float* x0 = (float*)(ws + p->ws_x0);
@@ -979,6 +995,7 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
   pa.split_scale_a = (float)SPLIT_GATE_SCALE_TANH;
   pa.split_scale_b = (float)SPLIT_GATE_SCALE_SIGM;
   pa.range_flag = split ? range_flag : nullptr;
+  pa.sticky = split ? h->d_status : nullptr;
   e = timed(PWG_KERNEL_UPSAMPLE, [&] { return launch_aux_proj(pa, h->L, s); });
   if (e != hipSuccess) return hip_fail(e, "aux projection launch");
 
@@ -1021,6 +1038,7 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
     sa.noise = fuse_first ? noise : nullptr;
     sa.fw = packed + h->off_first_w; sa.fb = packed + h->off_first_b;
     sa.range_flag = range_flag;
+    sa.sticky = h->d_status;
     pp.wg0 = reinterpret_cast<const unsigned*>(packed + h->off_layers + h->lo_split16);
     pp.wg_stride = (long long)h->layer_stride;
     pp.d0 = reinterpret_cast<const unsigned*>(dproj);
@@ -1041,7 +1059,8 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
   // B = 1 decode path)
   const long long n_blocks_all = p->n_tiles * (TILE / 32);
   const long long half_max_all = h->half_max >= 0 ? h->half_max : 4LL * h->n_cu;
-  const bool use_sync = split16 && h->split_ok && h->L >= 2 && h->L <= PIPE_MAX_LAYERS && h->KS == 3 &&
+  // (the grid deals its units to 8 XCD eighths: it needs at least 8 workgroups, one per CU)
+  const bool use_sync = split16 && h->split_ok && h->n_cu >= 8 && h->L >= 2 && h->L <= PIPE_MAX_LAYERS && h->KS == 3 &&
                         n_blocks_all <= (h->sync_max >= 0 ? h->sync_max : 64LL * h->n_cu) &&
                         (long long)h->RS * 4 * (p->Tpad + h->gap) < (1LL << 31);
   // the layers it covers: 0 .. L - 2 (from 1 on whole-block plans with the fused first_conv)
@@ -1069,6 +1088,7 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
     sa.noise = fuse_first ? noise : nullptr;
     sa.fw = packed + h->off_first_w; sa.fb = packed + h->off_first_b;
     sa.range_flag = range_flag;
+    sa.sticky = h->d_status;
     sy.wg0 = reinterpret_cast<const unsigned*>(packed + h->off_layers + h->lo_split16);
     sy.wg_stride = (long long)h->layer_stride;
     sy.d0 = reinterpret_cast<const unsigned*>(dproj);
@@ -1077,6 +1097,7 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
     sy.x[1] = reinterpret_cast<unsigned*>(x1);
     sy.half = n_blocks_all <= half_max_all;
     sy.force_abort = h->sync_abort;
+    sy.force_timeout = h->sync_timeout;
     sync_begin = (!sy.half && fuse_first) ? 1 : 0;
     sync_end = h->L - 1;
     sy.l0 = sync_begin;
@@ -1166,6 +1187,7 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
       sa.trace = nullptr;
       sa.noise = nullptr; sa.fw = sa.fb = nullptr;
       sa.range_flag = last ? range_flag : nullptr;
+      sa.sticky = last ? h->d_status : nullptr;
       if (fuse_first && l == 0) {
         sa.noise = noise; sa.fw = packed + h->off_first_w; sa.fb = packed + h->off_first_b;
       }
@@ -1176,25 +1198,34 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
       const int launch_w = split16 ? std::min(8, h->waves_per_wg) : wpw;
       if (split16 && units > 8LL * h->n_cu && units <= 32LL * h->n_cu) wpw = std::min(wpw, 4);
       sa.compute_waves = std::min(wpw, launch_w);
-      // diagnostic per-wave timeline (PWG_TRACE_FILE set; split16): every layer's records, dumped
-      // after the last layer of the run (tools/trace_layer.py)
-      static unsigned long long* d_trace_s = nullptr;
-      const char* trace_fn = split16 ? getenv("PWG_TRACE_FILE") : nullptr;
+      // diagnostic per-wave timeline (PWG_TRACE_FILE set at pwg_create; split16): every layer's
+      // records in the handle's buffer, dumped after the last layer of the run (tools/trace_layer.py)
+      const bool trace_on = split16 && !h->trace_fn.empty();
       const size_t per_layer_s = (size_t)nwg * launch_w * 8;
-      if (trace_fn) {
-        if (!d_trace_s && hipMalloc((void**)&d_trace_s, (size_t)nwg * 8 * 8 * 64 * sizeof(unsigned long long)) != hipSuccess)
-          return fail(PWG_ERR_HIP, "trace buffer");
-        sa.trace = d_trace_s + per_layer_s * (l % 64);
+      if (trace_on) {
+        const size_t need = per_layer_s * 64;
+        if (need > h->trace_words) {  // (re)allocate for this launch's grid: every layer slot fits
+          if (h->d_trace) {
+            (void)hipStreamSynchronize(s);
+            (void)hipFree(h->d_trace);
+            h->d_trace = nullptr;
+            h->trace_words = 0;
+          }
+          if (hipMalloc((void**)&h->d_trace, need * sizeof(unsigned long long)) != hipSuccess)
+            return fail(PWG_ERR_HIP, "trace buffer");
+          h->trace_words = need;
+        }
+        sa.trace = h->d_trace + per_layer_s * (l % 64);
       }
       e = timed(PWG_KERNEL_RESIDUAL_LAYER, [&] {
         return split16 ? launch_layer_split16(sa, last, la.tap_center, launch_w, nwg, s, half)
                        : launch_layer_split(sa, last, la.tap_center, wpw, nwg, s);
       });
-      if (e == hipSuccess && last && trace_fn) {
+      if (e == hipSuccess && last && trace_on) {
         std::vector<unsigned long long> host(per_layer_s * std::min(h->L, 64));
         e = hipStreamSynchronize(s);
-        if (e == hipSuccess) e = hipMemcpy(host.data(), d_trace_s, host.size() * 8, hipMemcpyDeviceToHost);
-        FILE* f = e == hipSuccess ? fopen(trace_fn, "wb") : nullptr;
+        if (e == hipSuccess) e = hipMemcpy(host.data(), h->d_trace, host.size() * 8, hipMemcpyDeviceToHost);
+        FILE* f = e == hipSuccess ? fopen(h->trace_fn.c_str(), "wb") : nullptr;
         if (f) {
           const long long hdr[4] = {std::min(h->L, 64), nwg, launch_w, 8};
           fwrite(hdr, sizeof(hdr), 1, f);
@@ -1220,40 +1251,7 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
       pa2.out_stride_t = (int)la.out_stride_t; pa2.out_stride_o = (int)la.out_stride_o;
       pa2.skip_scale = la.skip_scale;
       const int nwg = h->n_cu * h->wg_per_cu;
-      pa2.trace = nullptr;
       pa2.ctr = sched_ctr + (size_t)l * SCHED_CTR_STRIDE * 8;
-#if PWG_TRACE
-      // diagnostic build: every layer's per-wave records, dumped after the run (PWG_TRACE_FILE)
-      static unsigned long long* d_trace = nullptr;
-      const size_t per_layer = (size_t)nwg * 8 * 8;
-      if (!d_trace && hipMalloc((void**)&d_trace, per_layer * 64 * sizeof(unsigned long long)) != hipSuccess)
-        return fail(PWG_ERR_HIP, "trace buffer");
-      pa2.trace = d_trace + per_layer * (l % 64);
-      if (last) {
-        auto kick = [=, &e]() {
-          std::vector<unsigned long long> host(per_layer * h->L);
-          e = hipStreamSynchronize(s);
-          if (e == hipSuccess) e = hipMemcpy(host.data(), d_trace, host.size() * 8, hipMemcpyDeviceToHost);
-          const char* fn = getenv("PWG_TRACE_FILE");
-          if (e == hipSuccess && fn) {
-            FILE* f = fopen(fn, "wb");
-            if (f) {
-              const long long hdr[4] = {h->L, nwg, wpw, 8};
-              fwrite(hdr, sizeof(hdr), 1, f);
-              fwrite(host.data(), 8, host.size(), f);
-              fclose(f);
-            }
-          }
-        };
-        e = timed(PWG_KERNEL_RESIDUAL_LAYER, [&] {
-          return launch_layer_persistent(pa2, h->MT, h->M2T, last, wpw, nwg, s);
-        });
-        if (e == hipSuccess) kick();
-        if (e != hipSuccess) return hip_fail(e, "residual layer launch (trace)");
-        std::swap(xin, xout);
-        continue;
-      }
-#endif
       e = timed(PWG_KERNEL_RESIDUAL_LAYER, [&] {
         return launch_layer_persistent(pa2, h->MT, h->M2T, last, wpw, nwg, s);
       });
@@ -1271,19 +1269,30 @@ int pwg_run_status(PwgPlan* p, const void* workspace, void* stream) {
   if (!p || !workspace) return fail(PWG_ERR_INVALID, "null argument");
   DeviceGuard g(p->h->device);
   if (!g.ok) return fail(PWG_ERR_HIP, "hipSetDevice failed");
-  int flag = 0;
+  int flag[2] = {0, 0};
   hipStream_t s = (hipStream_t)stream;
-  hipError_t e = hipMemcpyAsync(&flag, (const char*)workspace + p->ws_flag, sizeof(int), hipMemcpyDeviceToHost, s);
+  hipError_t e = hipMemcpyAsync(&flag[0], (const char*)workspace + p->ws_flag, sizeof(int), hipMemcpyDeviceToHost, s);
+  // the handle's sticky word: every flag any run of this handle set since the previous status call
+  // (a serving loop that checks once per batch of runs still sees an earlier run's abort); cleared
+  // here, in stream order
+  if (e == hipSuccess && p->h->d_status != nullptr) {
+    e = hipMemcpyAsync(&flag[1], p->h->d_status, sizeof(int), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemsetAsync(p->h->d_status, 0, sizeof(int), s);
+  }
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return hip_fail(e, "run status");
-  if (flag & 4)
+  const int st = flag[0] | flag[1];
+  if (st & PWG_STATUS_SYNC_ABORT)
     return fail(PWG_ERR_RERUN, "grid-synchronised forward: not every workgroup could start (the GPU is shared "
-                               "with other work), so it did nothing; rerun with PWG_OPT_SYNC 0");
-  if (flag & 2)
-    return fail(PWG_ERR_HIP, "layer-pipelined or grid-synchronised forward: a dependency or barrier wait timed "
-                              "out (the output is invalid); rerun with PWG_OPT_PIPELINE 0 and PWG_OPT_SYNC 0 "
-                              "and report this");
-  if (flag != 0)
+                               "with other work), so it computed nothing and the output is NaN; rerun with "
+                               "PWG_OPT_SYNC 0");
+  if (st & PWG_STATUS_SYNC_TIMEOUT)
+    return fail(PWG_ERR_RERUN, "grid-synchronised forward: a grid-barrier wait gave up (a workgroup was "
+                               "descheduled?), so the output is NaN; rerun with PWG_OPT_SYNC 0");
+  if (st & PWG_STATUS_PIPE_TIMEOUT)
+    return fail(PWG_ERR_RERUN, "layer-pipelined forward: a dependency wait gave up, so the output is invalid; "
+                               "rerun with PWG_OPT_PIPELINE 0");
+  if (st != 0)
     return fail(PWG_ERR_RANGE,
                 "split-f16 range flag: a value left the fp16 pair range (an aux projection row, the "
                 "scaled final skip sum, or upstream x / first_conv values making a skip sum non-finite; or the "
@@ -1396,6 +1405,10 @@ int pwg_set_option(PwgHandle* h, int option, long long value) {
       if (value != 0 && value != 1) return fail(PWG_ERR_INVALID, "sync_abort must be 0 or 1");
       h->sync_abort = (int)value;
       return PWG_OK;
+    case PWG_OPT_SYNC_TIMEOUT:
+      if (value != 0 && value != 1) return fail(PWG_ERR_INVALID, "sync_timeout must be 0 or 1");
+      h->sync_timeout = (int)value;
+      return PWG_OK;
 
     default:
       return fail(PWG_ERR_INVALID, "unknown option");
@@ -1413,6 +1426,7 @@ int pwg_get_option(const PwgHandle* h, int option, long long* value) {
     case PWG_OPT_HALF_BLOCKS: *value = h->half_max >= 0 ? h->half_max : 4LL * h->n_cu; return PWG_OK;
     case PWG_OPT_SYNC: *value = h->sync_max >= 0 ? h->sync_max : 64LL * h->n_cu; return PWG_OK;
     case PWG_OPT_SYNC_ABORT: *value = h->sync_abort; return PWG_OK;
+    case PWG_OPT_SYNC_TIMEOUT: *value = h->sync_timeout; return PWG_OK;
 
     default: return fail(PWG_ERR_INVALID, "unknown option");
   }

@@ -2351,7 +2351,7 @@ __global__ void __launch_bounds__(128) pwg_cnet_thin_kernel(const CnConvArgs a, 
   for (int o = a.M; o < a.ld_dst; ++o) yrow[o] = 0.f;  // padding channels stay zero
   // program output in split-f16 mode: a value beyond the fp16 pair range anywhere upstream became
   // (inf, -inf), every later product NaN, and nothing on the way (LeakyReLU, tanh, sums) clears it
-  if (a.range_flag) flag_range(a.range_flag, bad, (int)(threadIdx.x & 63));
+  if (a.range_flag) flag_range(a.range_flag, nullptr, bad, (int)(threadIdx.x & 63));
 }
 
 // PQMF synthesis (layers/pqmf.py:133-149): y[t] = sum_m sum_k h[m][k] * S * x[(t+k-P)/S][m] over
@@ -2401,7 +2401,7 @@ __global__ void __launch_bounds__(256) pwg_cnet_pqmf_kernel(const CnPqmfArgs a) 
     for (int m = 0; m < S; ++m) acc = fmaf(s_h[m * NT + k], s_x[rr * S + m], acc);
   }
   a.y[(size_t)(sd.x + t) * a.ld_dst] = acc;
-  if (a.range_flag) flag_range(a.range_flag, !__builtin_isfinite(acc), (int)(threadIdx.x & 63));
+  if (a.range_flag) flag_range(a.range_flag, nullptr, !__builtin_isfinite(acc), (int)(threadIdx.x & 63));
 }
 
 // Non-finite check of the program output when its last op is not a thin or PQMF launch (split-f16
@@ -2410,7 +2410,7 @@ __global__ void __launch_bounds__(256) pwg_cnet_finite_kernel(const float* y, lo
   bool bad = false;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
     bad |= !__builtin_isfinite(y[i]);
-  flag_range(flag, bad, (int)(threadIdx.x & 63));
+  flag_range(flag, nullptr, bad, (int)(threadIdx.x & 63));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2496,6 +2496,7 @@ struct PwgCnetPlan {
   std::vector<int2*> d_xblocks;              // per phase: x-tile pair blocks (utt, q0 step XP_OUT), or null
   std::vector<int> n_xblocks;
   int pair_steps = 16;
+  bool host_only = false;                    // a handle created for device -1: built and checked, not uploaded
 };
 
 namespace {
@@ -3099,6 +3100,72 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
   }
   p->ws_flag = o;  // after the buffer slots (256-byte aligned)
   p->ws_bytes = o + 256;
+  // host side of every per-phase list first (block lists, columns per utterance, fused-pair strips,
+  // x-tile blocks), each checked before anything reaches the GPU: a bad list (a step or count that
+  // was never set, a block outside its utterance) fails here with PWG_ERR_ASSERT instead of turning
+  // into an illegal address in a kernel (round 3's fault: an uninitialised OpPhase field)
+  const size_t nph = n->phases.size();
+  std::vector<std::vector<int2>> h_blocks(nph), h_strips(nph), h_xblocks(nph);
+  std::vector<std::vector<int>> h_ncols(nph);
+  auto bad_list = [&](size_t pi, const char* what) {
+    delete p;
+    return fail(PWG_ERR_ASSERT, "internal: plan phase " + std::to_string(pi) + ": " + what);
+  };
+  for (size_t pi = 0; pi < nph; ++pi) {
+    const OpPhase& ph = n->phases[pi];
+    const PwgCnetOp& op = n->ops[ph.op];
+    std::vector<int2>& blocks = h_blocks[pi];
+    std::vector<int>& ncols = h_ncols[pi];
+    ncols.assign(n_utts, 0);
+    if (op.kind == PWG_CNET_PQMF) {
+      for (int u = 0; u < n_utts; ++u) {
+        const long long T = frames[u] * n->rate[op.dst];
+        for (long long t0 = 0; t0 < T; t0 += 256) blocks.push_back(make_int2(u, (int)t0));
+      }
+    } else {
+      if (ph.ostride < 1 || ph.ophase < 0 || ph.ophase >= ph.ostride) return bad_list(pi, "output stride / phase");
+      const int cols = ph.thin ? CN_COLS : 32 * ph.NW;
+      if (ph.NW != 4 && ph.NW != 8) return bad_list(pi, "waves per workgroup");
+      for (int u = 0; u < n_utts; ++u) {
+        const long long T = frames[u] * n->rate[op.dst];
+        const int nq = (int)((T - ph.ophase + ph.ostride - 1) / ph.ostride);
+        ncols[u] = nq;
+        for (int q0 = 0; q0 < nq; q0 += cols) blocks.push_back(make_int2(u, q0));
+      }
+    }
+    if (ph.pair_b >= 0) {
+      if (p->pair_steps < 1) return bad_list(pi, "pair strip steps");
+      for (int u = 0; u < n_utts; ++u)
+        for (int q0 = 0; q0 < ncols[u]; q0 += 128 * p->pair_steps) h_strips[pi].push_back(make_int2(u, q0));
+    }
+    if (ph.xpair_b >= 0 || (ph.stack_b >= 0 && ph.xtile) || ph.xt_convt_db) {
+      const int step = ph.xpair_b >= 0 ? XP_OUT : XT_COLS;
+      for (int u = 0; u < n_utts; ++u)
+        for (int q0 = 0; q0 < ncols[u]; q0 += step) h_xblocks[pi].push_back(make_int2(u, q0));
+    }
+    // every list: utterance in range, first column inside it
+    for (const std::vector<int2>* lst : {&blocks, &h_strips[pi], &h_xblocks[pi]})
+      for (const int2& b : *lst) {
+        if (b.x < 0 || b.x >= n_utts || b.y < 0) return bad_list(pi, "block outside the batch");
+        const long long lim = op.kind == PWG_CNET_PQMF ? frames[b.x] * n->rate[op.dst] : ncols[b.x];
+        if (b.y >= lim) return bad_list(pi, "block past its utterance");
+      }
+    if (blocks.size() > (size_t)INT32_MAX / 2) return bad_list(pi, "block count");
+  }
+  if (n->device < 0) {  // host-only handle: sizes and lists checked, nothing uploaded (cannot run)
+    p->host_only = true;
+    for (size_t pi = 0; pi < nph; ++pi) {
+      p->d_blocks.push_back(nullptr);
+      p->n_blocks.push_back((int)h_blocks[pi].size());
+      p->d_ncols.push_back(nullptr);
+      p->d_strips.push_back(nullptr);
+      p->n_strips.push_back((int)h_strips[pi].size());
+      p->d_xblocks.push_back(nullptr);
+      p->n_xblocks.push_back((int)h_xblocks[pi].size());
+    }
+    *out = p;
+    return PWG_OK;
+  }
   Guard g(n->device);
   if (!g.ok) { delete p; return fail(PWG_ERR_HIP, "hipSetDevice failed"); }
   hipError_t e = hipSuccess;
@@ -3116,59 +3183,31 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
   }
   e = hipMalloc(&p->d_seg, sizeof(int) * seg.size());
   if (e == hipSuccess) e = hipMemcpy(p->d_seg, seg.data(), sizeof(int) * seg.size(), hipMemcpyHostToDevice);
-  for (const OpPhase& ph : n->phases) {
-    const PwgCnetOp& op = n->ops[ph.op];
-    std::vector<int2> blocks;
-    std::vector<int> ncols(n_utts);
-    if (op.kind == PWG_CNET_PQMF) {
-      for (int u = 0; u < n_utts; ++u) {
-        const long long T = frames[u] * n->rate[op.dst];
-        for (long long t0 = 0; t0 < T; t0 += 256) blocks.push_back(make_int2(u, (int)t0));
-      }
-    } else {
-      for (int u = 0; u < n_utts; ++u) {
-        const long long T = frames[u] * n->rate[op.dst];
-        const int nq = (int)((T - ph.ophase + ph.ostride - 1) / ph.ostride);
-        ncols[u] = nq;
-        const int cols = ph.thin ? CN_COLS : 32 * ph.NW;
-        for (int q0 = 0; q0 < nq; q0 += cols) blocks.push_back(make_int2(u, q0));
-      }
-    }
+  auto upload = [&](const std::vector<int2>& v, int2** d) {
+    *d = nullptr;
+    if (e != hipSuccess || v.empty()) return;
+    e = hipMalloc(d, sizeof(int2) * v.size());
+    if (e == hipSuccess) e = hipMemcpy(*d, v.data(), sizeof(int2) * v.size(), hipMemcpyHostToDevice);
+  };
+  for (size_t pi = 0; pi < nph; ++pi) {
     int2* db = nullptr;
     int* dn = nullptr;
-    if (e == hipSuccess && !blocks.empty()) {
-      e = hipMalloc(&db, sizeof(int2) * blocks.size());
-      if (e == hipSuccess) e = hipMemcpy(db, blocks.data(), sizeof(int2) * blocks.size(), hipMemcpyHostToDevice);
-      if (e == hipSuccess) e = hipMalloc(&dn, sizeof(int) * n_utts);
-      if (e == hipSuccess) e = hipMemcpy(dn, ncols.data(), sizeof(int) * n_utts, hipMemcpyHostToDevice);
+    upload(h_blocks[pi], &db);
+    if (e == hipSuccess && !h_blocks[pi].empty()) {
+      e = hipMalloc(&dn, sizeof(int) * n_utts);
+      if (e == hipSuccess) e = hipMemcpy(dn, h_ncols[pi].data(), sizeof(int) * n_utts, hipMemcpyHostToDevice);
     }
     p->d_blocks.push_back(db);
-    p->n_blocks.push_back((int)blocks.size());
+    p->n_blocks.push_back((int)h_blocks[pi].size());
     p->d_ncols.push_back(dn);
-    std::vector<int2> strips;
-    if (ph.pair_b >= 0)
-      for (int u = 0; u < n_utts; ++u)
-        for (int q0 = 0; q0 < ncols[u]; q0 += 128 * p->pair_steps) strips.push_back(make_int2(u, q0));
     int2* dstr = nullptr;
-    if (e == hipSuccess && !strips.empty()) {
-      e = hipMalloc(&dstr, sizeof(int2) * strips.size());
-      if (e == hipSuccess) e = hipMemcpy(dstr, strips.data(), sizeof(int2) * strips.size(), hipMemcpyHostToDevice);
-    }
+    upload(h_strips[pi], &dstr);
     p->d_strips.push_back(dstr);
-    p->n_strips.push_back((int)strips.size());
-    std::vector<int2> xblocks;
-    if (ph.xpair_b >= 0 || (ph.stack_b >= 0 && ph.xtile) || ph.xt_convt_db) {
-      const int step = ph.xpair_b >= 0 ? XP_OUT : XT_COLS;
-      for (int u = 0; u < n_utts; ++u)
-        for (int q0 = 0; q0 < ncols[u]; q0 += step) xblocks.push_back(make_int2(u, q0));
-    }
+    p->n_strips.push_back((int)h_strips[pi].size());
     int2* dxb = nullptr;
-    if (e == hipSuccess && !xblocks.empty()) {
-      e = hipMalloc(&dxb, sizeof(int2) * xblocks.size());
-      if (e == hipSuccess) e = hipMemcpy(dxb, xblocks.data(), sizeof(int2) * xblocks.size(), hipMemcpyHostToDevice);
-    }
+    upload(h_xblocks[pi], &dxb);
     p->d_xblocks.push_back(dxb);
-    p->n_xblocks.push_back((int)xblocks.size());
+    p->n_xblocks.push_back((int)h_xblocks[pi].size());
   }
   if (e != hipSuccess) {
     const int rc = hipf(e, "cnet plan upload");
@@ -3181,6 +3220,10 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
 
 void pwg_cnet_plan_destroy(PwgCnetPlan* p) {
   if (!p) return;
+  if (p->host_only) {
+    delete p;
+    return;
+  }
   Guard g(p->n->device);
   if (p->d_seg) (void)hipFree(p->d_seg);
   for (auto* x : p->d_blocks) if (x) (void)hipFree(x);
@@ -3200,6 +3243,7 @@ long long pwg_cnet_plan_workspace_bytes(const PwgCnetPlan* p) { return p ? (long
 int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const float* mean, const float* scale,
                  float* out, void* workspace, void* stream) {
   if (!p || !packed || !mel || !out || !workspace) return fail(PWG_ERR_INVALID, "null argument");
+  if (p->host_only) return fail(PWG_ERR_INVALID, "a plan of a host-only handle (device -1) cannot run");
   PwgCnet* n = p->n;
   const int nb = (int)n->channels.size();
   Guard g(n->device);

@@ -73,6 +73,7 @@ struct AuxProjArgs {
   float split_scale_a, split_scale_b;
   int* range_flag;       // split modes: set to 1 when a scaled D value leaves the fp16 pair range
                          // (|v| >= 65520 or not finite; pwg_run_status)
+  int* sticky;           // the handle's sticky status word (every flag bit is also ORed there)
 };
 // Pre-scaling of the split kernel's gate rows (pwg_split.hip gate()): tanh rows by -2 log2(e),
 // sigmoid rows by -log2(e).
@@ -166,7 +167,6 @@ struct PersistArgs {
   int out_stride_t, out_stride_o;
   float skip_scale;
   int* ctr;                   // this layer's 8 per-XCD work-queue heads, SCHED_CTR_STRIDE ints apart (zeroed per run)
-  unsigned long long* trace;  // PWG_TRACE builds only: per-wave timestamps (tools/trace_layer.py)
 };
 
 // Split-f16 layer kernel (pwg_split.hip), PWG v1 shape: R = S = 64, 128 gate rows, kernel 3.
@@ -193,8 +193,13 @@ struct SplitArgs {
   const float* noise;         // split16 layer 0 with first_conv fused (else null): caller noise
   const float* fw;            // first_conv weight [64] and bias [64]
   const float* fb;
-  int* range_flag;            // last layer: set to 1 when a live column's final skip sum is not
-                              // finite (fp16 pair range exceeded somewhere upstream; pwg_run_status)
+  int* range_flag;            // the run's status word (pwg_run_status): the last layer sets
+                              // PWG_STATUS_RANGE when a live column's final skip sum is not finite
+                              // (fp16 pair range exceeded somewhere upstream); the pipelined and
+                              // synchronised forwards set their wait / abort bits; the last layer
+                              // writes NaN audio when a PWG_STATUS_REDO bit is set on entry
+  int* sticky;                // the handle's sticky status word: every bit set in range_flag is
+                              // also ORed here, so a status check once per batch of runs sees it
   int compute_waves;          // split16: waves per workgroup that take blocks (the rest only stage)
 };
 // dwords of one layer's split image (SplitSmem in pwg_split.hip without the head)
@@ -232,6 +237,7 @@ struct SyncArgs {
   int l0, L;                 // the launch runs layers l0 .. l0 + L - 1
   int half;                  // half-block work units
   int force_abort;           // test hook (PWG_OPT_SYNC_ABORT): take the "GPU shared" exit
+  int force_timeout;         // test hook (PWG_OPT_SYNC_TIMEOUT): every grid-barrier wait gives up
   int waves_mid;             // computing waves per workgroup
   int dil[PIPE_MAX_LAYERS];
 };
@@ -296,12 +302,24 @@ __device__ __forceinline__ void stage_lds(V* dst, const V* src, int n, int tid, 
   for (; i < n; i += nthr) dst[i] = src[i];
 }
 
+// Run status bits (the per-run word pwg_run_status reads, and the handle's sticky copy).
+constexpr int PWG_STATUS_RANGE = 1;         // a value left the fp16 pair range: rerun in exact fp32
+constexpr int PWG_STATUS_PIPE_TIMEOUT = 2;  // layer pipeline: a dependency wait gave up
+constexpr int PWG_STATUS_SYNC_ABORT = 4;    // grid-synchronised forward: not every workgroup started
+constexpr int PWG_STATUS_SYNC_TIMEOUT = 8;  // grid-synchronised forward: a grid-barrier wait gave up
+constexpr int PWG_STATUS_REDO = PWG_STATUS_PIPE_TIMEOUT | PWG_STATUS_SYNC_ABORT | PWG_STATUS_SYNC_TIMEOUT;
+
+// OR status bits into the run's word and the handle's sticky word (either may be null).
+__device__ __forceinline__ void flag_status(int* flag, int* sticky, int bits) {
+  if (flag != nullptr) __hip_atomic_fetch_or(flag, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (sticky != nullptr) __hip_atomic_fetch_or(sticky, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Split-f16 range flag: one vector atomic per wave (from its lowest flagging lane) when any active
 // lane saw a value the fp16 pair split cannot carry. Lanes that already exited simply do not vote.
-__device__ __forceinline__ void flag_range(int* flag, bool bad, int lane) {
+__device__ __forceinline__ void flag_range(int* flag, int* sticky, bool bad, int lane) {
   const unsigned long long m = __ballot(bad ? 1 : 0);
-  if (bad && flag != nullptr && lane == __builtin_ctzll(m))
-    __hip_atomic_fetch_or(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (bad && lane == __builtin_ctzll(m)) flag_status(flag, sticky, PWG_STATUS_RANGE);
 }
 
 }  // namespace pwg

@@ -247,7 +247,7 @@ __global__ void __launch_bounds__(256) pwg_aux_proj_kernel(const AuxProjArgs a) 
           s_d[wave][cl][(r & 15) * 8 + (r >> 4)] = __builtin_bit_cast(unsigned, f16x2{hi, (_Float16)(x - (float)hi)});
         }
       }
-    flag_range(a.range_flag, bad && f < a.F_total, lane);
+    flag_range(a.range_flag, a.sticky, bad && f < a.F_total, lane);
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes done (wave-private rows)
     __builtin_amdgcn_wave_barrier();
     const long long f0 = (long long)blockIdx.x * 128 + wave * 32;
@@ -285,7 +285,7 @@ __global__ void __launch_bounds__(256) pwg_aux_proj_kernel(const AuxProjArgs a) 
           u[i] = __builtin_bit_cast(unsigned, f16x2{hi, (_Float16)(x - (float)hi)});
         }
         if (bad && a.range_flag)  // rare; lanes of exited waves never reach here (f < F_total)
-          __hip_atomic_fetch_or(a.range_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          flag_status(a.range_flag, a.sticky, PWG_STATUS_RANGE);
         *reinterpret_cast<u32x4*>(d + 32 * m + 8 * j4 + 4 * hh) = u;
       } else {
         *reinterpret_cast<f32x4*>(d + 32 * m + 8 * j4 + 4 * hh) = v;
@@ -678,30 +678,18 @@ __device__ __forceinline__ float fast_gate(float a, float b) {
   return (1.f - e1) * __builtin_amdgcn_rcpf((1.f + e1) * (1.f + e2));
 }
 
-// Stores of the streamed outputs (x_out, skip). PWG_STORE_SC1=1 selects write-through sc1 stores
-// (cache policy 16), which drop the line from the XCD's L2; measured 11 % SLOWER than plain stores
-// on the LibriTTS bench (4.55 vs 4.10 ms per layer), so plain stores are the default.
-#ifndef PWG_STORE_SC1
-#define PWG_STORE_SC1 0
-#endif
+// Stores of the streamed outputs (x_out, skip): plain stores. Write-through sc1 stores (which drop
+// the line from the XCD's L2) measured 11 % slower on the LibriTTS bench (4.55 vs 4.10 ms per
+// layer). That variant and the other rejected A/B builds of this kernel (B-ring unrolling, A
+// prefetch, s_setprio, late aux / early skip loads, sequential GEMM-2 passes, the PWG_TRACE build)
+// are in git history before round 4.
 __device__ __forceinline__ void store_stream(float* wave_base, int byte_off, f32x4 v) {
-#if PWG_STORE_SC1
-  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(wave_base, 0, 0x7fffffff, 0x00020000);
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
-                                         rsrc, byte_off, 0, 16);
-#else
   *reinterpret_cast<f32x4*>(reinterpret_cast<char*>(wave_base) + byte_off) = v;
-#endif
 }
 
-#ifndef PWG_PERSIST_THREADS
-#define PWG_PERSIST_THREADS 512
-#endif
+constexpr int PWG_PERSIST_THREADS = 512;
 // RC / SC: compile-time residual / skip channels for the production shapes (0 = runtime).
 // 8 waves per CU (2 per SIMD): measured faster than 12 with the XCD-local schedule (L2 footprint).
-#ifndef PWG_BPF
-#define PWG_BPF 2  // B groups in flight ahead of the MFMAs (compile-time-K instances)
-#endif
 template <int MT, int M2T, int M3T, int GK, int RC, int SC, int KSC>
 __global__ void __launch_bounds__(PWG_PERSIST_THREADS, 1) pwg_layer_persistent_kernel(const PersistArgs a) {
   using SM = PersistSmem<MT, M2T, M3T>;
@@ -724,18 +712,6 @@ __global__ void __launch_bounds__(PWG_PERSIST_THREADS, 1) pwg_layer_persistent_k
   const int KS = KSC ? KSC : a.KS;
   const int K1 = KS * RS;
   const int NGRP = K1 / (2 * GK);
-  // compile-time K (KSC, RC): GEMM 1 fully unrolled with a PF-deep B register ring
-#ifndef PWG_NO_UNROLL
-#define PWG_NO_UNROLL 1  // the unrolled PF-deep ring measured equal (3.87-3.88 ms) at +30-50 VGPRs
-#endif
-#if PWG_NO_UNROLL
-  constexpr int NGRP_C = 0;
-#else
-  constexpr int NGRP_C = (KSC && RC) ? KSC * ((RC + KC - 1) / KC * KC) / (2 * GK) : 0;
-#endif
-  constexpr int PF = PWG_BPF;
-  constexpr int RING = PF + 1;
-  static_assert(NGRP_C == 0 || NGRP_C % RING == 0, "ring size must divide the group count");
   float* s_wg = smem;
   float* s_w2 = s_wg + K1 / 8 * MT * 256;
   float* s_bg = s_w2 + SM::W2;
@@ -803,33 +779,6 @@ __global__ void __launch_bounds__(PWG_PERSIST_THREADS, 1) pwg_layer_persistent_k
     return *reinterpret_cast<const bvec*>(a.x_in + (size_t)(c + cl + off) * RS + c0 + GK * hh);
   };
   // 4*GK-byte group of k-steps: 16 MFMAs per 4-k-step slice, A from LDS
-#if PWG_APREFETCH
-  // A fragments one 4-k-step slice ahead: av holds the slice about to run; the read of the next
-  // one (wrapping to slice 0, the next block's first: the weights are the same) is in flight
-  // during its 16 MFMAs.
-  const int n_slices = NGRP * NB;
-  f32x4 av[MT];
-#pragma unroll
-  for (int m = 0; m < MT; ++m) av[m] = wgl[m * 64];
-  auto group_mfma = [&](f32x16 (&acc)[MT], const bvec& b, int g) {
-#pragma unroll
-    for (int sub = 0; sub < NB; ++sub) {
-      int nxt = g * NB + sub + 1;
-      nxt = nxt == n_slices ? 0 : nxt;
-      f32x4 an[MT];
-#pragma unroll
-      for (int m = 0; m < MT; ++m) an[m] = wgl[(nxt * MT + m) * 64];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int m = 0; m < MT; ++m)
-          acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m][i], b[4 * sub + i], acc[m], 0, 0, 0);
-#pragma unroll
-      for (int m = 0; m < MT; ++m) av[m] = an[m];
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-#else
   auto group_mfma = [&](f32x16 (&acc)[MT], const bvec& b, int g) {
 #pragma unroll
     for (int sub = 0; sub < NB; ++sub) {
@@ -844,42 +793,14 @@ __global__ void __launch_bounds__(PWG_PERSIST_THREADS, 1) pwg_layer_persistent_k
       __builtin_amdgcn_sched_barrier(0);
     }
   };
-#endif
 
   int blk = x_first + (blockIdx.x >> 3) * nw + wave;  // static round 0
   int nblk = blk + x_waves;                           // static round 1
   if (blk >= x_end) blk = -1;
   if (nblk >= x_end) nblk = -1;
-#if PWG_SETPRIO
-  if (wave >= nw / 2) __builtin_amdgcn_s_setprio(1);  // younger half wins arbitration
-#endif
-#if PWG_TRACE
-  // diagnostic build: [start_rt, end_rt, blocks, gemm1_cyc, gate_cyc, gemm2_cyc, start_clk, end_clk]
-  unsigned long long* trw = a.trace + ((size_t)blockIdx.x * nw + wave) * 8;
-  const unsigned long long tr_rt0 = wall_clock64(), tr_c0 = clock64();
-  unsigned long long tr_g1 = 0, tr_gt = 0, tr_g2 = 0, tr_n = 0;
-  auto tr_done = [&] {
-    if (lane == 0) {
-      trw[0] = tr_rt0; trw[1] = wall_clock64(); trw[2] = tr_n; trw[3] = tr_g1; trw[4] = tr_gt;
-      trw[5] = tr_g2; trw[6] = tr_c0; trw[7] = clock64();
-    }
-  };
-#define PWG_TR(x) x
-#else
-#define PWG_TR(x)
-#endif
-  if (blk < 0) {
-    PWG_TR(tr_done());
-    return;
-  }
+  if (blk < 0) return;
   BlockDesc bdn = a.blocks[blk];  // descriptor of the block processed next (loaded a block ahead)
   bvec b0 = bload(bdn.col, 0);     // B operand of the next group (prefetched, across blocks)
-  bvec bq[RING];                   // compile-time-K path: groups g .. g+PF-1 in flight
-  if constexpr (NGRP_C > 0) {
-    bq[0] = b0;
-#pragma unroll
-    for (int i = 1; i < PF; ++i) bq[i] = bload(bdn.col, i);
-  }
 
   while (true) {
     const BlockDesc bd = bdn;
@@ -922,9 +843,7 @@ __global__ void __launch_bounds__(PWG_PERSIST_THREADS, 1) pwg_layer_persistent_k
         bw[s] = ok ? w : 0.f;
       }
     }
-#if !PWG_LATE_AUX
     load_dv();  // in flight during GEMM 1
-#endif
 
     // ---- GEMM 2 accumulators seeded with [skip_old; x_in]: the MFMA performs the skip sum and
     //      the residual add (residual_block.py:138, parallel_wavegan.py:164); pass-0 loads in flight
@@ -948,12 +867,8 @@ __global__ void __launch_bounds__(PWG_PERSIST_THREADS, 1) pwg_layer_persistent_k
           for (int i = 0; i < 4; ++i) acc2[mm][4 * j4 + i] = v[i];
         }
     };
-    PWG_TR(const unsigned long long tr_a = clock64());
     int ticket = 0;  // claim for the block after next, issued once GEMM 1's loads are out
     f32x16 accp0[MP], accp1[MP];
-#if PWG_EARLY_SKIP
-    init_pass(0, accp0);  // skip_old rows stream from HBM: issue them before GEMM 1
-#endif
     // ---- GEMM 1. acc starts from the gate bias (k-step against a ones row, zero C), B operands
     //      ping-pong between two register groups, the last group prefetching the next block's first
     f32x16 acc[MT];
@@ -967,33 +882,18 @@ __global__ void __launch_bounds__(PWG_PERSIST_THREADS, 1) pwg_layer_persistent_k
       for (int m = 0; m < MT; ++m)
         acc[m] = __builtin_amdgcn_mfma_f32_32x32x2f32(hh == 0 ? bgv[m] : 0.f, one, zero, 0, 0, 0);
     }
-    if constexpr (NGRP_C > 0) {
-#pragma unroll
-      for (int g = 0; g < NGRP_C; ++g) {
-        const int gn = g + PF;  // issue group g+PF (the next block's first groups at the end)
-        bq[gn % RING] = gn < NGRP_C ? bload(bd.col, gn) : bload(col_next, gn - NGRP_C);
-        group_mfma(acc, bq[g % RING], g);
+    for (int g = 0; g < NGRP; g += 2) {
+      const bvec b1 = bload(bd.col, g + 1 < NGRP ? g + 1 : g);
+      group_mfma(acc, b0, g);
+      if (g + 1 >= NGRP) {  // odd group count: b0 takes the next block's first group
+        b0 = bload(col_next, 0);
+        break;
       }
-    } else {
-      for (int g = 0; g < NGRP; g += 2) {
-        const bvec b1 = bload(bd.col, g + 1 < NGRP ? g + 1 : g);
-        group_mfma(acc, b0, g);
-        if (g + 1 >= NGRP) {  // odd group count: b0 takes the next block's first group
-          b0 = bload(col_next, 0);
-          break;
-        }
-        b0 = g + 2 < NGRP ? bload(bd.col, g + 2) : bload(col_next, 0);
-        group_mfma(acc, b1, g + 1);
-      }
+      b0 = g + 2 < NGRP ? bload(bd.col, g + 2) : bload(col_next, 0);
+      group_mfma(acc, b1, g + 1);
     }
 
-    PWG_TR(const unsigned long long tr_b = clock64());
-#if PWG_LATE_AUX
-    load_dv();  // 16 VGPRs fewer across GEMM 1 (3 waves/SIMD fit); latency covered by the others
-#endif
-#if !PWG_EARLY_SKIP
     init_pass(0, accp0);
-#endif
     if (nblk >= 0) ticket = ticket_issue();
 
     // ---- aux term: + sum_f D[f][row] * w_t[f - t/H + J1]
@@ -1013,10 +913,7 @@ __global__ void __launch_bounds__(PWG_PERSIST_THREADS, 1) pwg_layer_persistent_k
         if (MT == 1 && r >= 8) { gt[gm][r] = 0.f; continue; }
         gt[gm][r] = fast_gate(acc[gm][r], MT == 1 ? acc[0][r + 8] : acc[gm + MT / 2][r]);
       }
-#if !PWG_SEQ_PASS
     if (NPASS > 1) init_pass(1, accp1);
-#endif
-    PWG_TR(const unsigned long long tr_c = clock64());
 
     auto gemm2_pass = [&](int pass, f32x16 (&acc2)[MP]) {
 #pragma unroll
@@ -1055,9 +952,6 @@ __global__ void __launch_bounds__(PWG_PERSIST_THREADS, 1) pwg_layer_persistent_k
         }
     };
 
-#if PWG_SEQ_PASS
-    if (!LAST && NPASS > 1) init_pass(1, accp1);  // x_in rows: L2 hits, in flight during pass 0
-#endif
     gemm2_pass(0, accp0);
     if (!LAST) {
       store_pass(0, accp0);
@@ -1119,14 +1013,10 @@ __global__ void __launch_bounds__(PWG_PERSIST_THREADS, 1) pwg_layer_persistent_k
       }
     }
 
-    PWG_TR(const unsigned long long tr_d = clock64(); tr_g1 += tr_b - tr_a; tr_gt += tr_c - tr_b;
-           tr_g2 += tr_d - tr_c; ++tr_n);
     if (nblk < 0) break;
     blk = nblk;
     nblk = ticket_resolve(ticket);
   }
-  PWG_TR(tr_done());
-#undef PWG_TR
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -144,43 +144,17 @@ struct SplitSmem {
   static constexpr int dwords(bool last) { return WG + W2 + BG + BO + (last ? HW1 : 0); }
 };
 
-// Diagnostic builds only (timing experiments, wrong results): PWG_SPLIT_L2ONLY folds every
-// x / skip access into a small window that stays L2-resident; PWG_SPLIT_NOGATE replaces the gate
-// by a product.
-#if PWG_SPLIT_L2ONLY
-#define PWG_COL(c) (((c) & 8191) + 1024)
-#else
-#define PWG_COL(c) (c)
-#endif
 // dword offset of piece 0 of column c, lane half hh, in the tiled x / skip layout (header);
 // piece i is PWG_PIECE dwords further
-#define PWG_ROW(c, hh) ((size_t)(PWG_COL(c) >> 5) * 2048 + (size_t)(hh) * 1024 + (size_t)(PWG_COL(c) & 31) * 4)
+#define PWG_ROW(c, hh) ((size_t)((c) >> 5) * 2048 + (size_t)(hh) * 1024 + (size_t)((c) & 31) * 4)
 #define PWG_PIECE 128
 
 // Cache policy of the streams that are touched once per layer (skip sum in, skip sum and x out):
 // non-temporal, so the XCD's L2 keeps the x rows that the three dilated taps of neighbouring
-// blocks re-read.
-#ifndef PWG_SPLIT_NT
-#define PWG_SPLIT_NT 3  // both: 1.825 -> 1.747 ms per layer
-#endif
-#if PWG_SPLIT_NT & 1
+// blocks re-read (1.825 -> 1.747 ms per layer). The A/B variants (cached streams, diagnostic
+// builds) are in git history before round 4.
 #define PWG_ST_STREAM(p, v) __builtin_nontemporal_store((v), (p))
-#else
-#define PWG_ST_STREAM(p, v) (*(p) = (v))
-#endif
-#if PWG_SPLIT_NT & 2
 #define PWG_LD_SKIP(p) __builtin_nontemporal_load(p)
-#else
-#define PWG_LD_SKIP(p) (*(p))
-#endif
-
-#ifndef PWG_SPLIT_DIAG_NOTAP
-#define PWG_SPLIT_DIAG_NOTAP 0  // diagnostic: every tap reads the center row (wrong results)
-#endif
-
-#ifndef PWG_SPLIT_SEED_RELOAD
-#define PWG_SPLIT_SEED_RELOAD 0  // 1: re-load the center row for the seeds (diagnostic)
-#endif
 
 template <bool LAST, int TC>
 __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs a) {
@@ -238,7 +212,7 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
   // a lane's 128 B of tap row (block column c + lane column + tap offset): [0..3] hi k-steps,
   // [4..7] lo k-steps
   auto bload = [&](int c, int tap, u32x4 (&b)[8]) {
-    const u32x4* p = reinterpret_cast<const u32x4*>(a.x_in + PWG_ROW(c + cl + (PWG_SPLIT_DIAG_NOTAP ? 0 : (tap - TC) * a.dil), hh));
+    const u32x4* p = reinterpret_cast<const u32x4*>(a.x_in + PWG_ROW(c + cl + (tap - TC) * a.dil, hh));
 #pragma unroll
     for (int i = 0; i < 8; ++i) b[i] = p[i * (PWG_PIECE / 4)];
   };
@@ -249,22 +223,15 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
       u32x4 ah[4], al[4];
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
-#if PWG_SPLIT_DIAG_LDS1  // diagnostic: one A fragment pair for every k-step (wrong results)
-        ah[m] = wgl[(m * 2) * 64];
-        al[m] = wgl[(m * 2 + 1) * 64];
-#else
         ah[m] = wgl[(((tap * 4 + s) * 4 + m) * 2) * 64];
         al[m] = wgl[(((tap * 4 + s) * 4 + m) * 2 + 1) * 64];
-#endif
       }
 #pragma unroll
       for (int m = 0; m < 4; ++m) acc[m] = mma(ah[m], b[s], acc[m]);
-#if !PWG_SPLIT_DIAG_1PASS  // diagnostic: hi*hi only (wrong results)
 #pragma unroll
       for (int m = 0; m < 4; ++m) acc[m] = mma(ah[m], b[4 + s], acc[m]);
 #pragma unroll
       for (int m = 0; m < 4; ++m) acc[m] = mma(al[m], b[s], acc[m]);
-#endif
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -284,31 +251,7 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
   int nblk = blk + x_waves;
   if (blk >= x_end) blk = -1;
   if (nblk >= x_end) nblk = -1;
-#if PWG_TRACE
-  // diagnostic build: [start_rt, end_rt, blocks, gemm1_cyc, aux+gate_cyc, gemm2_cyc, start_clk, end_clk]
-  unsigned long long* trw = a.trace + ((size_t)blockIdx.x * nw + wave) * 8;
-  const unsigned long long tr_rt0 = wall_clock64(), tr_c0 = clock64();
-  unsigned long long tr_g1 = 0, tr_gt = 0, tr_g2 = 0, tr_n = 0;
-  auto tr_done = [&] {
-    if (lane == 0) {
-      trw[0] = tr_rt0; trw[1] = wall_clock64(); trw[2] = tr_n; trw[3] = tr_g1; trw[4] = tr_gt;
-      trw[5] = tr_g2; trw[6] = tr_c0; trw[7] = clock64();
-    }
-  };
-#define PWG_TR(x) x
-#else
-#define PWG_TR(x)
-#endif
-  if (blk < 0) {
-    PWG_TR(tr_done());
-    return;
-  }
-#if PWG_SPLIT_STAGGER
-  // diagnostic: the second wave of each SIMD starts later so the two waves' MFMA and VALU
-  // phases interleave
-  if (wave >= 4)
-    for (int i = 0; i < PWG_SPLIT_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
-#endif
+  if (blk < 0) return;
   BlockDesc bdn = a.blocks[blk];
   u32x4 b0[8], b1[8];
   bload(bdn.col, 0, b0);
@@ -362,12 +305,6 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
     f32x16 seed[2];
-    PWG_TR(const unsigned long long tr_a = clock64());
-#if PWG_SPLIT_PRIO == 1
-    __builtin_amdgcn_s_setprio(1);  // GEMM 1 (MFMA phase) wins issue arbitration
-#elif PWG_SPLIT_PRIO == 2
-    __builtin_amdgcn_s_setprio(0);
-#endif
     // taps in the order 0, the other, the center: the center row is in registers at the end of
     // GEMM 1 and becomes the GEMM-2 out-row seeds right there (re-loading it later missed L2 for
     // ~half the blocks: +1.05 GB of HBM reads per launch)
@@ -379,16 +316,8 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
     mma_tap(acc, b1, T1);
     bload(col_next, 0, b1);
     mma_tap(acc, b0, TC);
-#if !PWG_SPLIT_SEED_RELOAD
     x_seed(b0, seed);
-#endif
 
-    PWG_TR(const unsigned long long tr_b = clock64());
-#if PWG_SPLIT_PRIO == 1
-    __builtin_amdgcn_s_setprio(0);
-#elif PWG_SPLIT_PRIO == 2
-    __builtin_amdgcn_s_setprio(1);  // aux + gate (VALU phase) wins issue arbitration
-#endif
     int ticket = 0;
     if (nblk >= 0) ticket = ticket_issue();
     // skip seeds (old skip sum; layer 0: the sum of all layers' skip biases)
@@ -442,13 +371,7 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
       const int gm = s >> 1, r0 = 8 * (s & 1);
       float gv[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-#if PWG_SPLIT_NOGATE
-        gv[k] = acc[gm][r0 + k] * acc[gm + 2][r0 + k];
-#else
-        gv[k] = gate(acc[gm][r0 + k], acc[gm + 2][r0 + k]);
-#endif
-      }
+      for (int k = 0; k < 8; ++k) gv[k] = gate(acc[gm][r0 + k], acc[gm + 2][r0 + k]);
       unsigned hv[4], lv[4];
       split8<0>(gv, hv, lv);
 #pragma unroll
@@ -458,25 +381,10 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
       }
     }
     if (!LAST) {
-#if PWG_SPLIT_SEED_RELOAD
-      u32x4 bc[8];
-#if PWG_SPLIT_DIAG_NORELOAD  // diagnostic: no center reload (wrong results)
-      for (int i = 0; i < 8; ++i) bc[i] = b1[i];
-#else
-      bload(bd.col, TC, bc);  // the center tap row again (an L2 hit): fewer registers live in GEMM 1
-#endif
-      x_seed(bc, seed);
-#endif
       acc2[2] = seed[0];
       acc2[3] = seed[1];
     }
 
-    PWG_TR(const unsigned long long tr_c = clock64());
-#if PWG_SPLIT_PRIO == 2
-    __builtin_amdgcn_s_setprio(0);
-#elif PWG_SPLIT_PRIO == 3
-    __builtin_amdgcn_s_setprio(1);  // GEMM 2 + stores
-#endif
     // ---- GEMM 2: [skip; out] rows
     constexpr int M2 = LAST ? 2 : 4;
     const u32x4* w2l = reinterpret_cast<const u32x4*>(s_w2) + lane;
@@ -582,21 +490,13 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split_kernel(const SplitArgs
       }
     }
 
-#if PWG_SPLIT_PRIO == 3
-    __builtin_amdgcn_s_setprio(0);
-#endif
-    PWG_TR(const unsigned long long tr_d = clock64(); tr_g1 += tr_b - tr_a; tr_gt += tr_c - tr_b;
-           tr_g2 += tr_d - tr_c; ++tr_n);
     if (nblk < 0) break;
     blk = nblk;
     nblk = ticket_resolve(ticket);
 #pragma unroll
     for (int i = 0; i < 8; ++i) b0[i] = b1[i];
   }
-  if (LAST && nonfinite && a.range_flag)
-    __hip_atomic_fetch_or(a.range_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  PWG_TR(tr_done());
-#undef PWG_TR
+  if (LAST && nonfinite && a.range_flag) flag_status(a.range_flag, a.sticky, PWG_STATUS_RANGE);
 }
 
 // first_conv (1x1, 1 -> 64, bias) into the split x layout; gap tiles zero both buffers.

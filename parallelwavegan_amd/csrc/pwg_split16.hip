@@ -20,6 +20,13 @@
 // Reference: layers/residual_block.py:102-140, models/parallel_wavegan.py:131-138,160-171.
 #include "pwg_internal.h"
 
+// A/B build switch (round 4, temporary): where the next work unit's tap-0 row is loaded.
+// 0: during the center tap's MFMAs (into b1); 1: after the GEMM-2 seeds (into b0, dead by then);
+// 2: just before GEMM 2 (into b0).
+#ifndef PWG_S16_PF
+#define PWG_S16_PF 0
+#endif
+
 namespace pwg {
 
 namespace {
@@ -263,10 +270,13 @@ __device__ __forceinline__ void s16_load_skip(const SplitArgs& a, const BlockDes
 // bd.col + h16 + [0, 16)); the next unit's half is h16n. Every column's accumulators sum the same
 // products in the same order as with NTN = 2, and the aux K slots stay anchored at the 32-sample
 // block's first frame: bit-identical per column.
+// poison (LAST): the run's earlier layers did not complete (a PWG_STATUS_REDO bit was set when the
+// launch started), so the block writes NaN audio instead of a plausible-looking wrong result.
 template <bool LAST, int TC, bool FIRST, bool PIPE, int NTN = 2, typename Mid>
 __device__ __forceinline__ void s16_block(const SplitArgs& a, const unsigned* smem16, const BlockDesc& bd,
                                           const BlockDesc& bdn, bool has_next, u32x4 (&b0)[8], u32x4 (&b1)[8],
-                                          bool& nonfinite, Mid&& mid, int h16 = 0, int h16n = 0) {
+                                          bool& nonfinite, Mid&& mid, int h16 = 0, int h16n = 0,
+                                          bool poison = false) {
   static_assert(NTN == 2 || !LAST, "half blocks: middle layers");
   const unsigned* s_wg = smem16;
   const unsigned* s_w2 = s_wg + Split16Smem::WG;
@@ -342,7 +352,7 @@ __device__ __forceinline__ void s16_block(const SplitArgs& a, const unsigned* sm
   s16_load_dv(a, bd, dv, g, c);
   s16_bload<TC, FIRST, PIPE, NTN>(a, s_fwb, bd, TC, b0, g, c, h16);
   mma_tap(acc, b1, T1);
-  if (has_next) s16_bload<TC, FIRST, PIPE, NTN>(a, s_fwb, bdn, 0, b1, g, c, h16n);  // the next block's
+  if (PWG_S16_PF == 0 && has_next) s16_bload<TC, FIRST, PIPE, NTN>(a, s_fwb, bdn, 0, b1, g, c, h16n);  // the next block's
   mma_tap(acc, b0, TC);
   if (!LAST) {
     // GEMM-2 out-row seeds sqrt(.5)(x + b_out) from the center tap: acc2[4 + 2ks + (j>>2)][nt][j&3]
@@ -357,6 +367,7 @@ __device__ __forceinline__ void s16_block(const SplitArgs& a, const unsigned* sm
         for (int j = 0; j < 8; ++j) acc2[4 + 2 * ks + (j >> 2)][nt][j & 3] = o[j];
       }
   }
+  if (PWG_S16_PF == 1 && has_next) s16_bload<TC, FIRST, PIPE, NTN>(a, s_fwb, bdn, 0, b0, g, c, h16n);
   mid();
 
   {
@@ -405,6 +416,7 @@ __device__ __forceinline__ void s16_block(const SplitArgs& a, const unsigned* sm
       split8x<0>(gv, gh[nt][ks], gl[nt][ks]);
     }
 
+  if (PWG_S16_PF == 2 && has_next) s16_bload<TC, FIRST, PIPE, NTN>(a, s_fwb, bdn, 0, b0, g, c, h16n);
   // ---- GEMM 2: [skip; out] rows, 8 m-tiles (last layer: the 4 skip tiles)
   constexpr int M2 = LAST ? 4 : 8;
   const u32x4* w2l = reinterpret_cast<const u32x4*>(s_w2) + lane;
@@ -540,7 +552,7 @@ __device__ __forceinline__ void s16_block(const SplitArgs& a, const unsigned* sm
         }
         part += __shfl_xor(part, 16);
         part += __shfl_xor(part, 32);
-        if (g == 0 && live) out[(size_t)oc * a.out_stride_o] = part + a.hb2[oc];
+        if (g == 0 && live) out[(size_t)oc * a.out_stride_o] = poison ? __builtin_nanf("") : part + a.hb2[oc];
       }
     }
   }
@@ -578,6 +590,12 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
   // and tap-0 rows load while the workgroup stages (layer 0 with the fused first_conv builds tap 0
   // from the first_conv weights in LDS, after the barrier)
   const int blk0 = wave < nw ? (int)((long long)n_units * xcd / 8) + (blockIdx.x >> 3) * nw + wave : -1;
+  // LAST: the run's status on entry (a grid-synchronised or pipelined launch before this one that
+  // aborted or timed out leaves stale planes: poison the output, pwg_run_status reports the redo)
+  bool poison = false;
+  if constexpr (LAST)
+    if (a.range_flag != nullptr)
+      poison = (__hip_atomic_load(a.range_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & PWG_STATUS_REDO) != 0;
   const bool has0 = blk0 >= 0 && blk0 < (int)((long long)n_units * (xcd + 1) / 8);
   BlockDesc bdn;
   int h16n = 0;
@@ -650,16 +668,17 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
     int ticket = 0;
     s16_block<LAST, TC, FIRST, false, NTN>(a, smem16, bd, bdn, true, b0, b1, nonfinite, [&]() {
       if (nblk >= 0) ticket = ticket_issue();
-    }, h16, h16n);
+    }, h16, h16n, poison);
     if (tr && n_done++ == 0) t_first = __builtin_amdgcn_s_memrealtime();
     if (nblk < 0) break;
     blk = nblk;
     nblk = ticket_resolve(ticket);
-    b0[0] = b1[0]; b0[1] = b1[1]; b0[2] = b1[2]; b0[3] = b1[3];
-    b0[4] = b1[4]; b0[5] = b1[5]; b0[6] = b1[6]; b0[7] = b1[7];
+    if (PWG_S16_PF == 0) {
+      b0[0] = b1[0]; b0[1] = b1[1]; b0[2] = b1[2]; b0[3] = b1[3];
+      b0[4] = b1[4]; b0[5] = b1[5]; b0[6] = b1[6]; b0[7] = b1[7];
+    }
   }
-  if (LAST && nonfinite && a.range_flag)
-    __hip_atomic_fetch_or(a.range_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (LAST && nonfinite && a.range_flag) flag_status(a.range_flag, a.sticky, PWG_STATUS_RANGE);
   trace_out();
 }
 
@@ -672,8 +691,8 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
 // updated in place). prog[b] = layers finished on block b. Hand-off bytes (x, skip) are stored and
 // loaded sc1, each storing wave drains its stores (s_waitcnt vmcnt(0)) before it publishes
 // prog[b] with an sc1 atomic store; consumers poll prog relaxed (Guideline 16, R1 with sc1 loads).
-// Every spin is bounded: a wait that gives up sets bit 1 of the range word (pwg_run_status
-// reports it) and the grid still drains. Requires every workgroup resident: grid <= CUs, one
+// Every spin is bounded: a wait that gives up sets PWG_STATUS_PIPE_TIMEOUT (pwg_run_status reports
+// PWG_ERR_RERUN) and the grid still drains. Requires every workgroup resident: grid <= CUs, one
 // 512-thread workgroup per CU (the LDS image holds that).
 constexpr int PIPE_SPIN_LIMIT = 1 << 20;
 
@@ -713,7 +732,7 @@ __device__ __forceinline__ void pipe_layer(const PipeArgs& p, int l, unsigned* s
                          : 0x7fffffff;
       if (__all(v >= thr)) break;
       if (spins >= PIPE_SPIN_LIMIT) {
-        if (lane == 0) __hip_atomic_fetch_or(p.base.range_flag, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) flag_status(p.base.range_flag, p.base.sticky, PWG_STATUS_PIPE_TIMEOUT);
         break;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -737,8 +756,7 @@ __device__ __forceinline__ void pipe_layer(const PipeArgs& p, int l, unsigned* s
     }
     blk = next;
   }
-  if (LAST && nonfinite && a.range_flag)
-    __hip_atomic_fetch_or(a.range_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (LAST && nonfinite && a.range_flag) flag_status(a.range_flag, a.sticky, PWG_STATUS_RANGE);
 }
 
 template <int TC>
@@ -767,14 +785,18 @@ __global__ void __launch_bounds__(512, 1) pwg_pipe_split16_kernel(const PipeArgs
 // process holding CUs can prevent. So every workgroup first counts itself in, and the first one to
 // see either the full count or its bounded wait expire decides for all (one CAS): "run" (every
 // workgroup had started, so all are resident) or "abort" (every workgroup exits at once, no x or skip
-// written; pwg_run_status returns PWG_ERR_RERUN and the engine reruns on the per-layer launches).
+// written, PWG_STATUS_SYNC_ABORT: pwg_run_status returns PWG_ERR_RERUN, the last layer writes NaN
+// audio, and the engine reruns on the per-layer launches).
 // Measured: claiming units dynamically instead (one queue per layer, deadlock-free without the
 // check) cost 0.35 -> 0.89 ms at LJ T' = 64: the claims serialise on the queue head.
 // Hand-off (cdna_hip_programming.md Guideline 16; MI355X_MICROARCH.md hand-off table, row 1): every
 // store and every load of x and skip is sc1 (the PIPE forms of s16_block), every storing wave
 // drains (s_waitcnt vmcnt(0)) before a workgroup barrier, then one lane adds to the barrier counter
 // (agent-scope atomic); one lane polls it with sc1 loads and a workgroup barrier follows. Bounded
-// spins: a wait that gives up sets bit 1 of the range word (pwg_run_status reports it).
+// spins: a wait that gives up sets PWG_STATUS_SYNC_TIMEOUT (pwg_run_status returns PWG_ERR_RERUN,
+// the last layer writes NaN audio, and the engine reruns on the per-layer launches, which rebuild
+// every plane from the mel and the noise). The grid needs at least 8 workgroups (one per XCD
+// eighth of the work units; launch_sync_split16 checks).
 template <int TC, bool FIRST, int NTN>
 __device__ __forceinline__ void sync_layer(const SplitArgs& a, const unsigned* smem16) {
   constexpr int UB = NTN == 1 ? 1 : 0;
@@ -805,7 +827,8 @@ __device__ __forceinline__ void sync_layer(const SplitArgs& a, const unsigned* s
     bd = bdn;
     h16 = h16n;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) b0[q] = b1[q];
+    for (int q = 0; q < 8; ++q)
+      if (PWG_S16_PF == 0) b0[q] = b1[q];
   }
 }
 
@@ -861,7 +884,7 @@ __global__ void __launch_bounds__(512, 1) pwg_sync_split16_kernel(const SyncArgs
   }
   __syncthreads();
   if (s_decision != 1 || p.force_abort) {
-    if (threadIdx.x == 0) __hip_atomic_fetch_or(p.base.range_flag, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) flag_status(p.base.range_flag, p.base.sticky, PWG_STATUS_SYNC_ABORT);
     return;
   }
   bool timed_out = false;
@@ -881,6 +904,10 @@ __global__ void __launch_bounds__(512, 1) pwg_sync_split16_kernel(const SyncArgs
     if (threadIdx.x == 0) {
       const int target = (l - p.l0 + 1) * nwg;
       for (int spins = 0;; ++spins) {
+        if (p.force_timeout) {  // test hook: give up without waiting
+          timed_out = true;
+          break;
+        }
         if (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
         if (spins >= PIPE_SPIN_LIMIT) {
           timed_out = true;
@@ -891,7 +918,7 @@ __global__ void __launch_bounds__(512, 1) pwg_sync_split16_kernel(const SyncArgs
     }
     __syncthreads();
   }
-  if (timed_out) __hip_atomic_fetch_or(p.base.range_flag, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (timed_out) flag_status(p.base.range_flag, p.base.sticky, PWG_STATUS_SYNC_TIMEOUT);
 }
 
 // first_conv (1x1, 1 -> 64, bias) into the split16 x layout; gap tiles zero every residual plane.
@@ -980,6 +1007,7 @@ hipError_t launch_layer_split16(const SplitArgs& a, bool last, int tap_center, i
 hipError_t launch_sync_split16(const SyncArgs& p, int tap_center, int n_wg, hipStream_t s) {
   const size_t lds = sizeof(unsigned) * (Split16Smem::dwords(false) + 128);
   if (p.L < 1 || p.L > PIPE_MAX_LAYERS || p.waves_mid < 1 || p.waves_mid > 8) return hipErrorInvalidValue;
+  if (n_wg < 8) return hipErrorInvalidValue;  // sync_layer deals the units to 8 eighths by blockIdx & 7
   auto kfn = tap_center == 1 ? (p.half ? &pwg_sync_split16_kernel<1, 1> : &pwg_sync_split16_kernel<1, 2>)
              : tap_center == 2 ? (p.half ? &pwg_sync_split16_kernel<2, 1> : &pwg_sync_split16_kernel<2, 2>)
                                : nullptr;

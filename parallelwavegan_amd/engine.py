@@ -277,6 +277,12 @@ class Engine:
         self.split_range_ok = True
         self.range_reruns = 0  # runs redone on the exact-fp32 kernel after a split-f16 range flag
         self.sync_reruns = 0  # grid-synchronised runs redone per-layer (the GPU was shared)
+        # consecutive sync reruns; at SYNC_FAIL_STREAK the engine stops using the synchronised
+        # forward for SYNC_RETRY_RUNS runs (a persistently shared GPU would otherwise pay the
+        # residency wait, a stream sync and a full per-layer rerun on every call)
+        self._sync_streak = 0
+        self._sync_saved = None  # the sync plan limit while suspended
+        self._sync_retry_in = 0
         self.layer_kernel = self.get_option("layer_kernel")
 
     def __del__(self):
@@ -361,7 +367,10 @@ class Engine:
     _OPTS = {"layer_kernel": _lib.PWG_OPT_LAYER_KERNEL, "waves_per_wg": _lib.PWG_OPT_WAVES_PER_WG,
              "wg_per_cu": _lib.PWG_OPT_WG_PER_CU, "fuse_first_conv": _lib.PWG_OPT_FUSE_FIRST_CONV,
              "pipeline": _lib.PWG_OPT_PIPELINE, "half_blocks": _lib.PWG_OPT_HALF_BLOCKS,
-             "sync": _lib.PWG_OPT_SYNC, "sync_abort": _lib.PWG_OPT_SYNC_ABORT}
+             "sync": _lib.PWG_OPT_SYNC, "sync_abort": _lib.PWG_OPT_SYNC_ABORT,
+             "sync_timeout": _lib.PWG_OPT_SYNC_TIMEOUT}
+    SYNC_FAIL_STREAK = 3
+    SYNC_RETRY_RUNS = 256
 
     def get_option(self, option):
         v = ctypes.c_longlong()
@@ -397,16 +406,18 @@ class Engine:
 
     def _range_check(self, plan, mel, noise, out, mean, scale, stream):
         """Split-f16 range check of the run just enqueued on ``stream``; a flagged run is redone
-        on the exact-fp32 layer kernel. A grid-synchronised run that found the GPU shared
-        (PWG_ERR_RERUN: it wrote nothing) is redone on the per-layer launches first."""
+        on the exact-fp32 layer kernel. A grid-synchronised run that did not complete
+        (PWG_ERR_RERUN: the GPU was shared, or a grid-barrier wait gave up; its output is NaN) is
+        redone on the per-layer launches first."""
         if self.layer_kernel not in (2, 3):
             return
         try:
             try:
                 self.run_status(plan, stream)
-            except _lib.RerunError:
+                self._sync_streak = 0
+            except _lib.RerunError as e:
                 self._enqueue_per_layer(plan, mel, noise, out, mean, scale, stream)
-                self.sync_reruns += 1
+                self._note_sync_rerun(e)
                 self.run_status(plan, stream)
         except _lib.RangeError as e:
             logging.warning("%s; rerunning on the exact-fp32 layer kernel", e)
@@ -418,13 +429,41 @@ class Engine:
                 self.set_option("layer_kernel", kernel)
             self.range_reruns += 1
 
+    def _note_sync_rerun(self, err):
+        """Count a PWG_ERR_RERUN; after SYNC_FAIL_STREAK in a row, stop using the synchronised
+        forward for SYNC_RETRY_RUNS runs (then try it again)."""
+        self.sync_reruns += 1
+        self._sync_streak += 1
+        if self._sync_streak >= self.SYNC_FAIL_STREAK and self._sync_saved is None:
+            logging.warning("%s (%d runs in a row): per-layer launches for the next %d runs",
+                            err, self._sync_streak, self.SYNC_RETRY_RUNS)
+            self._sync_saved = self.get_option("sync")
+            self._sync_retry_in = self.SYNC_RETRY_RUNS
+            _lib.check(self._lib.pwg_set_option(self._h, _lib.PWG_OPT_SYNC, 0))
+
+    def _sync_tick(self):
+        """Called per enqueued run: restore the synchronised forward after a suspension. One more
+        failure then suspends it again at once."""
+        if self._sync_saved is None:
+            return
+        self._sync_retry_in -= 1
+        if self._sync_retry_in <= 0:
+            _lib.check(self._lib.pwg_set_option(self._h, _lib.PWG_OPT_SYNC, self._sync_saved))
+            self._sync_saved = None
+            self._sync_streak = self.SYNC_FAIL_STREAK - 1
+
     def _enqueue_per_layer(self, plan, mel, noise, out, mean, scale, stream):
-        sync = self.get_option("sync")
-        self.set_option("sync", 0)
+        """Redo a run on the per-layer launches: the grid-synchronised forward and the layer
+        pipeline off for this one enqueue (set through the C-ABI directly: the cached plans stay)."""
+        lib, h = self._lib, self._h
+        sync, pipe = self.get_option("sync"), self.get_option("pipeline")
+        _lib.check(lib.pwg_set_option(h, _lib.PWG_OPT_SYNC, 0))
+        _lib.check(lib.pwg_set_option(h, _lib.PWG_OPT_PIPELINE, 0))
         try:
             self._enqueue(plan, mel, noise, out, mean, scale, stream)
         finally:
-            self.set_option("sync", sync)
+            _lib.check(lib.pwg_set_option(h, _lib.PWG_OPT_SYNC, sync))
+            _lib.check(lib.pwg_set_option(h, _lib.PWG_OPT_PIPELINE, pipe))
 
     def run_status(self, plan, stream=None):
         """pwg_run_status of the last run on ``stream``'s workspace: raises _lib.RangeError when the
@@ -456,6 +495,7 @@ class Engine:
             scale = scale.to(self.device, torch.float32).contiguous()
             mp, sp = mean.data_ptr(), scale.data_ptr()
         ws = self.workspace(plan.workspace_bytes, stream)
+        self._sync_tick()
         _lib.check(
             self._lib.pwg_run(
                 plan._p,

@@ -174,13 +174,15 @@ def test_get_option_reports_default_layer_kernel(built_lib):
 
 
 def test_sync_options_round_trip_and_validate(built_lib):
-    """PWG_OPT_SYNC (grid-synchronised plan limit, >= 0) and PWG_OPT_SYNC_ABORT (test hook, 0/1):
+    """PWG_OPT_SYNC (grid-synchronised plan limit, >= 0), PWG_OPT_SYNC_ABORT and PWG_OPT_SYNC_TIMEOUT
+    (test hooks, 0/1):
     set / get round trip and argument checks, host-only; the error codes map to the Python
     exceptions (PWG_ERR_RERUN -> RerunError)."""
     h = HostHandle(configs.generator_params("ljspeech_v1"))
     v = ctypes.c_longlong()
     for opt, good, bad in ((_lib.PWG_OPT_SYNC, (0, 4096, 1 << 40), (-1,)),
-                           (_lib.PWG_OPT_SYNC_ABORT, (0, 1), (2, -1))):
+                           (_lib.PWG_OPT_SYNC_ABORT, (0, 1), (2, -1)),
+                           (_lib.PWG_OPT_SYNC_TIMEOUT, (0, 1), (2, -1))):
         for val in good:
             _lib.check(built_lib.pwg_set_option(h._h, opt, val))
             _lib.check(built_lib.pwg_get_option(h._h, opt, ctypes.byref(v)))

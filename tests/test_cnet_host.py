@@ -165,3 +165,36 @@ def test_plan_past_the_buffer_limit_is_refused(built_lib):
         eng.plan([131072, 131072])
     with pytest.raises(ValueError):
         eng.plan([0])
+
+
+@pytest.mark.parametrize("name", ["mb_melgan_v2", "melgan_v1", "hifigan_v1", "mb_melgan_v2_causal",
+                                  "hifigan_v1_causal", "hifigan_causal_test"])
+def test_host_only_plans_build_and_check_their_block_lists(name, built_lib):
+    """pwg_cnet_plan_create on a host-only handle (device -1) runs the whole host side of the plan
+    (buffer rows, workspace slots, every phase's block / strip / x-tile lists and their bounds
+    check) without a GPU, so the plan builder runs here and under the sanitizers
+    (tests/test_host_sanitized.py): ragged batches, the shortest utterances ReflectionPad1d allows, long utterances. A host-
+    only plan refuses to run."""
+    import ctypes
+
+    from parallelwavegan_amd import _lib
+    from parallelwavegan_amd.cnet import CnetEngine
+
+    m = _holder(name)
+    if isinstance(m, MelGANGenerator) and m.out_channels > 1:
+        m.pqmf = PQMF(m.out_channels)
+        P, _ = m.program(True)
+    elif isinstance(m, MelGANGenerator):
+        P, _ = m.program(False)
+    else:
+        P = m.program()
+    eng = CnetEngine(P, None, host_only=True)
+    hop = P.rate[-1]
+    for frames in ([8], [9, 8, 10], [64], [80, 1199, 517], [2048] * 4, [9000]):  # MelGAN: reflect pads up to 6
+        plan = eng.plan(frames)
+        assert plan.out_rows == sum(frames) * hop
+        assert plan.workspace_bytes >= 256
+    p = eng.plan([16])
+    rc = eng._lib.pwg_cnet_run(p._p, ctypes.c_void_p(16), ctypes.c_void_p(16), None, None, ctypes.c_void_p(16),
+                               ctypes.c_void_p(256), None)
+    assert rc == _lib.PWG_ERR_INVALID

@@ -214,3 +214,78 @@ def test_sync_abort_path_writes_nothing_and_reruns(built_lib, cuda_device):
         y = m.inference(mels[0], noises[0])
     assert m.engine().sync_reruns == 1
     assert torch.equal(y.reshape(-1), ref[0].reshape(-1))
+
+
+@pytest.mark.parametrize("hook", ["sync_abort", "sync_timeout"])
+def test_sync_failure_poisons_output_and_sticky_status(hook, built_lib, cuda_device):
+    """Both failure exits of the synchronised launch: the residency abort and a
+    grid-barrier wait that gives up (PWG_OPT_SYNC_TIMEOUT: every wait gives up at once, so the
+    workgroups run ahead on partial planes). Either way
+    - the last layer writes NaN audio, never a plausible wrong waveform;
+    - pwg_run_status returns PWG_ERR_RERUN, and it does so even when later runs completed, because
+      the handle's sticky status word keeps the bit until a status call reads it (a serving loop
+      that checks once per batch of runs);
+    - Engine.run(check=True) redoes the run on the per-layer launches: bit-identical output, one
+      rerun counted."""
+    from parallelwavegan_amd import _lib, configs
+
+    params = configs.generator_params("ljspeech_v1")
+    per_layer, sync = _engines(params, cuda_device, seed=10)
+    mels, noises = _inputs([64, 3], 256, cuda_device, seed=15)
+    ref = torch.cat([y.reshape(-1) for y in per_layer.infer(mels, noises)])
+    plan = sync.plan([64, 3])
+    mel = torch.cat([m.reshape(-1) for m in mels])
+    noise = torch.cat([n.reshape(-1) for n in noises])
+
+    sync.set_option(hook, 1)
+    out = torch.zeros(plan.total_samples, device=cuda_device)
+    sync.run(plan, mel, noise, out, check=False)
+    torch.cuda.synchronize(cuda_device)
+    assert torch.isnan(out).all()
+    with pytest.raises(_lib.RerunError):
+        sync.run_status(plan)
+
+    # the failed run first, then three good ones, one status call at the end: still reported
+    sync.run(plan, mel, noise, out, check=False)
+    sync.set_option(hook, 0)
+    good = torch.empty_like(out)
+    for _ in range(3):
+        sync.run(plan, mel, noise, good, check=False)
+    with pytest.raises(_lib.RerunError):
+        sync.run_status(plan)
+    sync.run_status(plan)  # read and cleared: the next call sees only the last (good) run
+    assert torch.equal(good, ref)
+
+    sync.set_option(hook, 1)
+    n0 = sync.sync_reruns
+    sync.run(plan, mel, noise, out)  # check=True: rerun per-layer
+    assert sync.sync_reruns == n0 + 1
+    assert torch.equal(out, ref)
+    sync.set_option(hook, 0)
+
+
+def test_engine_suspends_sync_after_repeated_failures(built_lib, cuda_device):
+    """on a GPU that is persistently shared every synchronised call would pay the
+    failed launch, a synchronisation and a full rerun. After Engine.SYNC_FAIL_STREAK reruns in a
+    row the engine stops using the synchronised forward, and tries it again after
+    SYNC_RETRY_RUNS runs."""
+    from parallelwavegan_amd import configs
+
+    params = configs.generator_params("ljspeech_v1")
+    per_layer, sync = _engines(params, cuda_device, seed=11)
+    sync.SYNC_RETRY_RUNS = 5
+    mels, noises = _inputs([64], 256, cuda_device, seed=16)
+    ref = per_layer.infer(mels, noises)[0].clone()
+    limit = sync.get_option("sync")
+    sync.set_option("sync_abort", 1)
+    for i in range(sync.SYNC_FAIL_STREAK):
+        assert torch.equal(sync.infer(mels, noises)[0], ref)
+    assert sync.sync_reruns == sync.SYNC_FAIL_STREAK
+    assert sync.get_option("sync") == 0  # suspended
+    for _ in range(4):
+        assert torch.equal(sync.infer(mels, noises)[0], ref)
+    assert sync.sync_reruns == sync.SYNC_FAIL_STREAK  # per-layer runs: no more reruns
+    sync.set_option("sync_abort", 0)
+    assert torch.equal(sync.infer(mels, noises)[0], ref)  # the 5th run: sync restored, and it works
+    assert sync.get_option("sync") == limit
+    assert sync.sync_reruns == sync.SYNC_FAIL_STREAK

@@ -1,5 +1,6 @@
 """Per-op time and MFMA rate of a MelGAN-family program on the GPU (diagnostic).
-Usage: python tools/cnet_profile.py mb_melgan_v2 [--utts 32] [--steps 3]"""
+Usage: python tools/cnet_profile.py mb_melgan_v2 [--utts 32] [--steps 3] [--frames 64 --batch 1]
+(--frames: B equal-length utterances of that many frames instead of the bench's ragged list)"""
 import argparse
 import os
 import sys
@@ -21,6 +22,8 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--nofuse", action="store_true")
     ap.add_argument("--pair-steps", type=int, default=None)
+    ap.add_argument("--frames", type=int, default=None)
+    ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--dump", default=None, help="save the first forward's output (.npy) for a bitwise A/B")
     a = ap.parse_args()
     cls, p = configs.vocoder_params(a.config)
@@ -35,7 +38,7 @@ def main():
     if a.pair_steps:
         eng.set_pair_steps(a.pair_steps)
     P = eng.program
-    lengths = synthetic.libritts_lengths(a.utts, seed=3)
+    lengths = (np.full(a.batch, a.frames) if a.frames else synthetic.libritts_lengths(a.utts, seed=3))
     frames = int(lengths.sum())
     plan = eng.plan(lengths.tolist())
     torch.manual_seed(0)
