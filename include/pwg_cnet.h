@@ -133,9 +133,16 @@ PWG_API int pwg_cnet_run_status(PwgCnetPlan* p, const void* workspace, void* str
  * tap-major one (channel-block-major summation: parity to the oracle, not bit identity).
  * PWG_CNET_OPT_XCD_ORDER (default 1): launches with several m-groups or ConvTranspose phases per
  * column block deal a block's siblings to one XCD in consecutive rounds, so they share its L2
- * instead of each fetching the block's input rows from HBM (0: grid order; same results). */
+ * instead of each fetching the block's input rows from HBM (0: grid order; same results).
+ * PWG_CNET_OPT_NARROW (default 1, x-tile mode, applies to plans created afterwards): x-tile
+ * launches (convs, conv pair / stack halves, ConvTranspose phases) whose 8-wave, 256-column
+ * workgroups would number fewer than the device's CUs run narrow workgroups instead: 1-4 waves
+ * (32-128 columns) and 1-2 m-tiles each, weights DMA-staged in tap groups, so a short utterance's
+ * op spreads over every CU (the B = 1 decode path, bin/decode.py:236-268); a fused pair or stack
+ * whose first conv runs narrow runs as its two ops. Bit-identical to the default launches.
+ * 0: never; 2: every x-tile launch (tests). */
 enum { PWG_CNET_OPT_SPLIT_F16 = 0, PWG_CNET_OPT_FUSE_PAIRS = 1, PWG_CNET_OPT_PAIR_STEPS = 2, PWG_CNET_OPT_XTILE = 3,
-       PWG_CNET_OPT_XT_DMA = 4, PWG_CNET_OPT_XCD_ORDER = 5 };
+       PWG_CNET_OPT_XT_DMA = 4, PWG_CNET_OPT_XCD_ORDER = 5, PWG_CNET_OPT_NARROW = 6 };
 PWG_API int pwg_cnet_set_option(PwgCnet* n, int option, long long value);
 PWG_API int pwg_cnet_set_timing(PwgCnet* n, int enable);
 /* Adds per-op milliseconds and launch counts (arrays of n_ops) and clears the records. */

@@ -424,6 +424,14 @@ class CnetEngine:
         column block run on one XCD back to back, sharing its L2 (default on; same results)."""
         _lib.check(self._lib.pwg_cnet_set_option(self._h, 5, int(bool(enable))))
 
+    def set_narrow(self, mode):
+        """pwg_cnet_set_option(PWG_CNET_OPT_NARROW): small launches of the x-tile family run narrow
+        workgroups (1-4 waves, 1-2 m-tiles) spread over every CU: 1 (default) when a launch would
+        have fewer workgroups than CUs, 2 always, 0 never. Plan-time: cached plans are dropped.
+        Bit-identical."""
+        _lib.check(self._lib.pwg_cnet_set_option(self._h, 6, int(mode)))
+        self._plans.clear()
+
     def set_pair_steps(self, steps):
         """pwg_cnet_set_option(PWG_CNET_OPT_PAIR_STEPS): 128-column tiles per fused-pair
         workgroup, for plans created afterwards (cached plans are dropped)."""

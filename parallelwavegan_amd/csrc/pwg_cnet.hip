@@ -428,6 +428,7 @@ struct CnXtileArgs {
 };
 __host__ __device__ constexpr bool xtile_supported(int k) { return k == 3 || k == 5 || k == 7 || k == 11; }
 constexpr int XT_COLS = 256;
+constexpr int NARROW_HALO = 64;  // narrow x-tile launches: (K - 1) dil at most this (register budget)
 constexpr int XT_ROWB = 80;  // bytes per staged input row: 16 hi + 16 lo halves + 16 B pad
 
 // SY (synchronous staging): no register prefetch of the next channel block; the kernel is held to
@@ -447,12 +448,14 @@ constexpr int xt_wpe() {
 // group's MFMAs and converted into the (single) row buffer after it. KS < K: two tap groups per
 // channel block, [0, KS) always in buffer 0 and [KS, K) in buffer 1; KS == K: the buffers alternate
 // per block. Same products in the same order as the other variants: bit-identical.
-template <int MT, int K, int CB, int NC = 1, bool SY = false, int KS = K, bool DB = false>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(xt_wpe<MT, K, CB, SY, DB>())))
+template <int MT, int K, int CB, int NC = 1, bool SY = false, int KS = K, bool DB = false, int NWV = 8>
+__global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(xt_wpe<MT, K, CB, SY, DB>())))
 pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
   static_assert(KS == K || SY || DB, "tap-split staging is a synchronous-staging or DMA variant");
   static_assert(!DB || (CB == 1 && NC == 1 && !SY), "DMA staging: one block, one column tile");
-  constexpr int NTH = 512;
+  static_assert(NWV == 8 || (DB && NC == 1), "narrow workgroups: the DMA-staged variant");
+  constexpr int NTH = 64 * NWV;
+  constexpr int XC = 32 * NWV;  // output columns per column tile (256 at 8 waves)
   constexpr int AV = CB * K * MT * 128;                // A vectors (16 B) per group of CB channel blocks
   constexpr int AQ = DB ? 1 : (AV + NTH - 1) / NTH;
   constexpr int A_BYTES = CB * KS * MT * 2048;
@@ -472,7 +475,7 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
   const int m0 = tid.y * MT;
   const int zp = tid.z;  // ConvTranspose phase (0 for convs)
   // column tiles holding live columns (uniform over the workgroup)
-  const int nc_live = NC == 1 ? 1 : (nq - q0 > XT_COLS ? NC : 1);
+  const int nc_live = NC == 1 ? 1 : (nq - q0 > XC ? NC : 1);
   const float* const wfrag_ = zp == 0 ? a.wfrag : a.z_wfrag[zp];
   const float* const bias_ = zp == 0 ? a.bias : a.z_bias[zp];
   const int ophase_ = a.ophase + zp;
@@ -480,7 +483,7 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
   const CnSrc& sx = a.src[0];
   const int2 sg = *reinterpret_cast<const int2*>(sx.seg + 2 * u);
   const int xv = CB * xt.span * 4;                     // input quads (4 channels) per group
-  constexpr int XQ_MAX = (CB * (NC * XT_COLS + 192) * 4 + NTH - 1) / NTH;
+  constexpr int XQ_MAX = (CB * (NC * XC + (NWV == 8 ? 192 : NARROW_HALO)) * 4 + NTH - 1) / NTH;
 
   f32x4v ar[AQ];
   f32x4v xr[XQ_MAX];
@@ -635,7 +638,7 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
 #pragma unroll
         for (int nc = 0; nc < NC; ++nc) {
           const unsigned char* row =
-              s_x + ((size_t)c * xt.span + nc * XT_COLS + wave * 32 + cl + tap * xt.dil) * XT_ROWB;
+              s_x + ((size_t)c * xt.span + nc * XC + wave * 32 + cl + tap * xt.dil) * XT_ROWB;
           bh[nc] = *reinterpret_cast<const u32x4v*>(row + 16 * hh);
           bl[nc] = *reinterpret_cast<const u32x4v*>(row + 32 + 16 * hh);
         }
@@ -739,7 +742,7 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
   const bool quad = (a.ld_dst & 3) == 0;
 #pragma unroll
   for (int nc = 0; nc < NC; ++nc) {
-    const int qb = q0 + nc * XT_COLS + wave * 32 + cl;
+    const int qb = q0 + nc * XC + wave * 32 + cl;
     if (qb >= nq) break;
     const int t = qb * a.ostride + ophase_;
     float* yrow = a.y + (size_t)(sd.x + t) * a.ld_dst;
@@ -899,6 +902,40 @@ hipError_t xtile_launch(int mt, int k, bool sync, int ks, dim3 grid, int lds, hi
     case 4: return xtile_launch_mt<4, 1>(k, grid, lds, s, a, xt);
     default: return hipErrorInvalidValue;
   }
+}
+
+// Narrow x-tile launches (PWG_CNET_OPT_NARROW, small plans: the B = 1 decode path of
+// bin/decode.py:236-268): NWV waves (32 NWV output columns) and MT m-tiles per workgroup, the A
+// fragments DMA-staged in tap groups of narrow_ks(K) taps, so an op whose 8-wave launch would
+// occupy a few dozen CUs spreads over all of them. Every column sums the same products in the same
+// order as on the 8-wave kernels: bit-identical.
+constexpr int narrow_ks(int k) { return k <= 3 ? k : (k == 5 ? 3 : 4); }
+template <int MT, int NWV>
+hipError_t xtile_launch_narrow_mt(int k, dim3 grid, int lds, hipStream_t s, const CnConvArgs& a, const CnXtileArgs& xt) {
+  auto go = [&](auto kfn) -> hipError_t {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kfn, grid, dim3(64 * NWV), (size_t)lds, s, a, xt);
+    return hipGetLastError();
+  };
+  switch (k) {
+    case 2: return go(pwg_cnet_xtile_kernel<MT, 2, 1, 1, false, narrow_ks(2), true, NWV>);
+    case 3: return go(pwg_cnet_xtile_kernel<MT, 3, 1, 1, false, narrow_ks(3), true, NWV>);
+    case 5: return go(pwg_cnet_xtile_kernel<MT, 5, 1, 1, false, narrow_ks(5), true, NWV>);
+    case 7: return go(pwg_cnet_xtile_kernel<MT, 7, 1, 1, false, narrow_ks(7), true, NWV>);
+    case 11: return go(pwg_cnet_xtile_kernel<MT, 11, 1, 1, false, narrow_ks(11), true, NWV>);
+    default: return hipErrorInvalidValue;
+  }
+}
+hipError_t xtile_launch_narrow(int mt, int nwv, int k, dim3 grid, int lds, hipStream_t s, const CnConvArgs& a,
+                               const CnXtileArgs& xt) {
+  if (mt == 1 && nwv == 1) return xtile_launch_narrow_mt<1, 1>(k, grid, lds, s, a, xt);
+  if (mt == 1 && nwv == 2) return xtile_launch_narrow_mt<1, 2>(k, grid, lds, s, a, xt);
+  if (mt == 1 && nwv == 4) return xtile_launch_narrow_mt<1, 4>(k, grid, lds, s, a, xt);
+  if (mt == 2 && nwv == 1) return xtile_launch_narrow_mt<2, 1>(k, grid, lds, s, a, xt);
+  if (mt == 2 && nwv == 2) return xtile_launch_narrow_mt<2, 2>(k, grid, lds, s, a, xt);
+  if (mt == 2 && nwv == 4) return xtile_launch_narrow_mt<2, 4>(k, grid, lds, s, a, xt);
+  return hipErrorInvalidValue;
 }
 
 // Fused conv pair on the x-tile scheme (split-f16; HiFiGAN ResBlock step x = c2(lrelu(c1(lrelu(x)))) + x,
@@ -2467,6 +2504,7 @@ struct PwgCnet {
   int xtile = 1;       // PWG_CNET_OPT_XTILE
   int xt_dma = 9;      // PWG_CNET_OPT_XT_DMA flags (CNET_DMA_RULE | CNET_DMA_CONVT)
   int xcd_order = 1;   // PWG_CNET_OPT_XCD_ORDER
+  int narrow = 1;      // PWG_CNET_OPT_NARROW (plan time): 0 off, 1 small launches, 2 every x-tile phase
   bool pair_attr_set = false;
   std::vector<PwgCnetOp> ops;
   std::vector<int> channels, rate, ld;
@@ -2497,6 +2535,10 @@ struct PwgCnetPlan {
   std::vector<int> n_xblocks;
   int pair_steps = 16;
   bool host_only = false;                    // a handle created for device -1: built and checked, not uploaded
+  int n_cu = 0;                              // CUs of the device (plan-time launch sizing)
+  // per phase: narrow x-tile launch (PWG_CNET_OPT_NARROW), 0 waves = the phase's default launch
+  std::vector<int> nar_nwv, nar_mt, nar_lds, n_nblocks;
+  std::vector<int2*> d_nblocks;              // its blocks (utt, q0 step 32 nar_nwv)
 };
 
 namespace {
@@ -3105,8 +3147,20 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
   // was never set, a block outside its utterance) fails here with PWG_ERR_ASSERT instead of turning
   // into an illegal address in a kernel (round 3's fault: an uninitialised OpPhase field)
   const size_t nph = n->phases.size();
-  std::vector<std::vector<int2>> h_blocks(nph), h_strips(nph), h_xblocks(nph);
+  std::vector<std::vector<int2>> h_blocks(nph), h_strips(nph), h_xblocks(nph), h_nblocks(nph);
   std::vector<std::vector<int>> h_ncols(nph);
+  p->nar_nwv.assign(nph, 0);
+  p->nar_mt.assign(nph, 0);
+  p->nar_lds.assign(nph, 0);
+  p->n_cu = 256;  // host-only handles size for an MI355X
+  if (n->device >= 0) {
+    int cu = 0;
+    if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, n->device) != hipSuccess || cu < 1) {
+      delete p;
+      return fail(PWG_ERR_HIP, "cannot query the CU count");
+    }
+    p->n_cu = cu;
+  }
   auto bad_list = [&](size_t pi, const char* what) {
     delete p;
     return fail(PWG_ERR_ASSERT, "internal: plan phase " + std::to_string(pi) + ": " + what);
@@ -3143,8 +3197,50 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
       for (int u = 0; u < n_utts; ++u)
         for (int q0 = 0; q0 < ncols[u]; q0 += step) h_xblocks[pi].push_back(make_int2(u, q0));
     }
+    // narrow x-tile launch: phases of the x-tile family (plain x-tile convs, x-tile pair / stack
+    // halves, ConvTranspose phases) whose default launch has fewer workgroups than CUs (or all of
+    // them with PWG_CNET_OPT_NARROW 2): the widest tile (waves, m-tiles) that gives every CU one
+    // workgroup, else the narrowest
+    p->nar_nwv[pi] = p->nar_mt[pi] = p->nar_lds[pi] = 0;
+    const bool xt_family = !ph.thin && op.kind != PWG_CNET_PQMF && (ph.xtile || ph.xt_convt_db) &&
+                           ph.z_phases > 0 && ph.MT >= 1;
+    const bool convt_ = op.kind == PWG_CNET_CONVT;
+    if (n->narrow && xt_family && (convt_ || (op.src[0].taps - 1) * op.src[0].dilation <= NARROW_HALO)) {
+      const bool convt = convt_;
+      const int xk = convt ? 2 : op.src[0].taps, xd = convt ? 1 : op.src[0].dilation;
+      const long long zn = ph.z_phases;
+      long long base = 0;
+      if (ph.xpair_b >= 0 || (ph.stack_b >= 0 && ph.xtile)) base = (long long)h_xblocks[pi].size();
+      else if (ph.xt_convt_db) base = (long long)h_xblocks[pi].size() * (ph.mt_total / ph.MT) * zn;
+      else base = (long long)blocks.size() * (ph.mt_total / ph.MT) * zn;
+      if (n->narrow == 2 || base < p->n_cu) {
+        int pick_w = 1, pick_m = 1;
+        bool found = false;
+        for (int w : {4, 2, 1}) {
+          for (int mtn : {2, 1}) {
+            if (mtn == 2 && ph.mt_total % 2 != 0) continue;
+            long long nwg = 0;
+            for (int u = 0; u < n_utts; ++u) nwg += (ncols[u] + 32 * w - 1) / (32 * w);
+            nwg *= (ph.mt_total / mtn) * zn;
+            if (nwg >= p->n_cu) {
+              pick_w = w;
+              pick_m = mtn;
+              found = true;
+              break;
+            }
+          }
+          if (found) break;
+        }
+        const int span = 32 * pick_w + (xk - 1) * xd;
+        p->nar_nwv[pi] = pick_w;
+        p->nar_mt[pi] = pick_m;
+        p->nar_lds[pi] = 2 * narrow_ks(xk) * pick_m * 2048 + span * XT_ROWB;
+        for (int u = 0; u < n_utts; ++u)
+          for (int q0 = 0; q0 < ncols[u]; q0 += 32 * pick_w) h_nblocks[pi].push_back(make_int2(u, q0));
+      }
+    }
     // every list: utterance in range, first column inside it
-    for (const std::vector<int2>* lst : {&blocks, &h_strips[pi], &h_xblocks[pi]})
+    for (const std::vector<int2>* lst : {&blocks, &h_strips[pi], &h_xblocks[pi], &h_nblocks[pi]})
       for (const int2& b : *lst) {
         if (b.x < 0 || b.x >= n_utts || b.y < 0) return bad_list(pi, "block outside the batch");
         const long long lim = op.kind == PWG_CNET_PQMF ? frames[b.x] * n->rate[op.dst] : ncols[b.x];
@@ -3162,6 +3258,8 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
       p->n_strips.push_back((int)h_strips[pi].size());
       p->d_xblocks.push_back(nullptr);
       p->n_xblocks.push_back((int)h_xblocks[pi].size());
+      p->d_nblocks.push_back(nullptr);
+      p->n_nblocks.push_back((int)h_nblocks[pi].size());
     }
     *out = p;
     return PWG_OK;
@@ -3208,6 +3306,10 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
     upload(h_xblocks[pi], &dxb);
     p->d_xblocks.push_back(dxb);
     p->n_xblocks.push_back((int)h_xblocks[pi].size());
+    int2* dnb = nullptr;
+    upload(h_nblocks[pi], &dnb);
+    p->d_nblocks.push_back(dnb);
+    p->n_nblocks.push_back((int)h_nblocks[pi].size());
   }
   if (e != hipSuccess) {
     const int rc = hipf(e, "cnet plan upload");
@@ -3230,6 +3332,7 @@ void pwg_cnet_plan_destroy(PwgCnetPlan* p) {
   for (auto* x : p->d_ncols) if (x) (void)hipFree(x);
   for (auto* x : p->d_strips) if (x) (void)hipFree(x);
   for (auto* x : p->d_xblocks) if (x) (void)hipFree(x);
+  for (auto* x : p->d_nblocks) if (x) (void)hipFree(x);
   delete p;
 }
 
@@ -3267,14 +3370,18 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
   }
   // a conv pair runs fused unless its convs run on the x-tile kernel (measured faster unfused)
   auto pair_fused = [&](const OpPhase& q) { return fuse && q.pair_b >= 0 && !(xt && q.xtile); };
+  // narrow x-tile launch of phase i (plan time; x-tile mode only): an x-tile pair or stack whose
+  // first conv runs narrow runs unfused (its second op as its own launch)
+  auto narrow = [&](size_t i) { return xt && p->nar_nwv[i] > 0; };
   for (size_t pi = 0; pi < n->phases.size(); ++pi) {
     const OpPhase& ph = n->phases[pi];
     const PwgCnetOp& op = n->ops[ph.op];
     if (pi > 0 && ((pair_fused(n->phases[pi - 1]) && n->phases[pi - 1].pair_b == (int)pi) ||
-                   (fuse && n->phases[pi - 1].stack_b == (int)pi)))
+                   (fuse && n->phases[pi - 1].stack_b == (int)pi && !narrow(pi - 1))))
       continue;  // ran inside the fused pair / stack
     if (ph.z_phases == 0) continue;  // ran in its ConvTranspose's one launch
-    if (xt && fuse && pi > 0 && n->phases[pi - 1].xpair_b == (int)pi) continue;  // ran in the x-tile pair
+    if (xt && fuse && pi > 0 && n->phases[pi - 1].xpair_b == (int)pi && !narrow(pi - 1))
+      continue;  // ran in the x-tile pair
     hipEvent_t ea = nullptr, eb = nullptr;
     if (n->timing) {
       for (hipEvent_t* ev : {&ea, &eb}) {
@@ -3319,7 +3426,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         else
           hipLaunchKernelGGL((pwg_cnet_pair_stream_kernel<4, 2, 2>), pgrid, dim3(256), (size_t)ph.pair_lds, s, a);
       }
-    } else if (fuse && ph.stack_b >= 0) {
+    } else if (fuse && ph.stack_b >= 0 && !narrow(pi)) {
       if (p->n_blocks[pi] > 0) {
         const bool xs_on = xt && ph.xtile;
         const OpPhase& pb = n->phases[ph.stack_b];
@@ -3428,7 +3535,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         else if (op.out_channels <= 4) hipLaunchKernelGGL(pwg_cnet_thin_kernel<4>, tgrid, tblock, tl, s, a, nsrc);
         else hipLaunchKernelGGL(pwg_cnet_thin_kernel<8>, tgrid, tblock, tl, s, a, nsrc);
       } else
-      if (xt && fuse && ph.xpair_b >= 0) {
+      if (xt && fuse && ph.xpair_b >= 0 && !narrow(pi)) {
         const OpPhase& pb = n->phases[ph.xpair_b];
         const PwgCnetOp& opb = n->ops[pb.op];
         CnXpairArgs xp;
@@ -3461,11 +3568,20 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
           a.blocks = p->d_xblocks[pi];
           xgrid.x = (unsigned)p->n_xblocks[pi];
         }
-        const bool db = ph.xt_convt_db ||
-                        (ph.xt_db && ((n->xt_dma & CNET_DMA_ALL) || ((n->xt_dma & CNET_DMA_RULE) && ph.xt_db_pick)));
-        const int dv = (n->xt_dma & CNET_DMA_FEWEST) ? 1 : 0;
-        const hipError_t ea2 = db ? xtile_launch(ph.MT, xt.K, false, ph.xt_db_ks[dv], xgrid, ph.xt_db_lds[dv], s, a, xt, true)
-                                  : xtile_launch(ph.MT, xt.K, ph.xt_sync, ph.xt_ks, xgrid, ph.xt_lds, s, a, xt);
+        hipError_t ea2;
+        if (narrow(pi)) {
+          const int nw = p->nar_nwv[pi], mtn = p->nar_mt[pi];
+          xt.span = 32 * nw + (xt.K - 1) * xt.dil;
+          a.blocks = p->d_nblocks[pi];
+          const dim3 ngrid((unsigned)p->n_nblocks[pi], (unsigned)(ph.mt_total / mtn), (unsigned)ph.z_phases);
+          ea2 = p->n_nblocks[pi] > 0 ? xtile_launch_narrow(mtn, nw, xt.K, ngrid, p->nar_lds[pi], s, a, xt) : hipSuccess;
+        } else {
+          const bool db = ph.xt_convt_db ||
+                          (ph.xt_db && ((n->xt_dma & CNET_DMA_ALL) || ((n->xt_dma & CNET_DMA_RULE) && ph.xt_db_pick)));
+          const int dv = (n->xt_dma & CNET_DMA_FEWEST) ? 1 : 0;
+          ea2 = db ? xtile_launch(ph.MT, xt.K, false, ph.xt_db_ks[dv], xgrid, ph.xt_db_lds[dv], s, a, xt, true)
+                   : xtile_launch(ph.MT, xt.K, ph.xt_sync, ph.xt_ks, xgrid, ph.xt_lds, s, a, xt);
+        }
         if (ea2 != hipSuccess) return hipf(ea2, "xtile kernel launch");
       } else if (split) {
         switch (ph.MT) {
@@ -3547,6 +3663,11 @@ int pwg_cnet_set_option(PwgCnet* n, int option, long long value) {
   if (option == PWG_CNET_OPT_PAIR_STEPS) {
     if (value < 1 || value > 4096) return fail(PWG_ERR_INVALID, "pair_steps must be in [1, 4096]");
     n->pair_steps = (int)value;
+    return PWG_OK;
+  }
+  if (option == PWG_CNET_OPT_NARROW) {
+    if (value < 0 || value > 2) return fail(PWG_ERR_INVALID, "narrow must be 0, 1 or 2");
+    n->narrow = (int)value;
     return PWG_OK;
   }
   int* slot = option == PWG_CNET_OPT_SPLIT_F16   ? &n->split_f16

@@ -178,3 +178,71 @@ def gather_outputs(local, n_utts, dst=0):
     if len(merged) != n_utts:
         raise RuntimeError(f"gathered {len(merged)} of {n_utts} utterances")
     return [merged[i] for i in range(n_utts)]
+
+
+def long_utterance_ranges(frames, world, halo, hop, causal=False):
+    """one very long utterance split over ``world`` ranks in time. Returns one
+    (lo, s, e, hi) frame range per rank: the rank computes frames [lo, hi) (its core [s, e) plus
+    ``halo`` frames of recomputed context, left only when causal) and keeps the core. Cores are
+    ceil(frames / world) frames rounded up to the engine's chunk alignment (streaming.align_frames:
+    a chunk that starts off the 32-sample block phase sums in another order), and ``lo`` is rounded
+    down to it, so the concatenated cores are BIT-IDENTICAL to one whole-utterance run. Ranks past
+    the end get an empty core (s == e)."""
+    from .streaming import align_frames
+
+    align = align_frames(hop)
+    per = -(-int(frames) // int(world))
+    per = -(-per // align) * align
+    out = []
+    for r in range(int(world)):
+        s = min(int(frames), r * per)
+        e = min(int(frames), s + per)
+        lo = max(0, (s - halo) // align * align)
+        hi = e if causal else min(int(frames), e + halo)
+        out.append((lo, s, e, hi))
+    return out
+
+
+def decode_long_sharded(engine, mel, noise, rank=None, world=None, halo=None, mean=None, scale=None):
+    """One long utterance decoded by every rank together (SURVEY.md sec 8(e) "split time into P
+    chunks whose inputs overlap by the receptive halo... no exchange" on the input side): each rank
+    runs its core plus recomputed halos (long_utterance_ranges) on its own GPU, then the cores are
+    all-gathered (RCCL on the nccl backend: the one data-path collective of this path, 4 B per
+    output sample over xGMI) and every rank returns the whole (T, out_channels) waveform,
+    bit-identical to ``engine.infer([mel], [noise])``. ``engine`` is an Engine (or anything with its
+    ``infer``, ``upsample_factor``, ``config``); mel (T', A) and noise (T,) live on the rank's device
+    (every rank holds the whole input, as every rank reads its own input in bin/decode.py)."""
+    from .streaming import halo_frames
+
+    init = dist.is_available() and dist.is_initialized()
+    if rank is None or world is None:
+        rank = dist.get_rank() if init else 0
+        world = dist.get_world_size() if init else 1
+    H = int(engine.upsample_factor)
+    O = int(engine.config.out_channels)
+    F = int(mel.shape[0])
+    noise = noise.reshape(-1)
+    if noise.numel() != F * H:
+        raise ValueError("noise must have frames * upsample_factor samples")
+    causal = bool(engine.config.use_causal_conv)
+    halo = halo_frames(engine) if halo is None else int(halo)
+    ranges = long_utterance_ranges(F, world, halo, H, causal)
+    per = max(e - s for _, s, e, _ in ranges)
+    lo, s, e, hi = ranges[rank]
+    piece = torch.zeros(per * H * O, dtype=torch.float32, device=mel.device)
+    if e > s:
+        y = engine.infer([mel[lo:hi].contiguous()], [noise[lo * H:hi * H].contiguous()], mean, scale)[0]
+        piece[:(e - s) * H * O] = y[(s - lo) * H:(e - lo) * H].reshape(-1)
+    if world == 1 or not init:
+        parts = [piece]
+    elif dist.get_backend() == "gloo":
+        host = piece.cpu()
+        parts = [torch.empty_like(host) for _ in range(world)]
+        dist.all_gather(parts, host)
+        parts = [p.to(mel.device) for p in parts]
+    else:
+        flat = torch.empty(world * piece.numel(), dtype=torch.float32, device=mel.device)
+        dist.all_gather_into_tensor(flat, piece)
+        parts = list(flat.view(world, -1))
+    out = torch.cat([p[:(e_ - s_) * H * O] for p, (_, s_, e_, _) in zip(parts, ranges)])
+    return out.view(F * H, O)

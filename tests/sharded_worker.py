@@ -5,7 +5,9 @@ multi-GPU decode path on the HIP engine, launched by the test as
 Ranks share cuda:0 (the test box has one GPU), so the process group is gloo: rank 0 packs the
 generator weights, broadcast_packed_weights ships the image, every rank decodes its LPT shard of
 a ragged LibriTTS v1 utterance list with Engine.infer (one ragged plan per rank), and rank 0
-gathers the outputs (utterance order) into OUT/sharded.npz with the per-rank shards and loads."""
+gathers the outputs (utterance order) into OUT/sharded.npz with the per-rank shards and loads.
+Then both ranks decode ONE long utterance together (sharding.decode_long_sharded: a core each,
+recomputed halos, all-gather of the cores) and each saves the whole waveform to OUT/long<rank>.npy."""
 
 import os
 import sys
@@ -20,6 +22,7 @@ sys.path.insert(0, REPO)
 from parallelwavegan_amd import Engine, configs, sharding, synthetic  # noqa: E402
 
 LENGTHS = [143, 17, 600, 88, 1, 250, 311, 45, 90]
+LONG = 3001  # frames of the utterance split in time across the ranks (37.5 s at 24 kHz)
 
 
 def inputs(i, f):
@@ -57,6 +60,9 @@ def main():
         arrays["loads"] = np.array(sharding.shard_loads(LENGTHS, shards))
         arrays["rank0"] = np.array(shards[0])
         np.savez(os.path.join(out_dir, "sharded.npz"), **arrays)
+    m, n = inputs(99, LONG)
+    y = sharding.decode_long_sharded(eng, torch.from_numpy(m).to(dev), torch.from_numpy(n).to(dev))
+    np.save(os.path.join(out_dir, f"long{rank}.npy"), y.cpu().numpy())
     dist.barrier()
     dist.destroy_process_group()
 

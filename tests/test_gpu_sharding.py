@@ -4,7 +4,8 @@ test_sharded_decode_two_ranks: two fresh child processes (torch.distributed.run,
 test as a subprocess) share cuda:0 over gloo, broadcast rank 0's packed weights, decode their LPT
 shards of a ragged LibriTTS v1 list and gather on rank 0; the result must be bit-identical to one
 single-process ragged decode of the whole list (utterances are independent and the engine's
-segment padding isolates them).
+segment padding isolates them); and one long utterance split in time over the
+two ranks (sharding.decode_long_sharded) must equal its unsplit decode bit for bit.
 
 test_rccl_broadcast_capi: the C-ABI RCCL path (pwg_rccl_unique_id / pwg_rccl_comm_create /
 pwg_broadcast_weights) in a one-rank process group: the image arrives intact and decodes as the
@@ -59,6 +60,12 @@ def test_sharded_decode_two_ranks(built_lib, cuda_device, tmp_path):
     ref = [y.cpu().numpy() for y in eng.infer(mels, noises)]
     for i, y in enumerate(ref):
         np.testing.assert_array_equal(got[f"y{i}"], y)
+    # one long utterance split in time over the two ranks: every rank ends
+    # with the whole waveform, bit-identical to one unsplit decode
+    m, n = w.inputs(99, w.LONG)
+    ref_long = eng.infer([torch.from_numpy(m).to(cuda_device)], [torch.from_numpy(n).to(cuda_device)])[0].cpu().numpy()
+    for r in range(2):
+        np.testing.assert_array_equal(np.load(os.path.join(tmp_path, f"long{r}.npy")), ref_long)
 
 
 def test_rccl_broadcast_capi(built_lib, cuda_device):

@@ -127,6 +127,7 @@ def test_xtile_pairs_bitwise_equal_to_unfused(causal, built_lib, cuda_device):
     m.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic.make_module_state_dict(m, seed=4).items()})
     m = m.to(cuda_device)
     eng = m.engine()
+    eng.set_narrow(0)  # the default (8-wave) launches themselves, not their small-plan form
     mels = [synthetic.make_mel(f, 80, seed=90 + i) for i, f in enumerate([3, 1, 14, 5])]
     with torch.no_grad():
         eng.set_fuse_pairs(False)
@@ -223,6 +224,7 @@ def test_fused_residual_stacks_bitwise_equal_to_unfused(cfg, xtile, built_lib, c
         m.pqmf = PQMF(**configs.VOCODER_PQMF[cfg])
     m = m.to(cuda_device)
     eng = m.engine()
+    eng.set_narrow(0)  # the default (8-wave) launches themselves, not their small-plan form
     eng.set_xtile(xtile)  # off: conv A unfused on the tap-major kernel; on: on the x-tile kernel
     mels = [synthetic.make_mel(f, 80, seed=70 + i) for i, f in enumerate([9, 40, 7, 23, 300])]
     with torch.no_grad():
@@ -289,6 +291,7 @@ def test_xtile_dma_staging_bitwise_equal(cfg, built_lib, cuda_device):
         m.pqmf = PQMF(**configs.VOCODER_PQMF[cfg])
     m = m.to(cuda_device)
     eng = m.engine()
+    eng.set_narrow(0)  # the default (8-wave) launches themselves, not their small-plan form
     mels = [synthetic.make_mel(f, 80, seed=120 + i) for i, f in enumerate([4, 5, 37, 9, 130])]
     C = CnetEngine
     outs = {}
@@ -322,6 +325,7 @@ def test_xcd_tile_order_bitwise_equal(cfg, built_lib, cuda_device):
         m.pqmf = PQMF(**configs.VOCODER_PQMF[cfg])
     m = m.to(cuda_device)
     eng = m.engine()
+    eng.set_narrow(0)  # the default (8-wave) launches themselves, not their small-plan form
     mels = [synthetic.make_mel(f, 80, seed=140 + i) for i, f in enumerate([7, 61, 4, 23, 150])]
     with torch.no_grad():
         for dma in (0, 9):
@@ -333,3 +337,35 @@ def test_xcd_tile_order_bitwise_equal(cfg, built_lib, cuda_device):
             for a, b in zip(*outs):
                 np.testing.assert_array_equal(a, b)
         eng.set_xt_dma(9)
+
+
+@pytest.mark.parametrize("cfg", ["hifigan_v1", "melgan_v1", "mb_melgan_v2", "hifigan_v1_causal", "mb_melgan_v2_causal"])
+def test_narrow_launches_bitwise_equal(cfg, built_lib, cuda_device):
+    """PWG_CNET_OPT_NARROW (the B = 1 path): x-tile launches with fewer workgroups than CUs run
+    1-4-wave, 1-2-m-tile workgroups, and the fused x-tile pairs / stacks whose first conv does run
+    as their two ops. Every column sums the same products in the same order, so the output is
+    bit-identical to the default launches: narrow off (0), automatic (1: the short utterance alone
+    and the ragged batch pick different launches) and forced on every x-tile launch (2)."""
+    from parallelwavegan_amd import configs, synthetic
+    from parallelwavegan_amd.hifigan import HiFiGANGenerator
+    from parallelwavegan_amd.melgan import PQMF, MelGANGenerator
+
+    cls_name, params = configs.vocoder_params(cfg)
+    m = {"MelGANGenerator": MelGANGenerator, "HiFiGANGenerator": HiFiGANGenerator}[cls_name](**params)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic.make_module_state_dict(m, seed=9).items()})
+    if cfg in configs.VOCODER_PQMF:
+        m.pqmf = PQMF(**configs.VOCODER_PQMF[cfg])
+    m = m.to(cuda_device)
+    eng = m.engine()
+    mels = [synthetic.make_mel(f, 80, seed=150 + i) for i, f in enumerate([64, 9, 23, 131])]
+    with torch.no_grad():
+        outs = {}
+        for mode in (0, 1, 2):
+            eng.set_narrow(mode)
+            outs[mode] = ([m.inference(torch.from_numpy(mels[0]).to(cuda_device)).cpu().numpy()] +
+                          [y.cpu().numpy() for y in m.inference_batch(mels)])
+        eng.set_narrow(1)
+    for mode in (1, 2):
+        for a, b in zip(outs[mode], outs[0]):
+            assert np.isfinite(a).all()
+            np.testing.assert_array_equal(a, b)

@@ -100,3 +100,66 @@ def test_world2_gloo_broadcast_decode_gather(tmp_path, built_lib):
     world = 2
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     assert (tmp_path / "ok").exists()
+
+
+def test_long_utterance_ranges_partition_and_align():
+    """Cores of one long utterance partition [0, F) in rank order, chunk starts sit on the
+    engine's alignment (hop 300: 8 frames), halos cover at least ``halo`` frames where the
+    utterance allows, causal chunks have no right halo; more ranks than cores leave empty ranks."""
+    for F, world, hop, causal in ((1000, 2, 300, False), (1000, 8, 300, True), (9, 4, 256, False),
+                                  (5, 8, 300, False), (60000, 8, 256, False)):
+        halo = 14
+        rng = sharding.long_utterance_ranges(F, world, halo, hop, causal)
+        assert len(rng) == world
+        align = 32 // np.gcd(hop, 32)
+        pos = 0
+        for lo, s, e, hi in rng:
+            assert s == pos and e >= s
+            pos = e
+            assert lo % align == 0 and lo <= max(0, s - halo)
+            assert hi == (e if causal else min(F, e + halo))
+        assert pos == F
+
+
+def _long_worker(rank, world, port, result_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import pwg_numpy  # test infrastructure: stands in for the GPU engine
+        from parallelwavegan_amd import HostHandle, configs, synthetic
+
+        params = configs.generator_params("yesno_debug")
+        host = HostHandle(params)
+        sd = synthetic.make_state_dict(params, seed=0)
+
+        class OracleEngine:
+            config = host.config
+            receptive_field_size = host.receptive_field_size
+            upsample_factor = host.upsample_factor
+
+            @staticmethod
+            def infer(mels, noises, mean=None, scale=None):
+                return [torch.from_numpy(pwg_numpy.inference(m.numpy(), z.numpy(), sd, params).astype(np.float32))
+                        for m, z in zip(mels, noises)]
+
+        F, H = 37, host.upsample_factor
+        mel = torch.from_numpy(synthetic.make_mel(F, 80, seed=5))
+        noise = torch.from_numpy(synthetic.make_noise(F * H, seed=6)).reshape(-1)
+        y = sharding.decode_long_sharded(OracleEngine, mel, noise)
+        ref = OracleEngine.infer([mel], [noise])[0]
+        assert y.shape == ref.shape
+        np.testing.assert_allclose(y.numpy(), ref.numpy(), rtol=0, atol=1e-6)
+        open(os.path.join(result_dir, f"ok{rank}"), "w").write("ok")
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_world2_gloo_long_utterance_split(tmp_path, built_lib):
+    """decode_long_sharded on two gloo ranks (the NumPy oracle standing in for each rank's GPU
+    engine): each rank computes its core with recomputed halos, the cores are all-gathered, and
+    every rank holds the whole waveform, equal to the unsplit decode."""
+    world = 2
+    mp.spawn(_long_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    assert (tmp_path / "ok0").exists() and (tmp_path / "ok1").exists()
