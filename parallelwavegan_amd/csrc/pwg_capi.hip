@@ -7,7 +7,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/pwg.h"
@@ -1460,4 +1463,23 @@ int pwg_timing_collect(PwgHandle* h, double* ms, long long* launches) {
 namespace pwg {
 // shared with pwg_cnet.hip: one thread-local last-error message for the whole library
 int set_error(int code, const char* msg) { return fail(code, msg); }
+
+hipError_t allow_lds(const void* kfn, int lds) {
+  static std::mutex mu;
+  static std::map<std::pair<int, const void*>, int> done;  // (device, kernel) -> largest size allowed
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = done.find({dev, kfn});
+    if (it != done.end() && it->second >= lds) return hipSuccess;
+  }
+  const hipError_t e = hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (e == hipSuccess) {
+    std::lock_guard<std::mutex> lk(mu);
+    int& v = done[{dev, kfn}];
+    v = std::max(v, lds);
+  }
+  return e;
+}
 }  // namespace pwg

@@ -48,6 +48,8 @@ constexpr int CN_MAX_CHUNKS = 4096;
 // round 3: two chunks per barrier, two column tiles per wave, 512-column x-tile workgroups, 2/4
 // channel blocks per staging step, two-deep load rings, explicit waves-per-SIMD requests).
 constexpr int CN_G = 1;                    // 16-channel chunks staged per barrier (2: 9 % slower)
+constexpr int CN_NARROW_G = 4;             // ... in narrow tap-major launches (small plans: fewer, longer
+                                           // steps between barriers; same product order)
 constexpr int CNET_NW8_MT = 4;             // conv ops with MT >= this run 8-wave workgroups (256 columns)
 constexpr int CNET_XTILE_LDS = 150 * 1024; // LDS budget of one x-tile workgroup
 constexpr int CNET_XPAIR_MAXK = 11;        // largest kernel size fused into an x-tile pair
@@ -237,14 +239,17 @@ __global__ void __launch_bounds__(64 * NW) pwg_cnet_conv_kernel(const CnConvArgs
   };
   // (G chunks are staged per barrier; the host pads the chunk list to a multiple of G with
   // zero-weight chunks)
+  // (narrow launches, G > 1: the last group may be partial; its missing chunks load nothing and
+  // run no MFMAs, so every accumulator sees the same product sequence as with G = 1)
   auto aload = [&](int cg, f32x4v (&r)[G][AQ]) {
 #pragma unroll
     for (int g2 = 0; g2 < G; ++g2) {
-      const f32x4v* gp = reinterpret_cast<const f32x4v*>(wfrag_ + ((size_t)(cg * G + g2) * a.mt_total + m0) * 512);
+      const bool live = G == 1 || cg * G + g2 < a.n_chunks;
+      const f32x4v* gp = reinterpret_cast<const f32x4v*>(wfrag_ + ((size_t)(live ? cg * G + g2 : 0) * a.mt_total + m0) * 512);
 #pragma unroll
       for (int i = 0; i < AQ; ++i) {
         const int idx = threadIdx.x + NTH * i;
-        r[g2][i] = idx < MT * 128 ? gp[idx] : f32x4v{0.f, 0.f, 0.f, 0.f};
+        r[g2][i] = idx < MT * 128 && live ? gp[idx] : f32x4v{0.f, 0.f, 0.f, 0.f};
       }
     }
   };
@@ -269,9 +274,10 @@ __global__ void __launch_bounds__(64 * NW) pwg_cnet_conv_kernel(const CnConvArgs
       for (int r = 0; r < 16; ++r) acc[m][n][r] = 0.f;
 
   // one chunk group's MFMAs from LDS buffer buf and the prepared B operands
-  auto compute = [&](int buf, const f32x8v (&bc)[G][NT]) {
+  auto compute = [&](int buf, const f32x8v (&bc)[G][NT], int n_live) {
 #pragma unroll
     for (int g2 = 0; g2 < G; ++g2) {
+      if (G > 1 && g2 >= n_live) break;
       if constexpr (SPLIT) {
         const u32x4v* sa = reinterpret_cast<const u32x4v*>(s_a[buf] + g2 * MT * 512) + lane;
         u32x4v bh[NT], bl[NT];
@@ -313,7 +319,8 @@ __global__ void __launch_bounds__(64 * NW) pwg_cnet_conv_kernel(const CnConvArgs
     }
   };
 
-  const int n_groups = a.n_chunks / G;
+  const int n_groups = (a.n_chunks + G - 1) / G;
+  auto cmin = [&](int c) { return c < a.n_chunks ? c : a.n_chunks - 1; };  // partial group: in-bounds reads
   f32x8v bcur[G][NT];
   f32x4v ar[G][AQ];
   aload(0, ar);
@@ -321,7 +328,7 @@ __global__ void __launch_bounds__(64 * NW) pwg_cnet_conv_kernel(const CnConvArgs
   BRaw bnext[G];
 #pragma unroll
   for (int g2 = 0; g2 < G; ++g2) {
-    braw(g2, bnext[g2]);
+    braw(cmin(g2), bnext[g2]);
     bprep(bnext[g2], bcur[g2]);
   }
   __syncthreads();
@@ -330,10 +337,10 @@ __global__ void __launch_bounds__(64 * NW) pwg_cnet_conv_kernel(const CnConvArgs
     if (more) {
       aload(cg + 1, ar);
 #pragma unroll
-      for (int g2 = 0; g2 < G; ++g2) braw((cg + 1) * G + g2, bnext[g2]);
+      for (int g2 = 0; g2 < G; ++g2) braw(cmin((cg + 1) * G + g2), bnext[g2]);
     }
     __builtin_amdgcn_sched_barrier(0);  // keep the loads issued before the MFMAs below
-    compute(cg & 1, bcur);
+    compute(cg & 1, bcur, a.n_chunks - cg * G);
     __builtin_amdgcn_sched_barrier(0);  // ... and their consumers after them
     if (more) astore((cg + 1) & 1, ar);
     __syncthreads();
@@ -798,8 +805,7 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
 
 template <int MT, int K, int CB, int NC = 1, bool SY = false, int KS = K, bool DB = false>
 hipError_t xtile_launch_k(dim3 grid, int lds, hipStream_t s, const CnConvArgs& a, const CnXtileArgs& xt) {
-  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(pwg_cnet_xtile_kernel<MT, K, CB, NC, SY, KS, DB>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  const hipError_t e = allow_lds(reinterpret_cast<const void*>(pwg_cnet_xtile_kernel<MT, K, CB, NC, SY, KS, DB>), lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((pwg_cnet_xtile_kernel<MT, K, CB, NC, SY, KS, DB>), grid, dim3(512), (size_t)lds, s, a, xt);
   return hipGetLastError();
@@ -913,7 +919,7 @@ constexpr int narrow_ks(int k) { return k <= 3 ? k : (k == 5 ? 3 : 4); }
 template <int MT, int NWV>
 hipError_t xtile_launch_narrow_mt(int k, dim3 grid, int lds, hipStream_t s, const CnConvArgs& a, const CnXtileArgs& xt) {
   auto go = [&](auto kfn) -> hipError_t {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    const hipError_t e = allow_lds(reinterpret_cast<const void*>(kfn), lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kfn, grid, dim3(64 * NWV), (size_t)lds, s, a, xt);
     return hipGetLastError();
@@ -1208,8 +1214,7 @@ __global__ void __launch_bounds__(512) pwg_cnet_xpair_kernel(const CnConvArgs a,
 
 template <int MT, int K1, int K2>
 hipError_t xpair_launch_k(dim3 grid, int lds, hipStream_t s, const CnConvArgs& a, const CnXpairArgs& xp) {
-  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(pwg_cnet_xpair_kernel<MT, K1, K2>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  const hipError_t e = allow_lds(reinterpret_cast<const void*>(pwg_cnet_xpair_kernel<MT, K1, K2>), lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((pwg_cnet_xpair_kernel<MT, K1, K2>), grid, dim3(512), (size_t)lds, s, a, xp);
   return hipGetLastError();
@@ -1770,8 +1775,7 @@ __global__ void __launch_bounds__(512) pwg_cnet_xstack_kernel(const CnStackArgs 
 
 template <int MT, int K1>
 hipError_t xstack_launch_k(dim3 grid, int lds, hipStream_t s, const CnStackArgs& a, const CnXstackArgs& xs) {
-  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(pwg_cnet_xstack_kernel<MT, K1>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  const hipError_t e = allow_lds(reinterpret_cast<const void*>(pwg_cnet_xstack_kernel<MT, K1>), lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((pwg_cnet_xstack_kernel<MT, K1>), grid, dim3(512), (size_t)lds, s, a, xs);
   return hipGetLastError();
@@ -2538,6 +2542,7 @@ struct PwgCnetPlan {
   int n_cu = 0;                              // CUs of the device (plan-time launch sizing)
   // per phase: narrow x-tile launch (PWG_CNET_OPT_NARROW), 0 waves = the phase's default launch
   std::vector<int> nar_nwv, nar_mt, nar_lds, n_nblocks;
+  std::vector<char> nar_tap;                 // ... on the tap-major kernel (not the x-tile family)
   std::vector<int2*> d_nblocks;              // its blocks (utt, q0 step 32 nar_nwv)
 };
 
@@ -3152,6 +3157,7 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
   p->nar_nwv.assign(nph, 0);
   p->nar_mt.assign(nph, 0);
   p->nar_lds.assign(nph, 0);
+  p->nar_tap.assign(nph, 0);
   p->n_cu = 256;  // host-only handles size for an MI355X
   if (n->device >= 0) {
     int cu = 0;
@@ -3235,6 +3241,40 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
         p->nar_nwv[pi] = pick_w;
         p->nar_mt[pi] = pick_m;
         p->nar_lds[pi] = 2 * narrow_ks(xk) * pick_m * 2048 + span * XT_ROWB;
+        for (int u = 0; u < n_utts; ++u)
+          for (int q0 = 0; q0 < ncols[u]; q0 += 32 * pick_w) h_nblocks[pi].push_back(make_int2(u, q0));
+      }
+    }
+    // narrow tap-major launch (split-f16 convs outside the x-tile family, e.g. MelGAN's two-source
+    // 1x1s; not the fused tap-major pairs / stacks): 1-2 waves, 1-2 m-tiles, CN_NARROW_G chunks per
+    // barrier
+    const bool tap_family = !xt_family && !ph.thin && op.kind != PWG_CNET_PQMF && ph.z_phases > 0 &&
+                            ph.pair_b < 0 && !(pi > 0 && n->phases[pi - 1].pair_b == (int)pi) && ph.stack_b < 0 &&
+                            !ph.xt_convt_db;
+    if (n->narrow && tap_family) {
+      const long long zn = ph.z_phases;
+      const long long base = (long long)blocks.size() * (ph.mt_total / ph.MT) * zn;
+      if (n->narrow == 2 || base < p->n_cu) {
+        int pick_w = 1, pick_m = 1;
+        bool found = false;
+        for (int w : {2, 1}) {
+          for (int mtn : {2, 1}) {
+            if (mtn == 2 && ph.mt_total % 2 != 0) continue;
+            long long nwg = 0;
+            for (int u = 0; u < n_utts; ++u) nwg += (ncols[u] + 32 * w - 1) / (32 * w);
+            nwg *= (ph.mt_total / mtn) * zn;
+            if (nwg >= p->n_cu) {
+              pick_w = w;
+              pick_m = mtn;
+              found = true;
+              break;
+            }
+          }
+          if (found) break;
+        }
+        p->nar_nwv[pi] = pick_w;
+        p->nar_mt[pi] = pick_m;
+        p->nar_tap[pi] = 1;
         for (int u = 0; u < n_utts; ++u)
           for (int q0 = 0; q0 < ncols[u]; q0 += 32 * pick_w) h_nblocks[pi].push_back(make_int2(u, q0));
       }
@@ -3372,7 +3412,8 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
   auto pair_fused = [&](const OpPhase& q) { return fuse && q.pair_b >= 0 && !(xt && q.xtile); };
   // narrow x-tile launch of phase i (plan time; x-tile mode only): an x-tile pair or stack whose
   // first conv runs narrow runs unfused (its second op as its own launch)
-  auto narrow = [&](size_t i) { return xt && p->nar_nwv[i] > 0; };
+  auto narrow = [&](size_t i) { return xt && p->nar_nwv[i] > 0 && !p->nar_tap[i]; };
+  auto narrow_tap = [&](size_t i) { return n->split_f16 && p->nar_nwv[i] > 0 && p->nar_tap[i]; };
   for (size_t pi = 0; pi < n->phases.size(); ++pi) {
     const OpPhase& ph = n->phases[pi];
     const PwgCnetOp& op = n->ops[ph.op];
@@ -3411,7 +3452,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
                                  reinterpret_cast<const void*>(pwg_cnet_pair_stream_kernel<1, 4, PR_SG>),
                                  reinterpret_cast<const void*>(pwg_cnet_pair_stream_kernel<2, 4, PR_SG>),
                                  reinterpret_cast<const void*>(pwg_cnet_pair_stream_kernel<4, 2, 2>)}) {
-            const hipError_t ea2 = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, PR_MAX_LDS);
+            const hipError_t ea2 = allow_lds(kf, PR_MAX_LDS);
             if (ea2 != hipSuccess) return hipf(ea2, "pair kernel LDS attribute");
           }
           n->pair_attr_set = true;
@@ -3469,7 +3510,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
           case 6: kf = reinterpret_cast<const void*>(pwg_cnet_stack_kernel<6>); break;
           default: kf = reinterpret_cast<const void*>(pwg_cnet_stack_kernel<7>); break;
         }
-        const hipError_t ea2 = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, ph.stack_lds);
+        const hipError_t ea2 = allow_lds(kf, ph.stack_lds);
         if (ea2 != hipSuccess) return hipf(ea2, "stack kernel LDS attribute");
         const dim3 sgrid((unsigned)p->n_blocks[pi]);
         switch (ph.mt_total) {
@@ -3583,6 +3624,14 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
                    : xtile_launch(ph.MT, xt.K, ph.xt_sync, ph.xt_ks, xgrid, ph.xt_lds, s, a, xt);
         }
         if (ea2 != hipSuccess) return hipf(ea2, "xtile kernel launch");
+      } else if (split && narrow_tap(pi)) {
+        a.blocks = p->d_nblocks[pi];
+        const int nw = p->nar_nwv[pi], mtn = p->nar_mt[pi];
+        const dim3 ngrid((unsigned)p->n_nblocks[pi], (unsigned)(ph.mt_total / mtn), (unsigned)ph.z_phases);
+        if (mtn == 1 && nw == 1) hipLaunchKernelGGL((pwg_cnet_conv_kernel<1, 1, CN_NARROW_G, true, 1>), ngrid, dim3(64), 0, s, a);
+        else if (mtn == 1) hipLaunchKernelGGL((pwg_cnet_conv_kernel<1, 1, CN_NARROW_G, true, 2>), ngrid, dim3(128), 0, s, a);
+        else if (nw == 1) hipLaunchKernelGGL((pwg_cnet_conv_kernel<2, 1, CN_NARROW_G, true, 1>), ngrid, dim3(64), 0, s, a);
+        else hipLaunchKernelGGL((pwg_cnet_conv_kernel<2, 1, CN_NARROW_G, true, 2>), ngrid, dim3(128), 0, s, a);
       } else if (split) {
         switch (ph.MT) {
           case 1:

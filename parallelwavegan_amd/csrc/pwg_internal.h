@@ -248,6 +248,11 @@ constexpr int SCHED_CTR_STRIDE = 32;
 // Sets the message pwg_last_error() returns and passes `code` through (pwg_capi.hip).
 int set_error(int code, const char* msg);
 
+// hipFuncSetAttribute(kfn, MaxDynamicSharedMemorySize, lds) once per (device, kernel) and size:
+// the launchers call it before every launch, so the host path of a run with dozens of launches
+// (the vocoders' B = 1 decode) keeps only the first call (pwg_capi.hip, thread-safe).
+hipError_t allow_lds(const void* kfn, int lds);
+
 // Kernel launchers (pwg_kernels.hip).
 // Plan descriptors built on the device at the start of every pwg_run, in the caller's workspace
 // (no per-plan hipMalloc / blocking hipMemcpy / hipFree; graph-capturable): up to PLAN_CHUNK

@@ -1144,8 +1144,7 @@ hipError_t launch_layer_persistent(const PersistArgs& a, int mt, int m2t, bool l
     const size_t lds = sizeof(float) * PersistSmem<MT_, M2T_, M3T_>::floats(k1);                           \
     if (lds > 160 * 1024) return hipErrorInvalidValue;                                                     \
     auto kfn = &pwg_layer_persistent_kernel<MT_, M2T_, M3T_, GK_, RC_, SC_, KSC_>;                         \
-    hipError_t e_ = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),                                \
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);              \
+    hipError_t e_ = allow_lds(reinterpret_cast<const void*>(kfn), (int)lds);              \
     if (e_ != hipSuccess) return e_;                                                                       \
     hipLaunchKernelGGL(kfn, grid, block, lds, s, a);                                                       \
     return hipGetLastError();                                                                              \

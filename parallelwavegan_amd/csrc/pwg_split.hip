@@ -553,8 +553,7 @@ hipError_t launch_layer_split(const SplitArgs& a, bool last, int tap_center, int
   {                                                                                                     \
     const size_t lds = sizeof(unsigned) * SplitSmem::dwords(LAST_);                                     \
     auto kfn = &pwg_layer_split_kernel<LAST_, TC_>;                                                     \
-    hipError_t e_ = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),                             \
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);           \
+    hipError_t e_ = allow_lds(reinterpret_cast<const void*>(kfn), (int)lds);           \
     if (e_ != hipSuccess) return e_;                                                                    \
     hipLaunchKernelGGL(kfn, grid, block, lds, s, a);                                                    \
     return hipGetLastError();                                                                           \

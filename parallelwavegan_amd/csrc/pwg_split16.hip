@@ -979,8 +979,7 @@ hipError_t launch_layer_split16(const SplitArgs& a, bool last, int tap_center, i
   {                                                                                                     \
     const size_t lds = sizeof(unsigned) * (Split16Smem::dwords(LAST_) + (FIRST_ ? 128 : 0));            \
     auto kfn = &pwg_layer_split16_kernel<LAST_, TC_, FIRST_, NTN_>;                                     \
-    hipError_t e_ = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),                             \
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);           \
+    hipError_t e_ = allow_lds(reinterpret_cast<const void*>(kfn), (int)lds);                           \
     if (e_ != hipSuccess) return e_;                                                                    \
     hipLaunchKernelGGL(kfn, grid, block, lds, s, a);                                                    \
     return hipGetLastError();                                                                           \
@@ -1012,8 +1011,7 @@ hipError_t launch_sync_split16(const SyncArgs& p, int tap_center, int n_wg, hipS
              : tap_center == 2 ? (p.half ? &pwg_sync_split16_kernel<2, 1> : &pwg_sync_split16_kernel<2, 2>)
                                : nullptr;
   if (kfn == nullptr) return hipErrorInvalidValue;
-  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)lds);
+  const hipError_t e = allow_lds(reinterpret_cast<const void*>(kfn), (int)lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kfn, dim3((unsigned)n_wg), dim3(512), lds, s, p);
   return hipGetLastError();
@@ -1025,8 +1023,7 @@ hipError_t launch_pipe_split16(const PipeArgs& p, int tap_center, int n_wg, hipS
   if (n_wg < p.L || n_wg % 8 != 0) return hipErrorInvalidValue;
   auto kfn = tap_center == 1 ? &pwg_pipe_split16_kernel<1> : tap_center == 2 ? &pwg_pipe_split16_kernel<2> : nullptr;
   if (kfn == nullptr) return hipErrorInvalidValue;
-  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)lds);
+  const hipError_t e = allow_lds(reinterpret_cast<const void*>(kfn), (int)lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kfn, dim3((unsigned)n_wg), dim3(512), lds, s, p);
   return hipGetLastError();
