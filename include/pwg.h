@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define PWG_ABI_VERSION 1
+#define PWG_ABI_VERSION 2  /* 2: PwgConfig.interpolate_mode */
 #if defined(__GNUC__) || defined(__clang__)
 #define PWG_API __attribute__((visibility("default")))
 #else
@@ -109,6 +109,9 @@ typedef struct PwgConfig {
   int use_conv_in;          /* 1: "ConvInUpsampleNetwork", 0: "UpsampleNetwork" */
   int num_scales;
   int upsample_scales[PWG_MAX_SCALES];
+  int interpolate_mode;     /* Stretch2d mode (layers/upsample.py:43-45, 62-128): 0 "nearest" (also
+                               "nearest-exact" / "area", the same map at integer scales), 1
+                               "bilinear" (linear along time, align_corners=False) */
 } PwgConfig;
 
 typedef struct PwgHandle PwgHandle;

@@ -53,11 +53,30 @@ def conv_in(c, w, causal=False, aux_context_window=0):
     return y
 
 
-def upsample_stage(c, scale, taps, causal=False):
-    """Stretch2d nearest xs (layers/upsample.py:43-45: out[t] = in[t // s]) followed by the
+def stretch(c, scale, mode="nearest"):
+    """Stretch2d (layers/upsample.py:43-45): F.interpolate(scale_factor=(1, s)) on (B, 1, C, T).
+    nearest (and nearest-exact / area at integer scales): out[t] = in[t // s]. bilinear
+    (align_corners=False; the channel axis at scale 1 is the identity): aten's linear source index
+    src = max((t + 0.5) / s - 0.5, 0), i0 = floor(src), i1 = min(i0 + 1, T - 1),
+    out[t] = (1 - l) in[i0] + l in[i1], l = src - i0."""
+    if mode in ("nearest", "nearest-exact", "area"):
+        return np.repeat(c, scale, axis=1)
+    if mode != "bilinear":
+        raise NotImplementedError(mode)
+    n = c.shape[1]
+    t = np.arange(n * scale, dtype=np.float64)
+    src = np.maximum((t + 0.5) / scale - 0.5, 0.0)
+    i0 = np.floor(src).astype(np.int64)
+    i1 = np.minimum(i0 + 1, n - 1)
+    lam = (src - i0).astype(c.dtype)
+    return (1 - lam) * c[:, i0] + lam * c[:, i1]
+
+
+def upsample_stage(c, scale, taps, causal=False, mode="nearest"):
+    """Stretch2d xs (stretch(); layers/upsample.py:43-45) followed by the
     Conv2d (1, 2s+1) FIR with zero padding (s, s) or causal (2s, 2s) + trim (:97-103,124-125),
     torch cross-correlation: out[t] = sum_k h[k] * up[t + k - pad]."""
-    up = np.repeat(c, scale, axis=1)
+    up = stretch(c, scale, mode)
     n = up.shape[1]
     pad = 2 * scale if causal else scale
     upp = np.pad(up, ((0, 0), (pad, pad)))
@@ -80,9 +99,10 @@ def upsample_net(c, sd, params, dtype=np.float64):
         prefix = "upsample_net.upsample.up_layers"
     else:
         prefix = "upsample_net.up_layers"
+    mode = params["upsample_params"].get("interpolate_mode", "nearest")
     for i, s in enumerate(scales):
         taps = _w(sd, f"{prefix}.{2 * i + 1}.weight", dtype).reshape(-1)
-        c = upsample_stage(c, s, taps, causal)
+        c = upsample_stage(c, s, taps, causal, mode)
     return c
 
 

@@ -29,6 +29,7 @@ class TorchCPUGenerator:
         self.causal = params.get("use_causal_conv", False)
         self.ctx = params.get("aux_context_window", 2)
         self.scales = params["upsample_params"]["upsample_scales"]
+        self.interpolate_mode = params["upsample_params"].get("interpolate_mode", "nearest")
         self.conv_in = params.get("upsample_net", "ConvInUpsampleNetwork") == "ConvInUpsampleNetwork"
 
     @torch.no_grad()
@@ -45,7 +46,7 @@ class TorchCPUGenerator:
             prefix = "upsample_net.up_layers"
         c = c.unsqueeze(1)  # layers/upsample.py:120-128
         for i, s in enumerate(self.scales):
-            c = F.interpolate(c, scale_factor=(1, s), mode="nearest")
+            c = F.interpolate(c, scale_factor=(1, s), mode=self.interpolate_mode)
             pad = (0, 2 * s) if self.causal else (0, s)
             n = c.size(-1)
             c = F.conv2d(c, w[f"{prefix}.{2 * i + 1}.weight"], padding=pad)

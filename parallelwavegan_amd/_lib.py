@@ -121,6 +121,7 @@ class PwgConfig(ctypes.Structure):
         ("use_conv_in", ctypes.c_int),
         ("num_scales", ctypes.c_int),
         ("upsample_scales", ctypes.c_int * PWG_MAX_SCALES),
+        ("interpolate_mode", ctypes.c_int),
     ]
 
 
@@ -310,7 +311,7 @@ def load():
         lib.pwg_set_timing.argtypes = [vp, ctypes.c_int]
         lib.pwg_set_option.argtypes = [vp, ctypes.c_int, ctypes.c_longlong]
         lib.pwg_timing_collect.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ll)]
-        if lib.pwg_abi_version() != 1:
+        if lib.pwg_abi_version() != 2:
             raise RuntimeError("libpwg_hip ABI version mismatch")
         _lib = lib
         return lib

@@ -112,15 +112,32 @@ struct AuxStruct {
   int nka = 1, nfwg = 1;
 };
 
-void up_stage(const std::vector<double>& in, int s, const double* h, bool causal, std::vector<double>& out) {
-  const long long n = (long long)in.size() * s;
+// One stage: Stretch2d (nearest: out[t] = in[t / s]; bilinear along time, align_corners=False as
+// aten's upsample_bilinear2d: src = max((t + 0.5) / s - 0.5, 0), i0 = floor(src), i1 = min(i0 + 1,
+// n - 1), out[t] = (1 - l) in[i0] + l in[i1], l = src - i0), then the (2s+1)-tap FIR with zero
+// padding s (causal: 2s, trimmed).
+void up_stage(const std::vector<double>& in, int s, const double* h, bool causal, int mode,
+              std::vector<double>& out) {
+  const long long n_in = (long long)in.size(), n = n_in * s;
+  std::vector<double> st((size_t)n);
+  for (long long t = 0; t < n; ++t) {
+    if (mode == 0) {
+      st[t] = in[t / s];
+    } else {  // src = (2t + 1 - s) / 2s in exact integers: the same weight for every period
+      const long long num = std::max(2 * t + 1 - s, 0LL);
+      const long long i0 = num / (2 * s);
+      const long long i1 = std::min(i0 + 1, n_in - 1);
+      const double l = (double)(num % (2 * s)) / (double)(2 * s);
+      st[t] = (1.0 - l) * in[i0] + l * in[i1];
+    }
+  }
   const int P = causal ? 2 * s : s;
   out.assign(n, 0.0);
   for (long long t = 0; t < n; ++t) {
     double v = 0.0;
     for (int k = 0; k < 2 * s + 1; ++k) {
       const long long u = t + k - P;
-      if (u >= 0 && u < n) v += h[k] * in[u / s];
+      if (u >= 0 && u < n) v += h[k] * st[u];
     }
     out[t] = v;
   }
@@ -134,7 +151,7 @@ std::vector<double> upsample_matrix(const PwgConfig& c, const std::vector<std::v
     a.assign(F, 0.0);
     a[f] = 1.0;
     for (int i = 0; i < c.num_scales; ++i) {
-      up_stage(a, c.upsample_scales[i], taps[i].data(), c.use_causal_conv != 0, b);
+      up_stage(a, c.upsample_scales[i], taps[i].data(), c.use_causal_conv != 0, c.interpolate_mode, b);
       a.swap(b);
     }
     for (long long t = 0; t < F * H; ++t) M[(size_t)t * F + f] = a[t];
@@ -167,6 +184,12 @@ void aux_window(const PwgConfig& c, long long H, int* J1, int* J2) {
   *J2 = j2;
 }
 
+// The same window for any stretch mode, from the exact matrix of positive generic taps: the
+// interior rows' nonzero frames relative to t / H (bilinear stretch reaches one more input
+// sample per stage than nearest).
+int aux_window_numeric(const PwgConfig& c, long long H, const std::vector<std::vector<double>>& taps, int* J1,
+                       int* J2);
+
 // Row weights as the layer kernel selects them (w has AUX_J4 entries).
 void decomposed_row(const AuxStruct& st, const std::vector<float>& interior, const std::vector<float>& left,
                     const std::vector<float>& right, const std::vector<float>& small, long long F, long long t,
@@ -187,15 +210,41 @@ void exact_row(const AuxStruct& st, const std::vector<double>& M, long long F, l
   }
 }
 
+int aux_window_numeric(const PwgConfig& c, long long H, const std::vector<std::vector<double>>& taps, int* J1,
+                       int* J2) {
+  const int Fb = 24;
+  const long long fm = Fb / 2;
+  const std::vector<double> M = upsample_matrix(c, taps, Fb, H);
+  int j1 = 0, j2 = 0;
+  for (long long p = 0; p < H; ++p) {
+    const long long t = fm * H + p;
+    for (int f = 0; f < Fb; ++f) {
+      if (M[(size_t)t * Fb + f] == 0.0) continue;
+      j1 = std::max(j1, (int)(fm - f));
+      j2 = std::max(j2, (int)(f - fm));
+    }
+  }
+  if (j1 >= fm - 2 || j2 >= fm - 2) return fail(PWG_ERR_UNSUPPORTED, "composite upsampler window too wide");
+  *J1 = j1;
+  *J2 = j2;
+  return PWG_OK;
+}
+
 // Structure (TL, TR, Fmin, window sizes) from generic taps; tables from the real taps.
 int aux_structure(const PwgConfig& c, AuxStruct* st) {
   long long H = 1;
   for (int i = 0; i < c.num_scales; ++i) H *= c.upsample_scales[i];
   st->H = H;
   if (H < 2 || H > 4096) return fail(PWG_ERR_UNSUPPORTED, "upsample factor must be in [2, 4096]");
-  aux_window(c, H, &st->J1, &st->J2);
-  st->J = st->J1 + st->J2 + 1;
-  if (st->J > AUX_J4) return fail(PWG_ERR_UNSUPPORTED, "composite upsampler spans more than 8 frames");
+  if (c.interpolate_mode != 0 && c.interpolate_mode != 1)
+    return fail(PWG_ERR_UNSUPPORTED, "interpolate_mode must be 0 (nearest) or 1 (bilinear)");
+  // bilinear: the reference's source index (t + 0.5) / s - 0.5 is fp32 (aten opmath), exact for
+  // power-of-two scales; at other scales its rounding grows with t (~t 2^-24 / s: 3e-3 of a weight
+  // at a million samples), which no periodic table reproduces, so those are refused
+  if (c.interpolate_mode == 1)
+    for (int i = 0; i < c.num_scales; ++i)
+      if ((c.upsample_scales[i] & (c.upsample_scales[i] - 1)) != 0)
+        return fail(PWG_ERR_UNSUPPORTED, "interpolate_mode bilinear needs power-of-two upsample scales");
   // generic taps: the unclean row set is structural (boundary truncation), not value-dependent
   std::vector<std::vector<double>> taps(c.num_scales);
   uint64_t x = 0x9E3779B97F4A7C15ULL;
@@ -204,6 +253,14 @@ int aux_structure(const PwgConfig& c, AuxStruct* st) {
       x = x * 6364136223846793005ULL + 1442695040888963407ULL;
       taps[i].push_back(0.5 + (double)(x >> 11) / (double)(1ULL << 53));
     }
+  if (c.interpolate_mode == 0) {
+    aux_window(c, H, &st->J1, &st->J2);
+  } else {
+    const int rc = aux_window_numeric(c, H, taps, &st->J1, &st->J2);
+    if (rc != PWG_OK) return rc;
+  }
+  st->J = st->J1 + st->J2 + 1;
+  if (st->J > AUX_J4) return fail(PWG_ERR_UNSUPPORTED, "composite upsampler spans more than 8 frames");
   const int Fb = 24;
   const std::vector<double> M = upsample_matrix(c, taps, Fb, H);
   const long long T = Fb * H, fm = Fb / 2;

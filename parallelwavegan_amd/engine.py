@@ -32,8 +32,9 @@ def make_config(params):
         raise NotImplementedError("upsample nonlinear_activation is not supported")
     if up.get("freq_axis_kernel_size", 1) != 1:
         raise NotImplementedError("freq_axis_kernel_size != 1 is not supported")
-    if up.get("interpolate_mode", "nearest") != "nearest":
-        raise NotImplementedError("only nearest interpolation is supported")
+    mode = up.get("interpolate_mode", "nearest")
+    if mode not in INTERPOLATE_MODES:
+        raise NotImplementedError(f"interpolate_mode={mode!r} is not supported (nearest, nearest-exact, area, bilinear)")
     scales = list(up.get("upsample_scales", [4, 4, 4, 4]))
     if not 1 <= len(scales) <= _lib.PWG_MAX_SCALES:
         raise NotImplementedError("1..8 upsample scales supported")
@@ -53,7 +54,14 @@ def make_config(params):
     cfg.num_scales = len(scales)
     for i, s in enumerate(scales):
         cfg.upsample_scales[i] = int(s)
+    cfg.interpolate_mode = INTERPOLATE_MODES[mode]
     return cfg
+
+
+# Stretch2d modes (layers/upsample.py:43-45) the engine computes: F.interpolate with scale_factor
+# (1, s) on (B, 1, C, T); "nearest-exact" and "area" give nearest's map at integer scales, and
+# "bilinear" is linear along time (scale 1 along the channel axis is the identity)
+INTERPOLATE_MODES = {"nearest": 0, "nearest-exact": 0, "area": 0, "bilinear": 1}
 
 
 def ref_weight_keys(params):

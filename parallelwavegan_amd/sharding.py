@@ -224,7 +224,7 @@ def decode_long_sharded(engine, mel, noise, rank=None, world=None, halo=None, me
     noise = noise.reshape(-1)
     if noise.numel() != F * H:
         raise ValueError("noise must have frames * upsample_factor samples")
-    causal = bool(engine.config.use_causal_conv)
+    causal = bool(engine.config.use_causal_conv) and int(getattr(engine.config, "interpolate_mode", 0)) != 1
     halo = halo_frames(engine) if halo is None else int(halo)
     ranges = long_utterance_ranges(F, world, halo, H, causal)
     per = max(e - s for _, s, e, _ in ranges)

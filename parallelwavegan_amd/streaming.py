@@ -22,15 +22,21 @@ import math
 import torch
 
 
-def upsample_reach_frames(scales, causal):
+def upsample_reach_frames(scales, causal, bilinear=False):
     """Input frames the FIR chain reaches from one output sample (layers/upsample.py:97-103,
     112-128): stage i filters at rate prod(s_1..s_i) with s_i taps per side (2 s_i to the left,
-    causal), i.e. 1 / prod(s_1..s_{i-1}) frames (2x causal). Summed over stages: <= 2 (<= 4)."""
+    causal), i.e. 1 / prod(s_1..s_{i-1}) frames (2x causal). Summed over stages: <= 2 (<= 4).
+    A bilinear stretch (Stretch2d interpolate_mode, :43-45) reaches one more input sample of its
+    stage on each side."""
     reach, prev = 0.0, 1
     for s in scales:
-        reach += (2.0 if causal else 1.0) / prev
+        reach += (2.0 if causal else 1.0) / prev + (1.0 / prev if bilinear else 0.0)
         prev *= int(s)
     return reach
+
+
+def _bilinear(engine):
+    return int(getattr(engine.config, "interpolate_mode", 0)) == 1
 
 
 def halo_frames(engine, causal=None):
@@ -44,7 +50,7 @@ def halo_frames(engine, causal=None):
     reach = rf - 1 if causal else (rf - 1) // 2
     H = int(engine.upsample_factor)
     scales = [int(cfg.upsample_scales[i]) for i in range(int(cfg.num_scales))]
-    up = upsample_reach_frames(scales, causal)
+    up = upsample_reach_frames(scales, causal, _bilinear(engine))
     return int(math.ceil(reach / H + up)) + int(cfg.aux_context_window) + 1
 
 
@@ -71,7 +77,8 @@ def chunk_ranges(frames, chunk_frames, halo, causal=False, align=1):
 def infer_chunked(engine, mel, noise, chunk_frames, halo=None, mean=None, scale=None):
     """One utterance (mel (T', A), noise (T,) or (T, 1), device tensors) -> (T, out_channels),
     computed as overlapping chunks in one ragged engine pass."""
-    causal = bool(engine.config.use_causal_conv)
+    # a bilinear stretch looks ahead even in a causal generator: right halos then too
+    causal = bool(engine.config.use_causal_conv) and not _bilinear(engine)
     halo = halo_frames(engine) if halo is None else int(halo)
     H = int(engine.upsample_factor)
     F = int(mel.shape[0])
@@ -95,6 +102,8 @@ class CausalStream:
     def __init__(self, engine, halo=None, mean=None, scale=None):
         if not engine.config.use_causal_conv:
             raise ValueError("CausalStream needs a use_causal_conv=True generator")
+        if _bilinear(engine):
+            raise ValueError("CausalStream: a bilinear upsampler stretch looks ahead (use infer_chunked)")
         self.engine = engine
         self.halo = halo_frames(engine) if halo is None else int(halo)
         self.H = int(engine.upsample_factor)

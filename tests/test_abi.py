@@ -45,7 +45,7 @@ def test_library_is_gfx950_code_object(built_lib):
 
 
 def test_abi_version(built_lib):
-    assert built_lib.pwg_abi_version() == 1
+    assert built_lib.pwg_abi_version() == 2  # 2: PwgConfig.interpolate_mode
 
 
 @pytest.mark.parametrize("name", ["yesno_debug", "ljspeech_v1", "libritts_v1", "reference_test"])
@@ -202,3 +202,25 @@ def test_rccl_entry_points_validate_arguments(built_lib):
     assert built_lib.pwg_rccl_comm_create(2, buf, 2, 0, ctypes.byref(comm)) == _lib.PWG_ERR_INVALID
     assert built_lib.pwg_broadcast_weights(None, None, 0, None, None) == _lib.PWG_ERR_INVALID
     assert built_lib.pwg_rccl_comm_destroy(None) == _lib.PWG_OK
+
+
+def test_interpolate_modes(built_lib):
+    """Stretch2d interpolate_mode (layers/upsample.py:43-45, 62-128): "nearest", "nearest-exact" and
+    "area" are the same map at integer scales, "bilinear" is linear along time; the handle builds
+    and verifies its composite upsampler tables for each (pwg_create fails otherwise). Bilinear at a
+    scale that is not a power of two, and other modes, are refused: aten computes the bilinear
+    source index in fp32, exact only at power-of-two scales."""
+    for cfg, scales in (("ljspeech_v1", [4, 4, 4, 4]), ("reference_test", [8, 2]), ("reference_test", [4, 4])):
+        for mode in ("nearest", "nearest-exact", "area", "bilinear"):
+            for causal in (False, True):
+                p = configs.generator_params(cfg, use_causal_conv=causal,
+                                             upsample_params={"upsample_scales": scales, "interpolate_mode": mode})
+                h = HostHandle(p)
+                assert h.config.interpolate_mode == (1 if mode == "bilinear" else 0)
+    with pytest.raises(NotImplementedError, match="power-of-two"):
+        HostHandle(configs.generator_params("libritts_v1", upsample_params={"upsample_scales": [4, 5, 3, 5],
+                                                                             "interpolate_mode": "bilinear"}))
+    for mode in ("bicubic", "linear", "trilinear"):
+        with pytest.raises(NotImplementedError):
+            HostHandle(configs.generator_params("ljspeech_v1", upsample_params={"upsample_scales": [4, 4, 4, 4],
+                                                                                 "interpolate_mode": mode}))

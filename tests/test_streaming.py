@@ -108,3 +108,24 @@ def test_causal_stream_rejects_noncausal(built_lib, cuda_device):
     eng = _engine("reference_test", cuda_device)
     with pytest.raises(ValueError):
         streaming.CausalStream(eng)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("causal", [False, True], ids=["noncausal", "causal"])
+def test_bilinear_upsampler_chunked(causal, built_lib, cuda_device):
+    """interpolate_mode="bilinear" (layers/upsample.py:43-45): the stretch reaches one more input
+    sample per stage (upsample_reach_frames) and looks ahead even in a causal generator, so chunks
+    take right halos then too; chunked decoding stays bit-identical to the whole utterance, and
+    CausalStream refuses the configuration."""
+    from parallelwavegan_amd import synthetic
+
+    eng = _engine("ljspeech_v1", cuda_device, use_causal_conv=causal,
+                  upsample_params={"upsample_scales": [4, 4, 4, 4], "interpolate_mode": "bilinear"})
+    H = eng.upsample_factor
+    mel = torch.from_numpy(synthetic.make_mel(203, 80, seed=13)).to(cuda_device)
+    noise = torch.from_numpy(synthetic.make_noise(203 * H, seed=14)).to(cuda_device)
+    full = eng.infer([mel], [noise])[0].cpu().numpy()
+    np.testing.assert_array_equal(streaming.infer_chunked(eng, mel, noise, 48).cpu().numpy(), full)
+    if causal:
+        with pytest.raises(ValueError):
+            streaming.CausalStream(eng)

@@ -21,6 +21,6 @@ for k, v in (d.get("vocoders") or {}).items():
     print(k, v["value"], v["roofline"]["frac"], v["roofline"]["traffic"], [(r["frames"], r["batch"], r["median_ms"]) for r in v["latency"]["rows"]])
 print("lat", [(r["frames"], r["batch"], r["median_ms"]) for r in d["latency"]["rows"]])
 PY
-bash tools/diag/voc_lat_ops.sh "$OUT/voc"
+mkdir -p "$OUT/voc" && timeout -k 10 300 python tools/diag/voc_lat_ab.py "$OUT/voc/lat_ab.json"
 bash tools/gpu_r4_diag_pwg.sh "$OUT/diag"
 echo pass-b done
