@@ -140,9 +140,14 @@ PWG_API int pwg_cnet_run_status(PwgCnetPlan* p, const void* workspace, void* str
  * (32-128 columns) and 1-2 m-tiles each, weights DMA-staged in tap groups, so a short utterance's
  * op spreads over every CU (the B = 1 decode path, bin/decode.py:236-268); a fused pair or stack
  * whose first conv runs narrow runs as its two ops. Bit-identical to the default launches.
- * 0: never; 2: every x-tile launch (tests). */
+ * 0: never; 2: every x-tile launch (tests).
+ * PWG_CNET_OPT_NARROW_DMA (default 1): narrow launches run the DMA-ring kernel: every step (a
+ * 16-channel block with all its taps, or one chunk of a tap-major op) is staged by global_load_lds
+ * a few steps ahead of its MFMAs, the input rows pre-activated LDS -> LDS; also takes the narrow
+ * launches of tap-major convs (MelGAN's two-source 1x1s). Bit-identical to 0 (the DMA-staged narrow
+ * x-tile kernel and the narrow tap-major kernel), which stays for A/B. */
 enum { PWG_CNET_OPT_SPLIT_F16 = 0, PWG_CNET_OPT_FUSE_PAIRS = 1, PWG_CNET_OPT_PAIR_STEPS = 2, PWG_CNET_OPT_XTILE = 3,
-       PWG_CNET_OPT_XT_DMA = 4, PWG_CNET_OPT_XCD_ORDER = 5, PWG_CNET_OPT_NARROW = 6 };
+       PWG_CNET_OPT_XT_DMA = 4, PWG_CNET_OPT_XCD_ORDER = 5, PWG_CNET_OPT_NARROW = 6, PWG_CNET_OPT_NARROW_DMA = 7 };
 PWG_API int pwg_cnet_set_option(PwgCnet* n, int option, long long value);
 PWG_API int pwg_cnet_set_timing(PwgCnet* n, int enable);
 /* Adds per-op milliseconds and launch counts (arrays of n_ops) and clears the records. */

@@ -944,6 +944,299 @@ hipError_t xtile_launch_narrow(int mt, int nwv, int k, dim3 grid, int lds, hipSt
   return hipErrorInvalidValue;
 }
 
+// Narrow DMA-ring launches (PWG_CNET_OPT_NARROW_DMA, default): the tiles of the narrow launches
+// above (NWV waves x 32 columns, MT m-tiles), with every byte a step needs staged by
+// global_load_lds into a ring of P slots and the steps issued P - 1 ahead of the MFMAs. A step is
+// one 16-channel block with all K taps (x-tile family: K > 1, or ConvTranspose phases, K = 2 rev)
+// or one chunk of the tap-major chunk list (K = 1 mode: any op, each chunk at its own row offset and
+// source). A slot holds the step's raw input rows (16 rows x 64 B per DMA instruction, edge rows
+// clamped) and its A fragments (1 KB per instruction); the raw rows of step g + 1 are pre-activated
+// (normalize, LeakyReLU, edge mask) and pair-split LDS -> LDS into one of two row buffers while the
+// MFMAs of step g run. At B = 1 a workgroup sums 2-16 steps of a few dozen MFMAs each; the narrow
+// x-tile kernel waited out the L2/HBM round trip of every step (~1.2 us each, HiFiGAN's 256-channel
+// convs 35-59 us), here it is paid about once per launch.
+// Per column the products and their order are those of pwg_cnet_xtile_kernel (channel block, tap,
+// hi.hi / hi.lo / lo.hi) or, in K = 1 mode, of pwg_cnet_conv_kernel (chunk order): bit-identical.
+struct CnXdmaArgs {
+  int dil;        // K > 1: dilation
+  int cs;         // K > 1: 16-channel blocks (weight chunk of tap t, block c: t cs + c)
+  int n_steps;    // K > 1: cs; K = 1: chunks of the op (pwg_cnet_conv_kernel's list)
+  int rev;        // ConvTranspose phases: tap t multiplies weight chunk K-1-t
+  int z_off[8];   // K > 1: row offset of tap 0 for phase blockIdx.z
+};
+template <int K, int MT, int NWV>
+struct XdmaShape {
+  static constexpr int XC = 32 * NWV;
+  static constexpr int XR = XC + (K == 1 ? 0 : NARROW_HALO);  // raw input rows per step
+  static constexpr int NA = K * MT * 2, NX = XR / 16;          // 1-KB DMA instructions per step
+  static constexpr int DA = (NA + NWV - 1) / NWV, DX = (NX + NWV - 1) / NWV;  // ... per wave
+  static constexpr int D = DA + DX;
+  static constexpr int SLOT = (NX + NA) * 1024;                // raw rows, then A fragments
+  static constexpr int CBUF = XR * XT_ROWB;                    // one converted-row buffer
+  // deepest ring (<= 6 slots) whose wait counts fit vmcnt (63) and whose LDS fits 152 KB
+  static constexpr int ring(int p) {
+    return p <= 2 ? 2 : (((p - 2) * D <= 63 && p * SLOT + 2 * CBUF <= 152 * 1024) ? p : ring(p - 1));
+  }
+  static constexpr int P = ring(6);
+  static constexpr int LDS = P * SLOT + 2 * CBUF;
+  static_assert(LDS <= 160 * 1024, "DMA-ring shape");
+};
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// s_waitcnt vmcnt(BASE + min(r, R) * D)
+template <int BASE, int D, int R>
+__device__ __forceinline__ void vm_wait_steps(int r) {
+  if constexpr (R > 0) {
+    if (r >= R) {
+      vm_wait<BASE + R * D>();
+      return;
+    }
+    vm_wait_steps<BASE, D, R - 1>(r);
+  } else {
+    vm_wait<BASE>();
+  }
+}
+
+template <int K, int MT, int NWV>
+__global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArgs a, const CnXdmaArgs xd) {
+  using S = XdmaShape<K, MT, NWV>;
+  constexpr int NTH = 64 * NWV, P = S::P;
+  extern __shared__ __attribute__((aligned(16))) unsigned char xt_smem[];
+  unsigned char* const s_cb = xt_smem + (size_t)P * S::SLOT;  // [2][XR][XT_ROWB]
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int hh = lane >> 5;
+  const int cl = lane & 31;
+  const TileId tid = xcd_tile(a.xcd_order);
+  const int2 blk = a.blocks[tid.x];
+  const int u = blk.x;
+  const int q0 = blk.y;
+  const int nq = a.ncols[u];
+  const int m0 = tid.y * MT;
+  const int zp = tid.z;
+  const float* const wfrag_ = zp == 0 ? a.wfrag : a.z_wfrag[zp];
+  const float* const bias_ = zp == 0 ? a.bias : a.z_bias[zp];
+  const ChunkDesc* const chunks_ = zp == 0 ? a.chunks : a.z_chunks[zp];
+  const int ns = xd.n_steps;
+  const int span = K == 1 ? S::XC : S::XC + (K - 1) * xd.dil;
+
+  struct Step {
+    int src, c0, off;  // source, first input channel, row offset of tap 0
+  };
+  auto step_of = [&](int s) -> Step {
+    if constexpr (K == 1) {
+      const ChunkDesc cd = chunks_[s];
+      return {cd.src, cd.c0, cd.row_off};
+    } else {
+      return {0, 16 * s, xd.z_off[zp]};
+    }
+  };
+  typedef __attribute__((address_space(1))) void* gptr_t;
+  typedef __attribute__((address_space(3))) void* lptr_t;
+  // step s -> slot s % P: DA A-fragment then DX raw-row instructions per wave (uniform counts: the
+  // last instruction of a kind is repeated by waves past the end, same bytes to the same place), so
+  // a wait for a step's rows covers its A fragments too
+  auto issue = [&](int s) {
+    unsigned char* const slot = xt_smem + (size_t)(s % P) * S::SLOT;
+    unsigned char* const sa = slot + S::NX * 1024;
+#pragma unroll
+    for (int k = 0; k < S::DA; ++k) {
+      int i = wave + NWV * k;
+      i = i < S::NA ? i : S::NA - 1;
+      const int tl = i / (MT * 2), j = i - tl * (MT * 2);
+      const int wt = xd.rev ? K - 1 - tl : tl;
+      const int chunk = K == 1 ? s : wt * xd.cs + s;
+      const float* src = wfrag_ + ((size_t)chunk * a.mt_total + m0) * 512 + j * 256 + lane * 4;
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(sa + (size_t)i * 1024), 16, 0, 0);
+    }
+    const Step st = step_of(s);
+    const CnSrc& sx = a.src[st.src];
+    const int2 sg = *reinterpret_cast<const int2*>(sx.seg + 2 * u);
+#pragma unroll
+    for (int k = 0; k < S::DX; ++k) {
+      int i = wave + NWV * k;
+      i = i < S::NX ? i : S::NX - 1;
+      int p = q0 + st.off + 16 * i + (lane >> 2);
+      (void)edge_row(p, sg.y, sx.pad_mode);
+      const float* src = sx.x + (size_t)(sg.x + p) * sx.ld + st.c0 + 4 * (lane & 3);
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(slot + (size_t)i * 1024), 16, 0, 0);
+    }
+  };
+  // raw rows of step s -> converted-row buffer s & 1 (pwg_cnet_xtile_kernel's xstore arithmetic)
+  auto convert = [&](int s) {
+    const unsigned char* const raw = xt_smem + (size_t)(s % P) * S::SLOT;
+    unsigned char* const cb = s_cb + (size_t)(s & 1) * S::CBUF;
+    const Step st = step_of(s);
+    const CnSrc& sx = a.src[st.src];
+    const int2 sg = *reinterpret_cast<const int2*>(sx.seg + 2 * u);
+    constexpr int NQ = (S::XR * 4 + NTH - 1) / NTH;
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+      const int idx = threadIdx.x + NTH * i;
+      const int r = idx >> 2, qd = idx & 3;
+      if (r >= span) continue;
+      int p = q0 + st.off + r;
+      const bool ok = edge_row(p, sg.y, sx.pad_mode);
+      f32x4v v = *reinterpret_cast<const f32x4v*>(raw + r * 64 + qd * 16);
+      const int ch = st.c0 + 4 * qd;
+      if (sx.normalize) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (v[e] - a.mean[ch + e]) / a.scale[ch + e];
+      }
+      if (sx.slope != 1.f) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * sx.slope;
+      }
+      if (!ok) v = f32x4v{0.f, 0.f, 0.f, 0.f};
+      _Float16 hv[4], lv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        hv[e] = (_Float16)v[e];
+        lv[e] = (_Float16)(v[e] - (float)hv[e]);
+      }
+      unsigned char* row = cb + (size_t)r * XT_ROWB;
+      *reinterpret_cast<f16x4v*>(row + 8 * qd) = f16x4v{hv[0], hv[1], hv[2], hv[3]};
+      *reinterpret_cast<f16x4v*>(row + 32 + 8 * qd) = f16x4v{lv[0], lv[1], lv[2], lv[3]};
+    }
+  };
+
+  f32x16 acc[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
+  auto mma = [&](int g) {
+    const unsigned char* const cb = s_cb + (size_t)(g & 1) * S::CBUF;
+    const u32x4v* const sa =
+        reinterpret_cast<const u32x4v*>(xt_smem + (size_t)(g % P) * S::SLOT + S::NX * 1024) + lane;
+#pragma unroll
+    for (int t = 0; t < K; ++t) {
+      const unsigned char* row = cb + (size_t)(wave * 32 + cl + (K == 1 ? 0 : t * xd.dil)) * XT_ROWB;
+      const u32x4v bh = *reinterpret_cast<const u32x4v*>(row + 16 * hh);
+      const u32x4v bl = *reinterpret_cast<const u32x4v*>(row + 32 + 16 * hh);
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const u32x4v ah = sa[(t * MT * 2 + m * 2) * 64], al = sa[(t * MT * 2 + m * 2 + 1) * 64];
+        acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, ah), __builtin_bit_cast(f16x8v, bh),
+                                                        acc[m], 0, 0, 0);
+        acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, ah), __builtin_bit_cast(f16x8v, bl),
+                                                        acc[m], 0, 0, 0);
+        acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, al), __builtin_bit_cast(f16x8v, bh),
+                                                        acc[m], 0, 0, 0);
+      }
+    }
+  };
+
+  // steps 0 .. P-2 in flight; wait for step 0 (the later steps may still land)
+  for (int s = 0; s < P - 1; ++s)
+    if (s < ns) issue(s);
+  vm_wait_steps<0, S::D, P - 2>(ns - 1);
+  __syncthreads();
+  convert(0);
+  __syncthreads();
+  for (int g = 0; g < ns; ++g) {
+    // slot (g - 1) % P: read by step g - 1's MFMAs and conversion, both before the last barrier
+    if (g + P - 1 < ns) issue(g + P - 1);
+    // step g + 1 landed (step g did before the last barrier)
+    if (g + 1 < ns) {
+      vm_wait_steps<0, S::D, P - 2>(ns - 2 - g);
+      __syncthreads();
+    }
+    mma(g);
+    if (g + 1 < ns) convert(g + 1);  // into the buffer step g - 1's MFMAs read
+    __syncthreads();
+  }
+
+  // epilogue (pwg_cnet_xtile_kernel's)
+  const int qb = q0 + wave * 32 + cl;
+  if (qb >= nq) return;
+  const int2 sd = *reinterpret_cast<const int2*>(a.seg_dst + 2 * u);
+  const int2 sr = a.res ? *reinterpret_cast<const int2*>(a.seg_res + 2 * u) : make_int2(0, 0);
+  const bool quad = (a.ld_dst & 3) == 0;
+  const int t = qb * a.ostride + a.ophase + zp;
+  float* yrow = a.y + (size_t)(sd.x + t) * a.ld_dst;
+  const float* rrow = a.res ? a.res + (size_t)(sr.x + t) * a.ld_res : nullptr;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int j4 = 0; j4 < 4; ++j4) {
+      const int row = 32 * (m0 + m) + 8 * j4 + 4 * hh;
+      if (row >= a.M) {
+        if (quad && row < a.ld_dst) *reinterpret_cast<f32x4v*>(yrow + row) = f32x4v{0.f, 0.f, 0.f, 0.f};
+        continue;
+      }
+      const f32x4v b = *reinterpret_cast<const f32x4v*>(bias_ + row);
+      f32x4v v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = acc[m][4 * j4 + i] + b[i];
+      if (quad) {
+        if (rrow) v += *reinterpret_cast<const f32x4v*>(rrow + row);
+        if (a.accumulate) v = *reinterpret_cast<const f32x4v*>(yrow + row) + v;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (row + i >= a.M) continue;
+          if (rrow) v[i] += rrow[row + i];
+          if (a.accumulate) v[i] = yrow[row + i] + v[i];
+        }
+      }
+      if (a.out_div != 1.f) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = v[i] / a.out_div;
+      }
+      if (a.post_act == PWG_ACT_LRELU) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = v[i] > 0.f ? v[i] : v[i] * a.post_slope;
+      } else if (a.post_act == PWG_ACT_TANH) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = tanhf(v[i]);
+      }
+      if (quad) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (row + i >= a.M) v[i] = 0.f;
+        *reinterpret_cast<f32x4v*>(yrow + row) = v;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (row + i < a.M) yrow[row + i] = v[i];
+      }
+    }
+}
+
+template <int K, int MT, int NWV>
+hipError_t xdma_go(dim3 grid, hipStream_t s, const CnConvArgs& a, const CnXdmaArgs& xd) {
+  constexpr int lds = XdmaShape<K, MT, NWV>::LDS;
+  const hipError_t e = allow_lds(reinterpret_cast<const void*>(pwg_cnet_xdma_kernel<K, MT, NWV>), lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((pwg_cnet_xdma_kernel<K, MT, NWV>), grid, dim3(64 * NWV), (size_t)lds, s, a, xd);
+  return hipGetLastError();
+}
+template <int MT, int NWV>
+hipError_t xdma_launch_k(int k, dim3 grid, hipStream_t s, const CnConvArgs& a, const CnXdmaArgs& xd) {
+  switch (k) {
+    case 1: return xdma_go<1, MT, NWV>(grid, s, a, xd);
+    case 2: return xdma_go<2, MT, NWV>(grid, s, a, xd);
+    case 3: return xdma_go<3, MT, NWV>(grid, s, a, xd);
+    case 5: return xdma_go<5, MT, NWV>(grid, s, a, xd);
+    case 7: return xdma_go<7, MT, NWV>(grid, s, a, xd);
+    case 11: return xdma_go<11, MT, NWV>(grid, s, a, xd);
+    default: return hipErrorInvalidValue;
+  }
+}
+// k = 1: K = 1 mode (steps = the tap-major chunk list)
+hipError_t xdma_launch(int mt, int nwv, int k, dim3 grid, hipStream_t s, const CnConvArgs& a, const CnXdmaArgs& xd) {
+  if (mt == 1 && nwv == 1) return xdma_launch_k<1, 1>(k, grid, s, a, xd);
+  if (mt == 1 && nwv == 2) return xdma_launch_k<1, 2>(k, grid, s, a, xd);
+  if (mt == 1 && nwv == 4) return xdma_launch_k<1, 4>(k, grid, s, a, xd);
+  if (mt == 2 && nwv == 1) return xdma_launch_k<2, 1>(k, grid, s, a, xd);
+  if (mt == 2 && nwv == 2) return xdma_launch_k<2, 2>(k, grid, s, a, xd);
+  if (mt == 2 && nwv == 4) return xdma_launch_k<2, 4>(k, grid, s, a, xd);
+  return hipErrorInvalidValue;
+}
+
 // Fused conv pair on the x-tile scheme (split-f16; HiFiGAN ResBlock step x = c2(lrelu(c1(lrelu(x)))) + x,
 // layers/residual_block.py:231-237, 32 or 64 channels, 128 at k = 3): one workgroup = 8 waves, 224 output columns.
 //   stage 1: h over the 256 columns [q0 - 16, q0 + 240) (wave w: 32 of them), channel-block-major
@@ -2509,6 +2802,8 @@ struct PwgCnet {
   int xt_dma = 9;      // PWG_CNET_OPT_XT_DMA flags (CNET_DMA_RULE | CNET_DMA_CONVT)
   int xcd_order = 1;   // PWG_CNET_OPT_XCD_ORDER
   int narrow = 1;      // PWG_CNET_OPT_NARROW (plan time): 0 off, 1 small launches, 2 every x-tile phase
+  int narrow_dma = 1;  // PWG_CNET_OPT_NARROW_DMA: narrow launches on the DMA-ring kernel (0: the narrow
+                       // x-tile / tap-major kernels)
   bool pair_attr_set = false;
   std::vector<PwgCnetOp> ops;
   std::vector<int> channels, rate, ld;
@@ -3615,7 +3910,16 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
           xt.span = 32 * nw + (xt.K - 1) * xt.dil;
           a.blocks = p->d_nblocks[pi];
           const dim3 ngrid((unsigned)p->n_nblocks[pi], (unsigned)(ph.mt_total / mtn), (unsigned)ph.z_phases);
-          ea2 = p->n_nblocks[pi] > 0 ? xtile_launch_narrow(mtn, nw, xt.K, ngrid, p->nar_lds[pi], s, a, xt) : hipSuccess;
+          if (p->n_nblocks[pi] == 0) {
+            ea2 = hipSuccess;
+          } else if (n->narrow_dma) {
+            CnXdmaArgs xd;
+            xd.dil = xt.dil; xd.cs = xt.cs; xd.n_steps = xt.cs; xd.rev = xt.rev;
+            for (int r = 0; r < 8; ++r) xd.z_off[r] = xt.z_off[r];
+            ea2 = xdma_launch(mtn, nw, xt.K, ngrid, s, a, xd);
+          } else {
+            ea2 = xtile_launch_narrow(mtn, nw, xt.K, ngrid, p->nar_lds[pi], s, a, xt);
+          }
         } else {
           const bool db = ph.xt_convt_db ||
                           (ph.xt_db && ((n->xt_dma & CNET_DMA_ALL) || ((n->xt_dma & CNET_DMA_RULE) && ph.xt_db_pick)));
@@ -3628,7 +3932,13 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         a.blocks = p->d_nblocks[pi];
         const int nw = p->nar_nwv[pi], mtn = p->nar_mt[pi];
         const dim3 ngrid((unsigned)p->n_nblocks[pi], (unsigned)(ph.mt_total / mtn), (unsigned)ph.z_phases);
-        if (mtn == 1 && nw == 1) hipLaunchKernelGGL((pwg_cnet_conv_kernel<1, 1, CN_NARROW_G, true, 1>), ngrid, dim3(64), 0, s, a);
+        if (n->narrow_dma) {
+          CnXdmaArgs xd;  // K = 1 mode: the chunk list, each chunk at its own source and row offset
+          xd.dil = 1; xd.cs = 0; xd.n_steps = a.n_chunks; xd.rev = 0;
+          for (int r = 0; r < 8; ++r) xd.z_off[r] = 0;
+          const hipError_t ea2 = p->n_nblocks[pi] > 0 ? xdma_launch(mtn, nw, 1, ngrid, s, a, xd) : hipSuccess;
+          if (ea2 != hipSuccess) return hipf(ea2, "xdma kernel launch");
+        } else if (mtn == 1 && nw == 1) hipLaunchKernelGGL((pwg_cnet_conv_kernel<1, 1, CN_NARROW_G, true, 1>), ngrid, dim3(64), 0, s, a);
         else if (mtn == 1) hipLaunchKernelGGL((pwg_cnet_conv_kernel<1, 1, CN_NARROW_G, true, 2>), ngrid, dim3(128), 0, s, a);
         else if (nw == 1) hipLaunchKernelGGL((pwg_cnet_conv_kernel<2, 1, CN_NARROW_G, true, 1>), ngrid, dim3(64), 0, s, a);
         else hipLaunchKernelGGL((pwg_cnet_conv_kernel<2, 1, CN_NARROW_G, true, 2>), ngrid, dim3(128), 0, s, a);
@@ -3724,6 +4034,7 @@ int pwg_cnet_set_option(PwgCnet* n, int option, long long value) {
               : option == PWG_CNET_OPT_XTILE      ? &n->xtile
               : option == PWG_CNET_OPT_XT_DMA     ? &n->xt_dma
               : option == PWG_CNET_OPT_XCD_ORDER  ? &n->xcd_order
+              : option == PWG_CNET_OPT_NARROW_DMA ? &n->narrow_dma
                                                   : nullptr;
   if (!slot) return fail(PWG_ERR_INVALID, "unknown option");
   if (value != 0 && value != 1 && !(option == PWG_CNET_OPT_XT_DMA && value >= 0 && value <= 15))

@@ -345,7 +345,8 @@ def test_narrow_launches_bitwise_equal(cfg, built_lib, cuda_device):
     1-4-wave, 1-2-m-tile workgroups, and the fused x-tile pairs / stacks whose first conv does run
     as their two ops. Every column sums the same products in the same order, so the output is
     bit-identical to the default launches: narrow off (0), automatic (1: the short utterance alone
-    and the ragged batch pick different launches) and forced on every x-tile launch (2)."""
+    and the ragged batch pick different launches) and forced on every x-tile launch (2), each on
+    the DMA-ring kernel (PWG_CNET_OPT_NARROW_DMA 1) and on the narrow x-tile / tap-major ones (0)."""
     from parallelwavegan_amd import configs, synthetic
     from parallelwavegan_amd.hifigan import HiFiGANGenerator
     from parallelwavegan_amd.melgan import PQMF, MelGANGenerator
@@ -360,12 +361,16 @@ def test_narrow_launches_bitwise_equal(cfg, built_lib, cuda_device):
     mels = [synthetic.make_mel(f, 80, seed=150 + i) for i, f in enumerate([64, 9, 23, 131])]
     with torch.no_grad():
         outs = {}
-        for mode in (0, 1, 2):
+        for mode, dma in ((0, 1), (1, 1), (2, 1), (1, 0), (2, 0)):
             eng.set_narrow(mode)
-            outs[mode] = ([m.inference(torch.from_numpy(mels[0]).to(cuda_device)).cpu().numpy()] +
-                          [y.cpu().numpy() for y in m.inference_batch(mels)])
+            eng.set_narrow_dma(dma)
+            outs[mode, dma] = ([m.inference(torch.from_numpy(mels[0]).to(cuda_device)).cpu().numpy()] +
+                               [y.cpu().numpy() for y in m.inference_batch(mels)])
         eng.set_narrow(1)
-    for mode in (1, 2):
-        for a, b in zip(outs[mode], outs[0]):
+        eng.set_narrow_dma(1)
+    # narrow_dma 1: the DMA-ring kernel (x-tile family and, K = 1 mode, the tap-major convs);
+    # 0: the DMA-staged narrow x-tile kernel and the narrow tap-major kernel
+    for key in ((1, 1), (2, 1), (1, 0), (2, 0)):
+        for a, b in zip(outs[key], outs[0, 1]):
             assert np.isfinite(a).all()
             np.testing.assert_array_equal(a, b)

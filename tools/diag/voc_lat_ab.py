@@ -1,5 +1,5 @@
 """Vocoder B = 1 latency A/B on the GPU box: the drop-in's inference() at T' = 64 / 512 with
-PWG_CNET_OPT_NARROW 0 / 1 / 2 (same library), median wall ms per synchronised call, the kernels'
+PWG_CNET_OPT_NARROW 0 / 1 / 2 and PWG_CNET_OPT_NARROW_DMA 0 / 1 (same library), median wall ms per synchronised call, the kernels'
 summed ms, and the per-op ms of the automatic mode (tools/diag/voc_lat_ops.sh's table, one line).
 Usage: python tools/diag/voc_lat_ab.py OUT.json"""
 import json
@@ -29,8 +29,9 @@ def main():
         eng = m.engine()
         for F in (64, 512):
             mel = torch.from_numpy(synthetic.make_mel(F, 80, seed=30)).to(dev)
-            for mode in (0, 1, 2):
+            for mode, dma in ((0, 1), (1, 0), (1, 1), (2, 1)):
                 eng.set_narrow(mode)
+                eng.set_narrow_dma(dma)
                 with torch.no_grad():
                     for _ in range(3):
                         m.inference(mel)
@@ -51,11 +52,12 @@ def main():
                 row = {"median_ms": round(ts[len(ts) // 2], 4), "min_ms": round(ts[0], 4),
                        "kernel_ms": round(sum(ms for _, ms, _ in t), 4),
                        "launches": int(sum(n for _, _, n in t))}
-                if mode == 1:
+                if mode == 1 and dma == 1:
                     row["ops"] = [(name, round(ms, 4), int(n)) for name, ms, n in t]
-                res[f"{cfg}_T{F}_narrow{mode}"] = row
-                print(cfg, F, mode, {k: v for k, v in row.items() if k != "ops"}, flush=True)
+                res[f"{cfg}_T{F}_narrow{mode}_dma{dma}"] = row
+                print(cfg, F, mode, dma, {k: v for k, v in row.items() if k != "ops"}, flush=True)
             eng.set_narrow(1)
+            eng.set_narrow_dma(1)
     json.dump(res, open(sys.argv[1], "w"), indent=1)
 
 
