@@ -2688,6 +2688,135 @@ __global__ void __launch_bounds__(128) pwg_cnet_thin_kernel(const CnConvArgs a, 
   if (a.range_flag) flag_range(a.range_flag, nullptr, bad, (int)(threadIdx.x & 63));
 }
 
+// One-pass form of pwg_cnet_thin_kernel (the ops whose whole staged input fits THIN1_LDS): the
+// input rows of EVERY 16-channel block of every source and the op's M x 16 weights of every chunk
+// are staged up front, 8 loads per thread in flight per batch, behind one barrier; then the same
+// FMAs in the same order (bit-identical). The per-block form pays a load round trip per block and
+// per 128-quad slice of it plus a scalar weight load per tap (HiFiGAN / MB-MelGAN output convs at
+// B = 1: 17-26 us for a few us of FMAs).
+constexpr int THIN1_LDS = 64 * 1024;
+template <int M>
+__global__ void __launch_bounds__(128) pwg_cnet_thin1_kernel(const CnConvArgs a, int nsrc) {
+  extern __shared__ __attribute__((aligned(16))) float s_x[];  // [src][cb][span][THIN_ROW], then [chunk][h][M][8]
+  const int2 blk = a.blocks[blockIdx.x];
+  const int u = blk.x;
+  const int q = blk.y + threadIdx.x;
+  const bool live = q < a.ncols[u];
+  const int xf0 = a.src[0].nc * a.src[0].span * THIN_ROW;
+  const int xf = xf0 + (nsrc > 1 ? a.src[1].nc * a.src[1].span * THIN_ROW : 0);
+  float* const s_w = s_x + xf;
+  constexpr int B = 8;
+  for (int si = 0; si < nsrc; ++si) {
+    const CnSrc& s = a.src[si];
+    const int2 sg = *reinterpret_cast<const int2*>(s.seg + 2 * u);
+    float* const sx = s_x + (si ? xf0 : 0);
+    const int total = s.nc * s.span * 4;  // quads: [cb][row][quad]
+    for (int b0 = 0; b0 < total; b0 += 128 * B) {
+      f32x4v v[B];
+      bool ok[B];
+#pragma unroll
+      for (int j = 0; j < B; ++j) {
+        const int i = b0 + threadIdx.x + 128 * j;
+        const int ii = i < total ? i : total - 1;
+        const int cb = ii / (s.span * 4), rq = ii - cb * (s.span * 4);
+        int p = blk.y + s.off_min + (rq >> 2);
+        ok[j] = edge_row(p, sg.y, s.pad_mode);
+        v[j] = *reinterpret_cast<const f32x4v*>(s.x + (size_t)(sg.x + p) * s.ld + 16 * cb + 4 * (rq & 3));
+      }
+#pragma unroll
+      for (int j = 0; j < B; ++j) {
+        const int i = b0 + threadIdx.x + 128 * j;
+        if (i >= total) break;
+        const int cb = i / (s.span * 4), rq = i - cb * (s.span * 4);
+        const int ch = 16 * cb + 4 * (rq & 3);
+        f32x4v x = v[j];
+        if (s.normalize) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) x[e] = (x[e] - a.mean[ch + e]) / a.scale[ch + e];
+        }
+        if (s.slope != 1.f) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) x[e] = x[e] > 0.f ? x[e] : x[e] * s.slope;
+        }
+        *reinterpret_cast<f32x4v*>(sx + THIN_ROW * (cb * s.span + (rq >> 2)) + 4 * (rq & 3)) =
+            ok[j] ? x : f32x4v{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  }
+  // weights: chunk c, h, output o -> 8 floats (k-steps 8 h + [0, 8)): sub 0 then sub 1 of lane o + 32 h
+  {
+    const int total = a.n_chunks * 2 * M * 2;  // quads: [chunk][h][o][sub]
+    for (int b0 = 0; b0 < total; b0 += 128 * B) {
+      f32x4v v[B];
+#pragma unroll
+      for (int j = 0; j < B; ++j) {
+        const int i = b0 + threadIdx.x + 128 * j;
+        const int ii = i < total ? i : total - 1;
+        const int sub = ii & 1, o = (ii >> 1) % M, h = ((ii >> 1) / M) & 1, c = (ii >> 1) / M >> 1;
+        v[j] = *reinterpret_cast<const f32x4v*>(a.wfrag + (size_t)c * a.mt_total * 512 + 256 * sub + (o + 32 * h) * 4);
+      }
+#pragma unroll
+      for (int j = 0; j < B; ++j) {
+        const int i = b0 + threadIdx.x + 128 * j;
+        if (i < total) *reinterpret_cast<f32x4v*>(s_w + 4 * i) = v[j];
+      }
+    }
+  }
+  __syncthreads();
+  float acc[M];
+#pragma unroll
+  for (int o = 0; o < M; ++o) acc[o] = 0.f;
+  for (int si = 0; si < nsrc; ++si) {
+    const CnSrc& s = a.src[si];
+    const float* const sx = s_x + (si ? xf0 : 0);
+    for (int cb = 0; cb < s.nc; ++cb) {
+      for (int k = 0; k < s.taps; ++k) {
+        const int c = s.chunk_base + k * s.nc + cb;
+        const int r = threadIdx.x + a.chunks[c].row_off - s.off_min;
+        const float* xr = sx + THIN_ROW * (cb * s.span + r);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f32x4v x0 = *reinterpret_cast<const f32x4v*>(xr + 8 * h);
+          const f32x4v x1 = *reinterpret_cast<const f32x4v*>(xr + 8 * h + 4);
+#pragma unroll
+          for (int o = 0; o < M; ++o) {
+            const f32x4v w0 = *reinterpret_cast<const f32x4v*>(s_w + ((c * 2 + h) * M + o) * 8);
+            const f32x4v w1 = *reinterpret_cast<const f32x4v*>(s_w + ((c * 2 + h) * M + o) * 8 + 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[o] = fmaf(w0[e], x0[e], acc[o]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[o] = fmaf(w1[e], x1[e], acc[o]);
+          }
+        }
+      }
+    }
+  }
+  if (!live) return;
+  const int t = q * a.ostride + a.ophase;
+  const int2 sd = *reinterpret_cast<const int2*>(a.seg_dst + 2 * u);
+  float* yrow = a.y + (size_t)(sd.x + t) * a.ld_dst;
+  const float* rrow = nullptr;
+  if (a.res) {
+    const int2 sr = *reinterpret_cast<const int2*>(a.seg_res + 2 * u);
+    rrow = a.res + (size_t)(sr.x + t) * a.ld_res;
+  }
+  bool bad = false;
+#pragma unroll
+  for (int o = 0; o < M; ++o) {
+    if (o >= a.M) break;
+    float v = acc[o] + a.bias[o];
+    if (rrow) v += rrow[o];
+    if (a.accumulate) v = yrow[o] + v;
+    if (a.out_div != 1.f) v = v / a.out_div;
+    if (a.post_act == PWG_ACT_LRELU) v = v > 0.f ? v : v * a.post_slope;
+    else if (a.post_act == PWG_ACT_TANH) v = tanhf(v);
+    bad |= !__builtin_isfinite(v);
+    yrow[o] = v;
+  }
+  for (int o = a.M; o < a.ld_dst; ++o) yrow[o] = 0.f;
+  if (a.range_flag) flag_range(a.range_flag, nullptr, bad, (int)(threadIdx.x & 63));
+}
+
 // PQMF synthesis (layers/pqmf.py:133-149): y[t] = sum_m sum_k h[m][k] * S * x[(t+k-P)/S][m] over
 // the k with (t+k-P) divisible by S and inside the utterance. One thread per output sample.
 struct CnPqmfArgs {
@@ -2719,12 +2848,33 @@ __global__ void __launch_bounds__(256) pwg_cnet_pqmf_kernel(const CnPqmfArgs a) 
   // subband rows j with S*j in [t0 - P, t0 + 255 + NT - 1 - P]
   const int j0 = (t0 - P) >= 0 ? (t0 - P) / S : -((P - t0 + S - 1) / S);
   const int nrow = (t0 + 255 + NT - 1 - P) / S - j0 + 1;
-  for (int i = threadIdx.x; i < nrow * S; i += 256) {
+  // every load in flight before the first store (the block's only global round trip): rows
+  // nrow * S <= 256 + NT + 2 S <= 2 x 256, filters S * NT <= 4 x 256
+  constexpr int XB = 2, HB = (PQ_MAX_S * PQ_MAX_NT + 255) / 256;
+  float xv[XB], hv[HB];
+#pragma unroll
+  for (int k = 0; k < XB; ++k) {
+    const int i = threadIdx.x + 256 * k;
+    const int r = i / S, m = i - r * S;
+    const int j = j0 + r;
+    xv[k] = (i < nrow * S && j >= 0 && j < ss.y) ? (float)S * a.x[(size_t)(ss.x + j) * a.ld_src + m] : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < HB; ++k) {
+    const int i = threadIdx.x + 256 * k;
+    hv[k] = i < S * NT ? a.h[i] : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < XB; ++k)
+    if (threadIdx.x + 256 * k < nrow * S) s_x[threadIdx.x + 256 * k] = xv[k];
+#pragma unroll
+  for (int k = 0; k < HB; ++k)
+    if (threadIdx.x + 256 * k < S * NT) s_h[threadIdx.x + 256 * k] = hv[k];
+  for (int i = threadIdx.x + 256 * XB; i < nrow * S; i += 256) {  // (not reached within the limits)
     const int r = i / S, m = i - r * S;
     const int j = j0 + r;
     s_x[i] = (j >= 0 && j < ss.y) ? (float)S * a.x[(size_t)(ss.x + j) * a.ld_src + m] : 0.f;
   }
-  for (int i = threadIdx.x; i < S * NT; i += 256) s_h[i] = a.h[i];
   __syncthreads();
   const int t = t0 + threadIdx.x;
   if (t >= sd.y) return;
@@ -3867,7 +4017,20 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         const size_t tl = (size_t)std::max(ph.thin_span[0], ph.thin_span[1]) * THIN_ROW * sizeof(float);
         a.range_flag = op.dst == nb - 1 ? rflag : nullptr;
         out_checked |= op.dst == nb - 1;
-        if (op.out_channels <= 1) hipLaunchKernelGGL(pwg_cnet_thin_kernel<1>, tgrid, tblock, tl, s, a, nsrc);
+        const int mt_ = op.out_channels <= 1 ? 1 : (op.out_channels <= 4 ? 4 : 8);
+        size_t tl1 = (size_t)a.n_chunks * 2 * mt_ * 8 * sizeof(float);
+        for (int si = 0; si < nsrc; ++si) tl1 += (size_t)ph.thin_nc[si] * ph.thin_span[si] * THIN_ROW * sizeof(float);
+        if (tl1 <= (size_t)THIN1_LDS) {
+          auto go = [&](auto kfn) -> hipError_t {
+            const hipError_t e1 = allow_lds(reinterpret_cast<const void*>(kfn), (int)tl1);
+            if (e1 != hipSuccess) return e1;
+            hipLaunchKernelGGL(kfn, tgrid, tblock, tl1, s, a, nsrc);
+            return hipGetLastError();
+          };
+          const hipError_t e1 = mt_ == 1 ? go(pwg_cnet_thin1_kernel<1>)
+                                : mt_ == 4 ? go(pwg_cnet_thin1_kernel<4>) : go(pwg_cnet_thin1_kernel<8>);
+          if (e1 != hipSuccess) return hipf(e1, "thin kernel launch");
+        } else if (op.out_channels <= 1) hipLaunchKernelGGL(pwg_cnet_thin_kernel<1>, tgrid, tblock, tl, s, a, nsrc);
         else if (op.out_channels <= 4) hipLaunchKernelGGL(pwg_cnet_thin_kernel<4>, tgrid, tblock, tl, s, a, nsrc);
         else hipLaunchKernelGGL(pwg_cnet_thin_kernel<8>, tgrid, tblock, tl, s, a, nsrc);
       } else

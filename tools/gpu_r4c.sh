@@ -13,4 +13,6 @@ timeout -k 10 300 python -u tools/diag/voc_lat_ab.py "$OUT/voc_lat_ab.json" > "$
 cat "$OUT/voc_lat_ab.log"
 timeout -k 10 300 python -u tools/diag/launch_floor.py "$OUT/launch_floor.json" > "$OUT/launch_floor.log" 2>&1
 tail -3 "$OUT/launch_floor.log"
+timeout -k 10 300 python -u tools/cnet_profile.py hifigan_v1 --utts 32 --steps 3 > "$OUT/hifigan_batch_ops.txt" 2>&1
+tail -1 "$OUT/hifigan_batch_ops.txt"
 timeout -k 10 900 bash tools/gpu_r4_diag_pwg.sh "$OUT/diag"
