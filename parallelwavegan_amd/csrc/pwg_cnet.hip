@@ -438,6 +438,89 @@ constexpr int XT_COLS = 256;
 constexpr int NARROW_HALO = 64;  // narrow x-tile launches: (K - 1) dil at most this (register budget)
 constexpr int XT_ROWB = 80;  // bytes per staged input row: 16 hi + 16 lo halves + 16 B pad
 
+// One lane's column of MT m-tiles: + bias [+ residual] [+ y_old] [/ div] [act] -> y (the conv
+// kernels' epilogue arithmetic). With quad-aligned rows every bias / residual / y_old load is issued
+// before the first store: the stores may alias the later loads for the compiler, which otherwise
+// serialises one load round trip per 4 rows (MT x 4 of them, ~1 us each at B = 1).
+template <int MT>
+__device__ __forceinline__ void cn_store_col(const CnConvArgs& a, const f32x16 (&acc)[MT], const float* bias_, int m0,
+                                             int hh, float* yrow, const float* rrow) {
+  auto finish = [&](f32x4v v) {
+    if (a.out_div != 1.f) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = v[i] / a.out_div;
+    }
+    if (a.post_act == PWG_ACT_LRELU) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = v[i] > 0.f ? v[i] : v[i] * a.post_slope;
+    } else if (a.post_act == PWG_ACT_TANH) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = tanhf(v[i]);
+    }
+    return v;
+  };
+  if ((a.ld_dst & 3) == 0) {
+    constexpr int GM = MT <= 2 ? MT : 1;  // m-tiles per load group (register budget at MT 3-4)
+#pragma unroll
+    for (int mg = 0; mg < MT; mg += GM) {
+      f32x4v bv[GM][4], rv[GM][4], yv[GM][4];
+#pragma unroll
+      for (int m = 0; m < GM; ++m)
+#pragma unroll
+        for (int j4 = 0; j4 < 4; ++j4) {
+          const int row = 32 * (m0 + mg + m) + 8 * j4 + 4 * hh;
+          const bool live = row < a.M;
+          const f32x4v z = {0.f, 0.f, 0.f, 0.f};
+          bv[m][j4] = live ? *reinterpret_cast<const f32x4v*>(bias_ + row) : z;
+          rv[m][j4] = live && rrow ? *reinterpret_cast<const f32x4v*>(rrow + row) : z;
+          yv[m][j4] = live && a.accumulate ? *reinterpret_cast<const f32x4v*>(yrow + row) : z;
+        }
+#pragma unroll
+      for (int m = 0; m < GM; ++m)
+#pragma unroll
+        for (int j4 = 0; j4 < 4; ++j4) {
+          const int row = 32 * (m0 + mg + m) + 8 * j4 + 4 * hh;
+          if (row >= a.M) {
+            if (row < a.ld_dst) *reinterpret_cast<f32x4v*>(yrow + row) = f32x4v{0.f, 0.f, 0.f, 0.f};
+            continue;
+          }
+          f32x4v v;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = acc[mg + m][4 * j4 + i] + bv[m][j4][i];
+          if (rrow) v += rv[m][j4];
+          if (a.accumulate) v = yv[m][j4] + v;
+          v = finish(v);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (row + i >= a.M) v[i] = 0.f;
+          *reinterpret_cast<f32x4v*>(yrow + row) = v;
+        }
+    }
+    return;
+  }
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int j4 = 0; j4 < 4; ++j4) {
+      const int row = 32 * (m0 + m) + 8 * j4 + 4 * hh;
+      if (row >= a.M) continue;
+      const f32x4v b = *reinterpret_cast<const f32x4v*>(bias_ + row);
+      f32x4v v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = acc[m][4 * j4 + i] + b[i];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (row + i >= a.M) continue;
+        if (rrow) v[i] += rrow[row + i];
+        if (a.accumulate) v[i] = yrow[row + i] + v[i];
+      }
+      v = finish(v);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (row + i < a.M) yrow[row + i] = v[i];
+    }
+}
+
 // SY (synchronous staging): no register prefetch of the next channel block; the kernel is held to
 // 128 VGPRs (4 waves per SIMD) so two workgroups share a CU and one's staging overlaps the other's
 // MFMAs. Same arithmetic and order: bit-identical.
@@ -743,10 +826,9 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
     }
   }
 
-  // epilogue (pwg_cnet_conv_kernel's)
+  // epilogue (pwg_cnet_conv_kernel's arithmetic)
   const int2 sd = *reinterpret_cast<const int2*>(a.seg_dst + 2 * u);
   const int2 sr = a.res ? *reinterpret_cast<const int2*>(a.seg_res + 2 * u) : make_int2(0, 0);
-  const bool quad = (a.ld_dst & 3) == 0;
 #pragma unroll
   for (int nc = 0; nc < NC; ++nc) {
     const int qb = q0 + nc * XC + wave * 32 + cl;
@@ -754,52 +836,7 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
     const int t = qb * a.ostride + ophase_;
     float* yrow = a.y + (size_t)(sd.x + t) * a.ld_dst;
     const float* rrow = a.res ? a.res + (size_t)(sr.x + t) * a.ld_res : nullptr;
-#pragma unroll
-    for (int m = 0; m < MT; ++m)
-#pragma unroll
-      for (int j4 = 0; j4 < 4; ++j4) {
-        const int row = 32 * (m0 + m) + 8 * j4 + 4 * hh;
-        if (row >= a.M) {
-          if (quad && row < a.ld_dst) *reinterpret_cast<f32x4v*>(yrow + row) = f32x4v{0.f, 0.f, 0.f, 0.f};
-          continue;
-        }
-        const f32x4v b = *reinterpret_cast<const f32x4v*>(bias_ + row);
-        f32x4v v;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = acc[nc][m][4 * j4 + i] + b[i];
-        if (quad) {
-          if (rrow) v += *reinterpret_cast<const f32x4v*>(rrow + row);
-          if (a.accumulate) v = *reinterpret_cast<const f32x4v*>(yrow + row) + v;
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            if (row + i >= a.M) continue;
-            if (rrow) v[i] += rrow[row + i];
-            if (a.accumulate) v[i] = yrow[row + i] + v[i];
-          }
-        }
-        if (a.out_div != 1.f) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = v[i] / a.out_div;
-        }
-        if (a.post_act == PWG_ACT_LRELU) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = v[i] > 0.f ? v[i] : v[i] * a.post_slope;
-        } else if (a.post_act == PWG_ACT_TANH) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = tanhf(v[i]);
-        }
-        if (quad) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (row + i >= a.M) v[i] = 0.f;
-          *reinterpret_cast<f32x4v*>(yrow + row) = v;
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (row + i < a.M) yrow[row + i] = v[i];
-        }
-      }
+    cn_store_col<MT>(a, acc[nc], bias_, m0, hh, yrow, rrow);
   }
 }
 
@@ -1021,6 +1058,20 @@ __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArg
   const ChunkDesc* const chunks_ = zp == 0 ? a.chunks : a.z_chunks[zp];
   const int ns = xd.n_steps;
   const int span = K == 1 ? S::XC : S::XC + (K - 1) * xd.dil;
+  // Every global value the loop needs is read here, before the first DMA, into scalar registers:
+  // while an LDS-DMA is outstanding the compiler waits vmcnt(0) at the next use of any ordinary
+  // global load (and at __syncthreads()), which would drain the ring each step
+  // (cdna_hip_programming.md, "Pipelining across barriers"). The loop's barriers are raw s_barriers.
+  int2 sg0 = *reinterpret_cast<const int2*>(a.src[0].seg + 2 * u);
+  int2 sg1 = *reinterpret_cast<const int2*>(a.src[1].seg + 2 * u);
+  sg0.x = __builtin_amdgcn_readfirstlane(sg0.x);
+  sg0.y = __builtin_amdgcn_readfirstlane(sg0.y);
+  sg1.x = __builtin_amdgcn_readfirstlane(sg1.x);
+  sg1.y = __builtin_amdgcn_readfirstlane(sg1.y);
+  auto barrier = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
 
   struct Step {
     int src, c0, off;  // source, first input channel, row offset of tap 0
@@ -1053,7 +1104,7 @@ __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArg
     }
     const Step st = step_of(s);
     const CnSrc& sx = a.src[st.src];
-    const int2 sg = *reinterpret_cast<const int2*>(sx.seg + 2 * u);
+    const int2 sg = st.src ? sg1 : sg0;
 #pragma unroll
     for (int k = 0; k < S::DX; ++k) {
       int i = wave + NWV * k;
@@ -1070,7 +1121,7 @@ __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArg
     unsigned char* const cb = s_cb + (size_t)(s & 1) * S::CBUF;
     const Step st = step_of(s);
     const CnSrc& sx = a.src[st.src];
-    const int2 sg = *reinterpret_cast<const int2*>(sx.seg + 2 * u);
+    const int2 sg = st.src ? sg1 : sg0;
     constexpr int NQ = (S::XR * 4 + NTH - 1) / NTH;
 #pragma unroll
     for (int i = 0; i < NQ; ++i) {
@@ -1080,11 +1131,7 @@ __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArg
       int p = q0 + st.off + r;
       const bool ok = edge_row(p, sg.y, sx.pad_mode);
       f32x4v v = *reinterpret_cast<const f32x4v*>(raw + r * 64 + qd * 16);
-      const int ch = st.c0 + 4 * qd;
-      if (sx.normalize) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = (v[e] - a.mean[ch + e]) / a.scale[ch + e];
-      }
+      // (no normalize: ops that normalize their input run the narrow x-tile kernel)
       if (sx.slope != 1.f) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * sx.slope;
@@ -1133,20 +1180,20 @@ __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArg
   for (int s = 0; s < P - 1; ++s)
     if (s < ns) issue(s);
   vm_wait_steps<0, S::D, P - 2>(ns - 1);
-  __syncthreads();
+  barrier();
   convert(0);
-  __syncthreads();
+  barrier();
   for (int g = 0; g < ns; ++g) {
     // slot (g - 1) % P: read by step g - 1's MFMAs and conversion, both before the last barrier
     if (g + P - 1 < ns) issue(g + P - 1);
     // step g + 1 landed (step g did before the last barrier)
     if (g + 1 < ns) {
       vm_wait_steps<0, S::D, P - 2>(ns - 2 - g);
-      __syncthreads();
+      barrier();
     }
     mma(g);
     if (g + 1 < ns) convert(g + 1);  // into the buffer step g - 1's MFMAs read
-    __syncthreads();
+    barrier();
   }
 
   // epilogue (pwg_cnet_xtile_kernel's)
@@ -1154,56 +1201,10 @@ __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArg
   if (qb >= nq) return;
   const int2 sd = *reinterpret_cast<const int2*>(a.seg_dst + 2 * u);
   const int2 sr = a.res ? *reinterpret_cast<const int2*>(a.seg_res + 2 * u) : make_int2(0, 0);
-  const bool quad = (a.ld_dst & 3) == 0;
   const int t = qb * a.ostride + a.ophase + zp;
   float* yrow = a.y + (size_t)(sd.x + t) * a.ld_dst;
   const float* rrow = a.res ? a.res + (size_t)(sr.x + t) * a.ld_res : nullptr;
-#pragma unroll
-  for (int m = 0; m < MT; ++m)
-#pragma unroll
-    for (int j4 = 0; j4 < 4; ++j4) {
-      const int row = 32 * (m0 + m) + 8 * j4 + 4 * hh;
-      if (row >= a.M) {
-        if (quad && row < a.ld_dst) *reinterpret_cast<f32x4v*>(yrow + row) = f32x4v{0.f, 0.f, 0.f, 0.f};
-        continue;
-      }
-      const f32x4v b = *reinterpret_cast<const f32x4v*>(bias_ + row);
-      f32x4v v;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = acc[m][4 * j4 + i] + b[i];
-      if (quad) {
-        if (rrow) v += *reinterpret_cast<const f32x4v*>(rrow + row);
-        if (a.accumulate) v = *reinterpret_cast<const f32x4v*>(yrow + row) + v;
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          if (row + i >= a.M) continue;
-          if (rrow) v[i] += rrow[row + i];
-          if (a.accumulate) v[i] = yrow[row + i] + v[i];
-        }
-      }
-      if (a.out_div != 1.f) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = v[i] / a.out_div;
-      }
-      if (a.post_act == PWG_ACT_LRELU) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = v[i] > 0.f ? v[i] : v[i] * a.post_slope;
-      } else if (a.post_act == PWG_ACT_TANH) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = tanhf(v[i]);
-      }
-      if (quad) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (row + i >= a.M) v[i] = 0.f;
-        *reinterpret_cast<f32x4v*>(yrow + row) = v;
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (row + i < a.M) yrow[row + i] = v[i];
-      }
-    }
+  cn_store_col<MT>(a, acc, bias_, m0, hh, yrow, rrow);
 }
 
 template <int K, int MT, int NWV>
@@ -4075,7 +4076,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
           const dim3 ngrid((unsigned)p->n_nblocks[pi], (unsigned)(ph.mt_total / mtn), (unsigned)ph.z_phases);
           if (p->n_nblocks[pi] == 0) {
             ea2 = hipSuccess;
-          } else if (n->narrow_dma) {
+          } else if (n->narrow_dma && !a.src[0].normalize) {
             CnXdmaArgs xd;
             xd.dil = xt.dil; xd.cs = xt.cs; xd.n_steps = xt.cs; xd.rev = xt.rev;
             for (int r = 0; r < 8; ++r) xd.z_off[r] = xt.z_off[r];
@@ -4095,7 +4096,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         a.blocks = p->d_nblocks[pi];
         const int nw = p->nar_nwv[pi], mtn = p->nar_mt[pi];
         const dim3 ngrid((unsigned)p->n_nblocks[pi], (unsigned)(ph.mt_total / mtn), (unsigned)ph.z_phases);
-        if (n->narrow_dma) {
+        if (n->narrow_dma && !a.src[0].normalize && !a.src[1].normalize) {
           CnXdmaArgs xd;  // K = 1 mode: the chunk list, each chunk at its own source and row offset
           xd.dil = 1; xd.cs = 0; xd.n_steps = a.n_chunks; xd.rev = 0;
           for (int r = 0; r < 8; ++r) xd.z_off[r] = 0;

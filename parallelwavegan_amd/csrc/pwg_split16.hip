@@ -20,12 +20,6 @@
 // Reference: layers/residual_block.py:102-140, models/parallel_wavegan.py:131-138,160-171.
 #include "pwg_internal.h"
 
-// A/B build switch (round 4, temporary): where the next work unit's tap-0 row is loaded.
-// 0: during the center tap's MFMAs (into b1); 1: after the GEMM-2 seeds (into b0, dead by then);
-// 2: just before GEMM 2 (into b0).
-#ifndef PWG_S16_PF
-#define PWG_S16_PF 0
-#endif
 
 namespace pwg {
 
@@ -352,7 +346,6 @@ __device__ __forceinline__ void s16_block(const SplitArgs& a, const unsigned* sm
   s16_load_dv(a, bd, dv, g, c);
   s16_bload<TC, FIRST, PIPE, NTN>(a, s_fwb, bd, TC, b0, g, c, h16);
   mma_tap(acc, b1, T1);
-  if (PWG_S16_PF == 0 && has_next) s16_bload<TC, FIRST, PIPE, NTN>(a, s_fwb, bdn, 0, b1, g, c, h16n);  // the next block's
   mma_tap(acc, b0, TC);
   if (!LAST) {
     // GEMM-2 out-row seeds sqrt(.5)(x + b_out) from the center tap: acc2[4 + 2ks + (j>>2)][nt][j&3]
@@ -367,7 +360,6 @@ __device__ __forceinline__ void s16_block(const SplitArgs& a, const unsigned* sm
         for (int j = 0; j < 8; ++j) acc2[4 + 2 * ks + (j >> 2)][nt][j & 3] = o[j];
       }
   }
-  if (PWG_S16_PF == 1 && has_next) s16_bload<TC, FIRST, PIPE, NTN>(a, s_fwb, bdn, 0, b0, g, c, h16n);
   mid();
 
   {
@@ -416,7 +408,11 @@ __device__ __forceinline__ void s16_block(const SplitArgs& a, const unsigned* sm
       split8x<0>(gv, gh[nt][ks], gl[nt][ks]);
     }
 
-  if (PWG_S16_PF == 2 && has_next) s16_bload<TC, FIRST, PIPE, NTN>(a, s_fwb, bdn, 0, b0, g, c, h16n);
+  // the next work unit's tap-0 row, into b0 (dead since the seeds): loaded here, just before
+  // GEMM 2, its rows are still in L2 (round 4 per-layer PMC: loading it during the center tap's
+  // MFMAs, ~0.7 unit-times earlier, re-read 1.30-1.38x the algorithmic bytes from HBM, here
+  // 1.02-1.13x; tools/diag/layer_fetch.sh)
+  if (has_next) s16_bload<TC, FIRST, PIPE, NTN>(a, s_fwb, bdn, 0, b0, g, c, h16n);
   // ---- GEMM 2: [skip; out] rows, 8 m-tiles (last layer: the 4 skip tiles)
   constexpr int M2 = LAST ? 4 : 8;
   const u32x4* w2l = reinterpret_cast<const u32x4*>(s_w2) + lane;
@@ -673,10 +669,6 @@ __global__ void __launch_bounds__(512, 1) pwg_layer_split16_kernel(const SplitAr
     if (nblk < 0) break;
     blk = nblk;
     nblk = ticket_resolve(ticket);
-    if (PWG_S16_PF == 0) {
-      b0[0] = b1[0]; b0[1] = b1[1]; b0[2] = b1[2]; b0[3] = b1[3];
-      b0[4] = b1[4]; b0[5] = b1[5]; b0[6] = b1[6]; b0[7] = b1[7];
-    }
   }
   if (LAST && nonfinite && a.range_flag) flag_status(a.range_flag, a.sticky, PWG_STATUS_RANGE);
   trace_out();
@@ -826,9 +818,6 @@ __device__ __forceinline__ void sync_layer(const SplitArgs& a, const unsigned* s
     u = un;
     bd = bdn;
     h16 = h16n;
-#pragma unroll
-    for (int q = 0; q < 8; ++q)
-      if (PWG_S16_PF == 0) b0[q] = b1[q];
   }
 }
 
