@@ -141,13 +141,20 @@ PWG_API int pwg_cnet_run_status(PwgCnetPlan* p, const void* workspace, void* str
  * op spreads over every CU (the B = 1 decode path, bin/decode.py:236-268); a fused pair or stack
  * whose first conv runs narrow runs as its two ops. Bit-identical to the default launches.
  * 0: never; 2: every x-tile launch (tests).
- * PWG_CNET_OPT_NARROW_DMA (default 1): narrow launches run the DMA-ring kernel: every step (a
- * 16-channel block with all its taps, or one chunk of a tap-major op) is staged by global_load_lds
- * a few steps ahead of its MFMAs, the input rows pre-activated LDS -> LDS; also takes the narrow
- * launches of tap-major convs (MelGAN's two-source 1x1s). Bit-identical to 0 (the DMA-staged narrow
- * x-tile kernel and the narrow tap-major kernel), which stays for A/B. */
+ * PWG_CNET_OPT_NARROW_DMA (default 1, plans created afterwards): narrow launches run the DMA-ring
+ * kernel (one m-tile, 1-4 waves per workgroup): every step (a 16-channel block with all its taps,
+ * or one chunk of a tap-major op) is staged by global_load_lds a few steps ahead of its MFMAs, the
+ * input rows pre-activated LDS -> LDS; also takes the narrow launches of tap-major convs (MelGAN's
+ * two-source 1x1s). Bit-identical to 0 (the DMA-staged narrow x-tile kernel and the narrow
+ * tap-major kernel, sized as described above), which stays for A/B.
+ * PWG_CNET_OPT_STREAMS (default 1): launches that do not depend on each other (HiFiGAN's parallel
+ * residual blocks, models/hifigan.py:159-168) run concurrently on up to 3 auxiliary streams of the
+ * handle, forked from and joined back into the caller's stream with events (graph-capturable):
+ * 1 for plans with narrow launches (latency-bound small plans), 2 for every plan, 0 never.
+ * The accumulated sum's writers stay in program order: bit-identical to one stream. */
 enum { PWG_CNET_OPT_SPLIT_F16 = 0, PWG_CNET_OPT_FUSE_PAIRS = 1, PWG_CNET_OPT_PAIR_STEPS = 2, PWG_CNET_OPT_XTILE = 3,
-       PWG_CNET_OPT_XT_DMA = 4, PWG_CNET_OPT_XCD_ORDER = 5, PWG_CNET_OPT_NARROW = 6, PWG_CNET_OPT_NARROW_DMA = 7 };
+       PWG_CNET_OPT_XT_DMA = 4, PWG_CNET_OPT_XCD_ORDER = 5, PWG_CNET_OPT_NARROW = 6, PWG_CNET_OPT_NARROW_DMA = 7,
+       PWG_CNET_OPT_STREAMS = 8 };
 PWG_API int pwg_cnet_set_option(PwgCnet* n, int option, long long value);
 PWG_API int pwg_cnet_set_timing(PwgCnet* n, int enable);
 /* Adds per-op milliseconds and launch counts (arrays of n_ops) and clears the records. */

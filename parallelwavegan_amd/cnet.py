@@ -432,10 +432,17 @@ class CnetEngine:
         _lib.check(self._lib.pwg_cnet_set_option(self._h, 6, int(mode)))
         self._plans.clear()
 
+    def set_streams(self, mode):
+        """pwg_cnet_set_option(PWG_CNET_OPT_STREAMS): independent launches on auxiliary streams
+        for plans with narrow launches (1, default), every plan (2) or never (0). Bit-identical."""
+        _lib.check(self._lib.pwg_cnet_set_option(self._h, 8, int(mode)))
+
     def set_narrow_dma(self, enable):
         """pwg_cnet_set_option(PWG_CNET_OPT_NARROW_DMA): narrow launches on the DMA-ring kernel
-        (default) or, 0, on the narrow x-tile / tap-major kernels. Run time; bit-identical."""
+        (default) or, 0, on the narrow x-tile / tap-major kernels. Plan-time (cached plans are
+        dropped); bit-identical."""
         _lib.check(self._lib.pwg_cnet_set_option(self._h, 7, 1 if enable else 0))
+        self._plans.clear()
 
     def set_pair_steps(self, steps):
         """pwg_cnet_set_option(PWG_CNET_OPT_PAIR_STEPS): 128-column tiles per fused-pair

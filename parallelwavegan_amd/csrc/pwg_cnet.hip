@@ -1000,7 +1000,15 @@ struct CnXdmaArgs {
   int n_steps;    // K > 1: cs; K = 1: chunks of the op (pwg_cnet_conv_kernel's list)
   int rev;        // ConvTranspose phases: tap t multiplies weight chunk K-1-t
   int z_off[8];   // K > 1: row offset of tap 0 for phase blockIdx.z
+  int probe_slot; // PWG_XDMA_PROBE builds only (timeline of workgroup 0, tools/diag/xdma_probe.py)
+  const int2* bfr;  // per block: (first frame, frames) of its utterance
+  int rate[2], rate_dst, rate_res;  // rows per frame of the sources', destination and residual buffers
 };
+constexpr int XDMA_CHUNKS_MAX = 256;  // K = 1 mode: chunks per op (the table sits in LDS)
+#ifdef PWG_XDMA_PROBE
+constexpr int XDMA_PROBE_SLOTS = 128, XDMA_PROBE_N = 96;
+__device__ unsigned long long g_xdma_probe[XDMA_PROBE_SLOTS][XDMA_PROBE_N];
+#endif
 template <int K, int MT, int NWV>
 struct XdmaShape {
   static constexpr int XC = 32 * NWV;
@@ -1009,13 +1017,15 @@ struct XdmaShape {
   static constexpr int DA = (NA + NWV - 1) / NWV, DX = (NX + NWV - 1) / NWV;  // ... per wave
   static constexpr int D = DA + DX;
   static constexpr int SLOT = (NX + NA) * 1024;                // raw rows, then A fragments
-  static constexpr int CBUF = XR * XT_ROWB;                    // one converted-row buffer
-  // deepest ring (<= 6 slots) whose wait counts fit vmcnt (63) and whose LDS fits 152 KB
+  // K > 1: two converted-row buffers; K = 1: none (B split in registers) but the chunk table
+  static constexpr int CBUF = K == 1 ? 0 : XR * XT_ROWB;
+  static constexpr int CHT = K == 1 ? XDMA_CHUNKS_MAX * (int)sizeof(ChunkDesc) : 0;
+  // deepest ring (<= 16 slots) whose wait counts fit vmcnt (63) and whose LDS fits 159 KB
   static constexpr int ring(int p) {
-    return p <= 2 ? 2 : (((p - 2) * D <= 63 && p * SLOT + 2 * CBUF <= 152 * 1024) ? p : ring(p - 1));
+    return p <= 2 ? 2 : (((p - 2) * D <= 63 && p * SLOT + 2 * CBUF + CHT <= 159 * 1024) ? p : ring(p - 1));
   }
-  static constexpr int P = ring(6);
-  static constexpr int LDS = P * SLOT + 2 * CBUF;
+  static constexpr int P = ring(16);
+  static constexpr int LDS = P * SLOT + 2 * CBUF + CHT;
   static_assert(LDS <= 160 * 1024, "DMA-ring shape");
 };
 template <int N>
@@ -1040,17 +1050,24 @@ template <int K, int MT, int NWV>
 __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArgs a, const CnXdmaArgs xd) {
   using S = XdmaShape<K, MT, NWV>;
   constexpr int NTH = 64 * NWV, P = S::P;
+  constexpr int NQ = (S::XR * 4 + NTH - 1) / NTH;  // raw 16-B quads converted per thread and step
   extern __shared__ __attribute__((aligned(16))) unsigned char xt_smem[];
   unsigned char* const s_cb = xt_smem + (size_t)P * S::SLOT;  // [2][XR][XT_ROWB]
+  typedef __attribute__((address_space(1))) void* gptr_t;
+  typedef __attribute__((address_space(3))) void* lptr_t;
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int hh = lane >> 5;
   const int cl = lane & 31;
   const TileId tid = xcd_tile(a.xcd_order);
+  // The block and its utterance's (first frame, frames): with the buffers' rates that gives every
+  // row range and the column count without a dependent second load. Every global value the loop
+  // needs is read here, before the first DMA: while an LDS-DMA is outstanding the compiler waits
+  // vmcnt(0) at the next use of any ordinary global load (and at __syncthreads()), which would drain
+  // the ring (cdna_hip_programming.md, "Pipelining across barriers"); the loop's barriers are raw.
   const int2 blk = a.blocks[tid.x];
-  const int u = blk.x;
+  const int2 fr = xd.bfr[tid.x];
   const int q0 = blk.y;
-  const int nq = a.ncols[u];
   const int m0 = tid.y * MT;
   const int zp = tid.z;
   const float* const wfrag_ = zp == 0 ? a.wfrag : a.z_wfrag[zp];
@@ -1058,90 +1075,136 @@ __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArg
   const ChunkDesc* const chunks_ = zp == 0 ? a.chunks : a.z_chunks[zp];
   const int ns = xd.n_steps;
   const int span = K == 1 ? S::XC : S::XC + (K - 1) * xd.dil;
-  // Every global value the loop needs is read here, before the first DMA, into scalar registers:
-  // while an LDS-DMA is outstanding the compiler waits vmcnt(0) at the next use of any ordinary
-  // global load (and at __syncthreads()), which would drain the ring each step
-  // (cdna_hip_programming.md, "Pipelining across barriers"). The loop's barriers are raw s_barriers.
-  int2 sg0 = *reinterpret_cast<const int2*>(a.src[0].seg + 2 * u);
-  int2 sg1 = *reinterpret_cast<const int2*>(a.src[1].seg + 2 * u);
-  sg0.x = __builtin_amdgcn_readfirstlane(sg0.x);
-  sg0.y = __builtin_amdgcn_readfirstlane(sg0.y);
-  sg1.x = __builtin_amdgcn_readfirstlane(sg1.x);
-  sg1.y = __builtin_amdgcn_readfirstlane(sg1.y);
+  const int sgx0 = fr.x * xd.rate[0], sgy0 = fr.y * xd.rate[0];
+  const int sgx1 = fr.x * xd.rate[1], sgy1 = fr.y * xd.rate[1];
   auto barrier = [] {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   };
 
-  struct Step {
-    int src, c0, off;  // source, first input channel, row offset of tap 0
-  };
-  auto step_of = [&](int s) -> Step {
-    if constexpr (K == 1) {
-      const ChunkDesc cd = chunks_[s];
-      return {cd.src, cd.c0, cd.row_off};
-    } else {
-      return {0, 16 * s, xd.z_off[zp]};
+  // epilogue operands (bias, residual, y_old) in flight from the start (pwg_cnet_conv_kernel's
+  // epilogue arithmetic; quad-aligned destinations, else loaded at the end)
+  const int nq = (fr.y * xd.rate_dst - a.ophase + a.ostride - 1) / a.ostride;
+  const int qb = q0 + wave * 32 + cl;
+  const int t_out = qb * a.ostride + a.ophase + zp;
+  float* const yrow = a.y + (size_t)(fr.x * xd.rate_dst + t_out) * a.ld_dst;
+  const float* const rrow = a.res ? a.res + (size_t)(fr.x * xd.rate_res + t_out) * a.ld_res : nullptr;
+  const bool quad = (a.ld_dst & 3) == 0;
+  f32x4v bv[MT][4], rv[MT][4], yv[MT][4];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int j4 = 0; j4 < 4; ++j4) {
+      const int row = 32 * (m0 + m) + 8 * j4 + 4 * hh;
+      const bool live = quad && qb < nq && row < a.M;
+      const f32x4v z = {0.f, 0.f, 0.f, 0.f};
+      bv[m][j4] = live ? *reinterpret_cast<const f32x4v*>(bias_ + row) : z;
+      rv[m][j4] = live && rrow ? *reinterpret_cast<const f32x4v*>(rrow + row) : z;
+      yv[m][j4] = live && a.accumulate ? *reinterpret_cast<const f32x4v*>(yrow + row) : z;
     }
+
+  // K > 1: the rows every step stages are the same (only the channel block moves): per-lane row
+  // offsets of this wave's raw-row DMA instructions and the edge mask of its converted quads, once
+  const CnSrc& s0 = a.src[0];
+  const int off0 = xd.z_off[zp];
+  int xoff[S::DX];
+  unsigned okm = 0;
+  if constexpr (K > 1) {
+#pragma unroll
+    for (int k = 0; k < S::DX; ++k) {
+      const int i = wave + NWV * k < S::NX ? wave + NWV * k : S::NX - 1;
+      int p = q0 + off0 + 16 * i + (lane >> 2);
+      (void)edge_row(p, sgy0, s0.pad_mode);
+      xoff[k] = (sgx0 + p) * s0.ld + 4 * (lane & 3);
+    }
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+      const int r = (int)(threadIdx.x + NTH * i) >> 2;
+      int p = q0 + off0 + r;
+      if (r < span && edge_row(p, sgy0, s0.pad_mode)) okm |= 1u << i;
+    }
+  }
+
+  // K = 1: the op's chunk list, staged in LDS before the first DMA (one ordinary load round trip)
+  ChunkDesc* const s_ch = reinterpret_cast<ChunkDesc*>(xt_smem + (size_t)P * S::SLOT + 2 * S::CBUF);
+  if constexpr (K == 1) {
+    for (int c = threadIdx.x; c < ns; c += NTH) s_ch[c] = chunks_[c];
+    __syncthreads();
+  }
+  auto chunk = [&](int s) -> ChunkDesc {
+    ChunkDesc c = s_ch[s];
+    c.src = __builtin_amdgcn_readfirstlane(c.src);
+    c.row_off = __builtin_amdgcn_readfirstlane(c.row_off);
+    c.c0 = __builtin_amdgcn_readfirstlane(c.c0);
+    return c;
   };
-  typedef __attribute__((address_space(1))) void* gptr_t;
-  typedef __attribute__((address_space(3))) void* lptr_t;
+
   // step s -> slot s % P: DA A-fragment then DX raw-row instructions per wave (uniform counts: the
   // last instruction of a kind is repeated by waves past the end, same bytes to the same place), so
-  // a wait for a step's rows covers its A fragments too
+  // a wait for a step's rows covers its A fragments too. Addresses: a scalar base + the lane's offset.
   auto issue = [&](int s) {
     unsigned char* const slot = xt_smem + (size_t)(s % P) * S::SLOT;
-    unsigned char* const sa = slot + S::NX * 1024;
 #pragma unroll
     for (int k = 0; k < S::DA; ++k) {
-      int i = wave + NWV * k;
-      i = i < S::NA ? i : S::NA - 1;
+      const int i = wave + NWV * k < S::NA ? wave + NWV * k : S::NA - 1;
       const int tl = i / (MT * 2), j = i - tl * (MT * 2);
       const int wt = xd.rev ? K - 1 - tl : tl;
       const int chunk = K == 1 ? s : wt * xd.cs + s;
-      const float* src = wfrag_ + ((size_t)chunk * a.mt_total + m0) * 512 + j * 256 + lane * 4;
-      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(sa + (size_t)i * 1024), 16, 0, 0);
+      const float* src = wfrag_ + ((size_t)chunk * a.mt_total + m0) * 512 + j * 256;
+      __builtin_amdgcn_global_load_lds((gptr_t)(src + lane * 4), (lptr_t)(slot + (S::NX + i) * 1024), 16, 0, 0);
     }
-    const Step st = step_of(s);
-    const CnSrc& sx = a.src[st.src];
-    const int2 sg = st.src ? sg1 : sg0;
+    if constexpr (K > 1) {
+      const float* const xs = s0.x + 16 * s;
 #pragma unroll
-    for (int k = 0; k < S::DX; ++k) {
-      int i = wave + NWV * k;
-      i = i < S::NX ? i : S::NX - 1;
-      int p = q0 + st.off + 16 * i + (lane >> 2);
-      (void)edge_row(p, sg.y, sx.pad_mode);
-      const float* src = sx.x + (size_t)(sg.x + p) * sx.ld + st.c0 + 4 * (lane & 3);
-      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(slot + (size_t)i * 1024), 16, 0, 0);
+      for (int k = 0; k < S::DX; ++k) {
+        const int i = wave + NWV * k < S::NX ? wave + NWV * k : S::NX - 1;
+        __builtin_amdgcn_global_load_lds((gptr_t)(xs + xoff[k]), (lptr_t)(slot + i * 1024), 16, 0, 0);
+      }
+    } else {
+      const ChunkDesc cd = chunk(s);
+      const CnSrc& sx = a.src[cd.src];
+      const int sgx = cd.src ? sgx1 : sgx0, sgy = cd.src ? sgy1 : sgy0;
+#pragma unroll
+      for (int k = 0; k < S::DX; ++k) {
+        const int i = wave + NWV * k < S::NX ? wave + NWV * k : S::NX - 1;
+        int p = q0 + cd.row_off + 16 * i + (lane >> 2);
+        (void)edge_row(p, sgy, sx.pad_mode);
+        const float* src = sx.x + (size_t)(sgx + p) * sx.ld + cd.c0 + 4 * (lane & 3);
+        __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(slot + i * 1024), 16, 0, 0);
+      }
     }
   };
-  // raw rows of step s -> converted-row buffer s & 1 (pwg_cnet_xtile_kernel's xstore arithmetic)
+  // raw rows of step s -> converted-row buffer s & 1 (pwg_cnet_xtile_kernel's xstore arithmetic):
+  // every read first, then the stores (they may alias the reads for the compiler)
   auto convert = [&](int s) {
     const unsigned char* const raw = xt_smem + (size_t)(s % P) * S::SLOT;
     unsigned char* const cb = s_cb + (size_t)(s & 1) * S::CBUF;
-    const Step st = step_of(s);
-    const CnSrc& sx = a.src[st.src];
-    const int2 sg = st.src ? sg1 : sg0;
-    constexpr int NQ = (S::XR * 4 + NTH - 1) / NTH;
+    const float slope = s0.slope;
+    const unsigned ok = okm;
+    f32x4v v[NQ];
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+      const int idx = threadIdx.x + NTH * i;
+      v[i] = (idx >> 2) < span ? *reinterpret_cast<const f32x4v*>(raw + (idx >> 2) * 64 + (idx & 3) * 16)
+                               : f32x4v{0.f, 0.f, 0.f, 0.f};
+    }
 #pragma unroll
     for (int i = 0; i < NQ; ++i) {
       const int idx = threadIdx.x + NTH * i;
       const int r = idx >> 2, qd = idx & 3;
       if (r >= span) continue;
-      int p = q0 + st.off + r;
-      const bool ok = edge_row(p, sg.y, sx.pad_mode);
-      f32x4v v = *reinterpret_cast<const f32x4v*>(raw + r * 64 + qd * 16);
+      f32x4v x = v[i];
       // (no normalize: ops that normalize their input run the narrow x-tile kernel)
-      if (sx.slope != 1.f) {
+      if (slope != 1.f) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : v[e] * sx.slope;
+        for (int e = 0; e < 4; ++e) x[e] = x[e] > 0.f ? x[e] : x[e] * slope;
       }
-      if (!ok) v = f32x4v{0.f, 0.f, 0.f, 0.f};
+      if (!((ok >> i) & 1u)) x = f32x4v{0.f, 0.f, 0.f, 0.f};
       _Float16 hv[4], lv[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        hv[e] = (_Float16)v[e];
-        lv[e] = (_Float16)(v[e] - (float)hv[e]);
+        hv[e] = (_Float16)x[e];
+        lv[e] = (_Float16)(x[e] - (float)hv[e]);
       }
       unsigned char* row = cb + (size_t)r * XT_ROWB;
       *reinterpret_cast<f16x4v*>(row + 8 * qd) = f16x4v{hv[0], hv[1], hv[2], hv[3]};
@@ -1154,62 +1217,165 @@ __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArg
   for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
+  // one step's MFMAs: every operand read first, then the MFMAs in pwg_cnet_xtile_kernel's order
   auto mma = [&](int g) {
     const unsigned char* const cb = s_cb + (size_t)(g & 1) * S::CBUF;
     const u32x4v* const sa =
         reinterpret_cast<const u32x4v*>(xt_smem + (size_t)(g % P) * S::SLOT + S::NX * 1024) + lane;
+    u32x4v bh[K], bl[K], ah[K][MT], al[K][MT];
 #pragma unroll
     for (int t = 0; t < K; ++t) {
-      const unsigned char* row = cb + (size_t)(wave * 32 + cl + (K == 1 ? 0 : t * xd.dil)) * XT_ROWB;
-      const u32x4v bh = *reinterpret_cast<const u32x4v*>(row + 16 * hh);
-      const u32x4v bl = *reinterpret_cast<const u32x4v*>(row + 32 + 16 * hh);
+      if constexpr (K == 1) {
+        // the lane's 8 channels of its raw row, pre-activated and pair-split in registers
+        // (pwg_cnet_conv_kernel's bprep + cn_split8)
+        const ChunkDesc cd = chunk(g);
+        const CnSrc& sx = a.src[cd.src];
+        const int r = wave * 32 + cl;
+        int p = q0 + cd.row_off + r;
+        const bool okr = edge_row(p, cd.src ? sgy1 : sgy0, sx.pad_mode);
+        const unsigned char* const raw = xt_smem + (size_t)(g % P) * S::SLOT + r * 64 + 32 * hh;
+        const f32x4v v0 = *reinterpret_cast<const f32x4v*>(raw), v1 = *reinterpret_cast<const f32x4v*>(raw + 16);
+        f32x8v x = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+        if (sx.slope != 1.f) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) x[e] = x[e] > 0.f ? x[e] : x[e] * sx.slope;
+        }
+        if (!okr) x = f32x8v{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        cn_split8(x, bh[t], bl[t]);
+      } else {
+        const unsigned char* row = cb + (size_t)(wave * 32 + cl + t * xd.dil) * XT_ROWB;
+        bh[t] = *reinterpret_cast<const u32x4v*>(row + 16 * hh);
+        bl[t] = *reinterpret_cast<const u32x4v*>(row + 32 + 16 * hh);
+      }
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
-        const u32x4v ah = sa[(t * MT * 2 + m * 2) * 64], al = sa[(t * MT * 2 + m * 2 + 1) * 64];
-        acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, ah), __builtin_bit_cast(f16x8v, bh),
-                                                        acc[m], 0, 0, 0);
-        acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, ah), __builtin_bit_cast(f16x8v, bl),
-                                                        acc[m], 0, 0, 0);
-        acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, al), __builtin_bit_cast(f16x8v, bh),
-                                                        acc[m], 0, 0, 0);
+        ah[t][m] = sa[(t * MT * 2 + m * 2) * 64];
+        al[t][m] = sa[(t * MT * 2 + m * 2 + 1) * 64];
       }
     }
+#pragma unroll
+    for (int t = 0; t < K; ++t)
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, ah[t][m]),
+                                                        __builtin_bit_cast(f16x8v, bh[t]), acc[m], 0, 0, 0);
+        acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, ah[t][m]),
+                                                        __builtin_bit_cast(f16x8v, bl[t]), acc[m], 0, 0, 0);
+        acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, al[t][m]),
+                                                        __builtin_bit_cast(f16x8v, bh[t]), acc[m], 0, 0, 0);
+      }
   };
 
+#ifdef PWG_XDMA_PROBE
+  // shader-clock stamps of workgroup (0, 0, 0), wave 0, kept in the LDS tail (no stores in flight)
+  unsigned long long* const s_probe = reinterpret_cast<unsigned long long*>(xt_smem + S::LDS);
+  const bool probe = xd.probe_slot >= 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0;
+  int np = 0;
+  auto stamp = [&] {
+    if (probe && np < XDMA_PROBE_N - 1) s_probe[np++] = __builtin_readcyclecounter();
+  };
+#else
+  auto stamp = [] {};
+#endif
+  stamp();
   // steps 0 .. P-2 in flight; wait for step 0 (the later steps may still land)
   for (int s = 0; s < P - 1; ++s)
     if (s < ns) issue(s);
+  stamp();
+  if constexpr (K == 1) {
+    // one barrier per step: after it every wave is done with step g - 1's slot, which the issue of
+    // step g + P - 1 refills
+    for (int g = 0; g < ns; ++g) {
+      vm_wait_steps<0, S::D, P - 2>(ns - 1 - g);
+      barrier();
+      stamp();
+      if (g + P - 1 < ns) issue(g + P - 1);
+      stamp();
+      mma(g);
+      stamp();
+      stamp();
+    }
+  } else {
   vm_wait_steps<0, S::D, P - 2>(ns - 1);
   barrier();
+  stamp();
   convert(0);
   barrier();
+  stamp();
   for (int g = 0; g < ns; ++g) {
     // slot (g - 1) % P: read by step g - 1's MFMAs and conversion, both before the last barrier
     if (g + P - 1 < ns) issue(g + P - 1);
+    stamp();
     // step g + 1 landed (step g did before the last barrier)
     if (g + 1 < ns) {
       vm_wait_steps<0, S::D, P - 2>(ns - 2 - g);
       barrier();
     }
+    stamp();
     mma(g);
+    stamp();
     if (g + 1 < ns) convert(g + 1);  // into the buffer step g - 1's MFMAs read
     barrier();
+    stamp();
+  }
   }
 
-  // epilogue (pwg_cnet_xtile_kernel's)
-  const int qb = q0 + wave * 32 + cl;
-  if (qb >= nq) return;
-  const int2 sd = *reinterpret_cast<const int2*>(a.seg_dst + 2 * u);
-  const int2 sr = a.res ? *reinterpret_cast<const int2*>(a.seg_res + 2 * u) : make_int2(0, 0);
-  const int t = qb * a.ostride + a.ophase + zp;
-  float* yrow = a.y + (size_t)(sd.x + t) * a.ld_dst;
-  const float* rrow = a.res ? a.res + (size_t)(sr.x + t) * a.ld_res : nullptr;
-  cn_store_col<MT>(a, acc, bias_, m0, hh, yrow, rrow);
+  // epilogue
+  if (qb < nq) {
+    if (quad) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int j4 = 0; j4 < 4; ++j4) {
+          const int row = 32 * (m0 + m) + 8 * j4 + 4 * hh;
+          if (row >= a.M) {
+            if (row < a.ld_dst) *reinterpret_cast<f32x4v*>(yrow + row) = f32x4v{0.f, 0.f, 0.f, 0.f};
+            continue;
+          }
+          f32x4v v;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = acc[m][4 * j4 + i] + bv[m][j4][i];
+          if (rrow) v += rv[m][j4];
+          if (a.accumulate) v = yv[m][j4] + v;
+          if (a.out_div != 1.f) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = v[i] / a.out_div;
+          }
+          if (a.post_act == PWG_ACT_LRELU) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = v[i] > 0.f ? v[i] : v[i] * a.post_slope;
+          } else if (a.post_act == PWG_ACT_TANH) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = tanhf(v[i]);
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (row + i >= a.M) v[i] = 0.f;
+          *reinterpret_cast<f32x4v*>(yrow + row) = v;
+        }
+    } else {
+      cn_store_col<MT>(a, acc, bias_, m0, hh, yrow, rrow);
+    }
+  }
+#ifdef PWG_XDMA_PROBE
+  if (probe) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp();
+    unsigned long long* dst = g_xdma_probe[xd.probe_slot % XDMA_PROBE_SLOTS];
+    dst[0] = (unsigned long long)np | ((unsigned long long)K << 16) | ((unsigned long long)MT << 24) |
+             ((unsigned long long)NWV << 32) | ((unsigned long long)ns << 40) | ((unsigned long long)P << 56);
+    for (int i = 0; i < np; ++i) dst[1 + i] = s_probe[i];
+  }
+#endif
 }
 
 template <int K, int MT, int NWV>
 hipError_t xdma_go(dim3 grid, hipStream_t s, const CnConvArgs& a, const CnXdmaArgs& xd) {
+#ifdef PWG_XDMA_PROBE
+  constexpr int lds = XdmaShape<K, MT, NWV>::LDS + XDMA_PROBE_N * 8;
+#else
   constexpr int lds = XdmaShape<K, MT, NWV>::LDS;
+#endif
   const hipError_t e = allow_lds(reinterpret_cast<const void*>(pwg_cnet_xdma_kernel<K, MT, NWV>), lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((pwg_cnet_xdma_kernel<K, MT, NWV>), grid, dim3(64 * NWV), (size_t)lds, s, a, xd);
@@ -1229,12 +1395,10 @@ hipError_t xdma_launch_k(int k, dim3 grid, hipStream_t s, const CnConvArgs& a, c
 }
 // k = 1: K = 1 mode (steps = the tap-major chunk list)
 hipError_t xdma_launch(int mt, int nwv, int k, dim3 grid, hipStream_t s, const CnConvArgs& a, const CnXdmaArgs& xd) {
-  if (mt == 1 && nwv == 1) return xdma_launch_k<1, 1>(k, grid, s, a, xd);
-  if (mt == 1 && nwv == 2) return xdma_launch_k<1, 2>(k, grid, s, a, xd);
-  if (mt == 1 && nwv == 4) return xdma_launch_k<1, 4>(k, grid, s, a, xd);
-  if (mt == 2 && nwv == 1) return xdma_launch_k<2, 1>(k, grid, s, a, xd);
-  if (mt == 2 && nwv == 2) return xdma_launch_k<2, 2>(k, grid, s, a, xd);
-  if (mt == 2 && nwv == 4) return xdma_launch_k<2, 4>(k, grid, s, a, xd);
+  if (mt != 1) return hipErrorInvalidValue;  // (the plan picks one m-tile per workgroup)
+  if (nwv == 1) return xdma_launch_k<1, 1>(k, grid, s, a, xd);
+  if (nwv == 2) return xdma_launch_k<1, 2>(k, grid, s, a, xd);
+  if (nwv == 4) return xdma_launch_k<1, 4>(k, grid, s, a, xd);
   return hipErrorInvalidValue;
 }
 
@@ -2955,6 +3119,10 @@ struct PwgCnet {
   int narrow = 1;      // PWG_CNET_OPT_NARROW (plan time): 0 off, 1 small launches, 2 every x-tile phase
   int narrow_dma = 1;  // PWG_CNET_OPT_NARROW_DMA: narrow launches on the DMA-ring kernel (0: the narrow
                        // x-tile / tap-major kernels)
+  int streams = 1;     // PWG_CNET_OPT_STREAMS: 0 one stream, 1 independent launches of plans with narrow
+                       // launches run on auxiliary streams, 2 every plan
+  static constexpr int N_AUX = 3;
+  hipStream_t aux[N_AUX] = {nullptr, nullptr, nullptr};
   bool pair_attr_set = false;
   std::vector<PwgCnetOp> ops;
   std::vector<int> channels, rate, ld;
@@ -2989,7 +3157,11 @@ struct PwgCnetPlan {
   // per phase: narrow x-tile launch (PWG_CNET_OPT_NARROW), 0 waves = the phase's default launch
   std::vector<int> nar_nwv, nar_mt, nar_lds, n_nblocks;
   std::vector<char> nar_tap;                 // ... on the tap-major kernel (not the x-tile family)
+  std::vector<char> nar_xdma;                // ... tap-major phases: on the DMA-ring kernel (K = 1 mode)
   std::vector<int2*> d_nblocks;              // its blocks (utt, q0 step 32 nar_nwv)
+  std::vector<int2*> d_nfr;                  // ... and their utterances' (first frame, frames)
+  bool has_narrow = false;                   // some phase runs narrow (PWG_CNET_OPT_STREAMS 1)
+  std::vector<hipEvent_t> xev;               // cross-stream dependency events (reused every run)
 };
 
 namespace {
@@ -3457,6 +3629,8 @@ void pwg_cnet_destroy(PwgCnet* n) {
     if (ph.d_chunks) (void)hipFree(ph.d_chunks);
   for (auto& r : n->records) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
   for (hipEvent_t e : n->pool) (void)hipEventDestroy(e);
+  for (hipStream_t x : n->aux)
+    if (x) (void)hipStreamDestroy(x);
   delete n;
 }
 
@@ -3571,28 +3745,33 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
       if (op.src[s2].buf >= 0) last_use[op.src[s2].buf] = std::max(last_use[op.src[s2].buf], oi);
     if (op.res >= 0) last_use[op.res] = std::max(last_use[op.res], oi);
   }
-  struct Slot { size_t off, bytes; int free_after; };
-  std::vector<Slot> slots;
-  size_t o = 0;
-  p->buf_off.assign(nb, SIZE_MAX);
-  std::vector<int> order;
-  for (int b = 1; b < nb - 1; ++b) order.push_back(b);
-  std::sort(order.begin(), order.end(), [&](int x, int y) { return first_def[x] < first_def[y]; });
-  for (int b : order) {
-    const size_t bytes = ((size_t)p->rows[b] * n->ld[b] * sizeof(float) + 255) / 256 * 256;
-    int pick = -1;
-    for (size_t si = 0; si < slots.size(); ++si)
-      if (slots[si].bytes == bytes && slots[si].free_after < first_def[b]) { pick = (int)si; break; }
-    if (pick < 0) {
-      slots.push_back({o, bytes, -1});
-      o += bytes;
-      pick = (int)slots.size() - 1;
+  // (reuse = false: every buffer its own slot, for plans whose independent launches run
+  // concurrently -- a shared slot would order them; PWG_CNET_OPT_STREAMS, set below)
+  auto assign_slots = [&](bool reuse) {
+    struct Slot { size_t off, bytes; int free_after; };
+    std::vector<Slot> slots;
+    size_t o = 0;
+    p->buf_off.assign(nb, SIZE_MAX);
+    std::vector<int> order;
+    for (int b = 1; b < nb - 1; ++b) order.push_back(b);
+    std::sort(order.begin(), order.end(), [&](int x, int y) { return first_def[x] < first_def[y]; });
+    for (int b : order) {
+      const size_t bytes = ((size_t)p->rows[b] * n->ld[b] * sizeof(float) + 255) / 256 * 256;
+      int pick = -1;
+      for (size_t si = 0; reuse && si < slots.size(); ++si)
+        if (slots[si].bytes == bytes && slots[si].free_after < first_def[b]) { pick = (int)si; break; }
+      if (pick < 0) {
+        slots.push_back({o, bytes, -1});
+        o += bytes;
+        pick = (int)slots.size() - 1;
+      }
+      p->buf_off[b] = slots[pick].off;
+      slots[pick].free_after = std::max(last_use[b], first_def[b]);
     }
-    p->buf_off[b] = slots[pick].off;
-    slots[pick].free_after = std::max(last_use[b], first_def[b]);
-  }
-  p->ws_flag = o;  // after the buffer slots (256-byte aligned)
-  p->ws_bytes = o + 256;
+    p->ws_flag = o;  // after the buffer slots (256-byte aligned)
+    p->ws_bytes = o + 256;
+  };
+  assign_slots(true);
   // host side of every per-phase list first (block lists, columns per utterance, fused-pair strips,
   // x-tile blocks), each checked before anything reaches the GPU: a bad list (a step or count that
   // was never set, a block outside its utterance) fails here with PWG_ERR_ASSERT instead of turning
@@ -3604,6 +3783,7 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
   p->nar_mt.assign(nph, 0);
   p->nar_lds.assign(nph, 0);
   p->nar_tap.assign(nph, 0);
+  p->nar_xdma.assign(nph, 0);
   p->n_cu = 256;  // host-only handles size for an MI355X
   if (n->device >= 0) {
     int cu = 0;
@@ -3613,6 +3793,16 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
     }
     p->n_cu = cu;
   }
+  // DMA-ring launches (PWG_CNET_OPT_NARROW_DMA): one m-tile and 4 waves (128 columns) per workgroup
+  // when the utterances are that long. A step's serial cost per wave -- DMA issue (~40 cycles per
+  // 1-KB instruction) and the pre-activation / pair split (~180 cycles per 16-B quad) -- shrinks with
+  // the waves sharing it while the MFMAs per wave stay; measured per step on HiFiGAN v1's 256-channel
+  // k = 11 convs at B = 1 (tools/diag/xdma_probe.py): 1 wave ~4,400 cycles.
+  auto xdma_waves = [&](const std::vector<int>& nc) {
+    int mx = 0;
+    for (int c : nc) mx = std::max(mx, c);
+    return mx >= 96 ? 4 : (mx >= 48 ? 2 : 1);
+  };
   auto bad_list = [&](size_t pi, const char* what) {
     delete p;
     return fail(PWG_ERR_ASSERT, "internal: plan phase " + std::to_string(pi) + ": " + what);
@@ -3667,21 +3857,25 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
       else base = (long long)blocks.size() * (ph.mt_total / ph.MT) * zn;
       if (n->narrow == 2 || base < p->n_cu) {
         int pick_w = 1, pick_m = 1;
-        bool found = false;
-        for (int w : {4, 2, 1}) {
-          for (int mtn : {2, 1}) {
-            if (mtn == 2 && ph.mt_total % 2 != 0) continue;
-            long long nwg = 0;
-            for (int u = 0; u < n_utts; ++u) nwg += (ncols[u] + 32 * w - 1) / (32 * w);
-            nwg *= (ph.mt_total / mtn) * zn;
-            if (nwg >= p->n_cu) {
-              pick_w = w;
-              pick_m = mtn;
-              found = true;
-              break;
+        if (n->narrow_dma) {
+          pick_w = xdma_waves(ncols);
+        } else {
+          bool found = false;
+          for (int w : {4, 2, 1}) {
+            for (int mtn : {2, 1}) {
+              if (mtn == 2 && ph.mt_total % 2 != 0) continue;
+              long long nwg = 0;
+              for (int u = 0; u < n_utts; ++u) nwg += (ncols[u] + 32 * w - 1) / (32 * w);
+              nwg *= (ph.mt_total / mtn) * zn;
+              if (nwg >= p->n_cu) {
+                pick_w = w;
+                pick_m = mtn;
+                found = true;
+                break;
+              }
             }
+            if (found) break;
           }
-          if (found) break;
         }
         const int span = 32 * pick_w + (xk - 1) * xd;
         p->nar_nwv[pi] = pick_w;
@@ -3702,21 +3896,29 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
       const long long base = (long long)blocks.size() * (ph.mt_total / ph.MT) * zn;
       if (n->narrow == 2 || base < p->n_cu) {
         int pick_w = 1, pick_m = 1;
-        bool found = false;
-        for (int w : {2, 1}) {
-          for (int mtn : {2, 1}) {
-            if (mtn == 2 && ph.mt_total % 2 != 0) continue;
-            long long nwg = 0;
-            for (int u = 0; u < n_utts; ++u) nwg += (ncols[u] + 32 * w - 1) / (32 * w);
-            nwg *= (ph.mt_total / mtn) * zn;
-            if (nwg >= p->n_cu) {
-              pick_w = w;
-              pick_m = mtn;
-              found = true;
-              break;
+        // the DMA-ring kernel (K = 1 mode) unless a source normalizes (the narrow tap-major kernel
+        // then runs it, 1-2 waves)
+        if (n->narrow_dma && !op.src[0].normalize && !(op.src[1].buf >= 0 && op.src[1].normalize) &&
+            ph.chunks.size() <= (size_t)XDMA_CHUNKS_MAX) {
+          pick_w = xdma_waves(ncols);
+          p->nar_xdma[pi] = 1;
+        } else {
+          bool found = false;
+          for (int w : {2, 1}) {
+            for (int mtn : {2, 1}) {
+              if (mtn == 2 && ph.mt_total % 2 != 0) continue;
+              long long nwg = 0;
+              for (int u = 0; u < n_utts; ++u) nwg += (ncols[u] + 32 * w - 1) / (32 * w);
+              nwg *= (ph.mt_total / mtn) * zn;
+              if (nwg >= p->n_cu) {
+                pick_w = w;
+                pick_m = mtn;
+                found = true;
+                break;
+              }
             }
+            if (found) break;
           }
-          if (found) break;
         }
         p->nar_nwv[pi] = pick_w;
         p->nar_mt[pi] = pick_m;
@@ -3734,6 +3936,14 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
       }
     if (blocks.size() > (size_t)INT32_MAX / 2) return bad_list(pi, "block count");
   }
+  for (size_t pi = 0; pi < nph; ++pi) p->has_narrow |= p->nar_nwv[pi] > 0;
+  if (n->streams == 2 || (n->streams == 1 && p->has_narrow)) assign_slots(false);
+  // narrow blocks' utterance frame ranges (the DMA-ring kernel derives every row range from them)
+  std::vector<long long> f0(n_utts, 0);
+  for (int u = 1; u < n_utts; ++u) f0[u] = f0[u - 1] + frames[u - 1];
+  std::vector<std::vector<int2>> h_nfr(nph);
+  for (size_t pi = 0; pi < nph; ++pi)
+    for (const int2& b : h_nblocks[pi]) h_nfr[pi].push_back(make_int2((int)f0[b.x], (int)frames[b.x]));
   if (n->device < 0) {  // host-only handle: sizes and lists checked, nothing uploaded (cannot run)
     p->host_only = true;
     for (size_t pi = 0; pi < nph; ++pi) {
@@ -3746,6 +3956,7 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
       p->n_xblocks.push_back((int)h_xblocks[pi].size());
       p->d_nblocks.push_back(nullptr);
       p->n_nblocks.push_back((int)h_nblocks[pi].size());
+      p->d_nfr.push_back(nullptr);
     }
     *out = p;
     return PWG_OK;
@@ -3796,6 +4007,9 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
     upload(h_nblocks[pi], &dnb);
     p->d_nblocks.push_back(dnb);
     p->n_nblocks.push_back((int)h_nblocks[pi].size());
+    int2* dnf = nullptr;
+    upload(h_nfr[pi], &dnf);
+    p->d_nfr.push_back(dnf);
   }
   if (e != hipSuccess) {
     const int rc = hipf(e, "cnet plan upload");
@@ -3819,6 +4033,8 @@ void pwg_cnet_plan_destroy(PwgCnetPlan* p) {
   for (auto* x : p->d_strips) if (x) (void)hipFree(x);
   for (auto* x : p->d_xblocks) if (x) (void)hipFree(x);
   for (auto* x : p->d_nblocks) if (x) (void)hipFree(x);
+  for (auto* x : p->d_nfr) if (x) (void)hipFree(x);
+  for (hipEvent_t e : p->xev) (void)hipEventDestroy(e);
   delete p;
 }
 
@@ -3837,7 +4053,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
   const int nb = (int)n->channels.size();
   Guard g(n->device);
   if (!g.ok) return fail(PWG_ERR_HIP, "hipSetDevice failed");
-  hipStream_t s = (hipStream_t)stream;
+  hipStream_t const s_main = (hipStream_t)stream;
   std::vector<float*> bufs(nb);
   bufs[0] = const_cast<float*>(mel);
   bufs[nb - 1] = out;
@@ -3851,7 +4067,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
   int* rflag = n->split_f16 ? flag_word : nullptr;
   bool out_checked = false;
   {
-    const hipError_t ez = hipMemsetAsync(flag_word, 0, sizeof(int), s);
+    const hipError_t ez = hipMemsetAsync(flag_word, 0, sizeof(int), s_main);
     if (ez != hipSuccess) return hipf(ez, "range flag reset");
   }
   // a conv pair runs fused unless its convs run on the x-tile kernel (measured faster unfused)
@@ -3860,15 +4076,146 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
   // first conv runs narrow runs unfused (its second op as its own launch)
   auto narrow = [&](size_t i) { return xt && p->nar_nwv[i] > 0 && !p->nar_tap[i]; };
   auto narrow_tap = [&](size_t i) { return n->split_f16 && p->nar_nwv[i] > 0 && p->nar_tap[i]; };
+  // the DMA-ring kernel's row ranges: per-block frames and the buffers' rows per frame
+  auto xdma_rows = [&](CnXdmaArgs& xd, size_t i) {
+    const PwgCnetOp& o = n->ops[n->phases[i].op];
+    xd.bfr = p->d_nfr[i];
+    xd.rate[0] = n->rate[o.src[0].buf];
+    xd.rate[1] = o.src[1].buf >= 0 && o.kind == PWG_CNET_CONV ? n->rate[o.src[1].buf] : xd.rate[0];
+    xd.rate_dst = n->rate[o.dst];
+    xd.rate_res = o.res >= 0 ? n->rate[o.res] : 0;
+  };
+#ifdef PWG_XDMA_PROBE
+  auto probe_slot = [](size_t i) { return (int)i; };  // phase index (tools/diag/xdma_probe.py)
+#else
+  auto probe_slot = [](size_t) { return -1; };
+#endif
+  // the launches of this run: (phase, second op fused into it or -1)
+  auto skipped = [&](size_t pi) {
+    const OpPhase& ph = n->phases[pi];
+    return (pi > 0 && ((pair_fused(n->phases[pi - 1]) && n->phases[pi - 1].pair_b == (int)pi) ||
+                       (fuse && n->phases[pi - 1].stack_b == (int)pi && !narrow(pi - 1)))) ||
+           ph.z_phases == 0 || (xt && fuse && pi > 0 && n->phases[pi - 1].xpair_b == (int)pi && !narrow(pi - 1));
+  };
+  std::vector<std::pair<int, int>> launches;
+  for (size_t pi = 0; pi < n->phases.size(); ++pi) {
+    if (skipped(pi)) continue;
+    const OpPhase& ph = n->phases[pi];
+    int second = -1;
+    if (pair_fused(ph)) second = n->phases[ph.pair_b].op;
+    else if (fuse && ph.stack_b >= 0 && !narrow(pi)) second = n->phases[ph.stack_b].op;
+    else if (xt && fuse && ph.xpair_b >= 0 && !narrow(pi)) second = n->phases[ph.xpair_b].op;
+    launches.push_back({(int)pi, second});
+  }
+  // Concurrent launches (PWG_CNET_OPT_STREAMS): a small plan's launches are each a few dozen
+  // workgroups and latency-bound, and a generator's parallel branches (HiFiGAN's multi-receptive-
+  // field blocks, models/hifigan.py:159-168) are independent until their sum: each launch follows
+  // the launch it depends on latest on that launch's stream when it is that stream's last, else
+  // takes the least recently used stream, and waits on an event for every dependency on another
+  // stream. Buffers are written once per run except an accumulated sum, whose writers stay in
+  // program order: same launches, same arithmetic, bit-identical to one stream.
+  const int NS = 1 + PwgCnet::N_AUX;
+  const bool conc = n->streams == 2 || (n->streams == 1 && p->has_narrow);
+  std::vector<int> l_stream(launches.size(), 0), l_event(launches.size(), -1);
+  std::vector<std::vector<int>> l_waits(launches.size());  // launch indices waited for (other streams)
+  bool stream_used[1 + PwgCnet::N_AUX] = {true, false, false, false};
+  if (conc) {
+    // dependencies by storage, not buffer id: buffers of a plan built for one stream share slots
+    std::vector<int> mem(nb);
+    for (int b = 0; b < nb; ++b) {
+      mem[b] = b;
+      if (b > 0 && b < nb - 1)
+        for (int c = 1; c < b; ++c)
+          if (p->buf_off[c] == p->buf_off[b]) { mem[b] = mem[c]; break; }
+    }
+    std::vector<int> last_writer(nb, -1);
+    std::vector<std::vector<int>> readers(nb);
+    int tail[1 + PwgCnet::N_AUX] = {-1, -1, -1, -1}, used_at[1 + PwgCnet::N_AUX] = {-1, -1, -1, -1};
+    for (size_t L = 0; L < launches.size(); ++L) {
+      std::vector<int> deps;
+      auto op_deps = [&](int oi) {
+        const PwgCnetOp& o = n->ops[oi];
+        auto rd = [&](int b) {
+          if (b >= 0 && last_writer[mem[b]] >= 0) deps.push_back(last_writer[mem[b]]);
+        };
+        rd(o.src[0].buf);
+        if (o.kind == PWG_CNET_CONV) rd(o.src[1].buf);
+        rd(o.res);
+        if (o.accumulate) rd(o.dst);
+        if (last_writer[mem[o.dst]] >= 0) deps.push_back(last_writer[mem[o.dst]]);  // WAW
+        for (int r : readers[mem[o.dst]]) deps.push_back(r);                          // WAR
+      };
+      op_deps(n->phases[launches[L].first].op);
+      if (launches[L].second >= 0) op_deps(launches[L].second);
+      int best = -1;  // the latest dependency that is its stream's tail
+      for (int d : deps)
+        if (tail[l_stream[d]] == d && (best < 0 || d > best)) best = d;
+      int st;
+      if (best >= 0) {
+        st = l_stream[best];
+      } else if (deps.empty()) {
+        st = 0;
+      } else {
+        st = 0;
+        for (int k = 1; k < NS; ++k)
+          if (used_at[k] < used_at[st]) st = k;
+      }
+      l_stream[L] = st;
+      for (int d : deps)
+        if (l_stream[d] != st && std::find(l_waits[L].begin(), l_waits[L].end(), d) == l_waits[L].end())
+          l_waits[L].push_back(d);
+      tail[st] = (int)L;
+      used_at[st] = (int)L;
+      stream_used[st] = true;
+      auto note = [&](int oi) {
+        const PwgCnetOp& o = n->ops[oi];
+        for (int b : {o.src[0].buf, o.kind == PWG_CNET_CONV ? o.src[1].buf : -1, o.res, o.accumulate ? o.dst : -1})
+          if (b >= 0) readers[mem[b]].push_back((int)L);
+      };
+      note(n->phases[launches[L].first].op);
+      if (launches[L].second >= 0) note(launches[L].second);
+      auto wrote = [&](int oi) {
+        const int b = mem[n->ops[oi].dst];
+        last_writer[b] = (int)L;
+        readers[b].clear();
+      };
+      wrote(n->phases[launches[L].first].op);
+      if (launches[L].second >= 0) wrote(launches[L].second);
+    }
+    // events: after every launch some launch on another stream waits for, and each aux stream's tail
+    int ne = 0;
+    for (size_t L = 0; L < launches.size(); ++L)
+      for (int d : l_waits[L])
+        if (l_event[d] < 0) l_event[d] = ne++;
+    for (int k = 1; k < NS; ++k)
+      if (stream_used[k] && tail[k] >= 0 && l_event[tail[k]] < 0) l_event[tail[k]] = ne++;
+    ne += 1;  // the fork event (s_main after the flag reset)
+    while ((int)p->xev.size() < ne) {
+      hipEvent_t e = nullptr;
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(PWG_ERR_HIP, "event create");
+      p->xev.push_back(e);
+    }
+    for (int k = 1; k < NS; ++k)
+      if (stream_used[k] && !n->aux[k - 1] &&
+          hipStreamCreateWithFlags(&n->aux[k - 1], hipStreamNonBlocking) != hipSuccess)
+        return fail(PWG_ERR_HIP, "auxiliary stream create");
+    // fork: the aux streams start after everything queued on the caller's stream so far
+    hipEvent_t fork = p->xev[ne - 1];
+    if (hipEventRecord(fork, s_main) != hipSuccess) return fail(PWG_ERR_HIP, "fork event");
+    for (int k = 1; k < NS; ++k)
+      if (stream_used[k] && hipStreamWaitEvent(n->aux[k - 1], fork, 0) != hipSuccess)
+        return fail(PWG_ERR_HIP, "fork wait");
+  }
+  auto stream_of = [&](int k) { return k == 0 ? s_main : n->aux[k - 1]; };
+  size_t li = 0;
   for (size_t pi = 0; pi < n->phases.size(); ++pi) {
     const OpPhase& ph = n->phases[pi];
     const PwgCnetOp& op = n->ops[ph.op];
-    if (pi > 0 && ((pair_fused(n->phases[pi - 1]) && n->phases[pi - 1].pair_b == (int)pi) ||
-                   (fuse && n->phases[pi - 1].stack_b == (int)pi && !narrow(pi - 1))))
-      continue;  // ran inside the fused pair / stack
-    if (ph.z_phases == 0) continue;  // ran in its ConvTranspose's one launch
-    if (xt && fuse && pi > 0 && n->phases[pi - 1].xpair_b == (int)pi && !narrow(pi - 1))
-      continue;  // ran in the x-tile pair
+    if (skipped(pi)) continue;
+    const size_t L = li++;
+    hipStream_t const s = stream_of(l_stream[L]);
+    for (int d : l_waits[L])
+      if (hipStreamWaitEvent(s, p->xev[l_event[d]], 0) != hipSuccess) return fail(PWG_ERR_HIP, "dependency wait");
     hipEvent_t ea = nullptr, eb = nullptr;
     if (n->timing) {
       for (hipEvent_t* ev : {&ea, &eb}) {
@@ -4079,6 +4426,8 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
           } else if (n->narrow_dma && !a.src[0].normalize) {
             CnXdmaArgs xd;
             xd.dil = xt.dil; xd.cs = xt.cs; xd.n_steps = xt.cs; xd.rev = xt.rev;
+            xd.probe_slot = probe_slot(pi);
+            xdma_rows(xd, pi);
             for (int r = 0; r < 8; ++r) xd.z_off[r] = xt.z_off[r];
             ea2 = xdma_launch(mtn, nw, xt.K, ngrid, s, a, xd);
           } else {
@@ -4096,9 +4445,11 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         a.blocks = p->d_nblocks[pi];
         const int nw = p->nar_nwv[pi], mtn = p->nar_mt[pi];
         const dim3 ngrid((unsigned)p->n_nblocks[pi], (unsigned)(ph.mt_total / mtn), (unsigned)ph.z_phases);
-        if (n->narrow_dma && !a.src[0].normalize && !a.src[1].normalize) {
+        if (p->nar_xdma[pi]) {
           CnXdmaArgs xd;  // K = 1 mode: the chunk list, each chunk at its own source and row offset
           xd.dil = 1; xd.cs = 0; xd.n_steps = a.n_chunks; xd.rev = 0;
+          xd.probe_slot = probe_slot(pi);
+          xdma_rows(xd, pi);
           for (int r = 0; r < 8; ++r) xd.z_off[r] = 0;
           const hipError_t ea2 = p->n_nblocks[pi] > 0 ? xdma_launch(mtn, nw, 1, ngrid, s, a, xd) : hipSuccess;
           if (ea2 != hipSuccess) return hipf(ea2, "xdma kernel launch");
@@ -4154,7 +4505,18 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
       (void)hipEventRecord(eb, s);
       n->records.push_back({ph.op, ea, eb});
     }
+    if (l_event[L] >= 0 && hipEventRecord(p->xev[l_event[L]], s) != hipSuccess)
+      return fail(PWG_ERR_HIP, "dependency event");
   }
+  // join: the caller's stream waits for every auxiliary stream's last launch
+  if (conc) {
+    int tail_of[1 + PwgCnet::N_AUX] = {-1, -1, -1, -1};
+    for (size_t L = 0; L < launches.size(); ++L) tail_of[l_stream[L]] = (int)L;
+    for (int k = 1; k < NS; ++k)
+      if (tail_of[k] >= 0 && hipStreamWaitEvent(s_main, p->xev[l_event[tail_of[k]]], 0) != hipSuccess)
+        return fail(PWG_ERR_HIP, "join wait");
+  }
+  hipStream_t const s = s_main;
   if (rflag && !out_checked && p->rows[nb - 1] > 0) {
     const long long cnt = p->rows[nb - 1] * n->ld[nb - 1];
     const long long nblk = std::min<long long>((cnt + 255) / 256, 4096);
@@ -4200,6 +4562,11 @@ int pwg_cnet_set_option(PwgCnet* n, int option, long long value) {
               : option == PWG_CNET_OPT_XCD_ORDER  ? &n->xcd_order
               : option == PWG_CNET_OPT_NARROW_DMA ? &n->narrow_dma
                                                   : nullptr;
+  if (option == PWG_CNET_OPT_STREAMS) {
+    if (value < 0 || value > 2) return fail(PWG_ERR_INVALID, "streams must be 0, 1 or 2");
+    n->streams = (int)value;
+    return PWG_OK;
+  }
   if (!slot) return fail(PWG_ERR_INVALID, "unknown option");
   if (value != 0 && value != 1 && !(option == PWG_CNET_OPT_XT_DMA && value >= 0 && value <= 15))
     return fail(PWG_ERR_INVALID, "option value must be 0 or 1 (PWG_CNET_OPT_XT_DMA: flags 0 - 15)");
@@ -4231,3 +4598,13 @@ int pwg_cnet_timing_collect(PwgCnet* n, double* ms, long long* launches) {
 }
 
 }  // extern "C"
+
+#ifdef PWG_XDMA_PROBE
+// probe builds only: the DMA-ring kernels' workgroup-0 timelines, [slot][XDMA_PROBE_N] words
+extern "C" PWG_API int pwg_cnet_debug_probe(unsigned long long* out, int n_words) {
+  const int total = XDMA_PROBE_SLOTS * XDMA_PROBE_N;
+  if (!out || n_words < total) return PWG_ERR_INVALID;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_xdma_probe), sizeof(unsigned long long) * total) == hipSuccess
+             ? PWG_OK : PWG_ERR_HIP;
+}
+#endif

@@ -374,3 +374,48 @@ def test_narrow_launches_bitwise_equal(cfg, built_lib, cuda_device):
         for a, b in zip(outs[key], outs[0, 1]):
             assert np.isfinite(a).all()
             np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("cfg", ["hifigan_v1", "mb_melgan_v2", "hifigan_v1_causal"])
+def test_concurrent_streams_bitwise_equal(cfg, built_lib, cuda_device):
+    """PWG_CNET_OPT_STREAMS: independent launches (HiFiGAN's parallel residual blocks) forked onto
+    auxiliary streams and joined back with events give the same bits as one stream, for the B = 1
+    plan (auto mode) and a ragged batch (forced on); a captured graph of the forked forward too."""
+    from parallelwavegan_amd import configs, synthetic
+    from parallelwavegan_amd.hifigan import HiFiGANGenerator
+    from parallelwavegan_amd.melgan import PQMF, MelGANGenerator
+
+    cls_name, params = configs.vocoder_params(cfg)
+    m = {"MelGANGenerator": MelGANGenerator, "HiFiGANGenerator": HiFiGANGenerator}[cls_name](**params)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic.make_module_state_dict(m, seed=11).items()})
+    if cfg in configs.VOCODER_PQMF:
+        m.pqmf = PQMF(**configs.VOCODER_PQMF[cfg])
+    m = m.to(cuda_device)
+    eng = m.engine()
+    mels = [synthetic.make_mel(f, 80, seed=170 + i) for i, f in enumerate([64, 9, 23])]
+    outs = {}
+    with torch.no_grad():
+        for mode in (0, 1, 2):
+            eng.set_streams(mode)
+            outs[mode] = ([m.inference(torch.from_numpy(mels[0]).to(cuda_device)).cpu().numpy()] +
+                          [y.cpu().numpy() for y in m.inference_batch(mels)])
+        eng.set_streams(1)
+        # graph capture of the forked forward (fork / join events become graph edges)
+        plan = eng.plan([64])
+        mel = torch.from_numpy(mels[0]).to(cuda_device).reshape(-1).contiguous()
+        out = torch.empty(plan.out_rows * eng.out_channels, device=cuda_device)
+        s = torch.cuda.Stream(cuda_device)
+        with torch.cuda.stream(s):
+            eng.run(plan, mel, out, stream=s)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                eng.run(plan, mel, out, stream=s, check=False)
+            out.zero_()
+            g.replay()
+            torch.cuda.synchronize()
+    for mode in (1, 2):
+        for a, b in zip(outs[mode], outs[0]):
+            assert np.isfinite(a).all()
+            np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(out.cpu().numpy().reshape(outs[0][0].shape), outs[0][0])
