@@ -455,6 +455,8 @@ def vocoder_setup(args, dev):
     eng = m.engine()
     eng.set_split_f16(not args.cnet_fp32)
     eng.set_fuse_pairs(not args.cnet_nofuse)
+    if getattr(args, "cnet_streams", None) is not None:
+        eng.set_streams(args.cnet_streams)
     if args.pair_steps:
         eng.set_pair_steps(args.pair_steps)
     return m, eng, cls_name, params, (sd, syn)
@@ -753,6 +755,8 @@ def main():
     ap.add_argument("--no-fuse-first", action="store_true", help="split16: standalone first_conv kernel (A/B)")
     ap.add_argument("--cnet-fp32", action="store_true", help="vocoder configs: exact fp32 MFMA instead of split-f16")
     ap.add_argument("--cnet-nofuse", action="store_true", help="vocoder configs: run fusable conv pairs unfused")
+    ap.add_argument("--cnet-streams", type=int, default=None, choices=[0, 1, 2],
+                    help="vocoder configs: PWG_CNET_OPT_STREAMS (A/B; default: the library's, 1)")
     ap.add_argument("--pair-steps", type=int, default=None, help="vocoder configs: 128-column tiles per fused-pair strip")
     args = ap.parse_args()
     if args.cpu_seconds is None:

@@ -3157,7 +3157,7 @@ struct PwgCnetPlan {
   // per phase: narrow x-tile launch (PWG_CNET_OPT_NARROW), 0 waves = the phase's default launch
   std::vector<int> nar_nwv, nar_mt, nar_lds, n_nblocks;
   std::vector<char> nar_tap;                 // ... on the tap-major kernel (not the x-tile family)
-  std::vector<char> nar_xdma;                // ... tap-major phases: on the DMA-ring kernel (K = 1 mode)
+  std::vector<char> nar_xdma;                // ... on the DMA-ring kernel (tap-major phases: K = 1 mode)
   std::vector<int2*> d_nblocks;              // its blocks (utt, q0 step 32 nar_nwv)
   std::vector<int2*> d_nfr;                  // ... and their utterances' (first frame, frames)
   bool has_narrow = false;                   // some phase runs narrow (PWG_CNET_OPT_STREAMS 1)
@@ -3803,6 +3803,14 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
     for (int c : nc) mx = std::max(mx, c);
     return mx >= 96 ? 4 : (mx >= 48 ? 2 : 1);
   };
+  // ... used while its workgroups fit one round over the CUs; past that (T' = 512: HiFiGAN's
+  // 128-channel stage, 1,024 of them) the narrow x-tile kernel's 2-m-tile workgroups reuse each
+  // staged input row twice as often and measured faster
+  auto xdma_fits = [&](const std::vector<int>& nc, int w, long long mt_groups) {
+    long long nwg = 0;
+    for (int c : nc) nwg += (c + 32 * w - 1) / (32 * w);
+    return nwg * mt_groups <= p->n_cu;
+  };
   auto bad_list = [&](size_t pi, const char* what) {
     delete p;
     return fail(PWG_ERR_ASSERT, "internal: plan phase " + std::to_string(pi) + ": " + what);
@@ -3857,8 +3865,9 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
       else base = (long long)blocks.size() * (ph.mt_total / ph.MT) * zn;
       if (n->narrow == 2 || base < p->n_cu) {
         int pick_w = 1, pick_m = 1;
-        if (n->narrow_dma) {
+        if (n->narrow_dma && xdma_fits(ncols, xdma_waves(ncols), (long long)ph.mt_total * zn)) {
           pick_w = xdma_waves(ncols);
+          p->nar_xdma[pi] = 1;
         } else {
           bool found = false;
           for (int w : {4, 2, 1}) {
@@ -3899,7 +3908,8 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
         // the DMA-ring kernel (K = 1 mode) unless a source normalizes (the narrow tap-major kernel
         // then runs it, 1-2 waves)
         if (n->narrow_dma && !op.src[0].normalize && !(op.src[1].buf >= 0 && op.src[1].normalize) &&
-            ph.chunks.size() <= (size_t)XDMA_CHUNKS_MAX) {
+            ph.chunks.size() <= (size_t)XDMA_CHUNKS_MAX &&
+            xdma_fits(ncols, xdma_waves(ncols), (long long)ph.mt_total * zn)) {
           pick_w = xdma_waves(ncols);
           p->nar_xdma[pi] = 1;
         } else {
@@ -4423,7 +4433,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
           const dim3 ngrid((unsigned)p->n_nblocks[pi], (unsigned)(ph.mt_total / mtn), (unsigned)ph.z_phases);
           if (p->n_nblocks[pi] == 0) {
             ea2 = hipSuccess;
-          } else if (n->narrow_dma && !a.src[0].normalize) {
+          } else if (p->nar_xdma[pi] && !a.src[0].normalize) {
             CnXdmaArgs xd;
             xd.dil = xt.dil; xd.cs = xt.cs; xd.n_steps = xt.cs; xd.rev = xt.rev;
             xd.probe_slot = probe_slot(pi);
