@@ -1005,6 +1005,9 @@ struct CnXdmaArgs {
   int rate[2], rate_dst, rate_res;  // rows per frame of the sources', destination and residual buffers
 };
 constexpr int XDMA_CHUNKS_MAX = 256;  // K = 1 mode: chunks per op (the table sits in LDS)
+#ifndef XDMA_K1_G
+#define XDMA_K1_G 4                   // K = 1 mode: chunks per step
+#endif
 #ifdef PWG_XDMA_PROBE
 constexpr int XDMA_PROBE_SLOTS = 128, XDMA_PROBE_N = 96;
 __device__ unsigned long long g_xdma_probe[XDMA_PROBE_SLOTS][XDMA_PROBE_N];
@@ -1012,19 +1015,30 @@ __device__ unsigned long long g_xdma_probe[XDMA_PROBE_SLOTS][XDMA_PROBE_N];
 template <int K, int MT, int NWV>
 struct XdmaShape {
   static constexpr int XC = 32 * NWV;
-  static constexpr int XR = XC + (K == 1 ? 0 : NARROW_HALO);  // raw input rows per step
-  static constexpr int NA = K * MT * 2, NX = XR / 16;          // 1-KB DMA instructions per step
+  // raw input rows per step: the tile + the taps' reach (ConvTranspose phases, K = 2: one row)
+  static constexpr int XR = XC + (K == 1 ? 0 : (K == 2 ? 16 : NARROW_HALO));
+  // K = 1 mode stages G chunks per step (each its own source rows), so a step's barrier and DMA
+  // round trip cover G chunks' few MFMAs
+  static constexpr int G = K == 1 ? XDMA_K1_G : 1;
+  static constexpr int KT = K == 1 ? G : K;                    // A fragments (taps / chunks) per step
+  static constexpr int NA = KT * MT * 2, NX = G * XR / 16;     // 1-KB DMA instructions per step
   static constexpr int DA = (NA + NWV - 1) / NWV, DX = (NX + NWV - 1) / NWV;  // ... per wave
   static constexpr int D = DA + DX;
   static constexpr int SLOT = (NX + NA) * 1024;                // raw rows, then A fragments
   // K > 1: two converted-row buffers; K = 1: none (B split in registers) but the chunk table
   static constexpr int CBUF = K == 1 ? 0 : XR * XT_ROWB;
   static constexpr int CHT = K == 1 ? XDMA_CHUNKS_MAX * (int)sizeof(ChunkDesc) : 0;
-  // deepest ring (<= 16 slots) whose wait counts fit vmcnt (63) and whose LDS fits 159 KB
+  // deepest ring (<= PWG_XDMA_RING_CAP slots) whose wait counts fit vmcnt (63) and LDS 159 KB
   static constexpr int ring(int p) {
     return p <= 2 ? 2 : (((p - 2) * D <= 63 && p * SLOT + 2 * CBUF + CHT <= 159 * 1024) ? p : ring(p - 1));
   }
-  static constexpr int P = ring(16);
+// at most 4 slots: the prologue issues P - 1 steps before the first MFMA, and deeper rings measured
+// slower at B = 1 (MB-MelGAN v2 T' = 64: 16 slots 0.507 ms, 8: 0.508, 4: 0.478; HiFiGAN v1 0.973 /
+// 0.989 / 0.954; profiles/r04_h)
+#ifndef PWG_XDMA_RING_CAP
+#define PWG_XDMA_RING_CAP 4
+#endif
+  static constexpr int P = ring(PWG_XDMA_RING_CAP);
   static constexpr int LDS = P * SLOT + 2 * CBUF + CHT;
   static_assert(LDS <= 160 * 1024, "DMA-ring shape");
 };
@@ -1073,7 +1087,8 @@ __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArg
   const float* const wfrag_ = zp == 0 ? a.wfrag : a.z_wfrag[zp];
   const float* const bias_ = zp == 0 ? a.bias : a.z_bias[zp];
   const ChunkDesc* const chunks_ = zp == 0 ? a.chunks : a.z_chunks[zp];
-  const int ns = xd.n_steps;
+  const int nch = xd.n_steps;                               // K > 1: channel blocks; K = 1: chunks
+  const int ns = K == 1 ? (nch + S::G - 1) / S::G : nch;     // steps
   const int span = K == 1 ? S::XC : S::XC + (K - 1) * xd.dil;
   const int sgx0 = fr.x * xd.rate[0], sgy0 = fr.y * xd.rate[0];
   const int sgx1 = fr.x * xd.rate[1], sgy1 = fr.y * xd.rate[1];
@@ -1128,7 +1143,7 @@ __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArg
   // K = 1: the op's chunk list, staged in LDS before the first DMA (one ordinary load round trip)
   ChunkDesc* const s_ch = reinterpret_cast<ChunkDesc*>(xt_smem + (size_t)P * S::SLOT + 2 * S::CBUF);
   if constexpr (K == 1) {
-    for (int c = threadIdx.x; c < ns; c += NTH) s_ch[c] = chunks_[c];
+    for (int c = threadIdx.x; c < nch; c += NTH) s_ch[c] = chunks_[c];
     __syncthreads();
   }
   auto chunk = [&](int s) -> ChunkDesc {
@@ -1149,7 +1164,7 @@ __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArg
       const int i = wave + NWV * k < S::NA ? wave + NWV * k : S::NA - 1;
       const int tl = i / (MT * 2), j = i - tl * (MT * 2);
       const int wt = xd.rev ? K - 1 - tl : tl;
-      const int chunk = K == 1 ? s : wt * xd.cs + s;
+      const int chunk = K == 1 ? min(s * S::G + tl, nch - 1) : wt * xd.cs + s;
       const float* src = wfrag_ + ((size_t)chunk * a.mt_total + m0) * 512 + j * 256;
       __builtin_amdgcn_global_load_lds((gptr_t)(src + lane * 4), (lptr_t)(slot + (S::NX + i) * 1024), 16, 0, 0);
     }
@@ -1161,13 +1176,14 @@ __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArg
         __builtin_amdgcn_global_load_lds((gptr_t)(xs + xoff[k]), (lptr_t)(slot + i * 1024), 16, 0, 0);
       }
     } else {
-      const ChunkDesc cd = chunk(s);
-      const CnSrc& sx = a.src[cd.src];
-      const int sgx = cd.src ? sgx1 : sgx0, sgy = cd.src ? sgy1 : sgy0;
 #pragma unroll
       for (int k = 0; k < S::DX; ++k) {
         const int i = wave + NWV * k < S::NX ? wave + NWV * k : S::NX - 1;
-        int p = q0 + cd.row_off + 16 * i + (lane >> 2);
+        const int t = i / (S::XC / 16), ii = i - t * (S::XC / 16);  // chunk of the step, row group
+        const ChunkDesc cd = chunk(min(s * S::G + t, nch - 1));
+        const CnSrc& sx = a.src[cd.src];
+        const int sgx = cd.src ? sgx1 : sgx0, sgy = cd.src ? sgy1 : sgy0;
+        int p = q0 + cd.row_off + 16 * ii + (lane >> 2);
         (void)edge_row(p, sgy, sx.pad_mode);
         const float* src = sx.x + (size_t)(sgx + p) * sx.ld + cd.c0 + 4 * (lane & 3);
         __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(slot + i * 1024), 16, 0, 0);
@@ -1222,18 +1238,19 @@ __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArg
     const unsigned char* const cb = s_cb + (size_t)(g & 1) * S::CBUF;
     const u32x4v* const sa =
         reinterpret_cast<const u32x4v*>(xt_smem + (size_t)(g % P) * S::SLOT + S::NX * 1024) + lane;
-    u32x4v bh[K], bl[K], ah[K][MT], al[K][MT];
+    constexpr int KT = S::KT;
+    u32x4v bh[KT], bl[KT], ah[KT][MT], al[KT][MT];
 #pragma unroll
-    for (int t = 0; t < K; ++t) {
+    for (int t = 0; t < KT; ++t) {
       if constexpr (K == 1) {
-        // the lane's 8 channels of its raw row, pre-activated and pair-split in registers
-        // (pwg_cnet_conv_kernel's bprep + cn_split8)
-        const ChunkDesc cd = chunk(g);
+        // chunk g G + t: the lane's 8 channels of its raw row, pre-activated and pair-split in
+        // registers (pwg_cnet_conv_kernel's bprep + cn_split8)
+        const ChunkDesc cd = chunk(min(g * S::G + t, nch - 1));
         const CnSrc& sx = a.src[cd.src];
         const int r = wave * 32 + cl;
         int p = q0 + cd.row_off + r;
         const bool okr = edge_row(p, cd.src ? sgy1 : sgy0, sx.pad_mode);
-        const unsigned char* const raw = xt_smem + (size_t)(g % P) * S::SLOT + r * 64 + 32 * hh;
+        const unsigned char* const raw = xt_smem + (size_t)(g % P) * S::SLOT + (t * S::XC + r) * 64 + 32 * hh;
         const f32x4v v0 = *reinterpret_cast<const f32x4v*>(raw), v1 = *reinterpret_cast<const f32x4v*>(raw + 16);
         f32x8v x = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
         if (sx.slope != 1.f) {
@@ -1254,7 +1271,8 @@ __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArg
       }
     }
 #pragma unroll
-    for (int t = 0; t < K; ++t)
+    for (int t = 0; t < KT; ++t) {
+      if (K == 1 && g * S::G + t >= nch) break;  // the last step's missing chunks: no products
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
         acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, ah[t][m]),
@@ -1264,6 +1282,7 @@ __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArg
         acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8v, al[t][m]),
                                                         __builtin_bit_cast(f16x8v, bh[t]), acc[m], 0, 0, 0);
       }
+    }
   };
 
 #ifdef PWG_XDMA_PROBE
@@ -2860,12 +2879,17 @@ __global__ void __launch_bounds__(128) pwg_cnet_thin_kernel(const CnConvArgs a, 
 // per 128-quad slice of it plus a scalar weight load per tap (HiFiGAN / MB-MelGAN output convs at
 // B = 1: 17-26 us for a few us of FMAs).
 constexpr int THIN1_LDS = 64 * 1024;
-template <int M>
-__global__ void __launch_bounds__(128) pwg_cnet_thin1_kernel(const CnConvArgs a, int nsrc) {
+// TPC threads per column, each summing the outputs o = sub, sub + TPC, ... (same per-output FMA
+// order): M = 4 / 8 outputs no longer serialise on one thread (MB-MelGAN's 4-band output conv).
+template <int M, int TPC>
+__global__ void __launch_bounds__(128 * TPC) pwg_cnet_thin1_kernel(const CnConvArgs a, int nsrc) {
+  constexpr int NT = 128 * TPC, MO = M / TPC;
+  static_assert(M % TPC == 0, "outputs split evenly over a column's threads");
+  const int col = threadIdx.x / TPC, sub = threadIdx.x - col * TPC;
   extern __shared__ __attribute__((aligned(16))) float s_x[];  // [src][cb][span][THIN_ROW], then [chunk][h][M][8]
   const int2 blk = a.blocks[blockIdx.x];
   const int u = blk.x;
-  const int q = blk.y + threadIdx.x;
+  const int q = blk.y + col;
   const bool live = q < a.ncols[u];
   const int xf0 = a.src[0].nc * a.src[0].span * THIN_ROW;
   const int xf = xf0 + (nsrc > 1 ? a.src[1].nc * a.src[1].span * THIN_ROW : 0);
@@ -2876,12 +2900,12 @@ __global__ void __launch_bounds__(128) pwg_cnet_thin1_kernel(const CnConvArgs a,
     const int2 sg = *reinterpret_cast<const int2*>(s.seg + 2 * u);
     float* const sx = s_x + (si ? xf0 : 0);
     const int total = s.nc * s.span * 4;  // quads: [cb][row][quad]
-    for (int b0 = 0; b0 < total; b0 += 128 * B) {
+    for (int b0 = 0; b0 < total; b0 += NT * B) {
       f32x4v v[B];
       bool ok[B];
 #pragma unroll
       for (int j = 0; j < B; ++j) {
-        const int i = b0 + threadIdx.x + 128 * j;
+        const int i = b0 + threadIdx.x + NT * j;
         const int ii = i < total ? i : total - 1;
         const int cb = ii / (s.span * 4), rq = ii - cb * (s.span * 4);
         int p = blk.y + s.off_min + (rq >> 2);
@@ -2890,7 +2914,7 @@ __global__ void __launch_bounds__(128) pwg_cnet_thin1_kernel(const CnConvArgs a,
       }
 #pragma unroll
       for (int j = 0; j < B; ++j) {
-        const int i = b0 + threadIdx.x + 128 * j;
+        const int i = b0 + threadIdx.x + NT * j;
         if (i >= total) break;
         const int cb = i / (s.span * 4), rq = i - cb * (s.span * 4);
         const int ch = 16 * cb + 4 * (rq & 3);
@@ -2911,42 +2935,43 @@ __global__ void __launch_bounds__(128) pwg_cnet_thin1_kernel(const CnConvArgs a,
   // weights: chunk c, h, output o -> 8 floats (k-steps 8 h + [0, 8)): sub 0 then sub 1 of lane o + 32 h
   {
     const int total = a.n_chunks * 2 * M * 2;  // quads: [chunk][h][o][sub]
-    for (int b0 = 0; b0 < total; b0 += 128 * B) {
+    for (int b0 = 0; b0 < total; b0 += NT * B) {
       f32x4v v[B];
 #pragma unroll
       for (int j = 0; j < B; ++j) {
-        const int i = b0 + threadIdx.x + 128 * j;
+        const int i = b0 + threadIdx.x + NT * j;
         const int ii = i < total ? i : total - 1;
         const int sub = ii & 1, o = (ii >> 1) % M, h = ((ii >> 1) / M) & 1, c = (ii >> 1) / M >> 1;
         v[j] = *reinterpret_cast<const f32x4v*>(a.wfrag + (size_t)c * a.mt_total * 512 + 256 * sub + (o + 32 * h) * 4);
       }
 #pragma unroll
       for (int j = 0; j < B; ++j) {
-        const int i = b0 + threadIdx.x + 128 * j;
+        const int i = b0 + threadIdx.x + NT * j;
         if (i < total) *reinterpret_cast<f32x4v*>(s_w + 4 * i) = v[j];
       }
     }
   }
   __syncthreads();
-  float acc[M];
+  float acc[MO];
 #pragma unroll
-  for (int o = 0; o < M; ++o) acc[o] = 0.f;
+  for (int o = 0; o < MO; ++o) acc[o] = 0.f;
   for (int si = 0; si < nsrc; ++si) {
     const CnSrc& s = a.src[si];
     const float* const sx = s_x + (si ? xf0 : 0);
     for (int cb = 0; cb < s.nc; ++cb) {
       for (int k = 0; k < s.taps; ++k) {
         const int c = s.chunk_base + k * s.nc + cb;
-        const int r = threadIdx.x + a.chunks[c].row_off - s.off_min;
+        const int r = col + a.chunks[c].row_off - s.off_min;
         const float* xr = sx + THIN_ROW * (cb * s.span + r);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const f32x4v x0 = *reinterpret_cast<const f32x4v*>(xr + 8 * h);
           const f32x4v x1 = *reinterpret_cast<const f32x4v*>(xr + 8 * h + 4);
 #pragma unroll
-          for (int o = 0; o < M; ++o) {
-            const f32x4v w0 = *reinterpret_cast<const f32x4v*>(s_w + ((c * 2 + h) * M + o) * 8);
-            const f32x4v w1 = *reinterpret_cast<const f32x4v*>(s_w + ((c * 2 + h) * M + o) * 8 + 4);
+          for (int o = 0; o < MO; ++o) {
+            const int oo = sub + TPC * o;
+            const f32x4v w0 = *reinterpret_cast<const f32x4v*>(s_w + ((c * 2 + h) * M + oo) * 8);
+            const f32x4v w1 = *reinterpret_cast<const f32x4v*>(s_w + ((c * 2 + h) * M + oo) * 8 + 4);
 #pragma unroll
             for (int e = 0; e < 4; ++e) acc[o] = fmaf(w0[e], x0[e], acc[o]);
 #pragma unroll
@@ -2967,18 +2992,19 @@ __global__ void __launch_bounds__(128) pwg_cnet_thin1_kernel(const CnConvArgs a,
   }
   bool bad = false;
 #pragma unroll
-  for (int o = 0; o < M; ++o) {
-    if (o >= a.M) break;
-    float v = acc[o] + a.bias[o];
-    if (rrow) v += rrow[o];
-    if (a.accumulate) v = yrow[o] + v;
+  for (int o = 0; o < MO; ++o) {
+    const int oo = sub + TPC * o;
+    if (oo >= a.M) break;
+    float v = acc[o] + a.bias[oo];
+    if (rrow) v += rrow[oo];
+    if (a.accumulate) v = yrow[oo] + v;
     if (a.out_div != 1.f) v = v / a.out_div;
     if (a.post_act == PWG_ACT_LRELU) v = v > 0.f ? v : v * a.post_slope;
     else if (a.post_act == PWG_ACT_TANH) v = tanhf(v);
     bad |= !__builtin_isfinite(v);
-    yrow[o] = v;
+    yrow[oo] = v;
   }
-  for (int o = a.M; o < a.ld_dst; ++o) yrow[o] = 0.f;
+  for (int o = a.M + sub; o < a.ld_dst; o += TPC) yrow[o] = 0.f;
   if (a.range_flag) flag_range(a.range_flag, nullptr, bad, (int)(threadIdx.x & 63));
 }
 
@@ -3909,8 +3935,8 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
         // then runs it, 1-2 waves)
         if (n->narrow_dma && !op.src[0].normalize && !(op.src[1].buf >= 0 && op.src[1].normalize) &&
             ph.chunks.size() <= (size_t)XDMA_CHUNKS_MAX &&
-            xdma_fits(ncols, xdma_waves(ncols), (long long)ph.mt_total * zn)) {
-          pick_w = xdma_waves(ncols);
+            xdma_fits(ncols, std::min(2, xdma_waves(ncols)), (long long)ph.mt_total * zn)) {
+          pick_w = std::min(2, xdma_waves(ncols));  // K = 1 mode: 2 waves keep a 4-chunk step's ring 6 deep
           p->nar_xdma[pi] = 1;
         } else {
           bool found = false;
@@ -4379,14 +4405,14 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         size_t tl1 = (size_t)a.n_chunks * 2 * mt_ * 8 * sizeof(float);
         for (int si = 0; si < nsrc; ++si) tl1 += (size_t)ph.thin_nc[si] * ph.thin_span[si] * THIN_ROW * sizeof(float);
         if (tl1 <= (size_t)THIN1_LDS) {
-          auto go = [&](auto kfn) -> hipError_t {
+          auto go = [&](auto kfn, int tpc) -> hipError_t {
             const hipError_t e1 = allow_lds(reinterpret_cast<const void*>(kfn), (int)tl1);
             if (e1 != hipSuccess) return e1;
-            hipLaunchKernelGGL(kfn, tgrid, tblock, tl1, s, a, nsrc);
+            hipLaunchKernelGGL(kfn, tgrid, dim3(CN_COLS * tpc), tl1, s, a, nsrc);
             return hipGetLastError();
           };
-          const hipError_t e1 = mt_ == 1 ? go(pwg_cnet_thin1_kernel<1>)
-                                : mt_ == 4 ? go(pwg_cnet_thin1_kernel<4>) : go(pwg_cnet_thin1_kernel<8>);
+          const hipError_t e1 = mt_ == 1 ? go(pwg_cnet_thin1_kernel<1, 1>, 1)
+                                : mt_ == 4 ? go(pwg_cnet_thin1_kernel<4, 4>, 4) : go(pwg_cnet_thin1_kernel<8, 4>, 4);
           if (e1 != hipSuccess) return hipf(e1, "thin kernel launch");
         } else if (op.out_channels <= 1) hipLaunchKernelGGL(pwg_cnet_thin_kernel<1>, tgrid, tblock, tl, s, a, nsrc);
         else if (op.out_channels <= 4) hipLaunchKernelGGL(pwg_cnet_thin_kernel<4>, tgrid, tblock, tl, s, a, nsrc);
