@@ -27,6 +27,8 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -1176,11 +1178,17 @@ __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArg
         __builtin_amdgcn_global_load_lds((gptr_t)(xs + xoff[k]), (lptr_t)(slot + i * 1024), 16, 0, 0);
       }
     } else {
+      // a chunk's XC rows are 2 NWV instructions: wave w's k-th is chunk k / 2, row group
+      // w + NWV (k & 1) (DX = 2 G, no clamping); the step's chunk descriptors are read once
+      static_assert(S::DX == 2 * S::G && S::NX == 2 * NWV * S::G, "K = 1 DMA layout");
+      ChunkDesc cds[S::G];
+#pragma unroll
+      for (int t = 0; t < S::G; ++t) cds[t] = chunk(min(s * S::G + t, nch - 1));
 #pragma unroll
       for (int k = 0; k < S::DX; ++k) {
-        const int i = wave + NWV * k < S::NX ? wave + NWV * k : S::NX - 1;
-        const int t = i / (S::XC / 16), ii = i - t * (S::XC / 16);  // chunk of the step, row group
-        const ChunkDesc cd = chunk(min(s * S::G + t, nch - 1));
+        const int t = k >> 1, ii = wave + NWV * (k & 1);
+        const int i = t * 2 * NWV + ii;
+        const ChunkDesc& cd = cds[t];
         const CnSrc& sx = a.src[cd.src];
         const int sgx = cd.src ? sgx1 : sgx0, sgy = cd.src ? sgy1 : sgy0;
         int p = q0 + cd.row_off + 16 * ii + (lane >> 2);
@@ -1240,12 +1248,17 @@ __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArg
         reinterpret_cast<const u32x4v*>(xt_smem + (size_t)(g % P) * S::SLOT + S::NX * 1024) + lane;
     constexpr int KT = S::KT;
     u32x4v bh[KT], bl[KT], ah[KT][MT], al[KT][MT];
+    ChunkDesc cds[S::G];
+    if constexpr (K == 1) {
+#pragma unroll
+      for (int t = 0; t < S::G; ++t) cds[t] = chunk(min(g * S::G + t, nch - 1));
+    }
 #pragma unroll
     for (int t = 0; t < KT; ++t) {
       if constexpr (K == 1) {
         // chunk g G + t: the lane's 8 channels of its raw row, pre-activated and pair-split in
         // registers (pwg_cnet_conv_kernel's bprep + cn_split8)
-        const ChunkDesc cd = chunk(min(g * S::G + t, nch - 1));
+        const ChunkDesc& cd = cds[t];
         const CnSrc& sx = a.src[cd.src];
         const int r = wave * 32 + cl;
         int p = q0 + cd.row_off + r;
@@ -1302,6 +1315,8 @@ __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArg
     if (s < ns) issue(s);
   stamp();
   if constexpr (K == 1) {
+    stamp();  // (probe builds: keep the K > 1 timeline's column layout)
+    stamp();
     // one barrier per step: after it every wave is done with step g - 1's slot, which the issue of
     // step g + P - 1 refills
     for (int g = 0; g < ns; ++g) {
@@ -3149,6 +3164,7 @@ struct PwgCnet {
                        // launches run on auxiliary streams, 2 every plan
   static constexpr int N_AUX = 3;
   hipStream_t aux[N_AUX] = {nullptr, nullptr, nullptr};
+  std::mutex mu;       // the auxiliary streams and the plans' event sets (concurrent runs from host threads)
   bool pair_attr_set = false;
   std::vector<PwgCnetOp> ops;
   std::vector<int> channels, rate, ld;
@@ -3187,7 +3203,9 @@ struct PwgCnetPlan {
   std::vector<int2*> d_nblocks;              // its blocks (utt, q0 step 32 nar_nwv)
   std::vector<int2*> d_nfr;                  // ... and their utterances' (first frame, frames)
   bool has_narrow = false;                   // some phase runs narrow (PWG_CNET_OPT_STREAMS 1)
-  std::vector<hipEvent_t> xev;               // cross-stream dependency events (reused every run)
+  // cross-stream dependency events, one set per caller stream (runs of one plan on two streams
+  // must not record into each other's events), reused every run; guarded by PwgCnet::mu
+  std::map<hipStream_t, std::vector<hipEvent_t>> xev_of;
 };
 
 namespace {
@@ -4070,7 +4088,8 @@ void pwg_cnet_plan_destroy(PwgCnetPlan* p) {
   for (auto* x : p->d_xblocks) if (x) (void)hipFree(x);
   for (auto* x : p->d_nblocks) if (x) (void)hipFree(x);
   for (auto* x : p->d_nfr) if (x) (void)hipFree(x);
-  for (hipEvent_t e : p->xev) (void)hipEventDestroy(e);
+  for (auto& kv : p->xev_of)
+    for (hipEvent_t e : kv.second) (void)hipEventDestroy(e);
   delete p;
 }
 
@@ -4152,6 +4171,9 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
   // program order: same launches, same arithmetic, bit-identical to one stream.
   const int NS = 1 + PwgCnet::N_AUX;
   const bool conc = n->streams == 2 || (n->streams == 1 && p->has_narrow);
+  std::unique_lock<std::mutex> lock(n->mu, std::defer_lock);
+  if (conc) lock.lock();  // held for the whole enqueue: the aux streams are the handle's
+  std::vector<hipEvent_t>* xev_run = nullptr;
   std::vector<int> l_stream(launches.size(), 0), l_event(launches.size(), -1);
   std::vector<std::vector<int>> l_waits(launches.size());  // launch indices waited for (other streams)
   bool stream_used[1 + PwgCnet::N_AUX] = {true, false, false, false};
@@ -4226,17 +4248,19 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
     for (int k = 1; k < NS; ++k)
       if (stream_used[k] && tail[k] >= 0 && l_event[tail[k]] < 0) l_event[tail[k]] = ne++;
     ne += 1;  // the fork event (s_main after the flag reset)
-    while ((int)p->xev.size() < ne) {
+    std::vector<hipEvent_t>& xev = p->xev_of[s_main];
+    xev_run = &xev;
+    while ((int)xev.size() < ne) {
       hipEvent_t e = nullptr;
       if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(PWG_ERR_HIP, "event create");
-      p->xev.push_back(e);
+      xev.push_back(e);
     }
     for (int k = 1; k < NS; ++k)
       if (stream_used[k] && !n->aux[k - 1] &&
           hipStreamCreateWithFlags(&n->aux[k - 1], hipStreamNonBlocking) != hipSuccess)
         return fail(PWG_ERR_HIP, "auxiliary stream create");
     // fork: the aux streams start after everything queued on the caller's stream so far
-    hipEvent_t fork = p->xev[ne - 1];
+    hipEvent_t fork = xev[ne - 1];
     if (hipEventRecord(fork, s_main) != hipSuccess) return fail(PWG_ERR_HIP, "fork event");
     for (int k = 1; k < NS; ++k)
       if (stream_used[k] && hipStreamWaitEvent(n->aux[k - 1], fork, 0) != hipSuccess)
@@ -4251,7 +4275,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
     const size_t L = li++;
     hipStream_t const s = stream_of(l_stream[L]);
     for (int d : l_waits[L])
-      if (hipStreamWaitEvent(s, p->xev[l_event[d]], 0) != hipSuccess) return fail(PWG_ERR_HIP, "dependency wait");
+      if (hipStreamWaitEvent(s, (*xev_run)[l_event[d]], 0) != hipSuccess) return fail(PWG_ERR_HIP, "dependency wait");
     hipEvent_t ea = nullptr, eb = nullptr;
     if (n->timing) {
       for (hipEvent_t* ev : {&ea, &eb}) {
@@ -4541,7 +4565,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
       (void)hipEventRecord(eb, s);
       n->records.push_back({ph.op, ea, eb});
     }
-    if (l_event[L] >= 0 && hipEventRecord(p->xev[l_event[L]], s) != hipSuccess)
+    if (l_event[L] >= 0 && hipEventRecord((*xev_run)[l_event[L]], s) != hipSuccess)
       return fail(PWG_ERR_HIP, "dependency event");
   }
   // join: the caller's stream waits for every auxiliary stream's last launch
@@ -4549,7 +4573,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
     int tail_of[1 + PwgCnet::N_AUX] = {-1, -1, -1, -1};
     for (size_t L = 0; L < launches.size(); ++L) tail_of[l_stream[L]] = (int)L;
     for (int k = 1; k < NS; ++k)
-      if (tail_of[k] >= 0 && hipStreamWaitEvent(s_main, p->xev[l_event[tail_of[k]]], 0) != hipSuccess)
+      if (tail_of[k] >= 0 && hipStreamWaitEvent(s_main, (*xev_run)[l_event[tail_of[k]]], 0) != hipSuccess)
         return fail(PWG_ERR_HIP, "join wait");
   }
   hipStream_t const s = s_main;

@@ -414,8 +414,23 @@ def test_concurrent_streams_bitwise_equal(cfg, built_lib, cuda_device):
             out.zero_()
             g.replay()
             torch.cuda.synchronize()
+        # one plan enqueued on two caller streams back to back (each run forks / joins its own events)
+        mel2 = torch.from_numpy(synthetic.make_mel(64, 80, seed=190)).to(cuda_device).reshape(-1).contiguous()
+        eng.set_streams(0)
+        ref2 = torch.empty_like(out)
+        eng.run(plan, mel2, ref2)
+        eng.set_streams(1)
+        s1, s2 = torch.cuda.Stream(cuda_device), torch.cuda.Stream(cuda_device)
+        o1, o2 = torch.empty_like(out), torch.empty_like(out)
+        torch.cuda.synchronize()
+        for _ in range(3):
+            eng.run(plan, mel, o1, stream=s1, check=False)
+            eng.run(plan, mel2, o2, stream=s2, check=False)
+        torch.cuda.synchronize()
     for mode in (1, 2):
         for a, b in zip(outs[mode], outs[0]):
             assert np.isfinite(a).all()
             np.testing.assert_array_equal(a, b)
     np.testing.assert_array_equal(out.cpu().numpy().reshape(outs[0][0].shape), outs[0][0])
+    np.testing.assert_array_equal(o1.cpu().numpy().reshape(outs[0][0].shape), outs[0][0])
+    np.testing.assert_array_equal(o2.cpu().numpy(), ref2.cpu().numpy())

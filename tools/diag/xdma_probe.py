@@ -58,10 +58,13 @@ def main():
         steps = d[3:3 + 4 * ns]
         per = steps[:4 * (len(steps) // 4)].reshape(-1, 4).mean(axis=0) if len(steps) >= 4 else np.zeros(4)
         tail = d[3 + 4 * ns:]
+        if K == 1:  # per step: wait + barrier, issue, MFMAs (in-register split), -
+            cols = f"per step wait {per[0]:6.0f} issue {per[1]:6.0f} mma {per[2]:6.0f}"
+        else:
+            cols = f"per step issue {per[0]:6.0f} wait {per[1]:6.0f} mma {per[2]:6.0f} conv {per[3]:6.0f}"
         print(f"phase {slot:3d} K{K:<2d} MT{MT} W{NWV} steps {ns:3d} P{P}  total {t[-1]:7d} cyc  "
-              f"prologue issue {head[0]:5d} wait {head[1]:6d} conv0 {head[2]:5d} | per step issue {per[0]:6.0f} "
-              f"wait {per[1]:6.0f} mma {per[2]:6.0f} conv {per[3]:6.0f} | epilogue {int(tail.sum()) if len(tail) else 0:6d}",
-              flush=True)
+              f"prologue issue {head[0]:5d} wait {head[1]:6d} conv0 {head[2]:5d} | {cols} | "
+              f"epilogue {int(tail.sum()) if len(tail) else 0:6d}", flush=True)
     print("ops:", len(names))
 
 
