@@ -215,9 +215,11 @@ class CnetPlan:
 
     def __del__(self):
         p = getattr(self, "_p", None)
-        if p is not None and p.value:
+        h = getattr(self.eng, "_h", None)
+        # (a plan outliving its engine's handle is leaked, not destroyed: its C struct points at it)
+        if p is not None and p.value and h is not None and h.value:
             self.eng._lib.pwg_cnet_plan_destroy(p)
-            self._p = None
+        self._p = None
 
 
 class CnetEngine:
@@ -246,12 +248,23 @@ class CnetEngine:
         self._plans = OrderedDict()
         self._workspaces = {}
         self.split_f16 = True       # PWG_CNET_OPT_SPLIT_F16 (the library default)
+        self.graphs = True          # replay captured forwards of small plans (set_graphs)
+        # ... of programs with parallel branches (an accumulated sum: HiFiGAN's MRF blocks), the ones
+        # PWG_CNET_OPT_STREAMS runs concurrently; a single chain (MelGAN) gains nothing from the graph
+        # and pays its input / output copies (MB-MelGAN v2 T' = 64: 0.449 -> 0.466 ms)
+        self._branchy = any(op["accumulate"] for op in program.ops)
+        self._graphs = OrderedDict()
+        self._graph_epoch = 0       # bumped by every option change: captured forwards are stale
+        self._last_ws = {}          # (plan, stream) -> workspace of its last replayed forward
+        self._timing = False
         self.split_range_ok = True  # the loaded weights fit the fp16 pair range
         self.range_reruns = 0       # runs redone in exact fp32 after a split-f16 range flag
 
     def __del__(self):
         h = getattr(self, "_h", None)
         if h is not None and h.value:
+            self._graphs = OrderedDict()  # captured forwards hold plans: release them first
+            self._last_ws = {}
             self._plans = OrderedDict()
             self._lib.pwg_cnet_destroy(h)
             self._h = None
@@ -327,10 +340,20 @@ class CnetEngine:
         semantics. check=False only enqueues (the bench's timed loop; ``run_status`` afterwards)."""
         if stream is None:
             stream = torch.cuda.current_stream(self.device)
-        self._enqueue(plan, mel, out, mean, scale, stream)
+        ws = None
+        key = (id(plan), stream.cuda_stream)
+        if self._graph_ok(plan, mean, stream):
+            ws = self._replay(plan, mel, out, stream)
+            self._last_ws[key] = ws  # run_status reads the captured forward's own workspace
+        else:
+            self._last_ws.pop(key, None)
+            self._enqueue(plan, mel, out, mean, scale, stream)
         if check and self.split_f16:
             try:
-                self.run_status(plan, stream)
+                if ws is None:
+                    self.run_status(plan, stream)
+                else:
+                    _lib.check(self._lib.pwg_cnet_run_status(plan._p, ws.data_ptr(), stream.cuda_stream))
             except _lib.RangeError as e:
                 logging.warning("%s; rerunning in exact fp32", e)
                 self._set_split(False)
@@ -341,12 +364,63 @@ class CnetEngine:
                 self.range_reruns += 1
         return out
 
+    # ------------------------------------------------------------------ captured forwards
+    # A small plan's forward is 30-80 latency-bound launches, and with PWG_CNET_OPT_STREAMS its
+    # independent launches only overlap if they are queued faster than the GPU runs them: enqueued
+    # from the host (~10 us per launch with its events) HiFiGAN v1's B = 1 forward was host-bound
+    # (profiles/r04_m). Small plans therefore run as a hipGraph captured once per (plan, caller
+    # stream, weights, options) and replayed: input copied into the graph's buffer, replay, output
+    # copied out. Same kernels, same arguments: bit-identical to the eager forward.
+    GRAPH_MAX_FRAMES = 512
+
+    def set_graphs(self, enable):
+        """Replay captured forwards of small plans (default on); off: every forward enqueued."""
+        self.graphs = bool(enable)
+        self._graphs.clear()
+
+    def _graph_ok(self, plan, mean, stream):
+        return (self.graphs and self._branchy and not self._timing and mean is None
+                and sum(plan.frames) <= self.GRAPH_MAX_FRAMES and not torch.cuda.is_current_stream_capturing())
+
+    def _replay(self, plan, mel, out, stream):
+        key = (id(plan), stream.cuda_stream, self.packed.data_ptr(), self.split_f16, self._graph_epoch)
+        ent = self._graphs.get(key)
+        if ent is None:
+            for name, t in (("mel", mel), ("out", out)):
+                if t.device != self.device or t.dtype != torch.float32 or not t.is_contiguous():
+                    raise ValueError(f"{name} must be a contiguous float32 tensor on {self.device}")
+            cs = torch.cuda.Stream(self.device)  # capture stream: its workspace belongs to this graph
+            g_mel, g_out = torch.empty_like(mel), torch.empty_like(out)
+            cs.wait_stream(stream)
+            with torch.cuda.stream(cs):
+                g_mel.copy_(mel)
+                self._enqueue(plan, g_mel, g_out, None, None, cs)  # warm-up: sizes the workspace
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=cs):
+                    self._enqueue(plan, g_mel, g_out, None, None, cs)
+            stream.wait_stream(cs)
+            # (the entry holds the plan, the weights and the workspace the graph's launches point at)
+            ent = (g, g_mel, g_out, cs, self.workspace(plan.workspace_bytes, cs), plan, self.packed)
+            self._graphs[key] = ent
+            while len(self._graphs) > 8:
+                self._graphs.popitem(last=False)
+        g, g_mel, g_out, cs, ws = ent[:5]
+        if mel.numel() != g_mel.numel() or out.numel() != g_out.numel():
+            raise ValueError("mel / output buffer has the wrong size for the plan")
+        with torch.cuda.stream(stream):
+            g_mel.copy_(mel)
+            g.replay()
+            out.copy_(g_out)
+        return ws
+
     def run_status(self, plan, stream=None):
         """pwg_cnet_run_status of the last run on ``stream``'s workspace: raises _lib.RangeError
         when the split-f16 range flag is set (synchronises the stream)."""
         if stream is None:
             stream = torch.cuda.current_stream(self.device)
-        ws = self.workspace(plan.workspace_bytes, stream)
+        ws = self._last_ws.get((id(plan), stream.cuda_stream))
+        if ws is None:
+            ws = self.workspace(plan.workspace_bytes, stream)
         _lib.check(self._lib.pwg_cnet_run_status(plan._p, ws.data_ptr(), stream.cuda_stream))
 
     def _enqueue(self, plan, mel, out, mean, scale, stream):
@@ -386,9 +460,11 @@ class CnetEngine:
 
     def set_timing(self, enable):
         _lib.check(self._lib.pwg_cnet_set_timing(self._h, int(enable)))
+        self._timing = bool(enable)  # per-op events: forwards run eagerly while on
 
     def _set_split(self, enable):
         _lib.check(self._lib.pwg_cnet_set_option(self._h, 0, int(bool(enable))))
+        self._graph_epoch += 1
 
     def set_split_f16(self, enable):
         """pwg_cnet_set_option(PWG_CNET_OPT_SPLIT_F16): fp16-pair operands on the f16 MFMA
@@ -403,12 +479,14 @@ class CnetEngine:
         other reader (HiFiGAN ResBlock steps) as one kernel, intermediate in LDS (default on,
         split-f16 mode only; bit-identical to the unfused ops)."""
         _lib.check(self._lib.pwg_cnet_set_option(self._h, 1, int(bool(enable))))
+        self._graph_epoch += 1
 
     def set_xtile(self, enable):
         """pwg_cnet_set_option(PWG_CNET_OPT_XTILE): dilated convs channel-block-major with the
         input tile staged once per 16-channel block (default on); off: the tap-major kernel and
         the fused conv pairs."""
         _lib.check(self._lib.pwg_cnet_set_option(self._h, 3, int(bool(enable))))
+        self._graph_epoch += 1
 
     XT_DMA_RULE, XT_DMA_ALL, XT_DMA_FEWEST, XT_DMA_CONVT = 1, 2, 4, 8  # include/pwg_cnet.h flags
 
@@ -418,11 +496,13 @@ class CnetEngine:
         the register-staged kernels): 1 the shapes where that measured faster, 2 every eligible conv,
         4 the fewest tap groups; 8 the wide ConvTranspose phases on that kernel. Default 9."""
         _lib.check(self._lib.pwg_cnet_set_option(self._h, 4, int(mode)))
+        self._graph_epoch += 1
 
     def set_xcd_order(self, enable):
         """pwg_cnet_set_option(PWG_CNET_OPT_XCD_ORDER): the m-groups / ConvTranspose phases of one
         column block run on one XCD back to back, sharing its L2 (default on; same results)."""
         _lib.check(self._lib.pwg_cnet_set_option(self._h, 5, int(bool(enable))))
+        self._graph_epoch += 1
 
     def set_narrow(self, mode):
         """pwg_cnet_set_option(PWG_CNET_OPT_NARROW): small launches of the x-tile family run narrow
@@ -430,24 +510,28 @@ class CnetEngine:
         have fewer workgroups than CUs, 2 always, 0 never. Plan-time: cached plans are dropped.
         Bit-identical."""
         _lib.check(self._lib.pwg_cnet_set_option(self._h, 6, int(mode)))
+        self._graph_epoch += 1
         self._plans.clear()
 
     def set_streams(self, mode):
         """pwg_cnet_set_option(PWG_CNET_OPT_STREAMS): independent launches on auxiliary streams
         for plans with narrow launches (1, default), every plan (2) or never (0). Bit-identical."""
         _lib.check(self._lib.pwg_cnet_set_option(self._h, 8, int(mode)))
+        self._graph_epoch += 1
 
     def set_narrow_dma(self, enable):
         """pwg_cnet_set_option(PWG_CNET_OPT_NARROW_DMA): narrow launches on the DMA-ring kernel
         (default) or, 0, on the narrow x-tile / tap-major kernels. Plan-time (cached plans are
         dropped); bit-identical."""
         _lib.check(self._lib.pwg_cnet_set_option(self._h, 7, 1 if enable else 0))
+        self._graph_epoch += 1
         self._plans.clear()
 
     def set_pair_steps(self, steps):
         """pwg_cnet_set_option(PWG_CNET_OPT_PAIR_STEPS): 128-column tiles per fused-pair
         workgroup, for plans created afterwards (cached plans are dropped)."""
         _lib.check(self._lib.pwg_cnet_set_option(self._h, 2, int(steps)))
+        self._graph_epoch += 1
         self._plans.clear()
 
     def collect_timing(self):

@@ -434,3 +434,35 @@ def test_concurrent_streams_bitwise_equal(cfg, built_lib, cuda_device):
     np.testing.assert_array_equal(out.cpu().numpy().reshape(outs[0][0].shape), outs[0][0])
     np.testing.assert_array_equal(o1.cpu().numpy().reshape(outs[0][0].shape), outs[0][0])
     np.testing.assert_array_equal(o2.cpu().numpy(), ref2.cpu().numpy())
+
+
+@pytest.mark.parametrize("cfg", ["hifigan_v1", "hifigan_v1_causal"])
+def test_graph_replay_bitwise_equal(cfg, built_lib, cuda_device):
+    """Small plans replay a captured forward (CnetEngine.graphs): same bits as the eager forward,
+    for two different inputs through one captured graph, after an option change (re-capture) and
+    with the range check reading the graph's own workspace."""
+    from parallelwavegan_amd import configs, synthetic
+    from parallelwavegan_amd.hifigan import HiFiGANGenerator
+    from parallelwavegan_amd.melgan import PQMF, MelGANGenerator
+
+    cls_name, params = configs.vocoder_params(cfg)
+    m = {"MelGANGenerator": MelGANGenerator, "HiFiGANGenerator": HiFiGANGenerator}[cls_name](**params)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic.make_module_state_dict(m, seed=13).items()})
+    if cfg in configs.VOCODER_PQMF:
+        m.pqmf = PQMF(**configs.VOCODER_PQMF[cfg])
+    m = m.to(cuda_device)
+    eng = m.engine()
+    mels = [torch.from_numpy(synthetic.make_mel(48, 80, seed=200 + i)).to(cuda_device) for i in range(2)]
+    with torch.no_grad():
+        eng.set_graphs(False)
+        ref = [m.inference(x).cpu().numpy() for x in mels]
+        eng.set_graphs(True)
+        got = [m.inference(x).cpu().numpy() for x in mels] + [m.inference(mels[0]).cpu().numpy()]
+        n_graphs = len(eng._graphs)
+        eng.set_streams(0)  # option change: captured forwards are stale, the next call re-captures
+        got.append(m.inference(mels[1]).cpu().numpy())
+        eng.set_streams(1)
+    assert n_graphs == 1
+    for a, b in zip(got, [ref[0], ref[1], ref[0], ref[1]]):
+        np.testing.assert_array_equal(a, b)
+

@@ -42,6 +42,25 @@ def run(cfg, T, dma):
     print("launches per forward marker", flush=True)
 
 
+def summarize_concurrent(d, per):
+    """The last forward's `per` launches by start time (forwards are serialised by the join), with
+    the queue they ran on and the idle time of the forward's span."""
+    rows = []
+    for path in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+        for r in csv.DictReader(open(path)):
+            q = r.get("Queue_Id") or r.get("Stream_Id") or "?"
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], q))
+    rows.sort()
+    last = rows[-per:]
+    t0 = last[0][0]
+    span = (max(e for _, e, _, _ in last) - t0) * 1e-3
+    busy = sum(e - s for s, e, _, _ in last) * 1e-3
+    for s, e, name, q in last:
+        short = name.split("(")[0].replace("void pwg::(anonymous namespace)::", "")[:60]
+        print(f"{(s - t0) * 1e-3:8.1f} .. {(e - t0) * 1e-3:8.1f} us  q{q:>3}  {short}")
+    print(f"forward span {span:.1f} us, kernel time {busy:.1f} us (sum over streams)")
+
+
 def summarize(d):
     rows = []
     for path in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
@@ -78,5 +97,7 @@ def summarize(d):
 if __name__ == "__main__":
     if sys.argv[1] == "run":
         run(sys.argv[2], int(sys.argv[3]), int(sys.argv[4]) if len(sys.argv) > 4 else 1)
+    elif sys.argv[1] == "concurrent":
+        summarize_concurrent(sys.argv[2], int(sys.argv[3]))
     else:
         summarize(sys.argv[2])
