@@ -1007,9 +1007,8 @@ struct CnXdmaArgs {
   int rate[2], rate_dst, rate_res;  // rows per frame of the sources', destination and residual buffers
 };
 constexpr int XDMA_CHUNKS_MAX = 256;  // K = 1 mode: chunks per op (the table sits in LDS)
-#ifndef XDMA_K1_G
-#define XDMA_K1_G 4                   // K = 1 mode: chunks per step
-#endif
+constexpr int XDMA_K1_G = 4;          // K = 1 mode: chunks per step
+constexpr int XDMA_RING_CAP = 4;      // ring slots at most (see XdmaShape::ring)
 #ifdef PWG_XDMA_PROBE
 constexpr int XDMA_PROBE_SLOTS = 128, XDMA_PROBE_N = 96;
 __device__ unsigned long long g_xdma_probe[XDMA_PROBE_SLOTS][XDMA_PROBE_N];
@@ -1030,17 +1029,14 @@ struct XdmaShape {
   // K > 1: two converted-row buffers; K = 1: none (B split in registers) but the chunk table
   static constexpr int CBUF = K == 1 ? 0 : XR * XT_ROWB;
   static constexpr int CHT = K == 1 ? XDMA_CHUNKS_MAX * (int)sizeof(ChunkDesc) : 0;
-  // deepest ring (<= PWG_XDMA_RING_CAP slots) whose wait counts fit vmcnt (63) and LDS 159 KB
+  // deepest ring (<= XDMA_RING_CAP slots) whose wait counts fit vmcnt (63) and LDS 159 KB
   static constexpr int ring(int p) {
     return p <= 2 ? 2 : (((p - 2) * D <= 63 && p * SLOT + 2 * CBUF + CHT <= 159 * 1024) ? p : ring(p - 1));
   }
-// at most 4 slots: the prologue issues P - 1 steps before the first MFMA, and deeper rings measured
-// slower at B = 1 (MB-MelGAN v2 T' = 64: 16 slots 0.507 ms, 8: 0.508, 4: 0.478; HiFiGAN v1 0.973 /
-// 0.989 / 0.954; profiles/r04_h)
-#ifndef PWG_XDMA_RING_CAP
-#define PWG_XDMA_RING_CAP 4
-#endif
-  static constexpr int P = ring(PWG_XDMA_RING_CAP);
+  // at most 4 slots: the prologue issues P - 1 steps before the first MFMA, and deeper rings
+  // measured slower at B = 1 (MB-MelGAN v2 T' = 64: 16 slots 0.507 ms, 8: 0.508, 4: 0.478;
+  // HiFiGAN v1 0.973 / 0.989 / 0.954; profiles/r04_h)
+  static constexpr int P = ring(XDMA_RING_CAP);
   static constexpr int LDS = P * SLOT + 2 * CBUF + CHT;
   static_assert(LDS <= 160 * 1024, "DMA-ring shape");
 };
