@@ -108,6 +108,11 @@ PWG_API int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, 
  * pwg_cnet_pack_weights likewise returns PWG_ERR_RANGE when a weight cannot be carried as an fp16
  * pair; the packed image is still complete for the exact-fp32 mode. */
 PWG_API int pwg_cnet_run_status(PwgCnetPlan* p, const void* workspace, void* stream);
+/* The launches pwg_cnet_run would make now (host only, no GPU needed; host-only plans too): their
+ * count, and for the first `cap` of them the program phase each starts at, the stream it goes to
+ * (0 = the caller's, 1-3 = the handle's auxiliary streams, PWG_CNET_OPT_STREAMS) and the enqueue
+ * order (order[i] = the launch enqueued i-th). For tests and tools. */
+PWG_API int pwg_cnet_plan_schedule(PwgCnetPlan* p, int cap, int* n_launches, int* phase, int* stream, int* order);
 /* Options. PWG_CNET_OPT_SPLIT_F16 (default 1): fp32 operands as fp16 hi+lo pairs on the f16
  * MFMA (three products, fp32 accumulate; error class of fp32); 0: fp32 MFMA.
  * PWG_CNET_OPT_FUSE_PAIRS (default 1, split-f16 mode): run "conv A -> t -> conv B" pairs whose

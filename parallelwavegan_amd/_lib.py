@@ -89,6 +89,7 @@ EXPORTED_SYMBOLS = (
     "pwg_cnet_plan_workspace_bytes",
     "pwg_cnet_run",
     "pwg_cnet_run_status",
+    "pwg_cnet_plan_schedule",
     "pwg_cnet_set_option",
     "pwg_cnet_set_timing",
     "pwg_cnet_timing_collect",

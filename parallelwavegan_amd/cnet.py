@@ -85,6 +85,8 @@ def lib():
         L.pwg_cnet_plan_workspace_bytes.restype = ll
         L.pwg_cnet_run.argtypes = [vp] * 8
         L.pwg_cnet_run_status.argtypes = [vp, vp, vp]
+        ip = ctypes.POINTER(ctypes.c_int)
+        L.pwg_cnet_plan_schedule.argtypes = [vp, ctypes.c_int, ip, ip, ip, ip]
         L.pwg_cnet_set_timing.argtypes = [vp, ctypes.c_int]
         L.pwg_cnet_set_option.argtypes = [vp, ctypes.c_int, ctypes.c_longlong]
         L.pwg_cnet_timing_collect.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ll)]
@@ -412,6 +414,16 @@ class CnetEngine:
             g.replay()
             out.copy_(g_out)
         return ws
+
+    def schedule(self, plan):
+        """pwg_cnet_plan_schedule: [(phase, stream)] per launch in program order, and the enqueue
+        order (launch indices) -- what ``run`` would enqueue with the current options."""
+        n = ctypes.c_int()
+        _lib.check(self._lib.pwg_cnet_plan_schedule(plan._p, 0, ctypes.byref(n), None, None, None))
+        k = n.value
+        ph, st, od = (ctypes.c_int * k)(), (ctypes.c_int * k)(), (ctypes.c_int * k)()
+        _lib.check(self._lib.pwg_cnet_plan_schedule(plan._p, k, ctypes.byref(n), ph, st, od))
+        return list(zip(ph, st)), list(od)
 
     def run_status(self, plan, stream=None):
         """pwg_cnet_run_status of the last run on ``stream``'s workspace: raises _lib.RangeError

@@ -3250,6 +3250,163 @@ float cn_h2f(uint16_t h) {
   return (h & 0x8000u) ? -v : v;
 }
 
+// The launches of one run and, with PWG_CNET_OPT_STREAMS, their streams, cross-stream waits and
+// enqueue order (host only: pwg_cnet_run and pwg_cnet_plan_schedule).
+struct CnSchedule {
+  std::vector<std::pair<int, int>> launches;  // (phase, second op fused into the launch or -1)
+  bool conc = false;
+  std::vector<int> stream, event;              // per launch: stream (0 = caller's), event slot or -1
+  std::vector<std::vector<int>> waits;         // per launch: launches on other streams it waits for
+  std::vector<size_t> order;                   // enqueue order
+  bool used[1 + PwgCnet::N_AUX] = {true, false, false, false};
+  int n_events = 0;
+};
+int cnet_schedule(PwgCnetPlan* p, CnSchedule& sc) {
+  PwgCnet* n = p->n;
+  const int nb = (int)n->channels.size();
+  const bool fuse = n->fuse_pairs && n->split_f16;
+  const bool xt = n->xtile && n->split_f16;
+  auto pair_fused = [&](const OpPhase& q) { return fuse && q.pair_b >= 0 && !(xt && q.xtile); };
+  auto narrow = [&](size_t i) { return xt && p->nar_nwv[i] > 0 && !p->nar_tap[i]; };
+  // the launches of this run: (phase, second op fused into it or -1)
+  auto skipped = [&](size_t pi) {
+    const OpPhase& ph = n->phases[pi];
+    return (pi > 0 && ((pair_fused(n->phases[pi - 1]) && n->phases[pi - 1].pair_b == (int)pi) ||
+                       (fuse && n->phases[pi - 1].stack_b == (int)pi && !narrow(pi - 1)))) ||
+           ph.z_phases == 0 || (xt && fuse && pi > 0 && n->phases[pi - 1].xpair_b == (int)pi && !narrow(pi - 1));
+  };
+  std::vector<std::pair<int, int>>& launches = sc.launches;
+  for (size_t pi = 0; pi < n->phases.size(); ++pi) {
+    if (skipped(pi)) continue;
+    const OpPhase& ph = n->phases[pi];
+    int second = -1;
+    if (pair_fused(ph)) second = n->phases[ph.pair_b].op;
+    else if (fuse && ph.stack_b >= 0 && !narrow(pi)) second = n->phases[ph.stack_b].op;
+    else if (xt && fuse && ph.xpair_b >= 0 && !narrow(pi)) second = n->phases[ph.xpair_b].op;
+    launches.push_back({(int)pi, second});
+  }
+  // Concurrent launches (PWG_CNET_OPT_STREAMS): a small plan's launches are each a few dozen
+  // workgroups and latency-bound, and a generator's parallel branches (HiFiGAN's multi-receptive-
+  // field blocks, models/hifigan.py:159-168) are independent until their sum: each launch follows
+  // the launch it depends on latest on that launch's stream when it is that stream's last, else
+  // takes the least recently used stream, and waits on an event for every dependency on another
+  // stream. Buffers are written once per run except an accumulated sum, whose writers stay in
+  // program order: same launches, same arithmetic, bit-identical to one stream.
+  const int NS = 1 + PwgCnet::N_AUX;
+  const bool conc = sc.conc = n->streams == 2 || (n->streams == 1 && p->has_narrow);
+  std::vector<int>& l_stream = sc.stream;
+  std::vector<int>& l_event = sc.event;
+  std::vector<std::vector<int>>& l_waits = sc.waits;
+  l_stream.assign(launches.size(), 0);
+  l_event.assign(launches.size(), -1);
+  l_waits.assign(launches.size(), {});
+  bool* const stream_used = sc.used;
+  if (conc) {
+    // dependencies by storage, not buffer id: buffers of a plan built for one stream share slots
+    std::vector<int> mem(nb);
+    for (int b = 0; b < nb; ++b) {
+      mem[b] = b;
+      if (b > 0 && b < nb - 1)
+        for (int c = 1; c < b; ++c)
+          if (p->buf_off[c] == p->buf_off[b]) { mem[b] = mem[c]; break; }
+    }
+    std::vector<int> last_writer(nb, -1);
+    std::vector<std::vector<int>> readers(nb);
+    int tail[1 + PwgCnet::N_AUX] = {-1, -1, -1, -1}, used_at[1 + PwgCnet::N_AUX] = {-1, -1, -1, -1};
+    for (size_t L = 0; L < launches.size(); ++L) {
+      std::vector<int> deps;
+      auto op_deps = [&](int oi) {
+        const PwgCnetOp& o = n->ops[oi];
+        auto rd = [&](int b) {
+          if (b >= 0 && last_writer[mem[b]] >= 0) deps.push_back(last_writer[mem[b]]);
+        };
+        rd(o.src[0].buf);
+        if (o.kind == PWG_CNET_CONV) rd(o.src[1].buf);
+        rd(o.res);
+        if (o.accumulate) rd(o.dst);
+        if (last_writer[mem[o.dst]] >= 0) deps.push_back(last_writer[mem[o.dst]]);  // WAW
+        for (int r : readers[mem[o.dst]]) deps.push_back(r);                          // WAR
+      };
+      op_deps(n->phases[launches[L].first].op);
+      if (launches[L].second >= 0) op_deps(launches[L].second);
+      int best = -1;  // the latest dependency that is its stream's tail
+      for (int d : deps)
+        if (tail[l_stream[d]] == d && (best < 0 || d > best)) best = d;
+      int st;
+      if (best >= 0) {
+        st = l_stream[best];
+      } else if (deps.empty()) {
+        st = 0;
+      } else {
+        st = 0;
+        for (int k = 1; k < NS; ++k)
+          if (used_at[k] < used_at[st]) st = k;
+      }
+      l_stream[L] = st;
+      for (int d : deps)
+        if (l_stream[d] != st && std::find(l_waits[L].begin(), l_waits[L].end(), d) == l_waits[L].end())
+          l_waits[L].push_back(d);
+      tail[st] = (int)L;
+      used_at[st] = (int)L;
+      stream_used[st] = true;
+      auto note = [&](int oi) {
+        const PwgCnetOp& o = n->ops[oi];
+        for (int b : {o.src[0].buf, o.kind == PWG_CNET_CONV ? o.src[1].buf : -1, o.res, o.accumulate ? o.dst : -1})
+          if (b >= 0) readers[mem[b]].push_back((int)L);
+      };
+      note(n->phases[launches[L].first].op);
+      if (launches[L].second >= 0) note(launches[L].second);
+      auto wrote = [&](int oi) {
+        const int b = mem[n->ops[oi].dst];
+        last_writer[b] = (int)L;
+        readers[b].clear();
+      };
+      wrote(n->phases[launches[L].first].op);
+      if (launches[L].second >= 0) wrote(launches[L].second);
+    }
+    // events: after every launch some launch on another stream waits for, and each aux stream's tail
+    int ne = 0;
+    for (size_t L = 0; L < launches.size(); ++L)
+      for (int d : l_waits[L])
+        if (l_event[d] < 0) l_event[d] = ne++;
+    for (int k = 1; k < NS; ++k)
+      if (stream_used[k] && tail[k] >= 0 && l_event[tail[k]] < 0) l_event[tail[k]] = ne++;
+    sc.n_events = ne;
+  }
+  // Enqueue order: program order on one stream; with concurrency, breadth-first over the streams
+  // (round robin, a launch once every launch it waits for is enqueued -- its event then recorded),
+  // so each branch's first launches reach the GPU before the host has enqueued a whole other branch
+  // (~5-10 us of host time per launch: in program order HiFiGAN's second and third residual chains
+  // started 60 and 140 us after the first, profiles/r04_m). Per stream the order is program order.
+  std::vector<size_t>& order = sc.order;
+  order.clear();
+  order.reserve(launches.size());
+  if (!conc) {
+    for (size_t L = 0; L < launches.size(); ++L) order.push_back(L);
+  } else {
+    std::vector<std::vector<size_t>> per(NS);
+    for (size_t L = 0; L < launches.size(); ++L) per[l_stream[L]].push_back(L);
+    std::vector<size_t> head(NS, 0);
+    std::vector<char> done(launches.size(), 0);
+    while (order.size() < launches.size()) {
+      bool progress = false;
+      for (int k = 0; k < NS; ++k) {
+        if (head[k] >= per[k].size()) continue;
+        const size_t L = per[k][head[k]];
+        bool ready = true;
+        for (int d : l_waits[L]) ready = ready && done[d];
+        if (!ready) continue;
+        order.push_back(L);
+        done[L] = 1;
+        ++head[k];
+        progress = true;
+      }
+      if (!progress) return fail(PWG_ERR_ASSERT, "internal: no enqueue order for the concurrent launches");
+    }
+  }
+  return PWG_OK;
+}
+
 int pick_mt(int mt_total) {
   if (mt_total <= 4) return mt_total;
   if (mt_total % 4 == 0) return 4;
@@ -4141,109 +4298,23 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
 #else
   auto probe_slot = [](size_t) { return -1; };
 #endif
-  // the launches of this run: (phase, second op fused into it or -1)
-  auto skipped = [&](size_t pi) {
-    const OpPhase& ph = n->phases[pi];
-    return (pi > 0 && ((pair_fused(n->phases[pi - 1]) && n->phases[pi - 1].pair_b == (int)pi) ||
-                       (fuse && n->phases[pi - 1].stack_b == (int)pi && !narrow(pi - 1)))) ||
-           ph.z_phases == 0 || (xt && fuse && pi > 0 && n->phases[pi - 1].xpair_b == (int)pi && !narrow(pi - 1));
-  };
-  std::vector<std::pair<int, int>> launches;
-  for (size_t pi = 0; pi < n->phases.size(); ++pi) {
-    if (skipped(pi)) continue;
-    const OpPhase& ph = n->phases[pi];
-    int second = -1;
-    if (pair_fused(ph)) second = n->phases[ph.pair_b].op;
-    else if (fuse && ph.stack_b >= 0 && !narrow(pi)) second = n->phases[ph.stack_b].op;
-    else if (xt && fuse && ph.xpair_b >= 0 && !narrow(pi)) second = n->phases[ph.xpair_b].op;
-    launches.push_back({(int)pi, second});
-  }
-  // Concurrent launches (PWG_CNET_OPT_STREAMS): a small plan's launches are each a few dozen
-  // workgroups and latency-bound, and a generator's parallel branches (HiFiGAN's multi-receptive-
-  // field blocks, models/hifigan.py:159-168) are independent until their sum: each launch follows
-  // the launch it depends on latest on that launch's stream when it is that stream's last, else
-  // takes the least recently used stream, and waits on an event for every dependency on another
-  // stream. Buffers are written once per run except an accumulated sum, whose writers stay in
-  // program order: same launches, same arithmetic, bit-identical to one stream.
   const int NS = 1 + PwgCnet::N_AUX;
-  const bool conc = n->streams == 2 || (n->streams == 1 && p->has_narrow);
+  CnSchedule sc;
+  {
+    const int rc = cnet_schedule(p, sc);
+    if (rc != PWG_OK) return rc;
+  }
+  const std::vector<std::pair<int, int>>& launches = sc.launches;
+  const bool conc = sc.conc;
+  const std::vector<int>& l_stream = sc.stream;
+  const std::vector<int>& l_event = sc.event;
+  const std::vector<std::vector<int>>& l_waits = sc.waits;
+  const std::vector<size_t>& order = sc.order;
   std::unique_lock<std::mutex> lock(n->mu, std::defer_lock);
   if (conc) lock.lock();  // held for the whole enqueue: the aux streams are the handle's
   std::vector<hipEvent_t>* xev_run = nullptr;
-  std::vector<int> l_stream(launches.size(), 0), l_event(launches.size(), -1);
-  std::vector<std::vector<int>> l_waits(launches.size());  // launch indices waited for (other streams)
-  bool stream_used[1 + PwgCnet::N_AUX] = {true, false, false, false};
   if (conc) {
-    // dependencies by storage, not buffer id: buffers of a plan built for one stream share slots
-    std::vector<int> mem(nb);
-    for (int b = 0; b < nb; ++b) {
-      mem[b] = b;
-      if (b > 0 && b < nb - 1)
-        for (int c = 1; c < b; ++c)
-          if (p->buf_off[c] == p->buf_off[b]) { mem[b] = mem[c]; break; }
-    }
-    std::vector<int> last_writer(nb, -1);
-    std::vector<std::vector<int>> readers(nb);
-    int tail[1 + PwgCnet::N_AUX] = {-1, -1, -1, -1}, used_at[1 + PwgCnet::N_AUX] = {-1, -1, -1, -1};
-    for (size_t L = 0; L < launches.size(); ++L) {
-      std::vector<int> deps;
-      auto op_deps = [&](int oi) {
-        const PwgCnetOp& o = n->ops[oi];
-        auto rd = [&](int b) {
-          if (b >= 0 && last_writer[mem[b]] >= 0) deps.push_back(last_writer[mem[b]]);
-        };
-        rd(o.src[0].buf);
-        if (o.kind == PWG_CNET_CONV) rd(o.src[1].buf);
-        rd(o.res);
-        if (o.accumulate) rd(o.dst);
-        if (last_writer[mem[o.dst]] >= 0) deps.push_back(last_writer[mem[o.dst]]);  // WAW
-        for (int r : readers[mem[o.dst]]) deps.push_back(r);                          // WAR
-      };
-      op_deps(n->phases[launches[L].first].op);
-      if (launches[L].second >= 0) op_deps(launches[L].second);
-      int best = -1;  // the latest dependency that is its stream's tail
-      for (int d : deps)
-        if (tail[l_stream[d]] == d && (best < 0 || d > best)) best = d;
-      int st;
-      if (best >= 0) {
-        st = l_stream[best];
-      } else if (deps.empty()) {
-        st = 0;
-      } else {
-        st = 0;
-        for (int k = 1; k < NS; ++k)
-          if (used_at[k] < used_at[st]) st = k;
-      }
-      l_stream[L] = st;
-      for (int d : deps)
-        if (l_stream[d] != st && std::find(l_waits[L].begin(), l_waits[L].end(), d) == l_waits[L].end())
-          l_waits[L].push_back(d);
-      tail[st] = (int)L;
-      used_at[st] = (int)L;
-      stream_used[st] = true;
-      auto note = [&](int oi) {
-        const PwgCnetOp& o = n->ops[oi];
-        for (int b : {o.src[0].buf, o.kind == PWG_CNET_CONV ? o.src[1].buf : -1, o.res, o.accumulate ? o.dst : -1})
-          if (b >= 0) readers[mem[b]].push_back((int)L);
-      };
-      note(n->phases[launches[L].first].op);
-      if (launches[L].second >= 0) note(launches[L].second);
-      auto wrote = [&](int oi) {
-        const int b = mem[n->ops[oi].dst];
-        last_writer[b] = (int)L;
-        readers[b].clear();
-      };
-      wrote(n->phases[launches[L].first].op);
-      if (launches[L].second >= 0) wrote(launches[L].second);
-    }
-    // events: after every launch some launch on another stream waits for, and each aux stream's tail
-    int ne = 0;
-    for (size_t L = 0; L < launches.size(); ++L)
-      for (int d : l_waits[L])
-        if (l_event[d] < 0) l_event[d] = ne++;
-    for (int k = 1; k < NS; ++k)
-      if (stream_used[k] && tail[k] >= 0 && l_event[tail[k]] < 0) l_event[tail[k]] = ne++;
-    ne += 1;  // the fork event (s_main after the flag reset)
+    const int ne = sc.n_events + 1;  // + the fork event (s_main after the flag reset)
     std::vector<hipEvent_t>& xev = p->xev_of[s_main];
     xev_run = &xev;
     while ((int)xev.size() < ne) {
@@ -4252,47 +4323,17 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
       xev.push_back(e);
     }
     for (int k = 1; k < NS; ++k)
-      if (stream_used[k] && !n->aux[k - 1] &&
+      if (sc.used[k] && !n->aux[k - 1] &&
           hipStreamCreateWithFlags(&n->aux[k - 1], hipStreamNonBlocking) != hipSuccess)
         return fail(PWG_ERR_HIP, "auxiliary stream create");
     // fork: the aux streams start after everything queued on the caller's stream so far
     hipEvent_t fork = xev[ne - 1];
     if (hipEventRecord(fork, s_main) != hipSuccess) return fail(PWG_ERR_HIP, "fork event");
     for (int k = 1; k < NS; ++k)
-      if (stream_used[k] && hipStreamWaitEvent(n->aux[k - 1], fork, 0) != hipSuccess)
+      if (sc.used[k] && hipStreamWaitEvent(n->aux[k - 1], fork, 0) != hipSuccess)
         return fail(PWG_ERR_HIP, "fork wait");
   }
   auto stream_of = [&](int k) { return k == 0 ? s_main : n->aux[k - 1]; };
-  // Enqueue order: program order on one stream; with concurrency, breadth-first over the streams
-  // (round robin, a launch once every launch it waits for is enqueued -- its event then recorded),
-  // so each branch's first launches reach the GPU before the host has enqueued a whole other branch
-  // (~5-10 us of host time per launch: in program order HiFiGAN's second and third residual chains
-  // started 60 and 140 us after the first, profiles/r04_m). Per stream the order is program order.
-  std::vector<size_t> order;
-  order.reserve(launches.size());
-  if (!conc) {
-    for (size_t L = 0; L < launches.size(); ++L) order.push_back(L);
-  } else {
-    std::vector<std::vector<size_t>> per(NS);
-    for (size_t L = 0; L < launches.size(); ++L) per[l_stream[L]].push_back(L);
-    std::vector<size_t> head(NS, 0);
-    std::vector<char> done(launches.size(), 0);
-    while (order.size() < launches.size()) {
-      bool progress = false;
-      for (int k = 0; k < NS; ++k) {
-        if (head[k] >= per[k].size()) continue;
-        const size_t L = per[k][head[k]];
-        bool ready = true;
-        for (int d : l_waits[L]) ready = ready && done[d];
-        if (!ready) continue;
-        order.push_back(L);
-        done[L] = 1;
-        ++head[k];
-        progress = true;
-      }
-      if (!progress) return fail(PWG_ERR_ASSERT, "internal: no enqueue order for the concurrent launches");
-    }
-  }
   for (size_t oi = 0; oi < order.size(); ++oi) {
     const size_t L = order[oi];
     const size_t pi = (size_t)launches[L].first;
@@ -4608,6 +4649,20 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
     hipLaunchKernelGGL(pwg_cnet_finite_kernel, dim3((unsigned)nblk), dim3(256), 0, s, (const float*)out, cnt, rflag);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hipf(e, "output range check launch");
+  }
+  return PWG_OK;
+}
+
+int pwg_cnet_plan_schedule(PwgCnetPlan* p, int cap, int* n_launches, int* phase, int* stream, int* order) {
+  if (!p || !n_launches || (cap > 0 && (!phase || !stream || !order))) return fail(PWG_ERR_INVALID, "null argument");
+  CnSchedule sc;
+  const int rc = cnet_schedule(p, sc);
+  if (rc != PWG_OK) return rc;
+  *n_launches = (int)sc.launches.size();
+  for (int L = 0; L < (int)sc.launches.size() && L < cap; ++L) {
+    phase[L] = sc.launches[L].first;
+    stream[L] = sc.stream[L];
+    order[L] = (int)sc.order[L];
   }
   return PWG_OK;
 }

@@ -205,3 +205,30 @@ def test_host_only_plans_build_and_check_their_block_lists(name, built_lib):
     assert eng._lib.pwg_cnet_set_option(eng._h, 6, 3) == _lib.PWG_ERR_INVALID
     assert eng._lib.pwg_cnet_set_option(eng._h, 7, 2) == _lib.PWG_ERR_INVALID
     assert eng.plan([64]).out_rows == 64 * hop
+
+
+def test_concurrent_schedule_host_only(built_lib):
+    """pwg_cnet_plan_schedule on a host-only plan: HiFiGAN v1 at B = 1 (narrow launches) spreads its
+    multi-receptive-field branches over the caller's stream and auxiliary ones, the enqueue order is
+    a permutation that keeps each stream's launches in program order and starts with the first
+    launch; PWG_CNET_OPT_STREAMS 0 and a large plan (no narrow launches) stay on one stream in
+    program order."""
+    from parallelwavegan_amd.cnet import CnetEngine
+
+    m = _holder("hifigan_v1")
+    eng = CnetEngine(m.program(), None, host_only=True)
+    launches, order = eng.schedule(eng.plan([64]))
+    streams = {st for _, st in launches}
+    assert len(streams) >= 3 and streams <= {0, 1, 2, 3}
+    assert sorted(order) == list(range(len(launches))) and order[0] == 0
+    pos = {L: i for i, L in enumerate(order)}
+    for k in streams:
+        ls = [L for L, (_, st) in enumerate(launches) if st == k]
+        assert [pos[L] for L in ls] == sorted(pos[L] for L in ls)
+    assert [ph for ph, _ in launches] == sorted(ph for ph, _ in launches)
+    eng.set_streams(0)
+    launches0, order0 = eng.schedule(eng.plan([64]))
+    assert {st for _, st in launches0} == {0} and order0 == list(range(len(launches0)))
+    eng.set_streams(1)
+    big, order_big = eng.schedule(eng.plan([4000] * 8))
+    assert {st for _, st in big} == {0} and order_big == list(range(len(big)))
