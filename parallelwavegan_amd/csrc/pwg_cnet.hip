@@ -1007,8 +1007,14 @@ struct CnXdmaArgs {
   int rate[2], rate_dst, rate_res;  // rows per frame of the sources', destination and residual buffers
 };
 constexpr int XDMA_CHUNKS_MAX = 256;  // K = 1 mode: chunks per op (the table sits in LDS)
-constexpr int XDMA_K1_G = 4;          // K = 1 mode: chunks per step
-constexpr int XDMA_RING_CAP = 4;      // ring slots at most (see XdmaShape::ring)
+#ifndef PWG_XDMA_K1_G
+#define PWG_XDMA_K1_G 4
+#endif
+#ifndef PWG_XDMA_RING_CAP
+#define PWG_XDMA_RING_CAP 4
+#endif
+constexpr int XDMA_K1_G = PWG_XDMA_K1_G;          // K = 1 mode: chunks per step
+constexpr int XDMA_RING_CAP = PWG_XDMA_RING_CAP;  // ring slots at most (see XdmaShape::ring)
 #ifdef PWG_XDMA_PROBE
 constexpr int XDMA_PROBE_SLOTS = 128, XDMA_PROBE_N = 96;
 __device__ unsigned long long g_xdma_probe[XDMA_PROBE_SLOTS][XDMA_PROBE_N];
@@ -1035,7 +1041,9 @@ struct XdmaShape {
   }
   // at most 4 slots: the prologue issues P - 1 steps before the first MFMA, and deeper rings
   // measured slower at B = 1 (MB-MelGAN v2 T' = 64: 16 slots 0.507 ms, 8: 0.508, 4: 0.478;
-  // HiFiGAN v1 0.973 / 0.989 / 0.954; profiles/r04_h)
+  // HiFiGAN v1 0.973 / 0.989 / 0.954; profiles/r04_h); 3 slots measured the same as 4 and 2 slots
+  // slower (MB-MelGAN 0.442 / 0.441 / 0.491 ms), K = 1 with 2 chunks per step no faster
+  // (profiles/r04_p; -DPWG_XDMA_RING_CAP / -DPWG_XDMA_K1_G build those variants)
   static constexpr int P = ring(XDMA_RING_CAP);
   static constexpr int LDS = P * SLOT + 2 * CBUF + CHT;
   static_assert(LDS <= 160 * 1024, "DMA-ring shape");
