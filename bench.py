@@ -164,10 +164,15 @@ def per_rank_seconds(local_s, world, dev):
     return [float(x.item()) for x in ts]
 
 
+PMC_PASSES = (("FETCH_SIZE",), ("WRITE_SIZE",), ("GRBM_GUI_ACTIVE", "SQ_VALU_MFMA_BUSY_CYCLES"))
+
+
 def _pmc_passes(args):
-    """Two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE: separate passes on gfx950) over a child
-    process (`bench.py --pmc-child`, never an exec) that runs two forwards of this workload.
-    Returns ({counter: {dispatch_id: (kernel_name, value)}}, None) or (None, failure note)."""
+    """rocprofv3 --pmc passes, one counter group each (FETCH_SIZE and WRITE_SIZE need separate
+    passes on gfx950; the third reads the shader clock and the matrix pipes' busy cycles) over a
+    child process (`bench.py --pmc-child`, never an exec) that runs two forwards of this workload.
+    Returns ({counter: {dispatch_id: (kernel_name, value, duration_ns)}}, None) or (None, failure
+    note); a failed clock pass leaves its counters out."""
     import csv
     import glob
     import shutil
@@ -177,9 +182,10 @@ def _pmc_passes(args):
     if prof is None:
         return None, "rocprofv3 not found"
     per = {}
-    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+    for group in PMC_PASSES:
+        optional = "FETCH_SIZE" not in group and "WRITE_SIZE" not in group
         with tempfile.TemporaryDirectory(prefix="pwg_pmc_", dir="/tmp") as d:
-            cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "pmc", "--", sys.executable,
+            cmd = [prof, "--pmc", *group, "--output-format", "csv", "-d", d, "-o", "pmc", "--", sys.executable,
                    os.path.abspath(__file__), "--pmc-child", "--config", args.config, "--utts", str(args.utts)]
             if args.layer_kernel:
                 cmd += ["--layer-kernel", args.layer_kernel]
@@ -189,56 +195,96 @@ def _pmc_passes(args):
             try:
                 r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=150)
             except subprocess.TimeoutExpired:
-                return None, f"rocprofv3 --pmc {ctr} pass timed out"
+                if optional:
+                    continue
+                return None, f"rocprofv3 --pmc {' '.join(group)} pass timed out"
             if r.returncode != 0:
-                return None, f"rocprofv3 --pmc {ctr} pass failed (rc {r.returncode})"
-            vals = {}
+                if optional:
+                    continue
+                return None, f"rocprofv3 --pmc {' '.join(group)} pass failed (rc {r.returncode})"
+            vals = {c: {} for c in group}
             for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
                 for row in csv.DictReader(open(path)):
-                    if row.get("Counter_Name") != ctr:
+                    ctr = row.get("Counter_Name")
+                    if ctr not in vals:
                         continue
                     disp = int(row.get("Dispatch_Id") or 0)
-                    name, v = vals.get(disp, (row.get("Kernel_Name", ""), 0.0))
-                    vals[disp] = (name, v + float(row.get("Counter_Value") or 0))
-            if not vals:
-                return None, f"rocprofv3 --pmc {ctr}: no dispatches recorded"
-            per[ctr] = vals
+                    try:
+                        dur = int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
+                    except (KeyError, TypeError, ValueError):
+                        dur = 0
+                    name, v, _ = vals[ctr].get(disp, (row.get("Kernel_Name", ""), 0.0, dur))
+                    vals[ctr][disp] = (name, v + float(row.get("Counter_Value") or 0), dur)
+            if not all(vals.values()):
+                if optional:
+                    continue
+                return None, f"rocprofv3 --pmc {' '.join(group)}: no dispatches recorded"
+            per.update(vals)
     return per, None
+
+
+def _clock_busy(per, pick):
+    """Shader clock (GHz: GRBM_GUI_ACTIVE / 8 XCDs / dispatch time, MI355X_MICROARCH.md 'DVFS
+    give-back') and matrix-pipe busy fraction (SQ_VALU_MFMA_BUSY_CYCLES / (cycles x 256 CUs x 4
+    SIMDs)) over the dispatches `pick(name)` selects, time-weighted; None without the clock pass."""
+    g, m = per.get("GRBM_GUI_ACTIVE"), per.get("SQ_VALU_MFMA_BUSY_CYCLES")
+    if not g or not m:
+        return None
+    cyc = busy = ns = 0.0
+    n = 0
+    for disp, (name, v, dur) in g.items():
+        if not pick(name) or dur <= 0 or disp not in m:
+            continue
+        cyc += v / 8.0
+        busy += m[disp][1]
+        ns += dur
+        n += 1
+    if n == 0 or ns <= 0:
+        return None
+    return {"shader_clock_ghz": round(cyc / ns, 3), "mfma_busy": round(busy / (cyc * 256 * 4), 4),
+            "dispatches": n,
+            "source": "rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES pass in this run (dispatch "
+                      "times of that pass; clock reads high on dispatches under ~0.3 ms)"}
 
 
 def measure_layer_traffic(args):
     """HBM bytes per middle residual-layer launch of THIS workload, measured in this run (two
     --pmc passes over a child running the same plan, _pmc_passes). FETCH_SIZE is doubled
     (MI355X_MICROARCH.md: gfx950 reports half the bytes of wide coalesced reads), KB -> bytes.
-    Runs before this process touches the GPU. Returns (bytes or None, source note)."""
+    Runs before this process touches the GPU. Returns (bytes or None, source note, clock/busy)."""
     per, err = _pmc_passes(args)
     if per is None:
-        return None, err
+        return None, err, None
     kernel = f"pwg_layer_{args.layer_kernel or 'split16'}_kernel<false"
     mean = {}
-    for ctr, vals in per.items():
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        vals = per[ctr]
         # middle layers: not the last (<true...>) and not layer 0 with the fused first_conv
-        v = [x for name, x in vals.values() if kernel in name and ", true>" not in name]
+        v = [x for name, x, _ in vals.values() if kernel in name and ", true>" not in name]
         if not v:
-            return None, f"rocprofv3 --pmc {ctr}: no {kernel}...> dispatches found"
+            return None, f"rocprofv3 --pmc {ctr}: no {kernel}...> dispatches found", None
         mean[ctr] = (sum(v) / len(v), len(v))
     fetch = mean["FETCH_SIZE"][0] * 1024 * 2
     write = mean["WRITE_SIZE"][0] * 1024
     note = (f"measured in this run: rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) and WRITE_SIZE passes over "
             f"two forwards of this workload in a child process, mean of {mean['FETCH_SIZE'][1]} middle-layer launches; "
             f"read {fetch / 1e9:.3f} GB + write {write / 1e9:.3f} GB")
-    return fetch + write, note
+    clk = _clock_busy(per, lambda name: kernel in name and ", true>" not in name)
+    return fetch + write, note, clk
 
 
 def measure_program_traffic(args):
     """Vocoder configs: HBM bytes of ONE whole forward (every launch of the conv program), measured
     as measure_layer_traffic does, from the second of the child's two forwards (the later half of
-    its dispatches). Returns (bytes or None, source note, {kernel: bytes} of the top kernels)."""
+    its dispatches). Returns (bytes or None, source note, {kernel: bytes} of the top kernels,
+    clock/busy of the whole program and of its top kernels)."""
     per, err = _pmc_passes(args)
     if per is None:
-        return None, err, None
+        return None, err, None, None
     tot, by_kernel, n_fwd = {}, {}, 0
-    for ctr, vals in per.items():
+    short = lambda name: name.replace("(anonymous namespace)::", "").replace("pwg::", "").split("(")[0].replace("void ", "")  # noqa: E731
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        vals = per[ctr]
         # the conv program's own launches only (module setup runs torch / copy kernels before them)
         ids = sorted(i for i in vals if "pwg_cnet_" in vals[i][0])
         second = ids[len(ids) // 2:]
@@ -246,14 +292,27 @@ def measure_program_traffic(args):
         scale = 2048.0 if ctr == "FETCH_SIZE" else 1024.0
         tot[ctr] = sum(vals[i][1] for i in second) * scale
         for i in second:
-            name = vals[i][0].replace("(anonymous namespace)::", "").replace("pwg::", "")
-            name = name.split("(")[0].replace("void ", "")
+            name = short(vals[i][0])
             by_kernel[name] = by_kernel.get(name, 0.0) + vals[i][1] * scale
     note = (f"measured in this run: rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) and WRITE_SIZE passes over "
             f"two forwards in a child process, the second forward's {n_fwd} conv-program launches; read "
             f"{tot['FETCH_SIZE'] / 1e9:.3f} GB + write {tot['WRITE_SIZE'] / 1e9:.3f} GB per forward")
     top = dict(sorted(((k, round(v / 1e9, 4)) for k, v in by_kernel.items()), key=lambda kv: -kv[1])[:6])
-    return tot["FETCH_SIZE"] + tot["WRITE_SIZE"], note, top
+    clk = _clock_busy(per, lambda name: "pwg_cnet_" in name and "desc_kernel" not in name)
+    if clk is not None:
+        # the kernels that take the most time in the clock pass
+        dur = {}
+        for name, _, d in per["GRBM_GUI_ACTIVE"].values():
+            if "pwg_cnet_" in name:
+                dur[short(name)] = dur.get(short(name), 0) + d
+        slow = sorted(dur, key=lambda k: -dur[k])[:5]
+        clk["per_kernel"] = {}
+        for k in slow:
+            v = _clock_busy(per, lambda name, k=k: short(name) == k) or {}
+            v.pop("source", None)
+            v["ms_per_forward"] = round(dur[k] / 2e6, 3)
+            clk["per_kernel"][k] = v
+    return tot["FETCH_SIZE"] + tot["WRITE_SIZE"], note, top, clk
 
 
 def pmc_child(args):
@@ -400,13 +459,47 @@ def program_bytes_per_frame(P):
     return b
 
 
+def decode_loop_row(call, lengths, dev, hop, noise=False):
+    """The reference's decode loop (bin/decode.py:236-268): one B = 1 call per utterance, each at its
+    own length, every call the first at that length (plan build, workspace growth and graph policy
+    included). Mean / median wall ms per call (synchronised), over all utterances and over those of
+    at most 512 frames."""
+    ms = []
+    for i, f in enumerate(lengths):
+        args = [torch.from_numpy(synthetic.make_mel(int(f), 80, seed=500 + i)).to(dev)]
+        if noise:  # explicit x (PWG), drawn outside the timed call
+            args.append(torch.from_numpy(synthetic.make_noise(int(f) * hop, seed=700 + i)).to(dev))
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        call(*args)
+        torch.cuda.synchronize(dev)
+        ms.append((time.perf_counter() - t0) * 1e3)
+    ms = np.array(ms)
+    short = ms[np.asarray(lengths) <= 512]
+    samples = int(np.sum(lengths)) * hop
+    return {"pattern": "decode loop: B=1, one call per utterance, every length new",
+            "utterances": len(lengths), "distinct_lengths": len(set(int(f) for f in lengths)),
+            "frames": f"RandomState(3) LibriTTS list, {int(np.min(lengths))}-{int(np.max(lengths))}",
+            "mean_ms_per_call": round(float(ms.mean()), 3), "median_ms_per_call": round(float(np.median(ms)), 3),
+            "max_ms_per_call": round(float(ms.max()), 3),
+            "short_utterances": int(short.size),
+            "mean_ms_per_call_le512_frames": round(float(short.mean()), 3) if short.size else None,
+            "samples_per_s": round(samples / (ms.sum() * 1e-3), 1)}
+
+
 def vocoder_latency_rows(m, dev, reps=10):
     """the drop-in's inference() (B = 1, the reference decode loop) and
     inference_batch (B = 16 equal-length) at T' in {64, 512, 2048}: median wall ms per call with
-    device-resident mels (synchronised), and the kernels' own ms."""
+    device-resident mels (synchronised), and the device span of one call's launches (first start
+    to last end over every stream, pwg_cnet_timing_span; kernel_sum_ms adds the per-launch times,
+    concurrent launches counted each). First: the decode loop over 32 distinct lengths."""
     rows = []
     eng = m.engine()
     hop = eng.hop
+    lengths = synthetic.libritts_lengths(32, seed=3)
+    with torch.no_grad():
+        m.inference(torch.from_numpy(synthetic.make_mel(7, 80, seed=1)).to(dev))  # engine built, weights packed
+        loop = decode_loop_row(lambda mel: m.inference(mel), lengths, dev, hop)
 
     def timed(fn):
         torch.cuda.synchronize(dev)
@@ -424,17 +517,59 @@ def vocoder_latency_rows(m, dev, reps=10):
                 for _ in range(2):
                     call()
                 ms = sorted(timed(call) for _ in range(reps))
-                eng.set_timing(True)
+                eng.set_timing(2)  # span: one event pair around the run
                 eng.collect_timing()
+                call()
+                torch.cuda.synchronize(dev)
+                span = eng.timing_span()
+                eng.collect_timing()
+                eng.set_timing(1)  # per-launch events
                 call()
                 torch.cuda.synchronize(dev)
                 eng.set_timing(False)
                 kern = sum(t for _, t, _ in eng.collect_timing())
                 med = ms[len(ms) // 2]
                 rows.append({"frames": F, "batch": B, "samples_per_call": F * hop * B, "first_call_ms": round(first, 3),
-                             "median_ms": round(med, 3), "kernel_ms": round(kern, 3),
+                             "median_ms": round(med, 3), "kernel_span_ms": round(span, 3),
+                             "kernel_sum_ms": round(kern, 3), "host_overhead_ms": round(med - span, 3),
                              "samples_per_s": round(F * hop * B / (med * 1e-3), 1)})
-    return {"model": f"{type(m).__name__}.inference / inference_batch (drop-in)", "rows": rows}
+    return {"model": f"{type(m).__name__}.inference / inference_batch (drop-in)", "decode_loop": loop,
+            "rows": rows,
+            "note": "kernel_span_ms: device span of one eager call (HIP events around the whole run only; graph "
+                    "replay is off while timing); median_ms: wall time of the default path (graph replay for "
+                    "repeated small HiFiGAN plans); kernel_sum_ms: per-launch event times summed (concurrent "
+                    "launches each counted)"}
+
+
+def vocoder_exact_fp32_leg(eng, plan, out_mel, out, flop_step, samples, steps):
+    """The precision-matched vocoder number: the same batch on the exact
+    fp32 MFMA kernels (PWG_CNET_OPT_SPLIT_F16 0, v_mfma_f32_32x32x2_f32, no fp16 pairs), one
+    warm-up and `steps` timed forwards; roofline on the fp32 MFMA peak with the program's
+    algorithmic FLOPs (every product executed once in this mode)."""
+    dev = eng.device
+    eng.set_split_f16(False)
+    try:
+        eng.run(plan, out_mel, out, check=False)
+        torch.cuda.synchronize(dev)
+        eng.set_timing(True)
+        eng.collect_timing()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            eng.run(plan, out_mel, out, check=False)
+        torch.cuda.synchronize(dev)
+        wall = time.perf_counter() - t0
+        eng.set_timing(False)
+        kern_s = sum(ms for _, ms, _ in eng.collect_timing()) / 1e3 / steps
+    finally:
+        eng.set_split_f16(True)
+    if not torch.isfinite(out).all():
+        raise RuntimeError("non-finite exact-fp32 vocoder output")
+    tf = flop_step / kern_s / 1e12
+    return {"kernel": "conv program on the exact-fp32 MFMA kernels (PWG_CNET_OPT_SPLIT_F16 0)", "dtype": "f32",
+            "value": round(samples * steps / wall, 1), "unit": "audio samples/s", "steps": steps,
+            "ms_per_step": round(wall / steps * 1e3, 3), "kernel_ms_per_step": round(kern_s * 1e3, 3),
+            "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(tf / FP32_PEAK_TFLOPS, 4), "flop_per_step": int(flop_step)}}
 
 
 def vocoder_setup(args, dev):
@@ -462,7 +597,7 @@ def vocoder_setup(args, dev):
     return m, eng, cls_name, params, (sd, syn)
 
 
-def bench_vocoder(args, rank, world, dev, live_traffic=(None, "off", None), embedded=False):
+def bench_vocoder(args, rank, world, dev, live_traffic=(None, "off", None, None), embedded=False):
     """MelGAN-family generator inference (BASELINE configs[2] multi_band_melgan.v2 and [3]
     hifigan.v1) on the conv-network executor: same ragged-batch workload shape
     as the PWG bench, weak scaling, utterance sharding, RCCL weight broadcast.
@@ -542,6 +677,9 @@ def bench_vocoder(args, rank, world, dev, live_traffic=(None, "off", None), embe
         cpu = dict({"value": round(done / tt, 1), "unit": "audio samples/s", "cores": threads, "kind": "port",
                     "sample": f"{args.config}: {used} utterances ({done} samples, first of the bench batch), B=1, "
                               f"torch-CPU restatement of the reference op sequence, {threads} threads"}, **info)
+    exact = None
+    if world == 1 and not args.cnet_fp32 and not getattr(args, "no_exact", False):
+        exact = vocoder_exact_fp32_leg(eng, plan, mel, out, fl_frame * frames, samples, max(2, min(args.steps, 3)))
     lat = None
     if not args.no_latency and world == 1:
         lat = vocoder_latency_rows(m, dev)
@@ -576,6 +714,7 @@ def bench_vocoder(args, rank, world, dev, live_traffic=(None, "off", None), embe
                       "traffic_source": live_traffic[1], "traffic_top_kernels_GB": live_traffic[2],
                       "hbm_GBs_measured": voc_bytes and round(voc_bytes / (kern_ms * 1e-3) / 1e9, 1),
                       "hbm_frac_measured": voc_bytes and round(voc_bytes / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                      "clock_pmc": live_traffic[3],
                       "flop_per_sample": round(fl_frame / hop, 1),
                       "algorithmic_bytes_per_sample": round(by_frame / hop, 1)} if args.cnet_fp32 else
                      # split-f16: every reference product runs as three f16 MFMA products
@@ -586,10 +725,12 @@ def bench_vocoder(args, rank, world, dev, live_traffic=(None, "off", None), embe
                       "hbm_GBs_measured": voc_bytes and round(voc_bytes / (kern_ms * 1e-3) / 1e9, 1),
                       "hbm_frac_measured": voc_bytes and round(voc_bytes / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                       "reference_tflops": round(achieved, 3),
+                      "clock_pmc": live_traffic[3],
                       "flop_per_sample": round(fl_frame / hop, 1),
                       "executed_f16_flop_per_sample": round(3 * fl_frame / hop, 1),
                       "algorithmic_bytes_per_sample": round(by_frame / hop, 1)}),
         "cpu_baseline": cpu,
+        "exact_fp32": exact,
         "latency": lat,
     }
     if embedded:
@@ -641,14 +782,24 @@ def exact_fp32_leg(eng, plan, mel, noise, out, params, steps):
     layer_ms, layer_n = timing["residual_layer"]
     avg_s = layer_ms / 1e3 / max(layer_n, 1)
     flop_launch = layer_flops_per_sample(params) * plan.total_samples
-    tf = flop_launch / avg_s / 1e12
+    # executed: the dilated conv and the skip / out 1x1s per sample; the aux 1x1 runs once per frame
+    # in pwg_aux_proj_kernel (its rows are interpolated in the layer), so the layer executes
+    # 2 (K R G + G/2 (S + R)) FLOP per sample (0.762 of the reference's per LibriTTS v1 layer)
+    R, G, S, K = (params[k] for k in ("residual_channels", "gate_channels", "skip_channels", "kernel_size"))
+    exec_launch = 2 * (K * R * G + (G // 2) * (S + R)) * plan.total_samples
+    tf = exec_launch / avg_s / 1e12
+    tf_ref = flop_launch / avg_s / 1e12
     return {"kernel": "pwg_layer_persistent_kernel (exact fp32, v_mfma_f32_32x32x2_f32)", "dtype": "f32",
             "value": round(plan.total_samples * steps / wall, 1), "unit": "audio samples/s",
             "steps": steps, "ms_per_step": round(wall / steps * 1e3, 3),
             "roofline": {"bound": "mfma", "achieved": round(tf, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(tf / FP32_PEAK_TFLOPS, 4), "avg_launch_ms": round(avg_s * 1e3, 4),
-                         "launches_timed": layer_n, "reference_flop_per_launch": int(flop_launch),
-                         "note": "reference-formulation FLOPs (the aux 1x1 runs at frame rate, so fewer are executed)"}}
+                         "launches_timed": layer_n, "executed_flop_per_launch": int(exec_launch),
+                         "reference_flop_per_launch": int(flop_launch),
+                         "reference_formulation_tflops": round(tf_ref, 2),
+                         "note": "frac on executed FLOPs (dilated conv + skip/out 1x1s per sample; the aux 1x1 "
+                                 "runs at frame rate); reference_formulation_tflops counts the per-sample aux 1x1 "
+                                 "the reference executes, and can exceed the fp32 peak"}}
 
 
 def latency_rows(dev, reps=20):
@@ -657,7 +808,8 @@ def latency_rows(dev, reps=20):
     B=1 and B=16 equal-length (inference_batch). Per call: wall ms of the first call at a new
     length (plan build included), median / min wall ms of repeated calls with device-resident
     inputs (synchronised, range check included), host-to-host ms (numpy mel/noise in, .cpu() out,
-    like decode.py), and the kernels' own ms (HIP events, summed over the call's launches)."""
+    like decode.py), and the device span of the call's launches (first start to last end, HIP
+    events). First: the decode loop over 32 distinct lengths (every call at a new length)."""
     from parallelwavegan_amd import ParallelWaveGANGenerator
 
     params = configs.generator_params("ljspeech_v1")
@@ -667,6 +819,11 @@ def latency_rows(dev, reps=20):
     m = m.eval().to(dev)
     H = m.upsample_factor
     rows = []
+    lengths = synthetic.libritts_lengths(32, seed=3)
+    with torch.no_grad():
+        m.inference(torch.from_numpy(synthetic.make_mel(7, 80, seed=1)).to(dev),
+                    torch.from_numpy(synthetic.make_noise(7 * H, seed=1)).to(dev))  # engine built, weights packed
+        loop = decode_loop_row(lambda mel, x: m.inference(mel, x), lengths, dev, H, noise=True)
 
     def timed(fn):
         torch.cuda.synchronize(dev)
@@ -703,21 +860,22 @@ def latency_rows(dev, reps=20):
                         g(mels[0], noises[0])
                     graph_ms = sorted(timed(lambda: g(mels[0], noises[0])) for _ in range(reps))
                     del g
-                eng.set_timing(True)
+                eng.set_timing(2)  # span: one event pair around the run
                 eng.collect_timing()
                 call()
                 torch.cuda.synchronize(dev)
                 eng.set_timing(False)
-                kern = sum(ms for ms, _ in eng.collect_timing().values())
+                kern = eng.timing_span()
+                eng.collect_timing()
                 med = dev_ms[len(dev_ms) // 2]
                 rows.append({"frames": F, "batch": B, "samples_per_call": F * H * B,
                              "first_call_ms": round(first, 3), "median_ms": round(med, 3),
                              "min_ms": round(dev_ms[0], 3), "host_to_host_median_ms": round(host_ms[len(host_ms) // 2], 3),
-                             "kernel_ms": round(kern, 3), "overhead_ms": round(med - kern, 3),
+                             "kernel_span_ms": round(kern, 3), "host_overhead_ms": round(med - kern, 3),
                              "graph_replay_median_ms": graph_ms and round(graph_ms[len(graph_ms) // 2], 3),
                              "samples_per_s": round(F * H * B / (med * 1e-3), 1)})
     return {"model": "ljspeech_v1 ParallelWaveGANGenerator.inference / inference_batch (drop-in)",
-            "rows": rows}
+            "decode_loop": loop, "rows": rows}
 
 
 def main():
@@ -771,13 +929,13 @@ def main():
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     # measured HBM traffic of the dominant kernel, before this process touches the GPU
-    live_traffic = (None, "off")
+    live_traffic = (None, "off", None)
     single = args.pmc == "auto" and int(os.environ.get("WORLD_SIZE", "1")) == 1
     if (single and args.config not in VOCODERS
             and not args.strong and args.sub_plans == 1 and args.layer_kernel in (None, "split16")
             and not args.no_fuse_first and not args.waves_per_wg and not args.wg_per_cu):
         live_traffic = measure_layer_traffic(args)
-    voc_traffic = (None, "off", None)
+    voc_traffic = (None, "off", None, None)
     if single and args.config in VOCODERS:
         voc_traffic = measure_program_traffic(args)
     embed = (int(os.environ.get("WORLD_SIZE", "1")) == 1 and args.config not in VOCODERS and not args.strong
@@ -786,7 +944,7 @@ def main():
     if embed:
         for vc in EMBED_VOCODERS:
             embed_traffic[vc] = (measure_program_traffic(with_config(args, vc)) if args.pmc == "auto"
-                                 else (None, "off", None))
+                                 else (None, "off", None, None))
     rank, world, dev = dist_setup(args.gpus)
     _lib.build()
     if args.config in VOCODERS:
@@ -935,7 +1093,7 @@ def main():
     traffic = mfma_insts = None
     traffic_source = None
     if live_traffic[0] is not None:
-        traffic, traffic_source = live_traffic
+        traffic, traffic_source = live_traffic[:2]
     elif os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
@@ -977,6 +1135,9 @@ def main():
             "reference_flop_per_launch": int(flops_launch),
             "reference_tflops": round(achieved_tflops, 1),
             "hbm_GBs_measured": traffic and round(traffic / layer_avg_s / 1e9, 1),
+            # shader clock and matrix-pipe busy of the middle-layer launches (in-run PMC pass): the
+            # layer runs power-limited well under the 2.4 GHz max clock
+            "clock_pmc": live_traffic[2],
         }
     else:
         roofline = {

@@ -183,7 +183,11 @@ PWG_API int pwg_run(PwgPlan* p, const float* packed, const float* mel, const flo
  * While PWG_OPT_SYNC is on (the default for small plans) a caller that enqueues runs without
  * checking each one must still call this before trusting any of their outputs: the sticky word
  * makes one call per batch of runs enough to learn that SOME run needs redoing (it does not say
- * which; redo them all, or check after every run as the drop-in does). */
+ * which; redo them all, or check after every run as the drop-in does). The sticky word belongs to
+ * the handle, not to a stream or workspace: the once-per-batch guarantee holds for a handle driven
+ * from ONE stream. A handle serving several streams must check after every run (each check then
+ * reads its own run's word exactly, and may also report -- and clear -- another stream's unchecked
+ * failure, which only costs a spurious rerun). */
 PWG_API int pwg_run_status(PwgPlan* p, const void* workspace, void* stream);
 
 /* HIP graph of one pwg_run with fixed buffers (no reference counterpart: the replay path for
@@ -253,8 +257,15 @@ PWG_API int pwg_get_option(const PwgHandle* h, int option, long long* value);
 /* Per-kernel HIP-event timing of pwg_run (off by default). collect synchronises
  * on the recorded events, adds ms and launch counts per PWG_KERNEL_* bucket into
  * the caller's arrays and clears the records. */
+/* Timing: 0 off, 1 HIP events around every launch (per-bucket / per-op sums), 2 one event pair
+ * around each whole run on the caller's stream (its device span only; no events between launches,
+ * so the run's launches are timed undisturbed). */
 PWG_API int pwg_set_timing(PwgHandle* h, int enable);
 PWG_API int pwg_timing_collect(PwgHandle* h, double* ms, long long* launches);
+/* Device span of the timed launches recorded since the last pwg_timing_collect: the first launch's
+ * start to the last launch's end, milliseconds (idle gaps between launches included, unlike the
+ * per-bucket sums). Call before pwg_timing_collect, which releases the records. */
+PWG_API int pwg_timing_span(PwgHandle* h, double* span_ms);
 
 /* ---- Multi-GPU: the one collective of the design -----------------
  * Utterances shard across GPUs with no data-path exchange; the only collective is a broadcast of

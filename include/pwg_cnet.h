@@ -91,8 +91,17 @@ PWG_API void pwg_cnet_destroy(PwgCnet* n);
 PWG_API long long pwg_cnet_packed_weight_count(const PwgCnet* n);
 /* Host -> host packing of the reference-order weight vector into the kernel image. */
 PWG_API int pwg_cnet_pack_weights(const PwgCnet* n, const float* ref_host, float* packed_host);
+/* Plans are host objects: creating one allocates and copies nothing on the GPU (the handle's
+ * per-program chunk tables aside, uploaded by its first plan). The plan's block lists live in the
+ * caller's workspace and are written by a descriptor kernel at the start of every pwg_cnet_run, so a
+ * new utterance length per call (the reference's decode loop, bin/decode.py:236-268) costs host
+ * work only, and a captured forward regenerates them on every replay. */
 PWG_API int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCnetPlan** out);
 PWG_API void pwg_cnet_plan_destroy(PwgCnetPlan* p);
+/* The device-list image pwg_cnet_run writes into the workspace: its byte offset there, its length
+ * in ints, and (cap > 0) its first `cap` ints as the host built and checked them. For tests. */
+PWG_API int pwg_cnet_plan_image(const PwgCnetPlan* p, long long* offset_bytes, long long* n_ints, int* out,
+                                long long cap);
 PWG_API long long pwg_cnet_plan_rows(const PwgCnetPlan* p, int buf); /* sum_u frames[u]*rate[buf] */
 PWG_API long long pwg_cnet_plan_workspace_bytes(const PwgCnetPlan* p);
 /* mel: buffer 0 contents (device, rows x channels[0], frames-major = time-major);
@@ -161,9 +170,17 @@ enum { PWG_CNET_OPT_SPLIT_F16 = 0, PWG_CNET_OPT_FUSE_PAIRS = 1, PWG_CNET_OPT_PAI
        PWG_CNET_OPT_XT_DMA = 4, PWG_CNET_OPT_XCD_ORDER = 5, PWG_CNET_OPT_NARROW = 6, PWG_CNET_OPT_NARROW_DMA = 7,
        PWG_CNET_OPT_STREAMS = 8 };
 PWG_API int pwg_cnet_set_option(PwgCnet* n, int option, long long value);
+/* Timing: 0 off, 1 HIP events around every launch (per-bucket / per-op sums), 2 one event pair
+ * around each whole run on the caller's stream (its device span only; no events between launches,
+ * so the run's launches are timed undisturbed). */
 PWG_API int pwg_cnet_set_timing(PwgCnet* n, int enable);
 /* Adds per-op milliseconds and launch counts (arrays of n_ops) and clears the records. */
 PWG_API int pwg_cnet_timing_collect(PwgCnet* n, double* ms, long long* launches);
+/* Device span of the timed launches recorded since the last collect: the first launch's start to
+ * the last launch's end over every stream (PWG_CNET_OPT_STREAMS), milliseconds. The per-op sums of
+ * pwg_cnet_timing_collect add up concurrent launches; this is wall time on the device. Call
+ * before pwg_cnet_timing_collect. */
+PWG_API int pwg_cnet_timing_span(PwgCnet* n, double* span_ms);
 
 #ifdef __cplusplus
 }

@@ -73,6 +73,7 @@ EXPORTED_SYMBOLS = (
     "pwg_get_option",
     "pwg_set_timing",
     "pwg_timing_collect",
+    "pwg_timing_span",
     "pwg_rccl_unique_id",
     "pwg_rccl_comm_create",
     "pwg_rccl_comm_destroy",
@@ -85,6 +86,7 @@ EXPORTED_SYMBOLS = (
     "pwg_cnet_pack_weights",
     "pwg_cnet_plan_create",
     "pwg_cnet_plan_destroy",
+    "pwg_cnet_plan_image",
     "pwg_cnet_plan_rows",
     "pwg_cnet_plan_workspace_bytes",
     "pwg_cnet_run",
@@ -93,6 +95,7 @@ EXPORTED_SYMBOLS = (
     "pwg_cnet_set_option",
     "pwg_cnet_set_timing",
     "pwg_cnet_timing_collect",
+    "pwg_cnet_timing_span",
 )
 
 PWG_OPT_LAYER_KERNEL = 0
@@ -312,6 +315,7 @@ def load():
         lib.pwg_set_timing.argtypes = [vp, ctypes.c_int]
         lib.pwg_set_option.argtypes = [vp, ctypes.c_int, ctypes.c_longlong]
         lib.pwg_timing_collect.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ll)]
+        lib.pwg_timing_span.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
         if lib.pwg_abi_version() != 2:
             raise RuntimeError("libpwg_hip ABI version mismatch")
         _lib = lib

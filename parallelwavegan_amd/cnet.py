@@ -79,6 +79,7 @@ def lib():
         L.pwg_cnet_plan_create.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ll), ctypes.POINTER(vp)]
         L.pwg_cnet_plan_destroy.argtypes = [vp]
         L.pwg_cnet_plan_destroy.restype = None
+        L.pwg_cnet_plan_image.argtypes = [vp, ctypes.POINTER(ll), ctypes.POINTER(ll), vp, ll]
         L.pwg_cnet_plan_rows.argtypes = [vp, ctypes.c_int]
         L.pwg_cnet_plan_rows.restype = ll
         L.pwg_cnet_plan_workspace_bytes.argtypes = [vp]
@@ -90,6 +91,7 @@ def lib():
         L.pwg_cnet_set_timing.argtypes = [vp, ctypes.c_int]
         L.pwg_cnet_set_option.argtypes = [vp, ctypes.c_int, ctypes.c_longlong]
         L.pwg_cnet_timing_collect.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ll)]
+        L.pwg_cnet_timing_span.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
         if L.pwg_cnet_abi_version() != 1:
             raise RuntimeError("libpwg_hip cnet ABI version mismatch")
         _bound = True
@@ -214,6 +216,17 @@ class CnetPlan:
         nb = len(eng.program.channels)
         self.out_rows = eng._lib.pwg_cnet_plan_rows(p, nb - 1)
         self.workspace_bytes = eng._lib.pwg_cnet_plan_workspace_bytes(p)
+        self.runs = 0  # forwards run with this plan (CnetEngine captures a graph from the second on)
+
+    def image(self):
+        """pwg_cnet_plan_image: (byte offset in the workspace, int32 array) of the device lists
+        every run writes there, as the host built and checked them."""
+        off, n = ctypes.c_longlong(), ctypes.c_longlong()
+        _lib.check(self.eng._lib.pwg_cnet_plan_image(self._p, ctypes.byref(off), ctypes.byref(n), None, 0))
+        img = np.zeros(n.value, np.int32)
+        _lib.check(self.eng._lib.pwg_cnet_plan_image(self._p, ctypes.byref(off), ctypes.byref(n),
+                                                     img.ctypes.data, n.value))
+        return off.value, img
 
     def __del__(self):
         p = getattr(self, "_p", None)
@@ -344,6 +357,7 @@ class CnetEngine:
             stream = torch.cuda.current_stream(self.device)
         ws = None
         key = (id(plan), stream.cuda_stream)
+        plan.runs += 1
         if self._graph_ok(plan, mean, stream):
             ws = self._replay(plan, mel, out, stream)
             self._last_ws[key] = ws  # run_status reads the captured forward's own workspace
@@ -373,7 +387,12 @@ class CnetEngine:
     # (profiles/r04_m). Small plans therefore run as a hipGraph captured once per (plan, caller
     # stream, weights, options) and replayed: input copied into the graph's buffer, replay, output
     # copied out. Same kernels, same arguments: bit-identical to the eager forward.
+    # A graph is captured only for a plan that runs again (GRAPH_AFTER-th run): the reference's
+    # decode loop gives nearly every utterance its own length (bin/decode.py:236-268), and a capture
+    # (eager warm-up, capture, instantiation) costs ~10 ms, far more than the eager forward it replaces.
     GRAPH_MAX_FRAMES = 512
+    GRAPH_AFTER = 2
+    GRAPH_CACHE = 8
 
     def set_graphs(self, enable):
         """Replay captured forwards of small plans (default on); off: every forward enqueued."""
@@ -382,30 +401,39 @@ class CnetEngine:
 
     def _graph_ok(self, plan, mean, stream):
         return (self.graphs and self._branchy and not self._timing and mean is None
-                and sum(plan.frames) <= self.GRAPH_MAX_FRAMES and not torch.cuda.is_current_stream_capturing())
+                and sum(plan.frames) <= self.GRAPH_MAX_FRAMES and not torch.cuda.is_current_stream_capturing()
+                and (plan.runs >= self.GRAPH_AFTER or self._graph_key(plan, stream) in self._graphs))
+
+    def _graph_key(self, plan, stream):
+        return (id(plan), stream.cuda_stream, self.packed.data_ptr(), self.split_f16, self._graph_epoch)
 
     def _replay(self, plan, mel, out, stream):
-        key = (id(plan), stream.cuda_stream, self.packed.data_ptr(), self.split_f16, self._graph_epoch)
+        key = self._graph_key(plan, stream)
         ent = self._graphs.get(key)
         if ent is None:
             for name, t in (("mel", mel), ("out", out)):
                 if t.device != self.device or t.dtype != torch.float32 or not t.is_contiguous():
                     raise ValueError(f"{name} must be a contiguous float32 tensor on {self.device}")
-            cs = torch.cuda.Stream(self.device)  # capture stream: its workspace belongs to this graph
+            # the graph's own buffers and workspace: no other run (eager forwards on a pool stream
+            # of the same handle value, other graphs) ever writes them
+            cs = torch.cuda.Stream(self.device)
             g_mel, g_out = torch.empty_like(mel), torch.empty_like(out)
+            g_ws = torch.empty(max(int(plan.workspace_bytes), 256), dtype=torch.uint8, device=self.device)
             cs.wait_stream(stream)
             with torch.cuda.stream(cs):
                 g_mel.copy_(mel)
-                self._enqueue(plan, g_mel, g_out, None, None, cs)  # warm-up: sizes the workspace
+                self._enqueue(plan, g_mel, g_out, None, None, cs, ws=g_ws)  # warm-up
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=cs):
-                    self._enqueue(plan, g_mel, g_out, None, None, cs)
+                with torch.cuda.graph(g, stream=cs, capture_error_mode="thread_local"):
+                    self._enqueue(plan, g_mel, g_out, None, None, cs, ws=g_ws)
             stream.wait_stream(cs)
             # (the entry holds the plan, the weights and the workspace the graph's launches point at)
-            ent = (g, g_mel, g_out, cs, self.workspace(plan.workspace_bytes, cs), plan, self.packed)
+            ent = (g, g_mel, g_out, cs, g_ws, plan, self.packed)
             self._graphs[key] = ent
-            while len(self._graphs) > 8:
+            while len(self._graphs) > self.GRAPH_CACHE:
                 self._graphs.popitem(last=False)
+        else:
+            self._graphs.move_to_end(key)
         g, g_mel, g_out, cs, ws = ent[:5]
         if mel.numel() != g_mel.numel() or out.numel() != g_out.numel():
             raise ValueError("mel / output buffer has the wrong size for the plan")
@@ -435,7 +463,7 @@ class CnetEngine:
             ws = self.workspace(plan.workspace_bytes, stream)
         _lib.check(self._lib.pwg_cnet_run_status(plan._p, ws.data_ptr(), stream.cuda_stream))
 
-    def _enqueue(self, plan, mel, out, mean, scale, stream):
+    def _enqueue(self, plan, mel, out, mean, scale, stream, ws=None):
         if self.packed is None:
             raise RuntimeError("no weights loaded")
         for name, t in (("mel", mel), ("out", out)):
@@ -450,7 +478,8 @@ class CnetEngine:
             mean = mean.to(self.device, torch.float32).contiguous()
             scale = scale.to(self.device, torch.float32).contiguous()
             mp, sp = mean.data_ptr(), scale.data_ptr()
-        ws = self.workspace(plan.workspace_bytes, stream)
+        if ws is None:
+            ws = self.workspace(plan.workspace_bytes, stream)
         _lib.check(self._lib.pwg_cnet_run(plan._p, self.packed.data_ptr(), mel.data_ptr(), mp, sp, out.data_ptr(),
                                           ws.data_ptr(), stream.cuda_stream))
         return out
@@ -545,6 +574,13 @@ class CnetEngine:
         _lib.check(self._lib.pwg_cnet_set_option(self._h, 2, int(steps)))
         self._graph_epoch += 1
         self._plans.clear()
+
+    def timing_span(self):
+        """pwg_cnet_timing_span: device ms from the first timed launch's start to the last one's
+        end (concurrent streams counted once); call before collect_timing."""
+        v = ctypes.c_double()
+        _lib.check(self._lib.pwg_cnet_timing_span(self._h, ctypes.byref(v)))
+        return v.value
 
     def collect_timing(self):
         n = len(self.program.ops)

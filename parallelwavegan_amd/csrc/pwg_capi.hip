@@ -389,7 +389,7 @@ struct PwgHandle {
   unsigned long long* d_trace = nullptr;
   size_t trace_words = 0;
   // timing
-  bool timing = false;
+  int timing = 0;  // pwg_set_timing: 1 per-launch events, 2 one event pair around each run
   std::vector<TimingRecord> records;
   std::vector<hipEvent_t> event_pool;
 };
@@ -968,8 +968,26 @@ static hipEvent_t pool_get(PwgHandle* h) {
   return e;
 }
 
+static int pwg_run_impl(PwgPlan* p, const float* packed, const float* mel, const float* noise, const float* mean,
+                        const float* scale, float* out, void* workspace, void* stream);
+
 int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* noise, const float* mean,
             const float* scale, float* out, void* workspace, void* stream) {
+  // timing mode 2: one event pair around the whole run (its device span, pwg_timing_span)
+  if (!p || p->h->timing != 2) return pwg_run_impl(p, packed, mel, noise, mean, scale, out, workspace, stream);
+  PwgHandle* h = p->h;
+  DeviceGuard g(h->device);
+  hipStream_t s = (hipStream_t)stream;
+  hipEvent_t a = pool_get(h), b = pool_get(h);
+  if (!a || !b || hipEventRecord(a, s) != hipSuccess) return fail(PWG_ERR_HIP, "timing event");
+  const int rc = pwg_run_impl(p, packed, mel, noise, mean, scale, out, workspace, stream);
+  if (hipEventRecord(b, s) != hipSuccess) return fail(PWG_ERR_HIP, "timing event");
+  h->records.push_back({-1, a, b});
+  return rc;
+}
+
+static int pwg_run_impl(PwgPlan* p, const float* packed, const float* mel, const float* noise, const float* mean,
+                        const float* scale, float* out, void* workspace, void* stream) {
   if (!p || !packed || !mel || !noise || !out || !workspace) return fail(PWG_ERR_INVALID, "null argument");
   if (((uintptr_t)workspace & 255) != 0) return fail(PWG_ERR_INVALID, "workspace must be 256-byte aligned");
   if ((mean == nullptr) != (scale == nullptr)) return fail(PWG_ERR_INVALID, "mean and scale go together");
@@ -998,7 +1016,7 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
   int* sched_ctr = (int*)(ws + p->ws_ctr);
 
   auto timed = [&](int bucket, auto&& launch) -> hipError_t {
-    if (!h->timing) return launch();
+    if (h->timing != 1) return launch();
     hipEvent_t a = pool_get(h), b = pool_get(h);
     if (!a || !b) return hipErrorOutOfMemory;
     hipError_t e = hipEventRecord(a, s);
@@ -1494,7 +1512,8 @@ int pwg_get_option(const PwgHandle* h, int option, long long* value) {
 
 int pwg_set_timing(PwgHandle* h, int enable) {
   if (!h) return fail(PWG_ERR_INVALID, "null handle");
-  h->timing = enable != 0;
+  if (enable < 0 || enable > 2) return fail(PWG_ERR_INVALID, "timing mode must be 0, 1 or 2");
+  h->timing = enable;
   return PWG_OK;
 }
 
@@ -1506,12 +1525,32 @@ int pwg_timing_collect(PwgHandle* h, double* ms, long long* launches) {
     float t = 0.f;
     if (e == hipSuccess) e = hipEventElapsedTime(&t, r.start, r.stop);
     if (e != hipSuccess) return hip_fail(e, "timing collect");
-    ms[r.bucket] += t;
-    launches[r.bucket] += 1;
+    if (r.bucket >= 0) {  // (-1: a whole-run span record of timing mode 2)
+      ms[r.bucket] += t;
+      launches[r.bucket] += 1;
+    }
     h->event_pool.push_back(r.start);
     h->event_pool.push_back(r.stop);
   }
   h->records.clear();
+  return PWG_OK;
+}
+
+int pwg_timing_span(PwgHandle* h, double* span_ms) {
+  if (!h || !span_ms) return fail(PWG_ERR_INVALID, "null argument");
+  *span_ms = 0.0;
+  if (h->records.empty()) return PWG_OK;
+  DeviceGuard g(h->device);
+  hipEvent_t ref = h->records[0].start;  // one stream: every later record is later
+  double hi = 0.0;
+  for (auto& r : h->records) {
+    hipError_t e = hipEventSynchronize(r.stop);
+    float t = 0.f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&t, ref, r.stop);
+    if (e != hipSuccess) return hip_fail(e, "timing span");
+    hi = std::max(hi, (double)t);
+  }
+  *span_ms = hi;
   return PWG_OK;
 }
 

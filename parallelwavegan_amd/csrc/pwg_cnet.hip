@@ -3108,6 +3108,82 @@ __global__ void __launch_bounds__(256) pwg_cnet_finite_kernel(const float* y, lo
 }
 
 // ---------------------------------------------------------------------------------------------
+// A plan's device lists (segments, block lists, columns per utterance, fused-pair strips, x-tile
+// and narrow blocks with their frame ranges) live in the caller's workspace and are written at the
+// start of every run by pwg_cnet_desc_kernel from the utterance lengths carried in its arguments:
+// a new plan costs host work only (no per-plan allocation or copy), and a captured forward
+// regenerates them itself. Every list is one enumeration over the plan's utterances:
+//   CN_L_SEG   per utterance: (first row, rows) of a buffer of `rate` rows per frame;
+//   CN_L_NCOL  per utterance: its columns n_u = ceil((frames * rate - ophase) / ostride);
+//   CN_L_BLK   per utterance, q0 = 0, step, .. < n_u: (utterance, q0);
+//   CN_L_NFR   same enumeration as CN_L_BLK: (first frame, frames) of the utterance.
+// The host builds the same image (pwg_cnet_plan_image) and checks it against the lists it
+// validated, so the kernel's output is the checked image.
+enum { CN_L_SEG = 0, CN_L_NCOL = 1, CN_L_BLK = 2, CN_L_NFR = 3 };
+constexpr int CN_DESC_UTTS = 64;   // utterances per descriptor launch
+constexpr int CN_DESC_SPECS = 40;  // lists per descriptor launch (kernel arguments ~2.6 KB)
+struct CnDescSpec {
+  int kind, rate, ostride, ophase, step;
+  int off;              // ints into the image
+  long long base_idx;   // entries of the utterances before this launch's first
+  long long base_row;   // CN_L_SEG: rows of the utterances before this launch's first
+};
+struct CnDescArgs {
+  int* img;
+  int* flag;            // first launch: the run's range flag, zeroed here (null otherwise)
+  int n_utts, u0, f0, n_specs;
+  int last;             // covers the plan's last utterances: also writes each odd-length CN_L_NCOL
+                        // list's pad int (0) before the next 8-byte-aligned list
+  int frames[CN_DESC_UTTS];
+  CnDescSpec specs[CN_DESC_SPECS];
+};
+
+__host__ __device__ inline long long cn_list_cols(int kind, long long frames, int rate, int ostride, int ophase) {
+  const long long T = frames * rate;
+  return kind == CN_L_SEG ? T : (T - ophase + ostride - 1) / ostride;
+}
+__host__ __device__ inline long long cn_list_count(int kind, long long cols, int step) {
+  return (kind == CN_L_SEG || kind == CN_L_NCOL) ? 1 : (cols + step - 1) / step;
+}
+
+// one workgroup per list: per-utterance entry counts, their prefix (thread 0; <= 64 utterances),
+// then the entries, 8-byte stores
+__global__ void __launch_bounds__(256) pwg_cnet_desc_kernel(const CnDescArgs a) {
+  const CnDescSpec& sp = a.specs[blockIdx.x];
+  __shared__ long long start[CN_DESC_UTTS + 1], row0[CN_DESC_UTTS + 1], frame0[CN_DESC_UTTS + 1];
+  if (threadIdx.x == 0) {
+    long long e = sp.base_idx, r = sp.base_row, f = a.f0;
+    for (int u = 0; u < a.n_utts; ++u) {
+      start[u] = e; row0[u] = r; frame0[u] = f;
+      const long long cols = cn_list_cols(sp.kind, a.frames[u], sp.rate, sp.ostride, sp.ophase);
+      e += cn_list_count(sp.kind, cols, sp.step);
+      r += (long long)a.frames[u] * sp.rate;
+      f += a.frames[u];
+    }
+    start[a.n_utts] = e;
+  }
+  if (a.flag != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *a.flag = 0;
+  __syncthreads();
+  if (a.last && sp.kind == CN_L_NCOL && threadIdx.x == 0 && (start[a.n_utts] & 1)) a.img[sp.off + start[a.n_utts]] = 0;
+  for (int u = 0; u < a.n_utts; ++u) {
+    const long long cols = cn_list_cols(sp.kind, a.frames[u], sp.rate, sp.ostride, sp.ophase);
+    const long long n = start[u + 1] - start[u];
+    for (long long j = threadIdx.x; j < n; j += 256) {
+      const long long at = start[u] + j;
+      if (sp.kind == CN_L_NCOL) {
+        a.img[sp.off + at] = (int)cols;
+      } else {
+        int2 v;
+        if (sp.kind == CN_L_SEG) v = make_int2((int)row0[u], (int)((long long)a.frames[u] * sp.rate));
+        else if (sp.kind == CN_L_BLK) v = make_int2(a.u0 + u, (int)(j * sp.step));
+        else v = make_int2((int)frame0[u], a.frames[u]);
+        reinterpret_cast<int2*>(a.img + sp.off)[at] = v;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 struct OpPhase {          // one launch
   int op = 0;
   int phase = 0;          // CONVT phase r, else 0
@@ -3167,15 +3243,24 @@ struct PwgCnet {
   int streams = 1;     // PWG_CNET_OPT_STREAMS: 0 one stream, 1 independent launches of plans with narrow
                        // launches run on auxiliary streams, 2 every plan
   static constexpr int N_AUX = 3;
-  hipStream_t aux[N_AUX] = {nullptr, nullptr, nullptr};
-  std::mutex mu;       // the auxiliary streams and the plans' event sets (concurrent runs from host threads)
+  // Auxiliary streams and cross-stream dependency events, one set per caller stream: a forward
+  // being captured on one caller stream forks into aux streams no other caller's run uses, and
+  // runs of one plan (or of two plans) on two caller streams never record into each other's events.
+  // Events are re-recorded every run (a wait binds the record made before it). Guarded by mu.
+  struct CallerSet {
+    hipStream_t aux[N_AUX] = {nullptr, nullptr, nullptr};
+    std::vector<hipEvent_t> ev;
+  };
+  std::map<hipStream_t, CallerSet> callers;
+  std::mutex mu;       // `callers` (concurrent runs from host threads)
+  int n_cu = 0;        // CUs of the device (queried once; plan-time launch sizing)
   bool pair_attr_set = false;
   std::vector<PwgCnetOp> ops;
   std::vector<int> channels, rate, ld;
   long long ref_count = 0;
   std::vector<OpPhase> phases;
   long long packed_count = 0;
-  bool timing = false;
+  int timing = 0;  // pwg_cnet_set_timing: 1 per-launch events, 2 one event pair around each run
   struct Rec { int op; hipEvent_t a, b; };
   std::vector<Rec> records;
   std::vector<hipEvent_t> pool;
@@ -3189,13 +3274,19 @@ struct PwgCnetPlan {
   std::vector<size_t> buf_off;               // workspace offsets (SIZE_MAX: external)
   size_t ws_bytes = 0;
   size_t ws_flag = 0;                        // split-f16 range flag (one int) in the workspace
-  int* d_seg = nullptr;                      // [n_bufs][n_utts][2]
-  std::vector<int2*> d_blocks;               // per phase
+  size_t ws_img = 0;                         // the device lists (pwg_cnet_desc_kernel) in the workspace
+  // Device lists as int offsets into that image (-1 = none); see CnDescSpec. The host image `img`
+  // is what the descriptor kernel writes (built and checked here, never uploaded).
+  std::vector<int> img;
+  std::vector<CnDescSpec> specs;
+  std::vector<CnDescArgs> desc;              // the descriptor launches' arguments (image / flag set per run)
+  std::vector<int> o_seg;                   // per buffer: [n_utts][2] (first row, rows)
+  std::vector<int> o_blocks;                 // per phase
   std::vector<int> n_blocks;
-  std::vector<int*> d_ncols;                 // per phase
-  std::vector<int2*> d_strips;               // per phase: fused-pair strips (utt, q0), or null
+  std::vector<int> o_ncols;                  // per phase
+  std::vector<int> o_strips;                 // per phase: fused-pair strips (utt, q0)
   std::vector<int> n_strips;
-  std::vector<int2*> d_xblocks;              // per phase: x-tile pair blocks (utt, q0 step XP_OUT), or null
+  std::vector<int> o_xblocks;                // per phase: x-tile pair blocks (utt, q0 step XP_OUT)
   std::vector<int> n_xblocks;
   int pair_steps = 16;
   bool host_only = false;                    // a handle created for device -1: built and checked, not uploaded
@@ -3204,12 +3295,9 @@ struct PwgCnetPlan {
   std::vector<int> nar_nwv, nar_mt, nar_lds, n_nblocks;
   std::vector<char> nar_tap;                 // ... on the tap-major kernel (not the x-tile family)
   std::vector<char> nar_xdma;                // ... on the DMA-ring kernel (tap-major phases: K = 1 mode)
-  std::vector<int2*> d_nblocks;              // its blocks (utt, q0 step 32 nar_nwv)
-  std::vector<int2*> d_nfr;                  // ... and their utterances' (first frame, frames)
+  std::vector<int> o_nblocks;                // its blocks (utt, q0 step 32 nar_nwv)
+  std::vector<int> o_nfr;                    // ... and their utterances' (first frame, frames)
   bool has_narrow = false;                   // some phase runs narrow (PWG_CNET_OPT_STREAMS 1)
-  // cross-stream dependency events, one set per caller stream (runs of one plan on two streams
-  // must not record into each other's events), reused every run; guarded by PwgCnet::mu
-  std::map<hipStream_t, std::vector<hipEvent_t>> xev_of;
 };
 
 namespace {
@@ -3834,8 +3922,11 @@ void pwg_cnet_destroy(PwgCnet* n) {
     if (ph.d_chunks) (void)hipFree(ph.d_chunks);
   for (auto& r : n->records) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
   for (hipEvent_t e : n->pool) (void)hipEventDestroy(e);
-  for (hipStream_t x : n->aux)
-    if (x) (void)hipStreamDestroy(x);
+  for (auto& kv : n->callers) {
+    for (hipStream_t x : kv.second.aux)
+      if (x) (void)hipStreamDestroy(x);
+    for (hipEvent_t e : kv.second.ev) (void)hipEventDestroy(e);
+  }
   delete n;
 }
 
@@ -3911,16 +4002,12 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
   p->n_utts = n_utts;
   p->pair_steps = n->pair_steps;
   p->frames.assign(frames, frames + n_utts);
-  std::vector<int> seg((size_t)nb * n_utts * 2);
   p->rows.assign(nb, 0);
   for (int b = 0; b < nb; ++b) {
     long long base = 0;
     for (int u = 0; u < n_utts; ++u) {
       if (frames[u] < 1) { delete p; return fail(PWG_ERR_INVALID, "every utterance needs >= 1 frame"); }
-      const long long r = frames[u] * n->rate[b];
-      seg[((size_t)b * n_utts + u) * 2] = (int)base;
-      seg[((size_t)b * n_utts + u) * 2 + 1] = (int)r;
-      base += r;
+      base += frames[u] * n->rate[b];
     }
     if (base >= (1LL << 31) / std::max(1, n->ld[b])) { delete p; return fail(PWG_ERR_UNSUPPORTED, "batch too large for one plan"); }
     p->rows[b] = base;
@@ -3977,13 +4064,14 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
     p->ws_bytes = o + 256;
   };
   assign_slots(true);
-  // host side of every per-phase list first (block lists, columns per utterance, fused-pair strips,
-  // x-tile blocks), each checked before anything reaches the GPU: a bad list (a step or count that
-  // was never set, a block outside its utterance) fails here with PWG_ERR_ASSERT instead of turning
-  // into an illegal address in a kernel (round 3's fault: an uninitialised OpPhase field)
+  // Per phase: its columns per utterance, the entry counts of its lists (block list, fused-pair
+  // strips, x-tile blocks, narrow blocks) and its launch sizing. The lists themselves are
+  // enumerations the descriptor kernel writes into the workspace (CnDescSpec), registered once per
+  // distinct (kind, rate, stride, phase, step) -- phases of one rate share them -- and checked below
+  // before the plan can run: a bad list (a step or stride that was never set, an entry outside its
+  // utterance) fails with PWG_ERR_ASSERT instead of turning into an illegal address in a kernel
+  // (round 3's fault: an uninitialised OpPhase field).
   const size_t nph = n->phases.size();
-  std::vector<std::vector<int2>> h_blocks(nph), h_strips(nph), h_xblocks(nph), h_nblocks(nph);
-  std::vector<std::vector<int>> h_ncols(nph);
   p->nar_nwv.assign(nph, 0);
   p->nar_mt.assign(nph, 0);
   p->nar_lds.assign(nph, 0);
@@ -3991,12 +4079,15 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
   p->nar_xdma.assign(nph, 0);
   p->n_cu = 256;  // host-only handles size for an MI355X
   if (n->device >= 0) {
-    int cu = 0;
-    if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, n->device) != hipSuccess || cu < 1) {
-      delete p;
-      return fail(PWG_ERR_HIP, "cannot query the CU count");
+    if (n->n_cu < 1) {
+      int cu = 0;
+      if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, n->device) != hipSuccess || cu < 1) {
+        delete p;
+        return fail(PWG_ERR_HIP, "cannot query the CU count");
+      }
+      n->n_cu = cu;
     }
-    p->n_cu = cu;
+    p->n_cu = n->n_cu;
   }
   // DMA-ring launches (PWG_CNET_OPT_NARROW_DMA): one m-tile and 4 waves (128 columns) per workgroup
   // when the utterances are that long. A step's serial cost per wave -- DMA issue (~40 cycles per
@@ -4020,56 +4111,79 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
     delete p;
     return fail(PWG_ERR_ASSERT, "internal: plan phase " + std::to_string(pi) + ": " + what);
   };
+  long long img_ints = 0;
+  auto list = [&](int kind, int rate, int ostride, int ophase, int step) -> int {
+    for (const CnDescSpec& sp : p->specs)  // a few dozen distinct lists
+      if (sp.kind == kind && sp.rate == rate && sp.ostride == ostride && sp.ophase == ophase && sp.step == step)
+        return sp.off;
+    long long cnt = 0;
+    for (int u = 0; u < n_utts; ++u)
+      cnt += cn_list_count(kind, cn_list_cols(kind, frames[u], rate, ostride, ophase), step);
+    img_ints = (img_ints + 1) / 2 * 2;  // int2 lists 8-byte aligned
+    CnDescSpec sp{kind, rate, ostride, ophase, step, (int)img_ints, 0, 0};
+    img_ints += cnt * (kind == CN_L_NCOL ? 1 : 2);
+    p->specs.push_back(sp);
+    return sp.off;
+  };
+  for (int b = 0; b < nb; ++b) p->o_seg.push_back(list(CN_L_SEG, n->rate[b], 1, 0, 1));
+  std::vector<int> ncols(n_utts, 0);
+  auto count = [&](int step) {
+    long long c = 0;
+    for (int u = 0; u < n_utts; ++u) c += (ncols[u] + step - 1) / step;
+    return c;
+  };
   for (size_t pi = 0; pi < nph; ++pi) {
     const OpPhase& ph = n->phases[pi];
     const PwgCnetOp& op = n->ops[ph.op];
-    std::vector<int2>& blocks = h_blocks[pi];
-    std::vector<int>& ncols = h_ncols[pi];
-    ncols.assign(n_utts, 0);
-    if (op.kind == PWG_CNET_PQMF) {
-      for (int u = 0; u < n_utts; ++u) {
-        const long long T = frames[u] * n->rate[op.dst];
-        for (long long t0 = 0; t0 < T; t0 += 256) blocks.push_back(make_int2(u, (int)t0));
-      }
-    } else {
-      if (ph.ostride < 1 || ph.ophase < 0 || ph.ophase >= ph.ostride) return bad_list(pi, "output stride / phase");
-      const int cols = ph.thin ? CN_COLS : 32 * ph.NW;
-      if (ph.NW != 4 && ph.NW != 8) return bad_list(pi, "waves per workgroup");
-      for (int u = 0; u < n_utts; ++u) {
-        const long long T = frames[u] * n->rate[op.dst];
-        const int nq = (int)((T - ph.ophase + ph.ostride - 1) / ph.ostride);
-        ncols[u] = nq;
-        for (int q0 = 0; q0 < nq; q0 += cols) blocks.push_back(make_int2(u, q0));
-      }
-    }
+    const int rate = n->rate[op.dst];
+    const bool pq = op.kind == PWG_CNET_PQMF;
+    if (!pq && (ph.ostride < 1 || ph.ophase < 0 || ph.ophase >= ph.ostride)) return bad_list(pi, "output stride / phase");
+    if (!pq && ph.NW != 4 && ph.NW != 8) return bad_list(pi, "waves per workgroup");
+    const int os = pq ? 1 : ph.ostride, oph = pq ? 0 : ph.ophase;
+    for (int u = 0; u < n_utts; ++u) ncols[u] = (int)cn_list_cols(CN_L_NCOL, frames[u], rate, os, oph);
+    const int blk_step = pq ? 256 : (ph.thin ? CN_COLS : 32 * ph.NW);
+    const long long n_blk = count(blk_step);
+    if (n_blk > (long long)INT32_MAX / 2) return bad_list(pi, "block count");
+    p->o_blocks.push_back(list(CN_L_BLK, rate, os, oph, blk_step));
+    p->n_blocks.push_back((int)n_blk);
+    p->o_ncols.push_back(pq ? -1 : list(CN_L_NCOL, rate, os, oph, 1));
     if (ph.pair_b >= 0) {
       if (p->pair_steps < 1) return bad_list(pi, "pair strip steps");
-      for (int u = 0; u < n_utts; ++u)
-        for (int q0 = 0; q0 < ncols[u]; q0 += 128 * p->pair_steps) h_strips[pi].push_back(make_int2(u, q0));
+      p->o_strips.push_back(list(CN_L_BLK, rate, os, oph, 128 * p->pair_steps));
+      p->n_strips.push_back((int)count(128 * p->pair_steps));
+    } else {
+      p->o_strips.push_back(-1);
+      p->n_strips.push_back(0);
     }
     if (ph.xpair_b >= 0 || (ph.stack_b >= 0 && ph.xtile) || ph.xt_convt_db) {
       const int step = ph.xpair_b >= 0 ? XP_OUT : XT_COLS;
-      for (int u = 0; u < n_utts; ++u)
-        for (int q0 = 0; q0 < ncols[u]; q0 += step) h_xblocks[pi].push_back(make_int2(u, q0));
+      p->o_xblocks.push_back(list(CN_L_BLK, rate, os, oph, step));
+      p->n_xblocks.push_back((int)count(step));
+    } else {
+      p->o_xblocks.push_back(-1);
+      p->n_xblocks.push_back(0);
     }
     // narrow x-tile launch: phases of the x-tile family (plain x-tile convs, x-tile pair / stack
     // halves, ConvTranspose phases) whose default launch has fewer workgroups than CUs (or all of
     // them with PWG_CNET_OPT_NARROW 2): the widest tile (waves, m-tiles) that gives every CU one
     // workgroup, else the narrowest
-    p->nar_nwv[pi] = p->nar_mt[pi] = p->nar_lds[pi] = 0;
-    const bool xt_family = !ph.thin && op.kind != PWG_CNET_PQMF && (ph.xtile || ph.xt_convt_db) &&
-                           ph.z_phases > 0 && ph.MT >= 1;
-    const bool convt_ = op.kind == PWG_CNET_CONVT;
-    if (n->narrow && xt_family && (convt_ || (op.src[0].taps - 1) * op.src[0].dilation <= NARROW_HALO)) {
-      const bool convt = convt_;
+    const bool xt_family = !ph.thin && !pq && (ph.xtile || ph.xt_convt_db) && ph.z_phases > 0 && ph.MT >= 1;
+    const bool convt = op.kind == PWG_CNET_CONVT;
+    // narrow tap-major launch (split-f16 convs outside the x-tile family, e.g. MelGAN's two-source
+    // 1x1s; not the fused tap-major pairs / stacks): 1-2 waves, 1-2 m-tiles, CN_NARROW_G chunks per
+    // barrier
+    const bool tap_family = !xt_family && !ph.thin && !pq && ph.z_phases > 0 && ph.pair_b < 0 &&
+                            !(pi > 0 && n->phases[pi - 1].pair_b == (int)pi) && ph.stack_b < 0 && !ph.xt_convt_db;
+    const long long zn = ph.z_phases;
+    int pick_w = 0, pick_m = 1;
+    if (n->narrow && xt_family && (convt || (op.src[0].taps - 1) * op.src[0].dilation <= NARROW_HALO)) {
       const int xk = convt ? 2 : op.src[0].taps, xd = convt ? 1 : op.src[0].dilation;
-      const long long zn = ph.z_phases;
       long long base = 0;
-      if (ph.xpair_b >= 0 || (ph.stack_b >= 0 && ph.xtile)) base = (long long)h_xblocks[pi].size();
-      else if (ph.xt_convt_db) base = (long long)h_xblocks[pi].size() * (ph.mt_total / ph.MT) * zn;
-      else base = (long long)blocks.size() * (ph.mt_total / ph.MT) * zn;
+      if (ph.xpair_b >= 0 || (ph.stack_b >= 0 && ph.xtile)) base = p->n_xblocks[pi];
+      else if (ph.xt_convt_db) base = (long long)p->n_xblocks[pi] * (ph.mt_total / ph.MT) * zn;
+      else base = n_blk * (ph.mt_total / ph.MT) * zn;
       if (n->narrow == 2 || base < p->n_cu) {
-        int pick_w = 1, pick_m = 1;
+        pick_w = 1;
         if (n->narrow_dma && xdma_fits(ncols, xdma_waves(ncols), (long long)ph.mt_total * zn)) {
           pick_w = xdma_waves(ncols);
           p->nar_xdma[pi] = 1;
@@ -4078,10 +4192,7 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
           for (int w : {4, 2, 1}) {
             for (int mtn : {2, 1}) {
               if (mtn == 2 && ph.mt_total % 2 != 0) continue;
-              long long nwg = 0;
-              for (int u = 0; u < n_utts; ++u) nwg += (ncols[u] + 32 * w - 1) / (32 * w);
-              nwg *= (ph.mt_total / mtn) * zn;
-              if (nwg >= p->n_cu) {
+              if (count(32 * w) * (ph.mt_total / mtn) * zn >= p->n_cu) {
                 pick_w = w;
                 pick_m = mtn;
                 found = true;
@@ -4092,24 +4203,12 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
           }
         }
         const int span = 32 * pick_w + (xk - 1) * xd;
-        p->nar_nwv[pi] = pick_w;
-        p->nar_mt[pi] = pick_m;
         p->nar_lds[pi] = 2 * narrow_ks(xk) * pick_m * 2048 + span * XT_ROWB;
-        for (int u = 0; u < n_utts; ++u)
-          for (int q0 = 0; q0 < ncols[u]; q0 += 32 * pick_w) h_nblocks[pi].push_back(make_int2(u, q0));
       }
-    }
-    // narrow tap-major launch (split-f16 convs outside the x-tile family, e.g. MelGAN's two-source
-    // 1x1s; not the fused tap-major pairs / stacks): 1-2 waves, 1-2 m-tiles, CN_NARROW_G chunks per
-    // barrier
-    const bool tap_family = !xt_family && !ph.thin && op.kind != PWG_CNET_PQMF && ph.z_phases > 0 &&
-                            ph.pair_b < 0 && !(pi > 0 && n->phases[pi - 1].pair_b == (int)pi) && ph.stack_b < 0 &&
-                            !ph.xt_convt_db;
-    if (n->narrow && tap_family) {
-      const long long zn = ph.z_phases;
-      const long long base = (long long)blocks.size() * (ph.mt_total / ph.MT) * zn;
+    } else if (n->narrow && tap_family) {
+      const long long base = n_blk * (ph.mt_total / ph.MT) * zn;
       if (n->narrow == 2 || base < p->n_cu) {
-        int pick_w = 1, pick_m = 1;
+        pick_w = 1;
         // the DMA-ring kernel (K = 1 mode) unless a source normalizes (the narrow tap-major kernel
         // then runs it, 1-2 waves)
         if (n->narrow_dma && !op.src[0].normalize && !(op.src[1].buf >= 0 && op.src[1].normalize) &&
@@ -4122,10 +4221,7 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
           for (int w : {2, 1}) {
             for (int mtn : {2, 1}) {
               if (mtn == 2 && ph.mt_total % 2 != 0) continue;
-              long long nwg = 0;
-              for (int u = 0; u < n_utts; ++u) nwg += (ncols[u] + 32 * w - 1) / (32 * w);
-              nwg *= (ph.mt_total / mtn) * zn;
-              if (nwg >= p->n_cu) {
+              if (count(32 * w) * (ph.mt_total / mtn) * zn >= p->n_cu) {
                 pick_w = w;
                 pick_m = mtn;
                 found = true;
@@ -4135,53 +4231,85 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
             if (found) break;
           }
         }
-        p->nar_nwv[pi] = pick_w;
-        p->nar_mt[pi] = pick_m;
         p->nar_tap[pi] = 1;
-        for (int u = 0; u < n_utts; ++u)
-          for (int q0 = 0; q0 < ncols[u]; q0 += 32 * pick_w) h_nblocks[pi].push_back(make_int2(u, q0));
       }
     }
-    // every list: utterance in range, first column inside it
-    for (const std::vector<int2>* lst : {&blocks, &h_strips[pi], &h_xblocks[pi], &h_nblocks[pi]})
-      for (const int2& b : *lst) {
-        if (b.x < 0 || b.x >= n_utts || b.y < 0) return bad_list(pi, "block outside the batch");
-        const long long lim = op.kind == PWG_CNET_PQMF ? frames[b.x] * n->rate[op.dst] : ncols[b.x];
-        if (b.y >= lim) return bad_list(pi, "block past its utterance");
-      }
-    if (blocks.size() > (size_t)INT32_MAX / 2) return bad_list(pi, "block count");
+    p->nar_nwv[pi] = pick_w;
+    p->nar_mt[pi] = pick_w > 0 ? pick_m : 0;
+    p->o_nblocks.push_back(pick_w > 0 ? list(CN_L_BLK, rate, os, oph, 32 * pick_w) : -1);
+    p->o_nfr.push_back(pick_w > 0 ? list(CN_L_NFR, rate, os, oph, 32 * pick_w) : -1);
+    p->n_nblocks.push_back(pick_w > 0 ? (int)count(32 * pick_w) : 0);
   }
   for (size_t pi = 0; pi < nph; ++pi) p->has_narrow |= p->nar_nwv[pi] > 0;
   if (n->streams == 2 || (n->streams == 1 && p->has_narrow)) assign_slots(false);
-  // narrow blocks' utterance frame ranges (the DMA-ring kernel derives every row range from them)
-  std::vector<long long> f0(n_utts, 0);
-  for (int u = 1; u < n_utts; ++u) f0[u] = f0[u - 1] + frames[u - 1];
-  std::vector<std::vector<int2>> h_nfr(nph);
-  for (size_t pi = 0; pi < nph; ++pi)
-    for (const int2& b : h_nblocks[pi]) h_nfr[pi].push_back(make_int2((int)f0[b.x], (int)frames[b.x]));
-  if (n->device < 0) {  // host-only handle: sizes and lists checked, nothing uploaded (cannot run)
-    p->host_only = true;
-    for (size_t pi = 0; pi < nph; ++pi) {
-      p->d_blocks.push_back(nullptr);
-      p->n_blocks.push_back((int)h_blocks[pi].size());
-      p->d_ncols.push_back(nullptr);
-      p->d_strips.push_back(nullptr);
-      p->n_strips.push_back((int)h_strips[pi].size());
-      p->d_xblocks.push_back(nullptr);
-      p->n_xblocks.push_back((int)h_xblocks[pi].size());
-      p->d_nblocks.push_back(nullptr);
-      p->n_nblocks.push_back((int)h_nblocks[pi].size());
-      p->d_nfr.push_back(nullptr);
+  img_ints = (img_ints + 1) / 2 * 2;  // room for a last odd NCOL list's pad int
+  if (img_ints >= (1LL << 30)) { delete p; return fail(PWG_ERR_UNSUPPORTED, "batch too large for one plan"); }
+  // host image (the descriptor kernel's algorithm), every entry checked: utterance in the batch,
+  // first column inside it, frame range and segment rows consistent with the plan
+  p->img.assign((size_t)img_ints, 0);
+  for (size_t si = 0; si < p->specs.size(); ++si) {
+    const CnDescSpec& sp = p->specs[si];
+    if (sp.kind < CN_L_SEG || sp.kind > CN_L_NFR || sp.rate < 1 || sp.ostride < 1 || sp.ophase < 0 ||
+        sp.ophase >= sp.ostride || sp.step < 1)
+      return bad_list(si, "device list with an unset step / stride");
+    long long at = 0, row = 0, f = 0;
+    for (int u = 0; u < n_utts; ++u) {
+      const long long cols = cn_list_cols(sp.kind, frames[u], sp.rate, sp.ostride, sp.ophase);
+      const long long cnt = cn_list_count(sp.kind, cols, sp.step);
+      for (long long j = 0; j < cnt; ++j, ++at) {
+        int* e = p->img.data() + sp.off;
+        if (sp.kind == CN_L_NCOL) { e[at] = (int)cols; continue; }
+        e += 2 * at;
+        if (sp.kind == CN_L_SEG) { e[0] = (int)row; e[1] = (int)(frames[u] * sp.rate); }
+        else if (sp.kind == CN_L_BLK) { e[0] = u; e[1] = (int)(j * sp.step); }
+        else { e[0] = (int)f; e[1] = (int)frames[u]; }
+        if (sp.kind == CN_L_BLK && (e[1] < 0 || e[1] >= cols)) return bad_list(si, "block past its utterance");
+      }
+      row += frames[u] * sp.rate;
+      f += frames[u];
     }
+    if ((size_t)sp.off + (size_t)at * (sp.kind == CN_L_NCOL ? 1 : 2) > p->img.size())
+      return bad_list(si, "device list outside the image");
+  }
+  // descriptor launches: CN_DESC_UTTS utterances x CN_DESC_SPECS lists each, argument blocks
+  // prebuilt here (pwg_cnet_run patches the image and flag pointers)
+  for (int u0 = 0; u0 < n_utts; u0 += CN_DESC_UTTS) {
+    const int nu = std::min(CN_DESC_UTTS, n_utts - u0);
+    long long f0 = 0;
+    for (int u = 0; u < u0; ++u) f0 += frames[u];
+    for (size_t s0 = 0; s0 < p->specs.size(); s0 += CN_DESC_SPECS) {
+      CnDescArgs a;
+      std::memset(&a, 0, sizeof(a));
+      a.n_utts = nu;
+      a.u0 = u0;
+      a.last = u0 + nu == n_utts;
+      a.f0 = (int)f0;
+      for (int u = 0; u < nu; ++u) a.frames[u] = (int)frames[u0 + u];
+      a.n_specs = (int)std::min<size_t>(CN_DESC_SPECS, p->specs.size() - s0);
+      for (int k = 0; k < a.n_specs; ++k) {
+        CnDescSpec sp = p->specs[s0 + k];
+        for (int u = 0; u < u0; ++u) {
+          sp.base_idx += cn_list_count(sp.kind, cn_list_cols(sp.kind, frames[u], sp.rate, sp.ostride, sp.ophase), sp.step);
+          sp.base_row += frames[u] * sp.rate;
+        }
+        a.specs[k] = sp;
+      }
+      p->desc.push_back(a);
+    }
+  }
+  p->ws_img = p->ws_bytes;  // after the buffer slots and the flag (256-byte aligned)
+  p->ws_bytes = p->ws_img + ((size_t)img_ints * sizeof(int) + 255) / 256 * 256;
+  if (n->device < 0) {  // host-only handle: sizes and lists checked (cannot run)
+    p->host_only = true;
     *out = p;
     return PWG_OK;
   }
+  // the handle's chunk tables (first plan only: they depend on the program, not the utterances)
   Guard g(n->device);
   if (!g.ok) { delete p; return fail(PWG_ERR_HIP, "hipSetDevice failed"); }
-  hipError_t e = hipSuccess;
   for (OpPhase& ph : n->phases) {
     if (ph.chunks.empty() || ph.d_chunks) continue;
-    e = hipMalloc(&ph.d_chunks, sizeof(ChunkDesc) * ph.chunks.size());
+    hipError_t e = hipMalloc(&ph.d_chunks, sizeof(ChunkDesc) * ph.chunks.size());
     if (e == hipSuccess)
       e = hipMemcpy(ph.d_chunks, ph.chunks.data(), sizeof(ChunkDesc) * ph.chunks.size(), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
@@ -4191,67 +4319,18 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
       return hipf(e, "chunk table upload");
     }
   }
-  e = hipMalloc(&p->d_seg, sizeof(int) * seg.size());
-  if (e == hipSuccess) e = hipMemcpy(p->d_seg, seg.data(), sizeof(int) * seg.size(), hipMemcpyHostToDevice);
-  auto upload = [&](const std::vector<int2>& v, int2** d) {
-    *d = nullptr;
-    if (e != hipSuccess || v.empty()) return;
-    e = hipMalloc(d, sizeof(int2) * v.size());
-    if (e == hipSuccess) e = hipMemcpy(*d, v.data(), sizeof(int2) * v.size(), hipMemcpyHostToDevice);
-  };
-  for (size_t pi = 0; pi < nph; ++pi) {
-    int2* db = nullptr;
-    int* dn = nullptr;
-    upload(h_blocks[pi], &db);
-    if (e == hipSuccess && !h_blocks[pi].empty()) {
-      e = hipMalloc(&dn, sizeof(int) * n_utts);
-      if (e == hipSuccess) e = hipMemcpy(dn, h_ncols[pi].data(), sizeof(int) * n_utts, hipMemcpyHostToDevice);
-    }
-    p->d_blocks.push_back(db);
-    p->n_blocks.push_back((int)h_blocks[pi].size());
-    p->d_ncols.push_back(dn);
-    int2* dstr = nullptr;
-    upload(h_strips[pi], &dstr);
-    p->d_strips.push_back(dstr);
-    p->n_strips.push_back((int)h_strips[pi].size());
-    int2* dxb = nullptr;
-    upload(h_xblocks[pi], &dxb);
-    p->d_xblocks.push_back(dxb);
-    p->n_xblocks.push_back((int)h_xblocks[pi].size());
-    int2* dnb = nullptr;
-    upload(h_nblocks[pi], &dnb);
-    p->d_nblocks.push_back(dnb);
-    p->n_nblocks.push_back((int)h_nblocks[pi].size());
-    int2* dnf = nullptr;
-    upload(h_nfr[pi], &dnf);
-    p->d_nfr.push_back(dnf);
-  }
-  if (e != hipSuccess) {
-    const int rc = hipf(e, "cnet plan upload");
-    pwg_cnet_plan_destroy(p);
-    return rc;
-  }
   *out = p;
   return PWG_OK;
 }
 
-void pwg_cnet_plan_destroy(PwgCnetPlan* p) {
-  if (!p) return;
-  if (p->host_only) {
-    delete p;
-    return;
-  }
-  Guard g(p->n->device);
-  if (p->d_seg) (void)hipFree(p->d_seg);
-  for (auto* x : p->d_blocks) if (x) (void)hipFree(x);
-  for (auto* x : p->d_ncols) if (x) (void)hipFree(x);
-  for (auto* x : p->d_strips) if (x) (void)hipFree(x);
-  for (auto* x : p->d_xblocks) if (x) (void)hipFree(x);
-  for (auto* x : p->d_nblocks) if (x) (void)hipFree(x);
-  for (auto* x : p->d_nfr) if (x) (void)hipFree(x);
-  for (auto& kv : p->xev_of)
-    for (hipEvent_t e : kv.second) (void)hipEventDestroy(e);
-  delete p;
+void pwg_cnet_plan_destroy(PwgCnetPlan* p) { delete p; }  // host memory only
+
+int pwg_cnet_plan_image(const PwgCnetPlan* p, long long* offset_bytes, long long* n_ints, int* out, long long cap) {
+  if (!p || !offset_bytes || !n_ints || (cap > 0 && !out)) return fail(PWG_ERR_INVALID, "null argument");
+  *offset_bytes = (long long)p->ws_img;
+  *n_ints = (long long)p->img.size();
+  if (cap > 0) std::memcpy(out, p->img.data(), sizeof(int) * (size_t)std::min<long long>(cap, (long long)p->img.size()));
+  return PWG_OK;
 }
 
 long long pwg_cnet_plan_rows(const PwgCnetPlan* p, int buf) {
@@ -4274,7 +4353,10 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
   bufs[0] = const_cast<float*>(mel);
   bufs[nb - 1] = out;
   for (int b = 1; b < nb - 1; ++b) bufs[b] = (float*)((char*)workspace + p->buf_off[b]);
-  auto seg_of = [&](int b) -> const int* { return p->d_seg + (size_t)b * p->n_utts * 2; };
+  int* const img = (int*)((char*)workspace + p->ws_img);
+  auto i2 = [&](int off) -> const int2* { return off < 0 ? nullptr : reinterpret_cast<const int2*>(img + off); };
+  auto i1 = [&](int off) -> const int* { return off < 0 ? nullptr : img + off; };
+  auto seg_of = [&](int b) -> const int* { return img + p->o_seg[b]; };
   const bool fuse = n->fuse_pairs && n->split_f16;
   const bool xt = n->xtile && n->split_f16;
   // split-f16 range flag: zeroed every run (exact-fp32 runs leave it clear), set by the launch that
@@ -4282,9 +4364,21 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
   int* const flag_word = (int*)((char*)workspace + p->ws_flag);
   int* rflag = n->split_f16 ? flag_word : nullptr;
   bool out_checked = false;
-  {
-    const hipError_t ez = hipMemsetAsync(flag_word, 0, sizeof(int), s_main);
-    if (ez != hipSuccess) return hipf(ez, "range flag reset");
+  // timing mode 2: one event pair around the whole run on the caller's stream (after the join)
+  hipEvent_t run_a = nullptr;
+  if (n->timing == 2) {
+    if (!n->pool.empty()) { run_a = n->pool.back(); n->pool.pop_back(); }
+    else if (hipEventCreate(&run_a) != hipSuccess) return fail(PWG_ERR_HIP, "event create");
+    if (hipEventRecord(run_a, s_main) != hipSuccess) return fail(PWG_ERR_HIP, "timing event");
+  }
+  // the plan's device lists, and the flag reset (a kernel: graph replays redo it)
+  for (size_t k = 0; k < p->desc.size(); ++k) {
+    CnDescArgs da = p->desc[k];
+    da.img = img;
+    da.flag = k == 0 ? flag_word : nullptr;
+    hipLaunchKernelGGL(pwg_cnet_desc_kernel, dim3((unsigned)da.n_specs), dim3(256), 0, s_main, da);
+    const hipError_t ez = hipGetLastError();
+    if (ez != hipSuccess) return hipf(ez, "descriptor kernel launch");
   }
   // a conv pair runs fused unless its convs run on the x-tile kernel (measured faster unfused)
   auto pair_fused = [&](const OpPhase& q) { return fuse && q.pair_b >= 0 && !(xt && q.xtile); };
@@ -4295,7 +4389,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
   // the DMA-ring kernel's row ranges: per-block frames and the buffers' rows per frame
   auto xdma_rows = [&](CnXdmaArgs& xd, size_t i) {
     const PwgCnetOp& o = n->ops[n->phases[i].op];
-    xd.bfr = p->d_nfr[i];
+    xd.bfr = i2(p->o_nfr[i]);
     xd.rate[0] = n->rate[o.src[0].buf];
     xd.rate[1] = o.src[1].buf >= 0 && o.kind == PWG_CNET_CONV ? n->rate[o.src[1].buf] : xd.rate[0];
     xd.rate_dst = n->rate[o.dst];
@@ -4321,9 +4415,12 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
   std::unique_lock<std::mutex> lock(n->mu, std::defer_lock);
   if (conc) lock.lock();  // held for the whole enqueue: the aux streams are the handle's
   std::vector<hipEvent_t>* xev_run = nullptr;
+  hipStream_t* aux = nullptr;
   if (conc) {
-    const int ne = sc.n_events + 1;  // + the fork event (s_main after the flag reset)
-    std::vector<hipEvent_t>& xev = p->xev_of[s_main];
+    const int ne = sc.n_events + 1;  // + the fork event (s_main after the descriptor launch)
+    PwgCnet::CallerSet& cs = n->callers[s_main];
+    aux = cs.aux;
+    std::vector<hipEvent_t>& xev = cs.ev;
     xev_run = &xev;
     while ((int)xev.size() < ne) {
       hipEvent_t e = nullptr;
@@ -4331,17 +4428,16 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
       xev.push_back(e);
     }
     for (int k = 1; k < NS; ++k)
-      if (sc.used[k] && !n->aux[k - 1] &&
-          hipStreamCreateWithFlags(&n->aux[k - 1], hipStreamNonBlocking) != hipSuccess)
+      if (sc.used[k] && !aux[k - 1] && hipStreamCreateWithFlags(&aux[k - 1], hipStreamNonBlocking) != hipSuccess)
         return fail(PWG_ERR_HIP, "auxiliary stream create");
     // fork: the aux streams start after everything queued on the caller's stream so far
     hipEvent_t fork = xev[ne - 1];
     if (hipEventRecord(fork, s_main) != hipSuccess) return fail(PWG_ERR_HIP, "fork event");
     for (int k = 1; k < NS; ++k)
-      if (sc.used[k] && hipStreamWaitEvent(n->aux[k - 1], fork, 0) != hipSuccess)
+      if (sc.used[k] && hipStreamWaitEvent(aux[k - 1], fork, 0) != hipSuccess)
         return fail(PWG_ERR_HIP, "fork wait");
   }
-  auto stream_of = [&](int k) { return k == 0 ? s_main : n->aux[k - 1]; };
+  auto stream_of = [&](int k) { return k == 0 ? s_main : aux[k - 1]; };
   for (size_t oi = 0; oi < order.size(); ++oi) {
     const size_t L = order[oi];
     const size_t pi = (size_t)launches[L].first;
@@ -4351,7 +4447,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
     for (int d : l_waits[L])
       if (hipStreamWaitEvent(s, (*xev_run)[l_event[d]], 0) != hipSuccess) return fail(PWG_ERR_HIP, "dependency wait");
     hipEvent_t ea = nullptr, eb = nullptr;
-    if (n->timing) {
+    if (n->timing == 1) {
       for (hipEvent_t* ev : {&ea, &eb}) {
         if (!n->pool.empty()) { *ev = n->pool.back(); n->pool.pop_back(); }
         else if (hipEventCreate(ev) != hipSuccess) return fail(PWG_ERR_HIP, "event create");
@@ -4371,7 +4467,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         a.ld_res = opb.res >= 0 ? n->ld[opb.res] : 0;
         a.y = bufs[opb.dst]; a.seg_y = seg_of(opb.dst); a.ld_y = n->ld[opb.dst];
         a.accumulate = opb.accumulate; a.out_div = opb.out_div; a.post_act = opb.post_act; a.post_slope = opb.post_slope;
-        a.strips = p->d_strips[pi]; a.ncols = p->d_ncols[pi]; a.steps = p->pair_steps * 128 / ph.pair_step;
+        a.strips = i2(p->o_strips[pi]); a.ncols = i1(p->o_ncols[pi]); a.steps = p->pair_steps * 128 / ph.pair_step;
         a.x_min_off = ph.pair_xmin; a.xs = ph.pair_xs;
         a.off1 = -op.src[0].pad; a.dil1 = op.src[0].dilation; a.off2 = -opb.src[0].pad; a.dil2 = opb.src[0].dilation;
         if (!n->pair_attr_set) {
@@ -4416,7 +4512,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         a.ld_res = opb.res >= 0 ? n->ld[opb.res] : 0;
         a.y = bufs[opb.dst]; a.seg_y = seg_of(opb.dst); a.ld_y = n->ld[opb.dst]; a.M = opb.out_channels;
         a.accumulate = opb.accumulate; a.out_div = opb.out_div; a.post_act = opb.post_act; a.post_slope = opb.post_slope;
-        a.blocks = xs_on ? p->d_xblocks[pi] : p->d_blocks[pi]; a.ncols = p->d_ncols[pi];
+        a.blocks = xs_on ? i2(p->o_xblocks[pi]) : i2(p->o_blocks[pi]); a.ncols = i1(p->o_ncols[pi]);
         a.mean = mean; a.scale = scale;
         if (xs_on) {
           CnXstackArgs xs;
@@ -4455,7 +4551,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
       CnPqmfArgs a;
       a.x = bufs[op.src[0].buf]; a.seg_src = seg_of(op.src[0].buf); a.ld_src = n->ld[op.src[0].buf];
       a.h = packed + ph.frag_off; a.y = bufs[op.dst]; a.seg_dst = seg_of(op.dst); a.ld_dst = n->ld[op.dst];
-      a.blocks = p->d_blocks[pi]; a.S = op.stride; a.NT = op.padding;
+      a.blocks = i2(p->o_blocks[pi]); a.S = op.stride; a.NT = op.padding;
       a.range_flag = op.dst == nb - 1 ? rflag : nullptr;
       out_checked |= op.dst == nb - 1;
       hipLaunchKernelGGL(pwg_cnet_pqmf_kernel, dim3((unsigned)p->n_blocks[pi]), dim3(256), 0, s, a);
@@ -4485,7 +4581,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
       a.ld_res = op.res >= 0 ? n->ld[op.res] : 0;
       a.y = bufs[op.dst]; a.seg_dst = seg_of(op.dst); a.ld_dst = n->ld[op.dst]; a.M = op.out_channels;
       a.accumulate = op.accumulate; a.out_div = op.out_div; a.post_act = op.post_act; a.post_slope = op.post_slope;
-      a.blocks = p->d_blocks[pi]; a.ncols = p->d_ncols[pi]; a.ostride = ph.ostride; a.ophase = ph.ophase;
+      a.blocks = i2(p->o_blocks[pi]); a.ncols = i1(p->o_ncols[pi]); a.ostride = ph.ostride; a.ophase = ph.ophase;
       a.mean = mean; a.scale = scale;
       for (int r = 0; r < 8; ++r) {
         const OpPhase& q = n->phases[pi + (r < ph.z_phases ? r : 0)];
@@ -4529,7 +4625,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         a.ld_res = opb.res >= 0 ? n->ld[opb.res] : 0;
         a.y = bufs[opb.dst]; a.seg_dst = seg_of(opb.dst); a.ld_dst = n->ld[opb.dst]; a.M = opb.out_channels;
         a.accumulate = opb.accumulate; a.out_div = opb.out_div; a.post_act = opb.post_act; a.post_slope = opb.post_slope;
-        a.blocks = p->d_xblocks[pi];
+        a.blocks = i2(p->o_xblocks[pi]);
         if (p->n_xblocks[pi] > 0) {
           const hipError_t ea2 = xpair_launch(ph.MT, xp.K1, dim3((unsigned)p->n_xblocks[pi]), ph.xpair_lds, s, a, xp);
           if (ea2 != hipSuccess) return hipf(ea2, "xpair kernel launch");
@@ -4546,14 +4642,14 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         dim3 xgrid = grid;
         // stack op A / wide ConvTranspose: 128-column d_blocks belong to the tap-major kernels
         if (ph.stack_b >= 0 || ph.xt_convt_db) {
-          a.blocks = p->d_xblocks[pi];
+          a.blocks = i2(p->o_xblocks[pi]);
           xgrid.x = (unsigned)p->n_xblocks[pi];
         }
         hipError_t ea2;
         if (narrow(pi)) {
           const int nw = p->nar_nwv[pi], mtn = p->nar_mt[pi];
           xt.span = 32 * nw + (xt.K - 1) * xt.dil;
-          a.blocks = p->d_nblocks[pi];
+          a.blocks = i2(p->o_nblocks[pi]);
           const dim3 ngrid((unsigned)p->n_nblocks[pi], (unsigned)(ph.mt_total / mtn), (unsigned)ph.z_phases);
           if (p->n_nblocks[pi] == 0) {
             ea2 = hipSuccess;
@@ -4576,7 +4672,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         }
         if (ea2 != hipSuccess) return hipf(ea2, "xtile kernel launch");
       } else if (split && narrow_tap(pi)) {
-        a.blocks = p->d_nblocks[pi];
+        a.blocks = i2(p->o_nblocks[pi]);
         const int nw = p->nar_nwv[pi], mtn = p->nar_mt[pi];
         const dim3 ngrid((unsigned)p->n_nblocks[pi], (unsigned)(ph.mt_total / mtn), (unsigned)ph.z_phases);
         if (p->nar_xdma[pi]) {
@@ -4635,7 +4731,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hipf(e, "cnet op launch");
-    if (n->timing) {
+    if (n->timing == 1) {
       (void)hipEventRecord(eb, s);
       n->records.push_back({ph.op, ea, eb});
     }
@@ -4657,6 +4753,13 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
     hipLaunchKernelGGL(pwg_cnet_finite_kernel, dim3((unsigned)nblk), dim3(256), 0, s, (const float*)out, cnt, rflag);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hipf(e, "output range check launch");
+  }
+  if (run_a != nullptr) {
+    hipEvent_t run_b = nullptr;
+    if (!n->pool.empty()) { run_b = n->pool.back(); n->pool.pop_back(); }
+    else if (hipEventCreate(&run_b) != hipSuccess) return fail(PWG_ERR_HIP, "event create");
+    if (hipEventRecord(run_b, s) != hipSuccess) return fail(PWG_ERR_HIP, "timing event");
+    n->records.push_back({-1, run_a, run_b});
   }
   return PWG_OK;
 }
@@ -4724,7 +4827,8 @@ int pwg_cnet_set_option(PwgCnet* n, int option, long long value) {
 
 int pwg_cnet_set_timing(PwgCnet* n, int enable) {
   if (!n) return fail(PWG_ERR_INVALID, "null handle");
-  n->timing = enable != 0;
+  if (enable < 0 || enable > 2) return fail(PWG_ERR_INVALID, "timing mode must be 0, 1 or 2");
+  n->timing = enable;
   return PWG_OK;
 }
 
@@ -4736,12 +4840,36 @@ int pwg_cnet_timing_collect(PwgCnet* n, double* ms, long long* launches) {
     float t = 0.f;
     if (e == hipSuccess) e = hipEventElapsedTime(&t, r.a, r.b);
     if (e != hipSuccess) return hipf(e, "cnet timing");
-    ms[r.op] += t;
-    launches[r.op] += 1;
+    if (r.op >= 0) {  // (-1: a whole-run span record of timing mode 2)
+      ms[r.op] += t;
+      launches[r.op] += 1;
+    }
     n->pool.push_back(r.a);
     n->pool.push_back(r.b);
   }
   n->records.clear();
+  return PWG_OK;
+}
+
+int pwg_cnet_timing_span(PwgCnet* n, double* span_ms) {
+  if (!n || !span_ms) return fail(PWG_ERR_INVALID, "null argument");
+  *span_ms = 0.0;
+  if (n->records.empty()) return PWG_OK;
+  Guard g(n->device);
+  // every launch of a run starts after the first one's start event (the auxiliary streams' launches
+  // all depend on some earlier launch), so offsets from it are >= 0
+  hipEvent_t ref = n->records[0].a;
+  double lo = 0.0, hi = 0.0;
+  for (auto& r : n->records) {
+    hipError_t e = hipEventSynchronize(r.b);
+    float ta = 0.f, tb = 0.f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&ta, ref, r.a);
+    if (e == hipSuccess) e = hipEventElapsedTime(&tb, ref, r.b);
+    if (e != hipSuccess) return hipf(e, "cnet timing span");
+    lo = std::min(lo, (double)ta);
+    hi = std::max(hi, (double)tb);
+  }
+  *span_ms = hi - lo;
   return PWG_OK;
 }
 

@@ -390,6 +390,13 @@ class Engine:
         self.timing_enabled = bool(enable)
         _lib.check(self._lib.pwg_set_timing(self._h, int(enable)))
 
+    def timing_span(self):
+        """pwg_timing_span: device ms from the first timed launch's start to the last one's end
+        (gaps included); call before collect_timing."""
+        v = ctypes.c_double()
+        _lib.check(self._lib.pwg_timing_span(self._h, ctypes.byref(v)))
+        return v.value
+
     def collect_timing(self):
         ms = (ctypes.c_double * len(_lib.KERNEL_BUCKETS))()
         n = (ctypes.c_longlong * len(_lib.KERNEL_BUCKETS))()
@@ -407,6 +414,7 @@ class Engine:
         ``run_status``)."""
         if stream is None:
             stream = torch.cuda.current_stream(self.device)
+        self._sync_tick()
         self._enqueue(plan, mel, noise, out, mean, scale, stream)
         if check:
             self._range_check(plan, mel, noise, out, mean, scale, stream)
@@ -450,8 +458,9 @@ class Engine:
             _lib.check(self._lib.pwg_set_option(self._h, _lib.PWG_OPT_SYNC, 0))
 
     def _sync_tick(self):
-        """Called per enqueued run: restore the synchronised forward after a suspension. One more
-        failure then suspends it again at once."""
+        """Called once per forward a caller asks for (run / infer), never from inside a rerun
+        (_enqueue_per_layer saves and restores PWG_OPT_SYNC around its own enqueue): restore the
+        synchronised forward after a suspension. One more failure then suspends it again at once."""
         if self._sync_saved is None:
             return
         self._sync_retry_in -= 1
@@ -503,7 +512,6 @@ class Engine:
             scale = scale.to(self.device, torch.float32).contiguous()
             mp, sp = mean.data_ptr(), scale.data_ptr()
         ws = self.workspace(plan.workspace_bytes, stream)
-        self._sync_tick()
         _lib.check(
             self._lib.pwg_run(
                 plan._p,
@@ -538,6 +546,7 @@ class Engine:
             self.run(plan, mel, noise, out, mean, scale)
         else:
             stream = torch.cuda.current_stream(self.device)
+            self._sync_tick()
             self._enqueue(plan, mel, noise, out, mean, scale, stream)
             if refresh():  # the weights changed under the enqueued forward: redo it on the new image
                 self._enqueue(plan, mel, noise, out, mean, scale, stream)

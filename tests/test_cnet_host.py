@@ -232,3 +232,36 @@ def test_concurrent_schedule_host_only(built_lib):
     eng.set_streams(1)
     big, order_big = eng.schedule(eng.plan([4000] * 8))
     assert {st for _, st in big} == {0} and order_big == list(range(len(big)))
+
+
+@pytest.mark.parametrize("name", ["hifigan_v1", "mb_melgan_v2"])
+def test_plan_image_is_host_built_and_cheap(name, built_lib):
+    """Plans are host objects (include/pwg_cnet.h): their device lists are an image the descriptor
+    kernel writes into the workspace every run. The host image has the segment lists of every
+    buffer rate (first row, rows per utterance, back to back) and stays small for B = 1; building a
+    plan for 32 distinct lengths (the reference's decode loop, bin/decode.py:236-268) costs host time
+    only, well under a millisecond per plan."""
+    import time
+
+    from parallelwavegan_amd.cnet import CnetEngine
+
+    m = _holder(name)
+    if isinstance(m, MelGANGenerator):
+        m.pqmf = PQMF(m.out_channels)
+        P, _ = m.program(True)
+    else:
+        P = m.program()
+    eng = CnetEngine(P, None, host_only=True)
+    frames = [9, 130, 17]
+    plan = eng.plan(frames)
+    off, img = plan.image()
+    assert off % 256 == 0 and off + 4 * img.size <= plan.workspace_bytes
+    # the first list is buffer 0's segments (rate 1: frames)
+    np.testing.assert_array_equal(img[:6], [0, 9, 9, 130, 139, 17])
+    lens = np.random.RandomState(3).randint(80, 1200, 32)
+    t0 = time.perf_counter()
+    for f in lens:
+        p = CnetEngine.plan(eng, [int(f)])
+        assert p.image()[1].size < 64 * 1024
+    per_plan_ms = (time.perf_counter() - t0) * 1e3 / len(lens)
+    assert per_plan_ms < 5.0, per_plan_ms

@@ -466,3 +466,73 @@ def test_graph_replay_bitwise_equal(cfg, built_lib, cuda_device):
     for a, b in zip(got, [ref[0], ref[1], ref[0], ref[1]]):
         np.testing.assert_array_equal(a, b)
 
+
+
+@pytest.mark.parametrize("cfg", ["hifigan_v1", "mb_melgan_v2", "hifigan_v1_causal"])
+def test_descriptor_kernel_writes_the_host_image(cfg, built_lib, cuda_device):
+    """Plans are host objects: every pwg_cnet_run starts with pwg_cnet_desc_kernel, which writes the
+    plan's device lists into the workspace from the utterance lengths in its arguments. The image
+    it writes is the one the host built and checked (pwg_cnet_plan_image), byte for byte, for a
+    B = 1 plan, a ragged batch and a batch of more utterances than one descriptor launch holds
+    (CN_DESC_UTTS = 64); a workspace full of garbage beforehand changes nothing."""
+    from parallelwavegan_amd import configs, synthetic
+    from parallelwavegan_amd.hifigan import HiFiGANGenerator
+    from parallelwavegan_amd.melgan import PQMF, MelGANGenerator
+
+    cls_name, params = configs.vocoder_params(cfg)
+    m = {"MelGANGenerator": MelGANGenerator, "HiFiGANGenerator": HiFiGANGenerator}[cls_name](**params)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic.make_module_state_dict(m, seed=21).items()})
+    if cfg in configs.VOCODER_PQMF:
+        m.pqmf = PQMF(**configs.VOCODER_PQMF[cfg])
+    m = m.to(cuda_device)
+    eng = m.engine()
+    rs = np.random.RandomState(5)
+    with torch.no_grad():
+        for frames in ([37], [9, 130, 17, 64], [int(f) for f in rs.randint(8, 24, 70)]):
+            plan = eng.plan(frames)
+            mel = torch.from_numpy(rs.standard_normal((sum(frames), 80)).astype(np.float32)).to(cuda_device)
+            out = torch.empty(plan.out_rows * eng.out_channels, device=cuda_device)
+            ws = torch.full((plan.workspace_bytes,), 0xA5, dtype=torch.uint8, device=cuda_device)
+            eng._enqueue(plan, mel.reshape(-1), out, None, None, torch.cuda.current_stream(), ws=ws)
+            torch.cuda.synchronize()
+            off, img = plan.image()
+            dev = ws[off:off + 4 * img.size].cpu().numpy().view(np.int32)
+            np.testing.assert_array_equal(dev, img)
+            assert np.isfinite(out.cpu().numpy()).all()
+
+
+@pytest.mark.parametrize("cfg", ["hifigan_v1", "mb_melgan_v2"])
+def test_distinct_length_decode_loop(cfg, built_lib, cuda_device):
+    """The reference's decode loop (bin/decode.py:236-268): one inference() per utterance, each with
+    its own length. Every call builds a new plan on the host; no graph is captured for a plan used
+    once, a repeated length is captured and replayed; every output is bit-identical to the same
+    utterance decoded with graphs off, and to its slice of one ragged batch."""
+    from parallelwavegan_amd import configs, synthetic
+    from parallelwavegan_amd.hifigan import HiFiGANGenerator
+    from parallelwavegan_amd.melgan import PQMF, MelGANGenerator
+
+    cls_name, params = configs.vocoder_params(cfg)
+    m = {"MelGANGenerator": MelGANGenerator, "HiFiGANGenerator": HiFiGANGenerator}[cls_name](**params)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic.make_module_state_dict(m, seed=22).items()})
+    if cfg in configs.VOCODER_PQMF:
+        m.pqmf = PQMF(**configs.VOCODER_PQMF[cfg])
+    m = m.to(cuda_device)
+    eng = m.engine()
+    lengths = [int(f) for f in np.random.RandomState(3).randint(16, 160, 10)]
+    mels = [torch.from_numpy(synthetic.make_mel(f, 80, seed=300 + i)).to(cuda_device) for i, f in enumerate(lengths)]
+    with torch.no_grad():
+        got = [m.inference(x).cpu().numpy() for x in mels]
+        assert len(eng._graphs) == 0
+        again = m.inference(mels[0]).cpu().numpy()  # second run of that plan: captured (HiFiGAN)
+        third = m.inference(mels[0]).cpu().numpy()  # replayed
+        n_graphs = len(eng._graphs)
+        eng.set_graphs(False)
+        ref = [m.inference(x).cpu().numpy() for x in mels]
+        eng.set_graphs(True)
+        batch = [y.cpu().numpy() for y in m.inference_batch([x.cpu().numpy() for x in mels])]
+    assert n_graphs == (1 if cls_name == "HiFiGANGenerator" else 0)
+    for a, b, c in zip(got, ref, batch):
+        np.testing.assert_array_equal(a, b)
+        np.testing.assert_array_equal(a, c)
+    np.testing.assert_array_equal(again, ref[0])
+    np.testing.assert_array_equal(third, ref[0])
