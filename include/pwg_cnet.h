@@ -165,10 +165,17 @@ PWG_API int pwg_cnet_plan_schedule(PwgCnetPlan* p, int cap, int* n_launches, int
  * residual blocks, models/hifigan.py:159-168) run concurrently on up to 3 auxiliary streams of the
  * handle, forked from and joined back into the caller's stream with events (graph-capturable):
  * 1 for plans with narrow launches (latency-bound small plans), 2 for every plan, 0 never.
- * The accumulated sum's writers stay in program order: bit-identical to one stream. */
+ * The accumulated sum's writers stay in program order: bit-identical to one stream.
+ * PWG_CNET_OPT_MSTACK (default 1, plans created afterwards, split-f16 x-tile mode with fused ops): a
+ * chain of up to 4 ResidualStacks of one MelGAN stage (layers/residual_stack.py:75-85; k = 3 conv +
+ * two-source 1x1 each, zero or reflect "same" padding, 32-128 channels) runs as ONE launch: each
+ * workgroup takes a block of output columns through every stack with the input tile (+- the summed
+ * dilations, recomputed by neighbouring blocks) in LDS and h in registers, instead of two launches per
+ * stack. 1: when the chain's first conv runs narrow (small plans); 2: every such chain; 0 never.
+ * Bit-identical to the unfused launches. */
 enum { PWG_CNET_OPT_SPLIT_F16 = 0, PWG_CNET_OPT_FUSE_PAIRS = 1, PWG_CNET_OPT_PAIR_STEPS = 2, PWG_CNET_OPT_XTILE = 3,
        PWG_CNET_OPT_XT_DMA = 4, PWG_CNET_OPT_XCD_ORDER = 5, PWG_CNET_OPT_NARROW = 6, PWG_CNET_OPT_NARROW_DMA = 7,
-       PWG_CNET_OPT_STREAMS = 8 };
+       PWG_CNET_OPT_STREAMS = 8, PWG_CNET_OPT_MSTACK = 9 };
 PWG_API int pwg_cnet_set_option(PwgCnet* n, int option, long long value);
 /* Timing: 0 off, 1 HIP events around every launch (per-bucket / per-op sums), 2 one event pair
  * around each whole run on the caller's stream (its device span only; no events between launches,

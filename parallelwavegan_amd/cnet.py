@@ -560,6 +560,14 @@ class CnetEngine:
         _lib.check(self._lib.pwg_cnet_set_option(self._h, 8, int(mode)))
         self._graph_epoch += 1
 
+    def set_mstack(self, mode):
+        """pwg_cnet_set_option(PWG_CNET_OPT_MSTACK): a MelGAN stage's chain of ResidualStacks as one
+        launch (pwg_mstack.hip): 1 (default) when the chain's first conv runs narrow, 2 every chain,
+        0 never. Plan-time (cached plans are dropped); bit-identical."""
+        _lib.check(self._lib.pwg_cnet_set_option(self._h, 9, int(mode)))
+        self._graph_epoch += 1
+        self._plans.clear()
+
     def set_narrow_dma(self, enable):
         """pwg_cnet_set_option(PWG_CNET_OPT_NARROW_DMA): narrow launches on the DMA-ring kernel
         (default) or, 0, on the narrow x-tile / tap-major kernels. Plan-time (cached plans are

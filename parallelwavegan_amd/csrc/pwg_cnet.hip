@@ -3222,6 +3222,8 @@ struct OpPhase {          // one launch
   int xstack_lds = 0;         // > 0: with x-tile on, the stack runs pwg_cnet_xstack_kernel (256-column blocks)
   int xstack_g2 = 0;          // its stage-2 chunks per staged group
   int xstack_xoff = 0;        // its input-row / h-tile region offset
+  int ms_n = 0;               // > 0: head of a chain of this many fusable ResidualStacks (pwg_mstack.hip)
+  int ms_halo = 0;            // ... their summed dilations
 };
 
 }  // namespace
@@ -3240,6 +3242,8 @@ struct PwgCnet {
   int narrow = 1;      // PWG_CNET_OPT_NARROW (plan time): 0 off, 1 small launches, 2 every x-tile phase
   int narrow_dma = 1;  // PWG_CNET_OPT_NARROW_DMA: narrow launches on the DMA-ring kernel (0: the narrow
                        // x-tile / tap-major kernels)
+  int mstack = 1;      // PWG_CNET_OPT_MSTACK (plan time): 0 off, 1 fused stack chains in plans whose first
+                       // conv of the chain runs narrow, 2 every chain
   int streams = 1;     // PWG_CNET_OPT_STREAMS: 0 one stream, 1 independent launches of plans with narrow
                        // launches run on auxiliary streams, 2 every plan
   static constexpr int N_AUX = 3;
@@ -3297,6 +3301,8 @@ struct PwgCnetPlan {
   std::vector<char> nar_xdma;                // ... on the DMA-ring kernel (tap-major phases: K = 1 mode)
   std::vector<int> o_nblocks;                // its blocks (utt, q0 step 32 nar_nwv)
   std::vector<int> o_nfr;                    // ... and their utterances' (first frame, frames)
+  // per phase: fused stack chain launch (pwg_mstack.hip) when > 0 output columns per block
+  std::vector<int> ms_oc, o_msblocks, n_msblocks;
   bool has_narrow = false;                   // some phase runs narrow (PWG_CNET_OPT_STREAMS 1)
 };
 
@@ -3357,6 +3363,12 @@ struct CnSchedule {
   bool used[1 + PwgCnet::N_AUX] = {true, false, false, false};
   int n_events = 0;
 };
+// phase pi heads a fused stack chain this run launches as one pwg_mstack_kernel (split-f16 x-tile
+// mode with fused ops, and the plan picked a block width for it)
+bool cnet_mstack_on(const PwgCnetPlan* p, size_t pi) {
+  const PwgCnet* n = p->n;
+  return n->split_f16 && n->xtile && n->fuse_pairs && pi < p->ms_oc.size() && p->ms_oc[pi] > 0;
+}
 int cnet_schedule(PwgCnetPlan* p, CnSchedule& sc) {
   PwgCnet* n = p->n;
   const int nb = (int)n->channels.size();
@@ -3364,9 +3376,15 @@ int cnet_schedule(PwgCnetPlan* p, CnSchedule& sc) {
   const bool xt = n->xtile && n->split_f16;
   auto pair_fused = [&](const OpPhase& q) { return fuse && q.pair_b >= 0 && !(xt && q.xtile); };
   auto narrow = [&](size_t i) { return xt && p->nar_nwv[i] > 0 && !p->nar_tap[i]; };
+  // phases inside a fused stack chain (pwg_mstack.hip) that runs as its head's launch
+  std::vector<char> in_chain(n->phases.size(), 0);
+  for (size_t pi = 0; pi < n->phases.size(); ++pi)
+    if (cnet_mstack_on(p, pi))
+      for (int k = 1; k < 2 * n->phases[pi].ms_n; ++k) in_chain[pi + k] = 1;
   // the launches of this run: (phase, second op fused into it or -1)
   auto skipped = [&](size_t pi) {
     const OpPhase& ph = n->phases[pi];
+    if (in_chain[pi]) return true;
     return (pi > 0 && ((pair_fused(n->phases[pi - 1]) && n->phases[pi - 1].pair_b == (int)pi) ||
                        (fuse && n->phases[pi - 1].stack_b == (int)pi && !narrow(pi - 1)))) ||
            ph.z_phases == 0 || (xt && fuse && pi > 0 && n->phases[pi - 1].xpair_b == (int)pi && !narrow(pi - 1));
@@ -3376,7 +3394,8 @@ int cnet_schedule(PwgCnetPlan* p, CnSchedule& sc) {
     if (skipped(pi)) continue;
     const OpPhase& ph = n->phases[pi];
     int second = -1;
-    if (pair_fused(ph)) second = n->phases[ph.pair_b].op;
+    if (cnet_mstack_on(p, pi)) second = n->phases[pi + 2 * ph.ms_n - 1].op;  // the chain's output op
+    else if (pair_fused(ph)) second = n->phases[ph.pair_b].op;
     else if (fuse && ph.stack_b >= 0 && !narrow(pi)) second = n->phases[ph.stack_b].op;
     else if (xt && fuse && ph.xpair_b >= 0 && !narrow(pi)) second = n->phases[ph.xpair_b].op;
     launches.push_back({(int)pi, second});
@@ -3911,6 +3930,70 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
       ph.xt_lds = 6 * 4 * 2048 + span * XT_ROWB;
     }
   }
+  // Fused residual-stack chains (pwg_mstack.hip, PWG_CNET_OPT_MSTACK): runs of ResidualStacks, each
+  // conv A (single-source k = 3 x-tile conv, "same" padding pad = dilation, zero or reflect edges, no
+  // epilogue extras) followed by its two-source 1x1 B over [h; x] (B's x source not pre-activated),
+  // C a multiple of 16 with every fragment image at C / 32 rounded-up m-tiles, h and every
+  // intermediate x read by nobody else, the next stack's conv reading this stack's output.
+  auto only_readers = [&](int buf, int op_a, int op_b, int writer) {
+    for (int k = 0; k < n_ops; ++k) {
+      if (k == op_a || k == op_b || k == writer) continue;
+      const PwgCnetOp& o2 = n->ops[k];
+      if (o2.src[0].buf == buf || o2.src[1].buf == buf || o2.res == buf || o2.dst == buf) return false;
+    }
+    return true;
+  };
+  auto stack_ok = [&](size_t i) {
+    if (i + 1 >= n->phases.size()) return false;
+    const OpPhase& pa = n->phases[i];
+    const OpPhase& pb = n->phases[i + 1];
+    if (pb.op != pa.op + 1 || !pa.xtile || pa.thin || pb.thin || pa.z_phases != 1 || pb.z_phases != 1) return false;
+    const PwgCnetOp& A = n->ops[pa.op];
+    const PwgCnetOp& B = n->ops[pb.op];
+    const PwgCnetSrc& a0 = A.src[0];
+    const int C = A.out_channels, cs = C / 16, mt = (cs + 1) / 2;
+    if (A.kind != PWG_CNET_CONV || B.kind != PWG_CNET_CONV || A.src[1].buf >= 0 || C % 16 != 0 ||
+        !mstack_supported(cs, 1))
+      return false;
+    if (a0.taps != 3 || a0.pad != a0.dilation || a0.channels != C || a0.normalize ||
+        (a0.pad_mode != PWG_PAD_ZERO && a0.pad_mode != PWG_PAD_REFLECT))
+      return false;
+    if (A.res >= 0 || A.accumulate || A.out_div != 1.f || A.post_act != PWG_ACT_NONE) return false;
+    const PwgCnetSrc& b0 = B.src[0];
+    const PwgCnetSrc& b1 = B.src[1];
+    if (b0.buf != A.dst || b1.buf != a0.buf || b0.taps != 1 || b1.taps != 1 || b0.pad != 0 || b1.pad != 0 ||
+        b0.channels != C || b1.channels != C || B.out_channels != C || b0.normalize || b1.normalize ||
+        b1.pre_slope != 1.f)
+      return false;
+    if (B.res >= 0 || B.accumulate || B.out_div != 1.f || B.post_act != PWG_ACT_NONE) return false;
+    if (n->ld[a0.buf] != C || n->ld[A.dst] != C || n->ld[B.dst] != C || B.dst == n_bufs - 1) return false;
+    if (pa.mt_total != mt || pb.mt_total != mt || (int)pb.chunks.size() != 2 * cs) return false;
+    for (int c = 0; c < 2 * cs; ++c)  // [h blocks][x blocks], the kernel's fixed chunk order
+      if (pb.chunks[c].src != (c >= cs) || pb.chunks[c].c0 != 16 * (c % cs) || pb.chunks[c].row_off != 0) return false;
+    return only_readers(A.dst, pa.op, pb.op, pa.op);
+  };
+  for (size_t i = 0; i < n->phases.size();) {
+    if (!stack_ok(i)) {
+      ++i;
+      continue;
+    }
+    const int C = n->ops[n->phases[i].op].out_channels;
+    int k = 1;  // stacks in the chain
+    while (k < MS_MAX && stack_ok(i + 2 * k)) {
+      const PwgCnetOp& prevB = n->ops[n->phases[i + 2 * k - 1].op];
+      const PwgCnetOp& nextA = n->ops[n->phases[i + 2 * k].op];
+      if (nextA.src[0].buf != prevB.dst || nextA.out_channels != C ||
+          !only_readers(prevB.dst, n->phases[i + 2 * k].op, n->phases[i + 2 * k + 1].op,
+                        n->phases[i + 2 * k - 1].op))
+        break;
+      ++k;
+    }
+    OpPhase& head = n->phases[i];
+    head.ms_n = k;
+    head.ms_halo = 0;
+    for (int s = 0; s < k; ++s) head.ms_halo += n->ops[n->phases[i + 2 * s].op].src[0].dilation;
+    i += 2 * k;
+  }
   *out = n;  // device tables are uploaded by the first plan: packing needs no GPU
   return PWG_OK;
 }
@@ -4240,6 +4323,26 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
     p->o_nfr.push_back(pick_w > 0 ? list(CN_L_NFR, rate, os, oph, 32 * pick_w) : -1);
     p->n_nblocks.push_back(pick_w > 0 ? (int)count(32 * pick_w) : 0);
   }
+  // fused stack chains (PWG_CNET_OPT_MSTACK): the widest block (a multiple of 32 columns, at most
+  // 128) whose first stack's output -- the block plus the later stacks' halos -- is at most one
+  // 32-column tile per wave and whose tile, ring and biases fit the LDS
+  p->ms_oc.assign(nph, 0);
+  p->o_msblocks.assign(nph, -1);
+  p->n_msblocks.assign(nph, 0);
+  for (size_t pi = 0; pi < nph; ++pi) {
+    const OpPhase& ph = n->phases[pi];
+    if (ph.ms_n == 0 || n->mstack == 0 || (n->mstack == 1 && p->nar_nwv[pi] == 0)) continue;
+    const PwgCnetOp& A = n->ops[ph.op];
+    const int cs = A.out_channels / 16, d0 = A.src[0].dilation, rate = n->rate[A.dst];
+    int oc = 0;
+    for (int o = 32; o <= 128; o += 32)
+      if ((o + 2 * (ph.ms_halo - d0) + 31) / 32 <= 4 && mstack_lds(cs, o, ph.ms_halo, ph.ms_n) <= PR_MAX_LDS) oc = o;
+    if (oc == 0) continue;
+    for (int u = 0; u < n_utts; ++u) ncols[u] = (int)(frames[u] * rate);
+    p->ms_oc[pi] = oc;
+    p->o_msblocks[pi] = list(CN_L_BLK, rate, 1, 0, oc);
+    p->n_msblocks[pi] = (int)count(oc);
+  }
   for (size_t pi = 0; pi < nph; ++pi) p->has_narrow |= p->nar_nwv[pi] > 0;
   if (n->streams == 2 || (n->streams == 1 && p->has_narrow)) assign_slots(false);
   img_ints = (img_ints + 1) / 2 * 2;  // room for a last odd NCOL list's pad int
@@ -4454,7 +4557,30 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
       }
       (void)hipEventRecord(ea, s);
     }
-    if (pair_fused(ph)) {
+    if (cnet_mstack_on(p, pi)) {
+      // a fused chain of ph.ms_n ResidualStacks (phases pi .. pi + 2 ms_n - 1) in one launch
+      const PwgCnetOp& Bn = n->ops[n->phases[pi + 2 * ph.ms_n - 1].op];
+      MstackArgs ma;
+      ma.x = bufs[op.src[0].buf]; ma.seg_x = seg_of(op.src[0].buf);
+      ma.y = bufs[Bn.dst]; ma.seg_y = seg_of(Bn.dst); ma.ld = n->ld[Bn.dst];
+      ma.blocks = i2(p->o_msblocks[pi]); ma.ns = ph.ms_n; ma.oc = p->ms_oc[pi]; ma.halo = ph.ms_halo;
+      for (int k = 0; k < MS_MAX; ++k) {
+        const int kk = k < ph.ms_n ? k : 0;  // (unused entries: copies of the first)
+        const OpPhase& pa = n->phases[pi + 2 * kk];
+        const OpPhase& pb = n->phases[pi + 2 * kk + 1];
+        const PwgCnetOp& A = n->ops[pa.op];
+        const PwgCnetOp& B = n->ops[pb.op];
+        MsStack& st = ma.st[k];
+        st.wA = packed + pa.frag16_off; st.bA = packed + pa.bias_off;
+        st.wB = packed + pb.frag16_off; st.bB = packed + pb.bias_off;
+        st.dil = A.src[0].dilation; st.pad = A.src[0].pad; st.mode = A.src[0].pad_mode;
+        st.slopeA = A.src[0].pre_slope; st.slopeH = B.src[0].pre_slope;
+      }
+      if (p->n_msblocks[pi] > 0) {
+        const hipError_t ea2 = launch_mstack(ma, op.out_channels / 16, 1, p->n_msblocks[pi], s);
+        if (ea2 != hipSuccess) return hipf(ea2, "fused stack chain launch");
+      }
+    } else if (pair_fused(ph)) {
       if (p->n_strips[pi] > 0) {
         const OpPhase& pb = n->phases[ph.pair_b];
         const PwgCnetOp& opb = n->ops[pb.op];
@@ -4813,6 +4939,11 @@ int pwg_cnet_set_option(PwgCnet* n, int option, long long value) {
               : option == PWG_CNET_OPT_XCD_ORDER  ? &n->xcd_order
               : option == PWG_CNET_OPT_NARROW_DMA ? &n->narrow_dma
                                                   : nullptr;
+  if (option == PWG_CNET_OPT_MSTACK) {
+    if (value < 0 || value > 2) return fail(PWG_ERR_INVALID, "mstack must be 0, 1 or 2");
+    n->mstack = (int)value;
+    return PWG_OK;
+  }
   if (option == PWG_CNET_OPT_STREAMS) {
     if (value < 0 || value > 2) return fail(PWG_ERR_INVALID, "streams must be 0, 1 or 2");
     n->streams = (int)value;

@@ -307,6 +307,36 @@ __device__ __forceinline__ void stage_lds(V* dst, const V* src, int n, int tid, 
   for (; i < n; i += nthr) dst[i] = src[i];
 }
 
+// Fused residual-stack chain of a MelGAN stage (pwg_mstack.hip, the conv-network executor's B = 1
+// path): NS consecutive ResidualStacks (layers/residual_stack.py:75-85) -- per stack a dilated
+// k = 3 conv h = W_A * lrelu(x) + b_A and the two-source 1x1 x' = W_1 lrelu(h) + W_s x + b -- for
+// one block of output columns in ONE workgroup, the input tile (columns +- the stacks' summed
+// dilations, recomputed by neighbouring blocks) kept in LDS between stacks, h in registers.
+constexpr int MS_MAX = 4;         // stacks per fused launch
+struct MsStack {
+  const float* wA;                // conv A split-f16 fragments [tap * cs + cb][MT][hi/lo][lane][4]
+  const float* bA;                // conv A bias (C floats)
+  const float* wB;                // 1x1 split-f16 fragments [chunk][MT][hi/lo][lane][4], chunks
+                                  // [h cb 0 .. cs-1][x cb 0 .. cs-1] (the executor's chunk order)
+  const float* bB;                // 1x1 bias (both biases summed)
+  int dil, pad, mode;             // conv A: dilation, pad (tap t reads column c - pad + t dil), edge mode
+  float slopeA, slopeH;           // LeakyReLU slope of conv A's input and of h
+};
+struct MstackArgs {
+  const float* x;                 // stage input (stack 0's x), [rows][ld]
+  const int* seg_x;               // [n_utts][2] (first row, rows)
+  float* y;                       // the last stack's output, [rows][ld]
+  const int* seg_y;
+  int ld;                         // row stride of x and y (floats)
+  const int2* blocks;             // (utterance, q0): oc output columns each
+  int ns, oc, halo;               // stacks, output columns per block, summed dilations
+  MsStack st[MS_MAX];
+};
+// cs: 16-channel blocks (2, 3, 4, 6, 8); tpw: column tiles per wave (1, 2). LDS bytes of a launch:
+int mstack_lds(int cs, int oc, int halo, int ns);
+bool mstack_supported(int cs, int tpw);
+hipError_t launch_mstack(const MstackArgs& a, int cs, int tpw, int n_blocks, hipStream_t s);
+
 // Run status bits (the per-run word pwg_run_status reads, and the handle's sticky copy).
 constexpr int PWG_STATUS_RANGE = 1;         // a value left the fp16 pair range: rerun in exact fp32
 constexpr int PWG_STATUS_PIPE_TIMEOUT = 2;  // layer pipeline: a dependency wait gave up

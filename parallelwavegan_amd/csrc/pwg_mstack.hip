@@ -1,0 +1,370 @@
+// Fused residual-stack chain of one MelGAN / multi-band MelGAN upsampling stage (split-f16 MFMA,
+// gfx950): the conv-network executor's B = 1 path for MelGANGenerator's ResidualStacks
+// (layers/residual_stack.py:75-85, models/melgan.py:117-130).
+//
+// A stage ends with NS ResidualStacks on C channels; stack j computes
+//   h     = W_A * lrelu(x_j)  + b_A      (k = 3, dilation d_j, ReflectionPad1d(d_j) or zero pad)
+//   x_j+1 = W_1 lrelu(h) + W_s x_j + b    (the stack's 1x1 and skip_layer as ONE two-source op)
+// The executor runs each of those as its own launch (2 NS dependent launches per stage, each a few
+// dozen workgroups at B = 1: latency-bound, ~8-16 us apiece on MB-MelGAN v2, profiles/r04_o). Here
+// ONE workgroup takes a block of `oc` output columns of one utterance through all NS stacks:
+//   * the stage input over [q0 - H, q0 + oc + H) (H = sum of the dilations: what the chain's taps
+//     reach) is copied into an LDS tile once (global_load_lds), and every stack rewrites it in place;
+//     stack j computes its output over [q0 - H_j, q0 + oc + H_j), H_j = sum of the later dilations,
+//     so neighbouring blocks recompute the halos instead of exchanging them;
+//   * h stays in registers: conv A's accumulators (+ b_A, lrelu) become the 1x1's B operands by one
+//     cross-half lane swap per 16 channels (the 32x32 MFMA's C layout holds rows 8 j + 4 hh + i, the
+//     B layout channels 8 hh + i);
+//   * the weight fragments stream through a 3-slot LDS ring by global_load_lds, two steps ahead
+//     (a step = one 16-channel block of conv A with its 3 taps, or 3 chunks of the 1x1), across
+//     stack boundaries.
+// Every output column sums the same products in the same order as the executor's launches (conv A
+// channel-block-major with taps inner, pwg_cnet_xtile_kernel / the DMA-ring kernel; the 1x1 in its
+// chunk order [h blocks][x blocks], pwg_cnet_conv_kernel), with the same pre-activations, pair
+// splits and epilogues (h = acc + b_A rounded to fp32 before the lrelu, exactly the value the
+// executor stores and reloads): bit-identical (tests/test_gpu_vocoders.py::test_fused_stack_chain).
+#include <hip/hip_runtime.h>
+
+#include "../../include/pwg_cnet.h"
+#include "pwg_internal.h"
+
+namespace pwg {
+namespace {
+
+typedef float ms_f32x16 __attribute__((ext_vector_type(16)));
+typedef float ms_f32x4 __attribute__((ext_vector_type(4)));
+typedef float ms_f32x8 __attribute__((ext_vector_type(8)));
+typedef unsigned ms_u32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 ms_f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 ms_f16x2 __attribute__((ext_vector_type(2)));
+
+constexpr int MS_NWV = 4, MS_NTH = 64 * MS_NWV;  // waves / threads per workgroup
+constexpr int MS_P = 3;                          // weight ring slots (two steps in flight)
+
+// row p of a T-row utterance under the edge mode (the executor's edge_row)
+__device__ __forceinline__ bool ms_edge(int& p, int T, int mode) {
+  if (mode == PWG_PAD_REFLECT) {
+    p = p < 0 ? -p : p;
+    p = p >= T ? 2 * (T - 1) - p : p;
+    p = p < 0 ? 0 : (p >= T ? T - 1 : p);
+    return true;
+  }
+  const bool inside = p >= 0 && p < T;
+  p = p < 0 ? 0 : (p >= T ? T - 1 : p);
+  return inside || mode == PWG_PAD_REPLICATE;
+}
+
+// 8 fp32 -> fp16 pairs hi = rne16(v), lo = rne16(v - hi) (the executor's cn_split8)
+__device__ __forceinline__ void ms_split8(const ms_f32x8& v, ms_u32x4& hi, ms_u32x4& lo) {
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const _Float16 h0 = (_Float16)v[2 * d], h1 = (_Float16)v[2 * d + 1];
+    hi[d] = __builtin_bit_cast(unsigned, ms_f16x2{h0, h1});
+    lo[d] = __builtin_bit_cast(unsigned, ms_f16x2{(_Float16)(v[2 * d] - (float)h0), (_Float16)(v[2 * d + 1] - (float)h1)});
+  }
+}
+
+__device__ __forceinline__ ms_f32x16 ms_mma3(const ms_u32x4& ah, const ms_u32x4& al, const ms_u32x4& bh,
+                                              const ms_u32x4& bl, ms_f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(ms_f16x8, ah), __builtin_bit_cast(ms_f16x8, bh), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(ms_f16x8, ah), __builtin_bit_cast(ms_f16x8, bl), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(ms_f16x8, al), __builtin_bit_cast(ms_f16x8, bh), acc, 0, 0, 0);
+  return acc;
+}
+
+template <int N>
+__device__ __forceinline__ void ms_vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int CS>
+struct MsShape {
+  static constexpr int MT = (CS + 1) / 2;   // 32-row m-tiles (C rounded up to 32)
+  static constexpr int C = 16 * CS;
+  static constexpr int LDX = C + 4;          // floats per LDS tile row (16-B pad: lanes on other banks)
+  static constexpr int NI = 3 * MT * 2;      // 1-KB fragment copies per step (3 taps or 3 chunks, hi + lo)
+  static constexpr int D = (NI + MS_NWV - 1) / MS_NWV;  // ... per wave (uniform: the last one repeats)
+  static constexpr int SLOT = NI * 1024;
+  static constexpr int SB = (2 * CS + 2) / 3;  // 1x1 steps per stack
+  static constexpr int SPS = CS + SB;          // steps per stack
+};
+
+template <int CS, int TPW>
+__global__ void __launch_bounds__(MS_NTH) pwg_mstack_kernel(const MstackArgs a) {
+  using S = MsShape<CS>;
+  constexpr int MT = S::MT, C = S::C, LDX = S::LDX;
+  typedef __attribute__((address_space(1))) void* gptr_t;
+  typedef __attribute__((address_space(3))) void* lptr_t;
+  extern __shared__ __attribute__((aligned(16))) unsigned char ms_smem[];
+  unsigned char* const ring = ms_smem;
+  float* const sx = reinterpret_cast<float*>(ms_smem + MS_P * S::SLOT);
+  const int xw = a.oc + 2 * a.halo;           // tile rows: utterance columns c0col .. c0col + xw - 1
+  float* const sb = sx + (size_t)xw * LDX;    // [stack][b_A | b] (2 C floats each)
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int hh = lane >> 5, cl = lane & 31;
+  const int2 blk = a.blocks[blockIdx.x];
+  const int2 sgx = *reinterpret_cast<const int2*>(a.seg_x + 2 * blk.x);
+  const int2 sgy = *reinterpret_cast<const int2*>(a.seg_y + 2 * blk.x);
+  const int T = sgx.y;
+  const int c0col = blk.y - a.halo;
+  const int ns = a.ns;
+  int hout[MS_MAX];  // columns each side stack j still has to produce for the later ones
+  {
+    int h = 0;
+#pragma unroll
+    for (int j = MS_MAX - 1; j >= 0; --j) {
+      hout[j] = h;
+      if (j < ns) h += a.st[j].dil;
+    }
+  }
+  // biases (ordinary loads, all landed before the first fragment copy)
+  for (int i = threadIdx.x; i < ns * 2 * C; i += MS_NTH) {
+    const int j = i / (2 * C), r = i - j * 2 * C;
+    sb[i] = r < C ? a.st[j].bA[r] : a.st[j].bB[r - C];
+  }
+  // step s -> ring slot s % 3: stack s / SPS, then CS conv-A blocks (fragments of taps 0-2 of block
+  // r) and SB 1x1 groups (chunks 3 (r - CS) .. + 2)
+  const int n_steps = ns * S::SPS;
+  auto issue = [&](int s) {
+    const int j = s / S::SPS, r = s - j * S::SPS;
+    unsigned char* const slot = ring + (size_t)(s % MS_P) * S::SLOT;
+    const float* const wa = a.st[j].wA;
+    const float* const wb = a.st[j].wB;
+#pragma unroll
+    for (int k = 0; k < S::D; ++k) {
+      const int i = wave + MS_NWV * k < S::NI ? wave + MS_NWV * k : S::NI - 1;
+      const int g = i / (2 * MT), rem = i - g * 2 * MT, m = rem >> 1, hl = rem & 1;
+      const float* src;
+      if (r < CS) {
+        src = wa + ((size_t)(g * CS + r) * MT + m) * 512 + hl * 256;
+      } else {
+        const int ch = min(3 * (r - CS) + g, 2 * CS - 1);
+        src = wb + ((size_t)ch * MT + m) * 512 + hl * 256;
+      }
+      __builtin_amdgcn_global_load_lds((gptr_t)(src + lane * 4), (lptr_t)(slot + i * 1024), 16, 0, 0);
+    }
+  };
+  auto barrier = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+
+  ms_f32x16 accA[TPW][MT], accB[TPW][MT];
+  __syncthreads();  // biases in LDS (ordinary loads and stores, done before the first LDS copy)
+  // the input tile: 1-KB copies of consecutive LDS bytes, each lane's 16 B from its row / quad
+  // (pad quads and rows outside the utterance copy a harmless in-bounds quad)
+  {
+    const int bytes = xw * LDX * 4;
+    const int n_ins = (bytes + 1023) / 1024;
+    for (int k = wave; k < n_ins; k += MS_NWV) {
+      const int o = k * 1024 + lane * 16;
+      const int r = o / (LDX * 4), q = (o - r * LDX * 4) >> 4;
+      int c = c0col + r;
+      c = c < 0 ? 0 : (c >= T ? T - 1 : c);
+      const float* src = a.x + (size_t)(sgx.x + c) * a.ld + 4 * (q < C / 4 ? q : 0);
+      if (o < bytes)
+        __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(reinterpret_cast<unsigned char*>(sx) + k * 1024), 16, 0, 0);
+    }
+  }
+
+  issue(0);
+  if (n_steps > 1) issue(1);
+  for (int s = 0; s < n_steps; ++s) {
+    // step s (and the input tile) landed: one later step may still be in flight
+    if (s + 1 < n_steps) ms_vm_wait<S::D>();
+    else ms_vm_wait<0>();
+    barrier();
+    if (s + 2 < n_steps) issue(s + 2);  // into the slot step s - 1 read (every wave is past it)
+    const int j = s / S::SPS, r = s - j * S::SPS;
+    const ms_u32x4* const sa = reinterpret_cast<const ms_u32x4*>(ring + (size_t)(s % MS_P) * S::SLOT) + lane;
+    const int i0 = a.halo - hout[j];                         // first tile row stack j produces
+    const int nt = (a.oc + 2 * hout[j] + 31) >> 5;           // its 32-column tiles
+    if (r < CS) {
+      // ---- conv A, channel block r: taps 0..2 (pwg_cnet_xtile_kernel's order)
+      if (r == 0) {
+#pragma unroll
+        for (int n = 0; n < TPW; ++n)
+#pragma unroll
+          for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) accA[n][m][e] = 0.f;
+      }
+      const MsStack& st = a.st[j];
+      ms_u32x4 ah[3][MT], al[3][MT];
+#pragma unroll
+      for (int t = 0; t < 3; ++t)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          ah[t][m] = sa[(t * MT * 2 + m * 2) * 64];
+          al[t][m] = sa[(t * MT * 2 + m * 2 + 1) * 64];
+        }
+#pragma unroll
+      for (int n = 0; n < TPW; ++n) {
+        const int tile = wave + MS_NWV * n;
+        if (tile >= nt) break;
+        const int i = i0 + 32 * tile + cl;  // this lane's tile row
+        ms_u32x4 bh[3], bl[3];
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+          int p = c0col + i - st.pad + t * st.dil;
+          const bool ok = ms_edge(p, T, st.mode);
+          int ir = p - c0col;
+          ir = ir < 0 ? 0 : (ir >= xw ? xw - 1 : ir);
+          const float* xr = sx + (size_t)ir * LDX + 16 * r + 8 * hh;
+          const ms_f32x4 v0 = *reinterpret_cast<const ms_f32x4*>(xr), v1 = *reinterpret_cast<const ms_f32x4*>(xr + 4);
+          ms_f32x8 x = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+          if (st.slopeA != 1.f) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) x[e] = x[e] > 0.f ? x[e] : x[e] * st.slopeA;
+          }
+          if (!ok) x = ms_f32x8{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+          ms_split8(x, bh[t], bl[t]);
+        }
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+#pragma unroll
+          for (int m = 0; m < MT; ++m) accA[n][m] = ms_mma3(ah[t][m], al[t][m], bh[t], bl[t], accA[n][m]);
+      }
+    } else {
+      // ---- the 1x1 over [lrelu(h); x_j], chunks 3 (r - CS) .. + 2 of [h blocks][x blocks]
+      const int kg = r - CS;
+      if (kg == 0) {
+#pragma unroll
+        for (int n = 0; n < TPW; ++n)
+#pragma unroll
+          for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) accB[n][m][e] = 0.f;
+      }
+      const float slopeH = a.st[j].slopeH;
+      const float* const bA = sb + (size_t)j * 2 * C;
+#pragma unroll
+      for (int ch = 0; ch < 2 * CS; ++ch) {
+        if (ch / 3 != kg) continue;
+        const int g = ch - 3 * kg;
+        ms_u32x4 ah[MT], al[MT];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          ah[m] = sa[(g * MT * 2 + m * 2) * 64];
+          al[m] = sa[(g * MT * 2 + m * 2 + 1) * 64];
+        }
+#pragma unroll
+        for (int n = 0; n < TPW; ++n) {
+          const int tile = wave + MS_NWV * n;
+          if (tile >= nt) break;
+          ms_f32x8 x;
+          if (ch < CS) {
+            // h channels 16 ch .. + 15 from conv A's accumulators: lane half hh needs rows
+            // 8 (J0 + hh) + 0..7, i.e. 4 of its own (j4 = J0 + hh, rows + 4 hh) and 4 of the other
+            // half's (same j4): one swap of 4 values across the halves
+            constexpr int dummy = 0;
+            (void)dummy;
+            const int mh = ch >> 1, J0 = (ch & 1) * 2;
+            ms_f32x4 own, snd;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              own[e] = hh ? accA[n][mh][4 * (J0 + 1) + e] : accA[n][mh][4 * J0 + e];
+              snd[e] = hh ? accA[n][mh][4 * J0 + e] : accA[n][mh][4 * (J0 + 1) + e];
+            }
+            ms_f32x4 rcv;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) rcv[e] = __shfl_xor(snd[e], 32);
+            const float* bb = bA + 16 * ch + 8 * hh;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              x[e] = (hh ? rcv[e] : own[e]) + bb[e];
+              x[4 + e] = (hh ? own[e] : rcv[e]) + bb[4 + e];
+            }
+            if (slopeH != 1.f) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) x[e] = x[e] > 0.f ? x[e] : x[e] * slopeH;
+            }
+          } else {
+            const int i = i0 + 32 * tile + cl;
+            const int ir = i < xw ? i : xw - 1;
+            const float* xr = sx + (size_t)ir * LDX + 16 * (ch - CS) + 8 * hh;
+            const ms_f32x4 v0 = *reinterpret_cast<const ms_f32x4*>(xr), v1 = *reinterpret_cast<const ms_f32x4*>(xr + 4);
+            x = ms_f32x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+          }
+          ms_u32x4 bh, bl;
+          ms_split8(x, bh, bl);
+#pragma unroll
+          for (int m = 0; m < MT; ++m) accB[n][m] = ms_mma3(ah[m], al[m], bh, bl, accB[n][m]);
+        }
+      }
+      if (kg == S::SB - 1) {
+        // ---- epilogue of stack j: x_j+1 = acc + b into the tile (own columns; the conv of stack
+        // j + 1 reads it after the next step's barrier), or, for the last stack, y
+        const float* const bB = sb + (size_t)j * 2 * C + C;
+        const bool last = j == ns - 1;
+#pragma unroll
+        for (int n = 0; n < TPW; ++n) {
+          const int tile = wave + MS_NWV * n;
+          if (tile >= nt) break;
+          const int i = i0 + 32 * tile + cl;
+          const int c = c0col + i;
+          const bool live = last ? (i >= a.halo && i < a.halo + a.oc && c < T) : i < xw;
+          if (!live) continue;
+          float* const dst = last ? a.y + (size_t)(sgy.x + c) * a.ld : sx + (size_t)i * LDX;
+#pragma unroll
+          for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int j4 = 0; j4 < 4; ++j4) {
+              const int row = 32 * m + 8 * j4 + 4 * hh;
+              if (row >= C) continue;
+              ms_f32x4 v;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = accB[n][m][4 * j4 + e] + bB[row + e];
+              *reinterpret_cast<ms_f32x4*>(dst + row) = v;
+            }
+        }
+      }
+    }
+  }
+}
+
+template <int CS, int TPW>
+hipError_t ms_go(const MstackArgs& a, int n_blocks, hipStream_t s) {
+  const int lds = mstack_lds(CS, a.oc, a.halo, a.ns);
+  const hipError_t e = allow_lds(reinterpret_cast<const void*>(pwg_mstack_kernel<CS, TPW>), lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((pwg_mstack_kernel<CS, TPW>), dim3((unsigned)n_blocks), dim3(MS_NTH), (size_t)lds, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+int mstack_lds(int cs, int oc, int halo, int ns) {
+  const int mt = (cs + 1) / 2;
+  return MS_P * 3 * mt * 2 * 1024 + (oc + 2 * halo) * (16 * cs + 4) * 4 + ns * 2 * 16 * cs * 4;
+}
+
+// accumulators: 2 x TPW x MT x 16 VGPRs; TPW x MT <= 4 keeps the kernel within one wave per SIMD's
+// registers without spills
+bool mstack_supported(int cs, int tpw) {
+  const int mt = (cs + 1) / 2;
+  return (cs == 2 || cs == 3 || cs == 4 || cs == 6 || cs == 8) && (tpw == 1 || tpw == 2) && tpw * mt <= 4;
+}
+
+hipError_t launch_mstack(const MstackArgs& a, int cs, int tpw, int n_blocks, hipStream_t s) {
+  if (!mstack_supported(cs, tpw) || a.ns < 1 || a.ns > MS_MAX || n_blocks < 1) return hipErrorInvalidValue;
+  if (tpw == 1) {
+    switch (cs) {
+      case 2: return ms_go<2, 1>(a, n_blocks, s);
+      case 3: return ms_go<3, 1>(a, n_blocks, s);
+      case 4: return ms_go<4, 1>(a, n_blocks, s);
+      case 6: return ms_go<6, 1>(a, n_blocks, s);
+      case 8: return ms_go<8, 1>(a, n_blocks, s);
+    }
+  } else {
+    switch (cs) {
+      case 2: return ms_go<2, 2>(a, n_blocks, s);
+      case 3: return ms_go<3, 2>(a, n_blocks, s);
+      case 4: return ms_go<4, 2>(a, n_blocks, s);
+    }
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace pwg

@@ -265,3 +265,30 @@ def test_plan_image_is_host_built_and_cheap(name, built_lib):
         assert p.image()[1].size < 64 * 1024
     per_plan_ms = (time.perf_counter() - t0) * 1e3 / len(lens)
     assert per_plan_ms < 5.0, per_plan_ms
+
+
+def test_fused_stack_chains_in_the_schedule(built_lib):
+    """PWG_CNET_OPT_MSTACK: MB-MelGAN v2's ResidualStacks form one chain per upsampling stage (4
+    stacks: a k = 3 conv + the two-source 1x1 each). At B = 1 the chains of the 96- and 48-channel
+    stages run as one launch each (192 channels: no, 6 m-tiles), so the plan's launches drop by
+    2 x (2 x 4 - 1); with the option off, or for a large plan in mode 1, nothing changes; mode 2
+    fuses the large plan's chains too."""
+    from parallelwavegan_amd.cnet import CnetEngine
+
+    m = _holder("mb_melgan_v2")
+    m.pqmf = PQMF(m.out_channels)
+    P, _ = m.program(True)
+    eng = CnetEngine(P, None, host_only=True)
+    n_on = len(eng.schedule(eng.plan([64]))[0])
+    eng.set_mstack(0)
+    n_off = len(eng.schedule(eng.plan([64]))[0])
+    assert n_off - n_on == 2 * (2 * 4 - 1), (n_off, n_on)
+    big_off = len(eng.schedule(eng.plan([1000] * 8))[0])
+    eng.set_mstack(1)
+    assert len(eng.schedule(eng.plan([1000] * 8))[0]) == big_off
+    eng.set_mstack(2)
+    assert len(eng.schedule(eng.plan([1000] * 8))[0]) < big_off
+    import ctypes
+
+    from parallelwavegan_amd import _lib
+    assert eng._lib.pwg_cnet_set_option(eng._h, 9, 3) == _lib.PWG_ERR_INVALID

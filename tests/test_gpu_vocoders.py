@@ -536,3 +536,43 @@ def test_distinct_length_decode_loop(cfg, built_lib, cuda_device):
         np.testing.assert_array_equal(a, c)
     np.testing.assert_array_equal(again, ref[0])
     np.testing.assert_array_equal(third, ref[0])
+
+
+@pytest.mark.parametrize("cfg", ["mb_melgan_v2", "melgan_v1", "mb_melgan_test"])
+def test_fused_stack_chain_bitwise_equal(cfg, built_lib, cuda_device):
+    """PWG_CNET_OPT_MSTACK (pwg_mstack.hip): a MelGAN stage's ResidualStack chain as one launch per
+    block of output columns, the input tile +- the summed dilations in LDS (reflect-padded edges
+    inside the tile), h in registers. Same products, order, splits and epilogues as the two launches
+    per stack: bit-identical to mstack off, at B = 1 (short utterances: every block touches an edge;
+    T' = 64 and 131) and on a forced ragged batch; the chains ran fused (their inner ops record no
+    launch)."""
+    from parallelwavegan_amd import configs, synthetic
+    from parallelwavegan_amd.melgan import PQMF, MelGANGenerator
+
+    _, params = configs.vocoder_params(cfg)
+    m = MelGANGenerator(**params)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic.make_module_state_dict(m, seed=31).items()})
+    if cfg in configs.VOCODER_PQMF:
+        m.pqmf = PQMF(**configs.VOCODER_PQMF[cfg])
+    m = m.to(cuda_device)
+    eng = m.engine()
+    singles = [synthetic.make_mel(f, 80, seed=400 + f) for f in (64, 9, 131, 5)]
+    batch = [synthetic.make_mel(f, 80, seed=410 + i) for i, f in enumerate([5, 40, 17, 64])]
+    with torch.no_grad():
+        outs = {}
+        for mode in (0, 1, 2):
+            eng.set_mstack(mode)
+            eng.set_timing(True)
+            eng.collect_timing()
+            outs[mode] = [m.inference(torch.from_numpy(x).to(cuda_device)).cpu().numpy() for x in singles]
+            t = eng.collect_timing()
+            eng.set_timing(False)
+            outs[mode] += [y.cpu().numpy() for y in m.inference_batch(batch)]
+            if mode == 1:
+                fused = sum(1 for name, _, n in t if n == 0 and "stack" in name)
+        eng.set_mstack(1)
+    assert fused > 0
+    for mode in (1, 2):
+        for a, b in zip(outs[mode], outs[0]):
+            assert np.isfinite(a).all()
+            np.testing.assert_array_equal(a, b)
