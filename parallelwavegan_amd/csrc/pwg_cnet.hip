@@ -4325,7 +4325,11 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
   }
   // fused stack chains (PWG_CNET_OPT_MSTACK): the widest block (a multiple of 32 columns, at most
   // 128) whose first stack's output -- the block plus the later stacks' halos -- is at most one
-  // 32-column tile per wave and whose tile, ring and biases fit the LDS
+  // 32-column tile per wave and whose tile, ring and biases fit the LDS. Mode 1 takes a chain when
+  // its blocks fit one round over the CUs (the halo recompute costs more than the launches it saves
+  // once the blocks queue: MB-MelGAN v2 T' = 512 0.54 -> 0.62 ms) and it has at most 128 channels
+  // (the 192-channel chain, one fragment unit per step, measured 0.23 ms against 0.15 ms for its
+  // 8 launches at T' = 64; profiles/r05_e)
   p->ms_oc.assign(nph, 0);
   p->o_msblocks.assign(nph, -1);
   p->n_msblocks.assign(nph, 0);
@@ -4337,8 +4341,9 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
     int oc = 0;
     for (int o = 32; o <= 128; o += 32)
       if ((o + 2 * (ph.ms_halo - d0) + 31) / 32 <= 4 && mstack_lds(cs, o, ph.ms_halo, ph.ms_n) <= PR_MAX_LDS) oc = o;
-    if (oc == 0) continue;
+    if (oc == 0 || (n->mstack == 1 && cs > 8)) continue;
     for (int u = 0; u < n_utts; ++u) ncols[u] = (int)(frames[u] * rate);
+    if (n->mstack == 1 && count(oc) > p->n_cu) continue;
     p->ms_oc[pi] = oc;
     p->o_msblocks[pi] = list(CN_L_BLK, rate, 1, 0, oc);
     p->n_msblocks[pi] = (int)count(oc);

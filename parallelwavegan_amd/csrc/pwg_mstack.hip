@@ -12,8 +12,8 @@
 //     reach) is copied into an LDS tile once (global_load_lds), and every stack rewrites it in place;
 //     stack j computes its output over [q0 - H_j, q0 + oc + H_j), H_j = sum of the later dilations,
 //     so neighbouring blocks recompute the halos instead of exchanging them;
-//   * h stays in registers: conv A's accumulators (+ b_A, lrelu) become the 1x1's B operands by one
-//     cross-half lane swap per 16 channels (the 32x32 MFMA's C layout holds rows 8 j + 4 hh + i, the
+//   * h stays in registers: conv A's accumulators (+ b_A, lrelu) become the 1x1's B operands by a
+//     cross-half exchange per 16 channels (the 32x32 MFMA's C layout holds rows 8 j + 4 hh + i, the
 //     B layout channels 8 hh + i);
 //   * the weight fragments stream through a 3-slot LDS ring by global_load_lds, two steps ahead
 //     (a step = one 16-channel block of conv A with its 3 taps, or 3 chunks of the 1x1), across
@@ -24,6 +24,8 @@
 // splits and epilogues (h = acc + b_A rounded to fp32 before the lrelu, exactly the value the
 // executor stores and reloads): bit-identical (tests/test_gpu_vocoders.py::test_fused_stack_chain).
 #include <hip/hip_runtime.h>
+
+#include <type_traits>
 
 #include "../../include/pwg_cnet.h"
 #include "pwg_internal.h"
@@ -39,7 +41,13 @@ typedef _Float16 ms_f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 ms_f16x2 __attribute__((ext_vector_type(2)));
 
 constexpr int MS_NWV = 4, MS_NTH = 64 * MS_NWV;  // waves / threads per workgroup
-constexpr int MS_P = 3;                          // weight ring slots (two steps in flight)
+// weight ring slots: P - 1 steps in flight. A step's MFMAs (~0.4 us) are far shorter than a
+// fragment copy's round trip, so the ring runs deep: 3 slots measured 2.85 us per step on
+// MB-MelGAN v2's 96-channel chain (the copy latency, profiles/r05_c)
+__host__ __device__ constexpr int ms_ring(int mt) { return mt <= 3 ? 6 : 4; }
+// fragment units per step (taps of one conv-A channel block, or 1x1 chunks): 3, or 1 at 6 m-tiles
+// (192 channels), whose 3-unit slots would not fit the LDS beside the 192-channel input tile
+__host__ __device__ constexpr int ms_units(int mt) { return mt <= 4 ? 3 : 1; }
 
 // row p of a T-row utterance under the edge mode (the executor's edge_row)
 __device__ __forceinline__ bool ms_edge(int& p, int T, int mode) {
@@ -76,17 +84,43 @@ template <int N>
 __device__ __forceinline__ void ms_vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
+// s_waitcnt vmcnt(min(r, R) * D): wait for a step while the r steps issued after it may still land
+template <int D, int R>
+__device__ __forceinline__ void ms_vm_wait_steps(int r) {
+  if constexpr (R > 0) {
+    if (r >= R) {
+      ms_vm_wait<R * D>();
+      return;
+    }
+    ms_vm_wait_steps<D, R - 1>(r);
+  } else {
+    ms_vm_wait<0>();
+  }
+}
+
+// f(integral_constant<int, i>) for i = B .. E - 1, unrolled at compile time (indices into
+// accumulator arrays must be constants, or the compiler selects registers by runtime compares)
+template <int B, int E, typename F>
+__device__ __forceinline__ void ms_static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    ms_static_for<B + 1, E>(f);
+  }
+}
 
 template <int CS>
 struct MsShape {
   static constexpr int MT = (CS + 1) / 2;   // 32-row m-tiles (C rounded up to 32)
   static constexpr int C = 16 * CS;
   static constexpr int LDX = C + 4;          // floats per LDS tile row (16-B pad: lanes on other banks)
-  static constexpr int NI = 3 * MT * 2;      // 1-KB fragment copies per step (3 taps or 3 chunks, hi + lo)
+  static constexpr int G = ms_units(MT);     // units per step
+  static constexpr int NI = G * MT * 2;      // 1-KB fragment copies per step (G taps or chunks, hi + lo)
   static constexpr int D = (NI + MS_NWV - 1) / MS_NWV;  // ... per wave (uniform: the last one repeats)
   static constexpr int SLOT = NI * 1024;
-  static constexpr int SB = (2 * CS + 2) / 3;  // 1x1 steps per stack
-  static constexpr int SPS = CS + SB;          // steps per stack
+  static constexpr int SA = CS * (3 / G);           // conv-A steps per stack (block-major, taps inner)
+  static constexpr int SB = (2 * CS + G - 1) / G;   // 1x1 steps per stack
+  static constexpr int SPS = SA + SB;               // steps per stack
+  static constexpr int P = ms_ring(MT);
 };
 
 template <int CS, int TPW>
@@ -97,7 +131,8 @@ __global__ void __launch_bounds__(MS_NTH) pwg_mstack_kernel(const MstackArgs a) 
   typedef __attribute__((address_space(3))) void* lptr_t;
   extern __shared__ __attribute__((aligned(16))) unsigned char ms_smem[];
   unsigned char* const ring = ms_smem;
-  float* const sx = reinterpret_cast<float*>(ms_smem + MS_P * S::SLOT);
+  constexpr int P = S::P;
+  float* const sx = reinterpret_cast<float*>(ms_smem + P * S::SLOT);
   const int xw = a.oc + 2 * a.halo;           // tile rows: utterance columns c0col .. c0col + xw - 1
   float* const sb = sx + (size_t)xw * LDX;    // [stack][b_A | b] (2 C floats each)
   const int lane = threadIdx.x & 63;
@@ -123,12 +158,12 @@ __global__ void __launch_bounds__(MS_NTH) pwg_mstack_kernel(const MstackArgs a) 
     const int j = i / (2 * C), r = i - j * 2 * C;
     sb[i] = r < C ? a.st[j].bA[r] : a.st[j].bB[r - C];
   }
-  // step s -> ring slot s % 3: stack s / SPS, then CS conv-A blocks (fragments of taps 0-2 of block
-  // r) and SB 1x1 groups (chunks 3 (r - CS) .. + 2)
+  // step s -> ring slot s % P: stack s / SPS, then SA conv-A steps (channel block r / (3 / G), its
+  // taps G (r % (3 / G)) .. + G - 1) and SB 1x1 steps (chunks G (r - SA) .. + G - 1)
   const int n_steps = ns * S::SPS;
   auto issue = [&](int s) {
     const int j = s / S::SPS, r = s - j * S::SPS;
-    unsigned char* const slot = ring + (size_t)(s % MS_P) * S::SLOT;
+    unsigned char* const slot = ring + (size_t)(s % P) * S::SLOT;
     const float* const wa = a.st[j].wA;
     const float* const wb = a.st[j].wB;
 #pragma unroll
@@ -136,10 +171,11 @@ __global__ void __launch_bounds__(MS_NTH) pwg_mstack_kernel(const MstackArgs a) 
       const int i = wave + MS_NWV * k < S::NI ? wave + MS_NWV * k : S::NI - 1;
       const int g = i / (2 * MT), rem = i - g * 2 * MT, m = rem >> 1, hl = rem & 1;
       const float* src;
-      if (r < CS) {
-        src = wa + ((size_t)(g * CS + r) * MT + m) * 512 + hl * 256;
+      if (r < S::SA) {
+        const int cb = r / (3 / S::G), t = S::G * (r - cb * (3 / S::G)) + g;
+        src = wa + ((size_t)(t * CS + cb) * MT + m) * 512 + hl * 256;
       } else {
-        const int ch = min(3 * (r - CS) + g, 2 * CS - 1);
+        const int ch = min(S::G * (r - S::SA) + g, 2 * CS - 1);
         src = wb + ((size_t)ch * MT + m) * 512 + hl * 256;
       }
       __builtin_amdgcn_global_load_lds((gptr_t)(src + lane * 4), (lptr_t)(slot + i * 1024), 16, 0, 0);
@@ -168,32 +204,34 @@ __global__ void __launch_bounds__(MS_NTH) pwg_mstack_kernel(const MstackArgs a) 
     }
   }
 
-  issue(0);
-  if (n_steps > 1) issue(1);
-  for (int s = 0; s < n_steps; ++s) {
-    // step s (and the input tile) landed: one later step may still be in flight
-    if (s + 1 < n_steps) ms_vm_wait<S::D>();
-    else ms_vm_wait<0>();
+  for (int s = 0; s < P - 1 && s < n_steps; ++s) issue(s);
+  // one step: its fragments (and the input tile) landed -- the steps issued after it may still be
+  // in flight --, every wave is past the previous step (whose slot the next issue refills)
+  int s = 0;
+  auto step_begin = [&]() {
+    ms_vm_wait_steps<S::D, P - 2>(n_steps - 1 - s);
     barrier();
-    if (s + 2 < n_steps) issue(s + 2);  // into the slot step s - 1 read (every wave is past it)
-    const int j = s / S::SPS, r = s - j * S::SPS;
-    const ms_u32x4* const sa = reinterpret_cast<const ms_u32x4*>(ring + (size_t)(s % MS_P) * S::SLOT) + lane;
-    const int i0 = a.halo - hout[j];                         // first tile row stack j produces
-    const int nt = (a.oc + 2 * hout[j] + 31) >> 5;           // its 32-column tiles
-    if (r < CS) {
-      // ---- conv A, channel block r: taps 0..2 (pwg_cnet_xtile_kernel's order)
-      if (r == 0) {
+    if (s + P - 1 < n_steps) issue(s + P - 1);
+    return reinterpret_cast<const ms_u32x4*>(ring + (size_t)(s % P) * S::SLOT) + lane;
+  };
+  constexpr int G = S::G;
+  for (int j = 0; j < ns; ++j) {
+    const MsStack& st = a.st[j];
+    const int i0 = a.halo - hout[j];                // first tile row stack j produces
+    const int nt = (a.oc + 2 * hout[j] + 31) >> 5;  // its 32-column tiles
 #pragma unroll
-        for (int n = 0; n < TPW; ++n)
+    for (int n = 0; n < TPW; ++n)
 #pragma unroll
-          for (int m = 0; m < MT; ++m)
+      for (int m = 0; m < MT; ++m)
 #pragma unroll
-            for (int e = 0; e < 16; ++e) accA[n][m][e] = 0.f;
-      }
-      const MsStack& st = a.st[j];
-      ms_u32x4 ah[3][MT], al[3][MT];
+        for (int e = 0; e < 16; ++e) accA[n][m][e] = accB[n][m][e] = 0.f;
+    // ---- conv A: channel block cb, taps t0 .. t0 + G - 1 per step (pwg_cnet_xtile_kernel's order)
+    for (int r = 0; r < S::SA; ++r, ++s) {
+      const ms_u32x4* const sa = step_begin();
+      const int cb = r / (3 / G), t0 = G * (r - cb * (3 / G));
+      ms_u32x4 ah[G][MT], al[G][MT];
 #pragma unroll
-      for (int t = 0; t < 3; ++t)
+      for (int t = 0; t < G; ++t)
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
           ah[t][m] = sa[(t * MT * 2 + m * 2) * 64];
@@ -204,14 +242,14 @@ __global__ void __launch_bounds__(MS_NTH) pwg_mstack_kernel(const MstackArgs a) 
         const int tile = wave + MS_NWV * n;
         if (tile >= nt) break;
         const int i = i0 + 32 * tile + cl;  // this lane's tile row
-        ms_u32x4 bh[3], bl[3];
+        ms_u32x4 bh[G], bl[G];
 #pragma unroll
-        for (int t = 0; t < 3; ++t) {
-          int p = c0col + i - st.pad + t * st.dil;
+        for (int t = 0; t < G; ++t) {
+          int p = c0col + i - st.pad + (t0 + t) * st.dil;
           const bool ok = ms_edge(p, T, st.mode);
           int ir = p - c0col;
           ir = ir < 0 ? 0 : (ir >= xw ? xw - 1 : ir);
-          const float* xr = sx + (size_t)ir * LDX + 16 * r + 8 * hh;
+          const float* xr = sx + (size_t)ir * LDX + 16 * cb + 8 * hh;
           const ms_f32x4 v0 = *reinterpret_cast<const ms_f32x4*>(xr), v1 = *reinterpret_cast<const ms_f32x4*>(xr + 4);
           ms_f32x8 x = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
           if (st.slopeA != 1.f) {
@@ -222,27 +260,22 @@ __global__ void __launch_bounds__(MS_NTH) pwg_mstack_kernel(const MstackArgs a) 
           ms_split8(x, bh[t], bl[t]);
         }
 #pragma unroll
-        for (int t = 0; t < 3; ++t)
+        for (int t = 0; t < G; ++t)
 #pragma unroll
           for (int m = 0; m < MT; ++m) accA[n][m] = ms_mma3(ah[t][m], al[t][m], bh[t], bl[t], accA[n][m]);
       }
-    } else {
-      // ---- the 1x1 over [lrelu(h); x_j], chunks 3 (r - CS) .. + 2 of [h blocks][x blocks]
-      const int kg = r - CS;
-      if (kg == 0) {
-#pragma unroll
-        for (int n = 0; n < TPW; ++n)
-#pragma unroll
-          for (int m = 0; m < MT; ++m)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) accB[n][m][e] = 0.f;
-      }
-      const float slopeH = a.st[j].slopeH;
-      const float* const bA = sb + (size_t)j * 2 * C;
-#pragma unroll
-      for (int ch = 0; ch < 2 * CS; ++ch) {
-        if (ch / 3 != kg) continue;
-        const int g = ch - 3 * kg;
+    }
+    // ---- the 1x1 over [lrelu(h); x_j]: chunks G kg .. + G - 1 of [h blocks][x blocks] per step
+    // (kg and the chunks are compile-time, so h's accumulator registers are indexed statically)
+    const float slopeH = st.slopeH;
+    const float* const bA = sb + (size_t)j * 2 * C;
+    ms_static_for<0, S::SB>([&](auto kgc) {
+      constexpr int kg = decltype(kgc)::value;
+      const ms_u32x4* const sa = step_begin();
+      ms_static_for<0, G>([&](auto gc) {
+        constexpr int g = decltype(gc)::value;
+        constexpr int ch = G * kg + g;
+        if constexpr (ch < 2 * CS) {
         ms_u32x4 ah[MT], al[MT];
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
@@ -254,27 +287,20 @@ __global__ void __launch_bounds__(MS_NTH) pwg_mstack_kernel(const MstackArgs a) 
           const int tile = wave + MS_NWV * n;
           if (tile >= nt) break;
           ms_f32x8 x;
-          if (ch < CS) {
+          if constexpr (ch < CS) {
             // h channels 16 ch .. + 15 from conv A's accumulators: lane half hh needs rows
-            // 8 (J0 + hh) + 0..7, i.e. 4 of its own (j4 = J0 + hh, rows + 4 hh) and 4 of the other
-            // half's (same j4): one swap of 4 values across the halves
-            constexpr int dummy = 0;
-            (void)dummy;
-            const int mh = ch >> 1, J0 = (ch & 1) * 2;
-            ms_f32x4 own, snd;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              own[e] = hh ? accA[n][mh][4 * (J0 + 1) + e] : accA[n][mh][4 * J0 + e];
-              snd[e] = hh ? accA[n][mh][4 * J0 + e] : accA[n][mh][4 * (J0 + 1) + e];
-            }
-            ms_f32x4 rcv;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) rcv[e] = __shfl_xor(snd[e], 32);
+            // 8 (J0 + hh) + 0..7, i.e. rows 8 (J0 + hh) + 0..3 (j4 = J0 + hh of half 0) and + 4..7
+            // (the same j4 of half 1). With A = acc[j4 = J0], B = acc[j4 = J0 + 1] (rows + 4 hh):
+            // half 0 takes (A, A of half 1), half 1 (B of half 0, B): one cross-half exchange of each
+            // (the selects pick between two values, never between accumulator registers)
+            constexpr int mh = ch >> 1, J0 = (ch & 1) * 2;
             const float* bb = bA + 16 * ch + 8 * hh;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              x[e] = (hh ? rcv[e] : own[e]) + bb[e];
-              x[4 + e] = (hh ? own[e] : rcv[e]) + bb[4 + e];
+              const float va = accA[n][mh][4 * J0 + e], vb = accA[n][mh][4 * (J0 + 1) + e];
+              const float xa = __shfl_xor(va, 32), xb = __shfl_xor(vb, 32);
+              x[e] = (hh ? xb : va) + bb[e];
+              x[4 + e] = (hh ? vb : xa) + bb[4 + e];
             }
             if (slopeH != 1.f) {
 #pragma unroll
@@ -292,34 +318,34 @@ __global__ void __launch_bounds__(MS_NTH) pwg_mstack_kernel(const MstackArgs a) 
 #pragma unroll
           for (int m = 0; m < MT; ++m) accB[n][m] = ms_mma3(ah[m], al[m], bh, bl, accB[n][m]);
         }
-      }
-      if (kg == S::SB - 1) {
-        // ---- epilogue of stack j: x_j+1 = acc + b into the tile (own columns; the conv of stack
-        // j + 1 reads it after the next step's barrier), or, for the last stack, y
-        const float* const bB = sb + (size_t)j * 2 * C + C;
-        const bool last = j == ns - 1;
-#pragma unroll
-        for (int n = 0; n < TPW; ++n) {
-          const int tile = wave + MS_NWV * n;
-          if (tile >= nt) break;
-          const int i = i0 + 32 * tile + cl;
-          const int c = c0col + i;
-          const bool live = last ? (i >= a.halo && i < a.halo + a.oc && c < T) : i < xw;
-          if (!live) continue;
-          float* const dst = last ? a.y + (size_t)(sgy.x + c) * a.ld : sx + (size_t)i * LDX;
-#pragma unroll
-          for (int m = 0; m < MT; ++m)
-#pragma unroll
-            for (int j4 = 0; j4 < 4; ++j4) {
-              const int row = 32 * m + 8 * j4 + 4 * hh;
-              if (row >= C) continue;
-              ms_f32x4 v;
-#pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] = accB[n][m][4 * j4 + e] + bB[row + e];
-              *reinterpret_cast<ms_f32x4*>(dst + row) = v;
-            }
         }
-      }
+      });
+      ++s;
+    });
+    // ---- epilogue of stack j: x_j+1 = acc + b into the tile (own columns; the conv of stack j + 1
+    // reads it after the next step's barrier), or, for the last stack, y
+    const float* const bB = sb + (size_t)j * 2 * C + C;
+    const bool last = j == ns - 1;
+#pragma unroll
+    for (int n = 0; n < TPW; ++n) {
+      const int tile = wave + MS_NWV * n;
+      if (tile >= nt) break;
+      const int i = i0 + 32 * tile + cl;
+      const int c = c0col + i;
+      const bool live = last ? (i >= a.halo && i < a.halo + a.oc && c < T) : i < xw;
+      if (!live) continue;
+      float* const dst = last ? a.y + (size_t)(sgy.x + c) * a.ld : sx + (size_t)i * LDX;
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int j4 = 0; j4 < 4; ++j4) {
+          const int row = 32 * m + 8 * j4 + 4 * hh;
+          if (row >= C) continue;
+          ms_f32x4 v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = accB[n][m][4 * j4 + e] + bB[row + e];
+          *reinterpret_cast<ms_f32x4*>(dst + row) = v;
+        }
     }
   }
 }
@@ -337,14 +363,15 @@ hipError_t ms_go(const MstackArgs& a, int n_blocks, hipStream_t s) {
 
 int mstack_lds(int cs, int oc, int halo, int ns) {
   const int mt = (cs + 1) / 2;
-  return MS_P * 3 * mt * 2 * 1024 + (oc + 2 * halo) * (16 * cs + 4) * 4 + ns * 2 * 16 * cs * 4;
+  return ms_ring(mt) * ms_units(mt) * mt * 2 * 1024 + (oc + 2 * halo) * (16 * cs + 4) * 4 + ns * 2 * 16 * cs * 4;
 }
 
-// accumulators: 2 x TPW x MT x 16 VGPRs; TPW x MT <= 4 keeps the kernel within one wave per SIMD's
-// registers without spills
+// accumulators: 2 x TPW x MT x 16 VGPRs; TPW x MT <= 4 (or one tile of 192 channels, one fragment unit
+// per step) keeps the kernel within one wave per SIMD's registers without spills
 bool mstack_supported(int cs, int tpw) {
   const int mt = (cs + 1) / 2;
-  return (cs == 2 || cs == 3 || cs == 4 || cs == 6 || cs == 8) && (tpw == 1 || tpw == 2) && tpw * mt <= 4;
+  return ((cs == 2 || cs == 3 || cs == 4 || cs == 6 || cs == 8) && (tpw == 1 || tpw == 2) && tpw * mt <= 4) ||
+         (cs == 12 && tpw == 1);
 }
 
 hipError_t launch_mstack(const MstackArgs& a, int cs, int tpw, int n_blocks, hipStream_t s) {
@@ -356,6 +383,7 @@ hipError_t launch_mstack(const MstackArgs& a, int cs, int tpw, int n_blocks, hip
       case 4: return ms_go<4, 1>(a, n_blocks, s);
       case 6: return ms_go<6, 1>(a, n_blocks, s);
       case 8: return ms_go<8, 1>(a, n_blocks, s);
+      case 12: return ms_go<12, 1>(a, n_blocks, s);
     }
   } else {
     switch (cs) {

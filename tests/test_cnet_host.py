@@ -269,10 +269,10 @@ def test_plan_image_is_host_built_and_cheap(name, built_lib):
 
 def test_fused_stack_chains_in_the_schedule(built_lib):
     """PWG_CNET_OPT_MSTACK: MB-MelGAN v2's ResidualStacks form one chain per upsampling stage (4
-    stacks: a k = 3 conv + the two-source 1x1 each). At B = 1 the chains of the 96- and 48-channel
-    stages run as one launch each (192 channels: no, 6 m-tiles), so the plan's launches drop by
-    2 x (2 x 4 - 1); with the option off, or for a large plan in mode 1, nothing changes; mode 2
-    fuses the large plan's chains too."""
+    stacks: a k = 3 conv + the two-source 1x1 each). At B = 1, T' = 64 the chains of the 96- and
+    48-channel stages run as one launch each (mode 1 leaves the 192-channel one unfused), so the
+    plan's launches drop by 2 x (2 x 4 - 1); mode 2 fuses all three; with the option off, or for a
+    large plan in mode 1, nothing changes; mode 2 fuses the large plan's chains too."""
     from parallelwavegan_amd.cnet import CnetEngine
 
     m = _holder("mb_melgan_v2")
@@ -280,9 +280,12 @@ def test_fused_stack_chains_in_the_schedule(built_lib):
     P, _ = m.program(True)
     eng = CnetEngine(P, None, host_only=True)
     n_on = len(eng.schedule(eng.plan([64]))[0])
+    eng.set_mstack(2)
+    n_all = len(eng.schedule(eng.plan([64]))[0])
     eng.set_mstack(0)
     n_off = len(eng.schedule(eng.plan([64]))[0])
     assert n_off - n_on == 2 * (2 * 4 - 1), (n_off, n_on)
+    assert n_off - n_all == 3 * (2 * 4 - 1), (n_off, n_all)
     big_off = len(eng.schedule(eng.plan([1000] * 8))[0])
     eng.set_mstack(1)
     assert len(eng.schedule(eng.plan([1000] * 8))[0]) == big_off
