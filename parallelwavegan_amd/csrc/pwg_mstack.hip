@@ -80,6 +80,15 @@ __device__ __forceinline__ ms_f32x16 ms_mma3(const ms_u32x4& ah, const ms_u32x4&
   return acc;
 }
 
+// Keep a prepared operand where it is computed: without it the compiler sinks the preparation past
+// the next step's wait and barrier, next to the MFMAs that use it, and nothing overlaps
+__device__ __forceinline__ void ms_pin(ms_u32x4& v) { asm volatile("" : "+v"(v)); }
+
+// LeakyReLU exactly as the executor computes it, unconditionally (slope 1: x either way), so the
+// preparation has no branch. (x * (x > 0 ? 1 : slope) would let the compiler contract the product
+// into the pair split's subtraction, an fma: other bits.)
+__device__ __forceinline__ float ms_lrelu(float x, float slope) { return x > 0.f ? x : x * slope; }
+
 template <int N>
 __device__ __forceinline__ void ms_vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -123,6 +132,12 @@ struct MsShape {
   static constexpr int P = ms_ring(MT);
 };
 
+#ifdef PWG_MSTACK_PROBE
+// probe builds only: shader-clock stamps of workgroup 0, wave 0 (tools/diag/mstack_probe.py)
+constexpr int MS_PROBE_N = 512;
+__device__ unsigned long long g_ms_probe[MS_PROBE_N];
+#endif
+
 template <int CS, int TPW>
 __global__ void __launch_bounds__(MS_NTH) pwg_mstack_kernel(const MstackArgs a) {
   using S = MsShape<CS>;
@@ -161,11 +176,21 @@ __global__ void __launch_bounds__(MS_NTH) pwg_mstack_kernel(const MstackArgs a) 
   // step s -> ring slot s % P: stack s / SPS, then SA conv-A steps (channel block r / (3 / G), its
   // taps G (r % (3 / G)) .. + G - 1) and SB 1x1 steps (chunks G (r - SA) .. + G - 1)
   const int n_steps = ns * S::SPS;
+  // every per-stack value the loop needs, in registers before the first barrier: the barriers'
+  // and waits' memory clobbers would otherwise reload them from the kernel arguments (a scalar
+  // load round trip) in every step
+  const float* wA_[MS_MAX];
+  const float* wB_[MS_MAX];
+#pragma unroll
+  for (int k = 0; k < MS_MAX; ++k) {
+    wA_[k] = a.st[k].wA;
+    wB_[k] = a.st[k].wB;
+  }
   auto issue = [&](int s) {
     const int j = s / S::SPS, r = s - j * S::SPS;
     unsigned char* const slot = ring + (size_t)(s % P) * S::SLOT;
-    const float* const wa = a.st[j].wA;
-    const float* const wb = a.st[j].wB;
+    const float* const wa = j == 0 ? wA_[0] : j == 1 ? wA_[1] : j == 2 ? wA_[2] : wA_[3];
+    const float* const wb = j == 0 ? wB_[0] : j == 1 ? wB_[1] : j == 2 ? wB_[2] : wB_[3];
 #pragma unroll
     for (int k = 0; k < S::D; ++k) {
       const int i = wave + MS_NWV * k < S::NI ? wave + MS_NWV * k : S::NI - 1;
@@ -187,6 +212,16 @@ __global__ void __launch_bounds__(MS_NTH) pwg_mstack_kernel(const MstackArgs a) 
   };
 
   ms_f32x16 accA[TPW][MT], accB[TPW][MT];
+#ifdef PWG_MSTACK_PROBE
+  const bool probe = blockIdx.x == 0 && threadIdx.x == 0;
+  int np = 1;
+  auto stamp = [&] {
+    if (probe && np < MS_PROBE_N) g_ms_probe[np++] = __builtin_readcyclecounter();
+  };
+#else
+  auto stamp = [] {};
+#endif
+  stamp();
   __syncthreads();  // biases in LDS (ordinary loads and stores, done before the first LDS copy)
   // the input tile: 1-KB copies of consecutive LDS bytes, each lane's 16 B from its row / quad
   // (pad quads and rows outside the utterance copy a harmless in-bounds quad)
@@ -204,95 +239,137 @@ __global__ void __launch_bounds__(MS_NTH) pwg_mstack_kernel(const MstackArgs a) 
     }
   }
 
-  for (int s = 0; s < P - 1 && s < n_steps; ++s) issue(s);
-  // one step: its fragments (and the input tile) landed -- the steps issued after it may still be
-  // in flight --, every wave is past the previous step (whose slot the next issue refills)
+  // Software-pipelined steps: the operands of step s + 1 (A fragments and B rows from LDS,
+  // pre-activation, pair split) are prepared while step s's MFMAs run, so one wave per SIMD keeps
+  // its matrix pipe fed (a step's MFMAs are ~0.6k cycles, its operand work ~1.5k, and serially they
+  // took ~2.5k cycles per step, tools/diag/mstack_probe.py). Step s + 1's fragments must therefore
+  // be visible before step s computes: the ring holds P steps, step s + P issues once every wave has
+  // prepared step s.
+  for (int s0 = 0; s0 < P && s0 < n_steps; ++s0) issue(s0);
   int s = 0;
-  auto step_begin = [&]() {
-    ms_vm_wait_steps<S::D, P - 2>(n_steps - 1 - s);
+  // step s + 1 landed and visible (the steps issued after it may still be in flight); every wave
+  // has prepared step s, so step s's slot takes step s + P
+  auto advance = [&]() {
+    stamp();  // (probe: previous step's work issued)
+    if (s + 1 < n_steps) ms_vm_wait_steps<S::D, P - 2>(n_steps - 2 - s);
+    stamp();
     barrier();
-    if (s + P - 1 < n_steps) issue(s + P - 1);
-    return reinterpret_cast<const ms_u32x4*>(ring + (size_t)(s % P) * S::SLOT) + lane;
+    stamp();
+    if (s + P < n_steps) issue(s + P);
   };
   constexpr int G = S::G;
-  for (int j = 0; j < ns; ++j) {
-    const MsStack& st = a.st[j];
-    const int i0 = a.halo - hout[j];                // first tile row stack j produces
-    const int nt = (a.oc + 2 * hout[j] + 31) >> 5;  // its 32-column tiles
+  int dil_[MS_MAX], pad_[MS_MAX], mode_[MS_MAX];
+  float slopeA_[MS_MAX], slopeH_[MS_MAX];
+#pragma unroll
+  for (int k = 0; k < MS_MAX; ++k) {
+    dil_[k] = a.st[k].dil;
+    pad_[k] = a.st[k].pad;
+    mode_[k] = a.st[k].mode;
+    slopeA_[k] = a.st[k].slopeA;
+    slopeH_[k] = a.st[k].slopeH;
+  }
+  // one step's operands: A fragments of its G units, B (hi, lo) per tile and unit
+  ms_u32x4 ah[G][MT], al[G][MT], bh[TPW][G], bl[TPW][G];
+  auto load_a = [&](int step) {
+    const ms_u32x4* const sa = reinterpret_cast<const ms_u32x4*>(ring + (size_t)(step % P) * S::SLOT) + lane;
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        ah[g][m] = sa[(g * MT * 2 + m * 2) * 64];
+        al[g][m] = sa[(g * MT * 2 + m * 2 + 1) * 64];
+      }
+  };
+  auto pin_ops = [&]() {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        ms_pin(ah[g][m]);
+        ms_pin(al[g][m]);
+      }
+#pragma unroll
+      for (int n = 0; n < TPW; ++n) {
+        ms_pin(bh[n][g]);
+        ms_pin(bl[n][g]);
+      }
+    }
+  };
+  int trow[TPW][3];  // conv A's tap rows of this lane's tiles (edge mode applied, x LDX)
+  bool tok[TPW][3];  // ... and their zero masks: the same in every channel block
+  int i0 = 0, nt = 0, dil = 1, pad = 0, mode = 0;
+  float slopeA = 1.f, slopeH = 1.f;
+  auto stack_setup = [&](int j) {
+    auto pick = [&](const auto& arr) { return j == 0 ? arr[0] : j == 1 ? arr[1] : j == 2 ? arr[2] : arr[3]; };
+    dil = pick(dil_); pad = pick(pad_); mode = pick(mode_);
+    slopeA = pick(slopeA_); slopeH = pick(slopeH_);
+    i0 = a.halo - hout[j];                // first tile row stack j produces
+    nt = (a.oc + 2 * hout[j] + 31) >> 5;  // its 32-column tiles
+#pragma unroll
+    for (int n = 0; n < TPW; ++n)
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        int p = c0col + i0 + 32 * (wave + MS_NWV * n) + cl - pad + t * dil;
+        tok[n][t] = ms_edge(p, T, mode);
+        int ir = p - c0col;
+        trow[n][t] = (ir < 0 ? 0 : (ir >= xw ? xw - 1 : ir)) * LDX;
+      }
 #pragma unroll
     for (int n = 0; n < TPW; ++n)
 #pragma unroll
       for (int m = 0; m < MT; ++m)
 #pragma unroll
         for (int e = 0; e < 16; ++e) accA[n][m][e] = accB[n][m][e] = 0.f;
-    // ---- conv A: channel block cb, taps t0 .. t0 + G - 1 per step (pwg_cnet_xtile_kernel's order)
-    for (int r = 0; r < S::SA; ++r, ++s) {
-      const ms_u32x4* const sa = step_begin();
-      const int cb = r / (3 / G), t0 = G * (r - cb * (3 / G));
-      ms_u32x4 ah[G][MT], al[G][MT];
+  };
+  // conv A step r: channel block cb, taps t0 .. t0 + G - 1 (pwg_cnet_xtile_kernel's order). Tiles
+  // past the stack's range compute garbage that is never stored (no branch: the preparation and
+  // the MFMAs stay one scheduling region)
+  auto prep_conv = [&](int step, int r) {
+    load_a(step);
+    const int cb = r / (3 / G), t0 = G * (r - cb * (3 / G));
+#pragma unroll
+    for (int n = 0; n < TPW; ++n)
+#pragma unroll
+      for (int t = 0; t < G; ++t) {
+        const int tt = G == 3 ? t : t0;  // (G = 1: the step's one tap)
+        const int tr = G == 3 ? trow[n][t] : (tt == 0 ? trow[n][0] : tt == 1 ? trow[n][1] : trow[n][2]);
+        const bool ok = G == 3 ? tok[n][t] : (tt == 0 ? tok[n][0] : tt == 1 ? tok[n][1] : tok[n][2]);
+        const float* xr = sx + tr + 16 * cb + 8 * hh;
+        const ms_f32x4 v0 = *reinterpret_cast<const ms_f32x4*>(xr), v1 = *reinterpret_cast<const ms_f32x4*>(xr + 4);
+        ms_f32x8 x = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = ok ? ms_lrelu(x[e], slopeA) : 0.f;
+        ms_split8(x, bh[n][t], bl[n][t]);
+      }
+    pin_ops();
+  };
+  auto mma_conv = [&]() {
+#pragma unroll
+    for (int n = 0; n < TPW; ++n)
 #pragma unroll
       for (int t = 0; t < G; ++t)
 #pragma unroll
-        for (int m = 0; m < MT; ++m) {
-          ah[t][m] = sa[(t * MT * 2 + m * 2) * 64];
-          al[t][m] = sa[(t * MT * 2 + m * 2 + 1) * 64];
-        }
-#pragma unroll
-      for (int n = 0; n < TPW; ++n) {
-        const int tile = wave + MS_NWV * n;
-        if (tile >= nt) break;
-        const int i = i0 + 32 * tile + cl;  // this lane's tile row
-        ms_u32x4 bh[G], bl[G];
-#pragma unroll
-        for (int t = 0; t < G; ++t) {
-          int p = c0col + i - st.pad + (t0 + t) * st.dil;
-          const bool ok = ms_edge(p, T, st.mode);
-          int ir = p - c0col;
-          ir = ir < 0 ? 0 : (ir >= xw ? xw - 1 : ir);
-          const float* xr = sx + (size_t)ir * LDX + 16 * cb + 8 * hh;
-          const ms_f32x4 v0 = *reinterpret_cast<const ms_f32x4*>(xr), v1 = *reinterpret_cast<const ms_f32x4*>(xr + 4);
-          ms_f32x8 x = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-          if (st.slopeA != 1.f) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) x[e] = x[e] > 0.f ? x[e] : x[e] * st.slopeA;
-          }
-          if (!ok) x = ms_f32x8{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-          ms_split8(x, bh[t], bl[t]);
-        }
-#pragma unroll
-        for (int t = 0; t < G; ++t)
-#pragma unroll
-          for (int m = 0; m < MT; ++m) accA[n][m] = ms_mma3(ah[t][m], al[t][m], bh[t], bl[t], accA[n][m]);
-      }
-    }
-    // ---- the 1x1 over [lrelu(h); x_j]: chunks G kg .. + G - 1 of [h blocks][x blocks] per step
-    // (kg and the chunks are compile-time, so h's accumulator registers are indexed statically)
-    const float slopeH = st.slopeH;
+        for (int m = 0; m < MT; ++m) accA[n][m] = ms_mma3(ah[t][m], al[t][m], bh[n][t], bl[n][t], accA[n][m]);
+  };
+  // the 1x1 over [lrelu(h); x_j], step kg: chunks G kg .. + G - 1 of [h blocks][x blocks], compile-
+  // time (h's accumulator registers are indexed statically)
+  auto prep_mm1 = [&](int step, int j, auto kgc) {
+    constexpr int kg = decltype(kgc)::value;
+    load_a(step);
     const float* const bA = sb + (size_t)j * 2 * C;
-    ms_static_for<0, S::SB>([&](auto kgc) {
-      constexpr int kg = decltype(kgc)::value;
-      const ms_u32x4* const sa = step_begin();
-      ms_static_for<0, G>([&](auto gc) {
-        constexpr int g = decltype(gc)::value;
-        constexpr int ch = G * kg + g;
-        if constexpr (ch < 2 * CS) {
-        ms_u32x4 ah[MT], al[MT];
-#pragma unroll
-        for (int m = 0; m < MT; ++m) {
-          ah[m] = sa[(g * MT * 2 + m * 2) * 64];
-          al[m] = sa[(g * MT * 2 + m * 2 + 1) * 64];
-        }
+    ms_static_for<0, G>([&](auto gc) {
+      constexpr int g = decltype(gc)::value;
+      constexpr int ch = G * kg + g;
+      if constexpr (ch < 2 * CS) {
 #pragma unroll
         for (int n = 0; n < TPW; ++n) {
-          const int tile = wave + MS_NWV * n;
-          if (tile >= nt) break;
           ms_f32x8 x;
           if constexpr (ch < CS) {
             // h channels 16 ch .. + 15 from conv A's accumulators: lane half hh needs rows
             // 8 (J0 + hh) + 0..7, i.e. rows 8 (J0 + hh) + 0..3 (j4 = J0 + hh of half 0) and + 4..7
             // (the same j4 of half 1). With A = acc[j4 = J0], B = acc[j4 = J0 + 1] (rows + 4 hh):
-            // half 0 takes (A, A of half 1), half 1 (B of half 0, B): one cross-half exchange of each
-            // (the selects pick between two values, never between accumulator registers)
+            // half 0 takes (A, A of half 1), half 1 (B of half 0, B): one cross-half exchange of
+            // each (the selects pick between two values, never between accumulator registers)
             constexpr int mh = ch >> 1, J0 = (ch & 1) * 2;
             const float* bb = bA + 16 * ch + 8 * hh;
 #pragma unroll
@@ -302,28 +379,59 @@ __global__ void __launch_bounds__(MS_NTH) pwg_mstack_kernel(const MstackArgs a) 
               x[e] = (hh ? xb : va) + bb[e];
               x[4 + e] = (hh ? vb : xa) + bb[4 + e];
             }
-            if (slopeH != 1.f) {
 #pragma unroll
-              for (int e = 0; e < 8; ++e) x[e] = x[e] > 0.f ? x[e] : x[e] * slopeH;
-            }
+            for (int e = 0; e < 8; ++e) x[e] = ms_lrelu(x[e], slopeH);
           } else {
-            const int i = i0 + 32 * tile + cl;
+            const int i = i0 + 32 * (wave + MS_NWV * n) + cl;
             const int ir = i < xw ? i : xw - 1;
             const float* xr = sx + (size_t)ir * LDX + 16 * (ch - CS) + 8 * hh;
             const ms_f32x4 v0 = *reinterpret_cast<const ms_f32x4*>(xr), v1 = *reinterpret_cast<const ms_f32x4*>(xr + 4);
             x = ms_f32x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
           }
-          ms_u32x4 bh, bl;
-          ms_split8(x, bh, bl);
+          ms_split8(x, bh[n][g], bl[n][g]);
+        }
+      }
+    });
+    pin_ops();
+  };
+  auto mma_mm1 = [&](auto kgc) {
+    constexpr int kg = decltype(kgc)::value;
+    ms_static_for<0, G>([&](auto gc) {
+      constexpr int g = decltype(gc)::value;
+      if constexpr (G * kg + g < 2 * CS) {
 #pragma unroll
-          for (int m = 0; m < MT; ++m) accB[n][m] = ms_mma3(ah[m], al[m], bh, bl, accB[n][m]);
-        }
-        }
-      });
+        for (int n = 0; n < TPW; ++n)
+#pragma unroll
+          for (int m = 0; m < MT; ++m) accB[n][m] = ms_mma3(ah[g][m], al[g][m], bh[n][g], bl[n][g], accB[n][m]);
+      }
+    });
+  };
+
+  // prologue: step 0 (and the input tile) landed, its operands prepared
+  ms_vm_wait_steps<S::D, P - 1>(n_steps - 1);
+  barrier();
+  stack_setup(0);
+  prep_conv(0, 0);
+  for (int j = 0; j < ns; ++j) {
+    // (no branch between a step's MFMAs and the next step's preparation: one scheduling region)
+    for (int r = 0; r + 1 < S::SA; ++r, ++s) {
+      advance();
+      mma_conv();
+      prep_conv(s + 1, r + 1);
+    }
+    advance();
+    mma_conv();
+    prep_mm1(s + 1, j, std::integral_constant<int, 0>{});  // waits for conv A's last MFMAs
+    ++s;
+    ms_static_for<0, S::SB>([&](auto kgc) {
+      constexpr int kg = decltype(kgc)::value;
+      advance();
+      mma_mm1(kgc);
+      if constexpr (kg + 1 < S::SB) prep_mm1(s + 1, j, std::integral_constant<int, kg + 1>{});
       ++s;
     });
-    // ---- epilogue of stack j: x_j+1 = acc + b into the tile (own columns; the conv of stack j + 1
-    // reads it after the next step's barrier), or, for the last stack, y
+    // ---- epilogue of stack j: x_j+1 = acc + b into the tile (own columns), or, for the last
+    // stack, y; then every wave's tile rows are visible before the next stack's first operands
     const float* const bB = sb + (size_t)j * 2 * C + C;
     const bool last = j == ns - 1;
 #pragma unroll
@@ -347,7 +455,16 @@ __global__ void __launch_bounds__(MS_NTH) pwg_mstack_kernel(const MstackArgs a) 
           *reinterpret_cast<ms_f32x4*>(dst + row) = v;
         }
     }
+    if (j + 1 < ns) {
+      barrier();
+      stack_setup(j + 1);
+      prep_conv(s, 0);
+    }
   }
+#ifdef PWG_MSTACK_PROBE
+  stamp();
+  if (probe) g_ms_probe[0] = (unsigned long long)np | ((unsigned long long)n_steps << 16) | ((unsigned long long)CS << 32);
+#endif
 }
 
 template <int CS, int TPW>
@@ -396,3 +513,10 @@ hipError_t launch_mstack(const MstackArgs& a, int cs, int tpw, int n_blocks, hip
 }
 
 }  // namespace pwg
+
+#ifdef PWG_MSTACK_PROBE
+extern "C" __attribute__((visibility("default"))) int pwg_mstack_debug_probe(unsigned long long* out, int n) {
+  if (!out || n < pwg::MS_PROBE_N) return 1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(pwg::g_ms_probe), sizeof(unsigned long long) * pwg::MS_PROBE_N) == hipSuccess ? 0 : 3;
+}
+#endif
