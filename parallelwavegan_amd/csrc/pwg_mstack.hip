@@ -41,10 +41,12 @@ typedef _Float16 ms_f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 ms_f16x2 __attribute__((ext_vector_type(2)));
 
 constexpr int MS_NWV = 4, MS_NTH = 64 * MS_NWV;  // waves / threads per workgroup
+constexpr int MS_CROW = 80;  // bytes per converted tile row (32 hi + 32 lo + pad: lanes on other banks)
 // weight ring slots: P - 1 steps in flight. A step's MFMAs (~0.4 us) are far shorter than a
 // fragment copy's round trip, so the ring runs deep: 3 slots measured 2.85 us per step on
-// MB-MelGAN v2's 96-channel chain (the copy latency, profiles/r05_c)
-__host__ __device__ constexpr int ms_ring(int mt) { return mt <= 3 ? 6 : 4; }
+// MB-MelGAN v2's 96-channel chain (the copy latency,
+// profiles/r05_c); deepest that fits the LDS beside a 32-column block's tile and converted blocks
+__host__ __device__ constexpr int ms_ring(int mt) { return mt <= 2 ? 6 : mt == 3 ? 5 : 3; }
 // fragment units per step (taps of one conv-A channel block, or 1x1 chunks): 3, or 1 at 6 m-tiles
 // (192 channels), whose 3-unit slots would not fit the LDS beside the 192-channel input tile
 __host__ __device__ constexpr int ms_units(int mt) { return mt <= 4 ? 3 : 1; }
@@ -149,7 +151,10 @@ __global__ void __launch_bounds__(MS_NTH) pwg_mstack_kernel(const MstackArgs a) 
   constexpr int P = S::P;
   float* const sx = reinterpret_cast<float*>(ms_smem + P * S::SLOT);
   const int xw = a.oc + 2 * a.halo;           // tile rows: utterance columns c0col .. c0col + xw - 1
-  float* const sb = sx + (size_t)xw * LDX;    // [stack][b_A | b] (2 C floats each)
+  // conv A's B operands of one channel block, pre-activated and pair-split ONCE per workgroup for
+  // all taps and waves: [2 blocks][xw rows][hi 16 f16 | lo 16 f16 | 16-B pad]
+  unsigned char* const cbuf = reinterpret_cast<unsigned char*>(sx + (size_t)xw * LDX);
+  float* const sb = reinterpret_cast<float*>(cbuf + (size_t)2 * xw * MS_CROW);  // [stack][b_A | b]
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int hh = lane >> 5, cl = lane & 31;
@@ -295,8 +300,7 @@ __global__ void __launch_bounds__(MS_NTH) pwg_mstack_kernel(const MstackArgs a) 
       }
     }
   };
-  int trow[TPW][3];  // conv A's tap rows of this lane's tiles (edge mode applied, x LDX)
-  bool tok[TPW][3];  // ... and their zero masks: the same in every channel block
+  int trow[TPW][3];  // conv A's tap rows of this lane's tiles in a converted block (x MS_CROW)
   int i0 = 0, nt = 0, dil = 1, pad = 0, mode = 0;
   float slopeA = 1.f, slopeH = 1.f;
   auto stack_setup = [&](int j) {
@@ -309,10 +313,12 @@ __global__ void __launch_bounds__(MS_NTH) pwg_mstack_kernel(const MstackArgs a) 
     for (int n = 0; n < TPW; ++n)
 #pragma unroll
       for (int t = 0; t < 3; ++t) {
-        int p = c0col + i0 + 32 * (wave + MS_NWV * n) + cl - pad + t * dil;
-        tok[n][t] = ms_edge(p, T, mode);
-        int ir = p - c0col;
-        trow[n][t] = (ir < 0 ? 0 : (ir >= xw ? xw - 1 : ir)) * LDX;
+        // a zero-padded tap outside the utterance reads its own (converted-to-zero) tile row: the
+        // taps of every stored column stay inside the tile (the halo); later tiles are garbage
+        const int pu = c0col + i0 + 32 * (wave + MS_NWV * n) + cl - pad + t * dil;
+        int p = pu;
+        const int ir = (ms_edge(p, T, mode) ? p : pu) - c0col;
+        trow[n][t] = (ir < 0 ? 0 : (ir >= xw ? xw - 1 : ir)) * MS_CROW;
       }
 #pragma unroll
     for (int n = 0; n < TPW; ++n)
@@ -321,25 +327,39 @@ __global__ void __launch_bounds__(MS_NTH) pwg_mstack_kernel(const MstackArgs a) 
 #pragma unroll
         for (int e = 0; e < 16; ++e) accA[n][m][e] = accB[n][m][e] = 0.f;
   };
-  // conv A step r: channel block cb, taps t0 .. t0 + G - 1 (pwg_cnet_xtile_kernel's order). Tiles
-  // past the stack's range compute garbage that is never stored (no branch: the preparation and
-  // the MFMAs stay one scheduling region)
-  auto prep_conv = [&](int step, int r) {
+  // channel block cb of x_j for conv A, every tile row: lrelu (or 0 for a zero-padded row outside
+  // the utterance: the executor's masked tap) and the pair split, into converted block cb & 1
+  auto convert = [&](int cb) {
+    unsigned char* const cv = cbuf + (size_t)(cb & 1) * xw * MS_CROW;
+    for (int k = threadIdx.x; k < 2 * xw; k += MS_NTH) {
+      const int i = k >> 1, hf = k & 1;
+      const float* xr = sx + (size_t)i * LDX + 16 * cb + 8 * hf;
+      const ms_f32x4 v0 = *reinterpret_cast<const ms_f32x4*>(xr), v1 = *reinterpret_cast<const ms_f32x4*>(xr + 4);
+      ms_f32x8 x = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      const int c = c0col + i;
+      const bool z = mode == PWG_PAD_ZERO && (c < 0 || c >= T);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = z ? 0.f : ms_lrelu(x[e], slopeA);
+      ms_u32x4 h, l;
+      ms_split8(x, h, l);
+      *reinterpret_cast<ms_u32x4*>(cv + (size_t)i * MS_CROW + 16 * hf) = h;
+      *reinterpret_cast<ms_u32x4*>(cv + (size_t)i * MS_CROW + 32 + 16 * hf) = l;
+    }
+  };
+  // conv A step r: channel block cb, taps t0 .. t0 + G - 1 (pwg_cnet_xtile_kernel's order), B read
+  // straight from the converted block. Tiles past the stack's range compute garbage that is never
+  // stored (no branch: the loads and the MFMAs stay one scheduling region)
+  auto load_conv = [&](int step, int r) {
     load_a(step);
     const int cb = r / (3 / G), t0 = G * (r - cb * (3 / G));
+    const unsigned char* const cv = cbuf + (size_t)(cb & 1) * xw * MS_CROW + 16 * hh;
 #pragma unroll
     for (int n = 0; n < TPW; ++n)
 #pragma unroll
       for (int t = 0; t < G; ++t) {
-        const int tt = G == 3 ? t : t0;  // (G = 1: the step's one tap)
-        const int tr = G == 3 ? trow[n][t] : (tt == 0 ? trow[n][0] : tt == 1 ? trow[n][1] : trow[n][2]);
-        const bool ok = G == 3 ? tok[n][t] : (tt == 0 ? tok[n][0] : tt == 1 ? tok[n][1] : tok[n][2]);
-        const float* xr = sx + tr + 16 * cb + 8 * hh;
-        const ms_f32x4 v0 = *reinterpret_cast<const ms_f32x4*>(xr), v1 = *reinterpret_cast<const ms_f32x4*>(xr + 4);
-        ms_f32x8 x = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-#pragma unroll
-        for (int e = 0; e < 8; ++e) x[e] = ok ? ms_lrelu(x[e], slopeA) : 0.f;
-        ms_split8(x, bh[n][t], bl[n][t]);
+        const int tr = G == 3 ? trow[n][t] : (t0 == 0 ? trow[n][0] : t0 == 1 ? trow[n][1] : trow[n][2]);
+        bh[n][t] = *reinterpret_cast<const ms_u32x4*>(cv + tr);
+        bl[n][t] = *reinterpret_cast<const ms_u32x4*>(cv + tr + 32);
       }
     pin_ops();
   };
@@ -407,18 +427,37 @@ __global__ void __launch_bounds__(MS_NTH) pwg_mstack_kernel(const MstackArgs a) 
     });
   };
 
-  // prologue: step 0 (and the input tile) landed, its operands prepared
+  // a stack starts once x_j is in the tile (a barrier): its first two channel blocks converted,
+  // then step s's operands
+  auto begin_stack = [&](int j) {
+    stack_setup(j);
+    convert(0);
+    if constexpr (G == 3) convert(1);
+    barrier();
+    load_conv(s, 0);
+  };
+  // prologue: step 0 (and the input tile) landed
   ms_vm_wait_steps<S::D, P - 1>(n_steps - 1);
   barrier();
-  stack_setup(0);
-  prep_conv(0, 0);
+  begin_stack(0);
   for (int j = 0; j < ns; ++j) {
-    // (no branch between a step's MFMAs and the next step's preparation: one scheduling region)
-    for (int r = 0; r + 1 < S::SA; ++r, ++s) {
+    // step r: its MFMAs, then step r + 1's operands and step r + 2's channel block (into the
+    // converted block step r read from, free once every wave passed this step's barrier). No
+    // branch between a step's MFMAs and the next step's loads: one scheduling region
+    for (int r = 0; r + 2 < S::SA; ++r, ++s) {
       advance();
       mma_conv();
-      prep_conv(s + 1, r + 1);
+      load_conv(s + 1, r + 1);
+      if constexpr (G == 3) {
+        convert(r + 2);
+      } else {
+        if ((r + 2) % 3 == 0) convert((r + 2) / 3);
+      }
     }
+    advance();
+    mma_conv();
+    load_conv(s + 1, S::SA - 1);
+    ++s;
     advance();
     mma_conv();
     prep_mm1(s + 1, j, std::integral_constant<int, 0>{});  // waits for conv A's last MFMAs
@@ -457,8 +496,7 @@ __global__ void __launch_bounds__(MS_NTH) pwg_mstack_kernel(const MstackArgs a) 
     }
     if (j + 1 < ns) {
       barrier();
-      stack_setup(j + 1);
-      prep_conv(s, 0);
+      begin_stack(j + 1);
     }
   }
 #ifdef PWG_MSTACK_PROBE
@@ -480,7 +518,8 @@ hipError_t ms_go(const MstackArgs& a, int n_blocks, hipStream_t s) {
 
 int mstack_lds(int cs, int oc, int halo, int ns) {
   const int mt = (cs + 1) / 2;
-  return ms_ring(mt) * ms_units(mt) * mt * 2 * 1024 + (oc + 2 * halo) * (16 * cs + 4) * 4 + ns * 2 * 16 * cs * 4;
+  return ms_ring(mt) * ms_units(mt) * mt * 2 * 1024 + (oc + 2 * halo) * ((16 * cs + 4) * 4 + 2 * MS_CROW) +
+         ns * 2 * 16 * cs * 4;
 }
 
 // accumulators: 2 x TPW x MT x 16 VGPRs; TPW x MT <= 4 (or one tile of 192 channels, one fragment unit
