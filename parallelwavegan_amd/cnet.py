@@ -568,6 +568,14 @@ class CnetEngine:
         self._graph_epoch += 1
         self._plans.clear()
 
+    def set_presplit(self, enable):
+        """pwg_cnet_set_option(PWG_CNET_OPT_PRESPLIT): DMA-ring launches write pre-split images of
+        the buffers other DMA-ring launches read, which stage them as they are (default) or, 0,
+        every reader converts its fp32 rows. Plan-time (cached plans are dropped); bit-identical."""
+        _lib.check(self._lib.pwg_cnet_set_option(self._h, 10, 1 if enable else 0))
+        self._graph_epoch += 1
+        self._plans.clear()
+
     def set_narrow_dma(self, enable):
         """pwg_cnet_set_option(PWG_CNET_OPT_NARROW_DMA): narrow launches on the DMA-ring kernel
         (default) or, 0, on the narrow x-tile / tap-major kernels. Plan-time (cached plans are

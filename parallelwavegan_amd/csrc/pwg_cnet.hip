@@ -1005,7 +1005,18 @@ struct CnXdmaArgs {
   int probe_slot; // PWG_XDMA_PROBE builds only (timeline of workgroup 0, tools/diag/xdma_probe.py)
   const int2* bfr;  // per block: (first frame, frames) of its utterance
   int rate[2], rate_dst, rate_res;  // rows per frame of the sources', destination and residual buffers
+  // Pre-split activation images (PWG_CNET_OPT_PRESPLIT): a buffer's rows as [16-channel block][hi 16
+  // f16 | lo 16 f16] (64 B per block, row = channels x 4 B), the consumer's LeakyReLU applied before
+  // the pair split. PRE launches DMA their B rows from simg (no per-step conversion); any launch
+  // writes n_oimg images of its output rows beside the fp32 store (quad epilogue path).
+  const unsigned char* simg[2];
+  int simg_rowb[2];
+  unsigned char* oimg[2];
+  float oslope[2];
+  int n_oimg, oimg_rowb;
 };
+// 16 zero bytes: the DMA source of a pre-split row outside a zero-padded utterance
+__device__ __attribute__((aligned(64))) unsigned g_cn_zero16[16];
 constexpr int XDMA_CHUNKS_MAX = 256;  // K = 1 mode: chunks per op (the table sits in LDS)
 #ifndef PWG_XDMA_K1_G
 #define PWG_XDMA_K1_G 4
@@ -1019,7 +1030,7 @@ constexpr int XDMA_RING_CAP = PWG_XDMA_RING_CAP;  // ring slots at most (see Xdm
 constexpr int XDMA_PROBE_SLOTS = 128, XDMA_PROBE_N = 96;
 __device__ unsigned long long g_xdma_probe[XDMA_PROBE_SLOTS][XDMA_PROBE_N];
 #endif
-template <int K, int MT, int NWV>
+template <int K, int MT, int NWV, bool PRE = false>
 struct XdmaShape {
   static constexpr int XC = 32 * NWV;
   // raw input rows per step: the tile + the taps' reach (ConvTranspose phases, K = 2: one row)
@@ -1028,12 +1039,18 @@ struct XdmaShape {
   // round trip cover G chunks' few MFMAs
   static constexpr int G = K == 1 ? XDMA_K1_G : 1;
   static constexpr int KT = K == 1 ? G : K;                    // A fragments (taps / chunks) per step
-  static constexpr int NA = KT * MT * 2, NX = G * XR / 16;     // 1-KB DMA instructions per step
-  static constexpr int DA = (NA + NWV - 1) / NWV, DX = (NX + NWV - 1) / NWV;  // ... per wave
+  // PRE: a step's rows arrive converted, XT_ROWB apart (a chunk's XC rows / the K > 1 tile's XR rows)
+  static constexpr int CHI = (XC * XT_ROWB + 1023) / 1024;     // PRE, K = 1: instructions per chunk
+  static constexpr int NA = KT * MT * 2;                       // 1-KB DMA instructions per step
+  static constexpr int NX = PRE ? (K == 1 ? G * CHI : (XR * XT_ROWB + 1023) / 1024) : G * XR / 16;
+  // PRE, K = 1: wave w copies instructions w, w + NWV, .. of every chunk (JW per chunk, the last
+  // repeated): compile-time chunk indices
+  static constexpr int JW = (CHI + NWV - 1) / NWV;
+  static constexpr int DA = (NA + NWV - 1) / NWV, DX = PRE && K == 1 ? G * JW : (NX + NWV - 1) / NWV;  // ... per wave
   static constexpr int D = DA + DX;
-  static constexpr int SLOT = (NX + NA) * 1024;                // raw rows, then A fragments
-  // K > 1: two converted-row buffers; K = 1: none (B split in registers) but the chunk table
-  static constexpr int CBUF = K == 1 ? 0 : XR * XT_ROWB;
+  static constexpr int SLOT = (NX + NA) * 1024;                // rows, then A fragments
+  // K > 1: two converted-row buffers (not PRE); K = 1: none (B split in registers) but the chunk table
+  static constexpr int CBUF = (K == 1 || PRE) ? 0 : XR * XT_ROWB;
   static constexpr int CHT = K == 1 ? XDMA_CHUNKS_MAX * (int)sizeof(ChunkDesc) : 0;
   // deepest ring (<= XDMA_RING_CAP slots) whose wait counts fit vmcnt (63) and LDS 159 KB
   static constexpr int ring(int p) {
@@ -1066,9 +1083,9 @@ __device__ __forceinline__ void vm_wait_steps(int r) {
   }
 }
 
-template <int K, int MT, int NWV>
+template <int K, int MT, int NWV, bool PRE>
 __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArgs a, const CnXdmaArgs xd) {
-  using S = XdmaShape<K, MT, NWV>;
+  using S = XdmaShape<K, MT, NWV, PRE>;
   constexpr int NTH = 64 * NWV, P = S::P;
   constexpr int NQ = (S::XR * 4 + NTH - 1) / NTH;  // raw 16-B quads converted per thread and step
   extern __shared__ __attribute__((aligned(16))) unsigned char xt_smem[];
@@ -1130,7 +1147,34 @@ __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArg
   const int off0 = xd.z_off[zp];
   int xoff[S::DX];
   unsigned okm = 0;
-  if constexpr (K > 1) {
+  // PRE, K > 1: each lane's 16 B of instruction k is (tile row r, piece q) of the XT_ROWB-strided
+  // rows (q = 4, the pad, and rows past the span repeat an in-bounds piece); the image byte offset of
+  // that piece in channel block 0, or -1 for a zero-padded row (the zero page)
+  long long pxo[PRE && K > 1 ? S::DX : 1];
+  int prow[PRE && K == 1 ? S::JW : 1], pq16[PRE && K == 1 ? S::JW : 1];  // PRE, K = 1: (row, piece) per jj
+  if constexpr (PRE && K == 1) {
+#pragma unroll
+    for (int jj = 0; jj < S::JW; ++jj) {
+      const int j = wave + NWV * jj < S::CHI ? wave + NWV * jj : S::CHI - 1;
+      const int o = j * 1024 + lane * 16;
+      const int r = o / XT_ROWB, q = (o - r * XT_ROWB) >> 4;
+      prow[jj] = r < S::XC ? r : S::XC - 1;
+      pq16[jj] = q < 4 ? q * 16 : 0;
+    }
+  }
+  if constexpr (PRE && K > 1) {
+#pragma unroll
+    for (int k = 0; k < S::DX; ++k) {
+      const int i = wave + NWV * k < S::NX ? wave + NWV * k : S::NX - 1;
+      const int o = i * 1024 + lane * 16;
+      int r = o / XT_ROWB, q = (o - r * XT_ROWB) >> 4;
+      q = q < 4 ? q : 0;
+      r = r < span ? r : span - 1;
+      int p = q0 + off0 + r;
+      const bool ok = edge_row(p, sgy0, s0.pad_mode);
+      pxo[k] = ok ? (long long)(sgx0 + p) * xd.simg_rowb[0] + q * 16 : -1;
+    }
+  } else if constexpr (K > 1) {
 #pragma unroll
     for (int k = 0; k < S::DX; ++k) {
       const int i = wave + NWV * k < S::NX ? wave + NWV * k : S::NX - 1;
@@ -1174,7 +1218,35 @@ __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArg
       const float* src = wfrag_ + ((size_t)chunk * a.mt_total + m0) * 512 + j * 256;
       __builtin_amdgcn_global_load_lds((gptr_t)(src + lane * 4), (lptr_t)(slot + (S::NX + i) * 1024), 16, 0, 0);
     }
-    if constexpr (K > 1) {
+    if constexpr (PRE && K > 1) {
+      const unsigned char* const xs = xd.simg[0] + 64 * s;
+#pragma unroll
+      for (int k = 0; k < S::DX; ++k) {
+        const int i = wave + NWV * k < S::NX ? wave + NWV * k : S::NX - 1;
+        const void* src = pxo[k] >= 0 ? (const void*)(xs + pxo[k]) : (const void*)g_cn_zero16;
+        __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(slot + i * 1024), 16, 0, 0);
+      }
+    } else if constexpr (PRE) {
+      // K = 1: chunk t's XC rows are instructions t CHI .. + CHI - 1, each lane's 16 B a (row,
+      // piece) of the XT_ROWB-strided rows, read from its source's image at the chunk's channels
+#pragma unroll
+      for (int t = 0; t < S::G; ++t) {
+        const ChunkDesc cd = chunk(min(s * S::G + t, nch - 1));
+        const bool s1 = cd.src != 0;  // (uniform: scalar selects, no indexed source array)
+        const unsigned char* const img = (s1 ? xd.simg[1] : xd.simg[0]) + cd.c0 * 4;
+        const int rowb = s1 ? xd.simg_rowb[1] : xd.simg_rowb[0];
+        const int sgx = s1 ? sgx1 : sgx0, sgy = s1 ? sgy1 : sgy0;
+        const int pm = s1 ? a.src[1].pad_mode : a.src[0].pad_mode;
+#pragma unroll
+        for (int jj = 0; jj < S::JW; ++jj) {
+          const int j = wave + NWV * jj < S::CHI ? wave + NWV * jj : S::CHI - 1;
+          int p = q0 + cd.row_off + prow[jj];
+          const bool ok = edge_row(p, sgy, pm);
+          const void* src = ok ? (const void*)(img + (long long)(sgx + p) * rowb + pq16[jj]) : (const void*)g_cn_zero16;
+          __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(slot + (t * S::CHI + j) * 1024), 16, 0, 0);
+        }
+      }
+    } else if constexpr (K > 1) {
       const float* const xs = s0.x + 16 * s;
 #pragma unroll
       for (int k = 0; k < S::DX; ++k) {
@@ -1253,13 +1325,20 @@ __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArg
     constexpr int KT = S::KT;
     u32x4v bh[KT], bl[KT], ah[KT][MT], al[KT][MT];
     ChunkDesc cds[S::G];
-    if constexpr (K == 1) {
+    if constexpr (K == 1 && !PRE) {
 #pragma unroll
       for (int t = 0; t < S::G; ++t) cds[t] = chunk(min(g * S::G + t, nch - 1));
     }
 #pragma unroll
     for (int t = 0; t < KT; ++t) {
-      if constexpr (K == 1) {
+      if constexpr (PRE) {
+        // converted rows straight from the step's slot (K = 1: chunk t's rows; K > 1: tap t's row)
+        const unsigned char* row = xt_smem + (size_t)(g % P) * S::SLOT +
+                                   (K == 1 ? t * S::CHI * 1024 + (wave * 32 + cl) * XT_ROWB
+                                           : (wave * 32 + cl + t * xd.dil) * XT_ROWB);
+        bh[t] = *reinterpret_cast<const u32x4v*>(row + 16 * hh);
+        bl[t] = *reinterpret_cast<const u32x4v*>(row + 32 + 16 * hh);
+      } else if constexpr (K == 1) {
         // chunk g G + t: the lane's 8 channels of its raw row, pre-activated and pair-split in
         // registers (pwg_cnet_conv_kernel's bprep + cn_split8)
         const ChunkDesc& cd = cds[t];
@@ -1318,7 +1397,7 @@ __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArg
   for (int s = 0; s < P - 1; ++s)
     if (s < ns) issue(s);
   stamp();
-  if constexpr (K == 1) {
+  if constexpr (K == 1 || PRE) {
     stamp();  // (probe builds: keep the K > 1 timeline's column layout)
     stamp();
     // one barrier per step: after it every wave is done with step g - 1's slot, which the issue of
@@ -1390,6 +1469,23 @@ __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArg
           for (int i = 0; i < 4; ++i)
             if (row + i >= a.M) v[i] = 0.f;
           *reinterpret_cast<f32x4v*>(yrow + row) = v;
+          // pre-split images of these 4 channels for the consumers (the conversion those consumers'
+          // own staging would apply to the stored values: bit-identical)
+          for (int j = 0; j < xd.n_oimg; ++j) {
+            const float sl = xd.oslope[j];
+            _Float16 hv[4], lv[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              float x = v[i];
+              if (sl != 1.f) x = x > 0.f ? x : x * sl;
+              hv[i] = (_Float16)x;
+              lv[i] = (_Float16)(x - (float)hv[i]);
+            }
+            unsigned char* const d = xd.oimg[j] + (long long)(fr.x * xd.rate_dst + t_out) * xd.oimg_rowb +
+                                     (row >> 4) * 64 + (row & 15) * 2;
+            *reinterpret_cast<f16x4v*>(d) = f16x4v{hv[0], hv[1], hv[2], hv[3]};
+            *reinterpret_cast<f16x4v*>(d + 32) = f16x4v{lv[0], lv[1], lv[2], lv[3]};
+          }
         }
     } else {
       cn_store_col<MT>(a, acc, bias_, m0, hh, yrow, rrow);
@@ -1407,36 +1503,44 @@ __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArg
 #endif
 }
 
-template <int K, int MT, int NWV>
+template <int K, int MT, int NWV, bool PRE>
 hipError_t xdma_go(dim3 grid, hipStream_t s, const CnConvArgs& a, const CnXdmaArgs& xd) {
 #ifdef PWG_XDMA_PROBE
-  constexpr int lds = XdmaShape<K, MT, NWV>::LDS + XDMA_PROBE_N * 8;
+  constexpr int lds = XdmaShape<K, MT, NWV, PRE>::LDS + XDMA_PROBE_N * 8;
 #else
-  constexpr int lds = XdmaShape<K, MT, NWV>::LDS;
+  constexpr int lds = XdmaShape<K, MT, NWV, PRE>::LDS;
 #endif
-  const hipError_t e = allow_lds(reinterpret_cast<const void*>(pwg_cnet_xdma_kernel<K, MT, NWV>), lds);
+  const hipError_t e = allow_lds(reinterpret_cast<const void*>(pwg_cnet_xdma_kernel<K, MT, NWV, PRE>), lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((pwg_cnet_xdma_kernel<K, MT, NWV>), grid, dim3(64 * NWV), (size_t)lds, s, a, xd);
+  hipLaunchKernelGGL((pwg_cnet_xdma_kernel<K, MT, NWV, PRE>), grid, dim3(64 * NWV), (size_t)lds, s, a, xd);
   return hipGetLastError();
 }
-template <int MT, int NWV>
+template <int MT, int NWV, bool PRE>
 hipError_t xdma_launch_k(int k, dim3 grid, hipStream_t s, const CnConvArgs& a, const CnXdmaArgs& xd) {
   switch (k) {
-    case 1: return xdma_go<1, MT, NWV>(grid, s, a, xd);
-    case 2: return xdma_go<2, MT, NWV>(grid, s, a, xd);
-    case 3: return xdma_go<3, MT, NWV>(grid, s, a, xd);
-    case 5: return xdma_go<5, MT, NWV>(grid, s, a, xd);
-    case 7: return xdma_go<7, MT, NWV>(grid, s, a, xd);
-    case 11: return xdma_go<11, MT, NWV>(grid, s, a, xd);
+    case 1: return xdma_go<1, MT, NWV, PRE>(grid, s, a, xd);
+    case 2: return xdma_go<2, MT, NWV, PRE>(grid, s, a, xd);
+    case 3: return xdma_go<3, MT, NWV, PRE>(grid, s, a, xd);
+    case 5: return xdma_go<5, MT, NWV, PRE>(grid, s, a, xd);
+    case 7: return xdma_go<7, MT, NWV, PRE>(grid, s, a, xd);
+    case 11: return xdma_go<11, MT, NWV, PRE>(grid, s, a, xd);
     default: return hipErrorInvalidValue;
   }
 }
-// k = 1: K = 1 mode (steps = the tap-major chunk list)
-hipError_t xdma_launch(int mt, int nwv, int k, dim3 grid, hipStream_t s, const CnConvArgs& a, const CnXdmaArgs& xd) {
+// k = 1: K = 1 mode (steps = the tap-major chunk list); pre: B rows from the sources' pre-split
+// images (xd.simg)
+hipError_t xdma_launch(int mt, int nwv, int k, bool pre, dim3 grid, hipStream_t s, const CnConvArgs& a,
+                       const CnXdmaArgs& xd) {
   if (mt != 1) return hipErrorInvalidValue;  // (the plan picks one m-tile per workgroup)
-  if (nwv == 1) return xdma_launch_k<1, 1>(k, grid, s, a, xd);
-  if (nwv == 2) return xdma_launch_k<1, 2>(k, grid, s, a, xd);
-  if (nwv == 4) return xdma_launch_k<1, 4>(k, grid, s, a, xd);
+  if (pre) {
+    if (nwv == 1) return xdma_launch_k<1, 1, true>(k, grid, s, a, xd);
+    if (nwv == 2) return xdma_launch_k<1, 2, true>(k, grid, s, a, xd);
+    if (nwv == 4) return xdma_launch_k<1, 4, true>(k, grid, s, a, xd);
+  } else {
+    if (nwv == 1) return xdma_launch_k<1, 1, false>(k, grid, s, a, xd);
+    if (nwv == 2) return xdma_launch_k<1, 2, false>(k, grid, s, a, xd);
+    if (nwv == 4) return xdma_launch_k<1, 4, false>(k, grid, s, a, xd);
+  }
   return hipErrorInvalidValue;
 }
 
@@ -3244,6 +3348,7 @@ struct PwgCnet {
                        // x-tile / tap-major kernels)
   int mstack = 1;      // PWG_CNET_OPT_MSTACK (plan time): 0 off, 1 fused stack chains in plans whose first
                        // conv of the chain runs narrow, 2 every chain
+  int presplit = 1;    // PWG_CNET_OPT_PRESPLIT (plan time): DMA-ring launches write / read pre-split images
   int streams = 1;     // PWG_CNET_OPT_STREAMS: 0 one stream, 1 independent launches of plans with narrow
                        // launches run on auxiliary streams, 2 every plan
   static constexpr int N_AUX = 3;
@@ -3304,6 +3409,13 @@ struct PwgCnetPlan {
   // per phase: fused stack chain launch (pwg_mstack.hip) when > 0 output columns per block
   std::vector<int> ms_oc, o_msblocks, n_msblocks;
   bool has_narrow = false;                   // some phase runs narrow (PWG_CNET_OPT_STREAMS 1)
+  // pre-split activation images (PWG_CNET_OPT_PRESPLIT): per image its buffer, the consumers'
+  // LeakyReLU slope and workspace offset; per phase (2 pi + k) the images its sources read and its
+  // launch writes (-1 none)
+  std::vector<int> simg_buf;
+  std::vector<float> simg_slope;
+  std::vector<size_t> simg_off;
+  std::vector<int> ph_simg, ph_oimg;
 };
 
 namespace {
@@ -4348,6 +4460,52 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
     p->o_msblocks[pi] = list(CN_L_BLK, rate, 1, 0, oc);
     p->n_msblocks[pi] = (int)count(oc);
   }
+  // Pre-split images: a buffer read by a DMA-ring launch (not inside a fused stack chain) with a
+  // LeakyReLU slope gets an image of its rows pre-activated with that slope and pair-split, written
+  // by its last writer's epilogue when that writer runs on the DMA-ring kernel too (run time decides:
+  // a consumer reads an image only once every launch of the last writer wrote it). At B = 1 every
+  // one of a column block's m-tile workgroups converted the same rows each step (~1k of a step's
+  // ~2.4k cycles, tools/diag/xdma_probe.py). Two images per buffer at most (MelGAN's x_j: conv A's
+  // slope and the 1x1's skip source, slope 1).
+  p->ph_simg.assign(2 * nph, -1);
+  p->ph_oimg.assign(2 * nph, -1);
+  if (n->presplit && n->split_f16 && n->narrow_dma) {
+    std::vector<char> in_chain(nph, 0);
+    for (size_t pi = 0; pi < nph; ++pi)
+      if (cnet_mstack_on(p, pi))
+        for (int k = 0; k < 2 * n->phases[pi].ms_n; ++k) in_chain[pi + k] = 1;
+    std::vector<int> last_wr(nb, -1);
+    for (int oi = 0; oi < nops; ++oi) last_wr[n->ops[oi].dst] = oi;
+    auto xdma_phase = [&](size_t q) { return p->nar_xdma[q] && p->nar_nwv[q] > 0 && !in_chain[q]; };
+    for (size_t pi = 0; pi < nph; ++pi) {
+      if (!xdma_phase(pi)) continue;
+      const PwgCnetOp& op = n->ops[n->phases[pi].op];
+      const int nsrc = p->nar_tap[pi] && op.src[1].buf >= 0 && op.kind == PWG_CNET_CONV ? 2 : 1;
+      for (int si = 0; si < nsrc; ++si) {
+        const PwgCnetSrc& src = op.src[si];
+        const int b = src.buf;
+        if (b <= 0 || b >= nb - 1 || src.normalize || n->channels[b] % 16 != 0 || last_wr[b] < 0) continue;
+        bool writer_dma = false;
+        for (size_t q = 0; q < nph; ++q) writer_dma |= n->phases[q].op == last_wr[b] && xdma_phase(q);
+        if (!writer_dma) continue;
+        int k = -1, per_buf = 0;
+        for (size_t j = 0; j < p->simg_buf.size(); ++j)
+          if (p->simg_buf[j] == b) {
+            ++per_buf;
+            if (p->simg_slope[j] == src.pre_slope) k = (int)j;
+          }
+        if (k < 0) {
+          if (per_buf >= 2) continue;
+          k = (int)p->simg_buf.size();
+          p->simg_buf.push_back(b);
+          p->simg_slope.push_back(src.pre_slope);
+          for (size_t q = 0; q < nph; ++q)
+            if (n->phases[q].op == last_wr[b]) p->ph_oimg[2 * q + (p->ph_oimg[2 * q] < 0 ? 0 : 1)] = k;
+        }
+        p->ph_simg[2 * pi + si] = k;
+      }
+    }
+  }
   for (size_t pi = 0; pi < nph; ++pi) p->has_narrow |= p->nar_nwv[pi] > 0;
   if (n->streams == 2 || (n->streams == 1 && p->has_narrow)) assign_slots(false);
   img_ints = (img_ints + 1) / 2 * 2;  // room for a last odd NCOL list's pad int
@@ -4407,6 +4565,13 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
   }
   p->ws_img = p->ws_bytes;  // after the buffer slots and the flag (256-byte aligned)
   p->ws_bytes = p->ws_img + ((size_t)img_ints * sizeof(int) + 255) / 256 * 256;
+  // the pre-split images, each its own region (live from its writer to its last reader: small
+  // plans only, the DMA-ring kernel runs where its workgroups fit one round over the CUs)
+  for (size_t k = 0; k < p->simg_buf.size(); ++k) {
+    const int b = p->simg_buf[k];
+    p->simg_off.push_back(p->ws_bytes);
+    p->ws_bytes += ((size_t)p->rows[b] * n->channels[b] * 4 + 255) / 256 * 256;
+  }
   if (n->device < 0) {  // host-only handle: sizes and lists checked (cannot run)
     p->host_only = true;
     *out = p;
@@ -4503,6 +4668,32 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
     xd.rate_dst = n->rate[o.dst];
     xd.rate_res = o.res >= 0 ? n->rate[o.res] : 0;
   };
+  // pre-split images: -1 not yet written this run, 1 written by every launch of the buffer's last
+  // writer so far, 0 some launch did not (its consumers then stage the fp32 rows)
+  std::vector<signed char> img_state(p->simg_buf.size(), -1);
+  auto img_ptr = [&](int k) { return (unsigned char*)workspace + p->simg_off[k]; };
+  // a DMA-ring launch of phase i: the images it writes; whether its nsrc sources' images are ready
+  auto xdma_images = [&](CnXdmaArgs& xd, size_t i, int nsrc) -> bool {
+    const PwgCnetOp& o = n->ops[n->phases[i].op];
+    xd.n_oimg = 0;
+    xd.oimg_rowb = n->channels[o.dst] * 4;
+    if ((n->ld[o.dst] & 3) == 0)
+      for (int j = 0; j < 2; ++j) {
+        const int k = p->ph_oimg[2 * i + j];
+        if (k < 0) continue;
+        xd.oimg[xd.n_oimg] = img_ptr(k);
+        xd.oslope[xd.n_oimg] = p->simg_slope[k];
+        ++xd.n_oimg;
+      }
+    bool pre = n->presplit != 0;
+    for (int si = 0; si < 2; ++si) {
+      const int k = si < nsrc ? p->ph_simg[2 * i + si] : -1;
+      pre &= si >= nsrc || (k >= 0 && img_state[k] == 1);
+      xd.simg[si] = k >= 0 ? img_ptr(k) : nullptr;
+      xd.simg_rowb[si] = k >= 0 ? n->channels[p->simg_buf[k]] * 4 : 0;
+    }
+    return pre;
+  };
 #ifdef PWG_XDMA_PROBE
   auto probe_slot = [](size_t i) { return (int)i; };  // phase index (tools/diag/xdma_probe.py)
 #else
@@ -4554,6 +4745,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
     hipStream_t const s = stream_of(l_stream[L]);
     for (int d : l_waits[L])
       if (hipStreamWaitEvent(s, (*xev_run)[l_event[d]], 0) != hipSuccess) return fail(PWG_ERR_HIP, "dependency wait");
+    bool wrote_img = false;  // this launch wrote its phase's pre-split images
     hipEvent_t ea = nullptr, eb = nullptr;
     if (n->timing == 1) {
       for (hipEvent_t* ev : {&ea, &eb}) {
@@ -4790,7 +4982,9 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
             xd.probe_slot = probe_slot(pi);
             xdma_rows(xd, pi);
             for (int r = 0; r < 8; ++r) xd.z_off[r] = xt.z_off[r];
-            ea2 = xdma_launch(mtn, nw, xt.K, ngrid, s, a, xd);
+            const bool pre = xdma_images(xd, pi, 1);
+            wrote_img = xd.n_oimg > 0;
+            ea2 = xdma_launch(mtn, nw, xt.K, pre, ngrid, s, a, xd);
           } else {
             ea2 = xtile_launch_narrow(mtn, nw, xt.K, ngrid, p->nar_lds[pi], s, a, xt);
           }
@@ -4812,7 +5006,9 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
           xd.probe_slot = probe_slot(pi);
           xdma_rows(xd, pi);
           for (int r = 0; r < 8; ++r) xd.z_off[r] = 0;
-          const hipError_t ea2 = p->n_nblocks[pi] > 0 ? xdma_launch(mtn, nw, 1, ngrid, s, a, xd) : hipSuccess;
+          const bool pre = xdma_images(xd, pi, nsrc);
+          wrote_img = xd.n_oimg > 0 && p->n_nblocks[pi] > 0;
+          const hipError_t ea2 = p->n_nblocks[pi] > 0 ? xdma_launch(mtn, nw, 1, pre, ngrid, s, a, xd) : hipSuccess;
           if (ea2 != hipSuccess) return hipf(ea2, "xdma kernel launch");
         } else if (mtn == 1 && nw == 1) hipLaunchKernelGGL((pwg_cnet_conv_kernel<1, 1, CN_NARROW_G, true, 1>), ngrid, dim3(64), 0, s, a);
         else if (mtn == 1) hipLaunchKernelGGL((pwg_cnet_conv_kernel<1, 1, CN_NARROW_G, true, 2>), ngrid, dim3(128), 0, s, a);
@@ -4862,6 +5058,10 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hipf(e, "cnet op launch");
+    for (int j = 0; j < 2; ++j) {
+      const int k = p->ph_oimg[2 * pi + j];
+      if (k >= 0) img_state[k] = wrote_img && img_state[k] != 0 ? 1 : 0;
+    }
     if (n->timing == 1) {
       (void)hipEventRecord(eb, s);
       n->records.push_back({ph.op, ea, eb});
@@ -4943,6 +5143,7 @@ int pwg_cnet_set_option(PwgCnet* n, int option, long long value) {
               : option == PWG_CNET_OPT_XT_DMA     ? &n->xt_dma
               : option == PWG_CNET_OPT_XCD_ORDER  ? &n->xcd_order
               : option == PWG_CNET_OPT_NARROW_DMA ? &n->narrow_dma
+              : option == PWG_CNET_OPT_PRESPLIT   ? &n->presplit
                                                   : nullptr;
   if (option == PWG_CNET_OPT_MSTACK) {
     if (value < 0 || value > 2) return fail(PWG_ERR_INVALID, "mstack must be 0, 1 or 2");

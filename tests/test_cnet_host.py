@@ -295,3 +295,29 @@ def test_fused_stack_chains_in_the_schedule(built_lib):
 
     from parallelwavegan_amd import _lib
     assert eng._lib.pwg_cnet_set_option(eng._h, 9, 3) == _lib.PWG_ERR_INVALID
+
+
+@pytest.mark.parametrize("cfg", ["mb_melgan_v2", "hifigan_v1"])
+def test_presplit_images_only_for_small_plans(cfg, built_lib):
+    """PWG_CNET_OPT_PRESPLIT: a B = 1 plan (DMA-ring launches) reserves workspace for pre-split
+    images of the buffers DMA-ring launches read from DMA-ring writers, each rows x channels x 4 B;
+    a large batched plan (no narrow launches) reserves none; with the option off, none either."""
+    from parallelwavegan_amd.cnet import CnetEngine
+
+    m = _holder(cfg)
+    if cfg == "mb_melgan_v2":
+        m.pqmf = PQMF(m.out_channels)
+        P, _ = m.program(True)
+    else:
+        P = m.program()
+    P = P[0] if isinstance(P, tuple) else P
+    eng = CnetEngine(P, None, host_only=True)
+    on_small = eng.plan([64]).workspace_bytes
+    on_big = eng.plan([1000] * 8).workspace_bytes
+    eng.set_presplit(False)
+    off_small = eng.plan([64]).workspace_bytes
+    off_big = eng.plan([1000] * 8).workspace_bytes
+    assert on_small > off_small, (on_small, off_small)
+    assert on_big == off_big
+    # every image is a multiple of one 64-frame buffer's rows x channels x 4 B (256-aligned)
+    assert (on_small - off_small) % 256 == 0

@@ -576,3 +576,39 @@ def test_fused_stack_chain_bitwise_equal(cfg, built_lib, cuda_device):
         for a, b in zip(outs[mode], outs[0]):
             assert np.isfinite(a).all()
             np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("cfg", ["mb_melgan_v2", "hifigan_v1", "melgan_v1", "hifigan_causal_test"])
+def test_presplit_images_bitwise_equal(cfg, built_lib, cuda_device):
+    """PWG_CNET_OPT_PRESPLIT: DMA-ring launches whose inputs were written by DMA-ring launches stage
+    the writers' pre-split images (pre-activated, fp16 hi / lo rows) instead of converting the fp32
+    rows in every workgroup and step. The same conversion of the same values, done once: bit-identical
+    to presplit off at B = 1 (short utterances: every block touches an edge; zero and reflect padding)
+    and on a ragged batch, with fused stack chains on and off."""
+    from parallelwavegan_amd import configs, synthetic
+    from parallelwavegan_amd.hifigan import HiFiGANGenerator
+    from parallelwavegan_amd.melgan import PQMF, MelGANGenerator
+
+    cls, params = configs.vocoder_params(cfg)
+    m = {"MelGANGenerator": MelGANGenerator, "HiFiGANGenerator": HiFiGANGenerator}[cls](**params)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic.make_module_state_dict(m, seed=37).items()})
+    if cfg in configs.VOCODER_PQMF:
+        m.pqmf = PQMF(**configs.VOCODER_PQMF[cfg])
+    m = m.to(cuda_device)
+    eng = m.engine()
+    singles = [synthetic.make_mel(f, 80, seed=500 + f) for f in (64, 9, 131, 5)]
+    batch = [synthetic.make_mel(f, 80, seed=510 + i) for i, f in enumerate([5, 40, 17, 64])]
+    with torch.no_grad():
+        outs = {}
+        for ms in (1, 0):
+            eng.set_mstack(ms)
+            for pre in (0, 1):
+                eng.set_presplit(pre)
+                outs[ms, pre] = [m.inference(torch.from_numpy(x).to(cuda_device)).cpu().numpy() for x in singles]
+                outs[ms, pre] += [y.cpu().numpy() for y in m.inference_batch(batch)]
+        eng.set_presplit(1)
+        eng.set_mstack(1)
+    for ms in (1, 0):
+        for a, b in zip(outs[ms, 1], outs[ms, 0]):
+            assert np.isfinite(a).all()
+            np.testing.assert_array_equal(a, b)

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--frames", type=int, default=None)
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--mstack", type=int, default=None, help="PWG_CNET_OPT_MSTACK (fused stack chains) 0/1/2")
+    ap.add_argument("--presplit", type=int, default=None, help="PWG_CNET_OPT_PRESPLIT 0/1")
     ap.add_argument("--dump", default=None, help="save the first forward's output (.npy) for a bitwise A/B")
     a = ap.parse_args()
     cls, p = configs.vocoder_params(a.config)
@@ -38,6 +39,8 @@ def main():
     eng.set_fuse_pairs(not a.nofuse)
     if a.mstack is not None:
         eng.set_mstack(a.mstack)
+    if a.presplit is not None:
+        eng.set_presplit(a.presplit)
     if a.pair_steps:
         eng.set_pair_steps(a.pair_steps)
     P = eng.program
