@@ -25,6 +25,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -1014,6 +1015,7 @@ struct CnXdmaArgs {
   unsigned char* oimg[2];
   float oslope[2];
   int n_oimg, oimg_rowb;
+  int row0[2];    // PRE, K = 1: the row offset every chunk of source s shares, or INT_MIN (1x1s: 0)
 };
 // 16 zero bytes: the DMA source of a pre-split row outside a zero-padded utterance
 __device__ __attribute__((aligned(64))) unsigned g_cn_zero16[16];
@@ -1039,12 +1041,15 @@ struct XdmaShape {
   // round trip cover G chunks' few MFMAs
   static constexpr int G = K == 1 ? XDMA_K1_G : 1;
   static constexpr int KT = K == 1 ? G : K;                    // A fragments (taps / chunks) per step
-  // PRE: a step's rows arrive converted, XT_ROWB apart (a chunk's XC rows / the K > 1 tile's XR rows)
-  static constexpr int CHI = (XC * XT_ROWB + 1023) / 1024;     // PRE, K = 1: instructions per chunk
+  // PRE: a step's rows arrive converted, 64 B each (hi 16 f16, lo 16 f16 as four 16-B pieces, piece
+  // q of row r at slot q ^ ((r >> 2) & 3): every 16-lane group of a ds_read_b128 of 16 consecutive
+  // rows then covers all 16 slots of a bank row, conflict-free, without the 16-B pad). Instruction j
+  // of a row block holds rows 16 j .. 16 j + 15, lane l row 16 j + l / 4, slot l & 3.
+  static constexpr int CHI = XC / 16;                          // PRE, K = 1: instructions per chunk
   static constexpr int NA = KT * MT * 2;                       // 1-KB DMA instructions per step
-  static constexpr int NX = PRE ? (K == 1 ? G * CHI : (XR * XT_ROWB + 1023) / 1024) : G * XR / 16;
-  // PRE, K = 1: wave w copies instructions w, w + NWV, .. of every chunk (JW per chunk, the last
-  // repeated): compile-time chunk indices
+  static constexpr int NX = PRE ? (K == 1 ? G * CHI : XR / 16) : G * XR / 16;
+  // PRE, K = 1: wave w copies instructions w, w + NWV, .. of every chunk (JW = 2 per chunk):
+  // compile-time chunk indices
   static constexpr int JW = (CHI + NWV - 1) / NWV;
   static constexpr int DA = (NA + NWV - 1) / NWV, DX = PRE && K == 1 ? G * JW : (NX + NWV - 1) / NWV;  // ... per wave
   static constexpr int D = DA + DX;
@@ -1147,31 +1152,36 @@ __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArg
   const int off0 = xd.z_off[zp];
   int xoff[S::DX];
   unsigned okm = 0;
-  // PRE, K > 1: each lane's 16 B of instruction k is (tile row r, piece q) of the XT_ROWB-strided
-  // rows (q = 4, the pad, and rows past the span repeat an in-bounds piece); the image byte offset of
-  // that piece in channel block 0, or -1 for a zero-padded row (the zero page)
+  // PRE, K > 1: each lane's 16 B of instruction k is (tile row r, piece q) of the swizzled 64-B rows;
+  // the image byte offset of that piece in channel block 0, or -1 (the zero page) for a zero-padded
+  // row or one past the span
   long long pxo[PRE && K > 1 ? S::DX : 1];
-  int prow[PRE && K == 1 ? S::JW : 1], pq16[PRE && K == 1 ? S::JW : 1];  // PRE, K = 1: (row, piece) per jj
+  int prow[PRE && K == 1 ? S::JW : 1], pq16[PRE && K == 1 ? S::JW : 1];  // PRE, K = 1: (row, piece x 16) per jj
+  // ... and, for a source whose chunks share one row offset, each instruction's image byte offset
+  // (-1: zero page), once: the per-step issue is then a base + offset per instruction
+  long long pk1[2][PRE && K == 1 ? S::JW : 1];
   if constexpr (PRE && K == 1) {
 #pragma unroll
     for (int jj = 0; jj < S::JW; ++jj) {
       const int j = wave + NWV * jj < S::CHI ? wave + NWV * jj : S::CHI - 1;
-      const int o = j * 1024 + lane * 16;
-      const int r = o / XT_ROWB, q = (o - r * XT_ROWB) >> 4;
-      prow[jj] = r < S::XC ? r : S::XC - 1;
-      pq16[jj] = q < 4 ? q * 16 : 0;
+      const int r = 16 * j + (lane >> 2);
+      prow[jj] = r;
+      pq16[jj] = ((lane & 3) ^ ((r >> 2) & 3)) * 16;
+#pragma unroll
+      for (int si = 0; si < 2; ++si) {
+        int p = q0 + (xd.row0[si] == INT_MIN ? 0 : xd.row0[si]) + prow[jj];
+        const bool ok = edge_row(p, si ? sgy1 : sgy0, a.src[si].pad_mode);
+        pk1[si][jj] = ok ? (long long)((si ? sgx1 : sgx0) + p) * xd.simg_rowb[si] + pq16[jj] : -1;
+      }
     }
   }
   if constexpr (PRE && K > 1) {
 #pragma unroll
     for (int k = 0; k < S::DX; ++k) {
       const int i = wave + NWV * k < S::NX ? wave + NWV * k : S::NX - 1;
-      const int o = i * 1024 + lane * 16;
-      int r = o / XT_ROWB, q = (o - r * XT_ROWB) >> 4;
-      q = q < 4 ? q : 0;
-      r = r < span ? r : span - 1;
+      const int r = 16 * i + (lane >> 2), q = (lane & 3) ^ ((r >> 2) & 3);
       int p = q0 + off0 + r;
-      const bool ok = edge_row(p, sgy0, s0.pad_mode);
+      const bool ok = edge_row(p, sgy0, s0.pad_mode) && r < span;
       pxo[k] = ok ? (long long)(sgx0 + p) * xd.simg_rowb[0] + q * 16 : -1;
     }
   } else if constexpr (K > 1) {
@@ -1229,20 +1239,32 @@ __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArg
     } else if constexpr (PRE) {
       // K = 1: chunk t's XC rows are instructions t CHI .. + CHI - 1, each lane's 16 B a (row,
       // piece) of the XT_ROWB-strided rows, read from its source's image at the chunk's channels
+      // the step's chunk descriptors: every LDS read first, one wait
+      ChunkDesc cdr[S::G];
+#pragma unroll
+      for (int t = 0; t < S::G; ++t) cdr[t] = s_ch[min(s * S::G + t, nch - 1)];
 #pragma unroll
       for (int t = 0; t < S::G; ++t) {
-        const ChunkDesc cd = chunk(min(s * S::G + t, nch - 1));
-        const bool s1 = cd.src != 0;  // (uniform: scalar selects, no indexed source array)
-        const unsigned char* const img = (s1 ? xd.simg[1] : xd.simg[0]) + cd.c0 * 4;
+        const int csrc = __builtin_amdgcn_readfirstlane(cdr[t].src);
+        const int crow = __builtin_amdgcn_readfirstlane(cdr[t].row_off);
+        const int cc0 = __builtin_amdgcn_readfirstlane(cdr[t].c0);
+        const bool s1 = csrc != 0;  // (uniform: scalar selects, no indexed source array)
+        const unsigned char* const img = (s1 ? xd.simg[1] : xd.simg[0]) + cc0 * 4;
+        const bool common = crow == (s1 ? xd.row0[1] : xd.row0[0]);
         const int rowb = s1 ? xd.simg_rowb[1] : xd.simg_rowb[0];
         const int sgx = s1 ? sgx1 : sgx0, sgy = s1 ? sgy1 : sgy0;
         const int pm = s1 ? a.src[1].pad_mode : a.src[0].pad_mode;
 #pragma unroll
         for (int jj = 0; jj < S::JW; ++jj) {
           const int j = wave + NWV * jj < S::CHI ? wave + NWV * jj : S::CHI - 1;
-          int p = q0 + cd.row_off + prow[jj];
-          const bool ok = edge_row(p, sgy, pm);
-          const void* src = ok ? (const void*)(img + (long long)(sgx + p) * rowb + pq16[jj]) : (const void*)g_cn_zero16;
+          long long off;
+          if (common) {
+            off = s1 ? pk1[1][jj] : pk1[0][jj];
+          } else {
+            int p = q0 + crow + prow[jj];
+            off = edge_row(p, sgy, pm) ? (long long)(sgx + p) * rowb + pq16[jj] : -1;
+          }
+          const void* src = off >= 0 ? (const void*)(img + off) : (const void*)g_cn_zero16;
           __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(slot + (t * S::CHI + j) * 1024), 16, 0, 0);
         }
       }
@@ -1332,12 +1354,13 @@ __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArg
 #pragma unroll
     for (int t = 0; t < KT; ++t) {
       if constexpr (PRE) {
-        // converted rows straight from the step's slot (K = 1: chunk t's rows; K > 1: tap t's row)
-        const unsigned char* row = xt_smem + (size_t)(g % P) * S::SLOT +
-                                   (K == 1 ? t * S::CHI * 1024 + (wave * 32 + cl) * XT_ROWB
-                                           : (wave * 32 + cl + t * xd.dil) * XT_ROWB);
-        bh[t] = *reinterpret_cast<const u32x4v*>(row + 16 * hh);
-        bl[t] = *reinterpret_cast<const u32x4v*>(row + 32 + 16 * hh);
+        // converted rows straight from the step's slot (K = 1: chunk t's rows; K > 1: tap t's row),
+        // pieces hh (hi) and 2 + hh (lo) at their swizzled slots
+        const int R = K == 1 ? wave * 32 + cl : wave * 32 + cl + t * xd.dil;
+        const int sw = (R >> 2) & 3;
+        const unsigned char* row = xt_smem + (size_t)(g % P) * S::SLOT + (K == 1 ? t * S::CHI * 1024 : 0) + R * 64;
+        bh[t] = *reinterpret_cast<const u32x4v*>(row + 16 * (hh ^ sw));
+        bl[t] = *reinterpret_cast<const u32x4v*>(row + 16 * ((2 + hh) ^ sw));
       } else if constexpr (K == 1) {
         // chunk g G + t: the lane's 8 channels of its raw row, pre-activated and pair-split in
         // registers (pwg_cnet_conv_kernel's bprep + cn_split8)
@@ -4982,6 +5005,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
             xd.probe_slot = probe_slot(pi);
             xdma_rows(xd, pi);
             for (int r = 0; r < 8; ++r) xd.z_off[r] = xt.z_off[r];
+            xd.row0[0] = xd.row0[1] = INT_MIN;
             const bool pre = xdma_images(xd, pi, 1);
             wrote_img = xd.n_oimg > 0;
             ea2 = xdma_launch(mtn, nw, xt.K, pre, ngrid, s, a, xd);
@@ -5006,6 +5030,16 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
           xd.probe_slot = probe_slot(pi);
           xdma_rows(xd, pi);
           for (int r = 0; r < 8; ++r) xd.z_off[r] = 0;
+          for (int si = 0; si < 2; ++si) {  // the row offset all of source si's chunks share
+            int r0 = INT_MIN;
+            bool same = true;
+            for (const ChunkDesc& c : ph.chunks)
+              if (c.src == si) {
+                if (r0 == INT_MIN) r0 = c.row_off;
+                same &= c.row_off == r0;
+              }
+            xd.row0[si] = same ? r0 : INT_MIN;
+          }
           const bool pre = xdma_images(xd, pi, nsrc);
           wrote_img = xd.n_oimg > 0 && p->n_nblocks[pi] > 0;
           const hipError_t ea2 = p->n_nblocks[pi] > 0 ? xdma_launch(mtn, nw, 1, pre, ngrid, s, a, xd) : hipSuccess;

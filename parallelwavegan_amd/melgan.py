@@ -20,7 +20,7 @@ import numpy as np
 import torch
 
 from . import causal, cnet
-from .engine import WeightTracker
+from .engine import WeightTracker, first_parameter, forget_device
 
 
 def _kaiser(m, beta):
@@ -221,7 +221,7 @@ class MelGANGenerator(torch.nn.Module):
         else:
             arr = np.load(stats)
             mean, scale = arr[0].reshape(-1), arr[1].reshape(-1)
-        dev = next(self.parameters()).device
+        dev = first_parameter(self).device
         self.register_buffer("mean", torch.from_numpy(np.asarray(mean)).float().to(dev))
         self.register_buffer("scale", torch.from_numpy(np.asarray(scale)).float().to(dev))
         logging.info("Successfully registered stats as buffer.")
@@ -323,13 +323,14 @@ class MelGANGenerator(torch.nn.Module):
 
     # ------------------------------------------------------------------ engine plumbing
     def _device(self):
-        dev = next(self.parameters()).device
+        dev = first_parameter(self).device
         if dev.type != "cuda":
             raise RuntimeError("parallelwavegan_amd.MelGANGenerator runs on a ROCm GPU only; move the module "
                                "with .to('cuda') (there is no CPU fallback)")
         return dev
 
     def _apply(self, fn, *args, **kwargs):
+        forget_device(self)
         for ent in getattr(self, "_engines", {}).values():
             ent[1].invalidate()  # .to() / .cuda() replace parameter storage
         return super()._apply(fn, *args, **kwargs)

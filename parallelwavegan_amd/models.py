@@ -20,7 +20,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .engine import Engine, WeightTracker
+from .engine import Engine, WeightTracker, first_parameter, forget_device
 
 
 def _kaiming_conv1d(*args, **kwargs):
@@ -205,14 +205,14 @@ class ParallelWaveGANGenerator(torch.nn.Module):
             arr = np.load(stats)
             mean = arr[0].reshape(-1)
             scale = arr[1].reshape(-1)
-        dev = next(self.parameters()).device
+        dev = first_parameter(self).device
         self.register_buffer("mean", torch.from_numpy(np.asarray(mean)).float().to(dev))
         self.register_buffer("scale", torch.from_numpy(np.asarray(scale)).float().to(dev))
         logging.info("Successfully registered stats as buffer.")
 
     # ------------------------------------------------------------------ engine plumbing
     def _device(self):
-        dev = next(self.parameters()).device
+        dev = first_parameter(self).device
         if dev.type != "cuda":
             raise RuntimeError(
                 "parallelwavegan_amd.ParallelWaveGANGenerator runs on a ROCm GPU only; move the "
@@ -220,6 +220,7 @@ class ParallelWaveGANGenerator(torch.nn.Module):
         return dev
 
     def _apply(self, fn, *args, **kwargs):
+        forget_device(self)
         if getattr(self, "_weights", None) is not None:
             self._weights.invalidate()  # .to() / .cuda() replace parameter storage
         return super()._apply(fn, *args, **kwargs)
