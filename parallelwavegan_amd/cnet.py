@@ -580,7 +580,7 @@ class CnetEngine:
         """pwg_cnet_set_option(PWG_CNET_OPT_NARROW_DMA): narrow launches on the DMA-ring kernel
         (default) or, 0, on the narrow x-tile / tap-major kernels. Plan-time (cached plans are
         dropped); bit-identical."""
-        _lib.check(self._lib.pwg_cnet_set_option(self._h, 7, 1 if enable else 0))
+        _lib.check(self._lib.pwg_cnet_set_option(self._h, 7, int(enable) if int(enable) == 2 else (1 if enable else 0)))
         self._graph_epoch += 1
         self._plans.clear()
 

@@ -4402,7 +4402,7 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
       else base = n_blk * (ph.mt_total / ph.MT) * zn;
       if (n->narrow == 2 || base < p->n_cu) {
         pick_w = 1;
-        if (n->narrow_dma && xdma_fits(ncols, xdma_waves(ncols), (long long)ph.mt_total * zn)) {
+        if (n->narrow_dma && (n->narrow_dma == 2 || xdma_fits(ncols, xdma_waves(ncols), (long long)ph.mt_total * zn))) {
           pick_w = xdma_waves(ncols);
           p->nar_xdma[pi] = 1;
         } else {
@@ -4431,7 +4431,7 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
         // then runs it, 1-2 waves)
         if (n->narrow_dma && !op.src[0].normalize && !(op.src[1].buf >= 0 && op.src[1].normalize) &&
             ph.chunks.size() <= (size_t)XDMA_CHUNKS_MAX &&
-            xdma_fits(ncols, std::min(2, xdma_waves(ncols)), (long long)ph.mt_total * zn)) {
+            (n->narrow_dma == 2 || xdma_fits(ncols, std::min(2, xdma_waves(ncols)), (long long)ph.mt_total * zn))) {
           pick_w = std::min(2, xdma_waves(ncols));  // K = 1 mode: 2 waves keep a 4-chunk step's ring 6 deep
           p->nar_xdma[pi] = 1;
         } else {
@@ -5190,7 +5190,8 @@ int pwg_cnet_set_option(PwgCnet* n, int option, long long value) {
     return PWG_OK;
   }
   if (!slot) return fail(PWG_ERR_INVALID, "unknown option");
-  if (value != 0 && value != 1 && !(option == PWG_CNET_OPT_XT_DMA && value >= 0 && value <= 15))
+  if (value != 0 && value != 1 && !(option == PWG_CNET_OPT_XT_DMA && value >= 0 && value <= 15) &&
+      !(option == PWG_CNET_OPT_NARROW_DMA && value == 2))
     return fail(PWG_ERR_INVALID, "option value must be 0 or 1 (PWG_CNET_OPT_XT_DMA: flags 0 - 15)");
   *slot = (int)value;
   return PWG_OK;

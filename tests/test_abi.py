@@ -77,6 +77,7 @@ def test_receptive_field_and_upsample_factor(built_lib):
         (dict(gate_channels=7), ValueError),
         (dict(upsample_net="MelGANGenerator"), NotImplementedError),
         (dict(upsample_params={"upsample_scales": [4], "nonlinear_activation": "ReLU"}), NotImplementedError),
+        (dict(upsample_params={"upsample_scales": [4], "freq_axis_kernel_size": 3}), NotImplementedError),
     ],
 )
 def test_invalid_configs_raise_reference_exceptions(built_lib, override, exc):

@@ -1,6 +1,7 @@
 """B = 1 latency of a vocoder drop-in under values of one CnetEngine option (diagnostic, GPU box).
 
   python tools/diag/opt_lat.py CFG SETTER V1,V2,.. [T1,T2,..]   e.g. mb_melgan_v2 set_mstack 0,1 64,512
+  (several setters: SETTER s1:s2 and values a1:a2,b1:b2 -- each value sets every setter in turn)
 
 Per (value, T'): median wall ms of 30 synchronised inference() calls, the device span of one call
 (timing mode 2) and, for the first value, whether every later value's output is bit-identical.
@@ -22,7 +23,7 @@ from parallelwavegan_amd.melgan import PQMF, MelGANGenerator  # noqa: E402
 
 def main():
     cfg, setter = sys.argv[1], sys.argv[2]
-    values = [int(v) for v in sys.argv[3].split(",")]
+    values = sys.argv[3].split(",")
     frames = [int(v) for v in (sys.argv[4] if len(sys.argv) > 4 else "64,512").split(",")]
     dev = torch.device("cuda", 0)
     cls, params = configs.vocoder_params(cfg)
@@ -36,7 +37,8 @@ def main():
     ref = {}
     with torch.no_grad():
         for v in values:
-            getattr(eng, setter)(v)
+            for st, sv in zip(setter.split(":"), v.split(":")):
+                getattr(eng, st)(int(sv))
             for F in frames:
                 mel = torch.from_numpy(synthetic.make_mel(F, 80, seed=7)).to(dev)
                 for _ in range(5):
