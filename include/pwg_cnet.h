@@ -161,7 +161,8 @@ PWG_API int pwg_cnet_plan_schedule(PwgCnetPlan* p, int cap, int* n_launches, int
  * input rows pre-activated LDS -> LDS; also takes the narrow launches of tap-major convs (MelGAN's
  * two-source 1x1s). Bit-identical to 0 (the DMA-staged narrow x-tile kernel and the narrow
  * tap-major kernel, sized as described above), which stays for A/B. 2: also narrow launches whose
- * DMA-ring workgroups would need more than one round over the CUs (measured slower; for A/B).
+ * DMA-ring workgroups would need more than one round over the CUs, with two m-tiles per workgroup
+ * where the op has k <= 7 (measured slower; for A/B).
  * PWG_CNET_OPT_STREAMS (default 1): launches that do not depend on each other (HiFiGAN's parallel
  * residual blocks, models/hifigan.py:159-168) run concurrently on up to 3 auxiliary streams of the
  * handle, forked from and joined back into the caller's stream with events (graph-capturable):

@@ -1540,21 +1540,43 @@ hipError_t xdma_go(dim3 grid, hipStream_t s, const CnConvArgs& a, const CnXdmaAr
 }
 template <int MT, int NWV, bool PRE>
 hipError_t xdma_launch_k(int k, dim3 grid, hipStream_t s, const CnConvArgs& a, const CnXdmaArgs& xd) {
-  switch (k) {
-    case 1: return xdma_go<1, MT, NWV, PRE>(grid, s, a, xd);
-    case 2: return xdma_go<2, MT, NWV, PRE>(grid, s, a, xd);
-    case 3: return xdma_go<3, MT, NWV, PRE>(grid, s, a, xd);
-    case 5: return xdma_go<5, MT, NWV, PRE>(grid, s, a, xd);
-    case 7: return xdma_go<7, MT, NWV, PRE>(grid, s, a, xd);
-    case 11: return xdma_go<11, MT, NWV, PRE>(grid, s, a, xd);
-    default: return hipErrorInvalidValue;
+  if constexpr (MT == 2) {  // two m-tiles: k > 1 up to 7 taps (a step's operands in registers)
+    switch (k) {
+      case 2: return xdma_go<2, 2, NWV, PRE>(grid, s, a, xd);
+      case 3: return xdma_go<3, 2, NWV, PRE>(grid, s, a, xd);
+      case 5: return xdma_go<5, 2, NWV, PRE>(grid, s, a, xd);
+      case 7: return xdma_go<7, 2, NWV, PRE>(grid, s, a, xd);
+      default: return hipErrorInvalidValue;
+    }
+  } else {
+    switch (k) {
+      case 1: return xdma_go<1, MT, NWV, PRE>(grid, s, a, xd);
+      case 2: return xdma_go<2, MT, NWV, PRE>(grid, s, a, xd);
+      case 3: return xdma_go<3, MT, NWV, PRE>(grid, s, a, xd);
+      case 5: return xdma_go<5, MT, NWV, PRE>(grid, s, a, xd);
+      case 7: return xdma_go<7, MT, NWV, PRE>(grid, s, a, xd);
+      case 11: return xdma_go<11, MT, NWV, PRE>(grid, s, a, xd);
+      default: return hipErrorInvalidValue;
+    }
   }
 }
 // k = 1: K = 1 mode (steps = the tap-major chunk list); pre: B rows from the sources' pre-split
 // images (xd.simg)
 hipError_t xdma_launch(int mt, int nwv, int k, bool pre, dim3 grid, hipStream_t s, const CnConvArgs& a,
                        const CnXdmaArgs& xd) {
-  if (mt != 1) return hipErrorInvalidValue;  // (the plan picks one m-tile per workgroup)
+  if (mt == 2) {
+    if (pre) {
+      if (nwv == 1) return xdma_launch_k<2, 1, true>(k, grid, s, a, xd);
+      if (nwv == 2) return xdma_launch_k<2, 2, true>(k, grid, s, a, xd);
+      if (nwv == 4) return xdma_launch_k<2, 4, true>(k, grid, s, a, xd);
+    } else {
+      if (nwv == 1) return xdma_launch_k<2, 1, false>(k, grid, s, a, xd);
+      if (nwv == 2) return xdma_launch_k<2, 2, false>(k, grid, s, a, xd);
+      if (nwv == 4) return xdma_launch_k<2, 4, false>(k, grid, s, a, xd);
+    }
+    return hipErrorInvalidValue;
+  }
+  if (mt != 1) return hipErrorInvalidValue;  // (the plan picks one or two m-tiles per workgroup)
   if (pre) {
     if (nwv == 1) return xdma_launch_k<1, 1, true>(k, grid, s, a, xd);
     if (nwv == 2) return xdma_launch_k<1, 2, true>(k, grid, s, a, xd);
@@ -4402,8 +4424,15 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
       else base = n_blk * (ph.mt_total / ph.MT) * zn;
       if (n->narrow == 2 || base < p->n_cu) {
         pick_w = 1;
-        if (n->narrow_dma && (n->narrow_dma == 2 || xdma_fits(ncols, xdma_waves(ncols), (long long)ph.mt_total * zn))) {
+        // NARROW_DMA 2 (A/B): the DMA-ring kernel for every narrow launch, rounds or not, with two
+        // m-tiles per workgroup (k <= 7: a step's A fragments stay in registers) where one would need
+        // more than a round. Measured slower than the narrow x-tile kernel's 2-m-tile workgroups
+        // there (HiFiGAN v1 T' = 256: 1.33 vs 1.23 ms, profiles/r05_mt2.json), so the default keeps
+        // the DMA-ring kernel to launches whose one-m-tile workgroups fit one round
+        const bool fit1 = xdma_fits(ncols, xdma_waves(ncols), (long long)ph.mt_total * zn);
+        if (n->narrow_dma && (fit1 || n->narrow_dma == 2)) {
           pick_w = xdma_waves(ncols);
+          pick_m = !fit1 && xk <= 7 && ph.mt_total % 2 == 0 ? 2 : 1;
           p->nar_xdma[pi] = 1;
         } else {
           bool found = false;

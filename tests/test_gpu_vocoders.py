@@ -359,12 +359,15 @@ def test_narrow_launches_bitwise_equal(cfg, built_lib, cuda_device):
     m = m.to(cuda_device)
     eng = m.engine()
     mels = [synthetic.make_mel(f, 80, seed=150 + i) for i, f in enumerate([64, 9, 23, 131])]
+    # 300 frames alone: HiFiGAN's 256-channel stage fits one round over the CUs only with two m-tiles
+    # per DMA-ring workgroup
+    long = synthetic.make_mel(300, 80, seed=149)
     with torch.no_grad():
         outs = {}
         for mode, dma in ((0, 1), (1, 1), (2, 1), (1, 0), (2, 0)):
             eng.set_narrow(mode)
             eng.set_narrow_dma(dma)
-            outs[mode, dma] = ([m.inference(torch.from_numpy(mels[0]).to(cuda_device)).cpu().numpy()] +
+            outs[mode, dma] = ([m.inference(torch.from_numpy(x).to(cuda_device)).cpu().numpy() for x in (mels[0], long)] +
                                [y.cpu().numpy() for y in m.inference_batch(mels)])
         eng.set_narrow(1)
         eng.set_narrow_dma(1)
