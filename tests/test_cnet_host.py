@@ -198,12 +198,14 @@ def test_host_only_plans_build_and_check_their_block_lists(name, built_lib):
     rc = eng._lib.pwg_cnet_run(p._p, ctypes.c_void_p(16), ctypes.c_void_p(16), None, None, ctypes.c_void_p(16),
                                ctypes.c_void_p(256), None)
     assert rc == _lib.PWG_ERR_INVALID
-    # launch options on the handle: PWG_CNET_OPT_NARROW (6) takes 0-2, PWG_CNET_OPT_NARROW_DMA (7) 0/1
+    # launch options on the handle: PWG_CNET_OPT_NARROW (6) takes 0-2, PWG_CNET_OPT_NARROW_DMA (7) 0-2
     eng.set_narrow(2)
     eng.set_narrow_dma(False)
+    eng.set_narrow_dma(2)
+    assert eng.plan([64]).out_rows == 64 * hop  # (mode 2: the DMA-ring kernel for every narrow launch)
     eng.set_narrow_dma(True)
     assert eng._lib.pwg_cnet_set_option(eng._h, 6, 3) == _lib.PWG_ERR_INVALID
-    assert eng._lib.pwg_cnet_set_option(eng._h, 7, 2) == _lib.PWG_ERR_INVALID
+    assert eng._lib.pwg_cnet_set_option(eng._h, 7, 3) == _lib.PWG_ERR_INVALID
     assert eng.plan([64]).out_rows == 64 * hop
 
 
