@@ -114,7 +114,34 @@ struct CnConvArgs {
   int* range_flag;        // thin kernel writing the program output (split-f16 mode): set to 1 on a
                           // non-finite output value (pwg_cnet_run_status), else null
   int xcd_order;          // 1: XCD-aware tile order (xcd_tile), PWG_CNET_OPT_XCD_ORDER
+  // pre-split images of the output rows written by the x-tile kernels' epilogue (cn_store_col's
+  // quad path; PWG_CNET_OPT_PRESPLIT): n_oimg of them, each with its readers' LeakyReLU slope,
+  // [row][16-channel block][hi 16 f16 | lo 16 f16], oimg_rowb = channels x 4 B
+  unsigned char* oimg[2];
+  float oslope[2];
+  int n_oimg, oimg_rowb;
 };
+
+// 16 zero bytes (64 allocated): the DMA source of a pre-split row outside a zero-padded utterance
+__device__ __attribute__((aligned(64))) unsigned g_cn_zero16[16];
+
+// 4 output channels row .. row + 3 of image row irow: the readers' LeakyReLU (as their staging
+// applies it) and the fp16 pair split of the values just stored
+__device__ __forceinline__ void cn_img4(unsigned char* img, long long irow, int rowb, int row, const float (&v)[4],
+                                        float slope) {
+  _Float16 hv[4], lv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float x = v[i];
+    if (slope != 1.f) x = x > 0.f ? x : x * slope;
+    hv[i] = (_Float16)x;
+    lv[i] = (_Float16)(x - (float)hv[i]);
+  }
+  typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+  unsigned char* const d = img + irow * rowb + (row >> 4) * 64 + (row & 15) * 2;
+  *reinterpret_cast<h4*>(d) = h4{hv[0], hv[1], hv[2], hv[3]};
+  *reinterpret_cast<h4*>(d + 32) = h4{lv[0], lv[1], lv[2], lv[3]};
+}
 
 // Workgroup -> (column block, m-group, ConvTranspose phase). Workgroup ids are dispatched x-fastest
 // and dealt round-robin over the 8 XCDs, each with its own L2: in grid order the m-groups and phases
@@ -435,6 +462,8 @@ struct CnXtileArgs {
   int span;               // input rows per block: 256 + (K-1) dil
   int rev;                // 1: tap t multiplies weight chunk K-1-t (ConvTranspose phases)
   int z_off[8];           // ConvTranspose: off_min of phase blockIdx.z (z_off[0] = off_min)
+  const unsigned char* simg;  // PRE (narrow DMA-staged launches): the source's pre-split image
+  int simg_rowb;              // ... its row bytes (channels x 4)
 };
 __host__ __device__ constexpr bool xtile_supported(int k) { return k == 3 || k == 5 || k == 7 || k == 11; }
 constexpr int XT_COLS = 256;
@@ -447,7 +476,7 @@ constexpr int XT_ROWB = 80;  // bytes per staged input row: 16 hi + 16 lo halves
 // serialises one load round trip per 4 rows (MT x 4 of them, ~1 us each at B = 1).
 template <int MT>
 __device__ __forceinline__ void cn_store_col(const CnConvArgs& a, const f32x16 (&acc)[MT], const float* bias_, int m0,
-                                             int hh, float* yrow, const float* rrow) {
+                                             int hh, float* yrow, const float* rrow, long long irow = 0) {
   auto finish = [&](f32x4v v) {
     if (a.out_div != 1.f) {
 #pragma unroll
@@ -497,6 +526,8 @@ __device__ __forceinline__ void cn_store_col(const CnConvArgs& a, const f32x16 (
           for (int i = 0; i < 4; ++i)
             if (row + i >= a.M) v[i] = 0.f;
           *reinterpret_cast<f32x4v*>(yrow + row) = v;
+          const float vv[4] = {v[0], v[1], v[2], v[3]};
+          for (int j = 0; j < a.n_oimg; ++j) cn_img4(a.oimg[j], irow, a.oimg_rowb, row, vv, a.oslope[j]);
         }
     }
     return;
@@ -541,10 +572,15 @@ constexpr int xt_wpe() {
 // group's MFMAs and converted into the (single) row buffer after it. KS < K: two tap groups per
 // channel block, [0, KS) always in buffer 0 and [KS, K) in buffer 1; KS == K: the buffers alternate
 // per block. Same products in the same order as the other variants: bit-identical.
-template <int MT, int K, int CB, int NC = 1, bool SY = false, int KS = K, bool DB = false, int NWV = 8>
+// PRE (narrow DMA-staged launches, PWG_CNET_OPT_PRESPLIT): the input rows come pre-activated and
+// pair-split from the source's image (its writer's epilogue), DMA'd straight into one of two row
+// buffers during the previous block's last tap group -- no register prefetch, no conversion, one
+// barrier per block end instead of two. Rows are 64 B with piece q of row r at slot q ^ ((r >> 2) & 3).
+template <int MT, int K, int CB, int NC = 1, bool SY = false, int KS = K, bool DB = false, int NWV = 8, bool PRE = false>
 __global__ void __launch_bounds__(64 * NWV) __attribute__((amdgpu_waves_per_eu(xt_wpe<MT, K, CB, SY, DB>())))
 pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
   static_assert(KS == K || SY || DB, "tap-split staging is a synchronous-staging or DMA variant");
+  static_assert(!PRE || (DB && NWV < 8), "pre-split rows: the narrow DMA-staged variant");
   static_assert(!DB || (CB == 1 && NC == 1 && !SY), "DMA staging: one block, one column tile");
   static_assert(NWV == 8 || (DB && NC == 1), "narrow workgroups: the DMA-staged variant");
   constexpr int NTH = 64 * NWV;
@@ -577,6 +613,21 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
   const int2 sg = *reinterpret_cast<const int2*>(sx.seg + 2 * u);
   const int xv = CB * xt.span * 4;                     // input quads (4 channels) per group
   constexpr int XQ_MAX = (CB * (NC * XC + (NWV == 8 ? 192 : NARROW_HALO)) * 4 + NTH - 1) / NTH;
+  // PRE: rows per buffer (the span, rounded to the 16 rows of a DMA instruction), instructions
+  constexpr int XRP = (XC + (K == 2 ? 16 : NARROW_HALO) + 15) / 16 * 16;
+  constexpr int NXI = XRP / 16, DXI = (NXI + NWV - 1) / NWV;
+  long long pxo[PRE ? DXI : 1];  // each lane's (row, piece) byte offset in the image's block 0, -1: zero
+  if constexpr (PRE) {
+#pragma unroll
+    for (int k = 0; k < DXI; ++k) {
+      const int i = wave + NWV * k;
+      const int r = 16 * i + (lane >> 2), q = (lane & 3) ^ ((r >> 2) & 3);
+      int p = q0 + off_min + r;
+      const bool ok = i < NXI && r < xt.span && edge_row(p, sg.y, sx.pad_mode);
+      pxo[k] = ok ? (long long)(sg.x + p) * xt.simg_rowb + q * 16 : -1;
+    }
+  }
+  const unsigned char* s_xcur = s_x;  // PRE: the row buffer of the block being computed
 
   f32x4v ar[AQ];
   f32x4v xr[XQ_MAX];
@@ -664,6 +715,20 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
       __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + (size_t)i * 64), 16, 0, 0);
     }
   };
+  // PRE: channel block grp's pre-split rows -> row buffer b
+  auto rdma = [&](int grp, int b) {
+    typedef __attribute__((address_space(1))) void* gptr_t;
+    typedef __attribute__((address_space(3))) void* lptr_t;
+    unsigned char* const dst = s_x + (size_t)b * XRP * 64;
+    const unsigned char* const src0 = xt.simg + 64 * grp;
+#pragma unroll
+    for (int k = 0; k < (PRE ? DXI : 0); ++k) {
+      const int i = wave + NWV * k;
+      if (i >= NXI) break;
+      const void* src = pxo[k] >= 0 ? (const void*)(src0 + pxo[k]) : (const void*)g_cn_zero16;
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(dst + (size_t)i * 1024), 16, 0, 0);
+    }
+  };
 
   // SY: each vector goes global -> LDS on its own (the compiler batches them within 128 VGPRs)
   constexpr int AVS = CB * KS * MT * 128, AQS = (AVS + NTH - 1) / NTH;
@@ -730,10 +795,17 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
         u32x4v bh[NC], bl[NC];
 #pragma unroll
         for (int nc = 0; nc < NC; ++nc) {
-          const unsigned char* row =
-              s_x + ((size_t)c * xt.span + nc * XC + wave * 32 + cl + tap * xt.dil) * XT_ROWB;
-          bh[nc] = *reinterpret_cast<const u32x4v*>(row + 16 * hh);
-          bl[nc] = *reinterpret_cast<const u32x4v*>(row + 32 + 16 * hh);
+          if constexpr (PRE) {
+            const int R = wave * 32 + cl + tap * xt.dil, sw = (R >> 2) & 3;
+            const unsigned char* row = s_xcur + (size_t)R * 64;
+            bh[nc] = *reinterpret_cast<const u32x4v*>(row + 16 * (hh ^ sw));
+            bl[nc] = *reinterpret_cast<const u32x4v*>(row + 16 * ((2 + hh) ^ sw));
+          } else {
+            const unsigned char* row =
+                s_x + ((size_t)c * xt.span + nc * XC + wave * 32 + cl + tap * xt.dil) * XT_ROWB;
+            bh[nc] = *reinterpret_cast<const u32x4v*>(row + 16 * hh);
+            bl[nc] = *reinterpret_cast<const u32x4v*>(row + 32 + 16 * hh);
+          }
         }
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
@@ -757,12 +829,17 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
     // computes from buffer g & 1 while the DMA of group g + 1 fills the other buffer
     constexpr int NH = (K + KS - 1) / KS;
     dma(0, 0, KS, s_a);
-    xload(0);
-    xstore(0);
+    if constexpr (PRE) {
+      rdma(0, 0);
+    } else {
+      xload(0);
+      xstore(0);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int grp = 0; grp < ngrp; ++grp) {
       const bool more = grp + 1 < ngrp;
+      if constexpr (PRE) s_xcur = s_x + (size_t)(grp & 1) * XRP * 64;
       auto stage = [&](auto hc) {
         constexpr int h = decltype(hc)::value;
         constexpr int T0 = h * KS, T1 = (h + 1) * KS < K ? (h + 1) * KS : K;
@@ -774,18 +851,24 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
           dma(grp, T1, T2 - T1, nxt);
         } else if (more) {
           dma(grp + 1, 0, KS, nxt);
-          if constexpr (MT < 4) xload(grp + 1);  // MT 4: after the MFMAs (128 VGPRs hold no prefetch)
+          if constexpr (PRE) rdma(grp + 1, (grp + 1) & 1);  // (its buffer's last reader: block grp - 1)
+          else if constexpr (MT < 4) xload(grp + 1);  // MT 4: after the MFMAs (128 VGPRs hold no prefetch)
         }
         mma_taps(std::integral_constant<int, T0>{}, std::integral_constant<int, T1>{}, cur);
         if constexpr (h + 1 < NH) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           __syncthreads();
         } else if (more) {
-          __syncthreads();  // every wave is done with this block's input rows
-          if constexpr (MT >= 4) xload(grp + 1);
-          xstore(grp + 1);
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __syncthreads();
+          if constexpr (PRE) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+          } else {
+            __syncthreads();  // every wave is done with this block's input rows
+            if constexpr (MT >= 4) xload(grp + 1);
+            xstore(grp + 1);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+          }
         }
       };
       stage(std::integral_constant<int, 0>{});
@@ -839,7 +922,7 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
     const int t = qb * a.ostride + ophase_;
     float* yrow = a.y + (size_t)(sd.x + t) * a.ld_dst;
     const float* rrow = a.res ? a.res + (size_t)(sr.x + t) * a.ld_res : nullptr;
-    cn_store_col<MT>(a, acc[nc], bias_, m0, hh, yrow, rrow);
+    cn_store_col<MT>(a, acc[nc], bias_, m0, hh, yrow, rrow, (long long)(sd.x + t));
   }
 }
 
@@ -956,31 +1039,43 @@ hipError_t xtile_launch(int mt, int k, bool sync, int ks, dim3 grid, int lds, hi
 // occupy a few dozen CUs spreads over all of them. Every column sums the same products in the same
 // order as on the 8-wave kernels: bit-identical.
 constexpr int narrow_ks(int k) { return k <= 3 ? k : (k == 5 ? 3 : 4); }
-template <int MT, int NWV>
+template <int MT, int NWV, bool PRE>
 hipError_t xtile_launch_narrow_mt(int k, dim3 grid, int lds, hipStream_t s, const CnConvArgs& a, const CnXtileArgs& xt) {
-  auto go = [&](auto kfn) -> hipError_t {
-    const hipError_t e = allow_lds(reinterpret_cast<const void*>(kfn), lds);
+  auto go = [&](auto kfn, int ks) -> hipError_t {
+    // PRE: two row buffers of the rounded span (64 B rows) after the two A buffers
+    const int l = PRE ? 2 * ks * MT * 2048 + 2 * ((32 * NWV + (k == 2 ? 16 : NARROW_HALO) + 15) / 16 * 16) * 64 : lds;
+    const hipError_t e = allow_lds(reinterpret_cast<const void*>(kfn), l);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kfn, grid, dim3(64 * NWV), (size_t)lds, s, a, xt);
+    hipLaunchKernelGGL(kfn, grid, dim3(64 * NWV), (size_t)l, s, a, xt);
     return hipGetLastError();
   };
   switch (k) {
-    case 2: return go(pwg_cnet_xtile_kernel<MT, 2, 1, 1, false, narrow_ks(2), true, NWV>);
-    case 3: return go(pwg_cnet_xtile_kernel<MT, 3, 1, 1, false, narrow_ks(3), true, NWV>);
-    case 5: return go(pwg_cnet_xtile_kernel<MT, 5, 1, 1, false, narrow_ks(5), true, NWV>);
-    case 7: return go(pwg_cnet_xtile_kernel<MT, 7, 1, 1, false, narrow_ks(7), true, NWV>);
-    case 11: return go(pwg_cnet_xtile_kernel<MT, 11, 1, 1, false, narrow_ks(11), true, NWV>);
+    case 2: return go(pwg_cnet_xtile_kernel<MT, 2, 1, 1, false, narrow_ks(2), true, NWV, PRE>, narrow_ks(2));
+    case 3: return go(pwg_cnet_xtile_kernel<MT, 3, 1, 1, false, narrow_ks(3), true, NWV, PRE>, narrow_ks(3));
+    case 5: return go(pwg_cnet_xtile_kernel<MT, 5, 1, 1, false, narrow_ks(5), true, NWV, PRE>, narrow_ks(5));
+    case 7: return go(pwg_cnet_xtile_kernel<MT, 7, 1, 1, false, narrow_ks(7), true, NWV, PRE>, narrow_ks(7));
+    case 11: return go(pwg_cnet_xtile_kernel<MT, 11, 1, 1, false, narrow_ks(11), true, NWV, PRE>, narrow_ks(11));
     default: return hipErrorInvalidValue;
   }
 }
-hipError_t xtile_launch_narrow(int mt, int nwv, int k, dim3 grid, int lds, hipStream_t s, const CnConvArgs& a,
+// pre: the input rows from the source's pre-split image (xt.simg)
+hipError_t xtile_launch_narrow(int mt, int nwv, int k, bool pre, dim3 grid, int lds, hipStream_t s, const CnConvArgs& a,
                                const CnXtileArgs& xt) {
-  if (mt == 1 && nwv == 1) return xtile_launch_narrow_mt<1, 1>(k, grid, lds, s, a, xt);
-  if (mt == 1 && nwv == 2) return xtile_launch_narrow_mt<1, 2>(k, grid, lds, s, a, xt);
-  if (mt == 1 && nwv == 4) return xtile_launch_narrow_mt<1, 4>(k, grid, lds, s, a, xt);
-  if (mt == 2 && nwv == 1) return xtile_launch_narrow_mt<2, 1>(k, grid, lds, s, a, xt);
-  if (mt == 2 && nwv == 2) return xtile_launch_narrow_mt<2, 2>(k, grid, lds, s, a, xt);
-  if (mt == 2 && nwv == 4) return xtile_launch_narrow_mt<2, 4>(k, grid, lds, s, a, xt);
+  if (pre) {
+    if (mt == 1 && nwv == 1) return xtile_launch_narrow_mt<1, 1, true>(k, grid, lds, s, a, xt);
+    if (mt == 1 && nwv == 2) return xtile_launch_narrow_mt<1, 2, true>(k, grid, lds, s, a, xt);
+    if (mt == 1 && nwv == 4) return xtile_launch_narrow_mt<1, 4, true>(k, grid, lds, s, a, xt);
+    if (mt == 2 && nwv == 1) return xtile_launch_narrow_mt<2, 1, true>(k, grid, lds, s, a, xt);
+    if (mt == 2 && nwv == 2) return xtile_launch_narrow_mt<2, 2, true>(k, grid, lds, s, a, xt);
+    if (mt == 2 && nwv == 4) return xtile_launch_narrow_mt<2, 4, true>(k, grid, lds, s, a, xt);
+    return hipErrorInvalidValue;
+  }
+  if (mt == 1 && nwv == 1) return xtile_launch_narrow_mt<1, 1, false>(k, grid, lds, s, a, xt);
+  if (mt == 1 && nwv == 2) return xtile_launch_narrow_mt<1, 2, false>(k, grid, lds, s, a, xt);
+  if (mt == 1 && nwv == 4) return xtile_launch_narrow_mt<1, 4, false>(k, grid, lds, s, a, xt);
+  if (mt == 2 && nwv == 1) return xtile_launch_narrow_mt<2, 1, false>(k, grid, lds, s, a, xt);
+  if (mt == 2 && nwv == 2) return xtile_launch_narrow_mt<2, 2, false>(k, grid, lds, s, a, xt);
+  if (mt == 2 && nwv == 4) return xtile_launch_narrow_mt<2, 4, false>(k, grid, lds, s, a, xt);
   return hipErrorInvalidValue;
 }
 
@@ -1017,8 +1112,7 @@ struct CnXdmaArgs {
   int n_oimg, oimg_rowb;
   int row0[2];    // PRE, K = 1: the row offset every chunk of source s shares, or INT_MIN (1x1s: 0)
 };
-// 16 zero bytes: the DMA source of a pre-split row outside a zero-padded utterance
-__device__ __attribute__((aligned(64))) unsigned g_cn_zero16[16];
+
 constexpr int XDMA_CHUNKS_MAX = 256;  // K = 1 mode: chunks per op (the table sits in LDS)
 #ifndef PWG_XDMA_K1_G
 #define PWG_XDMA_K1_G 4
@@ -1494,21 +1588,9 @@ __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArg
           *reinterpret_cast<f32x4v*>(yrow + row) = v;
           // pre-split images of these 4 channels for the consumers (the conversion those consumers'
           // own staging would apply to the stored values: bit-identical)
-          for (int j = 0; j < xd.n_oimg; ++j) {
-            const float sl = xd.oslope[j];
-            _Float16 hv[4], lv[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              float x = v[i];
-              if (sl != 1.f) x = x > 0.f ? x : x * sl;
-              hv[i] = (_Float16)x;
-              lv[i] = (_Float16)(x - (float)hv[i]);
-            }
-            unsigned char* const d = xd.oimg[j] + (long long)(fr.x * xd.rate_dst + t_out) * xd.oimg_rowb +
-                                     (row >> 4) * 64 + (row & 15) * 2;
-            *reinterpret_cast<f16x4v*>(d) = f16x4v{hv[0], hv[1], hv[2], hv[3]};
-            *reinterpret_cast<f16x4v*>(d + 32) = f16x4v{lv[0], lv[1], lv[2], lv[3]};
-          }
+          const float vv[4] = {v[0], v[1], v[2], v[3]};
+          for (int j = 0; j < xd.n_oimg; ++j)
+            cn_img4(xd.oimg[j], (long long)(fr.x * xd.rate_dst + t_out), xd.oimg_rowb, row, vv, xd.oslope[j]);
         }
     } else {
       cn_store_col<MT>(a, acc, bias_, m0, hh, yrow, rrow);
@@ -4529,8 +4611,18 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
     std::vector<int> last_wr(nb, -1);
     for (int oi = 0; oi < nops; ++oi) last_wr[n->ops[oi].dst] = oi;
     auto xdma_phase = [&](size_t q) { return p->nar_xdma[q] && p->nar_nwv[q] > 0 && !in_chain[q]; };
+    // narrow x-tile launches (the DMA-staged x-tile kernel) read images too, and every launch of
+    // the x-tile kernel writes them (its epilogue); whether a phase ends up on those kernels is
+    // decided per run (fused pairs / stacks, options), which the run-time image state follows
+    auto xtile_reader = [&](size_t q) {
+      return n->xtile && p->nar_nwv[q] > 0 && !p->nar_tap[q] && !p->nar_xdma[q] && !in_chain[q];
+    };
+    auto img_writer = [&](size_t q) {
+      const OpPhase& ph = n->phases[q];
+      return !in_chain[q] && (xdma_phase(q) || (n->xtile && (ph.xtile || ph.xt_convt_db)));
+    };
     for (size_t pi = 0; pi < nph; ++pi) {
-      if (!xdma_phase(pi)) continue;
+      if (!xdma_phase(pi) && !xtile_reader(pi)) continue;
       const PwgCnetOp& op = n->ops[n->phases[pi].op];
       const int nsrc = p->nar_tap[pi] && op.src[1].buf >= 0 && op.kind == PWG_CNET_CONV ? 2 : 1;
       for (int si = 0; si < nsrc; ++si) {
@@ -4538,7 +4630,7 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
         const int b = src.buf;
         if (b <= 0 || b >= nb - 1 || src.normalize || n->channels[b] % 16 != 0 || last_wr[b] < 0) continue;
         bool writer_dma = false;
-        for (size_t q = 0; q < nph; ++q) writer_dma |= n->phases[q].op == last_wr[b] && xdma_phase(q);
+        for (size_t q = 0; q < nph; ++q) writer_dma |= n->phases[q].op == last_wr[b] && img_writer(q);
         if (!writer_dma) continue;
         int k = -1, per_buf = 0;
         for (size_t j = 0; j < p->simg_buf.size(); ++j)
@@ -4934,6 +5026,8 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
       CnConvArgs a;
       a.range_flag = nullptr;
       a.xcd_order = n->xcd_order;
+      a.n_oimg = 0;
+      a.oimg_rowb = n->channels[op.dst] * 4;
       const int nsrc = (op.src[1].buf >= 0 && op.kind == PWG_CNET_CONV) ? 2 : 1;
       for (int si = 0; si < 2; ++si) {
         const PwgCnetSrc& src = op.src[si];
@@ -5007,6 +5101,8 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         }
       } else if (xt && (ph.xtile || (ph.xt_convt_db && (n->xt_dma & CNET_DMA_CONVT)))) {
         CnXtileArgs xt;
+        xt.simg = nullptr;
+        xt.simg_rowb = 0;
         const bool convt = op.kind == PWG_CNET_CONVT;
         xt.K = convt ? 2 : op.src[0].taps; xt.dil = convt ? 1 : op.src[0].dilation;
         xt.off_min = convt ? ph.off_a - 1 : -op.src[0].pad;
@@ -5021,6 +5117,19 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
           xgrid.x = (unsigned)p->n_xblocks[pi];
         }
         hipError_t ea2;
+        // pre-split images of this launch's output (the x-tile kernel's epilogue; the DMA-ring
+        // launches below set their own)
+        auto xtile_images = [&]() {
+          a.n_oimg = 0;
+          if ((n->ld[op.dst] & 3) != 0) return;
+          for (int j = 0; j < 2; ++j) {
+            const int k = p->ph_oimg[2 * pi + j];
+            if (k < 0) continue;
+            a.oimg[a.n_oimg] = img_ptr(k);
+            a.oslope[a.n_oimg] = p->simg_slope[k];
+            ++a.n_oimg;
+          }
+        };
         if (narrow(pi)) {
           const int nw = p->nar_nwv[pi], mtn = p->nar_mt[pi];
           xt.span = 32 * nw + (xt.K - 1) * xt.dil;
@@ -5039,9 +5148,18 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
             wrote_img = xd.n_oimg > 0;
             ea2 = xdma_launch(mtn, nw, xt.K, pre, ngrid, s, a, xd);
           } else {
-            ea2 = xtile_launch_narrow(mtn, nw, xt.K, ngrid, p->nar_lds[pi], s, a, xt);
+            xtile_images();
+            wrote_img = a.n_oimg > 0;
+            const int k0 = p->ph_simg[2 * pi];
+            const bool pre = n->presplit && !a.src[0].normalize && k0 >= 0 && img_state[k0] == 1;
+            xt.simg = pre ? img_ptr(k0) : nullptr;
+            xt.simg_rowb = pre ? n->channels[p->simg_buf[k0]] * 4 : 0;
+            ea2 = xtile_launch_narrow(mtn, nw, xt.K, pre, ngrid, p->nar_lds[pi], s, a, xt);
+            a.n_oimg = 0;
           }
         } else {
+          xtile_images();
+          wrote_img = a.n_oimg > 0;
           const bool db = ph.xt_convt_db ||
                           (ph.xt_db && ((n->xt_dma & CNET_DMA_ALL) || ((n->xt_dma & CNET_DMA_RULE) && ph.xt_db_pick)));
           const int dv = (n->xt_dma & CNET_DMA_FEWEST) ? 1 : 0;

@@ -583,9 +583,9 @@ def test_fused_stack_chain_bitwise_equal(cfg, built_lib, cuda_device):
 
 @pytest.mark.parametrize("cfg", ["mb_melgan_v2", "hifigan_v1", "melgan_v1", "hifigan_causal_test"])
 def test_presplit_images_bitwise_equal(cfg, built_lib, cuda_device):
-    """PWG_CNET_OPT_PRESPLIT: DMA-ring launches whose inputs were written by DMA-ring launches stage
-    the writers' pre-split images (pre-activated, fp16 hi / lo rows) instead of converting the fp32
-    rows in every workgroup and step. The same conversion of the same values, done once: bit-identical
+    """PWG_CNET_OPT_PRESPLIT: DMA-ring and narrow x-tile launches whose inputs were written by DMA-ring
+    or x-tile launches stage the writers' pre-split images (pre-activated, fp16 hi / lo rows) instead
+    of converting the fp32 rows in every workgroup and step. The same conversion of the same values, done once: bit-identical
     to presplit off at B = 1 (short utterances: every block touches an edge; zero and reflect padding)
     and on a ragged batch, with fused stack chains on and off."""
     from parallelwavegan_amd import configs, synthetic
@@ -599,7 +599,9 @@ def test_presplit_images_bitwise_equal(cfg, built_lib, cuda_device):
         m.pqmf = PQMF(**configs.VOCODER_PQMF[cfg])
     m = m.to(cuda_device)
     eng = m.engine()
-    singles = [synthetic.make_mel(f, 80, seed=500 + f) for f in (64, 9, 131, 5)]
+    # (131 and 300 frames: HiFiGAN's 128- and 64-channel stages on the narrow x-tile kernel, which
+    # reads images written by the x-tile kernels' epilogue)
+    singles = [synthetic.make_mel(f, 80, seed=500 + f) for f in (64, 9, 131, 5, 300)]
     batch = [synthetic.make_mel(f, 80, seed=510 + i) for i, f in enumerate([5, 40, 17, 64])]
     with torch.no_grad():
         outs = {}
