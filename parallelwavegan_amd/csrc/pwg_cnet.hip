@@ -474,7 +474,8 @@ constexpr int XT_ROWB = 80;  // bytes per staged input row: 16 hi + 16 lo halves
 // kernels' epilogue arithmetic). With quad-aligned rows every bias / residual / y_old load is issued
 // before the first store: the stores may alias the later loads for the compiler, which otherwise
 // serialises one load round trip per 4 rows (MT x 4 of them, ~1 us each at B = 1).
-template <int MT>
+// IMG: also the pre-split images a.oimg (narrow launches only: the wide kernels keep their epilogue)
+template <int MT, bool IMG = false>
 __device__ __forceinline__ void cn_store_col(const CnConvArgs& a, const f32x16 (&acc)[MT], const float* bias_, int m0,
                                              int hh, float* yrow, const float* rrow, long long irow = 0) {
   auto finish = [&](f32x4v v) {
@@ -526,8 +527,10 @@ __device__ __forceinline__ void cn_store_col(const CnConvArgs& a, const f32x16 (
           for (int i = 0; i < 4; ++i)
             if (row + i >= a.M) v[i] = 0.f;
           *reinterpret_cast<f32x4v*>(yrow + row) = v;
-          const float vv[4] = {v[0], v[1], v[2], v[3]};
-          for (int j = 0; j < a.n_oimg; ++j) cn_img4(a.oimg[j], irow, a.oimg_rowb, row, vv, a.oslope[j]);
+          if constexpr (IMG) {
+            const float vv[4] = {v[0], v[1], v[2], v[3]};
+            for (int j = 0; j < a.n_oimg; ++j) cn_img4(a.oimg[j], irow, a.oimg_rowb, row, vv, a.oslope[j]);
+          }
         }
     }
     return;
@@ -922,7 +925,7 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
     const int t = qb * a.ostride + ophase_;
     float* yrow = a.y + (size_t)(sd.x + t) * a.ld_dst;
     const float* rrow = a.res ? a.res + (size_t)(sr.x + t) * a.ld_res : nullptr;
-    cn_store_col<MT>(a, acc[nc], bias_, m0, hh, yrow, rrow, (long long)(sd.x + t));
+    cn_store_col<MT, DB && NWV < 8>(a, acc[nc], bias_, m0, hh, yrow, rrow, (long long)(sd.x + t));
   }
 }
 
@@ -4611,16 +4614,13 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
     std::vector<int> last_wr(nb, -1);
     for (int oi = 0; oi < nops; ++oi) last_wr[n->ops[oi].dst] = oi;
     auto xdma_phase = [&](size_t q) { return p->nar_xdma[q] && p->nar_nwv[q] > 0 && !in_chain[q]; };
-    // narrow x-tile launches (the DMA-staged x-tile kernel) read images too, and every launch of
-    // the x-tile kernel writes them (its epilogue); whether a phase ends up on those kernels is
-    // decided per run (fused pairs / stacks, options), which the run-time image state follows
+    // narrow x-tile launches (the DMA-staged x-tile kernel) read and, in their epilogue, write images
+    // too; whether a phase ends up on those kernels is decided per run (fused pairs / stacks,
+    // options), which the run-time image state follows
     auto xtile_reader = [&](size_t q) {
       return n->xtile && p->nar_nwv[q] > 0 && !p->nar_tap[q] && !p->nar_xdma[q] && !in_chain[q];
     };
-    auto img_writer = [&](size_t q) {
-      const OpPhase& ph = n->phases[q];
-      return !in_chain[q] && (xdma_phase(q) || (n->xtile && (ph.xtile || ph.xt_convt_db)));
-    };
+    auto img_writer = [&](size_t q) { return xdma_phase(q) || xtile_reader(q); };  // (narrow launches)
     for (size_t pi = 0; pi < nph; ++pi) {
       if (!xdma_phase(pi) && !xtile_reader(pi)) continue;
       const PwgCnetOp& op = n->ops[n->phases[pi].op];
@@ -5117,8 +5117,8 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
           xgrid.x = (unsigned)p->n_xblocks[pi];
         }
         hipError_t ea2;
-        // pre-split images of this launch's output (the x-tile kernel's epilogue; the DMA-ring
-        // launches below set their own)
+        // pre-split images of a narrow x-tile launch's output (its epilogue; the DMA-ring launches
+        // below set their own)
         auto xtile_images = [&]() {
           a.n_oimg = 0;
           if ((n->ld[op.dst] & 3) != 0) return;
@@ -5158,8 +5158,6 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
             a.n_oimg = 0;
           }
         } else {
-          xtile_images();
-          wrote_img = a.n_oimg > 0;
           const bool db = ph.xt_convt_db ||
                           (ph.xt_db && ((n->xt_dma & CNET_DMA_ALL) || ((n->xt_dma & CNET_DMA_RULE) && ph.xt_db_pick)));
           const int dv = (n->xt_dma & CNET_DMA_FEWEST) ? 1 : 0;
