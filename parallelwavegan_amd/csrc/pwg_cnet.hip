@@ -3355,12 +3355,14 @@ __global__ void __launch_bounds__(256) pwg_cnet_finite_kernel(const float* y, lo
 // validated, so the kernel's output is the checked image.
 enum { CN_L_SEG = 0, CN_L_NCOL = 1, CN_L_BLK = 2, CN_L_NFR = 3 };
 constexpr int CN_DESC_UTTS = 64;   // utterances per descriptor launch
-constexpr int CN_DESC_SPECS = 40;  // lists per descriptor launch (kernel arguments ~2.6 KB)
+// lists per descriptor launch: every list of a vocoder plan in one launch (MB-MelGAN v2 77, HiFiGAN
+// v1 ~100) -- each launch sits on the B = 1 forward's critical path before its first op
+constexpr int CN_DESC_SPECS = 96;
 struct CnDescSpec {
   int kind, rate, ostride, ophase, step;
   int off;              // ints into the image
-  long long base_idx;   // entries of the utterances before this launch's first
-  long long base_row;   // CN_L_SEG: rows of the utterances before this launch's first
+  int base_idx;         // entries of the utterances before this launch's first (< 2^30: the image)
+  int base_row;         // CN_L_SEG: rows of the utterances before this launch's first (< 2^31)
 };
 struct CnDescArgs {
   int* img;
@@ -3371,6 +3373,7 @@ struct CnDescArgs {
   int frames[CN_DESC_UTTS];
   CnDescSpec specs[CN_DESC_SPECS];
 };
+static_assert(sizeof(CnDescArgs) <= 3584, "descriptor launch arguments within the 4 KB kernel-argument block");
 
 __host__ __device__ inline long long cn_list_cols(int kind, long long frames, int rate, int ostride, int ophase) {
   const long long T = frames * rate;
@@ -4699,8 +4702,8 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
       for (int k = 0; k < a.n_specs; ++k) {
         CnDescSpec sp = p->specs[s0 + k];
         for (int u = 0; u < u0; ++u) {
-          sp.base_idx += cn_list_count(sp.kind, cn_list_cols(sp.kind, frames[u], sp.rate, sp.ostride, sp.ophase), sp.step);
-          sp.base_row += frames[u] * sp.rate;
+          sp.base_idx += (int)cn_list_count(sp.kind, cn_list_cols(sp.kind, frames[u], sp.rate, sp.ostride, sp.ophase), sp.step);
+          sp.base_row += (int)(frames[u] * sp.rate);
         }
         a.specs[k] = sp;
       }
