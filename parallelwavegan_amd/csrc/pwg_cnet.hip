@@ -3492,6 +3492,7 @@ struct PwgCnet {
   struct CallerSet {
     hipStream_t aux[N_AUX] = {nullptr, nullptr, nullptr};
     std::vector<hipEvent_t> ev;
+    int* hflag = nullptr;  // pinned host word pwg_cnet_run_status copies the range flag into
   };
   std::map<hipStream_t, CallerSet> callers;
   std::mutex mu;       // `callers` (concurrent runs from host threads)
@@ -4254,6 +4255,7 @@ void pwg_cnet_destroy(PwgCnet* n) {
     for (hipStream_t x : kv.second.aux)
       if (x) (void)hipStreamDestroy(x);
     for (hipEvent_t e : kv.second.ev) (void)hipEventDestroy(e);
+    if (kv.second.hflag) (void)hipHostFree(kv.second.hflag);
   }
   delete n;
 }
@@ -5295,11 +5297,23 @@ int pwg_cnet_run_status(PwgCnetPlan* p, const void* workspace, void* stream) {
   if (!p || !workspace) return fail(PWG_ERR_INVALID, "null argument");
   Guard g(p->n->device);
   if (!g.ok) return fail(PWG_ERR_HIP, "hipSetDevice failed");
-  int flag = 0;
   hipStream_t s = (hipStream_t)stream;
-  hipError_t e = hipMemcpyAsync(&flag, (const char*)workspace + p->ws_flag, sizeof(int), hipMemcpyDeviceToHost, s);
+  // a pinned word per caller stream (a copy into pageable memory takes HIP's staged path: ~20-30 us
+  // of a B = 1 call, tools/diag/host_overhead.py)
+  int* hf = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(p->n->mu);
+    PwgCnet::CallerSet& cs = p->n->callers[s];
+    if (!cs.hflag && hipHostMalloc(reinterpret_cast<void**>(&cs.hflag), sizeof(int), hipHostMallocDefault) != hipSuccess) {
+      cs.hflag = nullptr;
+      return fail(PWG_ERR_HIP, "pinned status word");
+    }
+    hf = cs.hflag;
+  }
+  hipError_t e = hipMemcpyAsync(hf, (const char*)workspace + p->ws_flag, sizeof(int), hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) return hipf(e, "cnet run status");
+  const int flag = *hf;
   if (flag != 0)
     return fail(PWG_ERR_RANGE,
                 "non-finite program output in split-f16 mode: a value left the fp16 pair range upstream (or the "
