@@ -392,6 +392,10 @@ struct PwgHandle {
   int timing = 0;  // pwg_set_timing: 1 per-launch events, 2 one event pair around each run
   std::vector<TimingRecord> records;
   std::vector<hipEvent_t> event_pool;
+  // pinned host words pwg_run_status copies the run's and the sticky status into, per caller stream
+  // (a copy into pageable memory takes HIP's staged path, ~10-20 us of a B = 1 call)
+  std::map<hipStream_t, int*> hstatus;
+  std::mutex hstatus_mu;
 };
 
 struct PwgPlan {
@@ -534,6 +538,7 @@ void pwg_destroy(PwgHandle* h) {
     for (auto e : h->event_pool) (void)hipEventDestroy(e);
     if (h->d_status) (void)hipFree(h->d_status);
     if (h->d_trace) (void)hipFree(h->d_trace);
+    for (auto& kv : h->hstatus) (void)hipHostFree(kv.second);
   }
   delete h;
 }
@@ -1347,8 +1352,18 @@ int pwg_run_status(PwgPlan* p, const void* workspace, void* stream) {
   if (!p || !workspace) return fail(PWG_ERR_INVALID, "null argument");
   DeviceGuard g(p->h->device);
   if (!g.ok) return fail(PWG_ERR_HIP, "hipSetDevice failed");
-  int flag[2] = {0, 0};
   hipStream_t s = (hipStream_t)stream;
+  int* flag = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(p->h->hstatus_mu);
+    int*& w = p->h->hstatus[s];
+    if (!w && hipHostMalloc(reinterpret_cast<void**>(&w), 2 * sizeof(int), hipHostMallocDefault) != hipSuccess) {
+      w = nullptr;
+      return fail(PWG_ERR_HIP, "pinned status words");
+    }
+    flag = w;
+  }
+  flag[0] = flag[1] = 0;
   hipError_t e = hipMemcpyAsync(&flag[0], (const char*)workspace + p->ws_flag, sizeof(int), hipMemcpyDeviceToHost, s);
   // the handle's sticky word: every flag any run of this handle set since the previous status call
   // (a serving loop that checks once per batch of runs still sees an earlier run's abort); cleared
