@@ -3509,8 +3509,22 @@ struct PwgCnet {
   std::vector<hipEvent_t> pool;
 };
 
+struct CnSchedule {
+  std::vector<std::pair<int, int>> launches;  // (phase, second op fused into the launch or -1)
+  bool conc = false;
+  std::vector<int> stream, event;              // per launch: stream (0 = caller's), event slot or -1
+  std::vector<std::vector<int>> waits;         // per launch: launches on other streams it waits for
+  std::vector<size_t> order;                   // enqueue order
+  bool used[1 + PwgCnet::N_AUX] = {true, false, false, false};
+  int n_events = 0;
+};
+
 struct PwgCnetPlan {
   PwgCnet* n = nullptr;
+  // the run's launch schedule (cnet_schedule), cached for the options it was built under
+  // (sched_key; ~15-30 us of host work per eager run otherwise)
+  CnSchedule sched;
+  int sched_key = -1;
   int n_utts = 0;
   std::vector<long long> frames;
   std::vector<long long> rows;               // per buffer
@@ -3600,15 +3614,6 @@ float cn_h2f(uint16_t h) {
 
 // The launches of one run and, with PWG_CNET_OPT_STREAMS, their streams, cross-stream waits and
 // enqueue order (host only: pwg_cnet_run and pwg_cnet_plan_schedule).
-struct CnSchedule {
-  std::vector<std::pair<int, int>> launches;  // (phase, second op fused into the launch or -1)
-  bool conc = false;
-  std::vector<int> stream, event;              // per launch: stream (0 = caller's), event slot or -1
-  std::vector<std::vector<int>> waits;         // per launch: launches on other streams it waits for
-  std::vector<size_t> order;                   // enqueue order
-  bool used[1 + PwgCnet::N_AUX] = {true, false, false, false};
-  int n_events = 0;
-};
 // phase pi heads a fused stack chain this run launches as one pwg_mstack_kernel (split-f16 x-tile
 // mode with fused ops, and the plan picked a block width for it)
 bool cnet_mstack_on(const PwgCnetPlan* p, size_t pi) {
@@ -4849,11 +4854,18 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
   auto probe_slot = [](size_t) { return -1; };
 #endif
   const int NS = 1 + PwgCnet::N_AUX;
-  CnSchedule sc;
   {
-    const int rc = cnet_schedule(p, sc);
-    if (rc != PWG_OK) return rc;
+    const int key = (n->fuse_pairs ? 1 : 0) | (n->split_f16 ? 2 : 0) | (n->xtile ? 4 : 0) | (n->streams << 3);
+    std::lock_guard<std::mutex> lk(n->mu);
+    if (p->sched_key != key) {
+      p->sched = CnSchedule{};
+      p->sched_key = -1;
+      const int rc = cnet_schedule(p, p->sched);
+      if (rc != PWG_OK) return rc;
+      p->sched_key = key;
+    }
   }
+  const CnSchedule& sc = p->sched;
   const std::vector<std::pair<int, int>>& launches = sc.launches;
   const bool conc = sc.conc;
   const std::vector<int>& l_stream = sc.stream;
