@@ -15,9 +15,13 @@
 //   * h stays in registers: conv A's accumulators (+ b_A, lrelu) become the 1x1's B operands by a
 //     cross-half exchange per 16 channels (the 32x32 MFMA's C layout holds rows 8 j + 4 hh + i, the
 //     B layout channels 8 hh + i);
-//   * the weight fragments stream through a 3-slot LDS ring by global_load_lds, two steps ahead
-//     (a step = one 16-channel block of conv A with its 3 taps, or 3 chunks of the 1x1), across
-//     stack boundaries.
+//   * the weight fragments stream through an LDS ring (3-6 slots by channel count) by
+//     global_load_lds, a few steps ahead (a step = one 16-channel block of conv A with its 3 taps,
+//     or 3 chunks of the 1x1), across stack boundaries;
+//   * conv A's B operands of a channel block are pre-activated and pair-split once per workgroup
+//     into one of two converted blocks, two steps ahead, and read by every tap and wave; the 1x1's
+//     operands (h from the accumulators, x_j's own columns) are prepared per wave, each step's
+//     during the previous step's MFMAs.
 // Every output column sums the same products in the same order as the executor's launches (conv A
 // channel-block-major with taps inner, pwg_cnet_xtile_kernel / the DMA-ring kernel; the 1x1 in its
 // chunk order [h blocks][x blocks], pwg_cnet_conv_kernel), with the same pre-activations, pair
