@@ -1114,6 +1114,8 @@ struct CnXdmaArgs {
   float oslope[2];
   int n_oimg, oimg_rowb;
   int row0[2];    // PRE, K = 1: the row offset every chunk of source s shares, or INT_MIN (1x1s: 0)
+  int k1_n0;      // K = 1: n0 >= 0 when the chunk list is [source 0 blocks 0..n0-1][source 1 blocks],
+                  // row offset 0 (every 1x1): descriptors by arithmetic, no table; else -1
 };
 
 constexpr int XDMA_CHUNKS_MAX = 256;  // K = 1 mode: chunks per op (the table sits in LDS)
@@ -1298,13 +1300,28 @@ __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArg
   }
 
   // K = 1: the op's chunk list, staged in LDS before the first DMA (one ordinary load round trip)
+  // (a 1x1's list is arithmetic: no table, so no global round trip and barrier before the first DMA)
   ChunkDesc* const s_ch = reinterpret_cast<ChunkDesc*>(xt_smem + (size_t)P * S::SLOT + 2 * S::CBUF);
+  const int k1n0 = xd.k1_n0;
   if constexpr (K == 1) {
-    for (int c = threadIdx.x; c < nch; c += NTH) s_ch[c] = chunks_[c];
-    __syncthreads();
+    if (k1n0 < 0) {
+      for (int c = threadIdx.x; c < nch; c += NTH) s_ch[c] = chunks_[c];
+      __syncthreads();
+    }
   }
+  auto chunk_at = [&](int i) -> ChunkDesc {
+    if (k1n0 >= 0) {
+      ChunkDesc c;
+      c.src = i >= k1n0 ? 1 : 0;
+      c.row_off = 0;
+      c.c0 = 16 * (i - (c.src ? k1n0 : 0));
+      c.pad = 0;
+      return c;
+    }
+    return s_ch[i];
+  };
   auto chunk = [&](int s) -> ChunkDesc {
-    ChunkDesc c = s_ch[s];
+    ChunkDesc c = chunk_at(s);
     c.src = __builtin_amdgcn_readfirstlane(c.src);
     c.row_off = __builtin_amdgcn_readfirstlane(c.row_off);
     c.c0 = __builtin_amdgcn_readfirstlane(c.c0);
@@ -1339,7 +1356,7 @@ __global__ void __launch_bounds__(64 * NWV) pwg_cnet_xdma_kernel(const CnConvArg
       // the step's chunk descriptors: every LDS read first, one wait
       ChunkDesc cdr[S::G];
 #pragma unroll
-      for (int t = 0; t < S::G; ++t) cdr[t] = s_ch[min(s * S::G + t, nch - 1)];
+      for (int t = 0; t < S::G; ++t) cdr[t] = chunk_at(min(s * S::G + t, nch - 1));
 #pragma unroll
       for (int t = 0; t < S::G; ++t) {
         const int csrc = __builtin_amdgcn_readfirstlane(cdr[t].src);
@@ -5161,6 +5178,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
             xdma_rows(xd, pi);
             for (int r = 0; r < 8; ++r) xd.z_off[r] = xt.z_off[r];
             xd.row0[0] = xd.row0[1] = INT_MIN;
+            xd.k1_n0 = -1;
             const bool pre = xdma_images(xd, pi, 1);
             wrote_img = xd.n_oimg > 0;
             ea2 = xdma_launch(mtn, nw, xt.K, pre, ngrid, s, a, xd);
@@ -5201,6 +5219,18 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
                 same &= c.row_off == r0;
               }
             xd.row0[si] = same ? r0 : INT_MIN;
+          }
+          {  // canonical 1x1 list: [source 0 blocks 0..n0-1][source 1 blocks 0..], row offset 0
+            const int nc = (int)ph.chunks.size();
+            int n0 = 0;
+            while (n0 < nc && ph.chunks[n0].src == 0) ++n0;
+            bool canon = true;
+            for (int i = 0; i < nc && canon; ++i) {
+              const ChunkDesc& c = ph.chunks[i];
+              const int src = i >= n0 ? 1 : 0;
+              canon = c.src == src && c.row_off == 0 && c.c0 == 16 * (i - (src ? n0 : 0));
+            }
+            xd.k1_n0 = canon ? n0 : -1;
           }
           const bool pre = xdma_images(xd, pi, nsrc);
           wrote_img = xd.n_oimg > 0 && p->n_nblocks[pi] > 0;
