@@ -179,10 +179,15 @@ PWG_API int pwg_cnet_plan_schedule(PwgCnetPlan* p, int cap, int* n_launches, int
  * launches): a buffer that DMA-ring launches read with a LeakyReLU slope gets a pre-split image
  * (its rows pre-activated and split into fp16 hi / lo pairs) written by its last writer's epilogue
  * when that writer is a DMA-ring launch too; the readers then stage those rows as they are instead of
- * converting them in every workgroup and step. Bit-identical (the same conversion, done once). */
+ * converting them in every workgroup and step. Bit-identical (the same conversion, done once).
+ * PWG_CNET_OPT_RSTACK (default 1, split-f16 x-tile mode with fused ops): the batched launch of a fused
+ * ResidualStack with 32-96 channels (16-channel multiples, no epilogue extras) runs the persistent
+ * LDS-ring kernel (weights and input rows streamed by global_load_lds two steps ahead across tiles,
+ * h in registers) instead of the x-tile stack kernel. Bit-identical; 0 for the x-tile stack (A/B). */
 enum { PWG_CNET_OPT_SPLIT_F16 = 0, PWG_CNET_OPT_FUSE_PAIRS = 1, PWG_CNET_OPT_PAIR_STEPS = 2, PWG_CNET_OPT_XTILE = 3,
        PWG_CNET_OPT_XT_DMA = 4, PWG_CNET_OPT_XCD_ORDER = 5, PWG_CNET_OPT_NARROW = 6, PWG_CNET_OPT_NARROW_DMA = 7,
-       PWG_CNET_OPT_STREAMS = 8, PWG_CNET_OPT_MSTACK = 9, PWG_CNET_OPT_PRESPLIT = 10 };
+       PWG_CNET_OPT_STREAMS = 8, PWG_CNET_OPT_MSTACK = 9, PWG_CNET_OPT_PRESPLIT = 10,
+       PWG_CNET_OPT_RSTACK = 11 };
 PWG_API int pwg_cnet_set_option(PwgCnet* n, int option, long long value);
 /* Timing: 0 off, 1 HIP events around every launch (per-bucket / per-op sums), 2 one event pair
  * around each whole run on the caller's stream (its device span only; no events between launches,

@@ -26,6 +26,7 @@ CSRC = [
     os.path.join(PKG_DIR, "csrc", "pwg_split16.hip"),
     os.path.join(PKG_DIR, "csrc", "pwg_rccl.hip"),
     os.path.join(PKG_DIR, "csrc", "pwg_mstack.hip"),
+    os.path.join(PKG_DIR, "csrc", "pwg_rstack.hip"),
 ]
 HEADERS = [
     os.path.join(REPO_DIR, "include", "pwg.h"),

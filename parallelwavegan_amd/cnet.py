@@ -576,6 +576,13 @@ class CnetEngine:
         self._graph_epoch += 1
         self._plans.clear()
 
+    def set_rstack(self, enable):
+        """pwg_cnet_set_option(PWG_CNET_OPT_RSTACK): batched fused ResidualStacks of 32-96 channels
+        on the persistent LDS-ring kernel (pwg_rstack.hip, default) or, 0, on the x-tile stack
+        kernel. Run-time; bit-identical."""
+        _lib.check(self._lib.pwg_cnet_set_option(self._h, 11, 1 if enable else 0))
+        self._graph_epoch += 1
+
     def set_narrow_dma(self, enable):
         """pwg_cnet_set_option(PWG_CNET_OPT_NARROW_DMA): narrow launches on the DMA-ring kernel
         (default) or, 0, on the narrow x-tile / tap-major kernels. Plan-time (cached plans are

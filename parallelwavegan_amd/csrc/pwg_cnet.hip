@@ -3476,6 +3476,7 @@ struct OpPhase {          // one launch
   int xstack_lds = 0;         // > 0: with x-tile on, the stack runs pwg_cnet_xstack_kernel (256-column blocks)
   int xstack_g2 = 0;          // its stage-2 chunks per staged group
   int xstack_xoff = 0;        // its input-row / h-tile region offset
+  int rstack_cs = 0;          // > 0: the stack also fits pwg_rstack.hip (16-channel blocks; PWG_CNET_OPT_RSTACK)
   int ms_n = 0;               // > 0: head of a chain of this many fusable ResidualStacks (pwg_mstack.hip)
   int ms_halo = 0;            // ... their summed dilations
 };
@@ -3498,6 +3499,7 @@ struct PwgCnet {
                        // x-tile / tap-major kernels)
   int mstack = 1;      // PWG_CNET_OPT_MSTACK (plan time): 0 off, 1 fused stack chains in plans whose first
                        // conv of the chain runs narrow, 2 every chain
+  int rstack = 1;      // PWG_CNET_OPT_RSTACK: batched ResidualStacks on pwg_rstack.hip (else the x-tile stack)
   int presplit = 1;    // PWG_CNET_OPT_PRESPLIT (plan time): DMA-ring launches write / read pre-split images
   int streams = 1;     // PWG_CNET_OPT_STREAMS: 0 one stream, 1 independent launches of plans with narrow
                        // launches run on auxiliary streams, 2 every plan
@@ -4120,6 +4122,23 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
       }
     }
     if (pa.xstack_lds == 0) pa.xtile = false;
+    // the batched stack kernel (pwg_rstack.hip): C = 16 cs channels in and out of both ops, y rows of
+    // exactly C floats, op B with the executor's chunk order [h blocks][x blocks] and no epilogue
+    // extras, conv A's taps within the kernel's row window
+    if (pa.xtile && pa.xstack_lds > 0) {
+      const int C = A.out_channels, cs = C / 16;
+      const PwgCnetSrc& xa = A.src[0];
+      bool rs = C % 16 == 0 && rstack_supported(cs) && xa.channels == C && B.out_channels == C &&
+                pa.MT == (cs + 1) / 2 && n->ld[B.dst] == C && n->ld[xa.buf] % 4 == 0 && n->ld[xa.buf] >= C &&
+                !xa.normalize && !b1.normalize && B.res < 0 && !B.accumulate && B.out_div == 1.f &&
+                B.post_act == PWG_ACT_NONE && xa.dilation >= 1 && 2 * xa.dilation <= RS_MAX_REACH &&
+                xa.pad >= 0 && xa.pad <= 2 * xa.dilation && (int)pb.chunks.size() == 2 * cs;
+      for (int c = 0; rs && c < 2 * cs; ++c) {
+        const ChunkDesc& cd = pb.chunks[c];
+        rs = cd.src == (c < cs ? 0 : 1) && cd.row_off == 0 && cd.c0 == 16 * (c % cs);
+      }
+      if (rs) pa.rstack_cs = cs;
+    }
   }
   // x-tile conv pairs (pwg_cnet_xpair_kernel): both convs on the x-tile kernel, 32 or 64 channels
   // (128 at k = 3) in one row tile, conv 1 single-source zero-padded with no epilogue extras, conv 2 the only
@@ -5020,9 +5039,23 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
           xs.K1 = op.src[0].taps; xs.dil1 = op.src[0].dilation; xs.off1 = -op.src[0].pad;
           xs.cs1 = op.src[0].channels / 16; xs.span1 = XT_COLS + (xs.K1 - 1) * xs.dil1; xs.g2 = ph.xstack_g2;
           xs.x_off = ph.xstack_xoff;
-          const hipError_t ea2 =
-              xstack_launch(ph.MT, xs.K1, dim3((unsigned)p->n_xblocks[pi]), ph.xstack_lds, s, a, xs);
-          if (ea2 != hipSuccess) return hipf(ea2, "xstack kernel launch");
+          if (n->rstack && ph.rstack_cs > 0) {
+            RstackArgs r;
+            r.x = a.x1.x; r.seg_x = a.x1.seg; r.ld_x = a.x1.ld; r.mode_x = a.x1.pad_mode;
+            r.dil = xs.dil1; r.off = xs.off1; r.slope1 = a.x1.slope;
+            r.mode_2 = a.x2.pad_mode; r.slope2 = a.x2.slope; r.slope_h = a.slope_h;
+            r.wA = a.w1; r.bA = a.b1; r.wB = a.w2; r.bB = a.b2;
+            r.y = a.y; r.seg_y = a.seg_y;
+            r.blocks = a.blocks; r.ncols = a.ncols; r.n_blocks = p->n_xblocks[pi];
+            // persistent workgroups, one per CU (the ring fills the LDS), each a contiguous range
+            const int n_wg = std::max(std::min(r.n_blocks, std::max(p->n_cu, 1)), (r.n_blocks + RS_MAX_TILES - 1) / RS_MAX_TILES);
+            const hipError_t ea2 = launch_rstack(r, ph.rstack_cs, n_wg, s);
+            if (ea2 != hipSuccess) return hipf(ea2, "rstack kernel launch");
+          } else {
+            const hipError_t ea2 =
+                xstack_launch(ph.MT, xs.K1, dim3((unsigned)p->n_xblocks[pi]), ph.xstack_lds, s, a, xs);
+            if (ea2 != hipSuccess) return hipf(ea2, "xstack kernel launch");
+          }
         } else {
         const void* kf = nullptr;
         switch (ph.mt_total) {
@@ -5382,6 +5415,7 @@ int pwg_cnet_set_option(PwgCnet* n, int option, long long value) {
               : option == PWG_CNET_OPT_XCD_ORDER  ? &n->xcd_order
               : option == PWG_CNET_OPT_NARROW_DMA ? &n->narrow_dma
               : option == PWG_CNET_OPT_PRESPLIT   ? &n->presplit
+              : option == PWG_CNET_OPT_RSTACK     ? &n->rstack
                                                   : nullptr;
   if (option == PWG_CNET_OPT_MSTACK) {
     if (value < 0 || value > 2) return fail(PWG_ERR_INVALID, "mstack must be 0, 1 or 2");

@@ -337,6 +337,35 @@ int mstack_lds(int cs, int oc, int halo, int ns);
 bool mstack_supported(int cs, int tpw);
 hipError_t launch_mstack(const MstackArgs& a, int cs, int tpw, int n_blocks, hipStream_t s);
 
+// Batched ResidualStack (pwg_rstack.hip, the conv-network executor's launch for large plans): one
+// stack -- h = W_A * lrelu(x) + b_A (k = 3, dilation dil), y = W_1 lrelu(h) + W_s x + b -- for
+// 256-column tiles, persistent workgroups streaming every step's weights and input rows through an
+// LDS ring, h in registers. C = 16 cs channels (cs = 2, 3, 4, 6), y rows of exactly C floats.
+constexpr int RS_MAX_REACH = 64;  // (k - 1) dil = 2 dil at most
+constexpr int RS_MAX_TILES = 64;  // 256-column tiles per workgroup at most
+struct RstackArgs {
+  const float* x;                 // stack input [rows][ld_x]
+  const int* seg_x;               // [n_utts][2] (first row, rows)
+  int ld_x, mode_x;               // row stride (floats, multiple of 4); conv A's edge mode
+  int dil, off;                   // conv A: dilation, first tap offset (-pad)
+  float slope1;                   // conv A's input LeakyReLU slope
+  int mode_2;                     // the 1x1's x source: edge mode and LeakyReLU slope
+  float slope2;
+  float slope_h;                  // the 1x1's LeakyReLU slope of h
+  const float* wA;                // conv A split-f16 fragments [tap * cs + cb][MT][hi/lo][lane][4]
+  const float* bA;                // conv A bias (C)
+  const float* wB;                // 1x1 fragments [chunk][MT][hi/lo][lane][4], chunks [h cb][x cb]
+  const float* bB;                // 1x1 bias (both biases summed, C)
+  float* y;                       // [rows][C] (no residual, accumulate, division or activation)
+  const int* seg_y;
+  const int2* blocks;             // (utterance, q0) of each 256-column tile
+  const int* ncols;               // output columns per utterance
+  int n_blocks;
+};
+bool rstack_supported(int cs);
+int rstack_lds(int cs);
+hipError_t launch_rstack(const RstackArgs& a, int cs, int n_wg, hipStream_t s);
+
 // Run status bits (the per-run word pwg_run_status reads, and the handle's sticky copy).
 constexpr int PWG_STATUS_RANGE = 1;         // a value left the fp16 pair range: rerun in exact fp32
 constexpr int PWG_STATUS_PIPE_TIMEOUT = 2;  // layer pipeline: a dependency wait gave up

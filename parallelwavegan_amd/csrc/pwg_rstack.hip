@@ -1,0 +1,592 @@
+// Batched ResidualStack (split-f16 MFMA, gfx950): the conv-network executor's launch for MelGAN /
+// multi-band MelGAN ResidualStacks over large plans (layers/residual_stack.py:75-85,
+// models/melgan.py:117-130). One stack is
+//   h = W_A * lrelu(x) + b_A            (k = 3, dilation d, ReflectionPad1d(d) or zero padding)
+//   y = W_1 lrelu(h) + W_s x + b        (the stack's 1x1 and skip_layer as ONE two-source op)
+// and this kernel computes both for 256-column tiles (8 waves x 32 columns), C <= 96 channels.
+//
+// Why a second kernel beside pwg_cnet_xstack_kernel (which computes the same thing): that kernel
+// stages each 16-channel block's weights and input rows global -> registers -> LDS one block ahead,
+// converts them between two barriers and parks h in a 100 KB LDS tile, so it runs one workgroup per
+// CU whose waves wait on every block's HBM rows (matrix pipe 25 % busy at ~2 GHz, not power-bound;
+// VERDICT round 5). Here:
+//   * a workgroup is persistent over a contiguous range of tiles, and every step's bytes (conv A:
+//     one channel block's fragments of all 3 taps + its raw fp32 input rows; the 1x1: a group of
+//     chunk fragments) stream through a 4-slot LDS ring by global_load_lds, two steps ahead of the
+//     step that computes, ACROSS tile boundaries (the next tile's rows load under this tile's 1x1);
+//   * a block's raw rows are converted in place (LeakyReLU, zero padding, fp16 hi/lo split) once per
+//     workgroup, one step before the MFMAs read them, by the lanes whose MFMA layout they match:
+//     the lane converting column q's row also keeps that row's raw channels, split, as the 1x1's x
+//     operand (registers, no second read);
+//   * h never leaves registers: conv A's accumulators (+ b_A, LeakyReLU, split) become the 1x1's B
+//     operands by one cross-half exchange per 16 channels (pwg_mstack.hip's form);
+//   * the only memory operations inside the loop are the ring's copies and the epilogue's buffer
+//     stores (out-of-range columns dropped by the descriptor's range check, so every wave issues the
+//     same count): the counted vmcnt waits stay exact, no hidden drains.
+// Every column sums the same products in the same order, with the same pre-activations, pair splits
+// and epilogue, as the x-tile conv + the tap-major 1x1 (and pwg_cnet_xstack_kernel): bit-identical.
+#include <hip/hip_runtime.h>
+
+#include <type_traits>
+
+#include "../../include/pwg_cnet.h"
+#include "pwg_internal.h"
+
+namespace pwg {
+namespace {
+
+typedef float rs_f32x16 __attribute__((ext_vector_type(16)));
+typedef float rs_f32x4 __attribute__((ext_vector_type(4)));
+typedef float rs_f32x8 __attribute__((ext_vector_type(8)));
+typedef unsigned rs_u32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 rs_f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 rs_f16x2 __attribute__((ext_vector_type(2)));
+
+constexpr int RS_NWV = 8, RS_NTH = 64 * RS_NWV;  // waves / threads per workgroup
+constexpr int RS_COLS = 32 * RS_NWV;             // output columns per tile
+constexpr int RS_P = 4;                          // ring slots: a step waits for the step after it,
+                                                 // issued two steps earlier
+constexpr int RS_ROWS = RS_COLS + RS_MAX_REACH;  // staged input rows per conv-A step at most
+constexpr int RS_TD = 8;                         // ints per tile descriptor in LDS
+
+// Diagnostic timeline (tools/diag/rstack_probe.py): when g_rs_probe_on is set, wave 0 of workgroup
+// g_rs_probe_wg stamps the shader clock at each phase of every step into g_rs_probe (off by default;
+// one scalar test per stamp)
+constexpr int RS_PROBE_N = 4096;
+__device__ unsigned long long g_rs_probe[RS_PROBE_N];
+__device__ int g_rs_probe_on;
+__device__ int g_rs_probe_wg;
+
+template <int CS>
+struct RsShape {
+  static constexpr int MT = (CS + 1) / 2;            // 32-row m-tiles
+  static constexpr int C = 16 * CS;
+  static constexpr int A1 = 3 * MT * 2;              // 1-KB fragment copies of a conv-A step (3 taps)
+  static constexpr int NR = RS_ROWS / 16;            // 1-KB row copies of a conv-A step (64-B rows)
+  static constexpr int N1 = A1 + NR;
+  static constexpr int SLOT = N1 * 1024;
+  // the 1x1's 2 CS chunk fragments (MT x 2 KB each) in S2 steps of G2 chunks
+  static constexpr int S2_MIN = (2 * CS * MT * 2 + N1 - 1) / N1;
+  static constexpr int S2 = (2 * CS) % S2_MIN == 0 ? S2_MIN : (2 * CS) % (S2_MIN + 1) == 0 ? S2_MIN + 1 : 2 * CS;
+  static constexpr int G2 = 2 * CS / S2;
+  static constexpr int N2 = G2 * MT * 2;
+  static constexpr int D = ((N1 > N2 ? N1 : N2) + RS_NWV - 1) / RS_NWV;  // copies per wave per step
+  static constexpr int SPT = CS + S2;                // steps per tile
+  static constexpr int E = CS;                       // in-tile step after whose copies the stores issue
+  static constexpr int MP = MT < 3 ? MT : 2;         // 1x1 m-tiles per pass (accumulators live at once)
+  static_assert(S2 <= RS_P - 2, "the 1x1's slots are all landed in its first step");
+  // epilogue stores per wave: (m, j4) groups of 4 rows below C (C is a multiple of 16)
+  static constexpr int NST = (C / 32) * 4 + (C % 32 ? 2 : 0);
+  static_assert(N2 * 1024 <= SLOT, "1x1 step fits a slot");
+};
+
+__device__ __forceinline__ bool rs_edge(int& p, int T, int mode) {  // the executor's edge_row
+  if (mode == PWG_PAD_REFLECT) {
+    p = p < 0 ? -p : p;
+    p = p >= T ? 2 * (T - 1) - p : p;
+    p = p < 0 ? 0 : (p >= T ? T - 1 : p);
+    return true;
+  }
+  const bool inside = p >= 0 && p < T;
+  p = p < 0 ? 0 : (p >= T ? T - 1 : p);
+  return inside || mode == PWG_PAD_REPLICATE;
+}
+
+// 8 fp32 -> fp16 pairs hi = rne16(v), lo = rne16(v - hi): the executor's cn_split8 in 12 instructions
+// (v_cvt_pk_f16_f32 for hi; v_fma_mix computes v - hi exactly in fp32 and rounds it to fp16 once,
+// as the C++ form's exact subtraction then conversion does). Trailing s_nop 1: the results may feed
+// MFMAs (pwg_split16.hip's split8x)
+__device__ __forceinline__ void rs_split8(const rs_f32x8& v, rs_u32x4& hi, rs_u32x4& lo) {
+  unsigned h0, h1, h2, h3, l0, l1, l2, l3;
+  asm volatile(
+      "v_cvt_pk_f16_f32 %0, %8, %9\n\t"
+      "v_cvt_pk_f16_f32 %1, %10, %11\n\t"
+      "v_cvt_pk_f16_f32 %2, %12, %13\n\t"
+      "v_cvt_pk_f16_f32 %3, %14, %15\n\t"
+      "v_fma_mixlo_f16 %4, %0, -1.0, %8 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixlo_f16 %5, %1, -1.0, %10 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixlo_f16 %6, %2, -1.0, %12 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixlo_f16 %7, %3, -1.0, %14 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %4, %0, -1.0, %9 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %5, %1, -1.0, %11 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %6, %2, -1.0, %13 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %7, %3, -1.0, %15 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "s_nop 1"
+      : "=&v"(h0), "=&v"(h1), "=&v"(h2), "=&v"(h3), "=&v"(l0), "=&v"(l1), "=&v"(l2), "=&v"(l3)
+      : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]));
+  hi = rs_u32x4{h0, h1, h2, h3};
+  lo = rs_u32x4{l0, l1, l2, l3};
+}
+
+__device__ __forceinline__ rs_f32x16 rs_mma3(const rs_u32x4& ah, const rs_u32x4& al, const rs_u32x4& bh,
+                                              const rs_u32x4& bl, rs_f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(rs_f16x8, ah), __builtin_bit_cast(rs_f16x8, bh), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(rs_f16x8, ah), __builtin_bit_cast(rs_f16x8, bl), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(rs_f16x8, al), __builtin_bit_cast(rs_f16x8, bh), acc, 0, 0, 0);
+  return acc;
+}
+
+// LeakyReLU with a slope in [0, 1] (host-checked) as max(x, slope x): the executor's select form
+// x > 0 ? x : slope x, value for value (signed zeros and NaN included), in two instructions
+__device__ __forceinline__ float rs_lrelu(float x, float slope) { return __builtin_fmaxf(x, x * slope); }
+
+template <int N>
+__device__ __forceinline__ void rs_vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// s_waitcnt vmcnt(n) for a wave-uniform n in [LO, HI] (binary dispatch on scalar compares)
+template <int LO, int HI>
+__device__ __forceinline__ void rs_vm_wait_rt(int n) {
+  if constexpr (LO == HI) {
+    rs_vm_wait<LO>();
+  } else {
+    constexpr int MID = (LO + HI) / 2;
+    if (n <= MID) rs_vm_wait_rt<LO, MID>(n);
+    else rs_vm_wait_rt<MID + 1, HI>(n);
+  }
+}
+
+template <int B, int E, typename F>
+__device__ __forceinline__ void rs_static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    rs_static_for<B + 1, E>(f);
+  }
+}
+
+template <int CS>
+__global__ void __launch_bounds__(RS_NTH) pwg_rstack_kernel(const RstackArgs a) {
+  using S = RsShape<CS>;
+  constexpr int MT = S::MT, C = S::C, P = RS_P, D = S::D, SPT = S::SPT, CS2 = 2 * CS;
+  typedef __attribute__((address_space(1))) void* gptr_t;
+  typedef __attribute__((address_space(3))) void* lptr_t;
+  extern __shared__ __attribute__((aligned(16))) unsigned char rs_smem[];
+  unsigned char* const ring = rs_smem;
+  float* const sbias = reinterpret_cast<float*>(rs_smem + P * S::SLOT);  // [b_A C][b C]
+  int* const stile = reinterpret_cast<int*>(sbias + 2 * C);             // [tile][RS_TD]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int hh = lane >> 5, cl = lane & 31;
+  // slot of step s. Opaque per use: the in-tile steps are unrolled and s % P is then known, and the
+  // compiler would keep one precomputed LDS address per (slot, offset) for offsets past the 64 KB
+  // an instruction's immediate reaches (spilled at 96 channels)
+  auto slot_of = [&](int s) {
+    unsigned o = (unsigned)(s % RS_P) * (unsigned)RsShape<CS>::SLOT;
+    asm volatile("" : "+s"(o));
+    return ring + o;
+  };
+  // this workgroup's tiles: a contiguous range of the block list
+  const int g = blockIdx.x, ng = gridDim.x;
+  const int t_begin = (int)(((long long)a.n_blocks * g) / ng);
+  const int nt = (int)(((long long)a.n_blocks * (g + 1)) / ng) - t_begin;
+  if (nt <= 0) return;
+  const bool probe = g_rs_probe_on == CS && (int)blockIdx.x == g_rs_probe_wg && threadIdx.x == 0;
+  int np = 1;
+  auto stamp = [&](int tag) {
+    if (probe && np + 1 < RS_PROBE_N) {
+      g_rs_probe[np++] = ((unsigned long long)tag << 56) | (__builtin_readcyclecounter() & 0xFFFFFFFFFFFFFFull);
+    }
+  };
+  // plain loads, all landed before the first copy: biases and the tiles' descriptors
+  for (int i = threadIdx.x; i < 2 * C; i += RS_NTH) sbias[i] = i < C ? a.bA[i] : a.bB[i - C];
+  for (int k = threadIdx.x; k < nt; k += RS_NTH) {
+    const int2 b = a.blocks[t_begin + k];
+    const int2 sx = *reinterpret_cast<const int2*>(a.seg_x + 2 * b.x);
+    const int2 sy = *reinterpret_cast<const int2*>(a.seg_y + 2 * b.x);
+    int* const td = stile + RS_TD * k;
+    td[0] = b.y;          // q0
+    td[1] = sx.x;         // first row of the utterance in x
+    td[2] = sx.y;         // its rows (T)
+    td[3] = sy.x;         // first row in y
+    td[4] = a.ncols[b.x]; // its output columns
+  }
+  __syncthreads();
+
+  const int n_steps = nt * SPT;
+  const int pad = -a.off;                       // tile row of column q0: pad (rows hold q0 + off + r)
+  const int nhalo = 2 * a.dil;                  // rows outside the tile's own 256 (k = 3)
+  const float* const wA0 = a.wA;
+  const float* const wB0 = a.wB;
+  const float* const xg0 = a.x;
+  const int ld = a.ld_x, mode = a.mode_x;
+  const int nr = (RS_COLS + nhalo + 15) / 16;   // row copies a conv-A step needs (the rest repeat one)
+  // Per-lane element offsets (x row * ld + 4 q) of this wave's row copies for the tile whose conv-A
+  // blocks are being issued: computed with its block 0's copies, reused for blocks 1 .. CS - 1 (only
+  // the channel block moves). Copies of the next tile's blocks start after the last of this one's.
+  int roff[D];
+  // step s (in-tile index R, tile k)'s copies into slot s % P: conv-A block R < CS (3 taps'
+  // fragments, then the block's raw rows, piece q of row r at position q ^ (r >> 2 & 3)), else the
+  // 1x1's chunk group R - CS
+  auto issue = [&](int s, int k, auto rc) {
+    constexpr int R = decltype(rc)::value;
+    // (opaque per call: the fragment addresses are the same in every tile, and hoisting them out of
+    // the tile loop would hold (CS + S2) x D 64-bit addresses in registers)
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int lane4 = ln * 4;
+    const float* wA = wA0;
+    const float* wB = wB0;
+    const float* xg = xg0;
+    asm volatile("" : "+s"(wA), "+s"(wB), "+s"(xg));
+    unsigned char* const slot = slot_of(s);
+    if constexpr (R < CS) {
+      if constexpr (R == 0) {
+        const int* const td = stile + RS_TD * k;
+        const int q0 = td[0], rx = td[1], T = td[2];
+#pragma unroll
+        for (int kk = 0; kk < D; ++kk) {
+          const int i = wave + RS_NWV * kk < S::N1 ? wave + RS_NWV * kk : S::N1 - 1;
+          const int j = min(max(i - S::A1, 0), nr - 1);
+          const int row = 16 * j + (ln >> 2);
+          const int q = (ln & 3) ^ ((row >> 2) & 3);
+          int p = q0 + a.off + row;
+          (void)rs_edge(p, T, mode);
+          roff[kk] = (rx + p) * ld + 4 * q;
+        }
+      }
+#pragma unroll
+      for (int kk = 0; kk < D; ++kk) {
+        const int i = wave + RS_NWV * kk < S::N1 ? wave + RS_NWV * kk : S::N1 - 1;
+        const float* src;
+        int dst = i;
+        if (i < S::A1) {
+          const int tap = i / (2 * MT), rem = i - tap * 2 * MT;
+          src = wA + ((tap * CS + R) * MT) * 512 + rem * 256 + lane4;
+        } else {
+          dst = S::A1 + min(i - S::A1, nr - 1);
+          src = xg + roff[kk] + 16 * R;
+        }
+        __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(slot + dst * 1024), 16, 0, 0);
+      }
+    } else {
+      constexpr int c0 = (R - CS) * S::G2;
+#pragma unroll
+      for (int kk = 0; kk < D; ++kk) {
+        const int i = wave + RS_NWV * kk < S::N2 ? wave + RS_NWV * kk : S::N2 - 1;
+        const int c = c0 + i / (2 * MT), rem = i - (i / (2 * MT)) * 2 * MT;
+        const float* src = wB + (c * MT) * 512 + rem * 256 + lane4;
+        __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(slot + i * 1024), 16, 0, 0);
+      }
+    }
+  };
+  // issue step s + P - 1 from in-tile step IS of tile k (its in-tile index and tile are compile-time
+  // offsets of the current ones)
+  auto issue_ahead = [&](int s, int k, auto isc) {
+    constexpr int IS = decltype(isc)::value;
+    constexpr int R = (IS + P - 1) % SPT, DK = (IS + P - 1) / SPT;
+    if (s + P - 1 < n_steps) issue(s + P - 1, k + DK, std::integral_constant<int, R>{});
+  };
+  // s_waitcnt before the copies of step t = w + DT are used, placed at the start of step w (in-tile
+  // index IW, before w's own issue). Younger than them in the wave's issue order: the copies of the
+  // later steps issued so far (up to w + P - 2; fewer at the end of the range) and the epilogue
+  // stores of a tile j (issued right after step j SPT + E's copies) when t was issued at or before
+  // that step and the stores came before w
+  auto wait_at = [&](auto iwc, auto dtc, int k) {
+    constexpr int IW = decltype(iwc)::value, DT = decltype(dtc)::value, E = S::E;
+    const int w = k * SPT + IW, t = w + DT;
+    const int nd = min(w + P - 2, n_steps - 1) - t;
+    constexpr bool prev = IW + DT - P + 1 <= E - SPT;  // tile k - 1's stores (k >= 1)
+    constexpr bool own = E < IW && IW + DT - P + 1 <= E;  // this tile's stores
+    const int nst = ((prev && k > 0) ? 1 : 0) + (own ? 1 : 0);
+    auto w2 = [&](auto nsc) {
+      constexpr int NS = decltype(nsc)::value * S::NST;
+      if (nd >= 2) rs_vm_wait<2 * D + NS>();
+      else if (nd == 1) rs_vm_wait<D + NS>();
+      else rs_vm_wait<NS>();
+    };
+    if (nst == 0) w2(std::integral_constant<int, 0>{});
+    else if (nst == 1) w2(std::integral_constant<int, 1>{});
+    else w2(std::integral_constant<int, 2>{});
+  };
+  auto barrier = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+
+  rs_f32x16 accA[MT], accB[S::MP];
+  rs_u32x4 xbh[CS], xbl[CS];  // the 1x1's x operands (this lane's column, channels 16 cb + 8 hh ..)
+  const float slope1 = a.slope1, slope2 = a.slope2, slopeH = a.slope_h;
+  const int mode2 = a.mode_2;
+  const bool id2 = slope2 == 1.f;  // the skip path's usual pre-activation: none
+  // convert the rows of conv-A block cb in slot s (tile k) in place: LeakyReLU (zero outside the
+  // utterance under zero padding), fp16 hi/lo split; the lane of column q0 + 32 wave + cl also keeps
+  // its raw channels 8 hh .. + 7, pre-activated for the 1x1 and split, as x operand cb
+  auto convert = [&](int s, int k, auto cbc) {
+    constexpr int cb = decltype(cbc)::value;
+    unsigned char* const rows = slot_of(s) + S::A1 * 1024;
+    const int* const td = stile + RS_TD * k;
+    const int q0 = td[0], T = td[2];
+    auto one = [&](int row, bool keep) {
+      const int sw = (row >> 2) & 3;
+      unsigned char* const rb = rows + (size_t)row * 64;
+      const rs_f32x4 v0 = *reinterpret_cast<const rs_f32x4*>(rb + 16 * ((2 * hh) ^ sw));
+      const rs_f32x4 v1 = *reinterpret_cast<const rs_f32x4*>(rb + 16 * ((2 * hh + 1) ^ sw));
+      const rs_f32x8 x = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      int p = q0 + a.off + row;
+      const bool ok = rs_edge(p, T, mode);
+      rs_f32x8 c;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) c[e] = ok ? rs_lrelu(x[e], slope1) : 0.f;
+      rs_u32x4 h, l;
+      rs_split8(c, h, l);
+      *reinterpret_cast<rs_u32x4*>(rb + 16 * (hh ^ sw)) = h;
+      *reinterpret_cast<rs_u32x4*>(rb + 16 * ((2 + hh) ^ sw)) = l;
+      if (keep) {
+        int p2 = q0 + 32 * wave + cl;
+        const bool ok2 = rs_edge(p2, T, mode2);
+        rs_f32x8 c2;
+        if (id2) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) c2[e] = ok2 ? x[e] : 0.f;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) c2[e] = ok2 ? rs_lrelu(x[e], slope2) : 0.f;
+        }
+        rs_split8(c2, xbh[cb], xbl[cb]);
+      }
+    };
+    one(pad + 32 * wave + cl, true);
+    const int j = 32 * wave + cl;
+    if (32 * wave < nhalo && j < nhalo) one(j < pad ? j : j + RS_COLS, false);
+  };
+  // conv A, block cb of slot s: 3 taps x MT m-tiles (the x-tile kernel's order)
+  // one unit's operands: A fragments (hi, lo) of every m-tile + the B pair. Units run as a 2-deep
+  // software pipeline (unit u + 1's LDS reads issued before unit u's MFMAs, fenced so the compiler
+  // does not hoist every unit's reads: 24-48 VGPRs of operands instead of all of a step's)
+  struct Ops {
+    rs_u32x4 ah[MT], al[MT], bh, bl;
+  };
+  // 96 channels: operands of one unit at a time (h, x and both accumulators take 192 VGPRs)
+  constexpr bool PF = true;
+  auto load_a = [&](Ops& o, const rs_u32x4* sa) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      o.ah[m] = sa[(m * 2) * 64];
+      o.al[m] = sa[(m * 2 + 1) * 64];
+    }
+  };
+  auto mma_ops = [&](rs_f32x16 (&acc)[MT], const Ops& o) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = rs_mma3(o.ah[m], o.al[m], o.bh, o.bl, acc[m]);
+  };
+  // conv A, block cb of slot s: 3 taps x MT m-tiles (the x-tile kernel's order)
+  auto mma_conv = [&](int s) {
+    const unsigned char* const slot = slot_of(s);
+    const unsigned char* const rows = slot + S::A1 * 1024;
+    auto load_tap = [&](Ops& o, int t) {
+      const int tr = 32 * wave + cl + t * a.dil;
+      const int sw = (tr >> 2) & 3;
+      o.bh = *reinterpret_cast<const rs_u32x4*>(rows + (size_t)tr * 64 + 16 * (hh ^ sw));
+      o.bl = *reinterpret_cast<const rs_u32x4*>(rows + (size_t)tr * 64 + 16 * ((2 + hh) ^ sw));
+      load_a(o, reinterpret_cast<const rs_u32x4*>(slot) + (size_t)t * MT * 128 + lane);
+    };
+    Ops o[2];
+    if constexpr (PF) load_tap(o[0], 0);
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      if constexpr (PF) {
+        if (t + 1 < 3) load_tap(o[(t + 1) & 1], t + 1);
+      } else {
+        load_tap(o[t & 1], t);
+      }
+      asm volatile("" ::: "memory");
+      mma_ops(accA, o[t & 1]);
+      asm volatile("" ::: "memory");
+    }
+  };
+
+  // epilogue of the m-tiles [M0, M1): y = acc + b, buffer stores
+  // whose range ends at the utterance's last column (dead columns dropped by the range check)
+  auto epilogue = [&](int k, auto m0c, auto m1c) {
+    constexpr int M0 = decltype(m0c)::value, M1 = decltype(m1c)::value;
+    const int* const td = stile + RS_TD * k;
+    const int q0 = td[0], ry = td[3], nq = td[4];
+    const int live = min(max(nq - q0, 0), RS_COLS);
+    const unsigned long long base = reinterpret_cast<unsigned long long>(a.y + ((size_t)ry + q0) * C);
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)base);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(base >> 32));
+    const int nbytes = __builtin_amdgcn_readfirstlane(live * C * 4);
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(((unsigned long long)hi << 32) | lo), (short)0, nbytes, 0x00020000);
+    const int voff = (32 * wave + cl) * C * 4;
+    const float* const bB = sbias + C;
+#pragma unroll
+    for (int m = M0; m < M1; ++m)
+#pragma unroll
+      for (int j4 = 0; j4 < 4; ++j4) {
+        const int row = 32 * m + 8 * j4 + 4 * hh;
+        if (32 * m + 8 * j4 >= C) continue;  // compile-time: C is a multiple of 16
+        rs_f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = accB[m - M0][4 * j4 + e] + bB[row + e];
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(rs_u32x4, v), rsrc, voff + row * 4, 0, 0);
+      }
+  };
+
+  rs_static_for<0, P - 1>([&](auto ic) {
+    constexpr int I = decltype(ic)::value;
+    if (I < n_steps) issue(I, I / SPT, std::integral_constant<int, I % SPT>{});
+  });
+  int s = 0;
+  for (int k = 0; k < nt; ++k) {
+    // tile start: block 0's rows landed -> convert them (slot s)
+    wait_at(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, k);
+    barrier();
+    convert(s, k, std::integral_constant<int, 0>{});
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) accA[m][e] = 0.f;
+    // conv A: step s = block cb; step s + 1 landed (its rows are converted during this step), every
+    // wave done with step s - 1 (its slot takes step s + P - 1)
+    rs_static_for<0, CS>([&](auto cbc) {
+      constexpr int cb = decltype(cbc)::value;
+      stamp(4);
+      if (s + 1 < n_steps) wait_at(cbc, std::integral_constant<int, 1>{}, k);
+      stamp(5);
+      barrier();
+      stamp(6);
+      issue_ahead(s, k, cbc);
+      stamp(7);
+      // the two waves of a SIMD (w, w + 4) in opposite order: one converts the next block while the
+      // other's MFMAs run, then the other way round
+      if (wave < RS_NWV / 2) {
+        mma_conv(s);
+        stamp(8);
+        if constexpr (cb + 1 < CS) convert(s + 1, k, std::integral_constant<int, cb + 1>{});
+      } else {
+        if constexpr (cb + 1 < CS) convert(s + 1, k, std::integral_constant<int, cb + 1>{});
+        mma_conv(s);
+      }
+      ++s;
+    });
+    // h = acc + b_A, LeakyReLU, split: the 1x1's h operands, by one cross-half exchange per chunk
+    rs_u32x4 hbh[CS], hbl[CS];
+    rs_static_for<0, CS>([&](auto chc) {
+      constexpr int ch = decltype(chc)::value;
+      constexpr int mh = ch >> 1, J0 = (ch & 1) * 2;
+      const float* const bb = sbias + 16 * ch + 8 * hh;
+      rs_f32x8 x;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float va = accA[mh][4 * J0 + e], vb = accA[mh][4 * (J0 + 1) + e];
+        const float xa = __shfl_xor(va, 32), xb = __shfl_xor(vb, 32);
+        x[e] = (hh ? xb : va) + bb[e];
+        x[4 + e] = (hh ? vb : xa) + bb[4 + e];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = rs_lrelu(x[e], slopeH);
+      rs_split8(x, hbh[ch], hbl[ch]);
+    });
+    // the 1x1 over [h; x] in chunk order, all in step s = the tile's step CS: its S2 (<= 2) slots
+    // have landed once step s + 1 has; m-tiles in passes of MP (accumulators of one pass live), each
+    // pass's epilogue right after it. Steps s + 1 .. (S2 = 2) only move the ring
+    rs_static_for<0, S::S2>([&](auto gc) {
+      constexpr int g2 = decltype(gc)::value;
+      stamp(9);
+      if (s + 1 < n_steps) wait_at(std::integral_constant<int, CS + g2>{}, std::integral_constant<int, 1>{}, k);
+      stamp(10);
+      barrier();
+      stamp(11);
+      issue_ahead(s, k, std::integral_constant<int, CS + g2>{});
+      stamp(12);
+      if constexpr (g2 == 0) {
+        rs_static_for<0, (MT + S::MP - 1) / S::MP>([&](auto pc) {
+          constexpr int M0 = decltype(pc)::value * S::MP;
+          constexpr int M1 = M0 + S::MP < MT ? M0 + S::MP : MT;
+#pragma unroll
+          for (int m = 0; m < M1 - M0; ++m)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) accB[m][e] = 0.f;
+          // A operands one chunk ahead (the chunk's MFMAs wait on nothing but the previous chunk's)
+          constexpr int NM = M1 - M0;
+          rs_u32x4 ah[2][NM], al[2][NM];
+          auto load_c = [&](auto cc, int buf) {
+            constexpr int c = decltype(cc)::value;
+            const rs_u32x4* const sa = reinterpret_cast<const rs_u32x4*>(slot_of(s + c / S::G2)) +
+                                       (size_t)(c % S::G2) * MT * 128 + lane;
+#pragma unroll
+            for (int m = M0; m < M1; ++m) {
+              ah[buf][m - M0] = sa[(m * 2) * 64];
+              al[buf][m - M0] = sa[(m * 2 + 1) * 64];
+            }
+          };
+          load_c(std::integral_constant<int, 0>{}, 0);
+          rs_static_for<0, CS2>([&](auto cc) {
+            constexpr int c = decltype(cc)::value;
+            if constexpr (c + 1 < CS2) load_c(std::integral_constant<int, c + 1>{}, (c + 1) & 1);
+            const rs_u32x4& bh = c < CS ? hbh[c < CS ? c : 0] : xbh[c < CS ? 0 : c - CS];
+            const rs_u32x4& bl = c < CS ? hbl[c < CS ? c : 0] : xbl[c < CS ? 0 : c - CS];
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int m = 0; m < NM; ++m) accB[m] = rs_mma3(ah[c & 1][m], al[c & 1][m], bh, bl, accB[m]);
+            asm volatile("" ::: "memory");
+          });
+          stamp(13);
+          epilogue(k, std::integral_constant<int, M0>{}, std::integral_constant<int, M1>{});
+        });
+        stamp(14);
+      }
+      ++s;
+    });
+  }
+  rs_vm_wait<0>();
+  if (probe) g_rs_probe[0] = (unsigned long long)np | ((unsigned long long)nt << 16) | ((unsigned long long)CS << 32);
+}
+
+template <int CS>
+hipError_t rs_go(const RstackArgs& a, int n_wg, hipStream_t s) {
+  const int lds = rstack_lds(CS);
+  const hipError_t e = allow_lds(reinterpret_cast<const void*>(pwg_rstack_kernel<CS>), lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((pwg_rstack_kernel<CS>), dim3((unsigned)n_wg), dim3(RS_NTH), (size_t)lds, s, a);
+  return hipGetLastError();
+}
+
+template <int CS>
+constexpr int rs_lds_of() {
+  return RS_P * RsShape<CS>::SLOT + 2 * RsShape<CS>::C * 4 + RS_MAX_TILES * RS_TD * 4;
+}
+
+}  // namespace
+
+bool rstack_supported(int cs) { return cs == 2 || cs == 3 || cs == 4 || cs == 6; }
+
+int rstack_lds(int cs) {
+  switch (cs) {
+    case 2: return rs_lds_of<2>();
+    case 3: return rs_lds_of<3>();
+    case 4: return rs_lds_of<4>();
+    case 6: return rs_lds_of<6>();
+  }
+  return 0;
+}
+
+hipError_t launch_rstack(const RstackArgs& a, int cs, int n_wg, hipStream_t s) {
+  if (!rstack_supported(cs) || a.n_blocks < 1 || n_wg < 1 || a.dil < 1 || 2 * a.dil > RS_MAX_REACH ||
+      (a.n_blocks + n_wg - 1) / n_wg > RS_MAX_TILES)
+    return hipErrorInvalidValue;
+  switch (cs) {
+    case 2: return rs_go<2>(a, n_wg, s);
+    case 3: return rs_go<3>(a, n_wg, s);
+    case 4: return rs_go<4>(a, n_wg, s);
+    case 6: return rs_go<6>(a, n_wg, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace pwg
+
+// Diagnostic (tools/diag/rstack_probe.py): enable = 1 arms the timeline for workgroup wg of the next
+// launches with cs = enable (0 disarms); out != null copies the last timeline (n >= RS_PROBE_N words).
+extern "C" __attribute__((visibility("default"))) int pwg_rstack_debug_probe(int enable, int wg, unsigned long long* out, int n) {
+  if (enable >= 0) {
+    if (hipMemcpyToSymbol(HIP_SYMBOL(pwg::g_rs_probe_on), &enable, sizeof(int)) != hipSuccess) return 3;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(pwg::g_rs_probe_wg), &wg, sizeof(int)) != hipSuccess) return 3;
+  }
+  if (out) {
+    if (n < pwg::RS_PROBE_N) return 1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(pwg::g_rs_probe), sizeof(unsigned long long) * pwg::RS_PROBE_N) == hipSuccess ? 0 : 3;
+  }
+  return 0;
+}

@@ -26,6 +26,9 @@ def main():
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--mstack", type=int, default=None, help="PWG_CNET_OPT_MSTACK (fused stack chains) 0/1/2")
     ap.add_argument("--presplit", type=int, default=None, help="PWG_CNET_OPT_PRESPLIT 0/1")
+    ap.add_argument("--rstack", type=int, default=None, help="PWG_CNET_OPT_RSTACK 0/1")
+    ap.add_argument("--bitwise-rstack", action="store_true",
+                    help="first compare one forward with PWG_CNET_OPT_RSTACK 0 and 1 bit for bit")
     ap.add_argument("--dump", default=None, help="save the first forward's output (.npy) for a bitwise A/B")
     a = ap.parse_args()
     cls, p = configs.vocoder_params(a.config)
@@ -41,6 +44,8 @@ def main():
         eng.set_mstack(a.mstack)
     if a.presplit is not None:
         eng.set_presplit(a.presplit)
+    if a.rstack is not None:
+        eng.set_rstack(a.rstack)
     if a.pair_steps:
         eng.set_pair_steps(a.pair_steps)
     P = eng.program
@@ -50,6 +55,17 @@ def main():
     torch.manual_seed(0)
     mel = torch.randn(frames * 80, device=dev)
     out = torch.empty(plan.out_rows * eng.out_channels, device=dev)
+    if a.bitwise_rstack:
+        eng.set_rstack(False)
+        eng.run(plan, mel, out)
+        ref = out.clone()
+        eng.set_rstack(True)
+        out.fill_(float("nan"))
+        eng.run(plan, mel, out)
+        torch.cuda.synchronize()
+        same = bool(torch.equal(ref, out))
+        print(f"bitwise rstack 0 vs 1: {'equal' if same else 'DIFFER'} max|d| {(ref - out).abs().max().item():.3e}"
+              f" finite {bool(torch.isfinite(out).all())}", flush=True)
     eng.run(plan, mel, out)
     torch.cuda.synchronize()
     if a.dump:
