@@ -459,6 +459,27 @@ def program_bytes_per_frame(P):
     return b
 
 
+# SURVEY sec. 8(d)(5)'s 512-utterance list (RandomState(3), 80-1199 frames): 97 lengths repeat
+REPEAT_LIST = [int(f) for f in synthetic.libritts_lengths(512, seed=3)]
+
+
+def span_and_overhead(eng, call, timed, reps):
+    """Device span and host overhead measured over the SAME calls: timing mode 2 (one event pair
+    around each run), per call its wall time (synchronised) and its device span; returns the median
+    span and the median of wall - span (clipped at 0: the span lies inside the wall clock)."""
+    spans, overs = [], []
+    eng.set_timing(2)
+    eng.collect_timing()
+    for _ in range(max(5, reps // 2)):
+        wall = timed(call)
+        sp = eng.timing_span()
+        eng.collect_timing()
+        spans.append(sp)
+        overs.append(max(wall - sp, 0.0))
+    eng.set_timing(False)
+    return float(np.median(spans)), float(np.median(overs))
+
+
 def decode_loop_row(call, lengths, dev, hop, noise=False):
     """The reference's decode loop (bin/decode.py:236-268): one B = 1 call per utterance, each at its
     own length, every call the first at that length (plan build, workspace growth and graph policy
@@ -477,7 +498,9 @@ def decode_loop_row(call, lengths, dev, hop, noise=False):
     ms = np.array(ms)
     short = ms[np.asarray(lengths) <= 512]
     samples = int(np.sum(lengths)) * hop
-    return {"pattern": "decode loop: B=1, one call per utterance, every length new",
+    return {"pattern": "decode loop: B=1, one call per utterance, in list order" +
+                       (", every length new" if len(set(int(f) for f in lengths)) == len(lengths) else
+                        " (lengths repeat: the reference's own list)"),
             "utterances": len(lengths), "distinct_lengths": len(set(int(f) for f in lengths)),
             "frames": f"RandomState(3) LibriTTS list, {int(np.min(lengths))}-{int(np.max(lengths))}",
             "mean_ms_per_call": round(float(ms.mean()), 3), "median_ms_per_call": round(float(np.median(ms)), 3),
@@ -500,6 +523,9 @@ def vocoder_latency_rows(m, dev, reps=10):
     with torch.no_grad():
         m.inference(torch.from_numpy(synthetic.make_mel(7, 80, seed=1)).to(dev))  # engine built, weights packed
         loop = decode_loop_row(lambda mel: m.inference(mel), lengths, dev, hop)
+        # the reference's own pattern with its repeats: the first 128 utterances of the 512-utterance
+        # RandomState(3) list, in order (10 repeated lengths)
+        loop_rep = decode_loop_row(lambda mel: m.inference(mel), REPEAT_LIST[:128], dev, hop)
 
     def timed(fn):
         torch.cuda.synchronize(dev)
@@ -517,12 +543,7 @@ def vocoder_latency_rows(m, dev, reps=10):
                 for _ in range(2):
                     call()
                 ms = sorted(timed(call) for _ in range(reps))
-                eng.set_timing(2)  # span: one event pair around the run
-                eng.collect_timing()
-                call()
-                torch.cuda.synchronize(dev)
-                span = eng.timing_span()
-                eng.collect_timing()
+                span, over = span_and_overhead(eng, call, timed, reps)
                 eng.set_timing(1)  # per-launch events
                 call()
                 torch.cuda.synchronize(dev)
@@ -531,14 +552,15 @@ def vocoder_latency_rows(m, dev, reps=10):
                 med = ms[len(ms) // 2]
                 rows.append({"frames": F, "batch": B, "samples_per_call": F * hop * B, "first_call_ms": round(first, 3),
                              "median_ms": round(med, 3), "kernel_span_ms": round(span, 3),
-                             "kernel_sum_ms": round(kern, 3), "host_overhead_ms": round(med - span, 3),
+                             "kernel_sum_ms": round(kern, 3), "host_overhead_ms": round(over, 3),
                              "samples_per_s": round(F * hop * B / (med * 1e-3), 1)})
     return {"model": f"{type(m).__name__}.inference / inference_batch (drop-in)", "decode_loop": loop,
-            "rows": rows,
-            "note": "kernel_span_ms: device span of one eager call (HIP events around the whole run only; graph "
-                    "replay is off while timing); median_ms: wall time of the default path (graph replay for "
-                    "repeated small HiFiGAN plans); kernel_sum_ms: per-launch event times summed (concurrent "
-                    "launches each counted)"}
+            "decode_loop_repeats": loop_rep, "rows": rows,
+            "note": "kernel_span_ms: median device span of eager calls (HIP events around the whole run only; "
+                    "graph replay is off while timing); host_overhead_ms: median over those same calls of wall "
+                    "minus span (>= 0 by construction); median_ms: wall time of the default path (graph replay "
+                    "for repeated small HiFiGAN plans); kernel_sum_ms: per-launch event times summed "
+                    "(concurrent launches each counted)"}
 
 
 def vocoder_exact_fp32_leg(eng, plan, out_mel, out, flop_step, samples, steps):
@@ -824,6 +846,7 @@ def latency_rows(dev, reps=20):
         m.inference(torch.from_numpy(synthetic.make_mel(7, 80, seed=1)).to(dev),
                     torch.from_numpy(synthetic.make_noise(7 * H, seed=1)).to(dev))  # engine built, weights packed
         loop = decode_loop_row(lambda mel, x: m.inference(mel, x), lengths, dev, H, noise=True)
+        loop_rep = decode_loop_row(lambda mel, x: m.inference(mel, x), REPEAT_LIST[:128], dev, H, noise=True)
 
     def timed(fn):
         torch.cuda.synchronize(dev)
@@ -860,22 +883,16 @@ def latency_rows(dev, reps=20):
                         g(mels[0], noises[0])
                     graph_ms = sorted(timed(lambda: g(mels[0], noises[0])) for _ in range(reps))
                     del g
-                eng.set_timing(2)  # span: one event pair around the run
-                eng.collect_timing()
-                call()
-                torch.cuda.synchronize(dev)
-                eng.set_timing(False)
-                kern = eng.timing_span()
-                eng.collect_timing()
+                kern, over = span_and_overhead(eng, call, timed, reps)
                 med = dev_ms[len(dev_ms) // 2]
                 rows.append({"frames": F, "batch": B, "samples_per_call": F * H * B,
                              "first_call_ms": round(first, 3), "median_ms": round(med, 3),
                              "min_ms": round(dev_ms[0], 3), "host_to_host_median_ms": round(host_ms[len(host_ms) // 2], 3),
-                             "kernel_span_ms": round(kern, 3), "host_overhead_ms": round(med - kern, 3),
+                             "kernel_span_ms": round(kern, 3), "host_overhead_ms": round(over, 3),
                              "graph_replay_median_ms": graph_ms and round(graph_ms[len(graph_ms) // 2], 3),
                              "samples_per_s": round(F * H * B / (med * 1e-3), 1)})
     return {"model": "ljspeech_v1 ParallelWaveGANGenerator.inference / inference_batch (drop-in)",
-            "decode_loop": loop, "rows": rows}
+            "decode_loop": loop, "decode_loop_repeats": loop_rep, "rows": rows}
 
 
 def main():

@@ -160,9 +160,9 @@ PWG_API int pwg_cnet_plan_schedule(PwgCnetPlan* p, int cap, int* n_launches, int
  * or one chunk of a tap-major op) is staged by global_load_lds a few steps ahead of its MFMAs, the
  * input rows pre-activated LDS -> LDS; also takes the narrow launches of tap-major convs (MelGAN's
  * two-source 1x1s). Bit-identical to 0 (the DMA-staged narrow x-tile kernel and the narrow
- * tap-major kernel, sized as described above), which stays for A/B. 2: also narrow launches whose
- * DMA-ring workgroups would need more than one round over the CUs, with two m-tiles per workgroup
- * where the op has k <= 7 (measured slower; for A/B).
+ * tap-major kernel, sized as described above), which stays for A/B. Launches whose DMA-ring
+ * workgroups would need more than one round over the CUs keep the narrow x-tile kernel (the
+ * DMA-ring forms for them measured slower and were removed in round 6).
  * PWG_CNET_OPT_STREAMS (default 1): launches that do not depend on each other (HiFiGAN's parallel
  * residual blocks, models/hifigan.py:159-168) run concurrently on up to 3 auxiliary streams of the
  * handle, forked from and joined back into the caller's stream with events (graph-capturable):
@@ -173,8 +173,9 @@ PWG_API int pwg_cnet_plan_schedule(PwgCnetPlan* p, int cap, int* n_launches, int
  * two-source 1x1 each, zero or reflect "same" padding, 32-128 channels) runs as ONE launch: each
  * workgroup takes a block of output columns through every stack with the input tile (+- the summed
  * dilations, recomputed by neighbouring blocks) in LDS and h in registers, instead of two launches per
- * stack. 1: when the chain's first conv runs narrow (small plans); 2: every such chain; 0 never.
- * Bit-identical to the unfused launches.
+ * stack. 1: when the chain's first conv runs narrow (small plans, blocks within one round over the
+ * CUs, <= 128 channels); 0 never. Bit-identical to the unfused launches. (Large plans run each
+ * stack on PWG_CNET_OPT_RSTACK's kernel: the halo recompute costs more than it saves there.)
  * PWG_CNET_OPT_PRESPLIT (default 1, plans created afterwards, split-f16 mode with narrow DMA-ring
  * launches): a buffer that DMA-ring launches read with a LeakyReLU slope gets a pre-split image
  * (its rows pre-activated and split into fp16 hi / lo pairs) written by its last writer's epilogue
@@ -183,7 +184,9 @@ PWG_API int pwg_cnet_plan_schedule(PwgCnetPlan* p, int cap, int* n_launches, int
  * PWG_CNET_OPT_RSTACK (default 1, split-f16 x-tile mode with fused ops): the batched launch of a fused
  * ResidualStack with 32-96 channels (16-channel multiples, no epilogue extras) runs the persistent
  * LDS-ring kernel (weights and input rows streamed by global_load_lds two steps ahead across tiles,
- * h in registers) instead of the x-tile stack kernel. Bit-identical; 0 for the x-tile stack (A/B). */
+ * h in registers) instead of the x-tile stack kernel; at <= 64 channels its weights stay resident in
+ * LDS (only input rows stream). Bit-identical; 0 for the x-tile stack, 2 for the streamed-weight form
+ * at every width (A/B). */
 enum { PWG_CNET_OPT_SPLIT_F16 = 0, PWG_CNET_OPT_FUSE_PAIRS = 1, PWG_CNET_OPT_PAIR_STEPS = 2, PWG_CNET_OPT_XTILE = 3,
        PWG_CNET_OPT_XT_DMA = 4, PWG_CNET_OPT_XCD_ORDER = 5, PWG_CNET_OPT_NARROW = 6, PWG_CNET_OPT_NARROW_DMA = 7,
        PWG_CNET_OPT_STREAMS = 8, PWG_CNET_OPT_MSTACK = 9, PWG_CNET_OPT_PRESPLIT = 10,
@@ -200,6 +203,15 @@ PWG_API int pwg_cnet_timing_collect(PwgCnet* n, double* ms, long long* launches)
  * pwg_cnet_timing_collect add up concurrent launches; this is wall time on the device. Call
  * before pwg_cnet_timing_collect. */
 PWG_API int pwg_cnet_timing_span(PwgCnet* n, double* span_ms);
+
+/* Diagnostics of the batched ResidualStack kernel (PWG_CNET_OPT_RSTACK, csrc/pwg_rstack.hip), for
+ * tests and tools/diag/rstack_probe.py; not part of the reference's surface.
+ * pwg_rstack_debug_launches: launches of that kernel enqueued since the library loaded (tests assert
+ * the kernel engaged). pwg_rstack_debug_probe: enable = cs (16-channel blocks) arms a shader-clock
+ * timeline of workgroup wg's wave 0 for the following launches of that width, 0 disarms, < 0 leaves
+ * it; out != NULL (n >= 4096 words) copies the last timeline. 0 on success. */
+PWG_API long long pwg_rstack_debug_launches(void);
+PWG_API int pwg_rstack_debug_probe(int enable, int wg, unsigned long long* out, int n);
 
 #ifdef __cplusplus
 }

@@ -98,6 +98,8 @@ EXPORTED_SYMBOLS = (
     "pwg_cnet_set_timing",
     "pwg_cnet_timing_collect",
     "pwg_cnet_timing_span",
+    "pwg_rstack_debug_launches",
+    "pwg_rstack_debug_probe",
 )
 
 PWG_OPT_LAYER_KERNEL = 0

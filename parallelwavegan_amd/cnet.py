@@ -269,6 +269,7 @@ class CnetEngine:
         # and pays its input / output copies (MB-MelGAN v2 T' = 64: 0.449 -> 0.466 ms)
         self._branchy = any(op["accumulate"] for op in program.ops)
         self._graphs = OrderedDict()
+        self._uses = OrderedDict()  # runs per batch shape (frames tuple), kept across plan evictions
         self._graph_epoch = 0       # bumped by every option change: captured forwards are stale
         self._last_ws = {}          # (plan, stream) -> workspace of its last replayed forward
         self._timing = False
@@ -358,7 +359,12 @@ class CnetEngine:
         ws = None
         key = (id(plan), stream.cuda_stream)
         plan.runs += 1
-        if self._graph_ok(plan, mean, stream):
+        uses = self._uses.get(plan.frames, 0) + 1
+        self._uses[plan.frames] = uses
+        self._uses.move_to_end(plan.frames)
+        while len(self._uses) > self.USES_CACHE:
+            self._uses.popitem(last=False)
+        if self._graph_ok(plan, mean, stream, uses):
             ws = self._replay(plan, mel, out, stream)
             self._last_ws[key] = ws  # run_status reads the captured forward's own workspace
         else:
@@ -387,22 +393,27 @@ class CnetEngine:
     # (profiles/r04_m). Small plans therefore run as a hipGraph captured once per (plan, caller
     # stream, weights, options) and replayed: input copied into the graph's buffer, replay, output
     # copied out. Same kernels, same arguments: bit-identical to the eager forward.
-    # A graph is captured only for a plan that runs again (GRAPH_AFTER-th run): the reference's
-    # decode loop gives nearly every utterance its own length (bin/decode.py:236-268), and a capture
-    # (eager warm-up, capture, instantiation) costs ~10 ms, far more than the eager forward it replaces.
+    # A graph is captured only for a batch shape that has run GRAPH_AFTER times (counted per frames
+    # tuple, surviving plan eviction): a capture (eager warm-up, capture, instantiation) costs 4-26 ms
+    # and a replay saves ~0.09 ms over the eager forward (HiFiGAN v1 B = 1: 1.67 vs 1.58 ms, DESIGN
+    # sec. 11), so it pays back after ~50-300 replays. The reference's decode loop (bin/decode.py:
+    # 236-268) repeats a length only occasionally (the 512-utterance RandomState(3) list: 97 repeated
+    # lengths, none more than a few times), which under the round-5 policy (capture on a plan's second
+    # run) paid captures it never recovered; a serving loop over a fixed shape still gets its graph.
     GRAPH_MAX_FRAMES = 512
-    GRAPH_AFTER = 2
+    GRAPH_AFTER = 64
     GRAPH_CACHE = 8
+    USES_CACHE = 4096
 
     def set_graphs(self, enable):
         """Replay captured forwards of small plans (default on); off: every forward enqueued."""
         self.graphs = bool(enable)
         self._graphs.clear()
 
-    def _graph_ok(self, plan, mean, stream):
+    def _graph_ok(self, plan, mean, stream, uses):
         return (self.graphs and self._branchy and not self._timing and mean is None
                 and sum(plan.frames) <= self.GRAPH_MAX_FRAMES and not torch.cuda.is_current_stream_capturing()
-                and (plan.runs >= self.GRAPH_AFTER or self._graph_key(plan, stream) in self._graphs))
+                and (uses >= self.GRAPH_AFTER or self._graph_key(plan, stream) in self._graphs))
 
     def _graph_key(self, plan, stream):
         return (id(plan), stream.cuda_stream, self.packed.data_ptr(), self.split_f16, self._graph_epoch)
@@ -576,11 +587,12 @@ class CnetEngine:
         self._graph_epoch += 1
         self._plans.clear()
 
-    def set_rstack(self, enable):
+    def set_rstack(self, mode):
         """pwg_cnet_set_option(PWG_CNET_OPT_RSTACK): batched fused ResidualStacks of 32-96 channels
-        on the persistent LDS-ring kernel (pwg_rstack.hip, default) or, 0, on the x-tile stack
-        kernel. Run-time; bit-identical."""
-        _lib.check(self._lib.pwg_cnet_set_option(self._h, 11, 1 if enable else 0))
+        on the persistent LDS-ring kernel (pwg_rstack.hip; 1 = default, weights resident in LDS at
+        <= 64 channels; 2 = weights streamed at every width) or, 0, on the x-tile stack kernel.
+        Run-time; bit-identical."""
+        _lib.check(self._lib.pwg_cnet_set_option(self._h, 11, int(mode)))
         self._graph_epoch += 1
 
     def set_narrow_dma(self, enable):

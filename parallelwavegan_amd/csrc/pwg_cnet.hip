@@ -1640,53 +1640,31 @@ hipError_t xdma_go(dim3 grid, hipStream_t s, const CnConvArgs& a, const CnXdmaAr
   hipLaunchKernelGGL((pwg_cnet_xdma_kernel<K, MT, NWV, PRE>), grid, dim3(64 * NWV), (size_t)lds, s, a, xd);
   return hipGetLastError();
 }
-template <int MT, int NWV, bool PRE>
+template <int NWV, bool PRE>
 hipError_t xdma_launch_k(int k, dim3 grid, hipStream_t s, const CnConvArgs& a, const CnXdmaArgs& xd) {
-  if constexpr (MT == 2) {  // two m-tiles: k > 1 up to 7 taps (a step's operands in registers)
-    switch (k) {
-      case 2: return xdma_go<2, 2, NWV, PRE>(grid, s, a, xd);
-      case 3: return xdma_go<3, 2, NWV, PRE>(grid, s, a, xd);
-      case 5: return xdma_go<5, 2, NWV, PRE>(grid, s, a, xd);
-      case 7: return xdma_go<7, 2, NWV, PRE>(grid, s, a, xd);
-      default: return hipErrorInvalidValue;
-    }
-  } else {
-    switch (k) {
-      case 1: return xdma_go<1, MT, NWV, PRE>(grid, s, a, xd);
-      case 2: return xdma_go<2, MT, NWV, PRE>(grid, s, a, xd);
-      case 3: return xdma_go<3, MT, NWV, PRE>(grid, s, a, xd);
-      case 5: return xdma_go<5, MT, NWV, PRE>(grid, s, a, xd);
-      case 7: return xdma_go<7, MT, NWV, PRE>(grid, s, a, xd);
-      case 11: return xdma_go<11, MT, NWV, PRE>(grid, s, a, xd);
-      default: return hipErrorInvalidValue;
-    }
+  switch (k) {
+    case 1: return xdma_go<1, 1, NWV, PRE>(grid, s, a, xd);
+    case 2: return xdma_go<2, 1, NWV, PRE>(grid, s, a, xd);
+    case 3: return xdma_go<3, 1, NWV, PRE>(grid, s, a, xd);
+    case 5: return xdma_go<5, 1, NWV, PRE>(grid, s, a, xd);
+    case 7: return xdma_go<7, 1, NWV, PRE>(grid, s, a, xd);
+    case 11: return xdma_go<11, 1, NWV, PRE>(grid, s, a, xd);
+    default: return hipErrorInvalidValue;
   }
 }
 // k = 1: K = 1 mode (steps = the tap-major chunk list); pre: B rows from the sources' pre-split
-// images (xd.simg)
+// images (xd.simg). One m-tile per workgroup (the plan's only DMA-ring form)
 hipError_t xdma_launch(int mt, int nwv, int k, bool pre, dim3 grid, hipStream_t s, const CnConvArgs& a,
                        const CnXdmaArgs& xd) {
-  if (mt == 2) {
-    if (pre) {
-      if (nwv == 1) return xdma_launch_k<2, 1, true>(k, grid, s, a, xd);
-      if (nwv == 2) return xdma_launch_k<2, 2, true>(k, grid, s, a, xd);
-      if (nwv == 4) return xdma_launch_k<2, 4, true>(k, grid, s, a, xd);
-    } else {
-      if (nwv == 1) return xdma_launch_k<2, 1, false>(k, grid, s, a, xd);
-      if (nwv == 2) return xdma_launch_k<2, 2, false>(k, grid, s, a, xd);
-      if (nwv == 4) return xdma_launch_k<2, 4, false>(k, grid, s, a, xd);
-    }
-    return hipErrorInvalidValue;
-  }
-  if (mt != 1) return hipErrorInvalidValue;  // (the plan picks one or two m-tiles per workgroup)
+  if (mt != 1) return hipErrorInvalidValue;
   if (pre) {
-    if (nwv == 1) return xdma_launch_k<1, 1, true>(k, grid, s, a, xd);
-    if (nwv == 2) return xdma_launch_k<1, 2, true>(k, grid, s, a, xd);
-    if (nwv == 4) return xdma_launch_k<1, 4, true>(k, grid, s, a, xd);
+    if (nwv == 1) return xdma_launch_k<1, true>(k, grid, s, a, xd);
+    if (nwv == 2) return xdma_launch_k<2, true>(k, grid, s, a, xd);
+    if (nwv == 4) return xdma_launch_k<4, true>(k, grid, s, a, xd);
   } else {
-    if (nwv == 1) return xdma_launch_k<1, 1, false>(k, grid, s, a, xd);
-    if (nwv == 2) return xdma_launch_k<1, 2, false>(k, grid, s, a, xd);
-    if (nwv == 4) return xdma_launch_k<1, 4, false>(k, grid, s, a, xd);
+    if (nwv == 1) return xdma_launch_k<1, false>(k, grid, s, a, xd);
+    if (nwv == 2) return xdma_launch_k<2, false>(k, grid, s, a, xd);
+    if (nwv == 4) return xdma_launch_k<4, false>(k, grid, s, a, xd);
   }
   return hipErrorInvalidValue;
 }
@@ -3495,11 +3473,12 @@ struct PwgCnet {
   int xt_dma = 9;      // PWG_CNET_OPT_XT_DMA flags (CNET_DMA_RULE | CNET_DMA_CONVT)
   int xcd_order = 1;   // PWG_CNET_OPT_XCD_ORDER
   int narrow = 1;      // PWG_CNET_OPT_NARROW (plan time): 0 off, 1 small launches, 2 every x-tile phase
-  int narrow_dma = 1;  // PWG_CNET_OPT_NARROW_DMA: narrow launches on the DMA-ring kernel (0: the narrow
-                       // x-tile / tap-major kernels)
+  int narrow_dma = 1;  // PWG_CNET_OPT_NARROW_DMA: narrow launches on the DMA-ring kernel where its
+                       // one-m-tile workgroups fit one round (0: the narrow x-tile / tap-major kernels)
   int mstack = 1;      // PWG_CNET_OPT_MSTACK (plan time): 0 off, 1 fused stack chains in plans whose first
-                       // conv of the chain runs narrow, 2 every chain
-  int rstack = 1;      // PWG_CNET_OPT_RSTACK: batched ResidualStacks on pwg_rstack.hip (else the x-tile stack)
+                       // conv of the chain runs narrow
+  int rstack = 1;      // PWG_CNET_OPT_RSTACK: batched ResidualStacks on pwg_rstack.hip, 1 weights resident in
+                       // LDS where they fit (<= 64 channels), 2 always streamed (A/B); 0 the x-tile stack
   int presplit = 1;    // PWG_CNET_OPT_PRESPLIT (plan time): DMA-ring launches write / read pre-split images
   int streams = 1;     // PWG_CNET_OPT_STREAMS: 0 one stream, 1 independent launches of plans with narrow
                        // launches run on auxiliary streams, 2 every plan
@@ -4555,15 +4534,14 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
       else base = n_blk * (ph.mt_total / ph.MT) * zn;
       if (n->narrow == 2 || base < p->n_cu) {
         pick_w = 1;
-        // NARROW_DMA 2 (A/B): the DMA-ring kernel for every narrow launch, rounds or not, with two
-        // m-tiles per workgroup (k <= 7: a step's A fragments stay in registers) where one would need
-        // more than a round. Measured slower than the narrow x-tile kernel's 2-m-tile workgroups
-        // there (HiFiGAN v1 T' = 256: 1.33 vs 1.23 ms, profiles/r05_mt2.json), so the default keeps
-        // the DMA-ring kernel to launches whose one-m-tile workgroups fit one round
+        // the DMA-ring kernel while its one-m-tile workgroups fit one round over the CUs; past that
+        // the narrow x-tile kernel's 2-m-tile workgroups were faster than every DMA-ring form tried
+        // (every narrow launch on it: HiFiGAN v1 T' = 512 1.67 -> 1.80 ms; two m-tiles per DMA-ring
+        // workgroup: T' = 256 1.23 -> 1.33 ms; profiles/r05_narrow_dma2.json, r05_mt2.json)
         const bool fit1 = xdma_fits(ncols, xdma_waves(ncols), (long long)ph.mt_total * zn);
-        if (n->narrow_dma && (fit1 || n->narrow_dma == 2)) {
+        if (n->narrow_dma && fit1) {
           pick_w = xdma_waves(ncols);
-          pick_m = !fit1 && xk <= 7 && ph.mt_total % 2 == 0 ? 2 : 1;
+          pick_m = 1;
           p->nar_xdma[pi] = 1;
         } else {
           bool found = false;
@@ -4591,7 +4569,7 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
         // then runs it, 1-2 waves)
         if (n->narrow_dma && !op.src[0].normalize && !(op.src[1].buf >= 0 && op.src[1].normalize) &&
             ph.chunks.size() <= (size_t)XDMA_CHUNKS_MAX &&
-            (n->narrow_dma == 2 || xdma_fits(ncols, std::min(2, xdma_waves(ncols)), (long long)ph.mt_total * zn))) {
+            xdma_fits(ncols, std::min(2, xdma_waves(ncols)), (long long)ph.mt_total * zn)) {
           pick_w = std::min(2, xdma_waves(ncols));  // K = 1 mode: 2 waves keep a 4-chunk step's ring 6 deep
           p->nar_xdma[pi] = 1;
         } else {
@@ -4630,19 +4608,35 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
   p->n_msblocks.assign(nph, 0);
   for (size_t pi = 0; pi < nph; ++pi) {
     const OpPhase& ph = n->phases[pi];
-    if (ph.ms_n == 0 || n->mstack == 0 || (n->mstack == 1 && p->nar_nwv[pi] == 0)) continue;
+    if (ph.ms_n == 0 || n->mstack == 0 || p->nar_nwv[pi] == 0) continue;
     const PwgCnetOp& A = n->ops[ph.op];
     const int cs = A.out_channels / 16, d0 = A.src[0].dilation, rate = n->rate[A.dst];
     int oc = 0;
     for (int o = 32; o <= 128; o += 32)
       if ((o + 2 * (ph.ms_halo - d0) + 31) / 32 <= 4 && mstack_lds(cs, o, ph.ms_halo, ph.ms_n) <= PR_MAX_LDS) oc = o;
-    if (oc == 0 || (n->mstack == 1 && cs > 8)) continue;
+    if (oc == 0 || cs > 8) continue;
     for (int u = 0; u < n_utts; ++u) ncols[u] = (int)(frames[u] * rate);
-    if (n->mstack == 1 && count(oc) > p->n_cu) continue;
+    if (count(oc) > p->n_cu) continue;
     p->ms_oc[pi] = oc;
     p->o_msblocks[pi] = list(CN_L_BLK, rate, 1, 0, oc);
     p->n_msblocks[pi] = (int)count(oc);
   }
+  // A chain's one launch reads its stage input (and, through the halos, neighbouring blocks' columns)
+  // for the whole launch while other workgroups write the chain's output: every buffer the chain's
+  // ops touch stays live until its last op, or slot reuse could place the output on the input's
+  // storage (per-op liveness would free the input after stack 0's 1x1)
+  bool chains = false;
+  for (size_t pi = 0; pi < nph; ++pi) {
+    if (p->ms_oc[pi] == 0) continue;
+    chains = true;
+    const int last_op = n->phases[pi + 2 * n->phases[pi].ms_n - 1].op;
+    for (int k = 0; k < 2 * n->phases[pi].ms_n; ++k) {
+      const PwgCnetOp& o2 = n->ops[n->phases[pi + k].op];
+      for (int b : {o2.dst, o2.src[0].buf, o2.src[1].buf, o2.res})
+        if (b >= 0) last_use[b] = std::max(last_use[b], last_op);
+    }
+  }
+  if (chains) assign_slots(true);
   // Pre-split images: a buffer read by a DMA-ring launch (not inside a fused stack chain) with a
   // LeakyReLU slope gets an image of its rows pre-activated with that slope and pair-split, written
   // by its last writer's epilogue when that writer runs on the DMA-ring kernel too (run time decides:
@@ -5049,7 +5043,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
             r.blocks = a.blocks; r.ncols = a.ncols; r.n_blocks = p->n_xblocks[pi];
             // persistent workgroups, one per CU (the ring fills the LDS), each a contiguous range
             const int n_wg = std::max(std::min(r.n_blocks, std::max(p->n_cu, 1)), (r.n_blocks + RS_MAX_TILES - 1) / RS_MAX_TILES);
-            const hipError_t ea2 = launch_rstack(r, ph.rstack_cs, n_wg, s);
+            const hipError_t ea2 = launch_rstack(r, ph.rstack_cs, n_wg, s, n->rstack == 1);
             if (ea2 != hipSuccess) return hipf(ea2, "rstack kernel launch");
           } else {
             const hipError_t ea2 =
@@ -5415,11 +5409,16 @@ int pwg_cnet_set_option(PwgCnet* n, int option, long long value) {
               : option == PWG_CNET_OPT_XCD_ORDER  ? &n->xcd_order
               : option == PWG_CNET_OPT_NARROW_DMA ? &n->narrow_dma
               : option == PWG_CNET_OPT_PRESPLIT   ? &n->presplit
-              : option == PWG_CNET_OPT_RSTACK     ? &n->rstack
+
                                                   : nullptr;
   if (option == PWG_CNET_OPT_MSTACK) {
-    if (value < 0 || value > 2) return fail(PWG_ERR_INVALID, "mstack must be 0, 1 or 2");
+    if (value < 0 || value > 1) return fail(PWG_ERR_INVALID, "mstack must be 0 or 1");
     n->mstack = (int)value;
+    return PWG_OK;
+  }
+  if (option == PWG_CNET_OPT_RSTACK) {
+    if (value < 0 || value > 2) return fail(PWG_ERR_INVALID, "rstack must be 0, 1 or 2");
+    n->rstack = (int)value;
     return PWG_OK;
   }
   if (option == PWG_CNET_OPT_STREAMS) {
@@ -5428,8 +5427,7 @@ int pwg_cnet_set_option(PwgCnet* n, int option, long long value) {
     return PWG_OK;
   }
   if (!slot) return fail(PWG_ERR_INVALID, "unknown option");
-  if (value != 0 && value != 1 && !(option == PWG_CNET_OPT_XT_DMA && value >= 0 && value <= 15) &&
-      !(option == PWG_CNET_OPT_NARROW_DMA && value == 2))
+  if (value != 0 && value != 1 && !(option == PWG_CNET_OPT_XT_DMA && value >= 0 && value <= 15))
     return fail(PWG_ERR_INVALID, "option value must be 0 or 1 (PWG_CNET_OPT_XT_DMA: flags 0 - 15)");
   *slot = (int)value;
   return PWG_OK;

@@ -364,7 +364,8 @@ struct RstackArgs {
 };
 bool rstack_supported(int cs);
 int rstack_lds(int cs);
-hipError_t launch_rstack(const RstackArgs& a, int cs, int n_wg, hipStream_t s);
+// resident: the weight-resident form where the fragments fit the LDS (<= 64 channels), else streamed
+hipError_t launch_rstack(const RstackArgs& a, int cs, int n_wg, hipStream_t s, bool resident = true);
 
 // Run status bits (the per-run word pwg_run_status reads, and the handle's sticky copy).
 constexpr int PWG_STATUS_RANGE = 1;         // a value left the fp16 pair range: rerun in exact fp32

@@ -27,6 +27,7 @@
 // and epilogue, as the x-tile conv + the tap-major 1x1 (and pwg_cnet_xstack_kernel): bit-identical.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <type_traits>
 
 #include "../../include/pwg_cnet.h"
@@ -44,10 +45,20 @@ typedef _Float16 rs_f16x2 __attribute__((ext_vector_type(2)));
 
 constexpr int RS_NWV = 8, RS_NTH = 64 * RS_NWV;  // waves / threads per workgroup
 constexpr int RS_COLS = 32 * RS_NWV;             // output columns per tile
-constexpr int RS_P = 4;                          // ring slots: a step waits for the step after it,
+#ifndef RS_PSLOTS
+#define RS_PSLOTS 4
+#endif
+constexpr int RS_P = RS_PSLOTS;                          // ring slots: a step waits for the step after it,
                                                  // issued two steps earlier
 constexpr int RS_ROWS = RS_COLS + RS_MAX_REACH;  // staged input rows per conv-A step at most
 constexpr int RS_TD = 8;                         // ints per tile descriptor in LDS
+// A/B and diagnostic builds (tools/rs_variant.sh): RS_ORDER 0 = the partner-phase order below,
+// 1 = every wave issues the copies right after the barrier, 2 = no partner offset (every wave: issue,
+// MFMAs, convert); RS_DIAG_NOCONV / RS_DIAG_NOROWS (wrong results, timing only): skip the row
+// conversion / the row copies (their copy slots repeat a fragment copy, so the waits stay exact)
+#ifndef RS_ORDER
+#define RS_ORDER 0
+#endif
 
 // Diagnostic timeline (tools/diag/rstack_probe.py): when g_rs_probe_on is set, wave 0 of workgroup
 // g_rs_probe_wg stamps the shader clock at each phase of every step into g_rs_probe (off by default;
@@ -181,10 +192,13 @@ __global__ void __launch_bounds__(RS_NTH) pwg_rstack_kernel(const RstackArgs a) 
   const int nt = (int)(((long long)a.n_blocks * (g + 1)) / ng) - t_begin;
   if (nt <= 0) return;
   const bool probe = g_rs_probe_on == CS && (int)blockIdx.x == g_rs_probe_wg && threadIdx.x == 0;
+  typedef __attribute__((address_space(1))) unsigned long long gu64;
+  gu64* probe_buf = (gu64*)g_rs_probe;
+  asm volatile("" : "+s"(probe_buf));  // (its address once, not a GOT load per stamp; global stores)
   int np = 1;
   auto stamp = [&](int tag) {
     if (probe && np + 1 < RS_PROBE_N) {
-      g_rs_probe[np++] = ((unsigned long long)tag << 56) | (__builtin_readcyclecounter() & 0xFFFFFFFFFFFFFFull);
+      probe_buf[np++] = ((unsigned long long)tag << 56) | (__builtin_readcyclecounter() & 0xFFFFFFFFFFFFFFull);
     }
   };
   // plain loads, all landed before the first copy: biases and the tiles' descriptors
@@ -210,6 +224,15 @@ __global__ void __launch_bounds__(RS_NTH) pwg_rstack_kernel(const RstackArgs a) 
   const float* const xg0 = a.x;
   const int ld = a.ld_x, mode = a.mode_x;
   const int nr = (RS_COLS + nhalo + 15) / 16;   // row copies a conv-A step needs (the rest repeat one)
+  // This wave's fragment copy sources of a conv-A step, block 0 (floats; block R adds R MT 512):
+  // copy i = wave + 8 kk of the step's 3 MT 2 one-KB fragment pieces (wave-uniform, computed once)
+  int aoff[D];
+#pragma unroll
+  for (int kk = 0; kk < D; ++kk) {
+    const int i = min(wave + RS_NWV * kk, S::A1 - 1);
+    const int tap = i / (2 * MT), rem = i - tap * 2 * MT;
+    aoff[kk] = __builtin_amdgcn_readfirstlane(tap * CS * MT * 512 + rem * 256);
+  }
   // Per-lane element offsets (x row * ld + 4 q) of this wave's row copies for the tile whose conv-A
   // blocks are being issued: computed with its block 0's copies, reused for blocks 1 .. CS - 1 (only
   // the channel block moves). Copies of the next tile's blocks start after the last of this one's.
@@ -250,11 +273,14 @@ __global__ void __launch_bounds__(RS_NTH) pwg_rstack_kernel(const RstackArgs a) 
         const float* src;
         int dst = i;
         if (i < S::A1) {
-          const int tap = i / (2 * MT), rem = i - tap * 2 * MT;
-          src = wA + ((tap * CS + R) * MT) * 512 + rem * 256 + lane4;
+          src = wA + (aoff[kk] + R * MT * 512) + lane4;
         } else {
           dst = S::A1 + min(i - S::A1, nr - 1);
           src = xg + roff[kk] + 16 * R;
+#ifdef RS_DIAG_NOROWS
+          dst = 0;
+          src = wA + (aoff[0] + R * MT * 512) + lane4;
+#endif
         }
         __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(slot + dst * 1024), 16, 0, 0);
       }
@@ -289,6 +315,9 @@ __global__ void __launch_bounds__(RS_NTH) pwg_rstack_kernel(const RstackArgs a) 
     constexpr bool own = E < IW && IW + DT - P + 1 <= E;  // this tile's stores
     const int nst = ((prev && k > 0) ? 1 : 0) + (own ? 1 : 0);
     auto w2 = [&](auto nsc) {
+#ifdef RS_DIAG_NOWAIT
+      return;  // (timing only: the copies are not waited for)
+#endif
       constexpr int NS = decltype(nsc)::value * S::NST;
       if (nd >= 2) rs_vm_wait<2 * D + NS>();
       else if (nd == 1) rs_vm_wait<D + NS>();
@@ -300,54 +329,88 @@ __global__ void __launch_bounds__(RS_NTH) pwg_rstack_kernel(const RstackArgs a) 
   };
   auto barrier = [] {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#ifndef RS_DIAG_NOBAR
     __builtin_amdgcn_s_barrier();
+#endif
   };
 
   rs_f32x16 accA[MT], accB[S::MP];
   rs_u32x4 xbh[CS], xbl[CS];  // the 1x1's x operands (this lane's column, channels 16 cb + 8 hh ..)
   const float slope1 = a.slope1, slope2 = a.slope2, slopeH = a.slope_h;
-  const int mode2 = a.mode_2;
   const bool id2 = slope2 == 1.f;  // the skip path's usual pre-activation: none
   // convert the rows of conv-A block cb in slot s (tile k) in place: LeakyReLU (zero outside the
   // utterance under zero padding), fp16 hi/lo split; the lane of column q0 + 32 wave + cl also keeps
   // its raw channels 8 hh .. + 7, pre-activated for the 1x1 and split, as x operand cb
-  auto convert = [&](int s, int k, auto cbc) {
+  // Converting the rows of conv-A block cb in slot s (tile k) in place: LeakyReLU (zero outside the
+  // utterance under zero padding), fp16 hi/lo split. Lane (cl, hh) of wave w converts half hh of the
+  // row of column q0 + 32 w + cl and keeps its raw channels 8 hh .. + 7, pre-activated for the 1x1 and
+  // split, as x operand cb (that column's only use of them; a dead column's garbage is never stored,
+  // so no edge test); waves 4 and 5 also convert the 2 dil halo rows. In two parts: the reads
+  // (cv_load) and the rest (cv_finish), so a wave can have the reads in flight over its MFMAs.
+  struct CvRaw {
+    rs_f32x4 c0, c1, h0, h1;
+    int rc, rh;
+    bool halo;
+  };
+  const bool zmode = mode == PWG_PAD_ZERO;
+  auto cv_load = [&](int s) {
+    unsigned char* const rows = slot_of(s) + S::A1 * 1024;
+    CvRaw r;
+    r.rc = pad + 32 * wave + cl;
+    const int swc = (r.rc >> 2) & 3;
+    r.c0 = *reinterpret_cast<const rs_f32x4*>(rows + (size_t)r.rc * 64 + 16 * ((2 * hh) ^ swc));
+    r.c1 = *reinterpret_cast<const rs_f32x4*>(rows + (size_t)r.rc * 64 + 16 * ((2 * hh + 1) ^ swc));
+    const int j = 32 * (wave - RS_NWV / 2) + cl;
+    r.halo = wave >= RS_NWV / 2 && 32 * (wave - RS_NWV / 2) < nhalo;  // wave-uniform
+    r.rh = j < pad ? j : j + RS_COLS;
+    r.h0 = r.h1 = rs_f32x4{0.f, 0.f, 0.f, 0.f};
+    if (r.halo && j < nhalo) {
+      const int swh = (r.rh >> 2) & 3;
+      r.h0 = *reinterpret_cast<const rs_f32x4*>(rows + (size_t)r.rh * 64 + 16 * ((2 * hh) ^ swh));
+      r.h1 = *reinterpret_cast<const rs_f32x4*>(rows + (size_t)r.rh * 64 + 16 * ((2 * hh + 1) ^ swh));
+    }
+    return r;
+  };
+  auto cv_finish = [&](int s, int k, const CvRaw& r, auto cbc) {
     constexpr int cb = decltype(cbc)::value;
     unsigned char* const rows = slot_of(s) + S::A1 * 1024;
     const int* const td = stile + RS_TD * k;
     const int q0 = td[0], T = td[2];
-    auto one = [&](int row, bool keep) {
-      const int sw = (row >> 2) & 3;
-      unsigned char* const rb = rows + (size_t)row * 64;
-      const rs_f32x4 v0 = *reinterpret_cast<const rs_f32x4*>(rb + 16 * ((2 * hh) ^ sw));
-      const rs_f32x4 v1 = *reinterpret_cast<const rs_f32x4*>(rb + 16 * ((2 * hh + 1) ^ sw));
+    auto put = [&](int row, const rs_f32x4& v0, const rs_f32x4& v1) {
       const rs_f32x8 x = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-      int p = q0 + a.off + row;
-      const bool ok = rs_edge(p, T, mode);
       rs_f32x8 c;
+      if (zmode) {
+        const int p = q0 + a.off + row;
+        const bool ok = p >= 0 && p < T;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) c[e] = ok ? rs_lrelu(x[e], slope1) : 0.f;
+        for (int e = 0; e < 8; ++e) c[e] = ok ? rs_lrelu(x[e], slope1) : 0.f;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) c[e] = rs_lrelu(x[e], slope1);
+      }
       rs_u32x4 h, l;
       rs_split8(c, h, l);
-      *reinterpret_cast<rs_u32x4*>(rb + 16 * (hh ^ sw)) = h;
-      *reinterpret_cast<rs_u32x4*>(rb + 16 * ((2 + hh) ^ sw)) = l;
-      if (keep) {
-        int p2 = q0 + 32 * wave + cl;
-        const bool ok2 = rs_edge(p2, T, mode2);
-        rs_f32x8 c2;
-        if (id2) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) c2[e] = ok2 ? x[e] : 0.f;
-        } else {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) c2[e] = ok2 ? rs_lrelu(x[e], slope2) : 0.f;
-        }
-        rs_split8(c2, xbh[cb], xbl[cb]);
-      }
+      const int sw = (row >> 2) & 3;
+      *reinterpret_cast<rs_u32x4*>(rows + (size_t)row * 64 + 16 * (hh ^ sw)) = h;
+      *reinterpret_cast<rs_u32x4*>(rows + (size_t)row * 64 + 16 * ((2 + hh) ^ sw)) = l;
     };
-    one(pad + 32 * wave + cl, true);
-    const int j = 32 * wave + cl;
-    if (32 * wave < nhalo && j < nhalo) one(j < pad ? j : j + RS_COLS, false);
+#ifndef RS_DIAG_NOCONV
+    put(r.rc, r.c0, r.c1);
+    if (r.halo && 32 * (wave - RS_NWV / 2) + cl < nhalo) put(r.rh, r.h0, r.h1);
+#endif
+    const rs_f32x8 x = {r.c0[0], r.c0[1], r.c0[2], r.c0[3], r.c1[0], r.c1[1], r.c1[2], r.c1[3]};
+    rs_f32x8 c2;
+    if (id2) {
+      c2 = x;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) c2[e] = rs_lrelu(x[e], slope2);
+    }
+    rs_split8(c2, xbh[cb], xbl[cb]);
+  };
+  auto convert = [&](int s, int k, auto cbc) {
+    const CvRaw r = cv_load(s);
+    cv_finish(s, k, r, cbc);
   };
   // conv A, block cb of slot s: 3 taps x MT m-tiles (the x-tile kernel's order)
   // one unit's operands: A fragments (hi, lo) of every m-tile + the B pair. Units run as a 2-deep
@@ -366,6 +429,10 @@ __global__ void __launch_bounds__(RS_NTH) pwg_rstack_kernel(const RstackArgs a) 
     }
   };
   auto mma_ops = [&](rs_f32x16 (&acc)[MT], const Ops& o) {
+#ifdef RS_DIAG_NOMFMA1
+    asm volatile("" :: "v"(o.ah[0]), "v"(o.al[MT - 1]), "v"(o.bh), "v"(o.bl));
+    return;
+#endif
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[m] = rs_mma3(o.ah[m], o.al[m], o.bh, o.bl, acc[m]);
   };
@@ -428,11 +495,15 @@ __global__ void __launch_bounds__(RS_NTH) pwg_rstack_kernel(const RstackArgs a) 
     if (I < n_steps) issue(I, I / SPT, std::integral_constant<int, I % SPT>{});
   });
   int s = 0;
+  // the first tile's block 0: rows landed -> converted (every later tile's block 0 is converted in
+  // the step before it, the previous tile's last)
+  stamp(1);
+  wait_at(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, 0);
+  stamp(2);
+  barrier();
+  stamp(3);
+  convert(0, 0, std::integral_constant<int, 0>{});
   for (int k = 0; k < nt; ++k) {
-    // tile start: block 0's rows landed -> convert them (slot s)
-    wait_at(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, k);
-    barrier();
-    convert(s, k, std::integral_constant<int, 0>{});
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -446,15 +517,24 @@ __global__ void __launch_bounds__(RS_NTH) pwg_rstack_kernel(const RstackArgs a) 
       stamp(5);
       barrier();
       stamp(6);
-      issue_ahead(s, k, cbc);
-      stamp(7);
-      // the two waves of a SIMD (w, w + 4) in opposite order: one converts the next block while the
-      // other's MFMAs run, then the other way round
-      if (wave < RS_NWV / 2) {
-        mma_conv(s);
-        stamp(8);
-        if constexpr (cb + 1 < CS) convert(s + 1, k, std::integral_constant<int, cb + 1>{});
+      // the two waves of a SIMD (w, w + 4) in opposite order: one starts its MFMAs at the barrier and
+      // then issues the copies and converts the next block, the other does that first, so the
+      // SIMD's matrix pipe has a wave to feed through the whole step
+      if (RS_ORDER != 0) issue_ahead(s, k, cbc);
+      if (wave < RS_NWV / 2 || RS_ORDER == 2) {
+        if constexpr (cb + 1 < CS) {
+          const CvRaw r = cv_load(s + 1);  // in flight over the MFMAs
+          mma_conv(s);
+          stamp(8);
+          if (RS_ORDER == 0) issue_ahead(s, k, cbc);
+          cv_finish(s + 1, k, r, std::integral_constant<int, cb + 1>{});
+        } else {
+          mma_conv(s);
+          stamp(8);
+          if (RS_ORDER == 0) issue_ahead(s, k, cbc);
+        }
       } else {
+        if (RS_ORDER == 0) issue_ahead(s, k, cbc);
         if constexpr (cb + 1 < CS) convert(s + 1, k, std::integral_constant<int, cb + 1>{});
         mma_conv(s);
       }
@@ -527,11 +607,375 @@ __global__ void __launch_bounds__(RS_NTH) pwg_rstack_kernel(const RstackArgs a) 
         });
         stamp(14);
       }
+      // the next tile's block 0 (slot s + 1, landed: waited for above)
+      if constexpr (g2 == S::S2 - 1) {
+        if (k + 1 < nt) convert(s + 1, k + 1, std::integral_constant<int, 0>{});
+      }
       ++s;
     });
   }
   rs_vm_wait<0>();
-  if (probe) g_rs_probe[0] = (unsigned long long)np | ((unsigned long long)nt << 16) | ((unsigned long long)CS << 32);
+  if (probe) probe_buf[0] = (unsigned long long)np | ((unsigned long long)nt << 16) | ((unsigned long long)CS << 32);
+}
+
+// Resident-weight variant (C <= 64: every fragment of both ops, <= 80 KB, fits the LDS beside the
+// ring): the workgroup copies the weights to LDS once and the ring carries only each conv-A block's
+// raw rows. The streamed kernel above re-copies 180 KB of L2-hot fragments per 256-column tile and is
+// bound by the CU's LDS-DMA intake (~8-13 B/cycle when every CU loads; MI355X_MICROARCH.md prologue
+// burst): with the fragments resident a step copies 17-20 KB instead of 32 KB (48 channels).
+// Same products, order, splits and epilogue: bit-identical to the streamed kernel.
+template <int CS>
+struct RrShape {
+  static constexpr int MT = (CS + 1) / 2;
+  static constexpr int C = 16 * CS;
+  static constexpr int WA = 3 * CS * MT * 2;        // 1-KB pieces of conv A's fragments
+  static constexpr int WB = 2 * CS * MT * 2;        // ... of the 1x1's
+  static constexpr int W = WA + WB;
+  static constexpr int NRMAX = RS_ROWS / 16;         // row copies of a step at most
+  static constexpr int D = (NRMAX + RS_NWV - 1) / RS_NWV;  // copies per wave per step
+  static constexpr int SPT = CS;                     // ring steps per tile (conv-A blocks)
+  static constexpr int E = CS - 1;                   // the stores follow this step's copies
+  static constexpr int NST = (C / 32) * 4 + (C % 32 ? 2 : 0);
+};
+
+template <int CS>
+__global__ void __launch_bounds__(RS_NTH) pwg_rstack_res_kernel(const RstackArgs a) {
+  using S = RrShape<CS>;
+  constexpr int MT = S::MT, C = S::C, P = RS_P, D = S::D, SPT = S::SPT;
+  typedef __attribute__((address_space(1))) void* gptr_t;
+  typedef __attribute__((address_space(3))) void* lptr_t;
+  extern __shared__ __attribute__((aligned(16))) unsigned char rr_smem[];
+  const int nhalo = 2 * a.dil;
+  const int nr = (RS_COLS + nhalo + 15) / 16;  // row copies a step needs (the rest repeat one)
+  const int slot_bytes = nr * 1024;
+  unsigned char* const wl = rr_smem;                                     // [W][1 KB] fragments
+  unsigned char* const ring = rr_smem + S::W * 1024;                     // [P][nr KB] raw rows
+  float* const sbias = reinterpret_cast<float*>(ring + P * slot_bytes);  // [b_A C][b C]
+  int* const stile = reinterpret_cast<int*>(sbias + 2 * C);             // [tile][RS_TD]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int hh = lane >> 5, cl = lane & 31;
+  auto slot_of = [&](int s) {
+    unsigned o = (unsigned)(s % RS_P) * (unsigned)slot_bytes;
+    asm volatile("" : "+s"(o));
+    return ring + o;
+  };
+  const int g = blockIdx.x, ng = gridDim.x;
+  const int t_begin = (int)(((long long)a.n_blocks * g) / ng);
+  const int nt = (int)(((long long)a.n_blocks * (g + 1)) / ng) - t_begin;
+  if (nt <= 0) return;
+  for (int i = threadIdx.x; i < 2 * C; i += RS_NTH) sbias[i] = i < C ? a.bA[i] : a.bB[i - C];
+  for (int k = threadIdx.x; k < nt; k += RS_NTH) {
+    const int2 b = a.blocks[t_begin + k];
+    const int2 sx = *reinterpret_cast<const int2*>(a.seg_x + 2 * b.x);
+    const int2 sy = *reinterpret_cast<const int2*>(a.seg_y + 2 * b.x);
+    int* const td = stile + RS_TD * k;
+    td[0] = b.y;
+    td[1] = sx.x;
+    td[2] = sx.y;
+    td[3] = sy.x;
+    td[4] = a.ncols[b.x];
+  }
+  // the weights, once: conv A's fragments [tap cs + cb][MT][hi/lo], then the 1x1's [chunk][MT][hi/lo]
+  for (int i = wave; i < S::W; i += RS_NWV) {
+    const float* src = (i < S::WA ? a.wA + (size_t)i * 256 : a.wB + (size_t)(i - S::WA) * 256) + lane * 4;
+    __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(wl + i * 1024), 16, 0, 0);
+  }
+  rs_vm_wait<0>();
+  __syncthreads();
+
+  const int n_steps = nt * SPT;
+  const int pad = -a.off;
+  const float* const xg0 = a.x;
+  const int ld = a.ld_x, mode = a.mode_x;
+  int roff[D];
+  // step s (block R of tile k): this wave's row copies i = wave + 8 kk (piece q of row r at position
+  // q ^ (r >> 2 & 3)); the row offsets are computed with block 0's copies
+  auto issue = [&](int s, int k, auto rc) {
+    constexpr int R = decltype(rc)::value;
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const float* xg = xg0;
+    asm volatile("" : "+s"(xg));
+    unsigned char* const slot = slot_of(s);
+    if constexpr (R == 0) {
+      const int* const td = stile + RS_TD * k;
+      const int q0 = td[0], rx = td[1], T = td[2];
+#pragma unroll
+      for (int kk = 0; kk < D; ++kk) {
+        const int j = min(wave + RS_NWV * kk, nr - 1);
+        const int row = 16 * j + (ln >> 2);
+        const int q = (ln & 3) ^ ((row >> 2) & 3);
+        int p = q0 + a.off + row;
+        (void)rs_edge(p, T, mode);
+        roff[kk] = (rx + p) * ld + 4 * q;
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < D; ++kk) {
+      const int j = min(wave + RS_NWV * kk, nr - 1);
+      __builtin_amdgcn_global_load_lds((gptr_t)(xg + roff[kk] + 16 * R), (lptr_t)(slot + j * 1024), 16, 0, 0);
+    }
+  };
+  auto issue_ahead = [&](int s, int k, auto isc) {
+    constexpr int IS = decltype(isc)::value;
+    constexpr int R = (IS + P - 1) % SPT, DK = (IS + P - 1) / SPT;
+    if (s + P - 1 < n_steps) issue(s + P - 1, k + DK, std::integral_constant<int, R>{});
+  };
+  // the waits (the streamed kernel's wait_at with SPT = CS and the stores after step E = CS - 1)
+  auto wait_at = [&](auto iwc, auto dtc, int k) {
+    constexpr int IW = decltype(iwc)::value, DT = decltype(dtc)::value, E = S::E;
+    const int w = k * SPT + IW, t = w + DT;
+    const int nd = min(w + P - 2, n_steps - 1) - t;
+    constexpr bool prev = IW + DT - P + 1 <= E - SPT;
+    constexpr bool own = E < IW && IW + DT - P + 1 <= E;
+    const int nst = ((prev && k > 0) ? 1 : 0) + (own ? 1 : 0);
+    auto w2 = [&](auto nsc) {
+      constexpr int NS = decltype(nsc)::value * S::NST;
+      if (nd >= 2) rs_vm_wait<2 * D + NS>();
+      else if (nd == 1) rs_vm_wait<D + NS>();
+      else rs_vm_wait<NS>();
+    };
+    if (nst == 0) w2(std::integral_constant<int, 0>{});
+    else if (nst == 1) w2(std::integral_constant<int, 1>{});
+    else w2(std::integral_constant<int, 2>{});
+  };
+  auto barrier = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+
+  rs_f32x16 accA[MT], accB[MT];
+  rs_u32x4 xbh[CS], xbl[CS];
+  const float slope1 = a.slope1, slope2 = a.slope2, slopeH = a.slope_h;
+  const bool id2 = slope2 == 1.f;
+  struct CvRaw {
+    rs_f32x4 c0, c1, h0, h1;
+    int rc, rh;
+    bool halo;
+  };
+  const bool zmode = mode == PWG_PAD_ZERO;
+  auto cv_load = [&](int s) {
+    unsigned char* const rows = slot_of(s);
+    CvRaw r;
+    r.rc = pad + 32 * wave + cl;
+    const int swc = (r.rc >> 2) & 3;
+    r.c0 = *reinterpret_cast<const rs_f32x4*>(rows + (size_t)r.rc * 64 + 16 * ((2 * hh) ^ swc));
+    r.c1 = *reinterpret_cast<const rs_f32x4*>(rows + (size_t)r.rc * 64 + 16 * ((2 * hh + 1) ^ swc));
+    const int j = 32 * (wave - RS_NWV / 2) + cl;
+    r.halo = wave >= RS_NWV / 2 && 32 * (wave - RS_NWV / 2) < nhalo;
+    r.rh = j < pad ? j : j + RS_COLS;
+    r.h0 = r.h1 = rs_f32x4{0.f, 0.f, 0.f, 0.f};
+    if (r.halo && j < nhalo) {
+      const int swh = (r.rh >> 2) & 3;
+      r.h0 = *reinterpret_cast<const rs_f32x4*>(rows + (size_t)r.rh * 64 + 16 * ((2 * hh) ^ swh));
+      r.h1 = *reinterpret_cast<const rs_f32x4*>(rows + (size_t)r.rh * 64 + 16 * ((2 * hh + 1) ^ swh));
+    }
+    return r;
+  };
+  auto cv_finish = [&](int s, int k, const CvRaw& r, auto cbc) {
+    constexpr int cb = decltype(cbc)::value;
+    unsigned char* const rows = slot_of(s);
+    const int* const td = stile + RS_TD * k;
+    const int q0 = td[0], T = td[2];
+    auto put = [&](int row, const rs_f32x4& v0, const rs_f32x4& v1) {
+      const rs_f32x8 x = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      rs_f32x8 c;
+      if (zmode) {
+        const int p = q0 + a.off + row;
+        const bool ok = p >= 0 && p < T;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) c[e] = ok ? rs_lrelu(x[e], slope1) : 0.f;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) c[e] = rs_lrelu(x[e], slope1);
+      }
+      rs_u32x4 h, l;
+      rs_split8(c, h, l);
+      const int sw = (row >> 2) & 3;
+      *reinterpret_cast<rs_u32x4*>(rows + (size_t)row * 64 + 16 * (hh ^ sw)) = h;
+      *reinterpret_cast<rs_u32x4*>(rows + (size_t)row * 64 + 16 * ((2 + hh) ^ sw)) = l;
+    };
+    put(r.rc, r.c0, r.c1);
+    if (r.halo && 32 * (wave - RS_NWV / 2) + cl < nhalo) put(r.rh, r.h0, r.h1);
+    const rs_f32x8 x = {r.c0[0], r.c0[1], r.c0[2], r.c0[3], r.c1[0], r.c1[1], r.c1[2], r.c1[3]};
+    rs_f32x8 c2;
+    if (id2) {
+      c2 = x;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) c2[e] = rs_lrelu(x[e], slope2);
+    }
+    rs_split8(c2, xbh[cb], xbl[cb]);
+  };
+  auto convert = [&](int s, int k, auto cbc) {
+    const CvRaw r = cv_load(s);
+    cv_finish(s, k, r, cbc);
+  };
+  const rs_u32x4* const wlA = reinterpret_cast<const rs_u32x4*>(wl) + lane;
+  const rs_u32x4* const wlB = reinterpret_cast<const rs_u32x4*>(wl + S::WA * 1024) + lane;
+  struct Ops {
+    rs_u32x4 ah[MT], al[MT], bh, bl;
+  };
+  // conv A, block cb (compile-time) of slot s: 3 taps x MT m-tiles, operands one tap ahead
+  auto mma_conv = [&](int s, auto cbc) {
+    constexpr int cb = decltype(cbc)::value;
+    const unsigned char* const rows = slot_of(s);
+    auto load_tap = [&](Ops& o, int t) {
+      const int tr = 32 * wave + cl + t * a.dil;
+      const int sw = (tr >> 2) & 3;
+      o.bh = *reinterpret_cast<const rs_u32x4*>(rows + (size_t)tr * 64 + 16 * (hh ^ sw));
+      o.bl = *reinterpret_cast<const rs_u32x4*>(rows + (size_t)tr * 64 + 16 * ((2 + hh) ^ sw));
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        o.ah[m] = wlA[(((t * CS + cb) * MT + m) * 2) * 64];
+        o.al[m] = wlA[(((t * CS + cb) * MT + m) * 2 + 1) * 64];
+      }
+    };
+    Ops o[2];
+    load_tap(o[0], 0);
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      if (t + 1 < 3) load_tap(o[(t + 1) & 1], t + 1);
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int m = 0; m < MT; ++m) accA[m] = rs_mma3(o[t & 1].ah[m], o[t & 1].al[m], o[t & 1].bh, o[t & 1].bl, accA[m]);
+      asm volatile("" ::: "memory");
+    }
+  };
+  // h operands, the 1x1 over [h; x] (all of it: its fragments are resident), the epilogue
+  auto stage2 = [&](int k) {
+    rs_u32x4 hbh[CS], hbl[CS];
+    rs_static_for<0, CS>([&](auto chc) {
+      constexpr int ch = decltype(chc)::value;
+      constexpr int mh = ch >> 1, J0 = (ch & 1) * 2;
+      const float* const bb = sbias + 16 * ch + 8 * hh;
+      rs_f32x8 x;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float va = accA[mh][4 * J0 + e], vb = accA[mh][4 * (J0 + 1) + e];
+        const float xa = __shfl_xor(va, 32), xb = __shfl_xor(vb, 32);
+        x[e] = (hh ? xb : va) + bb[e];
+        x[4 + e] = (hh ? vb : xa) + bb[4 + e];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = rs_lrelu(x[e], slopeH);
+      rs_split8(x, hbh[ch], hbl[ch]);
+    });
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) accB[m][e] = 0.f;
+    rs_u32x4 ah[2][MT], al[2][MT];
+    auto load_c = [&](auto cc, int buf) {
+      constexpr int c = decltype(cc)::value;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        ah[buf][m] = wlB[((c * MT + m) * 2) * 64];
+        al[buf][m] = wlB[((c * MT + m) * 2 + 1) * 64];
+      }
+    };
+    load_c(std::integral_constant<int, 0>{}, 0);
+    rs_static_for<0, 2 * CS>([&](auto cc) {
+      constexpr int c = decltype(cc)::value;
+      if constexpr (c + 1 < 2 * CS) load_c(std::integral_constant<int, c + 1>{}, (c + 1) & 1);
+      const rs_u32x4& bh = c < CS ? hbh[c < CS ? c : 0] : xbh[c < CS ? 0 : c - CS];
+      const rs_u32x4& bl = c < CS ? hbl[c < CS ? c : 0] : xbl[c < CS ? 0 : c - CS];
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int m = 0; m < MT; ++m) accB[m] = rs_mma3(ah[c & 1][m], al[c & 1][m], bh, bl, accB[m]);
+      asm volatile("" ::: "memory");
+    });
+    const int* const td = stile + RS_TD * k;
+    const int q0 = td[0], ry = td[3], nq = td[4];
+    const int live = min(max(nq - q0, 0), RS_COLS);
+    const unsigned long long base = reinterpret_cast<unsigned long long>(a.y + ((size_t)ry + q0) * C);
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)base);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(base >> 32));
+    const int nbytes = __builtin_amdgcn_readfirstlane(live * C * 4);
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(((unsigned long long)hi << 32) | lo), (short)0, nbytes, 0x00020000);
+    const int voff = (32 * wave + cl) * C * 4;
+    const float* const bB = sbias + C;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int j4 = 0; j4 < 4; ++j4) {
+        const int row = 32 * m + 8 * j4 + 4 * hh;
+        if (32 * m + 8 * j4 >= C) continue;
+        rs_f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = accB[m][4 * j4 + e] + bB[row + e];
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(rs_u32x4, v), rsrc, voff + row * 4, 0, 0);
+      }
+  };
+
+  rs_static_for<0, P - 1>([&](auto ic) {
+    constexpr int I = decltype(ic)::value;
+    if (I < n_steps) issue(I, I / SPT, std::integral_constant<int, I % SPT>{});
+  });
+  int s = 0;
+  wait_at(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, 0);
+  barrier();
+  convert(0, 0, std::integral_constant<int, 0>{});
+  for (int k = 0; k < nt; ++k) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) accA[m][e] = 0.f;
+    rs_static_for<0, CS>([&](auto cbc) {
+      constexpr int cb = decltype(cbc)::value;
+      if (s + 1 < n_steps) wait_at(cbc, std::integral_constant<int, 1>{}, k);
+      barrier();
+      if constexpr (cb + 1 < CS) {
+        // partner phases (the streamed kernel's order)
+        if (wave < RS_NWV / 2) {
+          const CvRaw r = cv_load(s + 1);
+          mma_conv(s, cbc);
+          issue_ahead(s, k, cbc);
+          cv_finish(s + 1, k, r, std::integral_constant<int, cb + 1>{});
+        } else {
+          issue_ahead(s, k, cbc);
+          convert(s + 1, k, std::integral_constant<int, cb + 1>{});
+          mma_conv(s, cbc);
+        }
+      } else {
+        // the tile's last block: its MFMAs, the 1x1 and the stores, then the next tile's block 0
+        // (slot s + 1, waited for above; its x operands replace this tile's after the 1x1)
+        issue_ahead(s, k, cbc);
+        mma_conv(s, cbc);
+        stage2(k);
+        if (k + 1 < nt) convert(s + 1, k + 1, std::integral_constant<int, 0>{});
+      }
+      ++s;
+    });
+  }
+  rs_vm_wait<0>();
+}
+
+template <int CS>
+constexpr int rr_lds_fixed() {
+  return RrShape<CS>::W * 1024 + 2 * RrShape<CS>::C * 4 + RS_MAX_TILES * RS_TD * 4;
+}
+int rr_lds(int cs, int dil) {
+  const int nr = (RS_COLS + 2 * dil + 15) / 16;
+  int fixed = 0;
+  switch (cs) {
+    case 2: fixed = rr_lds_fixed<2>(); break;
+    case 3: fixed = rr_lds_fixed<3>(); break;
+    case 4: fixed = rr_lds_fixed<4>(); break;
+    default: return 0;
+  }
+  return fixed + RS_P * nr * 1024;
+}
+
+template <int CS>
+hipError_t rr_go(const RstackArgs& a, int n_wg, hipStream_t s) {
+  const int lds = rr_lds(CS, a.dil);
+  const hipError_t e = allow_lds(reinterpret_cast<const void*>(pwg_rstack_res_kernel<CS>), lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((pwg_rstack_res_kernel<CS>), dim3((unsigned)n_wg), dim3(RS_NTH), (size_t)lds, s, a);
+  return hipGetLastError();
 }
 
 template <int CS>
@@ -562,10 +1006,27 @@ int rstack_lds(int cs) {
   return 0;
 }
 
-hipError_t launch_rstack(const RstackArgs& a, int cs, int n_wg, hipStream_t s) {
+hipError_t launch_rstack_impl(const RstackArgs& a, int cs, int n_wg, hipStream_t s, bool resident);
+static std::atomic<long long> g_rs_launches{0};  // launches enqueued (tests: the kernel engaged)
+
+hipError_t launch_rstack(const RstackArgs& a, int cs, int n_wg, hipStream_t s, bool resident) {
+  const hipError_t e = launch_rstack_impl(a, cs, n_wg, s, resident);
+  if (e == hipSuccess) g_rs_launches.fetch_add(1, std::memory_order_relaxed);
+  return e;
+}
+
+hipError_t launch_rstack_impl(const RstackArgs& a, int cs, int n_wg, hipStream_t s, bool resident) {
   if (!rstack_supported(cs) || a.n_blocks < 1 || n_wg < 1 || a.dil < 1 || 2 * a.dil > RS_MAX_REACH ||
       (a.n_blocks + n_wg - 1) / n_wg > RS_MAX_TILES)
     return hipErrorInvalidValue;
+  // the weights stay in LDS where they fit beside the ring (<= 64 channels)
+  if (resident && cs <= 4 && rr_lds(cs, a.dil) <= 160 * 1024) {
+    switch (cs) {
+      case 2: return rr_go<2>(a, n_wg, s);
+      case 3: return rr_go<3>(a, n_wg, s);
+      case 4: return rr_go<4>(a, n_wg, s);
+    }
+  }
   switch (cs) {
     case 2: return rs_go<2>(a, n_wg, s);
     case 3: return rs_go<3>(a, n_wg, s);
@@ -576,6 +1037,11 @@ hipError_t launch_rstack(const RstackArgs& a, int cs, int n_wg, hipStream_t s) {
 }
 
 }  // namespace pwg
+
+// Test hook: batched-stack launches enqueued since the library loaded
+extern "C" __attribute__((visibility("default"))) long long pwg_rstack_debug_launches(void) {
+  return pwg::g_rs_launches.load(std::memory_order_relaxed);
+}
 
 // Diagnostic (tools/diag/rstack_probe.py): enable = 1 arms the timeline for workgroup wg of the next
 // launches with cs = enable (0 disarms); out != null copies the last timeline (n >= RS_PROBE_N words).

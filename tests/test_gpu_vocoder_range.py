@@ -145,9 +145,13 @@ def test_full_length_ragged_batch_against_torch_cpu(cfg, built_lib, cuda_device)
     m = m.to(cuda_device)
     lengths = [1199, 80, 517]
     mels = [synthetic.make_mel(f, 80, seed=300 + i) for i, f in enumerate(lengths)]
+    from test_gpu_vocoders import _rstack_launches
+    n0 = _rstack_launches()
     with torch.no_grad():
         ys = [y.cpu().numpy() for y in m.inference_batch(mels)]
     assert m.engine().range_reruns == 0
+    if cfg == "mb_melgan_v2":  # its 48-channel stage runs batched: the LDS-ring stack kernel
+        assert _rstack_launches() > n0
     torch.set_num_threads(min(16, torch.get_num_threads()))
     gen = TorchCPUVocoder(cls_name, sd, params, syn)
     for f, mel, y in zip(lengths, mels, ys):

@@ -26,7 +26,8 @@ def main():
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--mstack", type=int, default=None, help="PWG_CNET_OPT_MSTACK (fused stack chains) 0/1/2")
     ap.add_argument("--presplit", type=int, default=None, help="PWG_CNET_OPT_PRESPLIT 0/1")
-    ap.add_argument("--rstack", type=int, default=None, help="PWG_CNET_OPT_RSTACK 0/1")
+    ap.add_argument("--rstack", type=int, default=None, help="PWG_CNET_OPT_RSTACK 0/1/2")
+    ap.add_argument("--nocheck", action="store_true", help="no range check / exact-fp32 rerun (diagnostic builds)")
     ap.add_argument("--bitwise-rstack", action="store_true",
                     help="first compare one forward with PWG_CNET_OPT_RSTACK 0 and 1 bit for bit")
     ap.add_argument("--dump", default=None, help="save the first forward's output (.npy) for a bitwise A/B")
@@ -56,24 +57,29 @@ def main():
     mel = torch.randn(frames * 80, device=dev)
     out = torch.empty(plan.out_rows * eng.out_channels, device=dev)
     if a.bitwise_rstack:
-        eng.set_rstack(False)
+        eng.set_rstack(0)
         eng.run(plan, mel, out)
         ref = out.clone()
-        eng.set_rstack(True)
+        eng.set_rstack(2)
+        out.fill_(float("nan"))
+        eng.run(plan, mel, out)
+        torch.cuda.synchronize()
+        print(f"bitwise rstack 0 vs 2: {'equal' if torch.equal(ref, out) else 'DIFFER'}", flush=True)
+        eng.set_rstack(1)
         out.fill_(float("nan"))
         eng.run(plan, mel, out)
         torch.cuda.synchronize()
         same = bool(torch.equal(ref, out))
         print(f"bitwise rstack 0 vs 1: {'equal' if same else 'DIFFER'} max|d| {(ref - out).abs().max().item():.3e}"
               f" finite {bool(torch.isfinite(out).all())}", flush=True)
-    eng.run(plan, mel, out)
+    eng.run(plan, mel, out, check=not a.nocheck)
     torch.cuda.synchronize()
     if a.dump:
         np.save(a.dump, out.cpu().numpy())
     eng.set_timing(True)
     eng.collect_timing()
     for _ in range(a.steps):
-        eng.run(plan, mel, out)
+        eng.run(plan, mel, out, check=not a.nocheck)
     t = eng.collect_timing()
     tot = 0.0
     rows = []
