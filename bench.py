@@ -998,11 +998,16 @@ def main():
             try:
                 broadcast_weights_rccl(eng, packed, src=0)
                 broadcast = "pwg_broadcast_weights (C-ABI, RCCL over xGMI)"
-            except (RuntimeError, OSError, NotImplementedError) as e:  # keep the scaling run alive
-                print(f"[bench] C-ABI RCCL broadcast failed ({e}); using torch.distributed.broadcast",
-                      file=sys.stderr)
+            except (RuntimeError, OSError, NotImplementedError) as e:
+                # the C-ABI broadcast is the design's one collective: a failure ends the run unless
+                # a fallback was asked for explicitly (every rank agrees on the outcome first,
+                # sharding.broadcast_weights_rccl, so no rank waits on a broken communicator)
+                if os.environ.get("PWG_BENCH_BCAST_FALLBACK") != "1":
+                    raise
+                print(f"[bench] C-ABI RCCL broadcast failed ({e}); PWG_BENCH_BCAST_FALLBACK=1: "
+                      "using torch.distributed.broadcast", file=sys.stderr)
                 broadcast_packed_weights(packed, src=0)
-                broadcast = "torch.distributed.broadcast over RCCL (C-ABI broadcast failed)"
+                broadcast = "torch.distributed.broadcast over RCCL (C-ABI broadcast failed, fallback asked for)"
         else:
             broadcast_packed_weights(packed, src=0)
             broadcast = "torch.distributed.broadcast (gloo rehearsal)"

@@ -260,6 +260,11 @@ PWG_API int pwg_get_option(const PwgHandle* h, int option, long long* value);
 /* Timing: 0 off, 1 HIP events around every launch (per-bucket / per-op sums), 2 one event pair
  * around each whole run on the caller's stream (its device span only; no events between launches,
  * so the run's launches are timed undisturbed). */
+/* Per caller stream the handle keeps a pinned host word for pwg_run_status (allocated on the first
+ * status read on that stream, released by pwg_destroy). A host that creates and destroys streams per
+ * request calls pwg_release_stream(h, stream) before destroying a stream: it waits for the stream and
+ * frees that word (a recycled stream handle would otherwise reuse it; a no-op for unknown streams). */
+PWG_API int pwg_release_stream(PwgHandle* h, void* stream);
 PWG_API int pwg_set_timing(PwgHandle* h, int enable);
 PWG_API int pwg_timing_collect(PwgHandle* h, double* ms, long long* launches);
 /* Device span of the timed launches recorded since the last pwg_timing_collect: the first launch's

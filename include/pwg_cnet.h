@@ -195,6 +195,12 @@ PWG_API int pwg_cnet_set_option(PwgCnet* n, int option, long long value);
 /* Timing: 0 off, 1 HIP events around every launch (per-bucket / per-op sums), 2 one event pair
  * around each whole run on the caller's stream (its device span only; no events between launches,
  * so the run's launches are timed undisturbed). */
+/* Per caller stream the handle keeps a set of 3 auxiliary streams, their cross-stream events and a
+ * pinned status word (PWG_CNET_OPT_STREAMS; pwg_cnet_run_status), created on first use and freed by
+ * pwg_cnet_destroy. A host that creates and destroys streams per request calls
+ * pwg_cnet_release_stream(n, stream) before destroying a stream: it waits for that stream and its
+ * auxiliary streams and frees the set (unknown streams and host-only handles: a no-op). */
+PWG_API int pwg_cnet_release_stream(PwgCnet* n, void* stream);
 PWG_API int pwg_cnet_set_timing(PwgCnet* n, int enable);
 /* Adds per-op milliseconds and launch counts (arrays of n_ops) and clears the records. */
 PWG_API int pwg_cnet_timing_collect(PwgCnet* n, double* ms, long long* launches);

@@ -74,6 +74,7 @@ EXPORTED_SYMBOLS = (
     "pwg_set_option",
     "pwg_get_option",
     "pwg_set_timing",
+    "pwg_release_stream",
     "pwg_timing_collect",
     "pwg_timing_span",
     "pwg_rccl_unique_id",
@@ -98,6 +99,7 @@ EXPORTED_SYMBOLS = (
     "pwg_cnet_set_timing",
     "pwg_cnet_timing_collect",
     "pwg_cnet_timing_span",
+    "pwg_cnet_release_stream",
     "pwg_rstack_debug_launches",
     "pwg_rstack_debug_probe",
 )
@@ -317,6 +319,7 @@ def load():
         lib.pwg_rccl_comm_destroy.argtypes = [vp]
         lib.pwg_broadcast_weights.argtypes = [vp, vp, ctypes.c_int, vp, vp]
         lib.pwg_set_timing.argtypes = [vp, ctypes.c_int]
+        lib.pwg_release_stream.argtypes = [vp, vp]
         lib.pwg_set_option.argtypes = [vp, ctypes.c_int, ctypes.c_longlong]
         lib.pwg_timing_collect.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ll)]
         lib.pwg_timing_span.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]

@@ -10,6 +10,7 @@ runs in libpwg_hip.so, and a missing library or a CPU device raises.
 
 import ctypes
 import logging
+import os
 from collections import OrderedDict
 
 import numpy as np
@@ -92,6 +93,7 @@ def lib():
         L.pwg_cnet_set_option.argtypes = [vp, ctypes.c_int, ctypes.c_longlong]
         L.pwg_cnet_timing_collect.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ll)]
         L.pwg_cnet_timing_span.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
+        L.pwg_cnet_release_stream.argtypes = [vp, vp]
         if L.pwg_cnet_abi_version() != 1:
             raise RuntimeError("libpwg_hip cnet ABI version mismatch")
         _bound = True
@@ -242,6 +244,7 @@ class CnetEngine:
 
     def __init__(self, program, device, host_only=False):
         self.program = program
+        self.host_only = bool(host_only)
         self.device = torch.device(device) if device is not None else None
         if not host_only and (self.device is None or self.device.type != "cuda"):
             raise RuntimeError("the conv-network engine runs on a ROCm GPU only (no CPU fallback)")
@@ -303,8 +306,27 @@ class CnetEngine:
             logging.warning("vocoder weights exceed the fp16 pair range of the split-f16 mode: using exact fp32")
             self._set_split(False)
             self.split_f16 = False
+        first = self.packed is None
         self.packed = torch.from_numpy(packed).to(self.device)
+        if first and not self.host_only:
+            self.reserve_workspace()
         return self.packed
+
+    # Workspace reserved when the weights load (outside any call; see Engine.WORKSPACE_RESERVE_MB):
+    # a first call at a new batch shape then pays no device allocation. A MelGAN-family plan needs
+    # ~0.5-1.5 KB per output sample; 256 MiB covers B = 16 x T' = 512 of HiFiGAN v1.
+    WORKSPACE_RESERVE_MB = 256
+
+    def reserve_workspace(self, nbytes=None, stream=None):
+        """Grow ``stream``'s cached workspace to ``nbytes`` (default PWG_CNET_WORKSPACE_RESERVE_MB or
+        WORKSPACE_RESERVE_MB MiB) and load the batch path's concatenation kernel."""
+        from .engine import warm_batch_kernels
+
+        if nbytes is None:
+            nbytes = int(os.environ.get("PWG_CNET_WORKSPACE_RESERVE_MB", self.WORKSPACE_RESERVE_MB)) << 20
+        if nbytes > 0:
+            self.workspace(nbytes, stream)
+        warm_batch_kernels(self.device)
 
     def plan(self, frames):
         key = tuple(int(f) for f in frames)
@@ -338,6 +360,18 @@ class CnetEngine:
     def release_workspace(self):
         """Drop the cached workspaces (the caching allocator keeps the memory for reuse)."""
         self._workspaces = {}
+
+    def release_stream(self, stream):
+        """pwg_cnet_release_stream: free what the handle keeps for ``stream`` (auxiliary streams,
+        events, pinned status word) and this engine's workspace and graphs for it; call before the
+        stream is destroyed when streams are created per request."""
+        key = stream.cuda_stream
+        self._workspaces.pop(key, None)
+        for gk in [k for k in self._graphs if k[1] == key]:
+            self._graphs.pop(gk)
+        for wk in [k for k in self._last_ws if k[1] == key]:
+            self._last_ws.pop(wk)
+        _lib.check(self._lib.pwg_cnet_release_stream(self._h, ctypes.c_void_p(key)))
 
     @property
     def out_channels(self):

@@ -984,9 +984,19 @@ int pwg_run(PwgPlan* p, const float* packed, const float* mel, const float* nois
   DeviceGuard g(h->device);
   hipStream_t s = (hipStream_t)stream;
   hipEvent_t a = pool_get(h), b = pool_get(h);
-  if (!a || !b || hipEventRecord(a, s) != hipSuccess) return fail(PWG_ERR_HIP, "timing event");
+  auto give_back = [&] {  // (a failed record returns both events to the pool instead of leaking them)
+    if (a) h->event_pool.push_back(a);
+    if (b) h->event_pool.push_back(b);
+  };
+  if (!a || !b || hipEventRecord(a, s) != hipSuccess) {
+    give_back();
+    return fail(PWG_ERR_HIP, "timing event");
+  }
   const int rc = pwg_run_impl(p, packed, mel, noise, mean, scale, out, workspace, stream);
-  if (hipEventRecord(b, s) != hipSuccess) return fail(PWG_ERR_HIP, "timing event");
+  if (hipEventRecord(b, s) != hipSuccess) {
+    give_back();
+    return fail(PWG_ERR_HIP, "timing event");
+  }
   h->records.push_back({-1, a, b});
   return rc;
 }
@@ -1023,12 +1033,25 @@ static int pwg_run_impl(PwgPlan* p, const float* packed, const float* mel, const
   auto timed = [&](int bucket, auto&& launch) -> hipError_t {
     if (h->timing != 1) return launch();
     hipEvent_t a = pool_get(h), b = pool_get(h);
-    if (!a || !b) return hipErrorOutOfMemory;
+    auto give_back = [&] {
+      if (a) h->event_pool.push_back(a);
+      if (b) h->event_pool.push_back(b);
+    };
+    if (!a || !b) {
+      give_back();
+      return hipErrorOutOfMemory;
+    }
     hipError_t e = hipEventRecord(a, s);
-    if (e != hipSuccess) return e;
+    if (e != hipSuccess) {
+      give_back();
+      return e;
+    }
     e = launch();
-    if (e != hipSuccess) return e;
-    e = hipEventRecord(b, s);
+    if (e == hipSuccess) e = hipEventRecord(b, s);
+    if (e != hipSuccess) {
+      give_back();
+      return e;
+    }
     h->records.push_back({bucket, a, b});
     return e;
   };
@@ -1523,6 +1546,19 @@ int pwg_get_option(const PwgHandle* h, int option, long long* value) {
 
     default: return fail(PWG_ERR_INVALID, "unknown option");
   }
+}
+
+int pwg_release_stream(PwgHandle* h, void* stream) {
+  if (!h) return fail(PWG_ERR_INVALID, "null handle");
+  std::lock_guard<std::mutex> lk(h->hstatus_mu);
+  auto it = h->hstatus.find((hipStream_t)stream);
+  if (it == h->hstatus.end()) return PWG_OK;
+  DeviceGuard g(h->device);
+  // the pinned word's copy is queued on that stream: let it land before the word is freed
+  if (stream && hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return fail(PWG_ERR_HIP, "stream synchronize");
+  (void)hipHostFree(it->second);
+  h->hstatus.erase(it);
+  return PWG_OK;
 }
 
 int pwg_set_timing(PwgHandle* h, int enable) {

@@ -4823,6 +4823,14 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
   bool out_checked = false;
   // timing mode 2: one event pair around the whole run on the caller's stream (after the join)
   hipEvent_t run_a = nullptr;
+  // (an early return hands the event back to the pool instead of leaking it)
+  struct PoolBack {
+    std::vector<hipEvent_t>& pool;
+    hipEvent_t* e;
+    ~PoolBack() {
+      if (*e) pool.push_back(*e);
+    }
+  } run_a_back{n->pool, &run_a};
   if (n->timing == 2) {
     if (!n->pool.empty()) { run_a = n->pool.back(); n->pool.pop_back(); }
     else if (hipEventCreate(&run_a) != hipSuccess) return fail(PWG_ERR_HIP, "event create");
@@ -5342,8 +5350,12 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
     hipEvent_t run_b = nullptr;
     if (!n->pool.empty()) { run_b = n->pool.back(); n->pool.pop_back(); }
     else if (hipEventCreate(&run_b) != hipSuccess) return fail(PWG_ERR_HIP, "event create");
-    if (hipEventRecord(run_b, s) != hipSuccess) return fail(PWG_ERR_HIP, "timing event");
+    if (hipEventRecord(run_b, s) != hipSuccess) {
+      n->pool.push_back(run_b);
+      return fail(PWG_ERR_HIP, "timing event");
+    }
     n->records.push_back({-1, run_a, run_b});
+    run_a = nullptr;  // (recorded: no longer the guard's)
   }
   return PWG_OK;
 }
@@ -5430,6 +5442,27 @@ int pwg_cnet_set_option(PwgCnet* n, int option, long long value) {
   if (value != 0 && value != 1 && !(option == PWG_CNET_OPT_XT_DMA && value >= 0 && value <= 15))
     return fail(PWG_ERR_INVALID, "option value must be 0 or 1 (PWG_CNET_OPT_XT_DMA: flags 0 - 15)");
   *slot = (int)value;
+  return PWG_OK;
+}
+
+int pwg_cnet_release_stream(PwgCnet* n, void* stream) {
+  if (!n) return fail(PWG_ERR_INVALID, "null handle");
+  if (n->device < 0) return PWG_OK;  // host-only handle: nothing per stream
+  Guard g(n->device);
+  if (!g.ok) return fail(PWG_ERR_HIP, "hipSetDevice failed");
+  std::lock_guard<std::mutex> lk(n->mu);
+  auto it = n->callers.find((hipStream_t)stream);
+  if (it == n->callers.end()) return PWG_OK;
+  PwgCnet::CallerSet& cs = it->second;
+  // the caller's stream and the set's auxiliary streams drain first (a run may still use them)
+  if (stream && hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return fail(PWG_ERR_HIP, "stream synchronize");
+  for (hipStream_t x : cs.aux)
+    if (x && hipStreamSynchronize(x) != hipSuccess) return fail(PWG_ERR_HIP, "stream synchronize");
+  for (hipStream_t x : cs.aux)
+    if (x) (void)hipStreamDestroy(x);
+  for (hipEvent_t e : cs.ev) (void)hipEventDestroy(e);
+  if (cs.hflag) (void)hipHostFree(cs.hflag);
+  n->callers.erase(it);
   return PWG_OK;
 }
 

@@ -355,11 +355,22 @@ class Engine:
 
     def reserve_workspace(self, nbytes=None, stream=None):
         """Grow ``stream``'s cached workspace to ``nbytes`` now (default: PWG_WORKSPACE_RESERVE_MB
-        or WORKSPACE_RESERVE_MB MiB)."""
+        or WORKSPACE_RESERVE_MB MiB), and run the batch path's concatenation once: torch loads a
+        kernel's code object on its first use, and the first ``inference_batch`` paid that (13 ms
+        for torch.cat, tools/diag/first_call_b16.py) inside the call."""
         if nbytes is None:
             nbytes = int(os.environ.get("PWG_WORKSPACE_RESERVE_MB", self.WORKSPACE_RESERVE_MB)) << 20
         if nbytes > 0:
             self.workspace(nbytes, stream)
+        warm_batch_kernels(self.device)
+
+
+def warm_batch_kernels(device):
+    """The drop-ins' batch path concatenates the utterances' inputs (torch.cat) and slices the
+    output: run both once on ``device`` so their first use is not inside a timed call."""
+    a = torch.zeros(3, dtype=torch.float32, device=device)
+    torch.cat([a[:1], a[1:]])
+    torch.cat([a.view(3, 1), a.view(3, 1)], dim=1)
 
     # ---------------------------------------------------------------- plans
     def plan(self, frames, layout=_lib.PWG_LAYOUT_INFERENCE):
@@ -394,6 +405,13 @@ class Engine:
     def release_workspace(self):
         """Drop the cached workspaces (the caching allocator keeps the memory for reuse)."""
         self._workspaces = {}
+
+    def release_stream(self, stream):
+        """pwg_release_stream: free the handle's pinned status word for ``stream`` and this engine's
+        workspace for it; call before the stream is destroyed when streams are created per request."""
+        key = stream.cuda_stream
+        self._workspaces.pop(key, None)
+        _lib.check(self._lib.pwg_release_stream(self._h, ctypes.c_void_p(key)))
 
     # ---------------------------------------------------------------- options
     LAYER_KERNELS = {"persistent": 0, "tiled": 1, "split": 2, "split16": 3}

@@ -225,3 +225,22 @@ def test_interpolate_modes(built_lib):
         with pytest.raises(NotImplementedError):
             HostHandle(configs.generator_params("ljspeech_v1", upsample_params={"upsample_scales": [4, 4, 4, 4],
                                                                                  "interpolate_mode": mode}))
+
+
+def test_release_stream_entry_points(built_lib):
+    """pwg_release_stream / pwg_cnet_release_stream (per-caller-stream resources): a null handle is
+    PWG_ERR_INVALID; an unknown stream, and any stream of a host-only conv-network handle, is a no-op."""
+    import ctypes
+
+    from parallelwavegan_amd import configs as cfgs
+    from parallelwavegan_amd.cnet import CnetEngine
+    from parallelwavegan_amd.melgan import MelGANGenerator
+
+    assert built_lib.pwg_release_stream(None, None) == _lib.PWG_ERR_INVALID
+    L = built_lib
+    L.pwg_cnet_release_stream.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    assert L.pwg_cnet_release_stream(None, None) == _lib.PWG_ERR_INVALID
+    _, p = cfgs.vocoder_params("mb_melgan_test")
+    P, _ = MelGANGenerator(**p).program(False)
+    eng = CnetEngine(P, None, host_only=True)
+    assert L.pwg_cnet_release_stream(eng._h, ctypes.c_void_p(1234)) == _lib.PWG_OK

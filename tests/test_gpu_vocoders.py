@@ -721,3 +721,25 @@ def test_fused_chains_and_presplit_against_oracle(cfg, frames, built_lib, cuda_d
     assert y.shape == ref.shape
     err = np.abs(y - ref).max()
     assert err < ATOL, f"{cfg}: max|d| = {err:.3e}"
+
+
+def test_release_stream_then_reuse(built_lib, cuda_device):
+    """pwg_cnet_release_stream: a caller stream's auxiliary streams, events and pinned status word
+    are freed on request; the next run on that stream builds them again and gives the same bits
+    (HiFiGAN v1 at B = 1: concurrent branches on the auxiliary streams)."""
+    from parallelwavegan_amd import configs, synthetic
+    from parallelwavegan_amd.hifigan import HiFiGANGenerator
+
+    _, params = configs.vocoder_params("hifigan_v1")
+    m = HiFiGANGenerator(**params)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic.make_module_state_dict(m, seed=51).items()})
+    m = m.to(cuda_device)
+    eng = m.engine()
+    mel = torch.from_numpy(synthetic.make_mel(40, 80, seed=52)).to(cuda_device)
+    s = torch.cuda.Stream(cuda_device)
+    with torch.no_grad(), torch.cuda.stream(s):
+        a = m.inference(mel).cpu().numpy()
+        eng.release_stream(s)
+        b = m.inference(mel).cpu().numpy()
+        eng.release_stream(s)
+    np.testing.assert_array_equal(a, b)
