@@ -278,6 +278,14 @@ class Plan:
             self._p = None
 
 
+def warm_batch_kernels(device):
+    """The drop-ins' batch path concatenates the utterances' inputs (torch.cat) and slices the
+    output: run both once on ``device`` so their first use is not inside a timed call."""
+    a = torch.zeros(3, dtype=torch.float32, device=device)
+    torch.cat([a[:1], a[1:]])
+    torch.cat([a.view(3, 1), a.view(3, 1)], dim=1)
+
+
 class Engine:
     """One generator configuration on one device.
 
@@ -363,14 +371,6 @@ class Engine:
         if nbytes > 0:
             self.workspace(nbytes, stream)
         warm_batch_kernels(self.device)
-
-
-def warm_batch_kernels(device):
-    """The drop-ins' batch path concatenates the utterances' inputs (torch.cat) and slices the
-    output: run both once on ``device`` so their first use is not inside a timed call."""
-    a = torch.zeros(3, dtype=torch.float32, device=device)
-    torch.cat([a[:1], a[1:]])
-    torch.cat([a.view(3, 1), a.view(3, 1)], dim=1)
 
     # ---------------------------------------------------------------- plans
     def plan(self, frames, layout=_lib.PWG_LAYOUT_INFERENCE):

@@ -244,3 +244,17 @@ def test_release_stream_entry_points(built_lib):
     P, _ = MelGANGenerator(**p).program(False)
     eng = CnetEngine(P, None, host_only=True)
     assert L.pwg_cnet_release_stream(eng._h, ctypes.c_void_p(1234)) == _lib.PWG_OK
+
+
+def test_engine_classes_carry_their_methods():
+    """The engines' GPU methods are only exercised by `-m gpu` tests: check here that the classes
+    still own them (a module-level def dropped into a class body silently ends the class)."""
+    from parallelwavegan_amd.cnet import CnetEngine
+    from parallelwavegan_amd.engine import Engine, warm_batch_kernels
+
+    for name in ("load_state_dict", "set_packed", "reserve_workspace", "plan", "workspace", "set_option",
+                 "get_option", "run", "run_status", "release_stream"):
+        assert callable(getattr(Engine, name, None)), name
+    for name in ("load_state_dict", "reserve_workspace", "release_stream", "set_rstack"):
+        assert callable(getattr(CnetEngine, name, None)), name
+    assert callable(warm_batch_kernels)
