@@ -3127,21 +3127,10 @@ __global__ void __launch_bounds__(128) pwg_cnet_thin_kernel(const CnConvArgs a, 
 // per 128-quad slice of it plus a scalar weight load per tap (HiFiGAN / MB-MelGAN output convs at
 // B = 1: 17-26 us for a few us of FMAs).
 constexpr int THIN1_LDS = 64 * 1024;
-// TPC threads per column, each summing the outputs o = sub, sub + TPC, ... (same per-output FMA
-// order): M = 4 / 8 outputs no longer serialise on one thread (MB-MelGAN's 4-band output conv).
-template <int M, int TPC>
-__global__ void __launch_bounds__(128 * TPC) pwg_cnet_thin1_kernel(const CnConvArgs a, int nsrc) {
-  constexpr int NT = 128 * TPC, MO = M / TPC;
-  static_assert(M % TPC == 0, "outputs split evenly over a column's threads");
-  const int col = threadIdx.x / TPC, sub = threadIdx.x - col * TPC;
-  extern __shared__ __attribute__((aligned(16))) float s_x[];  // [src][cb][span][THIN_ROW], then [chunk][h][M][8]
-  const int2 blk = a.blocks[blockIdx.x];
-  const int u = blk.x;
-  const int q = blk.y + col;
-  const bool live = q < a.ncols[u];
-  const int xf0 = a.src[0].nc * a.src[0].span * THIN_ROW;
-  const int xf = xf0 + (nsrc > 1 ? a.src[1].nc * a.src[1].span * THIN_ROW : 0);
-  float* const s_w = s_x + xf;
+// Stage the input rows of every 16-channel block of every source (pre-activated, edge rows
+// resolved) into LDS [src][cb][span][THIN_ROW], 8 loads per thread in flight per batch (NT threads).
+template <int NT>
+__device__ __forceinline__ void thin_stage_rows(const CnConvArgs& a, int nsrc, float* s_x, int xf0, int2 blk, int u) {
   constexpr int B = 8;
   for (int si = 0; si < nsrc; ++si) {
     const CnSrc& s = a.src[si];
@@ -3180,6 +3169,25 @@ __global__ void __launch_bounds__(128 * TPC) pwg_cnet_thin1_kernel(const CnConvA
       }
     }
   }
+}
+
+// TPC threads per column, each summing the outputs o = sub, sub + TPC, ... (same per-output FMA
+// order): M = 4 / 8 outputs no longer serialise on one thread (MB-MelGAN's 4-band output conv).
+template <int M, int TPC>
+__global__ void __launch_bounds__(128 * TPC) pwg_cnet_thin1_kernel(const CnConvArgs a, int nsrc) {
+  constexpr int NT = 128 * TPC, MO = M / TPC;
+  static_assert(M % TPC == 0, "outputs split evenly over a column's threads");
+  const int col = threadIdx.x / TPC, sub = threadIdx.x - col * TPC;
+  extern __shared__ __attribute__((aligned(16))) float s_x[];  // [src][cb][span][THIN_ROW], then [chunk][h][M][8]
+  const int2 blk = a.blocks[blockIdx.x];
+  const int u = blk.x;
+  const int q = blk.y + col;
+  const bool live = q < a.ncols[u];
+  const int xf0 = a.src[0].nc * a.src[0].span * THIN_ROW;
+  const int xf = xf0 + (nsrc > 1 ? a.src[1].nc * a.src[1].span * THIN_ROW : 0);
+  float* const s_w = s_x + xf;
+  thin_stage_rows<NT>(a, nsrc, s_x, xf0, blk, u);
+  constexpr int B = 8;
   // weights: chunk c, h, output o -> 8 floats (k-steps 8 h + [0, 8)): sub 0 then sub 1 of lane o + 32 h
   {
     const int total = a.n_chunks * 2 * M * 2;  // quads: [chunk][h][o][sub]
@@ -3256,6 +3264,84 @@ __global__ void __launch_bounds__(128 * TPC) pwg_cnet_thin1_kernel(const CnConvA
   if (a.range_flag) flag_range(a.range_flag, nullptr, bad, (int)(threadIdx.x & 63));
 }
 
+// Wide-plan form of pwg_cnet_thin1_kernel (launches of >= THINW_MIN_BLOCKS column blocks: the
+// batched MB-MelGAN output conv, 48 -> 4 channels x 7 taps over 1.5 M columns, took 0.19 ms at
+// ~2 TB/s). thin1 splits a column's outputs over TPC threads, so each thread re-reads the
+// column's rows from LDS for its one output and every weight quad is an LDS read too: the launch
+// was bound by LDS reads (4 x 16-B reads per 8 FMAs). Here one thread sums all M outputs of its
+// column (each staged row read once per 8 k-steps, shared by the M outputs) and the weights come
+// from global memory at wave-uniform addresses, i.e. into SGPRs by scalar loads (the loop has no
+// global store before it, so the loads are provably unclobbered), free as v_fma operands.
+// Per output the same FMAs in the same order as thin1: bit-identical.
+constexpr int THINW_MIN_BLOCKS = 1024;
+template <int M>
+__global__ void __launch_bounds__(128) pwg_cnet_thinw_kernel(const CnConvArgs a, int nsrc) {
+  constexpr int NT = 128;
+  extern __shared__ __attribute__((aligned(16))) float s_x[];  // [src][cb][span][THIN_ROW]
+  const int col = threadIdx.x;
+  const int2 blk = a.blocks[blockIdx.x];
+  const int u = blk.x;
+  const int q = blk.y + col;
+  const bool live = q < a.ncols[u];
+  const int xf0 = a.src[0].nc * a.src[0].span * THIN_ROW;
+  thin_stage_rows<NT>(a, nsrc, s_x, xf0, blk, u);
+  __syncthreads();
+  float acc[M];
+#pragma unroll
+  for (int o = 0; o < M; ++o) acc[o] = 0.f;
+  for (int si = 0; si < nsrc; ++si) {
+    const CnSrc& s = a.src[si];
+    const float* const sx = s_x + (si ? xf0 : 0);
+    for (int cb = 0; cb < s.nc; ++cb) {
+      for (int k = 0; k < s.taps; ++k) {
+        const int c = s.chunk_base + k * s.nc + cb;
+        const int r = col + a.chunks[c].row_off - s.off_min;
+        const float* xr = sx + THIN_ROW * (cb * s.span + r);
+        const float* wf = a.wfrag + (size_t)c * a.mt_total * 512;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f32x4v x0 = *reinterpret_cast<const f32x4v*>(xr + 8 * h);
+          const f32x4v x1 = *reinterpret_cast<const f32x4v*>(xr + 8 * h + 4);
+#pragma unroll
+          for (int o = 0; o < M; ++o) {
+            // k-steps 8 h + [0, 8) of output o: W[o][16 cb + 8 h + i][k] (sub 0, then sub 1)
+            const f32x4v w0 = *reinterpret_cast<const f32x4v*>(wf + (o + 32 * h) * 4);
+            const f32x4v w1 = *reinterpret_cast<const f32x4v*>(wf + 256 + (o + 32 * h) * 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[o] = fmaf(w0[e], x0[e], acc[o]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[o] = fmaf(w1[e], x1[e], acc[o]);
+          }
+        }
+      }
+    }
+  }
+  if (!live) return;
+  const int t = q * a.ostride + a.ophase;
+  const int2 sd = *reinterpret_cast<const int2*>(a.seg_dst + 2 * u);
+  float* yrow = a.y + (size_t)(sd.x + t) * a.ld_dst;
+  const float* rrow = nullptr;
+  if (a.res) {
+    const int2 sr = *reinterpret_cast<const int2*>(a.seg_res + 2 * u);
+    rrow = a.res + (size_t)(sr.x + t) * a.ld_res;
+  }
+  bool bad = false;
+#pragma unroll
+  for (int o = 0; o < M; ++o) {
+    if (o >= a.M) break;
+    float v = acc[o] + a.bias[o];
+    if (rrow) v += rrow[o];
+    if (a.accumulate) v = yrow[o] + v;
+    if (a.out_div != 1.f) v = v / a.out_div;
+    if (a.post_act == PWG_ACT_LRELU) v = v > 0.f ? v : v * a.post_slope;
+    else if (a.post_act == PWG_ACT_TANH) v = tanhf(v);
+    bad |= !__builtin_isfinite(v);
+    yrow[o] = v;
+  }
+  for (int o = a.M; o < a.ld_dst; ++o) yrow[o] = 0.f;
+  if (a.range_flag) flag_range(a.range_flag, nullptr, bad, (int)(threadIdx.x & 63));
+}
+
 // PQMF synthesis (layers/pqmf.py:133-149): y[t] = sum_m sum_k h[m][k] * S * x[(t+k-P)/S][m] over
 // the k with (t+k-P) divisible by S and inside the utterance. One thread per output sample.
 struct CnPqmfArgs {
@@ -3276,8 +3362,8 @@ struct CnPqmfArgs {
 // then sums its ~NT/S taps x S bands from LDS.
 constexpr int PQ_MAX_S = 8, PQ_MAX_NT = 128, PQ_ROWS = 256 + PQ_MAX_NT;
 __global__ void __launch_bounds__(256) pwg_cnet_pqmf_kernel(const CnPqmfArgs a) {
-  __shared__ float s_x[PQ_ROWS * PQ_MAX_S];
-  __shared__ float s_h[PQ_MAX_S * PQ_MAX_NT];
+  __shared__ __attribute__((aligned(16))) float s_x[PQ_ROWS * PQ_MAX_S];
+  __shared__ __attribute__((aligned(16))) float s_h[PQ_MAX_S * PQ_MAX_NT];  // [tap][band]
   const int2 blk = a.blocks[blockIdx.x];
   const int u = blk.x;
   const int2 sd = *reinterpret_cast<const int2*>(a.seg_dst + 2 * u);
@@ -3307,8 +3393,10 @@ __global__ void __launch_bounds__(256) pwg_cnet_pqmf_kernel(const CnPqmfArgs a) 
   for (int k = 0; k < XB; ++k)
     if (threadIdx.x + 256 * k < nrow * S) s_x[threadIdx.x + 256 * k] = xv[k];
 #pragma unroll
-  for (int k = 0; k < HB; ++k)
-    if (threadIdx.x + 256 * k < S * NT) s_h[threadIdx.x + 256 * k] = hv[k];
+  for (int k = 0; k < HB; ++k) {
+    const int i = threadIdx.x + 256 * k, m = i / NT;
+    if (i < S * NT) s_h[(i - m * NT) * S + m] = hv[k];  // filter m, tap k -> [k][m]
+  }
   for (int i = threadIdx.x + 256 * XB; i < nrow * S; i += 256) {  // (not reached within the limits)
     const int r = i / S, m = i - r * S;
     const int j = j0 + r;
@@ -3319,9 +3407,21 @@ __global__ void __launch_bounds__(256) pwg_cnet_pqmf_kernel(const CnPqmfArgs a) 
   if (t >= sd.y) return;
   float acc = 0.f;
   const int r0 = ((P - t) % S + S) % S;  // first tap k with (t + k - P) % S == 0
-  for (int k = r0; k < NT; k += S) {
-    const int rr = (t + k - P) / S - j0;  // exact division
-    for (int m = 0; m < S; ++m) acc = fmaf(s_h[m * NT + k], s_x[rr * S + m], acc);
+  // row of tap r0 (exact division); each later tap (k += S) is the next row: one division per
+  // thread instead of one per tap (S is a run-time value: ~30 instructions each)
+  const int rr0 = (t + r0 - P) / S - j0;
+  if (S == 4) {  // multi-band MelGAN: a row's 4 bands and a tap's 4 filters as one 16-B LDS read each
+    const f32x4v* x4 = reinterpret_cast<const f32x4v*>(s_x) + rr0;
+    const f32x4v* h4 = reinterpret_cast<const f32x4v*>(s_h) + r0;
+    for (int k = r0; k < NT; k += 4, ++x4, h4 += 4) {
+      const f32x4v xv = *x4, hw = *h4;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) acc = fmaf(hw[m], xv[m], acc);
+    }
+  } else {
+    int rr = rr0;
+    for (int k = r0; k < NT; k += S, ++rr)
+      for (int m = 0; m < S; ++m) acc = fmaf(s_h[k * S + m], s_x[rr * S + m], acc);
   }
   a.y[(size_t)(sd.x + t) * a.ld_dst] = acc;
   if (a.range_flag) flag_range(a.range_flag, nullptr, !__builtin_isfinite(acc), (int)(threadIdx.x & 63));
@@ -3479,6 +3579,8 @@ struct PwgCnet {
                        // conv of the chain runs narrow
   int rstack = 1;      // PWG_CNET_OPT_RSTACK: batched ResidualStacks on pwg_rstack.hip, 1 weights resident in
                        // LDS where they fit (<= 64 channels), 2 always streamed (A/B); 0 the x-tile stack
+  int thinw = 1;       // PWG_CNET_OPT_THINW: thin launches (<= 8 outputs) of >= THINW_MIN_BLOCKS column blocks
+                       // on pwg_cnet_thinw_kernel (weights by scalar loads), 0 on the thin1 kernel
   int presplit = 1;    // PWG_CNET_OPT_PRESPLIT (plan time): DMA-ring launches write / read pre-split images
   int streams = 1;     // PWG_CNET_OPT_STREAMS: 0 one stream, 1 independent launches of plans with narrow
                        // launches run on auxiliary streams, 2 every plan
@@ -5143,7 +5245,16 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
             hipLaunchKernelGGL(kfn, tgrid, dim3(CN_COLS * tpc), tl1, s, a, nsrc);
             return hipGetLastError();
           };
+          const size_t tlw = tl1 - (size_t)a.n_chunks * 2 * mt_ * 8 * sizeof(float);  // rows only
+          auto gow = [&](auto kfn) -> hipError_t {
+            const hipError_t e1 = allow_lds(reinterpret_cast<const void*>(kfn), (int)tlw);
+            if (e1 != hipSuccess) return e1;
+            hipLaunchKernelGGL(kfn, tgrid, dim3(CN_COLS), tlw, s, a, nsrc);
+            return hipGetLastError();
+          };
+          const bool wide = n->thinw && mt_ > 1 && p->n_blocks[pi] >= THINW_MIN_BLOCKS;
           const hipError_t e1 = mt_ == 1 ? go(pwg_cnet_thin1_kernel<1, 1>, 1)
+                                : wide ? (mt_ == 4 ? gow(pwg_cnet_thinw_kernel<4>) : gow(pwg_cnet_thinw_kernel<8>))
                                 : mt_ == 4 ? go(pwg_cnet_thin1_kernel<4, 4>, 4) : go(pwg_cnet_thin1_kernel<8, 4>, 4);
           if (e1 != hipSuccess) return hipf(e1, "thin kernel launch");
         } else if (op.out_channels <= 1) hipLaunchKernelGGL(pwg_cnet_thin_kernel<1>, tgrid, tblock, tl, s, a, nsrc);
@@ -5421,7 +5532,7 @@ int pwg_cnet_set_option(PwgCnet* n, int option, long long value) {
               : option == PWG_CNET_OPT_XCD_ORDER  ? &n->xcd_order
               : option == PWG_CNET_OPT_NARROW_DMA ? &n->narrow_dma
               : option == PWG_CNET_OPT_PRESPLIT   ? &n->presplit
-
+              : option == PWG_CNET_OPT_THINW      ? &n->thinw
                                                   : nullptr;
   if (option == PWG_CNET_OPT_MSTACK) {
     if (value < 0 || value > 1) return fail(PWG_ERR_INVALID, "mstack must be 0 or 1");

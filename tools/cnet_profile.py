@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--nocheck", action="store_true", help="no range check / exact-fp32 rerun (diagnostic builds)")
     ap.add_argument("--bitwise-rstack", action="store_true",
                     help="first compare one forward with PWG_CNET_OPT_RSTACK 0 and 1 bit for bit")
+    ap.add_argument("--opt", action="append", default=[],
+                    help="NAME=VALUE: eng.set_NAME(VALUE) before planning (e.g. xt_dma=2, xcd_order=0)")
     ap.add_argument("--dump", default=None, help="save the first forward's output (.npy) for a bitwise A/B")
     a = ap.parse_args()
     cls, p = configs.vocoder_params(a.config)
@@ -49,6 +51,9 @@ def main():
         eng.set_rstack(a.rstack)
     if a.pair_steps:
         eng.set_pair_steps(a.pair_steps)
+    for o in a.opt:
+        k, v = o.split("=")
+        getattr(eng, "set_" + k)(int(v))
     P = eng.program
     lengths = (np.full(a.batch, a.frames) if a.frames else synthetic.libritts_lengths(a.utts, seed=3))
     frames = int(lengths.sum())
