@@ -186,15 +186,11 @@ PWG_API int pwg_cnet_plan_schedule(PwgCnetPlan* p, int cap, int* n_launches, int
  * LDS-ring kernel (weights and input rows streamed by global_load_lds two steps ahead across tiles,
  * h in registers) instead of the x-tile stack kernel; at <= 64 channels its weights stay resident in
  * LDS (only input rows stream). Bit-identical; 0 for the x-tile stack, 2 for the streamed-weight form
- * at every width (A/B).
- * PWG_CNET_OPT_THINW (default 1): a thin launch (an op with <= 8 outputs and more than one, e.g.
- * multi-band MelGAN's 4-band output conv) of at least 1024 column blocks runs one thread per column
- * with the weights read at wave-uniform addresses (scalar loads) instead of the LDS-staged,
- * threads-per-column form; 0 keeps the latter. Run-time; bit-identical. */
+ * at every width (A/B). */
 enum { PWG_CNET_OPT_SPLIT_F16 = 0, PWG_CNET_OPT_FUSE_PAIRS = 1, PWG_CNET_OPT_PAIR_STEPS = 2, PWG_CNET_OPT_XTILE = 3,
        PWG_CNET_OPT_XT_DMA = 4, PWG_CNET_OPT_XCD_ORDER = 5, PWG_CNET_OPT_NARROW = 6, PWG_CNET_OPT_NARROW_DMA = 7,
        PWG_CNET_OPT_STREAMS = 8, PWG_CNET_OPT_MSTACK = 9, PWG_CNET_OPT_PRESPLIT = 10,
-       PWG_CNET_OPT_RSTACK = 11, PWG_CNET_OPT_THINW = 12 };
+       PWG_CNET_OPT_RSTACK = 11 };
 PWG_API int pwg_cnet_set_option(PwgCnet* n, int option, long long value);
 /* Timing: 0 off, 1 HIP events around every launch (per-bucket / per-op sums), 2 one event pair
  * around each whole run on the caller's stream (its device span only; no events between launches,

@@ -629,13 +629,6 @@ class CnetEngine:
         _lib.check(self._lib.pwg_cnet_set_option(self._h, 11, int(mode)))
         self._graph_epoch += 1
 
-    def set_thinw(self, enable):
-        """pwg_cnet_set_option(PWG_CNET_OPT_THINW): thin launches (2-8 outputs) of >= 1024 column
-        blocks with one thread per column and scalar-loaded weights (default on) or, 0, on the
-        LDS-staged thin kernel. Run-time; bit-identical."""
-        _lib.check(self._lib.pwg_cnet_set_option(self._h, 12, 1 if enable else 0))
-        self._graph_epoch += 1
-
     def set_narrow_dma(self, enable):
         """pwg_cnet_set_option(PWG_CNET_OPT_NARROW_DMA): narrow launches on the DMA-ring kernel
         (default) or, 0, on the narrow x-tile / tap-major kernels. Plan-time (cached plans are

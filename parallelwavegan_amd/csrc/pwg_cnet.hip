@@ -3264,84 +3264,6 @@ __global__ void __launch_bounds__(128 * TPC) pwg_cnet_thin1_kernel(const CnConvA
   if (a.range_flag) flag_range(a.range_flag, nullptr, bad, (int)(threadIdx.x & 63));
 }
 
-// Wide-plan form of pwg_cnet_thin1_kernel (launches of >= THINW_MIN_BLOCKS column blocks: the
-// batched MB-MelGAN output conv, 48 -> 4 channels x 7 taps over 1.5 M columns, took 0.19 ms at
-// ~2 TB/s). thin1 splits a column's outputs over TPC threads, so each thread re-reads the
-// column's rows from LDS for its one output and every weight quad is an LDS read too: the launch
-// was bound by LDS reads (4 x 16-B reads per 8 FMAs). Here one thread sums all M outputs of its
-// column (each staged row read once per 8 k-steps, shared by the M outputs) and the weights come
-// from global memory at wave-uniform addresses, i.e. into SGPRs by scalar loads (the loop has no
-// global store before it, so the loads are provably unclobbered), free as v_fma operands.
-// Per output the same FMAs in the same order as thin1: bit-identical.
-constexpr int THINW_MIN_BLOCKS = 1024;
-template <int M>
-__global__ void __launch_bounds__(128) pwg_cnet_thinw_kernel(const CnConvArgs a, int nsrc) {
-  constexpr int NT = 128;
-  extern __shared__ __attribute__((aligned(16))) float s_x[];  // [src][cb][span][THIN_ROW]
-  const int col = threadIdx.x;
-  const int2 blk = a.blocks[blockIdx.x];
-  const int u = blk.x;
-  const int q = blk.y + col;
-  const bool live = q < a.ncols[u];
-  const int xf0 = a.src[0].nc * a.src[0].span * THIN_ROW;
-  thin_stage_rows<NT>(a, nsrc, s_x, xf0, blk, u);
-  __syncthreads();
-  float acc[M];
-#pragma unroll
-  for (int o = 0; o < M; ++o) acc[o] = 0.f;
-  for (int si = 0; si < nsrc; ++si) {
-    const CnSrc& s = a.src[si];
-    const float* const sx = s_x + (si ? xf0 : 0);
-    for (int cb = 0; cb < s.nc; ++cb) {
-      for (int k = 0; k < s.taps; ++k) {
-        const int c = s.chunk_base + k * s.nc + cb;
-        const int r = col + a.chunks[c].row_off - s.off_min;
-        const float* xr = sx + THIN_ROW * (cb * s.span + r);
-        const float* wf = a.wfrag + (size_t)c * a.mt_total * 512;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const f32x4v x0 = *reinterpret_cast<const f32x4v*>(xr + 8 * h);
-          const f32x4v x1 = *reinterpret_cast<const f32x4v*>(xr + 8 * h + 4);
-#pragma unroll
-          for (int o = 0; o < M; ++o) {
-            // k-steps 8 h + [0, 8) of output o: W[o][16 cb + 8 h + i][k] (sub 0, then sub 1)
-            const f32x4v w0 = *reinterpret_cast<const f32x4v*>(wf + (o + 32 * h) * 4);
-            const f32x4v w1 = *reinterpret_cast<const f32x4v*>(wf + 256 + (o + 32 * h) * 4);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) acc[o] = fmaf(w0[e], x0[e], acc[o]);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) acc[o] = fmaf(w1[e], x1[e], acc[o]);
-          }
-        }
-      }
-    }
-  }
-  if (!live) return;
-  const int t = q * a.ostride + a.ophase;
-  const int2 sd = *reinterpret_cast<const int2*>(a.seg_dst + 2 * u);
-  float* yrow = a.y + (size_t)(sd.x + t) * a.ld_dst;
-  const float* rrow = nullptr;
-  if (a.res) {
-    const int2 sr = *reinterpret_cast<const int2*>(a.seg_res + 2 * u);
-    rrow = a.res + (size_t)(sr.x + t) * a.ld_res;
-  }
-  bool bad = false;
-#pragma unroll
-  for (int o = 0; o < M; ++o) {
-    if (o >= a.M) break;
-    float v = acc[o] + a.bias[o];
-    if (rrow) v += rrow[o];
-    if (a.accumulate) v = yrow[o] + v;
-    if (a.out_div != 1.f) v = v / a.out_div;
-    if (a.post_act == PWG_ACT_LRELU) v = v > 0.f ? v : v * a.post_slope;
-    else if (a.post_act == PWG_ACT_TANH) v = tanhf(v);
-    bad |= !__builtin_isfinite(v);
-    yrow[o] = v;
-  }
-  for (int o = a.M; o < a.ld_dst; ++o) yrow[o] = 0.f;
-  if (a.range_flag) flag_range(a.range_flag, nullptr, bad, (int)(threadIdx.x & 63));
-}
-
 // PQMF synthesis (layers/pqmf.py:133-149): y[t] = sum_m sum_k h[m][k] * S * x[(t+k-P)/S][m] over
 // the k with (t+k-P) divisible by S and inside the utterance. One thread per output sample.
 struct CnPqmfArgs {
@@ -3579,8 +3501,6 @@ struct PwgCnet {
                        // conv of the chain runs narrow
   int rstack = 1;      // PWG_CNET_OPT_RSTACK: batched ResidualStacks on pwg_rstack.hip, 1 weights resident in
                        // LDS where they fit (<= 64 channels), 2 always streamed (A/B); 0 the x-tile stack
-  int thinw = 1;       // PWG_CNET_OPT_THINW: thin launches (<= 8 outputs) of >= THINW_MIN_BLOCKS column blocks
-                       // on pwg_cnet_thinw_kernel (weights by scalar loads), 0 on the thin1 kernel
   int presplit = 1;    // PWG_CNET_OPT_PRESPLIT (plan time): DMA-ring launches write / read pre-split images
   int streams = 1;     // PWG_CNET_OPT_STREAMS: 0 one stream, 1 independent launches of plans with narrow
                        // launches run on auxiliary streams, 2 every plan
@@ -5245,16 +5165,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
             hipLaunchKernelGGL(kfn, tgrid, dim3(CN_COLS * tpc), tl1, s, a, nsrc);
             return hipGetLastError();
           };
-          const size_t tlw = tl1 - (size_t)a.n_chunks * 2 * mt_ * 8 * sizeof(float);  // rows only
-          auto gow = [&](auto kfn) -> hipError_t {
-            const hipError_t e1 = allow_lds(reinterpret_cast<const void*>(kfn), (int)tlw);
-            if (e1 != hipSuccess) return e1;
-            hipLaunchKernelGGL(kfn, tgrid, dim3(CN_COLS), tlw, s, a, nsrc);
-            return hipGetLastError();
-          };
-          const bool wide = n->thinw && mt_ > 1 && p->n_blocks[pi] >= THINW_MIN_BLOCKS;
           const hipError_t e1 = mt_ == 1 ? go(pwg_cnet_thin1_kernel<1, 1>, 1)
-                                : wide ? (mt_ == 4 ? gow(pwg_cnet_thinw_kernel<4>) : gow(pwg_cnet_thinw_kernel<8>))
                                 : mt_ == 4 ? go(pwg_cnet_thin1_kernel<4, 4>, 4) : go(pwg_cnet_thin1_kernel<8, 4>, 4);
           if (e1 != hipSuccess) return hipf(e1, "thin kernel launch");
         } else if (op.out_channels <= 1) hipLaunchKernelGGL(pwg_cnet_thin_kernel<1>, tgrid, tblock, tl, s, a, nsrc);
@@ -5532,7 +5443,6 @@ int pwg_cnet_set_option(PwgCnet* n, int option, long long value) {
               : option == PWG_CNET_OPT_XCD_ORDER  ? &n->xcd_order
               : option == PWG_CNET_OPT_NARROW_DMA ? &n->narrow_dma
               : option == PWG_CNET_OPT_PRESPLIT   ? &n->presplit
-              : option == PWG_CNET_OPT_THINW      ? &n->thinw
                                                   : nullptr;
   if (option == PWG_CNET_OPT_MSTACK) {
     if (value < 0 || value > 1) return fail(PWG_ERR_INVALID, "mstack must be 0 or 1");

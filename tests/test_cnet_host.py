@@ -210,9 +210,6 @@ def test_host_only_plans_build_and_check_their_block_lists(name, built_lib):
     eng.set_rstack(0)
     eng.set_rstack(2)
     eng.set_rstack(1)
-    assert eng._lib.pwg_cnet_set_option(eng._h, 12, 2) == _lib.PWG_ERR_INVALID  # PWG_CNET_OPT_THINW: 0-1
-    eng.set_thinw(False)
-    eng.set_thinw(True)
     assert eng.plan([64]).out_rows == 64 * hop
 
 

@@ -683,34 +683,6 @@ def test_rstack_bitwise_equal_on_a_large_batch(cfg, built_lib, cuda_device):
         np.testing.assert_array_equal(c, b)
 
 
-def test_thinw_and_pqmf_bitwise_equal_on_a_large_batch(built_lib, cuda_device):
-    """PWG_CNET_OPT_THINW: multi-band MelGAN v2's 4-band output conv over a batch of >= 1024 column
-    blocks on the one-thread-per-column kernel (weights by scalar loads) against the LDS-staged
-    thin kernel: bit-identical; the PQMF synthesis after it is checked against the oracle by the
-    golden / full-length tests."""
-    from parallelwavegan_amd import configs, synthetic
-    from parallelwavegan_amd.melgan import PQMF, MelGANGenerator
-
-    _, params = configs.vocoder_params("mb_melgan_v2")
-    m = MelGANGenerator(**params)
-    m.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic.make_module_state_dict(m, seed=43).items()})
-    m.pqmf = PQMF(**configs.VOCODER_PQMF["mb_melgan_v2"])
-    m = m.to(cuda_device)
-    eng = m.engine()
-    lengths = [int(f) for f in synthetic.libritts_lengths(6, seed=7)] + [13, 9]
-    # the output conv runs at hop / subbands = 64 columns per frame, 128 columns per block
-    assert sum((f * 64 + 127) // 128 for f in lengths) >= 1024
-    mels = [synthetic.make_mel(f, 80, seed=900 + i) for i, f in enumerate(lengths)]
-    with torch.no_grad():
-        eng.set_thinw(False)
-        ref = [y.cpu().numpy() for y in m.inference_batch(mels)]
-        eng.set_thinw(True)
-        got = [y.cpu().numpy() for y in m.inference_batch(mels)]
-    for a, b in zip(got, ref):
-        assert np.isfinite(a).all()
-        np.testing.assert_array_equal(a, b)
-
-
 @pytest.mark.parametrize("cfg, frames", [("mb_melgan_v2", 64), ("melgan_v1", 48), ("mb_melgan_test", 40)])
 def test_fused_chains_and_presplit_against_oracle(cfg, frames, built_lib, cuda_device):
     """The B = 1 path's own kernels against the float64 oracle (oracle/melgan_numpy.py), not only
