@@ -475,7 +475,9 @@ constexpr int XT_ROWB = 80;  // bytes per staged input row: 16 hi + 16 lo halves
 // before the first store: the stores may alias the later loads for the compiler, which otherwise
 // serialises one load round trip per 4 rows (MT x 4 of them, ~1 us each at B = 1).
 // IMG: also the pre-split images a.oimg (narrow launches only: the wide kernels keep their epilogue)
-template <int MT, bool IMG = false>
+// GM: m-tiles per load group (3 x 4 quads each in flight); 1 in kernels held to 128 VGPRs (the
+// DMA-staged and synchronous x-tile kernels: at MT 2 a group of 2 spilled 42-55 VGPRs to scratch)
+template <int MT, bool IMG = false, int GM = (MT <= 2 ? MT : 1)>
 __device__ __forceinline__ void cn_store_col(const CnConvArgs& a, const f32x16 (&acc)[MT], const float* bias_, int m0,
                                              int hh, float* yrow, const float* rrow, long long irow = 0) {
   auto finish = [&](f32x4v v) {
@@ -493,7 +495,6 @@ __device__ __forceinline__ void cn_store_col(const CnConvArgs& a, const f32x16 (
     return v;
   };
   if ((a.ld_dst & 3) == 0) {
-    constexpr int GM = MT <= 2 ? MT : 1;  // m-tiles per load group (register budget at MT 3-4)
 #pragma unroll
     for (int mg = 0; mg < MT; mg += GM) {
       f32x4v bv[GM][4], rv[GM][4], yv[GM][4];
@@ -925,7 +926,7 @@ pwg_cnet_xtile_kernel(const CnConvArgs a, const CnXtileArgs xt) {
     const int t = qb * a.ostride + ophase_;
     float* yrow = a.y + (size_t)(sd.x + t) * a.ld_dst;
     const float* rrow = a.res ? a.res + (size_t)(sr.x + t) * a.ld_res : nullptr;
-    cn_store_col<MT, DB && NWV < 8>(a, acc[nc], bias_, m0, hh, yrow, rrow, (long long)(sd.x + t));
+    cn_store_col<MT, DB && NWV < 8, (DB || SY || MT > 2 ? 1 : MT)>(a, acc[nc], bias_, m0, hh, yrow, rrow, (long long)(sd.x + t));
   }
 }
 
@@ -973,9 +974,7 @@ hipError_t xtile_launch_db(int k, int ks, dim3 grid, int lds, hipStream_t s, con
                            const CnXtileArgs& xt) {
   if (ks == k) {
     switch (k) {
-      case 2:  // ConvTranspose phases (3 or 4 m-tiles)
-        if constexpr (MT >= 3) return xtile_launch_db_ks<MT, 2, 2>(grid, lds, s, a, xt);
-        return hipErrorInvalidValue;
+      case 2: return xtile_launch_db_ks<MT, 2, 2>(grid, lds, s, a, xt);  // ConvTranspose phases
       case 3: return xtile_launch_db_ks<MT, 3, 3>(grid, lds, s, a, xt);
       case 5: return xtile_launch_db_ks<MT, 5, 5>(grid, lds, s, a, xt);
       case 7: return xtile_launch_db_ks<MT, 7, 7>(grid, lds, s, a, xt);
@@ -3942,6 +3941,16 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
         // one 16-channel block per staging step (2 or 4 measured 1 % slower, r02_xt5)
         const int span = XT_COLS + (xk - 1) * xd;
         ph.xt_lds = xk * MT * 2048 + span * XT_ROWB;
+        // ConvTranspose phases of 2 m-tiles: the DMA-staged form (128 VGPRs, two workgroups per CU)
+        // on the measured rule (CNET_DMA_RULE): MB-MelGAN v2's 96 -> 48 0.376 -> 0.296 ms, HiFiGAN
+        // v1's 128 -> 64 0.869 -> 0.695 ms; at 1 m-tile it lost (HiFiGAN 64 -> 32 0.576 -> 0.601 ms;
+        // profiles/r06_ab/ct_*)
+        if (convt) {
+          ph.xt_db = true;
+          ph.xt_db_pick = MT == 2;
+          ph.xt_db_ks[0] = ph.xt_db_ks[1] = 2;
+          ph.xt_db_lds[0] = ph.xt_db_lds[1] = 2 * 2 * MT * 2048 + span * XT_ROWB;
+        }
       } else if (convt && nsrc == 1 && (MT == 3 || MT == 4) && mt_total % MT == 0 && op.src[0].channels % 16 == 0) {
         ph.xt_convt_db = true;  // 2 taps: both tap groups' A (2 x MT x 4 KB) + 257 input rows, <= 53 KB
         ph.xt_db = ph.xt_db_pick = true;
