@@ -576,8 +576,9 @@ def test_fused_stack_chain_bitwise_equal(cfg, built_lib, cuda_device):
     block of output columns, the input tile +- the summed dilations in LDS (reflect-padded edges
     inside the tile), h in registers. Same products, order, splits and epilogues as the two launches
     per stack: bit-identical to mstack off, at B = 1 (short utterances: every block touches an edge;
-    T' = 64 and 131) and on a forced ragged batch; the chains ran fused (their inner ops record no
-    launch)."""
+    T' = 64 and 131) and on a forced ragged batch, also on one stream (workspace slots reused across
+    buffers, the chain's input kept live through the fused launch); the chains ran fused (their
+    inner ops record no launch)."""
     from parallelwavegan_amd import configs, synthetic
     from parallelwavegan_amd.melgan import PQMF, MelGANGenerator
 
@@ -602,9 +603,15 @@ def test_fused_stack_chain_bitwise_equal(cfg, built_lib, cuda_device):
             outs[mode] += [y.cpu().numpy() for y in m.inference_batch(batch)]
             if mode == 1:
                 fused = sum(1 for name, _, n in t if n == 0 and "stack" in name)
+        # one stream: the plan's workspace slots are reused across buffers (assign_slots(true)), so
+        # a chain's input and its output must not share a slot while the fused launch reads halos
         eng.set_mstack(1)
+        eng.set_streams(0)
+        outs["s0"] = [m.inference(torch.from_numpy(x).to(cuda_device)).cpu().numpy() for x in singles]
+        outs["s0"] += [y.cpu().numpy() for y in m.inference_batch(batch)]
+        eng.set_streams(1)
     assert fused > 0
-    for mode in (1,):
+    for mode in (1, "s0"):
         for a, b in zip(outs[mode], outs[0]):
             assert np.isfinite(a).all()
             np.testing.assert_array_equal(a, b)
