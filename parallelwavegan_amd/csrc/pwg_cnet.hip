@@ -56,6 +56,10 @@ constexpr int CN_NARROW_G = 4;             // ... in narrow tap-major launches (
 constexpr int CNET_NW8_MT = 4;             // conv ops with MT >= this run 8-wave workgroups (256 columns)
 constexpr int CNET_XTILE_LDS = 150 * 1024; // LDS budget of one x-tile workgroup
 constexpr int CNET_XPAIR_MAXK = 11;        // largest kernel size fused into an x-tile pair
+// x-tile ConvTranspose phases launched together too (A/B: -DCNET_CT_ZMERGE=0)
+#ifndef CNET_CT_ZMERGE
+#define CNET_CT_ZMERGE 1
+#endif
 constexpr int CNET_XTILE_CONVT = 2;        // ConvTranspose phases of <= this many m-tiles on the x-tile
                                            // kernel: faster up to 64 output channels, slower at 128-256
                                            // (stride 8; profiles/r02_ct)
@@ -4015,7 +4019,7 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
     const PwgCnetOp& op = n->ops[ph.op];
     if (op.kind != PWG_CNET_CONVT || ph.phase != 0) continue;
     const int s2 = op.stride;
-    bool ok = s2 <= 8 && i + s2 <= n->phases.size() && !ph.thin && !ph.xtile;
+    bool ok = s2 <= 8 && i + s2 <= n->phases.size() && !ph.thin && (!ph.xtile || CNET_CT_ZMERGE);
     for (int r = 1; ok && r < s2; ++r) {
       const OpPhase& q = n->phases[i + r];
       ok = q.op == ph.op && q.phase == r && q.MT == ph.MT && q.NW == ph.NW && !q.thin &&
