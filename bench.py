@@ -19,7 +19,6 @@ Prints ONE JSON line (rank 0) with the contract fields plus "roofline" and "cpu_
 """
 
 import argparse
-import gc
 import json
 import os
 import subprocess
@@ -540,7 +539,6 @@ def vocoder_latency_rows(m, dev, reps=10):
             for B in (1, 16):
                 mels = [torch.from_numpy(synthetic.make_mel(F, 80, seed=30 + b)).to(dev) for b in range(B)]
                 call = (lambda: m.inference(mels[0])) if B == 1 else (lambda: m.inference_batch(mels))
-                gc.collect()  # the bench's own garbage is not the engine's first-call cost
                 first = timed(call)
                 for _ in range(2):
                     call()
@@ -870,7 +868,6 @@ def latency_rows(dev, reps=20):
                 else:
                     call = lambda: m.inference_batch(mels, noises)  # noqa: E731
                     call_host = lambda: [y.cpu() for y in m.inference_batch(mels_h, noises_h)]  # noqa: E731
-                gc.collect()  # the bench's own garbage is not the engine's first-call cost
                 first = timed(call)
                 for _ in range(3):
                     call()
