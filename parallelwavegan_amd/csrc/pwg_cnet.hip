@@ -3480,6 +3480,7 @@ struct OpPhase {          // one launch
   int xstack_g2 = 0;          // its stage-2 chunks per staged group
   int xstack_xoff = 0;        // its input-row / h-tile region offset
   int rstack_cs = 0;          // > 0: the stack also fits pwg_rstack.hip (16-channel blocks; PWG_CNET_OPT_RSTACK)
+  int r1x1_mt = 0;            // > 0: a two-source 1x1 of 32 r1x1_mt outputs that pwg_r1x1_kernel runs alone
   int ms_n = 0;               // > 0: head of a chain of this many fusable ResidualStacks (pwg_mstack.hip)
   int ms_halo = 0;            // ... their summed dilations
 };
@@ -4154,6 +4155,33 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
       if (rs) pa.rstack_cs = cs;
     }
   }
+  // Two-source 1x1s run alone (MelGAN stacks too wide for the fused kernels: 128 / 192 / 256
+  // channels) on pwg_r1x1_kernel (PWG_CNET_OPT_RSTACK): [source 0 chunks][source 1 chunks] in the
+  // executor's order, each source 16-channel blocks of rows at the op's own rate, y rows of exactly
+  // the op's channels, no epilogue extras, LeakyReLU slopes in [0, 1]
+  for (size_t i = 0; i < n->phases.size(); ++i) {
+    OpPhase& ph = n->phases[i];
+    const PwgCnetOp& op = n->ops[ph.op];
+    if (op.kind != PWG_CNET_CONV || ph.thin || ph.z_phases != 1 || op.src[1].buf < 0) continue;
+    if (i > 0 && n->phases[i - 1].stack_b == (int)i) continue;
+    const PwgCnetSrc& s0 = op.src[0];
+    const PwgCnetSrc& s1 = op.src[1];
+    const int mt = ph.mt_total;
+    bool ok = r1x1_supported(mt) && op.out_channels == 32 * mt && n->ld[op.dst] == op.out_channels &&
+              op.res < 0 && !op.accumulate && op.out_div == 1.f && op.post_act == PWG_ACT_NONE &&
+              op.dst != n_bufs - 1 && ph.ostride == 1 && ph.ophase == 0;
+    for (const PwgCnetSrc* sp : {&s0, &s1})
+      ok = ok && sp->taps == 1 && sp->pad == 0 && !sp->normalize && sp->channels % 16 == 0 &&
+           n->ld[sp->buf] % 4 == 0 && n->ld[sp->buf] >= sp->channels && sp->pre_slope >= 0.f && sp->pre_slope <= 1.f &&
+           n->rate[sp->buf] == n->rate[op.dst];
+    const int n0 = s0.channels / 16, n1 = s1.channels / 16;
+    ok = ok && (int)ph.chunks.size() == n0 + n1;
+    for (int c = 0; ok && c < n0 + n1; ++c) {
+      const ChunkDesc& cd = ph.chunks[c];
+      ok = cd.src == (c < n0 ? 0 : 1) && cd.row_off == 0 && cd.c0 == 16 * (c < n0 ? c : c - n0);
+    }
+    if (ok) ph.r1x1_mt = mt;
+  }
   // x-tile conv pairs (pwg_cnet_xpair_kernel): both convs on the x-tile kernel, 32 or 64 channels
   // (128 at k = 3) in one row tile, conv 1 single-source zero-padded with no epilogue extras, conv 2 the only
   // reader of its output, same kernel size, dilation 1 and taps within +-16 columns.
@@ -4540,7 +4568,7 @@ int pwg_cnet_plan_create(PwgCnet* n, int n_utts, const long long* frames, PwgCne
       p->o_strips.push_back(-1);
       p->n_strips.push_back(0);
     }
-    if (ph.xpair_b >= 0 || (ph.stack_b >= 0 && ph.xtile) || ph.xt_convt_db) {
+    if (ph.xpair_b >= 0 || (ph.stack_b >= 0 && ph.xtile) || ph.xt_convt_db || ph.r1x1_mt > 0) {
       const int step = ph.xpair_b >= 0 ? XP_OUT : XT_COLS;
       p->o_xblocks.push_back(list(CN_L_BLK, rate, os, oph, step));
       p->n_xblocks.push_back((int)count(step));
@@ -5310,6 +5338,19 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         else if (mtn == 1) hipLaunchKernelGGL((pwg_cnet_conv_kernel<1, 1, CN_NARROW_G, true, 2>), ngrid, dim3(128), 0, s, a);
         else if (nw == 1) hipLaunchKernelGGL((pwg_cnet_conv_kernel<2, 1, CN_NARROW_G, true, 1>), ngrid, dim3(64), 0, s, a);
         else hipLaunchKernelGGL((pwg_cnet_conv_kernel<2, 1, CN_NARROW_G, true, 2>), ngrid, dim3(128), 0, s, a);
+      } else if (split && n->rstack && ph.r1x1_mt > 0 && p->n_xblocks[pi] > 0) {
+        R1x1Args r;
+        for (int si = 0; si < 2; ++si) {
+          const PwgCnetSrc& src = op.src[si];
+          r.src[si] = bufs[src.buf]; r.seg[si] = seg_of(src.buf); r.ld[si] = n->ld[src.buf]; r.slope[si] = src.pre_slope;
+        }
+        r.nch0 = op.src[0].channels / 16; r.nch = r.nch0 + op.src[1].channels / 16;
+        r.w = packed + ph.frag16_off; r.bias = packed + ph.bias_off;
+        r.y = bufs[op.dst]; r.seg_y = seg_of(op.dst);
+        r.blocks = i2(p->o_xblocks[pi]); r.ncols = i1(p->o_ncols[pi]); r.n_blocks = p->n_xblocks[pi];
+        const int n_wg = std::max(std::min(r.n_blocks, std::max(p->n_cu, 1)), (r.n_blocks + RS_MAX_TILES - 1) / RS_MAX_TILES);
+        const hipError_t ea2 = launch_r1x1(r, ph.r1x1_mt, n_wg, s);
+        if (ea2 != hipSuccess) return hipf(ea2, "r1x1 kernel launch");
       } else if (split) {
         switch (ph.MT) {
           case 1:

@@ -362,6 +362,25 @@ struct RstackArgs {
   const int* ncols;               // output columns per utterance
   int n_blocks;
 };
+// A two-source 1x1 op (MelGAN's stack 1x1 + skip_layer over [lrelu(h); x]) on its own, 32 MT
+// output channels, the executor's chunk order [source 0 blocks][source 1 blocks]
+// (pwg_r1x1_kernel, pwg_rstack.hip)
+struct R1x1Args {
+  const float* src[2];            // [rows][ld]
+  const int* seg[2];              // [n_utts][2] (first row, rows)
+  int ld[2];                      // row strides (floats, multiples of 4)
+  float slope[2];                 // each source's LeakyReLU slope (1: none)
+  int nch0, nch;                  // 16-channel chunks of source 0, of both
+  const float* w;                 // split-f16 fragments [chunk][MT][hi/lo][lane][4]
+  const float* bias;              // (32 MT)
+  float* y;                       // [rows][32 MT] (no residual, accumulate, division or activation)
+  const int* seg_y;
+  const int2* blocks;             // (utterance, q0) of each 256-column tile
+  const int* ncols;
+  int n_blocks;
+};
+bool r1x1_supported(int mt);
+hipError_t launch_r1x1(const R1x1Args& a, int mt, int n_wg, hipStream_t s);
 bool rstack_supported(int cs);
 int rstack_lds(int cs);
 // resident: the weight-resident form where the fragments fit the LDS (<= 64 channels), else streamed
