@@ -185,8 +185,10 @@ PWG_API int pwg_cnet_plan_schedule(PwgCnetPlan* p, int cap, int* n_launches, int
  * ResidualStack with 32-96 channels (16-channel multiples, no epilogue extras) runs the persistent
  * LDS-ring kernel (weights and input rows streamed by global_load_lds two steps ahead across tiles,
  * h in registers) instead of the x-tile stack kernel; at <= 64 channels its weights stay resident in
- * LDS (only input rows stream). Bit-identical; 0 for the x-tile stack, 2 for the streamed-weight form
- * at every width (A/B). */
+ * LDS (only input rows stream). The two-source 1x1 of stacks too wide for it (128-256 channels)
+ * runs alone on the same kind of persistent ring kernel (two 16-channel chunks per step where both
+ * sources allow it). Bit-identical; 0 for the x-tile stack and the tap-major 1x1, 2 for the
+ * streamed-weight form at every width and one chunk per 1x1 step (A/B). */
 enum { PWG_CNET_OPT_SPLIT_F16 = 0, PWG_CNET_OPT_FUSE_PAIRS = 1, PWG_CNET_OPT_PAIR_STEPS = 2, PWG_CNET_OPT_XTILE = 3,
        PWG_CNET_OPT_XT_DMA = 4, PWG_CNET_OPT_XCD_ORDER = 5, PWG_CNET_OPT_NARROW = 6, PWG_CNET_OPT_NARROW_DMA = 7,
        PWG_CNET_OPT_STREAMS = 8, PWG_CNET_OPT_MSTACK = 9, PWG_CNET_OPT_PRESPLIT = 10,

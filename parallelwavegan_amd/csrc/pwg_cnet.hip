@@ -5349,7 +5349,7 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
         r.y = bufs[op.dst]; r.seg_y = seg_of(op.dst);
         r.blocks = i2(p->o_xblocks[pi]); r.ncols = i1(p->o_ncols[pi]); r.n_blocks = p->n_xblocks[pi];
         const int n_wg = std::max(std::min(r.n_blocks, std::max(p->n_cu, 1)), (r.n_blocks + RS_MAX_TILES - 1) / RS_MAX_TILES);
-        const hipError_t ea2 = launch_r1x1(r, ph.r1x1_mt, n_wg, s);
+        const hipError_t ea2 = launch_r1x1(r, ph.r1x1_mt, n_wg, s, n->rstack == 1);
         if (ea2 != hipSuccess) return hipf(ea2, "r1x1 kernel launch");
       } else if (split) {
         switch (ph.MT) {

@@ -380,7 +380,8 @@ struct R1x1Args {
   int n_blocks;
 };
 bool r1x1_supported(int mt);
-hipError_t launch_r1x1(const R1x1Args& a, int mt, int n_wg, hipStream_t s);
+// pairs: two chunks per step where both sources allow it (PWG_CNET_OPT_RSTACK 1), else one
+hipError_t launch_r1x1(const R1x1Args& a, int mt, int n_wg, hipStream_t s, bool pairs);
 bool rstack_supported(int cs);
 int rstack_lds(int cs);
 // resident: the weight-resident form where the fragments fit the LDS (<= 64 channels), else streamed

@@ -1135,6 +1135,184 @@ __global__ void __launch_bounds__(RS_NTH) pwg_r1x1_kernel(const R1x1Args a) {
   rs_vm_wait<0>();
 }
 
+// Two chunks per step (both sources with an even chunk count): a row copy then moves 8 rows x 128 B
+// (32 channels, a whole cache line of each row) instead of 16 rows x 64 B; 2 slots of 2 chunks'
+// fragments + 32 KB of rows, the next step's copies issued after the barrier that opens a step.
+// Same chunk order and arithmetic: bit-identical to the one-chunk form.
+template <int MT>
+struct R2Shape {
+  static constexpr int NF = 4 * MT;             // 1-KB fragment copies (2 chunks)
+  static constexpr int NR = RS_COLS * 128 / 1024;  // 1-KB row copies (32)
+  static constexpr int N = NF + NR;
+  static constexpr int SLOT = N * 1024;
+  static constexpr int D = (N + RS_NWV - 1) / RS_NWV;
+  static constexpr int NST = MT * 4;
+  static constexpr int LDS = 2 * SLOT + 32 * MT * 4 + RS_MAX_TILES * RS_TD * 4;
+};
+
+template <int MT>
+__global__ void __launch_bounds__(RS_NTH) pwg_r1x1w_kernel(const R1x1Args a) {
+  using S = R2Shape<MT>;
+  constexpr int C = 32 * MT, D = S::D;
+  typedef __attribute__((address_space(1))) void* gptr_t;
+  typedef __attribute__((address_space(3))) void* lptr_t;
+  extern __shared__ __attribute__((aligned(16))) unsigned char rs_smem[];
+  unsigned char* const ring = rs_smem;
+  float* const sbias = reinterpret_cast<float*>(rs_smem + 2 * S::SLOT);
+  int* const stile = reinterpret_cast<int*>(sbias + C);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int hh = lane >> 5, cl = lane & 31;
+  auto slot_of = [&](int s) {
+    unsigned o = (unsigned)__builtin_amdgcn_readfirstlane(s & 1) * (unsigned)S::SLOT;
+    asm volatile("" : "+s"(o));
+    return ring + o;
+  };
+  const int g = blockIdx.x, ng = gridDim.x;
+  const int t_begin = (int)(((long long)a.n_blocks * g) / ng);
+  const int nt = (int)(((long long)a.n_blocks * (g + 1)) / ng) - t_begin;
+  if (nt <= 0) return;
+  for (int i = threadIdx.x; i < C; i += RS_NTH) sbias[i] = a.bias[i];
+  for (int k = threadIdx.x; k < nt; k += RS_NTH) {
+    const int2 b = a.blocks[t_begin + k];
+    const int2 s0 = *reinterpret_cast<const int2*>(a.seg[0] + 2 * b.x);
+    const int2 s1 = *reinterpret_cast<const int2*>(a.seg[1] + 2 * b.x);
+    const int2 sy = *reinterpret_cast<const int2*>(a.seg_y + 2 * b.x);
+    int* const td = stile + RS_TD * k;
+    td[0] = b.y;
+    td[1] = s0.x;
+    td[2] = s1.x;
+    td[3] = sy.x;
+    td[4] = a.ncols[b.x];
+  }
+  __syncthreads();
+
+  const int nst = a.nch / 2, nst0 = a.nch0 / 2;  // steps per tile, steps of source 0
+  const int n_steps = nt * nst;
+  // step s = chunk pair j (chunks 2j, 2j + 1) of tile k: both chunks' fragments, then 32 channels
+  // of the tile's 256 rows, piece q of row r at position q ^ (r & 7)
+  auto issue = [&](int s, int k, int j) {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const float* w = a.w;
+    const float* x0 = a.src[0];
+    const float* x1 = a.src[1];
+    asm volatile("" : "+s"(w), "+s"(x0), "+s"(x1));
+    unsigned char* const slot = slot_of(s);
+    const int* const td = stile + RS_TD * k;
+    const int q0 = td[0], n = td[4];
+    const bool second = j >= nst0;
+    const float* const xs = second ? x1 : x0;
+    const int r0 = second ? td[2] : td[1];
+    const int ld = second ? a.ld[1] : a.ld[0];
+    const int cb = 2 * (second ? j - nst0 : j);
+#pragma unroll
+    for (int kk = 0; kk < D; ++kk) {
+      const int i = min(wave + RS_NWV * kk, S::N - 1);
+      const float* src;
+      if (i < S::NF) {
+        src = w + (2 * j * MT) * 512 + i * 256 + ln * 4;
+      } else {
+        const int row = 8 * (i - S::NF) + (ln >> 3);
+        const int q = (ln & 7) ^ (row & 7);
+        const int p = min(q0 + row, n - 1);
+        src = xs + (size_t)(r0 + p) * ld + 16 * cb + 4 * q;
+      }
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(slot + i * 1024), 16, 0, 0);
+    }
+  };
+  auto barrier = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  rs_f32x16 acc[MT];
+  const int col = 32 * wave + cl;
+  auto epilogue = [&](int k) {
+    const int* const td = stile + RS_TD * k;
+    const int q0 = td[0], ry = td[3], nq = td[4];
+    const int live = min(max(nq - q0, 0), RS_COLS);
+    const unsigned long long base = reinterpret_cast<unsigned long long>(a.y + ((size_t)ry + q0) * C);
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)base);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(base >> 32));
+    const int nbytes = __builtin_amdgcn_readfirstlane(live * C * 4);
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(((unsigned long long)hi << 32) | lo), (short)0, nbytes, 0x00020000);
+    const int voff = col * C * 4;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int j4 = 0; j4 < 4; ++j4) {
+        const int row = 32 * m + 8 * j4 + 4 * hh;
+        rs_f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[m][4 * j4 + e] + sbias[row + e];
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(rs_u32x4, v), rsrc, voff + row * 4, 0, 0);
+      }
+  };
+
+  issue(0, 0, 0);
+  int s = 0;
+  for (int k = 0; k < nt; ++k) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[m][e] = 0.f;
+    for (int j = 0; j < nst; ++j, ++s) {
+      // newer than step s's copies (issued at the start of step s - 1): the epilogue stores of the
+      // tile before when step s - 1 was its last
+      if (j == 0 && k > 0) rs_vm_wait<S::NST>();
+      else rs_vm_wait<0>();
+      barrier();
+      if (s + 1 < n_steps) {
+        if (j + 1 < nst) issue(s + 1, k, j + 1);
+        else issue(s + 1, k + 1, 0);
+      }
+      const unsigned char* const slot = slot_of(s);
+      const unsigned char* const rows = slot + S::NF * 1024;
+      const float slope = j >= nst0 ? a.slope[1] : a.slope[0];
+      const int sw = col & 7;
+#pragma unroll
+      for (int gc = 0; gc < 2; ++gc) {
+        const int q = 4 * gc + 2 * hh;
+        const rs_f32x4 v0 = *reinterpret_cast<const rs_f32x4*>(rows + (size_t)col * 128 + 16 * (q ^ sw));
+        const rs_f32x4 v1 = *reinterpret_cast<const rs_f32x4*>(rows + (size_t)col * 128 + 16 * ((q + 1) ^ sw));
+        rs_f32x8 x = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+        if (slope != 1.f) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) x[e] = rs_lrelu(x[e], slope);
+        }
+        rs_u32x4 bh, bl;
+        rs_split8(x, bh, bl);
+        const rs_u32x4* const sa = reinterpret_cast<const rs_u32x4*>(slot + gc * (2 * MT) * 1024) + lane;
+        rs_u32x4 ah[2], al[2];
+        ah[0] = sa[0];
+        al[0] = sa[64];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          if (m + 1 < MT) {
+            ah[(m + 1) & 1] = sa[((m + 1) * 2) * 64];
+            al[(m + 1) & 1] = sa[((m + 1) * 2 + 1) * 64];
+          }
+          asm volatile("" ::: "memory");
+          acc[m] = rs_mma3(ah[m & 1], al[m & 1], bh, bl, acc[m]);
+          asm volatile("" ::: "memory");
+        }
+      }
+    }
+    epilogue(k);
+  }
+  rs_vm_wait<0>();
+}
+
+template <int MT>
+hipError_t r2_go(const R1x1Args& a, int n_wg, hipStream_t s) {
+  const int lds = R2Shape<MT>::LDS;
+  const hipError_t e = allow_lds(reinterpret_cast<const void*>(pwg_r1x1w_kernel<MT>), lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((pwg_r1x1w_kernel<MT>), dim3((unsigned)n_wg), dim3(RS_NTH), (size_t)lds, s, a);
+  return hipGetLastError();
+}
+
 template <int MT>
 hipError_t r1_go(const R1x1Args& a, int n_wg, hipStream_t s) {
   const int lds = R1Shape<MT>::LDS;
@@ -1229,15 +1407,17 @@ hipError_t launch_rstack_impl(const RstackArgs& a, int cs, int n_wg, hipStream_t
 
 bool r1x1_supported(int mt) { return mt == 4 || mt == 6 || mt == 8; }
 
-hipError_t launch_r1x1(const R1x1Args& a, int mt, int n_wg, hipStream_t s) {
+hipError_t launch_r1x1(const R1x1Args& a, int mt, int n_wg, hipStream_t s, bool pairs) {
   if (!r1x1_supported(mt) || a.n_blocks < 1 || n_wg < 1 || a.nch < 2 || a.nch0 < 1 || a.nch0 >= a.nch ||
       (a.n_blocks + n_wg - 1) / n_wg > RS_MAX_TILES || (a.ld[0] & 3) || (a.ld[1] & 3))
     return hipErrorInvalidValue;
+  // two chunks per step when both sources have an even chunk count
+  pairs = pairs && a.nch0 % 2 == 0 && (a.nch - a.nch0) % 2 == 0;
   hipError_t e = hipErrorInvalidValue;
   switch (mt) {
-    case 4: e = r1_go<4>(a, n_wg, s); break;
-    case 6: e = r1_go<6>(a, n_wg, s); break;
-    case 8: e = r1_go<8>(a, n_wg, s); break;
+    case 4: e = pairs ? r2_go<4>(a, n_wg, s) : r1_go<4>(a, n_wg, s); break;
+    case 6: e = pairs ? r2_go<6>(a, n_wg, s) : r1_go<6>(a, n_wg, s); break;
+    case 8: e = pairs ? r2_go<8>(a, n_wg, s) : r1_go<8>(a, n_wg, s); break;
   }
   if (e == hipSuccess) g_rs_launches.fetch_add(1, std::memory_order_relaxed);
   return e;
