@@ -3481,6 +3481,7 @@ struct OpPhase {          // one launch
   int xstack_xoff = 0;        // its input-row / h-tile region offset
   int rstack_cs = 0;          // > 0: the stack also fits pwg_rstack.hip (16-channel blocks; PWG_CNET_OPT_RSTACK)
   int r1x1_mt = 0;            // > 0: a two-source 1x1 of 32 r1x1_mt outputs that pwg_r1x1_kernel runs alone
+  int rconv_mt = 0;           // > 0: a k = 3 x-tile conv of 32 rconv_mt channels that pwg_rconv_kernel runs
   int ms_n = 0;               // > 0: head of a chain of this many fusable ResidualStacks (pwg_mstack.hip)
   int ms_halo = 0;            // ... their summed dilations
 };
@@ -4181,6 +4182,30 @@ int pwg_cnet_create(const PwgCnetOp* ops, int n_ops, int n_bufs, const int* chan
       ok = cd.src == (c < n0 ? 0 : 1) && cd.row_off == 0 && cd.c0 == 16 * (c < n0 ? c : c - n0);
     }
     if (ok) ph.r1x1_mt = mt;
+  }
+  // k = 3 convs of wide stacks on pwg_rconv_kernel (PWG_CNET_OPT_RSTACK): single source, C in = C
+  // out = 32 mt, x rows of >= C floats (multiple of 4), y rows of exactly C, taps within the row window
+  for (size_t i = 0; i < n->phases.size(); ++i) {
+    OpPhase& ph = n->phases[i];
+    const PwgCnetOp& op = n->ops[ph.op];
+    if (op.kind != PWG_CNET_CONV || !ph.xtile || ph.thin || ph.z_phases != 1 || op.src[1].buf >= 0) continue;
+    if (ph.stack_b >= 0 || ph.xpair_b >= 0 || (i > 0 && n->phases[i - 1].xpair_b == (int)i)) continue;
+    const PwgCnetSrc& x = op.src[0];
+    const int mt = ph.mt_total;
+    const bool ok = r1x1_supported(mt) && op.out_channels == 32 * mt && x.channels == op.out_channels &&
+                    n->ld[op.dst] == op.out_channels && n->ld[x.buf] % 4 == 0 && n->ld[x.buf] >= x.channels &&
+                    x.taps == 3 && x.dilation >= 1 && 2 * x.dilation <= RS_MAX_REACH && x.pad >= 0 &&
+                    x.pad <= 2 * x.dilation && !x.normalize && x.pre_slope >= 0.f && x.pre_slope <= 1.f &&
+                    op.res < 0 && !op.accumulate && op.out_div == 1.f && op.post_act == PWG_ACT_NONE &&
+                    op.dst != n_bufs - 1 && ph.ostride == 1 && ph.ophase == 0 && n->rate[x.buf] == n->rate[op.dst];
+    bool canon = ok && (int)ph.chunks.size() == 3 * mt * 2;
+    // chunk order tap-major over blocks: (k, cb) -> k cs + cb, row offset -pad + k dil
+    for (int c = 0; canon && c < (int)ph.chunks.size(); ++c) {
+      const ChunkDesc& cd = ph.chunks[c];
+      const int k = c / (2 * mt), cb = c % (2 * mt);
+      canon = cd.src == 0 && cd.c0 == 16 * cb && cd.row_off == -x.pad + k * x.dilation;
+    }
+    if (canon) ph.rconv_mt = mt;
   }
   // x-tile conv pairs (pwg_cnet_xpair_kernel): both convs on the x-tile kernel, 32 or 64 channels
   // (128 at k = 3) in one row tile, conv 1 single-source zero-padded with no epilogue extras, conv 2 the only
@@ -5290,6 +5315,16 @@ int pwg_cnet_run(PwgCnetPlan* p, const float* packed, const float* mel, const fl
             ea2 = xtile_launch_narrow(mtn, nw, xt.K, pre, ngrid, p->nar_lds[pi], s, a, xt);
             a.n_oimg = 0;
           }
+        } else if (n->rstack && ph.rconv_mt > 0 && !a.src[0].normalize) {
+          RstackArgs r;
+          r.x = a.src[0].x; r.seg_x = a.src[0].seg; r.ld_x = a.src[0].ld; r.mode_x = a.src[0].pad_mode;
+          r.dil = xt.dil; r.off = xt.off_min; r.slope1 = a.src[0].slope;
+          r.mode_2 = 0; r.slope2 = 1.f; r.slope_h = 1.f;
+          r.wA = packed + ph.frag16_off; r.bA = packed + ph.bias_off; r.wB = nullptr; r.bB = nullptr;
+          r.y = bufs[op.dst]; r.seg_y = seg_of(op.dst);
+          r.blocks = a.blocks; r.ncols = a.ncols; r.n_blocks = (int)grid.x;
+          const int n_wg = std::max(std::min(r.n_blocks, std::max(p->n_cu, 1)), (r.n_blocks + RS_MAX_TILES - 1) / RS_MAX_TILES);
+          ea2 = launch_rconv(r, ph.rconv_mt, n_wg, s);
         } else {
           const bool db = ph.xt_convt_db ||
                           (ph.xt_db && ((n->xt_dma & CNET_DMA_ALL) || ((n->xt_dma & CNET_DMA_RULE) && ph.xt_db_pick)));

@@ -382,6 +382,9 @@ struct R1x1Args {
 bool r1x1_supported(int mt);
 // pairs: two chunks per step where both sources allow it (PWG_CNET_OPT_RSTACK 1), else one
 hipError_t launch_r1x1(const R1x1Args& a, int mt, int n_wg, hipStream_t s, bool pairs);
+// a wide stack's k = 3 conv alone (pwg_rconv_kernel, 32 mt channels in and out, y = W lrelu(x) + b
+// with RstackArgs' conv-A fields; mt as r1x1_supported)
+hipError_t launch_rconv(const RstackArgs& a, int mt, int n_wg, hipStream_t s);
 bool rstack_supported(int cs);
 int rstack_lds(int cs);
 // resident: the weight-resident form where the fragments fit the LDS (<= 64 channels), else streamed

@@ -1313,6 +1313,199 @@ hipError_t r2_go(const R1x1Args& a, int n_wg, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------------
+// A wide stack's k = 3 conv alone (pwg_rconv_kernel<MT>, 32 MT channels in and out: MB-MelGAN v2's
+// 192-channel stacks, MelGAN v1's 128 / 256): h = W_A lrelu(x) + b_A for 256-column tiles with
+// every m-tile, persistent workgroups. On the x-tile kernel each m-group of 3-4 m-tiles staged the
+// block's rows again and waited on every block's loads. Here a step = one 16-channel block: its 3
+// taps' fragments (3 MT x 2 KB) + raw rows (256 + 2 dil, 64 B each) by global_load_lds into one of
+// 2 slots, the next step's copies issued right after the barrier that opens a step; each lane
+// converts its column's rows of the 3 taps in registers (LeakyReLU, zero padding, split: three times
+// the conversion VALU of converting each row once, no conversion pass and no second barrier).
+// The x-tile conv's blocks, taps, m-tiles, splits and epilogue: bit-identical.
+template <int MT>
+struct RcShape {
+  static constexpr int NF = 3 * MT * 2;         // fragment copies (36 at 192 channels)
+  static constexpr int NRMAX = (RS_COLS + RS_MAX_REACH + 15) / 16;
+  static constexpr int SLOT = (NF + NRMAX) * 1024;
+  static constexpr int D = (NF + NRMAX + RS_NWV - 1) / RS_NWV;
+  static constexpr int NST = MT * 4;
+  static constexpr int LDS = 2 * SLOT + 32 * MT * 4 + RS_MAX_TILES * RS_TD * 4;
+};
+
+template <int MT>
+__global__ void __launch_bounds__(RS_NTH) pwg_rconv_kernel(const RstackArgs a) {
+  using S = RcShape<MT>;
+  constexpr int C = 32 * MT, CS = 2 * MT, D = S::D;
+  typedef __attribute__((address_space(1))) void* gptr_t;
+  typedef __attribute__((address_space(3))) void* lptr_t;
+  extern __shared__ __attribute__((aligned(16))) unsigned char rs_smem[];
+  unsigned char* const ring = rs_smem;
+  float* const sbias = reinterpret_cast<float*>(rs_smem + 2 * S::SLOT);
+  int* const stile = reinterpret_cast<int*>(sbias + C);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int hh = lane >> 5, cl = lane & 31;
+  auto slot_of = [&](int s) {
+    unsigned o = (unsigned)__builtin_amdgcn_readfirstlane(s & 1) * (unsigned)S::SLOT;
+    asm volatile("" : "+s"(o));
+    return ring + o;
+  };
+  const int g = blockIdx.x, ng = gridDim.x;
+  const int t_begin = (int)(((long long)a.n_blocks * g) / ng);
+  const int nt = (int)(((long long)a.n_blocks * (g + 1)) / ng) - t_begin;
+  if (nt <= 0) return;
+  for (int i = threadIdx.x; i < C; i += RS_NTH) sbias[i] = a.bA[i];
+  for (int k = threadIdx.x; k < nt; k += RS_NTH) {
+    const int2 b = a.blocks[t_begin + k];
+    const int2 sx = *reinterpret_cast<const int2*>(a.seg_x + 2 * b.x);
+    const int2 sy = *reinterpret_cast<const int2*>(a.seg_y + 2 * b.x);
+    int* const td = stile + RS_TD * k;
+    td[0] = b.y;
+    td[1] = sx.x;
+    td[2] = sx.y;
+    td[3] = sy.x;
+    td[4] = a.ncols[b.x];
+  }
+  __syncthreads();
+
+  const int n_steps = nt * CS;
+  const int nr = (RS_COLS + 2 * a.dil + 15) / 16;
+  const int n1 = S::NF + nr;
+  const int ld = a.ld_x, mode = a.mode_x;
+  int roff[D];
+  // step s = block cb of tile k: the 3 taps' fragments, then the block's raw rows (piece q of row r
+  // at position q ^ (r >> 2 & 3)); the row sources are computed with a tile's block 0
+  auto issue = [&](int s, int k, int cb) {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const float* wA = a.wA;
+    const float* xg = a.x;
+    asm volatile("" : "+s"(wA), "+s"(xg));
+    unsigned char* const slot = slot_of(s);
+    if (cb == 0) {
+      const int* const td = stile + RS_TD * k;
+      const int q0 = td[0], rx = td[1], T = td[2];
+#pragma unroll
+      for (int kk = 0; kk < D; ++kk) {
+        const int i = min(wave + RS_NWV * kk, n1 - 1);
+        const int j = min(max(i - S::NF, 0), nr - 1);
+        const int row = 16 * j + (ln >> 2);
+        const int q = (ln & 3) ^ ((row >> 2) & 3);
+        int p = q0 + a.off + row;
+        (void)rs_edge(p, T, mode);
+        roff[kk] = (rx + p) * ld + 4 * q;
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < D; ++kk) {
+      const int i = min(wave + RS_NWV * kk, n1 - 1);
+      const float* src;
+      if (i < S::NF) {
+        const int tap = i / (2 * MT), rem = i - tap * (2 * MT);
+        src = wA + ((tap * CS + cb) * MT) * 512 + rem * 256 + ln * 4;
+      } else {
+        src = xg + roff[kk] + 16 * cb;
+      }
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(slot + i * 1024), 16, 0, 0);
+    }
+  };
+  auto barrier = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  rs_f32x16 acc[MT];
+  const float slope1 = a.slope1;
+  const bool zmode = mode == PWG_PAD_ZERO;
+  const int col = 32 * wave + cl;
+  auto epilogue = [&](int k) {
+    const int* const td = stile + RS_TD * k;
+    const int q0 = td[0], ry = td[3], nq = td[4];
+    const int live = min(max(nq - q0, 0), RS_COLS);
+    const unsigned long long base = reinterpret_cast<unsigned long long>(a.y + ((size_t)ry + q0) * C);
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)base);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(base >> 32));
+    const int nbytes = __builtin_amdgcn_readfirstlane(live * C * 4);
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(((unsigned long long)hi << 32) | lo), (short)0, nbytes, 0x00020000);
+    const int voff = col * C * 4;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int j4 = 0; j4 < 4; ++j4) {
+        const int row = 32 * m + 8 * j4 + 4 * hh;
+        rs_f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[m][4 * j4 + e] + sbias[row + e];
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(rs_u32x4, v), rsrc, voff + row * 4, 0, 0);
+      }
+  };
+
+  issue(0, 0, 0);
+  int s = 0;
+  for (int k = 0; k < nt; ++k) {
+    const int* const td = stile + RS_TD * k;
+    const int q0 = td[0], T = td[2];
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[m][e] = 0.f;
+    for (int cb = 0; cb < CS; ++cb, ++s) {
+      // newer than step s's copies (issued at the start of step s - 1): the previous tile's stores
+      if (cb == 0 && k > 0) rs_vm_wait<S::NST>();
+      else rs_vm_wait<0>();
+      barrier();
+      if (s + 1 < n_steps) {
+        if (cb + 1 < CS) issue(s + 1, k, cb + 1);
+        else issue(s + 1, k + 1, 0);
+      }
+      const unsigned char* const slot = slot_of(s);
+      const unsigned char* const rows = slot + S::NF * 1024;
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        const int tr = col + t * a.dil;
+        const int sw = (tr >> 2) & 3;
+        asm volatile("" ::: "memory");
+        const rs_f32x4 v0 = *reinterpret_cast<const rs_f32x4*>(rows + (size_t)tr * 64 + 16 * ((2 * hh) ^ sw));
+        const rs_f32x4 v1 = *reinterpret_cast<const rs_f32x4*>(rows + (size_t)tr * 64 + 16 * ((2 * hh + 1) ^ sw));
+        const int p = q0 + a.off + tr;
+        const bool ok = !zmode || (p >= 0 && p < T);
+        const rs_f32x8 xv = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+        rs_f32x8 c;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) c[e] = ok ? rs_lrelu(xv[e], slope1) : 0.f;
+        rs_u32x4 bh, bl;
+        rs_split8(c, bh, bl);
+        const rs_u32x4* const sa = reinterpret_cast<const rs_u32x4*>(slot + t * (2 * MT) * 1024) + lane;
+        rs_u32x4 ah[2], al[2];
+        ah[0] = sa[0];
+        al[0] = sa[64];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          if (m + 1 < MT) {
+            ah[(m + 1) & 1] = sa[((m + 1) * 2) * 64];
+            al[(m + 1) & 1] = sa[((m + 1) * 2 + 1) * 64];
+          }
+          asm volatile("" ::: "memory");
+          acc[m] = rs_mma3(ah[m & 1], al[m & 1], bh, bl, acc[m]);
+          asm volatile("" ::: "memory");
+        }
+      }
+    }
+    epilogue(k);
+  }
+  rs_vm_wait<0>();
+}
+
+template <int MT>
+hipError_t rc_go(const RstackArgs& a, int n_wg, hipStream_t s) {
+  const int lds = RcShape<MT>::LDS;
+  const hipError_t e = allow_lds(reinterpret_cast<const void*>(pwg_rconv_kernel<MT>), lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((pwg_rconv_kernel<MT>), dim3((unsigned)n_wg), dim3(RS_NTH), (size_t)lds, s, a);
+  return hipGetLastError();
+}
+
 template <int MT>
 hipError_t r1_go(const R1x1Args& a, int n_wg, hipStream_t s) {
   const int lds = R1Shape<MT>::LDS;
@@ -1406,6 +1599,20 @@ hipError_t launch_rstack_impl(const RstackArgs& a, int cs, int n_wg, hipStream_t
 }
 
 bool r1x1_supported(int mt) { return mt == 4 || mt == 6 || mt == 8; }
+
+hipError_t launch_rconv(const RstackArgs& a, int mt, int n_wg, hipStream_t s) {
+  if (!r1x1_supported(mt) || a.n_blocks < 1 || n_wg < 1 || a.dil < 1 || 2 * a.dil > RS_MAX_REACH ||
+      (a.n_blocks + n_wg - 1) / n_wg > RS_MAX_TILES || (a.ld_x & 3))
+    return hipErrorInvalidValue;
+  hipError_t e = hipErrorInvalidValue;
+  switch (mt) {
+    case 4: e = rc_go<4>(a, n_wg, s); break;
+    case 6: e = rc_go<6>(a, n_wg, s); break;
+    case 8: e = rc_go<8>(a, n_wg, s); break;
+  }
+  if (e == hipSuccess) g_rs_launches.fetch_add(1, std::memory_order_relaxed);
+  return e;
+}
 
 hipError_t launch_r1x1(const R1x1Args& a, int mt, int n_wg, hipStream_t s, bool pairs) {
   if (!r1x1_supported(mt) || a.n_blocks < 1 || n_wg < 1 || a.nch < 2 || a.nch0 < 1 || a.nch0 >= a.nch ||
