@@ -1323,39 +1323,47 @@ hipError_t r2_go(const R1x1Args& a, int n_wg, hipStream_t s) {
 // converts its column's rows of the 3 taps in registers (LeakyReLU, zero padding, split: three times
 // the conversion VALU of converting each row once, no conversion pass and no second barrier).
 // The x-tile conv's blocks, taps, m-tiles, splits and epilogue: bit-identical.
-template <int MT>
+// MT m-tiles per workgroup of NMG m-groups (NMG > 1: every m-group's workgroups stage the rows
+// again, for a slot small enough that 3 fit: the copies of two steps in flight instead of one;
+// measured slower at 192 / 256 channels, 0.205 -> 0.259 / 0.302 -> 0.337 ms, so the launcher runs
+// NMG = 1; profiles/r06_ab/rconv/mg_*)
+template <int MT, int NMG>
 struct RcShape {
-  static constexpr int NF = 3 * MT * 2;         // fragment copies (36 at 192 channels)
+  static constexpr int NF = 3 * MT * 2;         // fragment copies
   static constexpr int NRMAX = (RS_COLS + RS_MAX_REACH + 15) / 16;
   static constexpr int SLOT = (NF + NRMAX) * 1024;
   static constexpr int D = (NF + NRMAX + RS_NWV - 1) / RS_NWV;
   static constexpr int NST = MT * 4;
-  static constexpr int LDS = 2 * SLOT + 32 * MT * 4 + RS_MAX_TILES * RS_TD * 4;
+  static constexpr int FIXED = 32 * MT * 4 + RS_MAX_TILES * RS_TD * 4;
+  static constexpr int P = 3 * SLOT + FIXED <= 160 * 1024 ? 3 : 2;  // slots; 3: two steps ahead
+  static constexpr int LDS = P * SLOT + FIXED;
 };
 
-template <int MT>
+template <int MT, int NMG>
 __global__ void __launch_bounds__(RS_NTH) pwg_rconv_kernel(const RstackArgs a) {
-  using S = RcShape<MT>;
-  constexpr int C = 32 * MT, CS = 2 * MT, D = S::D;
+  using S = RcShape<MT, NMG>;
+  constexpr int C = 32 * MT, MTT = MT * NMG, CT = 32 * MTT, CS = 2 * MTT, D = S::D, P = S::P;
   typedef __attribute__((address_space(1))) void* gptr_t;
   typedef __attribute__((address_space(3))) void* lptr_t;
   extern __shared__ __attribute__((aligned(16))) unsigned char rs_smem[];
   unsigned char* const ring = rs_smem;
-  float* const sbias = reinterpret_cast<float*>(rs_smem + 2 * S::SLOT);
+  float* const sbias = reinterpret_cast<float*>(rs_smem + P * S::SLOT);
   int* const stile = reinterpret_cast<int*>(sbias + C);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int hh = lane >> 5, cl = lane & 31;
   auto slot_of = [&](int s) {
-    unsigned o = (unsigned)__builtin_amdgcn_readfirstlane(s & 1) * (unsigned)S::SLOT;
+    unsigned o = (unsigned)__builtin_amdgcn_readfirstlane(s % P) * (unsigned)S::SLOT;
     asm volatile("" : "+s"(o));
     return ring + o;
   };
-  const int g = blockIdx.x, ng = gridDim.x;
+  // workgroups [mg ng, (mg + 1) ng) take m-group mg (m-tiles [mg MT, mg MT + MT))
+  const int ng = gridDim.x / NMG, mg = blockIdx.x / ng, g = blockIdx.x - mg * ng;
+  const int m0 = mg * MT;
   const int t_begin = (int)(((long long)a.n_blocks * g) / ng);
   const int nt = (int)(((long long)a.n_blocks * (g + 1)) / ng) - t_begin;
   if (nt <= 0) return;
-  for (int i = threadIdx.x; i < C; i += RS_NTH) sbias[i] = a.bA[i];
+  for (int i = threadIdx.x; i < C; i += RS_NTH) sbias[i] = a.bA[32 * m0 + i];
   for (int k = threadIdx.x; k < nt; k += RS_NTH) {
     const int2 b = a.blocks[t_begin + k];
     const int2 sx = *reinterpret_cast<const int2*>(a.seg_x + 2 * b.x);
@@ -1403,7 +1411,7 @@ __global__ void __launch_bounds__(RS_NTH) pwg_rconv_kernel(const RstackArgs a) {
       const float* src;
       if (i < S::NF) {
         const int tap = i / (2 * MT), rem = i - tap * (2 * MT);
-        src = wA + ((tap * CS + cb) * MT) * 512 + rem * 256 + ln * 4;
+        src = wA + ((tap * CS + cb) * MTT + m0) * 512 + rem * 256 + ln * 4;
       } else {
         src = xg + roff[kk] + 16 * cb;
       }
@@ -1422,13 +1430,14 @@ __global__ void __launch_bounds__(RS_NTH) pwg_rconv_kernel(const RstackArgs a) {
     const int* const td = stile + RS_TD * k;
     const int q0 = td[0], ry = td[3], nq = td[4];
     const int live = min(max(nq - q0, 0), RS_COLS);
-    const unsigned long long base = reinterpret_cast<unsigned long long>(a.y + ((size_t)ry + q0) * C);
+    const unsigned long long base = reinterpret_cast<unsigned long long>(a.y + ((size_t)ry + q0) * CT + 32 * m0);
     const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)base);
     const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(base >> 32));
-    const int nbytes = __builtin_amdgcn_readfirstlane(live * C * 4);
+    // (the range ends after this m-group's channels of the last live column)
+    const int nbytes = __builtin_amdgcn_readfirstlane(live > 0 ? ((live - 1) * CT + C) * 4 : 0);
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         reinterpret_cast<void*>(((unsigned long long)hi << 32) | lo), (short)0, nbytes, 0x00020000);
-    const int voff = col * C * 4;
+    const int voff = col * CT * 4;
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -1442,6 +1451,9 @@ __global__ void __launch_bounds__(RS_NTH) pwg_rconv_kernel(const RstackArgs a) {
   };
 
   issue(0, 0, 0);
+  if constexpr (P == 3) {
+    if (n_steps > 1) issue(1, CS > 1 ? 0 : 1, CS > 1 ? 1 : 0);
+  }
   int s = 0;
   for (int k = 0; k < nt; ++k) {
     const int* const td = stile + RS_TD * k;
@@ -1451,13 +1463,25 @@ __global__ void __launch_bounds__(RS_NTH) pwg_rconv_kernel(const RstackArgs a) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[m][e] = 0.f;
     for (int cb = 0; cb < CS; ++cb, ++s) {
-      // newer than step s's copies (issued at the start of step s - 1): the previous tile's stores
-      if (cb == 0 && k > 0) rs_vm_wait<S::NST>();
-      else rs_vm_wait<0>();
-      barrier();
-      if (s + 1 < n_steps) {
-        if (cb + 1 < CS) issue(s + 1, k, cb + 1);
-        else issue(s + 1, k + 1, 0);
+      if constexpr (P == 3) {
+        // newer than step s's copies (issued two steps back): step s + 1's, and the previous
+        // tile's stores when step s - 1 or s - 2 was its last
+        const int n_new = (s + 1 < n_steps ? D : 0) + ((cb <= 1 && k > 0) ? S::NST : 0);
+        rs_vm_wait_rt<0, D + S::NST>(n_new);
+        barrier();
+        if (s + 2 < n_steps) {
+          if (cb + 2 < CS) issue(s + 2, k, cb + 2);
+          else issue(s + 2, k + 1, cb + 2 - CS);
+        }
+      } else {
+        // newer than step s's copies (issued at the start of step s - 1): the previous tile's stores
+        if (cb == 0 && k > 0) rs_vm_wait<S::NST>();
+        else rs_vm_wait<0>();
+        barrier();
+        if (s + 1 < n_steps) {
+          if (cb + 1 < CS) issue(s + 1, k, cb + 1);
+          else issue(s + 1, k + 1, 0);
+        }
       }
       const unsigned char* const slot = slot_of(s);
       const unsigned char* const rows = slot + S::NF * 1024;
@@ -1497,12 +1521,12 @@ __global__ void __launch_bounds__(RS_NTH) pwg_rconv_kernel(const RstackArgs a) {
   rs_vm_wait<0>();
 }
 
-template <int MT>
+template <int MT, int NMG>
 hipError_t rc_go(const RstackArgs& a, int n_wg, hipStream_t s) {
-  const int lds = RcShape<MT>::LDS;
-  const hipError_t e = allow_lds(reinterpret_cast<const void*>(pwg_rconv_kernel<MT>), lds);
+  const int lds = RcShape<MT, NMG>::LDS;
+  const hipError_t e = allow_lds(reinterpret_cast<const void*>(pwg_rconv_kernel<MT, NMG>), lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((pwg_rconv_kernel<MT>), dim3((unsigned)n_wg), dim3(RS_NTH), (size_t)lds, s, a);
+  hipLaunchKernelGGL((pwg_rconv_kernel<MT, NMG>), dim3((unsigned)(n_wg * NMG)), dim3(RS_NTH), (size_t)lds, s, a);
   return hipGetLastError();
 }
 
@@ -1600,15 +1624,16 @@ hipError_t launch_rstack_impl(const RstackArgs& a, int cs, int n_wg, hipStream_t
 
 bool r1x1_supported(int mt) { return mt == 4 || mt == 6 || mt == 8; }
 
+
 hipError_t launch_rconv(const RstackArgs& a, int mt, int n_wg, hipStream_t s) {
   if (!r1x1_supported(mt) || a.n_blocks < 1 || n_wg < 1 || a.dil < 1 || 2 * a.dil > RS_MAX_REACH ||
       (a.n_blocks + n_wg - 1) / n_wg > RS_MAX_TILES || (a.ld_x & 3))
     return hipErrorInvalidValue;
   hipError_t e = hipErrorInvalidValue;
   switch (mt) {
-    case 4: e = rc_go<4>(a, n_wg, s); break;
-    case 6: e = rc_go<6>(a, n_wg, s); break;
-    case 8: e = rc_go<8>(a, n_wg, s); break;
+    case 4: e = rc_go<4, 1>(a, n_wg, s); break;
+    case 6: e = rc_go<6, 1>(a, n_wg, s); break;
+    case 8: e = rc_go<8, 1>(a, n_wg, s); break;
   }
   if (e == hipSuccess) g_rs_launches.fetch_add(1, std::memory_order_relaxed);
   return e;
