@@ -273,6 +273,15 @@ def measure_layer_traffic(args):
     return fetch + write, note, clk
 
 
+# kernels of a conv-network forward: the executor's own (pwg_cnet_*) and those it launches from
+# pwg_mstack.hip / pwg_rstack.hip (fused stack chains, batched stacks, wide-stack conv and 1x1)
+_PROG_KERNELS = ("pwg_cnet_", "pwg_mstack_", "pwg_rstack_", "pwg_rconv_", "pwg_r1x1")
+
+
+def _prog_kernel(name):
+    return any(t in name for t in _PROG_KERNELS) and "desc_kernel" not in name
+
+
 def measure_program_traffic(args):
     """Vocoder configs: HBM bytes of ONE whole forward (every launch of the conv program), measured
     as measure_layer_traffic does, from the second of the child's two forwards (the later half of
@@ -286,7 +295,7 @@ def measure_program_traffic(args):
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         vals = per[ctr]
         # the conv program's own launches only (module setup runs torch / copy kernels before them)
-        ids = sorted(i for i in vals if "pwg_cnet_" in vals[i][0])
+        ids = sorted(i for i in vals if _prog_kernel(vals[i][0]) or "desc_kernel" in vals[i][0])
         second = ids[len(ids) // 2:]
         n_fwd = len(second)
         scale = 2048.0 if ctr == "FETCH_SIZE" else 1024.0
@@ -298,12 +307,12 @@ def measure_program_traffic(args):
             f"two forwards in a child process, the second forward's {n_fwd} conv-program launches; read "
             f"{tot['FETCH_SIZE'] / 1e9:.3f} GB + write {tot['WRITE_SIZE'] / 1e9:.3f} GB per forward")
     top = dict(sorted(((k, round(v / 1e9, 4)) for k, v in by_kernel.items()), key=lambda kv: -kv[1])[:6])
-    clk = _clock_busy(per, lambda name: "pwg_cnet_" in name and "desc_kernel" not in name)
+    clk = _clock_busy(per, _prog_kernel)
     if clk is not None:
         # the kernels that take the most time in the clock pass
         dur = {}
         for name, _, d in per["GRBM_GUI_ACTIVE"].values():
-            if "pwg_cnet_" in name:
+            if _prog_kernel(name):
                 dur[short(name)] = dur.get(short(name), 0) + d
         slow = sorted(dur, key=lambda k: -dur[k])[:5]
         clk["per_kernel"] = {}
